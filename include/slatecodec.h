@@ -1,0 +1,282 @@
+/*
+ * slatecodec.h — C-ABI of the MI355X-native SST block codec (drop-in for the
+ * slatedb-go `internal/sstable` block/bloom/builder/reader hot path).
+ *
+ * Every function here is `extern "C"`, takes plain pointers and sizes, never
+ * retains a caller pointer after it returns (cgo rule), and never aborts: Go
+ * `error` returns and Go `panic`s on corrupt input both become status codes.
+ * All compute (CRC32, Snappy, row packing/unpacking, bloom) runs in HIP kernels
+ * on the context's GPU; there is no CPU fallback — without a usable GPU every
+ * compute entry point returns SLATE_E_NO_DEVICE.
+ *
+ * Reference interface each group replaces (paths relative to slatedb-go):
+ *   block codec     internal/sstable/block/block.go:54 Encode, :78 Decode
+ *   row codec       internal/sstable/block/row.go:149 Encode, :191 Decode
+ *   bloom           internal/sstable/bloom/bloom.go:19 HasKey, :52 Encode, :70 Decode, :112 Build
+ *   compression     internal/compress/compression.go:80 Encode, :126 Decode
+ *   SST builder     internal/sstable/builder.go:136 NewBuilder, :149 AddValue, :160 Add,
+ *                   :185 NextBlock, :215 Build; flatbuf.go:143 EncodeTable
+ *   SST reader      internal/sstable/decode.go:25 ReadInfo, :50 ReadFilter, :73 ReadIndex,
+ *                   :86 ReadIndexRaw, :107 ReadBlocks, :151 ReadBlockRaw;
+ *                   flatbuf.go:62 EncodeInfo, :83 DecodeIndex, :102 DecodeInfo
+ */
+#ifndef SLATECODEC_H
+#define SLATECODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLATECODEC_ABI_VERSION 1
+
+/* ---- compression codec (internal/compress/compression.go:15-21) ---------------- */
+enum slate_codec {
+  SLATE_CODEC_NONE = 0,
+  SLATE_CODEC_SNAPPY = 1,
+  SLATE_CODEC_ZLIB = 2,
+  SLATE_CODEC_LZ4 = 3,
+  SLATE_CODEC_ZSTD = 4,
+};
+
+/* ---- status codes ---------------------------------------------------------------
+ * Each code maps 1:1 onto the reference's error string (slate_status_string) with
+ * the %d fields carried in slate_block_meta.detail / .aux.  Codes >= 100 are
+ * C-ABI conditions that have no Go counterpart. */
+enum slate_status {
+  SLATE_OK = 0,
+  /* block.Decode (block.go:79-131) */
+  SLATE_E_BLOCK_TOO_SMALL = 1,      /* "corrupted block: block is too small; must be at least 6 bytes" */
+  SLATE_E_BLOCK_CHECKSUM = 2,       /* "corrupted block: checksum mismatch" */
+  SLATE_E_BLOCK_UNCOMP_SMALL = 3,   /* "corrupted block: uncompressed block is too small; must be at least 2 bytes" */
+  SLATE_E_BLOCK_INDEX_OFFSET = 4,   /* "corrupted block: invalid index offset '%d'; cannot be negative" (detail) */
+  SLATE_E_BLOCK_OFFSET_BOUNDS = 5,  /* "corrupted block: block offset[%d] = %d exceeds key value bounds" (aux, detail) */
+  SLATE_E_BLOCK_NO_OFFSETS = 6,     /* "corrupted block: Block.Offsets must be greater than 0" */
+  SLATE_E_BLOCK_FIRSTKEY_PANIC = 7, /* Go panics slicing FirstKey (block.go:130-131) */
+  SLATE_E_BLOCK_EMPTY = 8,          /* "assertion failed; block cannot be empty" (block.go:197) */
+  /* compress (compression.go) and golang/snappy v0.0.4 */
+  SLATE_E_INVALID_CODEC = 10,       /* "corrupted; invalid compression codec" */
+  SLATE_E_SNAPPY_CORRUPT = 11,      /* "snappy: corrupt input" */
+  SLATE_E_SNAPPY_TOO_LARGE = 12,    /* "snappy: decoded block is too large" */
+  SLATE_E_CODEC_UNSUPPORTED = 13,   /* codec not yet implemented by this backend (zlib/lz4/zstd) */
+  /* v0 row codec (row.go:191-288) — per-row status in slate_row.status */
+  SLATE_E_ROW_TOO_SHORT = 20,       /* "corrupt v0 row: data length too short to decode a row" */
+  SLATE_E_ROW_PREFIX = 21,          /* "corrupt v0 row: key prefix length exceeds length of first key in block" */
+  SLATE_E_ROW_SUFFIX = 22,          /* "corrupt v0 row: key suffix length exceeds length of block" */
+  SLATE_E_ROW_EXPIRE = 23,          /* "corrupt v0 row: data length too short for expire" */
+  SLATE_E_ROW_CREATE = 24,          /* "corrupt v0 row: data length too short for create" */
+  SLATE_E_ROW_VALUE_LEN = 25,       /* "corrupt v0 row: data length too short for for value length" */
+  SLATE_E_ROW_VALUE = 26,           /* "corrupt v0 row: data length too short for for value" */
+  SLATE_E_ROW_PANIC = 27,           /* Go panics reading seq/flags (row.go:218-223) */
+  SLATE_E_ROW_PEEK_SHORT = 28,      /* "corrupt v0 row: data length too short to peek at row" */
+  SLATE_E_ROW_OFFSET_RANGE = 29,    /* offset beyond Block.Data (block/iterator.go:59-62 warns) */
+  /* bloom (bloom.go:70-91) */
+  SLATE_E_FILTER_TOO_SMALL = 30,    /* "corrupt filter: filter is too small; must be at least 2 bytes" */
+  SLATE_E_FILTER_CHECKSUM = 31,     /* "corrupt filter: invalid checksum" */
+  SLATE_E_FILTER_PANIC = 32,        /* Go panics on a 2..3 byte filter / short payload */
+  /* sstable (decode.go, flatbuf.go, blob.go) */
+  SLATE_E_INDEX_TOO_SHORT = 40,     /* "corrupted index; too short" */
+  SLATE_E_INDEX_CHECKSUM = 41,      /* "corrupted index; checksum mismatch" */
+  SLATE_E_INFO_TOO_SHORT = 42,      /* "corrupted info; too short" */
+  SLATE_E_INFO_CHECKSUM = 43,       /* "corrupted info; checksum mismatch" */
+  SLATE_E_SST_TOO_SHORT = 44,       /* "corrupted SSTable; too short" */
+  SLATE_E_BLOB_RANGE = 45,          /* "corrupted; [%d:%d] is an invalid range" */
+  SLATE_E_RANGE_START = 46,         /* "block start '%d' range cannot be greater than end range '%d'" */
+  SLATE_E_RANGE_END = 47,           /* "block end '%d' range cannot be greater than size of block meta range '%d'" */
+  SLATE_E_FLATBUF = 48,             /* malformed flatbuffer (Go would panic in GetRootAs / accessors) */
+  /* C-ABI / runtime conditions */
+  SLATE_E_NO_DEVICE = 100,          /* no usable HIP device / kernels not loadable */
+  SLATE_E_HIP = 101,                /* HIP runtime error */
+  SLATE_E_INVALID_ARG = 102,
+  SLATE_E_CAPACITY = 103,           /* caller-provided output buffer too small */
+  SLATE_E_OOM = 104,
+};
+
+/* ---- layouts ----------------------------------------------------------------- */
+
+/* Per-block result of block.Decode (block.go:78-134).  16 bytes. */
+typedef struct slate_block_meta {
+  int16_t status;     /* slate_status */
+  uint16_t flags;     /* SLATE_BLKF_* */
+  int32_t detail;     /* E_BLOCK_INDEX_OFFSET: offsetStartIndex; E_BLOCK_OFFSET_BOUNDS: offset value */
+  uint32_t data_len;  /* len(Block.Data) == offsetStartIndex */
+  uint16_t n_rows;    /* len(Block.Offsets) */
+  uint16_t aux;       /* E_BLOCK_OFFSET_BOUNDS: offending index; OK: len(Block.FirstKey) (quirk, block.go:130) */
+} slate_block_meta;
+
+#define SLATE_BLKF_ROWS_TRUNCATED 0x1u /* more offsets than row-descriptor capacity */
+
+/* Per-row descriptor emitted by the decode kernel: what v0Codec.Decode
+ * (row.go:191-261) extracts, against the block iterator's firstKey
+ * (block/iterator.go:84-107: row 0 is decoded with firstKey = nil).  16 bytes.
+ *   key suffix = Data[row_off + 4 .. + key_suffix_len]
+ *   seq (BE u64) at row_off + 4 + key_suffix_len, flags byte right after it
+ *   value = Data[row_off + 4 + key_suffix_len + meta_len .. + value_len]          */
+typedef struct slate_row {
+  uint32_t row_off;         /* Block.Offsets[i] */
+  uint16_t key_prefix_len;  /* bytes shared with the block's first key */
+  uint16_t key_suffix_len;
+  uint32_t value_len;       /* 0 for tombstones */
+  uint8_t flags;            /* v0 flags: 1 tombstone, 2 hasExpire, 4 hasCreate */
+  uint8_t meta_len;         /* seq(8)+flags(1)+[expire 8]+[create 8]+[value_len 4] */
+  int16_t status;           /* SLATE_OK or SLATE_E_ROW_* */
+} slate_row;
+
+/* sstable.Config (builder.go:118-133); defaults in decode.go:16-23. */
+typedef struct slate_sst_config {
+  uint64_t block_size;
+  uint32_t min_filter_keys;
+  uint32_t filter_bits_per_key;
+  int32_t codec; /* slate_codec */
+} slate_sst_config;
+
+/* sstable.Info (sstable.go:12-31); first_key bytes returned separately. */
+typedef struct slate_sst_info {
+  uint64_t index_offset;
+  uint64_t index_len;
+  uint64_t filter_offset;
+  uint64_t filter_len;
+  int32_t codec;
+  uint32_t first_key_len;
+} slate_sst_info;
+
+typedef struct slate_ctx slate_ctx;
+typedef struct slate_sst_builder slate_sst_builder;
+typedef struct slate_sst_table slate_sst_table;
+typedef struct slate_index slate_index;
+
+/* ---- library / context --------------------------------------------------------- */
+int slate_abi_version(void);
+const char* slate_status_string(int status); /* reference error text ("%d" left verbatim) */
+/* One context = one device + one HIP stream; contexts are independent and the
+ * library keeps no global mutable state, so one context per calling goroutine/
+ * thread is reentrant (SURVEY 8b "Threading"). */
+slate_ctx* slate_ctx_create(int device, int* status);
+void slate_ctx_destroy(slate_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream) for device-resident
+ * calls; NULL restores the context's own stream. */
+int slate_ctx_set_stream(slate_ctx* ctx, void* hip_stream);
+int slate_ctx_synchronize(slate_ctx* ctx);
+
+/* ---- block decode: block.Decode (block.go:78) ----------------------------------
+ * Device-resident batch.  Block i's encoded bytes are d_in[d_in_off[i] .. d_in_off[i+1]).
+ * Step 1 (plan): decoded lengths and row capacities -> exclusive scans into
+ *   d_out_off[n+1] (bytes) and d_row_base[n+1] (slate_row slots); the totals are
+ *   d_out_off[n] and d_row_base[n].  d_scratch must hold slate_decode_scratch_bytes(n).
+ * Step 2 (decode): writes the decoded buffer (rows || BE16 offsets || BE16 count)
+ *   of block i at d_out + d_out_off[i], its meta and its row descriptors.
+ * Both enqueue on the context stream and return without synchronising. */
+size_t slate_decode_scratch_bytes(uint32_t n_blocks);
+int slate_block_decode_plan_device(slate_ctx* ctx, int codec, const uint8_t* d_in,
+                                   const uint64_t* d_in_off, uint32_t n_blocks,
+                                   uint64_t* d_out_off, uint64_t* d_row_base, void* d_scratch);
+int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in,
+                              const uint64_t* d_in_off, uint32_t n_blocks, uint8_t* d_out,
+                              const uint64_t* d_out_off, slate_block_meta* d_meta,
+                              slate_row* d_rows, const uint64_t* d_row_base);
+
+/* Host-buffer convenience (object-store GET buffers in, caller buffers out):
+ * stages through pinned memory, runs plan+decode, copies back, synchronises.
+ * out_off/row_base are outputs (n+1 each); out_cap/rows_cap are capacities. */
+int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off,
+                             uint32_t n_blocks, uint8_t* out, uint64_t out_cap, uint64_t* out_off,
+                             slate_block_meta* meta, slate_row* rows, uint64_t rows_cap,
+                             uint64_t* row_base);
+/* Single block: block.Decode(&b, input, codec).  Data = out[0 .. meta.data_len);
+ * offsets[] receives Block.Offsets (meta.n_rows entries, capacity offsets_cap). */
+int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_len, uint8_t* out,
+                       size_t out_cap, size_t* out_len, slate_block_meta* meta, uint16_t* offsets,
+                       size_t offsets_cap);
+
+/* ---- block encode: block.Encode (block.go:54) ----------------------------------
+ * Encodes one block (Data + Offsets) with codec: compress(Data || BE16 offsets ||
+ * BE16 n) || BE32 CRC32-IEEE. */
+int slate_block_encode(slate_ctx* ctx, int codec, const uint8_t* data, size_t data_len,
+                       const uint16_t* offsets, size_t n_offsets, uint8_t* out, size_t out_cap,
+                       size_t* out_len);
+
+/* ---- SST builder: sstable.Builder (builder.go:92-268) ----------------------------
+ * Keys/values are copied on Add.  Blocks are cut on the GPU (greedy fill of
+ * block.Builder.Add, block.go:162-182) when NextBlock/Build needs them. */
+slate_sst_builder* slate_sst_builder_new(slate_ctx* ctx, const slate_sst_config* cfg, int* status);
+void slate_sst_builder_free(slate_sst_builder* b);
+/* Add (builder.go:160): kind 0 = KindKeyValue, 1 = KindTombStone. */
+int slate_sst_builder_add(slate_sst_builder* b, const uint8_t* key, size_t key_len,
+                          const uint8_t* value, size_t value_len, int kind);
+/* AddValue (builder.go:149): empty value => tombstone. */
+int slate_sst_builder_add_value(slate_sst_builder* b, const uint8_t* key, size_t key_len,
+                                const uint8_t* value, size_t value_len);
+/* Bulk AddValue of n sorted KVs: key i = keys[key_off[i]..key_off[i+1]), same for
+ * values; is_tomb may be NULL (then empty value => tombstone as AddValue). */
+int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const uint64_t* key_off,
+                                const uint8_t* values, const uint64_t* value_off,
+                                const uint8_t* is_tomb, uint64_t n);
+/* NextBlock (builder.go:185): *present = 0 when no finished block is queued.
+ * The block is copied into out (capacity out_cap); *len receives its size
+ * (also when it does not fit, with SLATE_E_CAPACITY). */
+int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_cap, size_t* len,
+                                 int* present);
+/* Build (builder.go:215): consumes the builder's pending KVs; the table owns the
+ * remaining block queue (last element = last block || filter || index || info || BE32 offset). */
+int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table);
+void slate_sst_table_free(slate_sst_table* t);
+int slate_sst_table_info(const slate_sst_table* t, slate_sst_info* info, uint8_t* first_key,
+                         size_t first_key_cap);
+size_t slate_sst_table_num_chunks(const slate_sst_table* t); /* Table.Blocks.Len() */
+int slate_sst_table_chunk(const slate_sst_table* t, size_t i, const uint8_t** data, size_t* len);
+/* EncodeTable (flatbuf.go:143): concatenation of the remaining chunks. */
+size_t slate_sst_table_encoded_len(const slate_sst_table* t);
+int slate_sst_table_encode(const slate_sst_table* t, uint8_t* out, size_t out_cap);
+/* Table.Bloom: *present = 0 when absent; filter bits copied into bits. */
+int slate_sst_table_bloom(const slate_sst_table* t, int* present, uint16_t* num_probes,
+                          uint8_t* bits, size_t bits_cap, size_t* bits_len);
+
+/* ---- SST reader (decode.go / flatbuf.go) ------------------------------------------
+ * The caller performs the object-store reads (ReadOnlyBlob.ReadRange) and hands
+ * the byte ranges in; nothing is retained. */
+/* ReadInfo (decode.go:25) over the whole SST object (only its tail is touched). */
+int slate_sst_read_info(const uint8_t* sst, size_t sst_len, slate_sst_info* info,
+                        uint8_t* first_key, size_t first_key_cap);
+/* DecodeInfo (flatbuf.go:102) on info||crc bytes; EncodeInfo (flatbuf.go:62). */
+int slate_decode_info(const uint8_t* buf, size_t len, slate_sst_info* info, uint8_t* first_key,
+                      size_t first_key_cap);
+int slate_encode_info(const slate_sst_info* info, const uint8_t* first_key, uint8_t* out,
+                      size_t out_cap, size_t* out_len);
+/* DecodeIndex (flatbuf.go:83): CRC verify + decompress; index handle owns the bytes. */
+int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, slate_index** index);
+void slate_index_free(slate_index* index);
+size_t slate_index_num_blocks(const slate_index* index); /* BlockMetaLength() */
+int slate_index_block_meta(const slate_index* index, size_t i, uint64_t* offset,
+                           const uint8_t** first_key, size_t* first_key_len);
+/* ReadBlocks (decode.go:107): data = the object's bytes [meta[start].Offset, end offset)
+ * (slate_read_blocks_range gives that range).  Blocks are decoded as one GPU batch;
+ * outputs as slate_block_decode_batch.  *failed_block receives the first failing
+ * block index (the reference wraps its error with that index and range). */
+int slate_read_blocks_range(const slate_sst_info* info, const slate_index* index, uint64_t start,
+                            uint64_t end, uint64_t* range_start, uint64_t* range_end);
+int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_index* index,
+                      uint64_t start, uint64_t end, const uint8_t* data, size_t data_len,
+                      uint8_t* out, uint64_t out_cap, uint64_t* out_off, slate_block_meta* meta,
+                      slate_row* rows, uint64_t rows_cap, uint64_t* row_base,
+                      uint64_t* failed_block);
+
+/* ---- bloom filter (bloom.go) -------------------------------------------------------- */
+/* Build (bloom.go:112) over n keys (key i = keys[key_off[i]..key_off[i+1])) on the GPU. */
+int slate_bloom_build(slate_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                      uint32_t bits_per_key, uint8_t* bits, size_t bits_cap, size_t* bits_len,
+                      uint16_t* num_probes);
+/* Encode (bloom.go:52) / Decode (bloom.go:70).  Decode's bits alias nothing: copied out. */
+int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len,
+                       int codec, uint8_t* out, size_t out_cap, size_t* out_len);
+int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec,
+                       uint16_t* num_probes, uint8_t* bits, size_t bits_cap, size_t* bits_len);
+/* Filter.HasKey (bloom.go:19), batched on the GPU: out[i] = 1 if key i may be present. */
+int slate_bloom_has_keys(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len,
+                         const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLATECODEC_H */
