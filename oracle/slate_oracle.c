@@ -591,7 +591,7 @@ int or_block_decode_batch(int codec, const uint8_t* in, const uint64_t* in_off, 
     if (len >= 6 && or_decompress_len(codec, in + in_off[i], len - 4, &dl) != OR_OK) dl = 0;
     if (codec == OR_CODEC_SNAPPY && dl > 22ull * (len - 4)) dl = 0; /* provably corrupt (> 64/3 expansion) */
     out_off[i] = o; row_base[i] = r;
-    o += dl; r += or_row_capacity(dl);
+    o += (dl + 15) & ~15ull; r += or_row_capacity(dl); /* 16-byte aligned blocks, as the GPU plan */
   }
   out_off[n] = o; row_base[n] = r;
   if (o > out_cap || r > rows_cap) return OR_E_CAPACITY;

@@ -1,0 +1,597 @@
+// Block decode on MI355X: block.Decode (internal/sstable/block/block.go:78-134)
+// followed by the block iterator's per-row v0 decode (row.go:191-261,
+// block/iterator.go:84-107), for a batch of independent blocks resident in HBM.
+//
+// Layout in HBM (see DESIGN.md "Data layout"):
+//   in   : encoded blocks back to back, block i = in[in_off[i] .. in_off[i+1])
+//   out  : decoded block i (rows || BE16 offsets || BE16 count) at out + out_off[i];
+//          out_off is 16-byte aligned so every block is written with aligned
+//          dwordx4 stores
+//   meta : one 16-byte slate_block_meta per block
+//   rows : slate_row descriptors of block i at rows + row_base[i]
+//
+// Kernels:
+//   plan_sizes_kernel     decoded length per block (Snappy varint header) -> sizes
+//   scan_* (3 passes)     exclusive scans of the sizes -> out_off / row_base
+//   decode_fast_kernel    one wavefront per block, block staged in LDS:
+//                         CRC32 (64 lanes x 64-byte segments, GF(2) combine),
+//                         Snappy tag walk (wave-uniform) with lane-parallel copies,
+//                         offset checks, row descriptors, aligned write-back
+//   decode_large_kernel   same device code for blocks that exceed the fast
+//                         kernel's LDS budget (one wave per workgroup, ~150 KiB LDS)
+#include "common.h"
+#include "kernels.h"
+
+namespace slate {
+
+__constant__ CrcTables g_crc_tables = CrcTables();
+__constant__ CrcShift g_crc_shift = CrcShift();
+
+// ------------------------------------------------------------------ sizes
+// golang/snappy decode.go decodedLen: binary.Uvarint, n <= 0 || v > 0xffffffff
+// => ErrCorrupt.  Returns false for a corrupt header.
+__device__ inline bool snappy_header(const uint8_t* p, uint64_t n, uint64_t* dlen, uint32_t* hdr) {
+  uint64_t x = 0;
+  uint32_t s = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (i == 10) return false;
+    uint32_t b = p[i];
+    if (b < 0x80) {
+      if (i == 9 && b > 1) return false;
+      x |= uint64_t(b) << s;
+      if (x > 0xffffffffull) return false;
+      *dlen = x;
+      *hdr = i + 1;
+      return true;
+    }
+    x |= uint64_t(b & 0x7f) << s;
+    s += 7;
+  }
+  return false;
+}
+
+// Decoded length of a block: false when the block cannot decode (too small,
+// corrupt Snappy header, provably corrupt length, unsupported codec).
+__device__ inline bool decoded_len(int codec, const uint8_t* in, uint64_t len, uint64_t* dl, uint32_t* hdr) {
+  *hdr = 0;
+  *dl = 0;
+  if (len < 6) return false;
+  uint64_t clen = len - 4;
+  if (codec == SLATE_CODEC_NONE) {
+    *dl = clen;
+    return true;
+  }
+  if (codec == SLATE_CODEC_SNAPPY) {
+    uint64_t v;
+    if (!snappy_header(in, clen, &v, hdr)) return false;
+    if (v > kSnappyMaxExpansion * clen) return false;
+    *dl = v;
+    return true;
+  }
+  return false;
+}
+
+__global__ void plan_sizes_kernel(int codec, const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                  uint32_t n, uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {  // the scans turn the trailing zero into the totals
+    out_sz[n] = 0;
+    row_sz[n] = 0;
+    return;
+  }
+  uint64_t s0 = in_off[i];
+  uint32_t hdr;
+  uint64_t dl;
+  decoded_len(codec, in + s0, in_off[i + 1] - s0, &dl, &hdr);
+  out_sz[i] = align16(dl);
+  row_sz[i] = row_capacity(dl);
+}
+
+// ------------------------------------------------ exclusive scan (2 arrays)
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+template <typename T>
+__device__ inline T block_exclusive_scan(T v, T* sh, T* total) {
+  int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  T wsum = 0, all = 0;
+  for (int k = 0; k < kScanThreads / 64; k++) {
+    if (k < w) wsum += sh[k];
+    all += sh[k];
+  }
+  __syncthreads();
+  *total = all;
+  return x - v + wsum;
+}
+
+__global__ void scan_reduce_kernel(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, uint32_t n,
+                                   uint64_t* __restrict__ pa, uint64_t* __restrict__ pb) {
+  __shared__ uint64_t sh[2][kScanThreads / 64];
+  uint64_t base = uint64_t(blockIdx.x) * kScanTile;
+  uint64_t sa = 0, sb = 0;
+  for (int k = 0; k < kScanItems; k++) {
+    uint64_t i = base + uint64_t(k) * kScanThreads + threadIdx.x;
+    if (i < n) { sa += a[i]; sb += b[i]; }
+  }
+  uint64_t ta, tb;
+  block_exclusive_scan(sa, sh[0], &ta);
+  block_exclusive_scan(sb, sh[1], &tb);
+  if (threadIdx.x == 0) { pa[blockIdx.x] = ta; pb[blockIdx.x] = tb; }
+}
+
+// Single workgroup: exclusive scan of the per-tile partials in place.
+__global__ void scan_partials_kernel(uint64_t* __restrict__ pa, uint64_t* __restrict__ pb, uint32_t m) {
+  __shared__ uint64_t sh[2][kScanThreads / 64];
+  uint64_t ca = 0, cb = 0;
+  for (uint32_t base = 0; base < m; base += kScanThreads) {
+    uint32_t i = base + threadIdx.x;
+    uint64_t va = i < m ? pa[i] : 0, vb = i < m ? pb[i] : 0;
+    uint64_t ta, tb;
+    uint64_t ea = block_exclusive_scan(va, sh[0], &ta);
+    uint64_t eb = block_exclusive_scan(vb, sh[1], &tb);
+    if (i < m) { pa[i] = ca + ea; pb[i] = cb + eb; }
+    ca += ta;
+    cb += tb;
+  }
+}
+
+__global__ void scan_apply_kernel(uint64_t* __restrict__ a, uint64_t* __restrict__ b, uint32_t n,
+                                  const uint64_t* __restrict__ pa, const uint64_t* __restrict__ pb) {
+  __shared__ uint64_t sh[2][kScanThreads / 64];
+  uint64_t base = uint64_t(blockIdx.x) * kScanTile + uint64_t(threadIdx.x) * kScanItems;
+  uint64_t va[kScanItems], vb[kScanItems], sa = 0, sb = 0;
+  for (int k = 0; k < kScanItems; k++) {
+    uint64_t i = base + k;
+    va[k] = i < n ? a[i] : 0;
+    vb[k] = i < n ? b[i] : 0;
+    sa += va[k];
+    sb += vb[k];
+  }
+  uint64_t ta, tb;
+  uint64_t ea = block_exclusive_scan(sa, sh[0], &ta) + pa[blockIdx.x];
+  uint64_t eb = block_exclusive_scan(sb, sh[1], &tb) + pb[blockIdx.x];
+  for (int k = 0; k < kScanItems; k++) {
+    uint64_t i = base + k;
+    if (i < n) { a[i] = ea; b[i] = eb; }
+    ea += va[k];
+    eb += vb[k];
+  }
+}
+
+// ------------------------------------------------------------ LDS helpers
+// 4 bytes at an arbitrary byte offset of a 4-aligned LDS buffer (little-endian).
+__device__ inline uint32_t lds_u32(const uint8_t* base, int32_t off) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (off & ~3));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], uint32_t(off) & 3u);
+}
+
+__device__ inline uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ inline uint32_t crc_word(const uint32_t* tab, uint32_t c, uint32_t w) {
+  c ^= w;
+  return tab[768 + (c & 0xff)] ^ tab[512 + ((c >> 8) & 0xff)] ^ tab[256 + ((c >> 16) & 0xff)] ^ tab[c >> 24];
+}
+
+// crc32.ChecksumIEEE of msg[0..n) staged in LDS, computed by one wavefront.
+// 64 lanes x 64-byte segments per 4 KiB stripe, end-aligned so each lane's
+// shift factor x^(8*64*(63-l)) is a compile-time constant; the 0xFFFFFFFF init
+// is folded in by xoring the first four message bytes with 0xFF.
+__device__ uint32_t wave_crc32(const uint32_t* tab, const uint8_t* lds, uint32_t msg, uint32_t n, int lane) {
+  if (n < 4) {  // tiny message: lane-uniform bytewise loop
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < n; i++) c = tab[(c ^ lds[msg + i]) & 0xff] ^ (c >> 8);
+    return ~c;
+  }
+  uint32_t stripes = (n + kCrcStripe - 1) / kCrcStripe;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < stripes; k++) {
+    if (k) acc = gf2_mulmod(acc, g_crc_shift.stripe);
+    // segment start relative to the message (may be negative)
+    int64_t p0 = int64_t(n) - int64_t(stripes - k) * kCrcStripe + int64_t(lane) * kCrcSeg;
+    uint32_t c = 0;
+    if (p0 + int64_t(kCrcSeg) > 0) {
+#pragma unroll 4
+      for (uint32_t q = 0; q < kCrcSeg / 4; q++) {
+        int64_t p = p0 + 4 * q;
+        uint32_t w = 0;
+        if (p > -4) {
+          w = lds_u32(lds, int32_t(int64_t(msg) + p));
+          if (p < 0) w &= 0xFFFFFFFFu << (8 * uint32_t(-p));
+          if (p < 4) {  // init fold: bytes at message positions 0..3 ^= 0xFF
+            uint32_t m = 0;
+            for (int b = 0; b < 4; b++) {
+              int64_t pos = p + b;
+              if (pos >= 0 && pos < 4) m |= 0xFFu << (8 * b);
+            }
+            w ^= m;
+          }
+        }
+        c = crc_word(tab, c, w);
+      }
+    }
+    acc ^= c;
+  }
+  uint32_t v = gf2_mulmod(acc, g_crc_shift.lane[lane]);
+  return ~wave_xor(v);
+}
+
+// ------------------------------------------------------------- Snappy decode
+// golang/snappy v0.0.4 decode (decode_other.go), one wavefront: the tag walk is
+// wave-uniform (scalar values), each literal/copy is spread over the 64 lanes.
+// Returns SLATE_OK or SLATE_E_SNAPPY_CORRUPT.
+__device__ int wave_snappy_decode(const uint8_t* src, uint32_t sn, uint32_t s, uint8_t* dst, uint32_t dn,
+                                  int lane) {
+  uint32_t d = 0;
+  while (s < sn) {
+    uint32_t c = __builtin_amdgcn_readfirstlane(src[s]);
+    uint32_t t = c & 3;
+    if (t == 0) {
+      uint32_t x = c >> 2;
+      if (x < 60) {
+        s += 1;
+      } else {
+        uint32_t nb = x - 59;
+        s += 1 + nb;
+        if (s > sn) return SLATE_E_SNAPPY_CORRUPT;
+        x = 0;
+        for (uint32_t k = 0; k < nb; k++) x |= uint32_t(src[s - nb + k]) << (8 * k);
+        x = __builtin_amdgcn_readfirstlane(x);
+      }
+      uint64_t len = uint64_t(x) + 1;
+      if (len > uint64_t(dn - d) || len > uint64_t(sn - s)) return SLATE_E_SNAPPY_CORRUPT;
+      for (uint32_t j = lane; j < uint32_t(len); j += kWave) dst[d + j] = src[s + j];
+      d += uint32_t(len);
+      s += uint32_t(len);
+      continue;
+    }
+    uint32_t len, off;
+    if (t == 1) {
+      s += 2;
+      if (s > sn) return SLATE_E_SNAPPY_CORRUPT;
+      len = 4 + ((c >> 2) & 7);
+      off = ((c & 0xe0) << 3) | __builtin_amdgcn_readfirstlane(src[s - 1]);
+    } else if (t == 2) {
+      s += 3;
+      if (s > sn) return SLATE_E_SNAPPY_CORRUPT;
+      len = 1 + (c >> 2);
+      off = __builtin_amdgcn_readfirstlane(uint32_t(src[s - 2]) | uint32_t(src[s - 1]) << 8);
+    } else {
+      s += 5;
+      if (s > sn) return SLATE_E_SNAPPY_CORRUPT;
+      len = 1 + (c >> 2);
+      off = __builtin_amdgcn_readfirstlane(uint32_t(src[s - 4]) | uint32_t(src[s - 3]) << 8 |
+                                           uint32_t(src[s - 2]) << 16 | uint32_t(src[s - 1]) << 24);
+    }
+    if (off == 0 || d < off || len > dn - d) return SLATE_E_SNAPPY_CORRUPT;
+    if (off >= len) {
+      if (uint32_t(lane) < len) dst[d + lane] = dst[d - off + lane];
+    } else {
+      // forward byte-by-byte semantics: byte j repeats the off-byte pattern
+      for (uint32_t j = lane; j < len; j += kWave) dst[d + j] = dst[d - off + (j % off)];
+    }
+    d += len;
+  }
+  return d == dn ? SLATE_OK : SLATE_E_SNAPPY_CORRUPT;
+}
+
+// ---------------------------------------------------------------- v0 rows
+// row.go:191-261 against firstKey of length fk (fk < 0: firstKey == nil).
+__device__ inline void decode_row(const uint8_t* data, uint32_t data_len, uint32_t off, int fk, slate_row& r,
+                                  uint32_t* suffix_len_out) {
+  r.row_off = off;
+  r.key_prefix_len = 0;
+  r.key_suffix_len = 0;
+  r.value_len = 0;
+  r.flags = 0;
+  r.meta_len = 0;
+  const uint8_t* p = data + off;
+  uint32_t n = data_len - off;
+  *suffix_len_out = 0;
+  if (n >= 4) {
+    r.key_prefix_len = ld_be16(p);
+    r.key_suffix_len = ld_be16(p + 2);
+  }
+  if (n < 13) { r.status = SLATE_E_ROW_TOO_SHORT; return; }
+  uint16_t pl = r.key_prefix_len, sl = r.key_suffix_len;
+  if (pl > uint16_t(fk < 0 ? 0 : fk)) { r.status = SLATE_E_ROW_PREFIX; return; }
+  uint32_t o = 4;
+  if (n - o < sl) { r.status = SLATE_E_ROW_SUFFIX; return; }
+  o += sl;
+  if (n - o < 9) { r.status = SLATE_E_ROW_PANIC; return; }
+  uint8_t flags = p[o + 8];
+  o += 9;
+  if (flags & 2) {
+    if (n - o < 8) { r.status = SLATE_E_ROW_EXPIRE; return; }
+    o += 8;
+  }
+  if (flags & 4) {
+    if (n - o < 8) { r.status = SLATE_E_ROW_CREATE; return; }
+    o += 8;
+  }
+  if ((flags & 1) == 0) {
+    if (n - o < 4) { r.status = SLATE_E_ROW_VALUE_LEN; return; }
+    uint32_t vl = ld_be32(p + o);
+    o += 4;
+    if (n - o < vl) { r.status = SLATE_E_ROW_VALUE; return; }
+    r.value_len = vl;
+  }
+  r.flags = flags & 7;
+  r.meta_len = uint8_t(o - 4 - sl);
+  r.status = SLATE_OK;
+  *suffix_len_out = sl;
+}
+
+// ------------------------------------------------------------ one block
+struct WaveBufs {
+  const uint32_t* tab;  // CRC tables in LDS (4 x 256)
+  uint8_t* in;          // staging for the encoded block (in_cap bytes, 16-aligned)
+  uint8_t* out;         // decoded block (out_cap bytes, 16-aligned)
+  uint32_t in_cap, out_cap;
+};
+
+__device__ inline void write_meta(slate_block_meta* m, const slate_block_meta& v, int lane) {
+  if (lane == 0) *m = v;
+}
+
+// Returns false when the block does not fit this wave's LDS budget (caller defers it).
+__device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBufs& w, int lane, bool defer_large) {
+  slate_block_meta m{};
+  uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
+  const uint8_t* gin = a.in + s0;
+  if (len < 6) {
+    m.status = SLATE_E_BLOCK_TOO_SMALL;
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  uint32_t hdr = 0;
+  uint64_t dl = 0;
+  const bool dl_ok = decoded_len(a.codec, gin, len, &dl, &hdr);
+  uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
+  if (shift + len > w.in_cap || (a.codec != SLATE_CODEC_NONE && dl > w.out_cap)) {
+    if (defer_large) return false;
+    m.status = SLATE_E_CAPACITY;  // beyond the large kernel's LDS budget
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  // ---- stage the encoded block into LDS with aligned 16-byte loads
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(gin - shift);
+    uint4* dst = reinterpret_cast<uint4*>(w.in);
+    uint32_t chunks = uint32_t((shift + len + 15) / 16);
+    for (uint32_t c = lane; c < chunks; c += kWave) dst[c] = src[c];
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // LDS stores visible to the whole wave (in-order LDS)
+  __builtin_amdgcn_wave_barrier();
+  uint32_t clen = uint32_t(len - 4);
+  uint32_t stored = ld_be32(w.in + shift + clen);
+  uint32_t crc = wave_crc32(w.tab, w.in, shift, clen, lane);
+  if (stored != crc) {
+    m.status = SLATE_E_BLOCK_CHECKSUM;
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  // ---- decompress (compress.Decode, compression.go:126-157)
+  const uint8_t* buf;  // decoded buffer in LDS
+  uint32_t n;
+  if (a.codec == SLATE_CODEC_NONE) {
+    buf = w.in + shift;
+    n = clen;
+  } else if (a.codec == SLATE_CODEC_SNAPPY) {
+    if (!dl_ok) {  // corrupt varint header or provably corrupt length
+      m.status = SLATE_E_SNAPPY_CORRUPT;
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    int st = wave_snappy_decode(w.in + shift, clen, hdr, w.out, uint32_t(dl), lane);
+    if (st != SLATE_OK) {
+      m.status = int16_t(st);
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    buf = w.out;
+    n = uint32_t(dl);
+  } else {
+    m.status = (a.codec >= SLATE_CODEC_ZLIB && a.codec <= SLATE_CODEC_ZSTD) ? SLATE_E_CODEC_UNSUPPORTED
+                                                                               : SLATE_E_INVALID_CODEC;
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ---- write the decoded buffer back (16-aligned destination)
+  {
+    uint8_t* gout = a.out + a.out_off[b];
+    uint32_t chunks = (n + 15) / 16;
+    if (buf == w.out) {
+      const uint4* s = reinterpret_cast<const uint4*>(buf);
+      for (uint32_t c = lane; c < chunks; c += kWave) reinterpret_cast<uint4*>(gout)[c] = s[c];
+    } else {
+      uint32_t base = uint32_t(buf - w.in);
+      for (uint32_t c = lane; c < chunks; c += kWave) {
+        int32_t o = int32_t(base + 16 * c);
+        uint4 v;
+        v.x = lds_u32(w.in, o);
+        v.y = lds_u32(w.in, o + 4);
+        v.z = lds_u32(w.in, o + 8);
+        v.w = lds_u32(w.in, o + 12);
+        reinterpret_cast<uint4*>(gout)[c] = v;
+      }
+    }
+  }
+  // ---- block.Decode structure checks (block.go:95-131)
+  if (n < 2) {
+    m.status = SLATE_E_BLOCK_UNCOMP_SMALL;
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  uint32_t cnt = ld_be16(buf + n - 2);
+  int64_t osi = int64_t(n) - 2 - 2 * int64_t(cnt);
+  if (osi <= 0) {
+    m.status = SLATE_E_BLOCK_INDEX_OFFSET;
+    m.detail = int32_t(osi);
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  uint16_t osi16 = uint16_t(osi);
+  uint32_t bad = 0xFFFFFFFFu;  // first offset index exceeding uint16(offsetStartIndex)
+  for (uint32_t i = lane; i < cnt; i += kWave) {
+    if (ld_be16(buf + osi + 2 * i) > osi16 && i < bad) bad = i;
+  }
+  for (int o = 32; o >= 1; o >>= 1) bad = min(bad, uint32_t(__shfl_xor(int(bad), o, 64)));
+  if (bad != 0xFFFFFFFFu) {
+    m.status = SLATE_E_BLOCK_OFFSET_BOUNDS;
+    m.aux = uint16_t(bad);
+    m.detail = ld_be16(buf + osi + 2 * bad);
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  m.data_len = uint32_t(osi);
+  m.n_rows = uint16_t(cnt);
+  if (cnt == 0) {
+    m.status = SLATE_E_BLOCK_NO_OFFSETS;
+    write_meta(&a.meta[b], m, lane);
+    return true;
+  }
+  // FirstKey quirk (block.go:130-131): uint16 arithmetic, panics out of range
+  {
+    uint32_t off0 = ld_be16(buf + osi);
+    if (uint64_t(osi) - off0 < 2) {
+      m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    uint16_t kl = ld_be16(buf + off0);
+    uint16_t lo = uint16_t(off0 + 2), hi = uint16_t(off0 + 2 + kl);
+    if (lo > hi || hi > n) {
+      m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    m.aux = kl;
+  }
+  // ---- row descriptors
+  uint64_t rb = a.row_base[b];
+  uint32_t rcap = uint32_t(min(uint64_t(0xFFFFFFFFu), a.row_base[b + 1] - rb));
+  uint32_t nr = cnt;
+  if (nr > rcap) {
+    nr = rcap;
+    m.flags |= SLATE_BLKF_ROWS_TRUNCATED;
+  }
+  int fk = -1;
+  {
+    slate_row r0;
+    uint32_t sl0;
+    decode_row(buf, uint32_t(osi), ld_be16(buf + osi), -1, r0, &sl0);
+    if (r0.status == SLATE_OK) fk = int(sl0);
+  }
+  slate_row* grows = a.rows + rb;
+  for (uint32_t i = lane; i < nr; i += kWave) {
+    slate_row r;
+    uint32_t sl;
+    decode_row(buf, uint32_t(osi), ld_be16(buf + osi + 2 * i), i == 0 ? -1 : fk, r, &sl);
+    grows[i] = r;
+  }
+  write_meta(&a.meta[b], m, lane);
+  return true;
+}
+
+constexpr uint32_t kTabBytes = 4096;
+
+__device__ inline void load_crc_tables(uint32_t* tab) {
+  const uint32_t* src = &g_crc_tables.t[0][0];
+  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t per_wave = kFastInCap + kFastOutCap;
+  WaveBufs w{tab, smem + kTabBytes + wave * per_wave, smem + kTabBytes + wave * per_wave + kFastInCap,
+             kFastInCap, kFastOutCap};
+  const uint32_t waves = gridDim.x * (kDecodeThreads / 64);
+  for (uint32_t b = blockIdx.x * (kDecodeThreads / 64) + wave; b < a.n; b += waves) {
+    if (!decode_block_wave(a, b, w, lane, true)) {
+      if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = b;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63;
+  WaveBufs w{tab, smem + kTabBytes, smem + kTabBytes + kLargeInCap, kLargeInCap, kLargeOutCap};
+  uint32_t count = *a.large_count;
+  for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) decode_block_wave(a, a.large_list[k], w, lane, false);
+}
+
+// --------------------------------------------------------------- launchers
+hipError_t decode_kernels_available() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&decode_fast_kernel));
+}
+
+size_t decode_scratch_bytes(uint32_t n) {
+  size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
+  return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t));
+}
+
+static DecodeScratch carve(void* scratch, uint32_t n) {
+  DecodeScratch s;
+  size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  s.pa = reinterpret_cast<uint64_t*>(p);
+  s.pb = s.pa + tiles;
+  p += align16(2 * tiles * sizeof(uint64_t));
+  s.large_count = reinterpret_cast<uint32_t*>(p);
+  p += 16;
+  s.large_list = reinterpret_cast<uint32_t*>(p);
+  s.tiles = uint32_t(tiles);
+  return s;
+}
+
+hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
+                              uint64_t* out_off, uint64_t* row_base, void* scratch) {
+  DecodeScratch s = carve(scratch, n);
+  uint32_t m = n + 1;
+  plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
+  scan_reduce_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
+  scan_partials_kernel<<<1, kScanThreads, 0, st>>>(s.pa, s.pb, s.tiles);
+  scan_apply_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratch, int num_cus) {
+  DecodeArgs a = args_in;
+  DecodeScratch s = carve(scratch, a.n);
+  a.large_list = s.large_list;
+  a.large_count = s.large_count;
+  (void)hipMemsetAsync(s.large_count, 0, sizeof(uint32_t), st);
+  if (a.n == 0) return hipGetLastError();
+  const size_t lds = kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap);
+  uint32_t wgs_needed = (a.n + kDecodeThreads / 64 - 1) / (kDecodeThreads / 64);
+  uint32_t grid = min(wgs_needed, uint32_t(num_cus) * kDecodeWgPerCu);
+  decode_fast_kernel<<<grid, kDecodeThreads, lds, st>>>(a);
+  const size_t lds_large = kTabBytes + size_t(kLargeInCap) + kLargeOutCap;
+  decode_large_kernel<<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace slate

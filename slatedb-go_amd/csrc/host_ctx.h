@@ -1,0 +1,63 @@
+// Host-side context: one device + one HIP stream + reusable device/pinned
+// buffers.  Each slate_ctx is used by one caller thread at a time; the library
+// keeps no global mutable state (SURVEY 8b "Threading").
+#pragma once
+#include <cstring>
+#include <vector>
+
+#include "kernels.h"
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = n < 4096 ? 4096 : n + n / 4;
+    hipError_t e = hipMalloc(&p, c);
+    if (e != hipSuccess) return e;
+    cap = c;
+    return hipSuccess;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct slate_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  // decode batch buffers
+  DevBuf d_in, d_in_off, d_out, d_out_off, d_meta, d_rows, d_row_base, d_scratch;
+  // encode / misc buffers
+  DevBuf e_a, e_b, e_c, e_d, e_e, e_f, e_g, e_h, e_i, e_j;
+  void release_all() {
+    for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
+                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j})
+      b->release();
+  }
+};
+
+#define SLATE_HIP(expr)                                   \
+  do {                                                    \
+    hipError_t _e = (expr);                               \
+    if (_e != hipSuccess) return hip_status(_e);          \
+  } while (0)
+
+inline int hip_status(hipError_t e) {
+  if (e == hipErrorOutOfMemory) return SLATE_E_OOM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorNoBinaryForGpu ||
+      e == hipErrorInvalidDeviceFunction)
+    return SLATE_E_NO_DEVICE;
+  return SLATE_E_HIP;
+}
+
+inline hipError_t ctx_bind(slate_ctx* ctx) { return hipSetDevice(ctx->device); }

@@ -1,0 +1,45 @@
+// Kernel launch interfaces shared between the HIP translation units and the
+// C-ABI host code.
+#pragma once
+#include "common.h"
+
+namespace slate {
+
+// ---------------------------------------------------------------- decode
+constexpr int kDecodeThreads = 256;          // 4 wavefronts, one block each at a time
+constexpr uint32_t kDecodeWgPerCu = 4;       // LDS-limited residency (4 x 40 KiB)
+constexpr uint32_t kFastInCap = 4608;        // staged encoded block (incl. 16-byte misalignment)
+constexpr uint32_t kFastOutCap = 4608;       // decoded block
+constexpr uint32_t kLargeInCap = 65552;      // large-block kernel, one wave per workgroup
+constexpr uint32_t kLargeOutCap = 90112;
+
+struct DecodeArgs {
+  int codec;
+  const uint8_t* in;
+  const uint64_t* in_off;
+  uint32_t n;
+  uint8_t* out;
+  const uint64_t* out_off;
+  slate_block_meta* meta;
+  slate_row* rows;
+  const uint64_t* row_base;
+  uint32_t* large_list;   // filled by the launcher from scratch
+  uint32_t* large_count;
+};
+
+struct DecodeScratch {
+  uint64_t* pa;
+  uint64_t* pb;
+  uint32_t* large_count;
+  uint32_t* large_list;
+  uint32_t tiles;
+};
+
+size_t decode_scratch_bytes(uint32_t n);
+hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
+                              uint64_t* out_off, uint64_t* row_base, void* scratch);
+hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
+// Validates that the code object loads on the current device.
+hipError_t decode_kernels_available();
+
+}  // namespace slate

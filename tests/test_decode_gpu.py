@@ -1,0 +1,139 @@
+"""GPU parity: block decode through the HIP C-ABI vs the CPU oracle.
+
+Bit-exact on every field: plan layout (out_off / row_base), per-block meta
+(status, detail, aux, data_len, n_rows, flags), decoded bytes, row descriptors.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from tests import blockgen as bg
+from oracle import binding as ob
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import slatecodec as sc
+    return sc.Context(0)
+
+
+def _compare(ctx, codec, blocks, misalign=0):
+    blob, off = bg.pack(blocks, misalign)
+    g_out, g_off, g_meta, g_rows, g_rb = ctx.decode_batch(codec, blob, off)
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(codec, blob, off)
+    n = len(blocks)
+    assert np.array_equal(g_off, o_off), "plan: out_off"
+    assert np.array_equal(g_rb, o_rb), "plan: row_base"
+    for i in range(n):
+        gm, om = g_meta[i], o_meta[i]
+        assert gm.tobytes() == om.tobytes(), (i, gm, om, blocks[i][:32].hex())
+        st = int(om["status"])
+        if st == 0 or 3 <= st <= 7:
+            dl = bg.decoded_len(blocks[i], codec)
+            a, b = int(o_off[i]), int(o_off[i]) + dl
+            assert g_out[a:b].tobytes() == o_out[a:b].tobytes(), i
+        if st == 0:
+            r0 = int(o_rb[i])
+            nr = min(int(om["n_rows"]), int(o_rb[i + 1]) - r0)
+            assert g_rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+    return g_meta
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+def test_reference_fixture_blocks(ctx, ref_vectors, codec):
+    blocks = []
+    for c in ref_vectors["block_roundtrips"]:
+        bb = ob.BlockBuilder(c["block_size"])
+        for k, v in c["kvs"]:
+            bb.add_value(k.encode(), (v or "").encode())
+        data, offs, _ = bb.build()
+        blocks.append(ob.block_encode(data, offs, codec)[1])
+    meta = _compare(ctx, codec, blocks)
+    assert (meta["status"] == 0).all()
+
+
+def test_reference_corrupt_blocks(ctx, ref_vectors):
+    from tests.test_oracle import _corrupt
+    v = ref_vectors["corrupt_block"]
+    bb = ob.BlockBuilder(v["block_size"])
+    for k, val in v["kvs"]:
+        bb.add_value(k.encode(), val.encode())
+    data, offs, _ = bb.build()
+    enc = ob.block_encode(data, offs, ob.NONE)[1]
+    blocks = [_corrupt(enc, c["mutation"]) for c in v["cases"]]
+    meta = _compare(ctx, ob.NONE, blocks)
+    import slatecodec as sc
+    for c, m in zip(v["cases"], meta):
+        assert c["error"] in sc.status_string(int(m["status"])), c["name"]
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+@pytest.mark.parametrize("seed", range(4))
+def test_random_ssts(ctx, codec, seed):
+    rng = random.Random(seed)
+    kvs = bg.random_kvs(rng, rng.randint(200, 2000), alphabet=rng.choice([4, 256]))
+    blocks = bg.sst_blocks(kvs, rng.choice([64, 512, 4096]), codec)
+    meta = _compare(ctx, codec, blocks, misalign=rng.randrange(16))
+    assert (meta["status"] == 0).all()
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+@pytest.mark.parametrize("fix_crc", [False, True])
+def test_random_corruption(ctx, codec, fix_crc):
+    rng = random.Random(1000 + codec * 2 + fix_crc)
+    kvs = bg.random_kvs(rng, 3000, alphabet=8)
+    blocks = bg.sst_blocks(kvs, 1024, codec)
+    bad = [bg.mutate(rng, b, fix_crc) for b in blocks]
+    meta = _compare(ctx, codec, bad + blocks[:5])
+    assert len(set(meta["status"].tolist())) > 1
+
+
+def test_edge_lengths(ctx):
+    blocks = [b"", b"\x00", b"\x00" * 5, bg.recrc(b"\x00\x00"), bg.recrc(b"\x00\x01"), bg.recrc(b"\x00\x00\x00"),
+              bg.recrc(b"\xff\xff\x00\x00"), bg.recrc(b"\x00\x00\x00\x00\x00\x01")]
+    _compare(ctx, ob.NONE, blocks)
+    sn = [bg.recrc(b"\x00"), bg.recrc(b"\x02\x04ab"), bg.recrc(b"\xff" * 11), bg.recrc(b"\x80"),
+          bg.recrc(b"\x05\x00a\x01\x01"), bg.recrc(b"\x7f\x00a")]
+    _compare(ctx, ob.SNAPPY, sn)
+
+
+def test_empty_batch(ctx):
+    out, off, meta, rows, rb = ctx.decode_batch(ob.NONE, np.zeros(16, np.uint8), np.zeros(1, np.uint64))
+    assert len(meta) == 0 and off[0] == 0
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+def test_large_blocks(ctx, codec):
+    """Blocks beyond the fast kernel's LDS budget go through decode_large_kernel."""
+    rng = random.Random(5)
+    kvs = [(b"big%05d" % i, bytes(rng.randrange(4) for _ in range(rng.choice([100, 6000, 20000]))))
+           for i in range(40)]
+    blocks = bg.sst_blocks(kvs, 32768, codec)
+    assert max(len(b) for b in blocks) > 4608 or codec == ob.SNAPPY
+    meta = _compare(ctx, codec, blocks)
+    assert (meta["status"] == 0).all()
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+def test_vhalf_workload(ctx, codec):
+    """The bench workload shape (38 rows x 100 B KV per 4 KiB block) at 2000 blocks."""
+    kvs = bg.kv_synthetic(38 * 2000, half=True, tomb_every=20)
+    blocks = bg.sst_blocks(kvs, 4096, codec)
+    meta = _compare(ctx, codec, blocks)
+    assert (meta["status"] == 0).all()
+
+
+def test_single_block_api(ctx, ref_vectors):
+    bb = ob.BlockBuilder(4096)
+    for k, v in (("key1", "value1"), ("key2", "value2")):
+        bb.add_value(k.encode(), v.encode())
+    data, offs, _ = bb.build()
+    for codec in (ob.NONE, ob.SNAPPY):
+        enc = ob.block_encode(data, offs, codec)[1]
+        st, m, d, o = ctx.block_decode(enc, codec)
+        assert st == 0 and d == data and o == offs
+        st, m, d, o = ctx.block_decode(enc[:-1] + bytes([enc[-1] ^ 1]), codec)
+        assert st == 2
