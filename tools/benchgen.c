@@ -1,0 +1,127 @@
+/* Bench input tooling (not product, not oracle): compress a batch of decoded
+ * blocks with the C++ snappy library in /opt/conda (dlopen) and append the
+ * block CRC32 trailer (block.go:54-75 layout), in parallel.  Used only to
+ * synthesise encoded Snappy blocks for bench.py's workload. */
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+typedef int (*compress_fn)(const char*, size_t, char*, size_t*);
+static compress_fn g_compress;
+static uint32_t g_tab[256];
+
+static uint32_t crc32(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = g_tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return ~c;
+}
+
+int bg_init(const char* libsnappy) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+    g_tab[i] = c;
+  }
+  void* h = dlopen(libsnappy, RTLD_NOW);
+  if (!h) return -1;
+  g_compress = (compress_fn)dlsym(h, "snappy_compress");
+  return g_compress ? 0 : -2;
+}
+
+typedef struct {
+  int codec; const uint8_t* src; const uint64_t* src_off; uint8_t* dst; uint64_t stride; uint64_t* dst_len;
+  uint64_t lo, hi; int rc;
+} job_t;
+
+static void* work(void* arg) {
+  job_t* j = (job_t*)arg;
+  for (uint64_t i = j->lo; i < j->hi; i++) {
+    const uint8_t* s = j->src + j->src_off[i];
+    size_t n = j->src_off[i + 1] - j->src_off[i];
+    uint8_t* d = j->dst + i * j->stride;
+    size_t cl = j->stride - 4;
+    if (j->codec == 0) { memcpy(d, s, n); cl = n; }
+    else if (g_compress((const char*)s, n, (char*)d, &cl) != 0) { j->rc = -3; return NULL; }
+    uint32_t c = crc32(d, cl);
+    d[cl] = (uint8_t)(c >> 24); d[cl + 1] = (uint8_t)(c >> 16); d[cl + 2] = (uint8_t)(c >> 8); d[cl + 3] = (uint8_t)c;
+    j->dst_len[i] = cl + 4;
+  }
+  return NULL;
+}
+
+/* dst has n slots of `stride` bytes; dst_len receives each encoded length. */
+int bg_encode_blocks(int codec, const uint8_t* src, const uint64_t* src_off, uint64_t n, uint8_t* dst,
+                     uint64_t stride, uint64_t* dst_len, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  pthread_t th[64];
+  job_t jobs[64];
+  for (int t = 0; t < nthreads; t++) {
+    job_t jb = {codec, src, src_off, dst, stride, dst_len, n * t / nthreads, n * (t + 1) / nthreads, 0};
+    jobs[t] = jb;
+    pthread_create(&th[t], NULL, work, &jobs[t]);
+  }
+  int rc = 0;
+  for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
+  return rc;
+}
+
+/* Decoded v0 blocks for the SURVEY 8d synthetic KVs: key i = "k%015d", value =
+ * r_i || r_i (half) or r_i (84 random bytes), greedy block fill of
+ * block.Builder.Add (block.go:162-182) with prefix compression against each
+ * block's first key.  out receives blocks back to back (rows || BE16 offsets ||
+ * BE16 count); returns the number of blocks. */
+static void put16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+uint64_t bg_build_blocks(uint64_t kv_begin, uint64_t n_kv, const uint8_t* rv, uint32_t rv_len, int half,
+                         uint64_t block_size, uint8_t* out, uint64_t* out_off, uint64_t max_blocks) {
+  char first[17], key[17];
+  uint32_t vlen = half ? 2 * rv_len : rv_len;
+  uint64_t nb = 0, pos = 0;
+  uint64_t i = 0;
+  uint16_t offs[65536];
+  while (i < n_kv && nb < max_blocks) {
+    out_off[nb] = pos;
+    uint8_t* blk = out + pos;
+    uint32_t n = 0, dlen = 0;
+    for (; i < n_kv; i++) {
+      snprintf(key, sizeof key, "k%015llu", (unsigned long long)(kv_begin + i));
+      uint32_t p = 0;
+      if (n) while (p < 16 && first[p] == key[p]) p++;
+      uint32_t row = 4 + (16 - p) + 9 + 4 + vlen;
+      if ((uint64_t)2 + 2 * n + dlen + 2 + row > block_size && n) break;
+      uint8_t* r = blk + dlen;
+      put16(r, p); put16(r + 2, 16 - p);
+      memcpy(r + 4, key + p, 16 - p);
+      memset(r + 4 + 16 - p, 0, 9);
+      uint8_t* v = r + 4 + 16 - p + 9;
+      v[0] = (uint8_t)(vlen >> 24); v[1] = (uint8_t)(vlen >> 16); v[2] = (uint8_t)(vlen >> 8); v[3] = (uint8_t)vlen;
+      memcpy(v + 4, rv + i * rv_len, rv_len);
+      if (half) memcpy(v + 4 + rv_len, rv + i * rv_len, rv_len);
+      offs[n++] = (uint16_t)dlen;
+      dlen += row;
+      if (n == 1) memcpy(first, key, 17);
+    }
+    for (uint32_t k = 0; k < n; k++) put16(blk + dlen + 2 * k, offs[k]);
+    put16(blk + dlen + 2 * n, n);
+    pos += dlen + 2 * n + 2;
+    nb++;
+  }
+  out_off[nb] = pos;
+  return nb;
+}
+
+/* Pack fixed-stride slots into a contiguous blob; blob_off[n] = total. */
+void bg_compact(const uint8_t* slots, uint64_t stride, const uint64_t* len, uint64_t n, uint8_t* blob,
+                uint64_t* blob_off) {
+  uint64_t p = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    blob_off[i] = p;
+    memcpy(blob + p, slots + i * stride, len[i]);
+    p += len[i];
+  }
+  blob_off[n] = p;
+}

@@ -1,0 +1,74 @@
+"""Synthetic SST-block workloads for bench.py, built with
+tools/benchgen.c: keys b"k%015d", 84-byte values (V-half r||r from
+numpy.random.default_rng(20250307), or V-rand), BlockSize 4096, then Snappy
+(C++ libsnappy from /opt/conda) or None, plus the block CRC32 trailer."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libbenchgen.so")
+LIBSNAPPY = "/opt/conda/lib/libsnappy.so.1"
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = C.CDLL(LIB)
+        L.bg_init.argtypes = [C.c_char_p]
+        L.bg_build_blocks.restype = C.c_uint64
+        L.bg_build_blocks.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_int, C.c_uint64,
+                                      C.c_void_p, C.c_void_p, C.c_uint64]
+        L.bg_encode_blocks.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                       C.c_void_p, C.c_int]
+        L.bg_compact.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        rc = L.bg_init(LIBSNAPPY.encode())
+        if rc != 0:
+            raise RuntimeError(f"benchgen: cannot load {LIBSNAPPY} ({rc})")
+        _lib = L
+    return _lib
+
+
+def decoded_blocks(n_blocks: int, seed: int = 20250307, half: bool = True, block_size: int = 4096,
+                   kv_begin: int = 0):
+    """-> (decoded blob uint8, offsets uint64[n+1]) for exactly n_blocks blocks."""
+    kv_per_block = 40  # >= rows per 4 KiB block for 100-byte KVs (38 typical)
+    n_kv = n_blocks * kv_per_block + 64
+    rng = np.random.default_rng(seed)
+    rv = rng.integers(0, 256, (n_kv, 42 if half else 84), dtype=np.uint8)
+    out = np.empty(n_blocks * (block_size + 256), np.uint8)
+    off = np.zeros(n_blocks + 1, np.uint64)
+    nb = lib().bg_build_blocks(kv_begin, n_kv, rv.ctypes.data, rv.shape[1], int(half), block_size,
+                               out.ctypes.data, off.ctypes.data, n_blocks)
+    assert nb == n_blocks, (nb, n_blocks)
+    return out[: int(off[nb])], off
+
+
+def encode_blocks(codec: int, dec: np.ndarray, dec_off: np.ndarray, threads: int = 16):
+    n = len(dec_off) - 1
+    lens = np.diff(dec_off.astype(np.int64))
+    stride = int(lens.max()) + int(lens.max()) // 6 + 64
+    slots = np.empty(n * stride, np.uint8)
+    elen = np.zeros(n, np.uint64)
+    rc = lib().bg_encode_blocks(codec, dec.ctypes.data, dec_off.ctypes.data, n, slots.ctypes.data, stride,
+                                elen.ctypes.data, threads)
+    assert rc == 0, rc
+    blob = np.empty(int(elen.sum()) + 16, np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    lib().bg_compact(slots.ctypes.data, stride, elen.ctypes.data, n, blob.ctypes.data, off.ctypes.data)
+    return blob, off
+
+
+def snappy_vhalf(n_blocks: int, codec: int = 1, seed: int = 20250307, half: bool = True, threads: int = 16,
+                 kv_begin: int = 0):
+    dec, doff = decoded_blocks(n_blocks, seed=seed, half=half, kv_begin=kv_begin)
+    blob, off = encode_blocks(codec, dec, doff, threads)
+    return blob, off, int(doff[-1])
