@@ -76,7 +76,10 @@ def main():
     enc_bytes = int(in_off[-1])
 
     ctx = sc.Context(local)
-    stream = torch.cuda.current_stream(device)
+    # An explicit (non-null) stream: the C-ABI launches on it and the HIP events
+    # that time the decode kernel are recorded on it.
+    stream = torch.cuda.Stream(device)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     d_in = torch.from_numpy(blob).to(device)

@@ -125,7 +125,7 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
   SLATE_HIP(ctx_bind(ctx));
   // the scratch is owned by the context for the device-resident call
   SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes(n)));
-  DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr};
+  DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
   SLATE_HIP(launch_decode(ctx->stream, a, ctx->d_scratch.p, ctx->num_cus));
   return SLATE_OK;
 }
@@ -162,7 +162,7 @@ int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const
   SLATE_HIP(ctx->d_rows.ensure((total_rows + 1) * sizeof(slate_row)));
   DecodeArgs a{codec, ctx->d_in.as<uint8_t>(), ctx->d_in_off.as<uint64_t>(), n, ctx->d_out.as<uint8_t>(),
                ctx->d_out_off.as<uint64_t>(), ctx->d_meta.as<slate_block_meta>(), ctx->d_rows.as<slate_row>(),
-               ctx->d_row_base.as<uint64_t>(), nullptr, nullptr};
+               ctx->d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
   SLATE_HIP(launch_decode(st, a, ctx->d_scratch.p, ctx->num_cus));
   if (total_out) SLATE_HIP(hipMemcpyAsync(out, ctx->d_out.p, total_out, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipMemcpyAsync(meta, ctx->d_meta.p, size_t(n) * sizeof(slate_block_meta), hipMemcpyDeviceToHost, st));

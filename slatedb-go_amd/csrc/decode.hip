@@ -19,13 +19,14 @@
 //                         offset checks, row descriptors, aligned write-back
 //   decode_large_kernel   same device code for blocks that exceed the fast
 //                         kernel's LDS budget (one wave per workgroup, ~150 KiB LDS)
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
+#include "encode.h"
+#include "wave_crc.h"
 
 namespace slate {
-
-__constant__ CrcTables g_crc_tables = CrcTables();
-__constant__ CrcShift g_crc_shift = CrcShift();
 
 // ------------------------------------------------------------------ sizes
 // golang/snappy decode.go decodedLen: binary.Uvarint, n <= 0 || v > 0xffffffff
@@ -121,7 +122,7 @@ __global__ void scan_reduce_kernel(const uint64_t* __restrict__ a, const uint64_
   uint64_t sa = 0, sb = 0;
   for (int k = 0; k < kScanItems; k++) {
     uint64_t i = base + uint64_t(k) * kScanThreads + threadIdx.x;
-    if (i < n) { sa += a[i]; sb += b[i]; }
+    if (i < n) { sa += a[i]; if (b) sb += b[i]; }
   }
   uint64_t ta, tb;
   block_exclusive_scan(sa, sh[0], &ta);
@@ -153,7 +154,7 @@ __global__ void scan_apply_kernel(uint64_t* __restrict__ a, uint64_t* __restrict
   for (int k = 0; k < kScanItems; k++) {
     uint64_t i = base + k;
     va[k] = i < n ? a[i] : 0;
-    vb[k] = i < n ? b[i] : 0;
+    vb[k] = (b && i < n) ? b[i] : 0;
     sa += va[k];
     sb += vb[k];
   }
@@ -162,71 +163,10 @@ __global__ void scan_apply_kernel(uint64_t* __restrict__ a, uint64_t* __restrict
   uint64_t eb = block_exclusive_scan(sb, sh[1], &tb) + pb[blockIdx.x];
   for (int k = 0; k < kScanItems; k++) {
     uint64_t i = base + k;
-    if (i < n) { a[i] = ea; b[i] = eb; }
+    if (i < n) { a[i] = ea; if (b) b[i] = eb; }
     ea += va[k];
     eb += vb[k];
   }
-}
-
-// ------------------------------------------------------------ LDS helpers
-// 4 bytes at an arbitrary byte offset of a 4-aligned LDS buffer (little-endian).
-__device__ inline uint32_t lds_u32(const uint8_t* base, int32_t off) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (off & ~3));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], uint32_t(off) & 3u);
-}
-
-__device__ inline uint32_t wave_xor(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
-  return v;
-}
-
-__device__ inline uint32_t crc_word(const uint32_t* tab, uint32_t c, uint32_t w) {
-  c ^= w;
-  return tab[768 + (c & 0xff)] ^ tab[512 + ((c >> 8) & 0xff)] ^ tab[256 + ((c >> 16) & 0xff)] ^ tab[c >> 24];
-}
-
-// crc32.ChecksumIEEE of msg[0..n) staged in LDS, computed by one wavefront.
-// 64 lanes x 64-byte segments per 4 KiB stripe, end-aligned so each lane's
-// shift factor x^(8*64*(63-l)) is a compile-time constant; the 0xFFFFFFFF init
-// is folded in by xoring the first four message bytes with 0xFF.
-__device__ uint32_t wave_crc32(const uint32_t* tab, const uint8_t* lds, uint32_t msg, uint32_t n, int lane) {
-  if (n < 4) {  // tiny message: lane-uniform bytewise loop
-    uint32_t c = 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < n; i++) c = tab[(c ^ lds[msg + i]) & 0xff] ^ (c >> 8);
-    return ~c;
-  }
-  uint32_t stripes = (n + kCrcStripe - 1) / kCrcStripe;
-  uint32_t acc = 0;
-  for (uint32_t k = 0; k < stripes; k++) {
-    if (k) acc = gf2_mulmod(acc, g_crc_shift.stripe);
-    // segment start relative to the message (may be negative)
-    int64_t p0 = int64_t(n) - int64_t(stripes - k) * kCrcStripe + int64_t(lane) * kCrcSeg;
-    uint32_t c = 0;
-    if (p0 + int64_t(kCrcSeg) > 0) {
-#pragma unroll 4
-      for (uint32_t q = 0; q < kCrcSeg / 4; q++) {
-        int64_t p = p0 + 4 * q;
-        uint32_t w = 0;
-        if (p > -4) {
-          w = lds_u32(lds, int32_t(int64_t(msg) + p));
-          if (p < 0) w &= 0xFFFFFFFFu << (8 * uint32_t(-p));
-          if (p < 4) {  // init fold: bytes at message positions 0..3 ^= 0xFF
-            uint32_t m = 0;
-            for (int b = 0; b < 4; b++) {
-              int64_t pos = p + b;
-              if (pos >= 0 && pos < 4) m |= 0xFFu << (8 * b);
-            }
-            w ^= m;
-          }
-        }
-        c = crc_word(tab, c, w);
-      }
-    }
-    acc ^= c;
-  }
-  uint32_t v = gf2_mulmod(acc, g_crc_shift.lane[lane]);
-  return ~wave_xor(v);
 }
 
 // ------------------------------------------------------------- Snappy decode
@@ -378,7 +318,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   __builtin_amdgcn_wave_barrier();
   uint32_t clen = uint32_t(len - 4);
   uint32_t stored = ld_be32(w.in + shift + clen);
-  uint32_t crc = wave_crc32(w.tab, w.in, shift, clen, lane);
+  uint32_t crc = (a.debug & 1) ? stored : wave_crc32(w.tab, w.in, int32_t(shift), clen, lane);
   if (stored != crc) {
     m.status = SLATE_E_BLOCK_CHECKSUM;
     write_meta(&a.meta[b], m, lane);
@@ -396,7 +336,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
       write_meta(&a.meta[b], m, lane);
       return true;
     }
-    int st = wave_snappy_decode(w.in + shift, clen, hdr, w.out, uint32_t(dl), lane);
+    int st = (a.debug & 2) ? SLATE_OK : wave_snappy_decode(w.in + shift, clen, hdr, w.out, uint32_t(dl), lane);
     if (st != SLATE_OK) {
       m.status = int16_t(st);
       write_meta(&a.meta[b], m, lane);
@@ -412,7 +352,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   }
   __builtin_amdgcn_wave_barrier();
   // ---- write the decoded buffer back (16-aligned destination)
-  {
+  if (!(a.debug & 8)) {
     uint8_t* gout = a.out + a.out_off[b];
     uint32_t chunks = (n + 15) / 16;
     if (buf == w.out) {
@@ -498,6 +438,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     if (r0.status == SLATE_OK) fk = int(sl0);
   }
   slate_row* grows = a.rows + rb;
+  if (a.debug & 4) nr = 0;
   for (uint32_t i = lane; i < nr; i += kWave) {
     slate_row r;
     uint32_t sl;
@@ -506,14 +447,6 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   }
   write_meta(&a.meta[b], m, lane);
   return true;
-}
-
-constexpr uint32_t kTabBytes = 4096;
-
-__device__ inline void load_crc_tables(uint32_t* tab) {
-  const uint32_t* src = &g_crc_tables.t[0][0];
-  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];
-  __syncthreads();
 }
 
 __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs a) {
@@ -578,8 +511,22 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
   return hipGetLastError();
 }
 
+size_t scan_scratch_bytes(uint32_t m) { return 2 * size_t((m + kScanTile - 1) / kScanTile + 1) * sizeof(uint64_t); }
+
+hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t m, void* scratch) {
+  uint32_t tiles = (m + kScanTile - 1) / kScanTile;
+  uint64_t* pa = static_cast<uint64_t*>(scratch);
+  uint64_t* pb = pa + tiles + 1;
+  scan_reduce_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
+  scan_partials_kernel<<<1, kScanThreads, 0, st>>>(pa, pb, tiles);
+  scan_apply_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
+  return hipGetLastError();
+}
+
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratch, int num_cus) {
   DecodeArgs a = args_in;
+  const char* dbg = getenv("SLATE_DEBUG_MODE");  // profiling ablations only
+  a.debug = dbg ? uint32_t(strtoul(dbg, nullptr, 0)) : 0u;
   DecodeScratch s = carve(scratch, a.n);
   a.large_list = s.large_list;
   a.large_count = s.large_count;

@@ -1,0 +1,56 @@
+// Encode-side kernel interfaces (SST builder, bloom, large-buffer CRC).
+#pragma once
+#include "common.h"
+
+namespace slate {
+
+constexpr int kPackThreads = 256;        // 4 wavefronts, one block each
+constexpr uint32_t kPackCap = 8192;      // LDS bytes per wavefront for one encoded block
+constexpr uint32_t kPackBigCap = 155648; // one wavefront per workgroup
+
+struct EncodeArgs {
+  const uint8_t* keys;
+  const uint64_t* key_off;
+  const uint8_t* vals;
+  const uint64_t* val_off;
+  const uint8_t* tomb;  // 1 = KindTombStone
+  uint32_t n;
+  uint64_t block_size;
+  int codec;
+};
+
+// Device work buffers for one encode batch (sized by the host for n KVs).
+struct EncodeBufs {
+  uint64_t* hashes;      // [n] FNV-1 64 of every key (bloom input), appended per batch
+  uint32_t* adj;         // [n]
+  uint32_t* next;        // [n]
+  uint64_t* bytes;       // [n]
+  uint32_t* exit_pos;    // [n]
+  uint32_t* entry;       // [chunks]
+  uint32_t* starts_tmp;  // [n]
+  uint64_t* counts;      // [chunks + 1] -> exclusive scan = chunk_base
+  uint64_t* chunk_base;  // alias of counts after the scan
+  uint32_t* block_start; // [n]
+  uint64_t* block_size;  // [n + 1] -> exclusive scan = out_off
+  uint32_t* big_list;    // [n]
+  uint32_t* flags;       // 4 words: flags, maxlen, big_count, status
+  uint32_t* maxlen;
+  uint32_t* big_count;
+  uint32_t* status;
+};
+
+hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, int num_cus);
+hipError_t launch_encode_blocks(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w);
+hipError_t launch_pack(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, uint32_t nblocks,
+                       const uint64_t* out_off, uint8_t* out, int num_cus);
+hipError_t launch_bloom_build(hipStream_t st, const uint64_t* hashes, uint64_t n, uint32_t num_probes,
+                              uint32_t filter_bits, uint32_t* words);
+hipError_t launch_bloom_check(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                              const uint8_t* bits, uint64_t bits_len, uint32_t num_probes, uint8_t* out);
+size_t crc_scratch_bytes(uint64_t n);
+hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out);
+// In-place exclusive scan of one u64 array of n+1 entries (the last becomes the total).
+hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t n_plus_1, void* scratch);
+size_t scan_scratch_bytes(uint32_t n_plus_1);
+
+}  // namespace slate

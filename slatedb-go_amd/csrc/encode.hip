@@ -1,0 +1,518 @@
+// SST block encode on MI355X: the data-parallel part of sstable.Builder
+// (internal/sstable/builder.go:160-213) + block.Builder (block/block.go:136-204)
+// + block.Encode (block.go:54-75) for a batch of sorted KVs resident in HBM,
+// plus the bloom filter build (bloom/bloom.go:107-172) and a large-buffer CRC32.
+//
+// Pipeline for one batch of n KVs (all launched on one stream):
+//   enc_kv_kernel      per KV: FNV-1 64 hash (bloom.go:141), LCP with the previous
+//                      key, sortedness flag
+//   enc_next_kernel    per KV j: next[j] = first KV that does not fit in a block
+//                      starting at j (greedy fill rule, block.go:171) + its size
+//   enc_exit_kernel    per 4096-KV chunk: pointer jumping in LDS -> exit[j] =
+//                      first position >= chunk end on j's block chain
+//   enc_chain_kernel   one workgroup chains chunk entries e_{c+1} = exit[e_c]
+//                      (windowed prefetch into LDS)
+//   enc_mark_kernel    per chunk: walk the true block starts from its entry
+//   enc_blocks_kernel  compact starts -> block list, encoded block sizes
+//   enc_pack_kernel    one wavefront per block: rows packed in LDS (v0 row codec,
+//                      row.go:149-189), BE16 offsets + count, CRC32, byte-exact
+//                      write into the SST byte stream
+//   bloom kernels      probes (enhanced double hashing) -> atomicOr bitset
+//   crc kernels        CRC32 of a large device buffer (filter / index)
+#include <cstdlib>
+
+#include "common.h"
+#include "encode.h"
+#include "wave_crc.h"
+
+namespace slate {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// ------------------------------------------------------------------ KV pass
+__global__ void enc_kv_kernel(EncodeArgs a, uint64_t* __restrict__ hashes, uint32_t* __restrict__ adj,
+                              uint32_t* __restrict__ flags) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const uint8_t* k = a.keys + a.key_off[i];
+  uint64_t kl = a.key_off[i + 1] - a.key_off[i];
+  uint64_t h = 0xcbf29ce484222325ull;  // FNV-1 64 (hash/fnv New64)
+  for (uint64_t b = 0; b < kl; b++) {
+    h *= 0x100000001b3ull;
+    h ^= k[b];
+  }
+  hashes[i] = h;
+  uint32_t l = 0;
+  if (i > 0) {
+    const uint8_t* p = a.keys + a.key_off[i - 1];
+    uint64_t pl = a.key_off[i] - a.key_off[i - 1];
+    uint64_t m = pl < kl ? pl : kl, o = 0;
+    while (o < m && p[o] == k[o]) o++;
+    l = o > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(o);
+    bool desc = (o < m) ? (p[o] > k[o]) : (pl > kl);
+    if (desc) atomicOr(flags, 1u);  // not sorted: the min-LCP shortcut does not hold
+  }
+  adj[i] = l;
+}
+
+__device__ inline uint64_t value_len(const EncodeArgs& a, uint32_t i) {
+  return a.tomb[i] ? 0 : a.val_off[i + 1] - a.val_off[i];
+}
+
+// v0Size (row.go:95-107) of KV i with prefix p16 against the block's first key,
+// plus its 2-byte offset slot.  Seq 0, no timestamps on the builder path.
+__device__ inline uint64_t row_slot(const EncodeArgs& a, uint32_t i, uint32_t p16) {
+  uint64_t kl = a.key_off[i + 1] - a.key_off[i];
+  uint64_t sz = 4 + (kl - p16) + 9;
+  if (!a.tomb[i]) sz += 4 + value_len(a, i);
+  return sz + 2;
+}
+
+__device__ inline uint32_t lcp_direct(const EncodeArgs& a, uint32_t x, uint32_t y) {
+  const uint8_t* p = a.keys + a.key_off[x];
+  const uint8_t* q = a.keys + a.key_off[y];
+  uint64_t m = min(a.key_off[x + 1] - a.key_off[x], a.key_off[y + 1] - a.key_off[y]), o = 0;
+  while (o < m && p[o] == q[o]) o++;
+  return o > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(o);
+}
+
+// block.Builder.Add fill rule (block.go:171): cur + 2 + v0Size(row) > blockSize
+// rejects unless the block is empty.  prefix = uint16(computePrefixLen(first, key)).
+__global__ void enc_next_kernel(EncodeArgs a, const uint32_t* __restrict__ adj, const uint32_t* __restrict__ flags,
+                                uint32_t* __restrict__ next, uint64_t* __restrict__ bytes,
+                                uint32_t* __restrict__ maxlen) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= a.n) return;
+  const bool sorted = (*flags & 1u) == 0;
+  uint64_t cur = 2 + row_slot(a, j, 0);
+  uint32_t p = 0xFFFFFFFFu, k = j + 1;
+  for (; k < a.n; k++) {
+    p = sorted ? min(p, adj[k]) : lcp_direct(a, j, k);
+    uint64_t rs = row_slot(a, k, p & 0xFFFFu);
+    if (cur + rs > a.block_size) break;
+    cur += rs;
+  }
+  next[j] = k;
+  bytes[j] = cur;
+  atomicMax(maxlen, k - j);
+}
+
+// ------------------------------------------------------------ block chains
+constexpr uint32_t kChunk = 4096;
+constexpr int kChunkThreads = 256;
+
+__global__ __launch_bounds__(kChunkThreads) void enc_exit_kernel(uint32_t n, const uint32_t* __restrict__ next,
+                                                                 uint32_t* __restrict__ exit_pos) {
+  __shared__ uint32_t J[kChunk];
+  uint32_t cs = blockIdx.x * kChunk, ce = min(cs + kChunk, n), m = ce - cs;
+  for (uint32_t x = threadIdx.x; x < m; x += kChunkThreads) J[x] = next[cs + x];
+  __syncthreads();
+  // pointer jumping: after r rounds J[x] is >= 2^r hops ahead or has left the chunk
+  for (int r = 0; r < 13; r++) {
+    for (uint32_t x = threadIdx.x; x < m; x += kChunkThreads) {
+      uint32_t v = J[x];
+      if (v < ce) J[x] = J[v - cs];
+    }
+    __syncthreads();
+  }
+  for (uint32_t x = threadIdx.x; x < m; x += kChunkThreads) exit_pos[cs + x] = J[x];
+}
+
+// Sequential over chunks: entry[c] = first true block start in chunk c (kNone if
+// a block spans the whole chunk).  Windows exit[cs .. cs+W) of upcoming chunks are
+// prefetched into LDS; the true entry is always inside its chunk's window
+// (W = longest block in KVs).
+__global__ __launch_bounds__(kChunkThreads) void enc_chain_kernel(uint32_t n, const uint32_t* __restrict__ exit_pos,
+                                                                  const uint32_t* __restrict__ maxlen,
+                                                                  uint32_t* __restrict__ entry) {
+  __shared__ uint32_t win[8192];
+  __shared__ uint32_t e_sh;
+  uint32_t nchunks = (n + kChunk - 1) / kChunk;
+  uint32_t W = min(*maxlen, kChunk);
+  if (W == 0) W = 1;
+  uint32_t G = max(1u, 8192u / W);
+  if (threadIdx.x == 0) e_sh = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < nchunks; c0 += G) {
+    uint32_t g = min(G, nchunks - c0);
+    for (uint32_t t = threadIdx.x; t < g * W; t += kChunkThreads) {
+      uint32_t c = c0 + t / W, x = c * kChunk + t % W;
+      win[t] = x < n ? exit_pos[x] : n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t e = e_sh;
+      for (uint32_t q = 0; q < g; q++) {
+        uint32_t cs = (c0 + q) * kChunk, ce = min(cs + kChunk, n);
+        if (e >= ce) {
+          entry[c0 + q] = kNone;
+        } else {
+          entry[c0 + q] = e;
+          e = win[q * W + (e - cs)];
+        }
+      }
+      e_sh = e;
+    }
+    __syncthreads();
+  }
+}
+
+// Per chunk: list the true block starts (walk next[] in LDS from the entry).
+__global__ __launch_bounds__(kChunkThreads) void enc_mark_kernel(uint32_t n, const uint32_t* __restrict__ next,
+                                                                 const uint32_t* __restrict__ entry,
+                                                                 uint32_t* __restrict__ starts_tmp,
+                                                                 uint64_t* __restrict__ counts) {
+  __shared__ uint32_t J[kChunk];
+  uint32_t c = blockIdx.x, cs = c * kChunk, ce = min(cs + kChunk, n), m = ce - cs;
+  for (uint32_t x = threadIdx.x; x < m; x += kChunkThreads) J[x] = next[cs + x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t e = entry[c], cnt = 0;
+    if (e != kNone)
+      while (e < ce) {
+        starts_tmp[cs + cnt++] = e;
+        e = J[e - cs];
+      }
+    counts[c] = cnt;
+  }
+}
+
+// Block list: block b = KVs [start, next[start]).  The block whose end is n is
+// still open unless this is the final flush.  Sizes of the encoded blocks
+// (CodecNone: data + offsets + count + CRC).
+__global__ void enc_blocks_kernel(uint32_t n, const uint32_t* __restrict__ starts_tmp,
+                                  const uint64_t* __restrict__ chunk_base, const uint64_t* __restrict__ counts,
+                                  const uint32_t* __restrict__ next, const uint64_t* __restrict__ bytes,
+                                  uint32_t* __restrict__ block_start, uint64_t* __restrict__ block_size) {
+  uint32_t c = blockIdx.x, cs = c * kChunk;
+  uint32_t cnt = uint32_t(counts[c]);
+  uint64_t base = chunk_base[c];
+  for (uint32_t t = threadIdx.x; t < cnt; t += blockDim.x) {
+    uint32_t s = starts_tmp[cs + t];
+    block_start[base + t] = s;
+    block_size[base + t] = bytes[s] + 4;
+    (void)next;
+  }
+}
+
+// ------------------------------------------------------------- block packing
+// One wavefront per block: rows assembled in LDS, then CRC and a byte-exact
+// write into the SST stream at out + out_off[b].
+__device__ inline void write_bytes_from_lds(uint8_t* gdst, const uint8_t* lds, uint32_t len, int lane) {
+  // head bytes until gdst is 16-aligned, 16-byte chunks, tail bytes
+  uint32_t head = uint32_t((16 - (reinterpret_cast<uintptr_t>(gdst) & 15)) & 15);
+  if (head > len) head = len;
+  if (uint32_t(lane) < head) gdst[lane] = lds[lane];
+  uint32_t body = (len - head) / 16;
+  uint4* d4 = reinterpret_cast<uint4*>(gdst + head);
+  for (uint32_t c = lane; c < body; c += kWave) {
+    int32_t o = int32_t(head + 16 * c);
+    uint4 v;
+    v.x = lds_u32(lds, o);
+    v.y = lds_u32(lds, o + 4);
+    v.z = lds_u32(lds, o + 8);
+    v.w = lds_u32(lds, o + 12);
+    d4[c] = v;
+  }
+  uint32_t tail0 = head + body * 16;
+  for (uint32_t t = tail0 + lane; t < len; t += kWave) gdst[t] = lds[t];
+}
+
+template <bool kLds>
+__device__ void pack_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
+                           uint8_t* buf, const uint32_t* tab, uint8_t* gdst, uint64_t enc_len, int lane) {
+  const uint32_t nrows = e - s;
+  const uint32_t data_len = uint32_t(enc_len - 4 - 2 * uint64_t(nrows) - 2);
+  // rows, 64 at a time: prefix (running min of adjacent LCPs), row offset (scan)
+  uint32_t carry_off = 0, carry_min = 0xFFFFFFFFu;
+  for (uint32_t r0 = 0; r0 < nrows; r0 += kWave) {
+    uint32_t r = r0 + lane;
+    bool live = r < nrows;
+    uint32_t i = s + r;
+    uint32_t p = 0xFFFFFFFFu;
+    if (live && r > 0) p = sorted ? adj[i] : lcp_direct(a, s, i);
+    if (sorted) {  // inclusive min-scan over the rows of this group
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(p, o, 64);
+        if (lane >= o) p = min(p, y);
+      }
+      p = min(p, carry_min);
+    }
+    uint32_t p16 = (live && r > 0) ? (p & 0xFFFFu) : 0;
+    uint32_t sz = live ? uint32_t(row_slot(a, i, p16) - 2) : 0;
+    uint32_t incl = sz;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    uint32_t off = carry_off + incl - sz;
+    if (live) {
+      const uint8_t* key = a.keys + a.key_off[i];
+      uint32_t kl = uint32_t(a.key_off[i + 1] - a.key_off[i]);
+      uint32_t sl = kl - p16;
+      uint8_t* row = buf + off;
+      st_be16(row, uint16_t(p16));
+      st_be16(row + 2, uint16_t(sl));
+      for (uint32_t b = 0; b < sl; b++) row[4 + b] = key[p16 + b];
+      uint8_t* q = row + 4 + sl;
+      for (int b = 0; b < 8; b++) q[b] = 0;  // seq 0 (builder.go:162 Row{Value: ...})
+      bool tomb = a.tomb[i] != 0;
+      q[8] = tomb ? 1 : 0;
+      if (!tomb) {
+        uint32_t vl = uint32_t(value_len(a, i));
+        st_be32(q + 9, vl);
+        const uint8_t* v = a.vals + a.val_off[i];
+        for (uint32_t b = 0; b < vl; b++) q[13 + b] = v[b];
+      }
+      st_be16(buf + data_len + 2 * r, uint16_t(off));  // uint16(len(b.data)) (block.go:176)
+    }
+    carry_off += __shfl(incl, 63, 64);
+    if (sorted) carry_min = __shfl(p, 63, 64);
+  }
+  if (lane == 0) st_be16(buf + data_len + 2 * nrows, uint16_t(nrows));
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0);
+  uint32_t raw_len = uint32_t(enc_len - 4);
+  uint32_t crc = wave_crc32(tab, buf, 0, raw_len, lane);
+  if (lane == 0) st_be32(buf + raw_len, crc);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0);
+  write_bytes_from_lds(gdst, buf, uint32_t(enc_len), lane);
+}
+
+__global__ __launch_bounds__(kPackThreads) void enc_pack_kernel(EncodeArgs a, const uint32_t* __restrict__ adj,
+                                                                const uint32_t* __restrict__ flags,
+                                                                const uint32_t* __restrict__ block_start,
+                                                                const uint32_t* __restrict__ next,
+                                                                const uint64_t* __restrict__ out_off,
+                                                                uint32_t nblocks, uint8_t* __restrict__ out,
+                                                                uint32_t* __restrict__ big_list,
+                                                                uint32_t* __restrict__ big_count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* buf = smem + kTabBytes + wave * kPackCap;
+  const bool sorted = (*flags & 1u) == 0;
+  const uint32_t waves = gridDim.x * (kPackThreads / 64);
+  for (uint32_t b = blockIdx.x * (kPackThreads / 64) + wave; b < nblocks; b += waves) {
+    uint64_t enc_len = out_off[b + 1] - out_off[b];
+    if (enc_len + 8 > kPackCap) {
+      if (lane == 0) big_list[atomicAdd(big_count, 1u)] = b;
+      continue;
+    }
+    uint32_t s = block_start[b];
+    pack_block<true>(a, adj, sorted, s, next[s], buf, tab, out + out_off[b], enc_len, lane);
+  }
+}
+
+// Blocks larger than the LDS budget: one wavefront per workgroup with the
+// largest dynamic LDS allocation.
+__global__ __launch_bounds__(64) void enc_pack_big_kernel(EncodeArgs a, const uint32_t* __restrict__ adj,
+                                                          const uint32_t* __restrict__ flags,
+                                                          const uint32_t* __restrict__ block_start,
+                                                          const uint32_t* __restrict__ next,
+                                                          const uint64_t* __restrict__ out_off,
+                                                          uint8_t* __restrict__ out,
+                                                          const uint32_t* __restrict__ big_list,
+                                                          const uint32_t* __restrict__ big_count,
+                                                          uint32_t* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63;
+  uint8_t* buf = smem + kTabBytes;
+  const bool sorted = (*flags & 1u) == 0;
+  uint32_t cnt = *big_count;
+  for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+    uint32_t b = big_list[k];
+    uint64_t enc_len = out_off[b + 1] - out_off[b];
+    if (enc_len + 8 > kPackBigCap) {
+      if (lane == 0) atomicOr(status, 1u);  // beyond the LDS budget
+      continue;
+    }
+    uint32_t s = block_start[b];
+    pack_block<true>(a, adj, sorted, s, next[s], buf, tab, out + out_off[b], enc_len, lane);
+  }
+}
+
+// ------------------------------------------------------------------- bloom
+__device__ inline uint32_t mod_u32(uint32_t x, uint32_t m) { return x % m; }
+
+// bloom.go:147-160 probes for one key hash, setBit (bloom.go:169-172) as an
+// atomicOr on the little-endian 32-bit word holding byte p/8.
+__global__ void bloom_build_kernel(const uint64_t* __restrict__ hashes, uint64_t n, uint32_t num_probes,
+                                   uint32_t filter_bits, uint32_t* __restrict__ words) {
+  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h64 = hashes[i];
+  uint64_t m = filter_bits;
+  uint64_t h = (h64 & 0xFFFFFFFFull) % m;
+  uint64_t delta = (h64 >> 32) % m;
+  for (uint32_t k = 0; k < num_probes; k++) {
+    delta = (delta + k) % m;
+    uint32_t p = uint32_t(h);
+    atomicOr(&words[p >> 5], 1u << (p & 31));
+    h = (h + delta) % m;
+  }
+}
+
+__global__ void bloom_check_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, uint64_t n,
+                                   const uint8_t* __restrict__ bits, uint64_t bits_len, uint32_t num_probes,
+                                   uint8_t* __restrict__ out) {
+  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (bits_len == 0) { out[i] = 0; return; }  // Filter.HasKey on an empty filter
+  const uint8_t* k = keys + key_off[i];
+  uint64_t kl = key_off[i + 1] - key_off[i];
+  uint64_t h64 = 0xcbf29ce484222325ull;
+  for (uint64_t b = 0; b < kl; b++) {
+    h64 *= 0x100000001b3ull;
+    h64 ^= k[b];
+  }
+  uint64_t m = bits_len * 8;
+  m &= 0xFFFFFFFFull;  // uint32(len(f.Data)*8) (bloom.go:24)
+  uint8_t res = 1;
+  if (m == 0) { out[i] = 0; return; }
+  uint64_t h = (h64 & 0xFFFFFFFFull) % m;
+  uint64_t delta = (h64 >> 32) % m;
+  for (uint32_t q = 0; q < num_probes; q++) {
+    delta = (delta + q) % m;
+    uint32_t p = uint32_t(h);
+    if (!(bits[p >> 3] & (1u << (p & 7)))) { res = 0; break; }
+    h = (h + delta) % m;
+  }
+  out[i] = res;
+}
+
+// --------------------------------------------------------- large-buffer CRC
+// Chunks of 4096 bytes, front-aligned; chunk partials R(0, chunk) (chunk 0 with
+// the 0xFFFFFFFF init folded in), combined by one wavefront.
+constexpr int kCrcThreads = 256;
+
+__global__ __launch_bounds__(kCrcThreads) void crc_chunks_kernel(const uint8_t* __restrict__ data, uint64_t n,
+                                                                 uint32_t* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* buf = smem + kTabBytes + wave * (kCrcStripe + 32);
+  uint64_t nchunks = (n + kCrcStripe - 1) / kCrcStripe;
+  uint64_t k = uint64_t(blockIdx.x) * (kCrcThreads / 64) + wave;
+  if (k >= nchunks) return;
+  uint64_t s0 = k * kCrcStripe;
+  uint32_t len = uint32_t(min<uint64_t>(kCrcStripe, n - s0));
+  const uint8_t* g = data + s0;
+  uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(g) & 15);
+  const uint4* src = reinterpret_cast<const uint4*>(g - shift);
+  uint32_t chunks = (shift + len + 15) / 16;
+  for (uint32_t c = lane; c < chunks; c += kWave) reinterpret_cast<uint4*>(buf)[c] = src[c];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t r;
+  if (k == 0 && len < 4) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < len; i++) c = tab[(c ^ buf[shift + i]) & 0xff] ^ (c >> 8);
+    r = c;  // register after the tiny message (n < 4 => single chunk)
+  } else {
+    r = wave_crc_raw(tab, buf, int32_t(shift), len, lane, k == 0);
+  }
+  if (lane == 0) partial[k] = r;
+}
+
+// One wavefront: total = sum_k partial_k * x^(8 * bytes after chunk k), inverted.
+__global__ void crc_combine_kernel(const uint32_t* __restrict__ partial, uint64_t n, uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  uint64_t nchunks = (n + kCrcStripe - 1) / kCrcStripe;
+  if (nchunks == 0) {
+    if (lane == 0) *out = 0;  // ChecksumIEEE of nothing
+    return;
+  }
+  // Horner over full chunks 0..K-2 per lane (stride 64), then the tail shift.
+  const uint32_t x_stripe = g_crc_shift.stripe;  // x^(8*4096)
+  uint64_t full = nchunks - 1;
+  // lane l handles chunks l, l+64, ...: acc_l = sum partial_k x^(8*4096*(#own later chunks)*64)
+  uint32_t x64 = x_stripe;
+  for (int q = 0; q < 6; q++) x64 = gf2_mulmod(x64, x64);  // x^(8*4096*64)
+  uint32_t acc = 0;
+  uint64_t mine = 0;
+  for (uint64_t k = lane; k < full; k += 64) {
+    acc = gf2_mulmod(acc, x64) ^ partial[k];
+    mine++;
+  }
+  // chunk k = l + 64*j is followed by (full-1-k) full chunks; lanes differ by how
+  // many of their own chunks follow and by their position modulo 64.
+  uint64_t last_k = mine ? uint64_t(lane) + 64 * (mine - 1) : 0;
+  uint32_t v = 0;
+  if (mine) v = gf2_mulmod(acc, x8n(uint64_t(kCrcStripe) * (full - 1 - last_k)));
+  for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
+  if (lane == 0) {
+    uint64_t tail = n - full * kCrcStripe;
+    uint32_t total = gf2_mulmod(v, x8n(tail)) ^ partial[full];
+    *out = ~total;
+  }
+}
+
+// --------------------------------------------------------------- launchers
+static inline uint32_t blocks_for(uint64_t n, uint32_t t) { return uint32_t((n + t - 1) / t); }
+
+hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, int num_cus) {
+  const uint32_t n = a.n;
+  (void)hipMemsetAsync(w.flags, 0, 16, st);  // flags, maxlen, big_count, status
+  if (n == 0) return hipGetLastError();
+  enc_kv_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.hashes, w.adj, w.flags);
+  enc_next_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.adj, w.flags, w.next, w.bytes, w.maxlen);
+  uint32_t nchunks = blocks_for(n, kChunk);
+  enc_exit_kernel<<<nchunks, kChunkThreads, 0, st>>>(n, w.next, w.exit_pos);
+  enc_chain_kernel<<<1, kChunkThreads, 0, st>>>(n, w.exit_pos, w.maxlen, w.entry);
+  enc_mark_kernel<<<nchunks, kChunkThreads, 0, st>>>(n, w.next, w.entry, w.starts_tmp, w.counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_blocks(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w) {
+  uint32_t nchunks = blocks_for(a.n, kChunk);
+  if (a.n == 0) return hipGetLastError();
+  enc_blocks_kernel<<<nchunks, 256, 0, st>>>(a.n, w.starts_tmp, w.chunk_base, w.counts, w.next, w.bytes,
+                                             w.block_start, w.block_size);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, uint32_t nblocks,
+                       const uint64_t* out_off, uint8_t* out, int num_cus) {
+  if (nblocks == 0) return hipGetLastError();
+  const size_t lds = kTabBytes + (kPackThreads / 64) * size_t(kPackCap);
+  uint32_t grid = min(blocks_for(nblocks, kPackThreads / 64), uint32_t(num_cus) * 8);
+  enc_pack_kernel<<<grid, kPackThreads, lds, st>>>(a, w.adj, w.flags, w.block_start, w.next, out_off, nblocks, out,
+                                                   w.big_list, w.big_count);
+  enc_pack_big_kernel<<<uint32_t(num_cus), 64, kTabBytes + kPackBigCap, st>>>(
+      a, w.adj, w.flags, w.block_start, w.next, out_off, out, w.big_list, w.big_count, w.status);
+  return hipGetLastError();
+}
+
+hipError_t launch_bloom_build(hipStream_t st, const uint64_t* hashes, uint64_t n, uint32_t num_probes,
+                              uint32_t filter_bits, uint32_t* words) {
+  if (n == 0) return hipGetLastError();
+  bloom_build_kernel<<<uint32_t((n + 255) / 256), 256, 0, st>>>(hashes, n, num_probes, filter_bits, words);
+  return hipGetLastError();
+}
+
+hipError_t launch_bloom_check(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
+                              const uint8_t* bits, uint64_t bits_len, uint32_t num_probes, uint8_t* out) {
+  if (n == 0) return hipGetLastError();
+  bloom_check_kernel<<<uint32_t((n + 255) / 256), 256, 0, st>>>(keys, key_off, n, bits, bits_len, num_probes, out);
+  return hipGetLastError();
+}
+
+size_t crc_scratch_bytes(uint64_t n) { return ((n + kCrcStripe - 1) / kCrcStripe + 1) * 4 + 16; }
+
+hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out) {
+  uint64_t nchunks = (n + kCrcStripe - 1) / kCrcStripe;
+  if (nchunks) {
+    const size_t lds = kTabBytes + (kCrcThreads / 64) * size_t(kCrcStripe + 32);
+    crc_chunks_kernel<<<uint32_t((nchunks + 3) / 4), kCrcThreads, lds, st>>>(data, n, scratch);
+  }
+  crc_combine_kernel<<<1, 64, 0, st>>>(scratch, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace slate

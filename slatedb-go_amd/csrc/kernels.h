@@ -25,6 +25,7 @@ struct DecodeArgs {
   const uint64_t* row_base;
   uint32_t* large_list;   // filled by the launcher from scratch
   uint32_t* large_count;
+  uint32_t debug;         // ablation switches for profiling only (SLATE_DEBUG_MODE); 0 in production
 };
 
 struct DecodeScratch {

@@ -1,0 +1,84 @@
+// Wave-level CRC32-IEEE over bytes staged in LDS (shared by decode and encode).
+#pragma once
+#include "common.h"
+
+namespace slate {
+
+// Per translation unit (no relocatable device code): each TU gets its own copy.
+static __constant__ CrcTables g_crc_tables = CrcTables();
+static __constant__ CrcShift g_crc_shift = CrcShift();
+
+constexpr uint32_t kTabBytes = 4096;  // 4 x 256 u32 slicing tables in LDS
+
+__device__ inline void load_crc_tables(uint32_t* tab) {
+  const uint32_t* src = &g_crc_tables.t[0][0];
+  for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];
+  __syncthreads();
+}
+
+// 4 bytes at an arbitrary (possibly negative) byte offset of a 4-aligned LDS buffer.
+__device__ inline uint32_t lds_u32(const uint8_t* base, int32_t off) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (off & ~3));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], uint32_t(off) & 3u);
+}
+
+__device__ inline uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ inline uint32_t crc_word(const uint32_t* tab, uint32_t c, uint32_t w) {
+  c ^= w;
+  return tab[768 + (c & 0xff)] ^ tab[512 + ((c >> 8) & 0xff)] ^ tab[256 + ((c >> 16) & 0xff)] ^ tab[c >> 24];
+}
+
+// R(init, msg[0..n)) with the CRC register semantics of crc32.ChecksumIEEE but
+// without the final inversion: fold_init = true starts from 0xFFFFFFFF (folded
+// into the first four bytes), false from 0.  n >= 4 when fold_init.
+// 64 lanes x 64-byte segments per 4 KiB stripe, end-aligned so each lane's shift
+// x^(8*64*(63-l)) is a compile-time constant (CrcShift).
+__device__ inline uint32_t wave_crc_raw(const uint32_t* tab, const uint8_t* lds, int32_t msg, uint32_t n, int lane,
+                                        bool fold_init) {
+  uint32_t stripes = (n + kCrcStripe - 1) / kCrcStripe;
+  uint32_t acc = 0;
+  for (uint32_t k = 0; k < stripes; k++) {
+    if (k) acc = gf2_mulmod(acc, g_crc_shift.stripe);
+    int64_t p0 = int64_t(n) - int64_t(stripes - k) * kCrcStripe + int64_t(lane) * kCrcSeg;
+    uint32_t c = 0;
+    if (p0 + int64_t(kCrcSeg) > 0) {
+#pragma unroll 4
+      for (uint32_t q = 0; q < kCrcSeg / 4; q++) {
+        int64_t p = p0 + 4 * q;
+        uint32_t w = 0;
+        if (p > -4) {
+          w = lds_u32(lds, int32_t(int64_t(msg) + p));
+          if (p < 0) w &= 0xFFFFFFFFu << (8 * uint32_t(-p));
+          if (fold_init && p < 4) {
+            uint32_t m = 0;
+            for (int b = 0; b < 4; b++) {
+              int64_t pos = p + b;
+              if (pos >= 0 && pos < 4) m |= 0xFFu << (8 * b);
+            }
+            w ^= m;
+          }
+        }
+        c = crc_word(tab, c, w);
+      }
+    }
+    acc ^= c;
+  }
+  return wave_xor(gf2_mulmod(acc, g_crc_shift.lane[lane]));
+}
+
+// crc32.ChecksumIEEE of msg[0..n) in LDS.
+__device__ inline uint32_t wave_crc32(const uint32_t* tab, const uint8_t* lds, int32_t msg, uint32_t n, int lane) {
+  if (n < 4) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < n; i++) c = tab[(c ^ lds[msg + int32_t(i)]) & 0xff] ^ (c >> 8);
+    return ~c;
+  }
+  return ~wave_crc_raw(tab, lds, msg, n, lane, true);
+}
+
+}  // namespace slate
