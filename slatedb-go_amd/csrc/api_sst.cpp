@@ -1,0 +1,701 @@
+// C-ABI: SST builder (builder.go), table (flatbuf.go:143 EncodeTable), reader
+// (decode.go), bloom (bloom.go) and single-block encode (block.go:54).
+// Compute runs in the encode/decode kernels; this file does queueing and the
+// flatbuffer footer framing only.
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <vector>
+
+#include "encode.h"
+#include "flatbuf.h"
+#include "host_ctx.h"
+
+using namespace slate;
+
+namespace {
+
+inline uint64_t bloom_filter_bytes(uint32_t nk, uint32_t bpk) {  // bloom.go:135-139 (uint32 math)
+  uint32_t bits = nk * bpk;
+  return uint64_t(uint32_t(bits + 7) / 8);
+}
+inline uint16_t bloom_num_probes(uint32_t bpk) {  // bloom.go:174-178
+  volatile float f = float(bpk) * 0.69f;
+  return uint16_t(f);
+}
+inline void put_be32(std::vector<uint8_t>& v, uint32_t x) {
+  v.push_back(uint8_t(x >> 24));
+  v.push_back(uint8_t(x >> 16));
+  v.push_back(uint8_t(x >> 8));
+  v.push_back(uint8_t(x));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------- GPU CRC helpers
+int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* crc) {
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(ctx->e_j.ensure(crc_scratch_bytes(n) + 16));
+  uint32_t* scratch = ctx->e_j.as<uint32_t>();
+  uint32_t* out = scratch + (crc_scratch_bytes(n) / 4);
+  SLATE_HIP(launch_crc32(ctx->stream, d_data, n, scratch, out));
+  SLATE_HIP(hipMemcpyAsync(crc, out, 4, hipMemcpyDeviceToHost, ctx->stream));
+  SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  return SLATE_OK;
+}
+
+int ctx_crc32_host_buffer(slate_ctx* ctx, const uint8_t* data, size_t n, uint32_t* crc) {
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(ctx->e_i.ensure(n + 16));
+  if (n) SLATE_HIP(hipMemcpyAsync(ctx->e_i.p, data, n, hipMemcpyHostToDevice, ctx->stream));
+  return ctx_crc32_device(ctx, ctx->e_i.as<uint8_t>(), n, crc);
+}
+
+// --------------------------------------------------------------- SST builder
+struct slate_sst_table {
+  slate_sst_info info{};
+  std::vector<uint8_t> first_key;
+  std::deque<std::vector<uint8_t>> chunks;
+  bool has_bloom = false;
+  uint16_t num_probes = 0;
+  std::vector<uint8_t> bloom_bits;
+};
+
+struct slate_sst_builder {
+  slate_ctx* ctx;
+  slate_sst_config cfg;
+  // pending KVs (not yet in a finished block)
+  std::vector<uint8_t> keys, vals, tomb;
+  std::vector<uint64_t> key_off{0}, val_off{0};
+  uint64_t pending_lower = 2;  // lower bound of the pending KVs' encoded size
+  bool dirty = false;
+  std::deque<std::vector<uint8_t>> blocks;  // finished, not yet popped
+  std::vector<uint64_t> meta_off;
+  std::vector<uint8_t> meta_keys;
+  std::vector<uint64_t> meta_key_off{0};
+  std::vector<uint8_t> first_key;
+  bool has_first_key = false;
+  uint64_t current_len = 0;
+  uint32_t num_keys = 0;  // builder.go:111 (uint32)
+  DevBuf d_hashes;        // FNV-1 hashes of every key added (bloom input)
+  uint64_t n_hashes = 0;
+  std::vector<uint8_t> last_block;  // the final block (Build keeps it in the last chunk)
+  int sticky = SLATE_OK;
+  bool built = false;
+};
+
+static int builder_flush(slate_sst_builder* b, bool final) {
+  slate_ctx* ctx = b->ctx;
+  hipStream_t st = ctx->stream;
+  const uint64_t n64 = b->key_off.size() - 1;
+  b->dirty = false;
+  if (n64 == 0) return SLATE_OK;
+  if (n64 >= 0xFFFFFFF0ull) return SLATE_E_INVALID_ARG;
+  const uint32_t n = uint32_t(n64);
+  SLATE_HIP(ctx_bind(ctx));
+  // ---- upload the pending KVs
+  SLATE_HIP(ctx->e_a.ensure(b->keys.size() + 16));
+  SLATE_HIP(ctx->e_b.ensure(b->vals.size() + 16));
+  SLATE_HIP(ctx->e_c.ensure((n64 + 1) * 16 + n64 + 16));
+  uint8_t* d_keys = ctx->e_a.as<uint8_t>();
+  uint8_t* d_vals = ctx->e_b.as<uint8_t>();
+  uint64_t* d_key_off = ctx->e_c.as<uint64_t>();
+  uint64_t* d_val_off = d_key_off + n64 + 1;
+  uint8_t* d_tomb = reinterpret_cast<uint8_t*>(d_val_off + n64 + 1);
+  if (!b->keys.empty()) SLATE_HIP(hipMemcpyAsync(d_keys, b->keys.data(), b->keys.size(), hipMemcpyHostToDevice, st));
+  if (!b->vals.empty()) SLATE_HIP(hipMemcpyAsync(d_vals, b->vals.data(), b->vals.size(), hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_key_off, b->key_off.data(), (n64 + 1) * 8, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_val_off, b->val_off.data(), (n64 + 1) * 8, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_tomb, b->tomb.data(), n64, hipMemcpyHostToDevice, st));
+  SLATE_HIP(b->d_hashes.grow_keep((b->n_hashes + n64) * 8 + 64, b->n_hashes * 8, st));
+  // ---- work buffers
+  const uint64_t chunks = (n64 + 4095) / 4096;
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  size_t o_adj = carve(n64 * 4), o_next = carve(n64 * 4), o_bytes = carve(n64 * 8), o_exit = carve(n64 * 4),
+         o_entry = carve(chunks * 4), o_starts = carve(n64 * 4), o_counts = carve((chunks + 1) * 8),
+         o_bstart = carve(n64 * 4), o_bsize = carve((n64 + 1) * 8), o_big = carve(n64 * 4), o_flags = carve(64),
+         o_scan = carve(scan_scratch_bytes(uint32_t(n64 + 1)));
+  SLATE_HIP(ctx->e_d.ensure(off));
+  uint8_t* base = ctx->e_d.as<uint8_t>();
+  EncodeBufs w;
+  w.hashes = b->d_hashes.as<uint64_t>() + b->n_hashes;
+  w.adj = reinterpret_cast<uint32_t*>(base + o_adj);
+  w.next = reinterpret_cast<uint32_t*>(base + o_next);
+  w.bytes = reinterpret_cast<uint64_t*>(base + o_bytes);
+  w.exit_pos = reinterpret_cast<uint32_t*>(base + o_exit);
+  w.entry = reinterpret_cast<uint32_t*>(base + o_entry);
+  w.starts_tmp = reinterpret_cast<uint32_t*>(base + o_starts);
+  w.counts = reinterpret_cast<uint64_t*>(base + o_counts);
+  w.chunk_base = w.counts;
+  w.block_start = reinterpret_cast<uint32_t*>(base + o_bstart);
+  w.block_size = reinterpret_cast<uint64_t*>(base + o_bsize);
+  w.big_list = reinterpret_cast<uint32_t*>(base + o_big);
+  w.flags = reinterpret_cast<uint32_t*>(base + o_flags);
+  w.maxlen = w.flags + 1;
+  w.big_count = w.flags + 2;
+  w.status = w.flags + 3;
+  void* scan_scratch = base + o_scan;
+  EncodeArgs a{d_keys, d_key_off, d_vals, d_val_off, d_tomb, n, b->cfg.block_size, b->cfg.codec};
+  SLATE_HIP(launch_encode(st, a, w, ctx->num_cus));
+  SLATE_HIP(hipMemsetAsync(w.counts + chunks, 0, 8, st));
+  SLATE_HIP(launch_scan_u64(st, w.counts, uint32_t(chunks + 1), scan_scratch));
+  uint64_t nb_total = 0;
+  SLATE_HIP(hipMemcpyAsync(&nb_total, w.counts + chunks, 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  SLATE_HIP(launch_encode_blocks(st, a, w));
+  // the last block is still open unless this is the final flush (Build)
+  const uint64_t nb = final ? nb_total : nb_total - 1;
+  std::vector<uint32_t> starts(nb_total);
+  SLATE_HIP(hipMemcpyAsync(starts.data(), w.block_start, nb_total * 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipMemsetAsync(w.block_size + nb, 0, 8, st));
+  SLATE_HIP(launch_scan_u64(st, w.block_size, uint32_t(nb + 1), scan_scratch));
+  std::vector<uint64_t> out_off(nb + 1);
+  SLATE_HIP(hipMemcpyAsync(out_off.data(), w.block_size, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  const uint64_t total = out_off[nb];
+  std::vector<uint8_t> out(total);
+  if (nb) {
+    SLATE_HIP(ctx->e_e.ensure(total + 16));
+    SLATE_HIP(launch_pack(st, a, w, uint32_t(nb), w.block_size, ctx->e_e.as<uint8_t>(), ctx->num_cus));
+    uint32_t status = 0;
+    SLATE_HIP(hipMemcpyAsync(&status, w.status, 4, hipMemcpyDeviceToHost, st));
+    if (total) SLATE_HIP(hipMemcpyAsync(out.data(), ctx->e_e.p, total, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (status) return SLATE_E_CAPACITY;
+  }
+  // ---- queue the finished blocks (builder.go:169-176, finishBlock :192-213)
+  for (uint64_t k = 0; k < nb; k++) {
+    uint32_t s = starts[k];
+    b->meta_off.push_back(b->current_len);
+    b->meta_keys.insert(b->meta_keys.end(), b->keys.begin() + b->key_off[s], b->keys.begin() + b->key_off[s + 1]);
+    b->meta_key_off.push_back(b->meta_keys.size());
+    std::vector<uint8_t> blk(out.begin() + out_off[k], out.begin() + out_off[k + 1]);
+    if (final && k + 1 == nb) {
+      b->last_block.swap(blk);  // Build: the last block opens the final chunk
+    } else {
+      b->current_len += blk.size();
+      b->blocks.push_back(std::move(blk));
+    }
+  }
+  uint64_t consumed = final ? n64 : starts[nb_total - 1];
+  b->n_hashes += consumed;
+  if (!final) {  // keep the open block's KVs pending
+    uint64_t k0 = b->key_off[consumed], v0 = b->val_off[consumed];
+    b->keys.erase(b->keys.begin(), b->keys.begin() + k0);
+    b->vals.erase(b->vals.begin(), b->vals.begin() + v0);
+    b->tomb.erase(b->tomb.begin(), b->tomb.begin() + consumed);
+    std::vector<uint64_t> ko(b->key_off.begin() + consumed, b->key_off.end());
+    std::vector<uint64_t> vo(b->val_off.begin() + consumed, b->val_off.end());
+    for (auto& x : ko) x -= k0;
+    for (auto& x : vo) x -= v0;
+    b->key_off.swap(ko);
+    b->val_off.swap(vo);
+    b->pending_lower = 2;
+    for (size_t i = 0; i + 1 < b->key_off.size(); i++)
+      b->pending_lower += 2 + 13 + (b->tomb[i] ? 0 : 4 + (b->val_off[i + 1] - b->val_off[i]));
+  } else {
+    b->keys.clear();
+    b->vals.clear();
+    b->tomb.clear();
+    b->key_off.assign(1, 0);
+    b->val_off.assign(1, 0);
+    b->pending_lower = 2;
+  }
+  return SLATE_OK;
+}
+
+extern "C" {
+
+slate_sst_builder* slate_sst_builder_new(slate_ctx* ctx, const slate_sst_config* cfg, int* status) {
+  int dummy;
+  if (!status) status = &dummy;
+  if (!ctx || !cfg) {
+    *status = SLATE_E_INVALID_ARG;
+    return nullptr;
+  }
+  if (cfg->codec < SLATE_CODEC_NONE || cfg->codec > SLATE_CODEC_ZSTD) {
+    *status = SLATE_E_INVALID_CODEC;
+    return nullptr;
+  }
+  if (cfg->codec != SLATE_CODEC_NONE) {  // GPU Snappy/Zstd/LZ4/Zlib encode: not yet
+    *status = SLATE_E_CODEC_UNSUPPORTED;
+    return nullptr;
+  }
+  slate_sst_builder* b = new slate_sst_builder();
+  b->ctx = ctx;
+  b->cfg = *cfg;
+  *status = SLATE_OK;
+  return b;
+}
+
+void slate_sst_builder_free(slate_sst_builder* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->ctx->device);
+  b->d_hashes.release();
+  delete b;
+}
+
+int slate_sst_builder_add(slate_sst_builder* b, const uint8_t* key, size_t key_len, const uint8_t* value,
+                          size_t value_len, int kind) {
+  if (!b || (!key && key_len)) return SLATE_E_INVALID_ARG;
+  if (b->built) return SLATE_E_INVALID_ARG;
+  if (key_len == 0) return SLATE_E_INVALID_ARG;  // block.go:163 assert (panic in Go)
+  b->num_keys += 1;
+  bool tomb = kind == 1;
+  b->keys.insert(b->keys.end(), key, key + key_len);
+  b->key_off.push_back(b->keys.size());
+  if (!tomb && value_len) b->vals.insert(b->vals.end(), value, value + value_len);
+  b->val_off.push_back(b->vals.size());
+  b->tomb.push_back(tomb ? 1 : 0);
+  b->pending_lower += 2 + 13 + (tomb ? 0 : 4 + value_len);
+  b->dirty = true;
+  if (!b->has_first_key) {  // builder.go:178-180
+    b->first_key.assign(key, key + key_len);
+    b->has_first_key = true;
+  }
+  return SLATE_OK;
+}
+
+int slate_sst_builder_add_value(slate_sst_builder* b, const uint8_t* key, size_t key_len, const uint8_t* value,
+                                size_t value_len) {
+  return slate_sst_builder_add(b, key, key_len, value, value_len, value_len == 0 ? 1 : 0);
+}
+
+int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const uint64_t* key_off,
+                                const uint8_t* values, const uint64_t* value_off, const uint8_t* is_tomb, uint64_t n) {
+  if (!b || (n && (!keys || !key_off || !value_off))) return SLATE_E_INVALID_ARG;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t vl = value_off[i + 1] - value_off[i];
+    int kind = is_tomb ? (is_tomb[i] ? 1 : 0) : (vl == 0 ? 1 : 0);
+    int st = slate_sst_builder_add(b, keys + key_off[i], key_off[i + 1] - key_off[i], values + value_off[i], vl, kind);
+    if (st) return st;
+  }
+  return SLATE_OK;
+}
+
+int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_cap, size_t* len, int* present) {
+  if (!b || !present) return SLATE_E_INVALID_ARG;
+  *present = 0;
+  if (b->sticky) return b->sticky;
+  // A finished block exists only once the pending KVs overflow one block; the
+  // lower bound avoids a GPU pass while they certainly fit.
+  if (b->blocks.empty() && b->dirty && b->pending_lower > b->cfg.block_size) {
+    int st = builder_flush(b, false);
+    if (st) return b->sticky = st;
+  }
+  if (b->blocks.empty()) return SLATE_OK;
+  std::vector<uint8_t>& blk = b->blocks.front();
+  if (len) *len = blk.size();
+  if (blk.size() > out_cap || (!out && blk.size())) return SLATE_E_CAPACITY;
+  if (!blk.empty()) memcpy(out, blk.data(), blk.size());
+  b->blocks.pop_front();
+  *present = 1;
+  return SLATE_OK;
+}
+
+int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
+  if (!b || !table || b->built) return SLATE_E_INVALID_ARG;
+  if (b->sticky) return b->sticky;
+  slate_ctx* ctx = b->ctx;
+  int st = builder_flush(b, true);
+  if (st) return st;
+  b->built = true;
+  slate_sst_table* t = new slate_sst_table();
+  std::vector<uint8_t> buf = b->last_block;
+  const uint64_t filter_off = b->current_len + buf.size();
+  uint64_t filter_len = 0;
+  // ---- bloom filter (builder.go:225-235, bloom.go:112-133 Build, :52-67 Encode)
+  if (b->num_keys >= b->cfg.min_filter_keys) {
+    uint16_t np = 0;
+    uint64_t nb = 0;
+    if (b->num_keys > 0) {
+      np = bloom_num_probes(b->cfg.filter_bits_per_key);
+      nb = bloom_filter_bytes(b->num_keys, b->cfg.filter_bits_per_key);
+      if (nb * 8 == 0 || nb * 8 > 0xFFFFFFFFull) {  // Go: divide by zero panic / uint32 bits
+        delete t;
+        return SLATE_E_INVALID_ARG;
+      }
+    }
+    SLATE_HIP(ctx_bind(ctx));
+    SLATE_HIP(ctx->e_f.ensure(((nb + 3) & ~uint64_t(3)) + 16));
+    SLATE_HIP(ctx->e_g.ensure(nb + 2 + 16));
+    uint32_t* words = ctx->e_f.as<uint32_t>();
+    if (nb) {
+      SLATE_HIP(hipMemsetAsync(words, 0, (nb + 3) & ~uint64_t(3), ctx->stream));
+      SLATE_HIP(launch_bloom_build(ctx->stream, b->d_hashes.as<uint64_t>(), b->n_hashes, np, uint32_t(nb * 8), words));
+    }
+    // encoded filter = BE16 numProbes || bits || BE32 CRC (None codec)
+    uint8_t hdr[2] = {uint8_t(np >> 8), uint8_t(np)};
+    uint8_t* enc = ctx->e_g.as<uint8_t>();
+    SLATE_HIP(hipMemcpyAsync(enc, hdr, 2, hipMemcpyHostToDevice, ctx->stream));
+    if (nb) SLATE_HIP(hipMemcpyAsync(enc + 2, words, nb, hipMemcpyDeviceToDevice, ctx->stream));
+    uint32_t crc = 0;
+    st = ctx_crc32_device(ctx, enc, nb + 2, &crc);
+    if (st) { delete t; return st; }
+    t->bloom_bits.resize(nb);
+    if (nb) SLATE_HIP(hipMemcpy(t->bloom_bits.data(), words, nb, hipMemcpyDeviceToHost));
+    t->has_bloom = true;
+    t->num_probes = np;
+    buf.push_back(hdr[0]);
+    buf.push_back(hdr[1]);
+    buf.insert(buf.end(), t->bloom_bits.begin(), t->bloom_bits.end());
+    put_be32(buf, crc);
+    filter_len = nb + 6;
+  }
+  // ---- index (builder.go:238-244, flatbuf.go:126-139)
+  std::vector<uint8_t> index = fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
+  uint32_t icrc = 0;
+  st = ctx_crc32_host_buffer(ctx, index.data(), index.size(), &icrc);
+  if (st) { delete t; return st; }
+  put_be32(index, icrc);
+  const uint64_t index_off = b->current_len + buf.size();
+  buf.insert(buf.end(), index.begin(), index.end());
+  const uint64_t meta_off = b->current_len + buf.size();
+  // ---- info (builder.go:246-258, flatbuf.go:62-81)
+  InfoFields inf;
+  inf.index_offset = index_off;
+  inf.index_len = index.size();
+  inf.filter_offset = filter_off;
+  inf.filter_len = filter_len;
+  inf.codec = b->cfg.codec;
+  inf.has_first_key = b->has_first_key;
+  inf.first_key = b->first_key;
+  std::vector<uint8_t> info = fb_encode_info(inf);
+  uint32_t fcrc = 0;
+  st = ctx_crc32_host_buffer(ctx, info.data(), info.size(), &fcrc);
+  if (st) { delete t; return st; }
+  put_be32(info, fcrc);
+  buf.insert(buf.end(), info.begin(), info.end());
+  put_be32(buf, uint32_t(meta_off));  // builder.go:260 uint32(metaOffset)
+  t->info.index_offset = index_off;
+  t->info.index_len = index.size();
+  t->info.filter_offset = filter_off;
+  t->info.filter_len = filter_len;
+  t->info.codec = b->cfg.codec;
+  t->info.first_key_len = uint32_t(b->first_key.size());
+  t->first_key = b->first_key;
+  t->chunks.swap(b->blocks);
+  t->chunks.push_back(std::move(buf));
+  *table = t;
+  return SLATE_OK;
+}
+
+void slate_sst_table_free(slate_sst_table* t) { delete t; }
+
+int slate_sst_table_info(const slate_sst_table* t, slate_sst_info* info, uint8_t* first_key, size_t first_key_cap) {
+  if (!t || !info) return SLATE_E_INVALID_ARG;
+  *info = t->info;
+  if (t->first_key.size() > first_key_cap) return SLATE_E_CAPACITY;
+  if (!t->first_key.empty() && first_key) memcpy(first_key, t->first_key.data(), t->first_key.size());
+  return SLATE_OK;
+}
+
+size_t slate_sst_table_num_chunks(const slate_sst_table* t) { return t ? t->chunks.size() : 0; }
+
+int slate_sst_table_chunk(const slate_sst_table* t, size_t i, const uint8_t** data, size_t* len) {
+  if (!t || i >= t->chunks.size() || !data || !len) return SLATE_E_INVALID_ARG;
+  *data = t->chunks[i].data();
+  *len = t->chunks[i].size();
+  return SLATE_OK;
+}
+
+size_t slate_sst_table_encoded_len(const slate_sst_table* t) {
+  size_t n = 0;
+  if (t)
+    for (auto& c : t->chunks) n += c.size();
+  return n;
+}
+
+int slate_sst_table_encode(const slate_sst_table* t, uint8_t* out, size_t out_cap) {
+  if (!t) return SLATE_E_INVALID_ARG;
+  size_t o = 0;
+  for (auto& c : t->chunks) {
+    if (o + c.size() > out_cap) return SLATE_E_CAPACITY;
+    if (!c.empty()) memcpy(out + o, c.data(), c.size());
+    o += c.size();
+  }
+  return SLATE_OK;
+}
+
+int slate_sst_table_bloom(const slate_sst_table* t, int* present, uint16_t* num_probes, uint8_t* bits,
+                          size_t bits_cap, size_t* bits_len) {
+  if (!t || !present) return SLATE_E_INVALID_ARG;
+  *present = t->has_bloom;
+  if (num_probes) *num_probes = t->num_probes;
+  if (bits_len) *bits_len = t->bloom_bits.size();
+  if (!t->has_bloom) return SLATE_OK;
+  if (t->bloom_bits.size() > bits_cap) return SLATE_E_CAPACITY;
+  if (!t->bloom_bits.empty() && bits) memcpy(bits, t->bloom_bits.data(), t->bloom_bits.size());
+  return SLATE_OK;
+}
+
+// ---------------------------------------------------------------- reader side
+// DecodeInfo (flatbuf.go:102-124).  The info footer is ~80 bytes of host framing:
+// its CRC is checked on the host.
+int slate_decode_info(const uint8_t* buf, size_t len, slate_sst_info* info, uint8_t* first_key,
+                      size_t first_key_cap) {
+  if (!info || (len && !buf)) return SLATE_E_INVALID_ARG;
+  if (len <= 4) return SLATE_E_INFO_TOO_SHORT;
+  size_t ci = len - 4;
+  if (ld_be32(buf + ci) != crc32_host(buf, ci)) return SLATE_E_INFO_CHECKSUM;
+  InfoFields f;
+  if (!fb_decode_info(buf, len, &f)) return SLATE_E_FLATBUF;
+  info->index_offset = f.index_offset;
+  info->index_len = f.index_len;
+  info->filter_offset = f.filter_offset;
+  info->filter_len = f.filter_len;
+  info->codec = f.codec;  // unchecked cast (flatbuf.go:121)
+  info->first_key_len = uint32_t(f.first_key.size());
+  if (f.first_key.size() > first_key_cap) return SLATE_E_CAPACITY;
+  if (!f.first_key.empty() && first_key) memcpy(first_key, f.first_key.data(), f.first_key.size());
+  return SLATE_OK;
+}
+
+int slate_encode_info(const slate_sst_info* info, const uint8_t* first_key, uint8_t* out, size_t out_cap,
+                      size_t* out_len) {
+  if (!info) return SLATE_E_INVALID_ARG;
+  InfoFields f;
+  f.index_offset = info->index_offset;
+  f.index_len = info->index_len;
+  f.filter_offset = info->filter_offset;
+  f.filter_len = info->filter_len;
+  f.codec = info->codec;
+  f.has_first_key = first_key != nullptr;
+  if (first_key) f.first_key.assign(first_key, first_key + info->first_key_len);
+  std::vector<uint8_t> v = fb_encode_info(f);
+  put_be32(v, crc32_host(v.data(), v.size()));
+  if (out_len) *out_len = v.size();
+  if (v.size() > out_cap || !out) return SLATE_E_CAPACITY;
+  memcpy(out, v.data(), v.size());
+  return SLATE_OK;
+}
+
+// ReadInfo (decode.go:25-48) over the whole object.
+int slate_sst_read_info(const uint8_t* sst, size_t sst_len, slate_sst_info* info, uint8_t* first_key,
+                        size_t first_key_cap) {
+  if (!info || (sst_len && !sst)) return SLATE_E_INVALID_ARG;
+  if (sst_len <= 4) return SLATE_E_SST_TOO_SHORT;
+  uint64_t oi = sst_len - 4;
+  uint32_t mo = ld_be32(sst + oi);
+  if (mo > oi) return SLATE_E_BLOB_RANGE;  // bytesBlob.ReadRange (blob.go:24)
+  return slate_decode_info(sst + mo, size_t(oi - mo), info, first_key, first_key_cap);
+}
+
+}  // extern "C"
+
+struct slate_index {
+  std::vector<uint64_t> offsets;
+  std::vector<uint8_t> keys;
+  std::vector<uint64_t> key_off;
+  std::vector<uint8_t> data;  // decoded flatbuffer bytes (Index.Data)
+};
+
+extern "C" {
+
+// DecodeIndex (flatbuf.go:83-100) + Index.BlockMeta() (flatbuf.go:22-31).
+int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, slate_index** index) {
+  if (!ctx || !index || (len && !buf)) return SLATE_E_INVALID_ARG;
+  if (len <= 4) return SLATE_E_INDEX_TOO_SHORT;
+  size_t ci = len - 4;
+  uint32_t crc = 0;
+  int st = ctx_crc32_host_buffer(ctx, buf, ci, &crc);
+  if (st) return st;
+  if (crc != ld_be32(buf + ci)) return SLATE_E_INDEX_CHECKSUM;
+  if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;  // GPU stream decode of large buffers: next
+  slate_index* x = new slate_index();
+  x->data.assign(buf, buf + ci);
+  if (!fb_decode_index(x->data.data(), x->data.size(), &x->offsets, &x->keys, &x->key_off)) {
+    delete x;
+    return SLATE_E_FLATBUF;
+  }
+  *index = x;
+  return SLATE_OK;
+}
+
+void slate_index_free(slate_index* index) { delete index; }
+
+size_t slate_index_num_blocks(const slate_index* index) { return index ? index->offsets.size() : 0; }
+
+int slate_index_block_meta(const slate_index* index, size_t i, uint64_t* offset, const uint8_t** first_key,
+                           size_t* first_key_len) {
+  if (!index || i >= index->offsets.size()) return SLATE_E_INVALID_ARG;
+  if (offset) *offset = index->offsets[i];
+  if (first_key) *first_key = index->keys.data() + index->key_off[i];
+  if (first_key_len) *first_key_len = index->key_off[i + 1] - index->key_off[i];
+  return SLATE_OK;
+}
+
+// getBlockRange (decode.go:93-103).
+int slate_read_blocks_range(const slate_sst_info* info, const slate_index* index, uint64_t start, uint64_t end,
+                            uint64_t* range_start, uint64_t* range_end) {
+  if (!info || !index || !range_start || !range_end) return SLATE_E_INVALID_ARG;
+  if (start >= end) return SLATE_E_RANGE_START;
+  if (end > index->offsets.size()) return SLATE_E_RANGE_END;
+  *range_start = index->offsets[start];
+  *range_end = end < index->offsets.size() ? index->offsets[end] : info->filter_offset;
+  return SLATE_OK;
+}
+
+// ReadBlocks (decode.go:107-149): one GPU batch for the whole range.
+int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_index* index, uint64_t start,
+                      uint64_t end, const uint8_t* data, size_t data_len, uint8_t* out, uint64_t out_cap,
+                      uint64_t* out_off, slate_block_meta* meta, slate_row* rows, uint64_t rows_cap,
+                      uint64_t* row_base, uint64_t* failed_block) {
+  uint64_t rs, re;
+  int st = slate_read_blocks_range(info, index, start, end, &rs, &re);
+  if (st) return st;
+  if (re < rs || data_len != re - rs) return SLATE_E_BLOB_RANGE;
+  const uint64_t n = end - start;
+  std::vector<uint64_t> in_off(n + 1);
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t s = index->offsets[start + i] - rs;
+    // the last block of the index runs to the end of the range (decode.go:132-133)
+    uint64_t e = (start + i + 1 == index->offsets.size()) ? data_len : index->offsets[start + i + 1] - rs;
+    if (s > data_len || e > data_len || s > e) return SLATE_E_BLOB_RANGE;
+    in_off[i] = s;
+    in_off[i + 1] = e;
+  }
+  // blocks are contiguous in the range; in_off[i+1] of one block is in_off of the next
+  st = slate_block_decode_batch(ctx, info->codec, data, in_off.data(), uint32_t(n), out, out_cap, out_off, meta, rows,
+                                rows_cap, row_base);
+  if (st) return st;
+  if (failed_block) {
+    *failed_block = UINT64_MAX;
+    for (uint64_t i = 0; i < n; i++)
+      if (meta[i].status != SLATE_OK) {
+        *failed_block = start + i;
+        break;
+      }
+  }
+  return SLATE_OK;
+}
+
+// ---------------------------------------------------------------------- bloom
+int slate_bloom_build(slate_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t bits_per_key,
+                      uint8_t* bits, size_t bits_cap, size_t* bits_len, uint16_t* num_probes) {
+  if (!ctx || (n && (!keys || !key_off))) return SLATE_E_INVALID_ARG;
+  if (n == 0) {  // Build on an empty builder: Filter{}
+    if (bits_len) *bits_len = 0;
+    if (num_probes) *num_probes = 0;
+    return SLATE_OK;
+  }
+  uint16_t np = bloom_num_probes(bits_per_key);
+  uint64_t nb = bloom_filter_bytes(uint32_t(n), bits_per_key);
+  if (bits_len) *bits_len = nb;
+  if (num_probes) *num_probes = np;
+  if (nb * 8 == 0 || nb * 8 > 0xFFFFFFFFull) return SLATE_E_INVALID_ARG;
+  if (nb > bits_cap || !bits) return SLATE_E_CAPACITY;
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->e_a.ensure(key_off[n] - key_off[0] + 16));
+  SLATE_HIP(ctx->e_c.ensure((n + 1) * 8 + n * 8 + 16));
+  SLATE_HIP(ctx->e_f.ensure(((nb + 3) & ~uint64_t(3)) + 16));
+  std::vector<uint64_t> rel(n + 1);
+  for (uint64_t i = 0; i <= n; i++) rel[i] = key_off[i] - key_off[0];
+  uint64_t* d_off = ctx->e_c.as<uint64_t>();
+  uint64_t* d_hash = d_off + n + 1;
+  SLATE_HIP(hipMemcpyAsync(ctx->e_a.p, keys + key_off[0], rel[n], hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  // FNV-1 hashes by the encode KV pass
+  SLATE_HIP(ctx->e_d.ensure(n * 4 + 64));
+  uint32_t* adj = ctx->e_d.as<uint32_t>();
+  uint32_t* flags = adj + n;
+  SLATE_HIP(hipMemsetAsync(flags, 0, 16, st));
+  EncodeArgs a{ctx->e_a.as<uint8_t>(), d_off, ctx->e_a.as<uint8_t>(), d_off, nullptr, uint32_t(n), 0, 0};
+  SLATE_HIP(launch_kv_hashes(st, a, d_hash, adj, flags));
+  SLATE_HIP(hipMemsetAsync(ctx->e_f.p, 0, (nb + 3) & ~uint64_t(3), st));
+  SLATE_HIP(launch_bloom_build(st, d_hash, n, np, uint32_t(nb * 8), ctx->e_f.as<uint32_t>()));
+  SLATE_HIP(hipMemcpyAsync(bits, ctx->e_f.p, nb, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  return SLATE_OK;
+}
+
+int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len, int codec,
+                       uint8_t* out, size_t out_cap, size_t* out_len) {
+  if (!ctx || (bits_len && !bits)) return SLATE_E_INVALID_ARG;
+  if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;
+  std::vector<uint8_t> buf(bits_len + 2);
+  buf[0] = uint8_t(num_probes >> 8);
+  buf[1] = uint8_t(num_probes);
+  if (bits_len) memcpy(buf.data() + 2, bits, bits_len);
+  uint32_t crc = 0;
+  int st = ctx_crc32_host_buffer(ctx, buf.data(), buf.size(), &crc);
+  if (st) return st;
+  put_be32(buf, crc);
+  if (out_len) *out_len = buf.size();
+  if (buf.size() > out_cap || !out) return SLATE_E_CAPACITY;
+  memcpy(out, buf.data(), buf.size());
+  return SLATE_OK;
+}
+
+int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, uint16_t* num_probes, uint8_t* bits,
+                       size_t bits_cap, size_t* bits_len) {
+  if (!ctx || (len && !buf)) return SLATE_E_INVALID_ARG;
+  if (len < 2) return SLATE_E_FILTER_TOO_SMALL;
+  if (len < 4) return SLATE_E_FILTER_PANIC;
+  size_t ci = len - 4;
+  uint32_t crc = 0;
+  int st = ctx_crc32_host_buffer(ctx, buf, ci, &crc);
+  if (st) return st;
+  if (crc != ld_be32(buf + ci)) return SLATE_E_FILTER_CHECKSUM;
+  if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;
+  if (ci < 2) return SLATE_E_FILTER_PANIC;
+  if (num_probes) *num_probes = ld_be16(buf);
+  if (bits_len) *bits_len = ci - 2;
+  if (ci - 2 > bits_cap || (!bits && ci > 2)) return SLATE_E_CAPACITY;
+  if (ci > 2) memcpy(bits, buf + 2, ci - 2);
+  return SLATE_OK;
+}
+
+int slate_bloom_has_keys(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len, const uint8_t* keys,
+                         const uint64_t* key_off, uint64_t n, uint8_t* out) {
+  if (!ctx || (n && (!keys || !key_off || !out)) || (bits_len && !bits)) return SLATE_E_INVALID_ARG;
+  if (n == 0) return SLATE_OK;
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  uint64_t kb = key_off[n] - key_off[0];
+  SLATE_HIP(ctx->e_a.ensure(kb + 16));
+  SLATE_HIP(ctx->e_c.ensure((n + 1) * 8 + 16));
+  SLATE_HIP(ctx->e_f.ensure(bits_len + 16));
+  SLATE_HIP(ctx->e_b.ensure(n + 16));
+  std::vector<uint64_t> rel(n + 1);
+  for (uint64_t i = 0; i <= n; i++) rel[i] = key_off[i] - key_off[0];
+  SLATE_HIP(hipMemcpyAsync(ctx->e_a.p, keys + key_off[0], kb, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(ctx->e_c.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  if (bits_len) SLATE_HIP(hipMemcpyAsync(ctx->e_f.p, bits, bits_len, hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_bloom_check(st, ctx->e_a.as<uint8_t>(), ctx->e_c.as<uint64_t>(), n, ctx->e_f.as<uint8_t>(), bits_len,
+                               num_probes, ctx->e_b.as<uint8_t>()));
+  SLATE_HIP(hipMemcpyAsync(out, ctx->e_b.p, n, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  return SLATE_OK;
+}
+
+// block.Encode (block.go:54-75) for one block: buffer framing on the host, CRC on the GPU.
+int slate_block_encode(slate_ctx* ctx, int codec, const uint8_t* data, size_t data_len, const uint16_t* offsets,
+                       size_t n_offsets, uint8_t* out, size_t out_cap, size_t* out_len) {
+  if (!ctx || (data_len && !data) || (n_offsets && !offsets)) return SLATE_E_INVALID_ARG;
+  if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;
+  std::vector<uint8_t> buf(data_len + 2 * n_offsets + 2);
+  if (data_len) memcpy(buf.data(), data, data_len);
+  for (size_t i = 0; i < n_offsets; i++) st_be16(buf.data() + data_len + 2 * i, offsets[i]);
+  st_be16(buf.data() + data_len + 2 * n_offsets, uint16_t(n_offsets));
+  uint32_t crc = 0;
+  int st = ctx_crc32_host_buffer(ctx, buf.data(), buf.size(), &crc);
+  if (st) return st;
+  put_be32(buf, crc);
+  if (out_len) *out_len = buf.size();
+  if (buf.size() > out_cap || !out) return SLATE_E_CAPACITY;
+  memcpy(out, buf.data(), buf.size());
+  return SLATE_OK;
+}
+
+}  // extern "C"

@@ -39,6 +39,7 @@ struct EncodeBufs {
   uint32_t* status;
 };
 
+hipError_t launch_kv_hashes(hipStream_t st, const EncodeArgs& a, uint64_t* hashes, uint32_t* adj, uint32_t* flags);
 hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, int num_cus);
 hipError_t launch_encode_blocks(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w);
 hipError_t launch_pack(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, uint32_t nblocks,

@@ -456,6 +456,11 @@ __global__ void crc_combine_kernel(const uint32_t* __restrict__ partial, uint64_
 // --------------------------------------------------------------- launchers
 static inline uint32_t blocks_for(uint64_t n, uint32_t t) { return uint32_t((n + t - 1) / t); }
 
+hipError_t launch_kv_hashes(hipStream_t st, const EncodeArgs& a, uint64_t* hashes, uint32_t* adj, uint32_t* flags) {
+  if (a.n) enc_kv_kernel<<<blocks_for(a.n, 256), 256, 0, st>>>(a, hashes, adj, flags);
+  return hipGetLastError();
+}
+
 hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, int num_cus) {
   const uint32_t n = a.n;
   (void)hipMemsetAsync(w.flags, 0, 16, st);  // flags, maxlen, big_count, status

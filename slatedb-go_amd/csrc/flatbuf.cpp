@@ -2,7 +2,18 @@
 
 #include <cstring>
 
+#include "common.h"
+
 namespace slate {
+
+// Host CRC for the ~80-byte info footer only (flatbuf.go:62-124 framing); every
+// block, filter and index CRC runs on the GPU.
+static const CrcTables kHostCrc = CrcTables();
+uint32_t crc32_host(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = kHostCrc.t[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return ~c;
+}
 
 FbBuilder::FbBuilder(size_t reserve) : buf_(reserve), head_(reserve) {}
 

@@ -21,6 +21,24 @@ struct DevBuf {
     cap = c;
     return hipSuccess;
   }
+  // grow preserving the first `keep` bytes (stream-ordered copy)
+  hipError_t grow_keep(size_t n, size_t keep, hipStream_t st) {
+    if (n <= cap) return hipSuccess;
+    void* q = nullptr;
+    size_t c = n + n / 2;
+    hipError_t e = hipMalloc(&q, c);
+    if (e != hipSuccess) return e;
+    if (p && keep) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, st);
+      if (e != hipSuccess) return e;
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    cap = c;
+    return hipSuccess;
+  }
   template <typename T>
   T* as() const { return static_cast<T*>(p); }
   void release() {
@@ -61,3 +79,8 @@ inline int hip_status(hipError_t e) {
 }
 
 inline hipError_t ctx_bind(slate_ctx* ctx) { return hipSetDevice(ctx->device); }
+
+// CRC32-IEEE of a host buffer computed on the context's GPU (stream-synchronous).
+int ctx_crc32_host_buffer(slate_ctx* ctx, const uint8_t* data, size_t n, uint32_t* crc);
+// CRC32-IEEE of a device buffer (stream-synchronous, result to host).
+int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* crc);

@@ -73,6 +73,34 @@ _SIGS = {
                                            C.c_uint64, vp]),
     "slate_block_decode": (C.c_int, [vp, C.c_int, vp, C.c_size_t, vp, C.c_size_t, szp, vp, vp, C.c_size_t]),
     "slate_block_encode": (C.c_int, [vp, C.c_int, vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, szp]),
+    "slate_sst_builder_new": (vp, [vp, C.POINTER(SstConfig), C.POINTER(C.c_int)]),
+    "slate_sst_builder_free": (None, [vp]),
+    "slate_sst_builder_add": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t, C.c_int]),
+    "slate_sst_builder_add_value": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t]),
+    "slate_sst_builder_add_batch": (C.c_int, [vp, vp, vp, vp, vp, vp, C.c_uint64]),
+    "slate_sst_builder_next_block": (C.c_int, [vp, vp, C.c_size_t, szp, C.POINTER(C.c_int)]),
+    "slate_sst_builder_build": (C.c_int, [vp, C.POINTER(vp)]),
+    "slate_sst_table_free": (None, [vp]),
+    "slate_sst_table_info": (C.c_int, [vp, C.POINTER(SstInfo), vp, C.c_size_t]),
+    "slate_sst_table_num_chunks": (C.c_size_t, [vp]),
+    "slate_sst_table_chunk": (C.c_int, [vp, C.c_size_t, C.POINTER(vp), szp]),
+    "slate_sst_table_encoded_len": (C.c_size_t, [vp]),
+    "slate_sst_table_encode": (C.c_int, [vp, vp, C.c_size_t]),
+    "slate_sst_table_bloom": (C.c_int, [vp, C.POINTER(C.c_int), u16p, vp, C.c_size_t, szp]),
+    "slate_sst_read_info": (C.c_int, [vp, C.c_size_t, C.POINTER(SstInfo), vp, C.c_size_t]),
+    "slate_decode_info": (C.c_int, [vp, C.c_size_t, C.POINTER(SstInfo), vp, C.c_size_t]),
+    "slate_encode_info": (C.c_int, [C.POINTER(SstInfo), vp, vp, C.c_size_t, szp]),
+    "slate_decode_index": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.POINTER(vp)]),
+    "slate_index_free": (None, [vp]),
+    "slate_index_num_blocks": (C.c_size_t, [vp]),
+    "slate_index_block_meta": (C.c_int, [vp, C.c_size_t, u64p, C.POINTER(vp), szp]),
+    "slate_read_blocks_range": (C.c_int, [C.POINTER(SstInfo), vp, C.c_uint64, C.c_uint64, u64p, u64p]),
+    "slate_read_blocks": (C.c_int, [vp, C.POINTER(SstInfo), vp, C.c_uint64, C.c_uint64, vp, C.c_size_t, vp,
+                                    C.c_uint64, vp, vp, vp, C.c_uint64, vp, u64p]),
+    "slate_bloom_build": (C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, vp, C.c_size_t, szp, u16p]),
+    "slate_bloom_encode": (C.c_int, [vp, C.c_uint16, vp, C.c_size_t, C.c_int, vp, C.c_size_t, szp]),
+    "slate_bloom_decode": (C.c_int, [vp, vp, C.c_size_t, C.c_int, u16p, vp, C.c_size_t, szp]),
+    "slate_bloom_has_keys": (C.c_int, [vp, C.c_uint16, vp, C.c_size_t, vp, vp, C.c_uint64, vp]),
 }
 
 _lib = None
@@ -182,6 +210,213 @@ class Context:
                       d_rows: int, d_row_base: int):
         _check(lib().slate_block_decode_device(self._h, codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows,
                                                d_row_base), "slate_block_decode_device")
+
+
+    # ------------------------------------------------------------ encode / SST
+    def block_encode(self, data: bytes, offsets: list[int], codec: int) -> tuple[int, bytes]:
+        d = np.frombuffer(bytes(data) or b"\0", dtype=np.uint8)
+        o = np.array(offsets or [0], dtype=np.uint16)
+        cap = len(data) * 2 + 2 * len(offsets) + 64
+        out = np.zeros(cap, np.uint8)
+        ol = C.c_size_t()
+        st = lib().slate_block_encode(self._h, codec, _ptr(d), len(data), _ptr(o), len(offsets), _ptr(out), cap,
+                                      C.byref(ol))
+        return st, (out[: ol.value].tobytes() if st == OK else b"")
+
+    def bloom_build(self, keys: list[bytes], bits_per_key: int) -> tuple[int, bytes]:
+        kd, ko = _arena(keys)
+        cap = max(((len(keys) * bits_per_key) & 0xFFFFFFFF) // 8 + 8, 8)
+        out = np.zeros(cap, np.uint8)
+        bl = C.c_size_t()
+        npr = C.c_uint16()
+        _check(lib().slate_bloom_build(self._h, _ptr(kd), _ptr(ko), len(keys), bits_per_key, _ptr(out), cap,
+                                       C.byref(bl), C.byref(npr)), "slate_bloom_build")
+        return npr.value, out[: bl.value].tobytes()
+
+    def bloom_has_keys(self, num_probes: int, bits: bytes, keys: list[bytes]) -> list[bool]:
+        kd, ko = _arena(keys)
+        b = np.frombuffer(bytes(bits) or b"\0", dtype=np.uint8)
+        out = np.zeros(max(len(keys), 1), np.uint8)
+        _check(lib().slate_bloom_has_keys(self._h, num_probes, _ptr(b), len(bits), _ptr(kd), _ptr(ko), len(keys),
+                                          _ptr(out)), "slate_bloom_has_keys")
+        return [bool(x) for x in out[: len(keys)]]
+
+    def bloom_encode(self, num_probes: int, bits: bytes, codec: int) -> tuple[int, bytes]:
+        b = np.frombuffer(bytes(bits) or b"\0", dtype=np.uint8)
+        cap = len(bits) + 64
+        out = np.zeros(cap, np.uint8)
+        ol = C.c_size_t()
+        st = lib().slate_bloom_encode(self._h, num_probes, _ptr(b), len(bits), codec, _ptr(out), cap, C.byref(ol))
+        return st, (out[: ol.value].tobytes() if st == OK else b"")
+
+    def bloom_decode(self, buf: bytes, codec: int) -> tuple[int, int, bytes]:
+        b = np.frombuffer(bytes(buf) or b"\0", dtype=np.uint8)
+        cap = len(buf) + 64
+        out = np.zeros(cap, np.uint8)
+        npr = C.c_uint16()
+        bl = C.c_size_t()
+        st = lib().slate_bloom_decode(self._h, _ptr(b), len(buf), codec, C.byref(npr), _ptr(out), cap, C.byref(bl))
+        return st, npr.value, (out[: bl.value].tobytes() if st == OK else b"")
+
+    def decode_index(self, buf: bytes, codec: int):
+        b = np.frombuffer(bytes(buf) or b"\0", dtype=np.uint8)
+        h = C.c_void_p()
+        st = lib().slate_decode_index(self._h, _ptr(b), len(buf), codec, C.byref(h))
+        if st != OK:
+            return st, None
+        return st, Index(h)
+
+    def read_blocks(self, info: "SstInfo", index: "Index", start: int, end: int, sst: bytes):
+        """ReadBlocks over the object bytes: returns (status, failed_block, decode outputs)."""
+        rs, re_ = C.c_uint64(), C.c_uint64()
+        st = lib().slate_read_blocks_range(C.byref(info), index.handle, start, end, C.byref(rs), C.byref(re_))
+        if st != OK:
+            return st, None, None
+        data = np.frombuffer(sst[rs.value:re_.value] or b"\0", dtype=np.uint8)
+        n = end - start
+        out_cap = (re_.value - rs.value) * 24 + 64
+        out = np.zeros(out_cap, np.uint8)
+        out_off = np.zeros(n + 1, np.uint64)
+        row_base = np.zeros(n + 1, np.uint64)
+        meta = np.zeros(n, META_DTYPE)
+        rows = np.zeros(out_cap // 15 + 8, ROW_DTYPE)
+        failed = C.c_uint64()
+        st = lib().slate_read_blocks(self._h, C.byref(info), index.handle, start, end, _ptr(data),
+                                     re_.value - rs.value, _ptr(out), out_cap, _ptr(out_off), _ptr(meta), _ptr(rows),
+                                     rows.size, _ptr(row_base), C.byref(failed))
+        return st, failed.value, (out, out_off, meta, rows, row_base)
+
+
+class Index:
+    def __init__(self, h):
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().slate_index_free(self._h)
+            self._h = None
+
+    def block_metas(self) -> list[tuple[int, bytes]]:
+        out = []
+        for i in range(lib().slate_index_num_blocks(self._h)):
+            off = C.c_uint64()
+            p = C.c_void_p()
+            ln = C.c_size_t()
+            _check(lib().slate_index_block_meta(self._h, i, C.byref(off), C.byref(p), C.byref(ln)), "block_meta")
+            out.append((off.value, C.string_at(p.value, ln.value) if ln.value else b""))
+        return out
+
+
+class SstBuilder:
+    """sstable.Builder (builder.go:92-268) on the GPU through the C-ABI."""
+
+    def __init__(self, ctx: Context, block_size=4096, min_filter_keys=0, filter_bits_per_key=10, codec=NONE):
+        cfg = SstConfig(block_size, min_filter_keys, filter_bits_per_key, codec)
+        st = C.c_int()
+        self._ctx = ctx
+        self._h = lib().slate_sst_builder_new(ctx.handle, C.byref(cfg), C.byref(st))
+        if not self._h:
+            raise SlateError(st.value, "slate_sst_builder_new")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().slate_sst_builder_free(self._h)
+            self._h = None
+
+    def add_value(self, key: bytes, value: bytes) -> int:
+        return lib().slate_sst_builder_add_value(self._h, C.c_char_p(key), len(key), C.c_char_p(value), len(value))
+
+    def add(self, key: bytes, value: bytes | None) -> int:
+        return lib().slate_sst_builder_add(self._h, C.c_char_p(key), len(key), C.c_char_p(value or b""),
+                                           len(value or b""), 1 if value is None else 0)
+
+    def add_batch(self, keys: np.ndarray, key_off: np.ndarray, vals: np.ndarray, val_off: np.ndarray,
+                  is_tomb: np.ndarray | None = None) -> int:
+        return lib().slate_sst_builder_add_batch(self._h, _ptr(keys), _ptr(key_off), _ptr(vals), _ptr(val_off),
+                                                 _ptr(is_tomb) if is_tomb is not None else None, len(key_off) - 1)
+
+    def next_block(self) -> bytes | None:
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, np.uint8)
+            ln = C.c_size_t()
+            present = C.c_int()
+            st = lib().slate_sst_builder_next_block(self._h, _ptr(out), cap, C.byref(ln), C.byref(present))
+            if st == E_CAPACITY:
+                cap = ln.value + 64
+                continue
+            _check(st, "slate_sst_builder_next_block")
+            return out[: ln.value].tobytes() if present.value else None
+
+    def build(self) -> "SstTable":
+        t = C.c_void_p()
+        _check(lib().slate_sst_builder_build(self._h, C.byref(t)), "slate_sst_builder_build")
+        return SstTable(t)
+
+
+class SstTable:
+    def __init__(self, h):
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().slate_sst_table_free(self._h)
+            self._h = None
+
+    def chunks(self) -> list[bytes]:
+        out = []
+        for i in range(lib().slate_sst_table_num_chunks(self._h)):
+            p = C.c_void_p()
+            ln = C.c_size_t()
+            _check(lib().slate_sst_table_chunk(self._h, i, C.byref(p), C.byref(ln)), "chunk")
+            out.append(C.string_at(p.value, ln.value) if ln.value else b"")
+        return out
+
+    def encode(self) -> bytes:
+        n = lib().slate_sst_table_encoded_len(self._h)
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(lib().slate_sst_table_encode(self._h, _ptr(out), out.size), "encode")
+        return out[:n].tobytes()
+
+    def info(self) -> dict:
+        info = SstInfo()
+        fk = np.zeros(1 << 16, np.uint8)
+        _check(lib().slate_sst_table_info(self._h, C.byref(info), _ptr(fk), fk.size), "info")
+        d = {f: getattr(info, f) for f, _ in SstInfo._fields_}
+        d["first_key"] = fk[: info.first_key_len].tobytes()
+        return d
+
+    def bloom(self):
+        present = C.c_int()
+        npr = C.c_uint16()
+        bl = C.c_size_t()
+        lib().slate_sst_table_bloom(self._h, C.byref(present), C.byref(npr), None, 0, C.byref(bl))
+        if not present.value:
+            return None
+        out = np.zeros(max(bl.value, 1), np.uint8)
+        _check(lib().slate_sst_table_bloom(self._h, C.byref(present), C.byref(npr), _ptr(out), out.size,
+                                           C.byref(bl)), "bloom")
+        return npr.value, out[: bl.value].tobytes()
+
+
+def _arena(items: list[bytes]):
+    off = np.zeros(len(items) + 1, np.uint64)
+    if items:
+        off[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
+    data = np.frombuffer(b"".join(items) or b"\0", dtype=np.uint8).copy()
+    return data, off
+
+
+def read_info(sst: bytes) -> tuple[int, "SstInfo", bytes]:
+    b = np.frombuffer(bytes(sst) or b"\0", dtype=np.uint8)
+    info = SstInfo()
+    fk = np.zeros(max(len(sst), 16), np.uint8)
+    st = lib().slate_sst_read_info(_ptr(b), len(sst), C.byref(info), _ptr(fk), fk.size)
+    return st, info, fk[: info.first_key_len].tobytes()
 
 
 def decode_scratch_bytes(n: int) -> int:

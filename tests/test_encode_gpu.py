@@ -1,0 +1,179 @@
+"""GPU parity: SST build (blocks, bloom, index, info), block encode, bloom and the
+SST reader through the HIP C-ABI vs the CPU oracle — byte for byte (CodecNone)."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+from tests import blockgen as bg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sc():
+    import slatecodec
+    return slatecodec
+
+
+@pytest.fixture(scope="module")
+def ctx(sc):
+    return sc.Context(0)
+
+
+def _build_both(sc, ctx, kvs, block_size=4096, mfk=0, bpk=10, batch=False, next_every=0):
+    g = sc.SstBuilder(ctx, block_size, mfk, bpk, sc.NONE)
+    o = ob.SstBuilder(block_size, mfk, bpk, ob.NONE)
+    g_blocks, o_blocks = [], []
+    if batch:
+        keys = [k for k, _ in kvs]
+        vals = [v for _, v in kvs]
+        kd, ko = sc._arena(keys)
+        vd, vo = sc._arena(vals)
+        assert g.add_batch(kd, ko, vd, vo) == 0
+        for k, v in kvs:
+            assert o.add_value(k, v) == 0
+    else:
+        for i, (k, v) in enumerate(kvs):
+            assert g.add_value(k, v) == 0
+            assert o.add_value(k, v) == 0
+            if next_every and i % next_every == 0:
+                while (b := g.next_block()) is not None:
+                    g_blocks.append(b)
+                while (b := o.next_block()) is not None:
+                    o_blocks.append(b)
+    assert g_blocks == o_blocks
+    t = g.build()
+    assert o.build() == 0
+    return t, o, g_blocks
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_sst_bytes(sc, ctx, seed):
+    rng = random.Random(seed)
+    kvs = bg.random_kvs(rng, rng.randint(1, 1500), alphabet=rng.choice([3, 256]), tomb_p=0.15)
+    bs = rng.choice([40, 128, 1024, 4096])
+    mfk = rng.choice([0, 10, 100000])
+    bpk = rng.choice([1, 10, 20])
+    t, o, _ = _build_both(sc, ctx, kvs, bs, mfk, bpk, batch=seed % 2 == 0, next_every=rng.choice([0, 1, 7]))
+    assert t.chunks() == o.chunks()
+    assert t.encode() == o.encode_table()
+    assert t.info() == o.info()
+    assert t.bloom() == o.bloom()
+
+
+def test_unsorted_and_duplicate_keys(sc, ctx):
+    rng = random.Random(9)
+    kvs = [(bytes(rng.randrange(3) for _ in range(rng.randint(1, 6))), b"v" * rng.randint(0, 40)) for _ in range(800)]
+    kvs += [(b"dup", b"x")] * 20
+    t, o, _ = _build_both(sc, ctx, kvs, 256, 0, 10)
+    assert t.encode() == o.encode_table()
+
+
+def test_make_blocks_available(sc, ctx, ref_vectors):
+    v = ref_vectors["make_blocks_available"]
+    g = sc.SstBuilder(ctx, v["block_size"], 0, 10, sc.NONE)
+    for k, val in v["adds1"]:
+        assert g.add_value(k.encode(), val.encode()) == 0
+    for expect in v["blocks1"]:
+        blk = g.next_block()
+        meta, buf, rows = ob.block_decode(blk, ob.NONE)
+        assert buf[4:4 + rows[0]["key_suffix_len"]] == expect[0].encode()
+    assert g.next_block() is None
+    for k, val in v["adds2"]:
+        assert g.add_value(k.encode(), val.encode()) == 0
+    blk = g.next_block()
+    meta, buf, rows = ob.block_decode(blk, ob.NONE)
+    assert buf[4:12] == v["blocks2"][0][0].encode()
+    assert g.next_block() is None
+
+
+@pytest.mark.parametrize("name", ["read_blocks_52", "read_all_blocks"])
+def test_reference_layouts_and_reader(sc, ctx, ref_vectors, name):
+    v = ref_vectors[name]
+    bs = v.get("block_size") or ob.v0_estimate_block_size([(k.encode(), x.encode()) for k, x in v["estimate_kvs"]])
+    kvs = [(k.encode(), x.encode()) for k, x in v["kvs"]]
+    t, o, _ = _build_both(sc, ctx, kvs, bs, v["min_filter_keys"], 10)
+    sst = t.encode()
+    assert sst == o.encode_table()
+    st, info, fk = sc.read_info(sst)
+    assert st == 0 and fk == kvs[0][0]
+    st, index = ctx.decode_index(sst[info.index_offset: info.index_offset + info.index_len], info.codec)
+    assert st == 0
+    metas = index.block_metas()
+    assert [m[1] for m in metas] == [blk[0].encode() for blk in v["blocks"]]
+    st, failed, (out, out_off, meta, rows, rb) = ctx.read_blocks(info, index, 0, len(metas), sst)
+    assert st == 0 and failed == 2**64 - 1
+    for i, blk in enumerate(v["blocks"]):
+        assert meta[i]["n_rows"] == len(blk)
+    # range errors (decode.go:108-114)
+    assert ctx.read_blocks(info, index, 1, 1, sst)[0] == 46
+    assert ctx.read_blocks(info, index, 0, len(metas) + 1, sst)[0] == 47
+
+
+def test_dump_layout(sc, ctx, ref_vectors):
+    v = ref_vectors["dump_layout_derived"]
+    kvs = [(k.encode(), x.encode()) for k, x in v["kvs"]]
+    t, o, _ = _build_both(sc, ctx, kvs, 35, 0, 10)
+    info = t.info()
+    assert info["filter_offset"] == v["filter_offset"] and info["filter_len"] == v["filter_len_now"]
+    assert info["index_offset"] == v["index_offset_now"]
+    assert info["index_len"] - 4 == v["dump_stale"]["index_len"]
+
+
+def test_filter_encoded_len(sc, ctx, ref_vectors):
+    for c in ref_vectors["filter_encoded_len"]:
+        kvs = [(k.encode(), c["value"].encode()) for k in c["keys"]]
+        t, o, _ = _build_both(sc, ctx, kvs, 4096, 0, c["bits_per_key"])
+        assert t.info()["filter_len"] == c["expected_len"]
+
+
+def test_bloom_api(sc, ctx, ref_vectors):
+    v = ref_vectors["filter_has_key"]
+    keys = [s.encode() for s in v["add"]]
+    k, bits = ctx.bloom_build(keys, v["bits_per_key"])
+    assert (k, bits) == ob.bloom_build(keys, v["bits_per_key"])
+    probe = [s.encode() for s in v["present"] + v["absent"]]
+    assert ctx.bloom_has_keys(k, bits, probe) == [True] * len(v["present"]) + [False] * len(v["absent"])
+    st, enc = ctx.bloom_encode(k, bits, sc.NONE)
+    assert st == 0 and enc == ob.bloom_encode(k, bits, ob.NONE)
+    assert ctx.bloom_decode(enc, sc.NONE) == (0, k, bits)
+    assert ctx.bloom_decode(enc[:-1] + bytes([enc[-1] ^ 1]), sc.NONE)[0] == 31
+    assert ctx.bloom_decode(b"\x00", sc.NONE)[0] == 30
+    # TestFilterEffective scale
+    many = [struct.pack(">I", i) for i in range(100000)]
+    k2, bits2 = ctx.bloom_build(many, 10)
+    assert bits2 == ob.bloom_build(many, 10)[1]
+    res = ctx.bloom_has_keys(k2, bits2, [struct.pack(">I", i) for i in range(100000, 200000)])
+    assert sum(res) / 100000 < 0.01
+    assert ctx.bloom_has_keys(0, b"", [b"x"]) == [False]
+
+
+def test_block_encode_single(sc, ctx, ref_vectors):
+    for c in ref_vectors["block_roundtrips"]:
+        bb = ob.BlockBuilder(c["block_size"])
+        for k, val in c["kvs"]:
+            bb.add_value(k.encode(), (val or "").encode())
+        data, offs, _ = bb.build()
+        st, enc = ctx.block_encode(data, offs, sc.NONE)
+        assert st == 0 and enc == ob.block_encode(data, offs, ob.NONE)[1]
+
+
+def test_large_rows(sc, ctx):
+    """Single rows larger than the pack kernel's per-wave LDS budget."""
+    kvs = [(b"a%03d" % i, bytes([i % 251]) * n) for i, n in enumerate([10, 9000, 30000, 5, 20000, 100])]
+    t, o, _ = _build_both(sc, ctx, kvs, 4096, 0, 10)
+    assert t.encode() == o.encode_table()
+
+
+def test_vhalf_workload_batch(sc, ctx):
+    kvs = bg.kv_synthetic(38 * 500, half=True, tomb_every=20)
+    t, o, _ = _build_both(sc, ctx, kvs, 4096, 0, 10, batch=True)
+    assert t.encode() == o.encode_table()
+
+
+def test_empty_builder(sc, ctx):
+    t, o, _ = _build_both(sc, ctx, [], 4096, 0, 10)
+    assert t.encode() == o.encode_table()
