@@ -181,17 +181,17 @@ __global__ __launch_bounds__(kChunkThreads) void enc_mark_kernel(uint32_t n, con
 // still open unless this is the final flush.  Sizes of the encoded blocks
 // (CodecNone: data + offsets + count + CRC).
 __global__ void enc_blocks_kernel(uint32_t n, const uint32_t* __restrict__ starts_tmp,
-                                  const uint64_t* __restrict__ chunk_base, const uint64_t* __restrict__ counts,
-                                  const uint32_t* __restrict__ next, const uint64_t* __restrict__ bytes,
+                                  const uint64_t* __restrict__ chunk_base, const uint64_t* __restrict__ bytes,
                                   uint32_t* __restrict__ block_start, uint64_t* __restrict__ block_size) {
   uint32_t c = blockIdx.x, cs = c * kChunk;
-  uint32_t cnt = uint32_t(counts[c]);
   uint64_t base = chunk_base[c];
+  // chunk_base is the exclusive scan of the per-chunk start counts
+  uint32_t cnt = uint32_t(min<uint64_t>(chunk_base[c + 1] - base, kChunk));
   for (uint32_t t = threadIdx.x; t < cnt; t += blockDim.x) {
+    if (base + t >= n) break;
     uint32_t s = starts_tmp[cs + t];
     block_start[base + t] = s;
     block_size[base + t] = bytes[s] + 4;
-    (void)next;
   }
 }
 
@@ -477,8 +477,8 @@ hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& 
 hipError_t launch_encode_blocks(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w) {
   uint32_t nchunks = blocks_for(a.n, kChunk);
   if (a.n == 0) return hipGetLastError();
-  enc_blocks_kernel<<<nchunks, 256, 0, st>>>(a.n, w.starts_tmp, w.chunk_base, w.counts, w.next, w.bytes,
-                                             w.block_start, w.block_size);
+  enc_blocks_kernel<<<nchunks, 256, 0, st>>>(a.n, w.starts_tmp, w.chunk_base, w.bytes, w.block_start,
+                                             w.block_size);
   return hipGetLastError();
 }
 
