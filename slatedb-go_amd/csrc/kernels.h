@@ -12,6 +12,10 @@ constexpr uint32_t kFastInCap = 4608;        // staged encoded block (incl. 16-b
 constexpr uint32_t kFastOutCap = 4608;       // decoded block
 constexpr uint32_t kLargeInCap = 65552;      // large-block kernel, one wave per workgroup
 constexpr uint32_t kLargeOutCap = 90112;
+// lane-per-block Snappy decode (decode_lpb.hip): one wave per workgroup, 432 B of
+// LDS per lane + 4 KiB CRC tables -> 5 workgroups (waves) per CU
+constexpr int kLpbThreads = 64;
+constexpr uint32_t kLpbWgPerCu = 5;
 
 struct DecodeArgs {
   int codec;
@@ -40,6 +44,7 @@ size_t decode_scratch_bytes(uint32_t n);
 hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
+hipError_t launch_decode_lpb(hipStream_t st, const DecodeArgs& a, int num_cus);
 // Validates that the code object loads on the current device.
 hipError_t decode_kernels_available();
 
