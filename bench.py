@@ -68,8 +68,8 @@ def main():
     codec = sc.SNAPPY if args.codec == "snappy" else sc.NONE
     n = args.blocks
     t0 = time.time()
-    dec, dec_off = wl.decoded_blocks(n, seed=20250307 + rank, half=(args.values == "half"),
-                                     kv_begin=rank * n * 40)
+    spec = shard_spec(rank, n)
+    dec, dec_off = wl.decoded_blocks(n, seed=spec["seed"], half=(args.values == "half"), kv_begin=spec["kv_begin"])
     blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=min(16, os.cpu_count() or 4))
     gen_s = time.time() - t0
     dec_bytes = int(dec_off[-1])
@@ -137,15 +137,12 @@ def main():
         dist.barrier()
     elapsed = t_end - t_start
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, elapsed, device)
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * dec_bytes * args.steps / elapsed / 2**30
 
-    # roofline of the dominant kernel (decode_fast_kernel): algorithmic bytes per launch
+    # roofline of the dominant kernel (decode_lpb_kernel for Snappy): algorithmic bytes per launch
     alg_read = enc_bytes + 8 * (n + 1) * 3  # encoded blocks incl. CRC + in_off/out_off/row_base
     alg_write = dec_bytes + 16 * n_rows + 16 * n  # decoded bytes + row descriptors + block meta
     alg = alg_read + alg_write
@@ -160,7 +157,7 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": "decode_fast_kernel", "kernel_ms": round(kern_ms, 4),
+                "kernel": "decode_lpb_kernel" if args.codec == "snappy" else "decode_fast_kernel", "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg, "alg_read_bytes": alg_read, "alg_write_bytes": alg_write,
                 "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
@@ -176,6 +173,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_host_io:
         result["host_io"] = host_io_rate(torch, sc, ctx, codec, blob, in_off, dec_bytes, device)
+        result["host_io_pinned"] = host_io_pinned(torch, sc, codec, blob, in_off, device)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(codec, blob, in_off, args.cpu_seconds)
@@ -185,6 +183,94 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def shard_spec(rank: int, blocks_per_rank: int) -> dict:
+    """Rank r decodes its own blocks: a disjoint key range (38 keys per block, 40
+    reserved) and its own value seed, so every rank's shard is distinct data."""
+    return {"seed": 20250307 + rank, "kv_begin": rank * blocks_per_rank * 40}
+
+
+def max_over_ranks(dist, elapsed: float, device) -> float:
+    """Whole-job time = the slowest rank's time (one all-reduce, outside the timed region)."""
+    if not dist:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def host_io_pinned(torch, sc, codec, blob, in_off, device, n_streams=4, chunk=32768, max_blocks=262144):
+    """Host-in/host-out with pinned buffers: per chunk of blocks, H2D of the encoded
+    blocks + offsets, plan + decode, D2H of decoded bytes + block meta + row
+    descriptors; chunks round-robin over n_streams streams (one slate_ctx each) so
+    copies overlap kernels.  For DESIGN.md (PCIe-bound), never `value`."""
+    n = min(len(in_off) - 1, max_blocks)
+    streams = [torch.cuda.Stream(device) for _ in range(n_streams)]
+    ctxs = []
+    for s in streams:
+        c = sc.Context(device.index)
+        c.set_stream(s.cuda_stream)
+        ctxs.append(c)
+    jobs = []
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        m = b - a
+        lo, hi = int(in_off[a]), int(in_off[b])
+        h_in = torch.from_numpy(blob[lo:hi].copy()).pin_memory()
+        h_off = torch.from_numpy((in_off[a:b + 1] - in_off[a]).astype(np.int64)).pin_memory()
+        d_in = torch.empty(hi - lo, dtype=torch.uint8, device=device)
+        d_off = torch.empty(m + 1, dtype=torch.int64, device=device)
+        d_oo = torch.empty(m + 1, dtype=torch.int64, device=device)
+        d_rb = torch.empty(m + 1, dtype=torch.int64, device=device)
+        d_sc = torch.empty(sc.decode_scratch_bytes(m) + 64, dtype=torch.uint8, device=device)
+        d_in.copy_(h_in)
+        d_off.copy_(h_off)
+        ctxs[0].set_stream(torch.cuda.current_stream(device).cuda_stream)
+        ctxs[0].decode_plan_device(codec, d_in.data_ptr(), d_off.data_ptr(), m, d_oo.data_ptr(), d_rb.data_ptr(),
+                                   d_sc.data_ptr())
+        torch.cuda.synchronize(device)
+        ctxs[0].set_stream(streams[0].cuda_stream)
+        tot, rows = int(d_oo[m].item()), int(d_rb[m].item())
+        jobs.append(dict(m=m, h_in=h_in, h_off=h_off, d_in=d_in, d_off=d_off, d_oo=d_oo, d_rb=d_rb, d_sc=d_sc,
+                         d_out=torch.empty(tot + 16, dtype=torch.uint8, device=device),
+                         d_meta=torch.empty(m * 16, dtype=torch.uint8, device=device),
+                         d_rows=torch.empty(max(rows, 1) * 16, dtype=torch.uint8, device=device),
+                         h_out=torch.empty(tot + 16, dtype=torch.uint8).pin_memory(),
+                         h_meta=torch.empty(m * 16, dtype=torch.uint8).pin_memory(),
+                         h_rows=torch.empty(max(rows, 1) * 16, dtype=torch.uint8).pin_memory()))
+
+    def run():
+        for i, j in enumerate(jobs):
+            s, c = streams[i % n_streams], ctxs[i % n_streams]
+            with torch.cuda.stream(s):
+                j["d_in"].copy_(j["h_in"], non_blocking=True)
+                j["d_off"].copy_(j["h_off"], non_blocking=True)
+                c.decode_plan_device(codec, j["d_in"].data_ptr(), j["d_off"].data_ptr(), j["m"], j["d_oo"].data_ptr(),
+                                     j["d_rb"].data_ptr(), j["d_sc"].data_ptr())
+                c.decode_device(codec, j["d_in"].data_ptr(), j["d_off"].data_ptr(), j["m"], j["d_out"].data_ptr(),
+                                j["d_oo"].data_ptr(), j["d_meta"].data_ptr(), j["d_rows"].data_ptr(),
+                                j["d_rb"].data_ptr())
+                j["h_out"].copy_(j["d_out"], non_blocking=True)
+                j["h_meta"].copy_(j["d_meta"], non_blocking=True)
+                j["h_rows"].copy_(j["d_rows"], non_blocking=True)
+        torch.cuda.synchronize(device)
+
+    run()  # warm
+    t = time.perf_counter()
+    run()
+    el = time.perf_counter() - t
+    meta = np.concatenate([np.frombuffer(j["h_meta"].numpy().tobytes(), dtype=sc.META_DTYPE) for j in jobs])
+    assert (meta["status"] == 0).all()
+    dec = int(np.sum(meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2))
+    h2d = int(in_off[n]) + 8 * (n + len(jobs))
+    d2h = sum(j["h_out"].numel() + j["h_meta"].numel() + j["h_rows"].numel() for j in jobs)
+    for c in ctxs:
+        c.close()
+    return {"GiBps_decoded": round(dec / el / 2**30, 2), "blocks": n, "streams": n_streams, "chunk_blocks": chunk,
+            "h2d_GBps": round(h2d / el / 1e9, 2), "d2h_GBps": round(d2h / el / 1e9, 2),
+            "path": "pinned H2D + plan + decode + D2H (data, meta, rows), overlapped over streams"}
 
 
 def host_io_rate(torch, sc, ctx, codec, blob, in_off, dec_bytes, device):

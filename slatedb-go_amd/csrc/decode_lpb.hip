@@ -453,6 +453,8 @@ __global__ __launch_bounds__(kLpbThreads) void decode_lpb_kernel(DecodeArgs a) {
           reinterpret_cast<uint4*>(L.gout)[L.fl] = v;
           L.fl++;
         }
+        // let the row walker catch up on the block's last bytes (still in the ring)
+        for (int i = 0; i < 16 && L.d >= L.rneed; i++) walk_rows(L, ring);
         if (dn < 2) {
           m.status = SLATE_E_BLOCK_UNCOMP_SMALL;
         } else {
