@@ -51,6 +51,105 @@ int ctx_crc32_host_buffer(slate_ctx* ctx, const uint8_t* data, size_t n, uint32_
   return ctx_crc32_device(ctx, ctx->e_i.as<uint8_t>(), n, crc);
 }
 
+// ---------------------------------------------------------- Snappy helpers
+// snappy.Encode (golang/snappy encode.go:17-42) of a device buffer: one wave per
+// 64 KiB chunk on the GPU; the host only concatenates varint ‖ chunk outputs.
+int ctx_snappy_encode_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std::vector<uint8_t>& out) {
+  SLATE_HIP(ctx_bind(ctx));
+  const uint64_t nch = (uint64_t(n) + kSnapMaxChunk - 1) / kSnapMaxChunk;
+  SLATE_HIP(ctx->e_h.ensure(nch * kSnapChunkSlot + nch * 4 + 64));
+  uint8_t* slots = ctx->e_h.as<uint8_t>();
+  uint32_t* lens = reinterpret_cast<uint32_t*>(slots + nch * kSnapChunkSlot);
+  SLATE_HIP(launch_snappy_chunks(ctx->stream, d_src, n, slots, lens, ctx->num_cus));
+  std::vector<uint32_t> hl(nch);
+  if (nch) SLATE_HIP(hipMemcpyAsync(hl.data(), lens, nch * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  out.clear();
+  uint64_t v = n;
+  while (v >= 0x80) {
+    out.push_back(uint8_t(v) | 0x80);
+    v >>= 7;
+  }
+  out.push_back(uint8_t(v));
+  size_t o = out.size(), total = out.size();
+  for (uint64_t c = 0; c < nch; c++) total += hl[c];
+  out.resize(total);
+  for (uint64_t c = 0; c < nch; c++) {
+    if (hl[c]) SLATE_HIP(hipMemcpyAsync(out.data() + o, slots + c * kSnapChunkSlot, hl[c], hipMemcpyDeviceToHost,
+                                        ctx->stream));
+    o += hl[c];
+  }
+  SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  return SLATE_OK;
+}
+
+int ctx_snappy_encode_host(slate_ctx* ctx, const uint8_t* data, size_t n, std::vector<uint8_t>& out) {
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(ctx->e_i.ensure(n + 16));
+  if (n) SLATE_HIP(hipMemcpyAsync(ctx->e_i.p, data, n, hipMemcpyHostToDevice, ctx->stream));
+  return ctx_snappy_encode_device(ctx, ctx->e_i.as<uint8_t>(), n, out);
+}
+
+// compress.Encode (compression.go:80-116) for the codecs the GPU implements.
+static int codec_encode_host(slate_ctx* ctx, int codec, const uint8_t* data, size_t n, std::vector<uint8_t>& out) {
+  if (codec == SLATE_CODEC_NONE) {
+    out.assign(data, data + n);
+    return SLATE_OK;
+  }
+  if (codec == SLATE_CODEC_SNAPPY) return ctx_snappy_encode_host(ctx, data, n, out);
+  return SLATE_E_CODEC_UNSUPPORTED;
+}
+
+// CRC32 verify + snappy.Decode of one `payload ‖ BE32 CRC` buffer (index,
+// filter) on the GPU: the lane-per-block decoder in raw mode.  *bstatus gets
+// SLATE_OK, SLATE_E_BLOCK_CHECKSUM or SLATE_E_SNAPPY_CORRUPT.
+int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
+                             int* bstatus) {
+  if (len < 4) return SLATE_E_INVALID_ARG;
+  const size_t clen = len - 4;
+  uint64_t dl = 0;
+  {
+    uint64_t x = 0;
+    uint32_t sft = 0;
+    bool ok = false;
+    for (size_t i = 0; i < clen && i < 10; i++) {
+      uint32_t bt = buf[i];
+      if (bt < 0x80) {
+        if (i == 9 && bt > 1) break;
+        x |= uint64_t(bt) << sft;
+        ok = x <= 0xffffffffull;
+        break;
+      }
+      x |= uint64_t(bt & 0x7f) << sft;
+      sft += 7;
+    }
+    if (ok && x <= kSnappyMaxExpansion * uint64_t(clen)) dl = x;  // else the kernel reports it
+  }
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->d_in.ensure(len + 16));
+  SLATE_HIP(ctx->d_out.ensure(align16(dl) + 32));
+  SLATE_HIP(ctx->d_scratch.ensure(128));
+  uint64_t* u = ctx->d_scratch.as<uint64_t>();  // in_off[2] | out_off[2] | row_base[2] | meta(16) | rows(16)
+  const uint64_t hv[6] = {0, len, 0, align16(dl), 0, 0};
+  SLATE_HIP(hipMemcpyAsync(ctx->d_in.p, buf, len, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(u, hv, sizeof(hv), hipMemcpyHostToDevice, st));
+  DecodeArgs a{SLATE_CODEC_SNAPPY, ctx->d_in.as<uint8_t>(), u, 1, ctx->d_out.as<uint8_t>(), u + 2,
+               reinterpret_cast<slate_block_meta*>(u + 6), reinterpret_cast<slate_row*>(u + 8), u + 4,
+               nullptr, reinterpret_cast<uint32_t*>(u + 10), 0};
+  a.raw = 1;
+  SLATE_HIP(launch_decode_lpb(st, a, ctx->num_cus));
+  slate_block_meta m;
+  SLATE_HIP(hipMemcpyAsync(&m, u + 6, sizeof(m), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  *bstatus = m.status;
+  if (m.status == SLATE_OK) {
+    out.resize(m.data_len);
+    if (m.data_len) SLATE_HIP(hipMemcpy(out.data(), ctx->d_out.p, m.data_len, hipMemcpyDeviceToHost));
+  }
+  return SLATE_OK;
+}
+
 // --------------------------------------------------------------- SST builder
 struct slate_sst_table {
   slate_sst_info info{};
@@ -157,9 +256,38 @@ static int builder_flush(slate_sst_builder* b, bool final) {
   std::vector<uint64_t> out_off(nb + 1);
   SLATE_HIP(hipMemcpyAsync(out_off.data(), w.block_size, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
-  const uint64_t total = out_off[nb];
-  std::vector<uint8_t> out(total);
-  if (nb) {
+  std::vector<uint8_t> out;
+  if (nb && b->cfg.codec == SLATE_CODEC_SNAPPY) {
+    // raw sizes -> per-block slots; golang/snappy + CRC per block; scan of the
+    // compressed sizes; compaction into back-to-back blocks
+    const uint64_t raw_total = out_off[nb];
+    SLATE_HIP(ctx->s_slots.ensure(snappy_slots_bytes(raw_total, nb)));
+    SLATE_HIP(ctx->s_aux.ensure((nb + 1) * 8 + 64));
+    uint8_t* slots = ctx->s_slots.as<uint8_t>();
+    uint64_t* csize = ctx->s_aux.as<uint64_t>();
+    SLATE_HIP(hipMemsetAsync(csize + nb, 0, 8, st));
+    SLATE_HIP(launch_pack_snappy(st, a, w, uint32_t(nb), w.block_size, slots, csize, ctx->num_cus));
+    uint32_t big = 0;
+    SLATE_HIP(hipMemcpyAsync(&big, w.big_count, 4, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (big) {
+      SLATE_HIP(ctx->s_raw.ensure(raw_total + 64));
+      SLATE_HIP(launch_pack_snappy_big(st, a, w, w.block_size, ctx->s_raw.as<uint8_t>(), slots, csize, big,
+                                       ctx->num_cus));
+    }
+    SLATE_HIP(launch_scan_u64(st, csize, uint32_t(nb + 1), scan_scratch));
+    std::vector<uint64_t> fin(nb + 1);
+    SLATE_HIP(hipMemcpyAsync(fin.data(), csize, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    SLATE_HIP(ctx->e_e.ensure(fin[nb] + 16));
+    SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
+    out.resize(fin[nb]);
+    if (fin[nb]) SLATE_HIP(hipMemcpyAsync(out.data(), ctx->e_e.p, fin[nb], hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    out_off.swap(fin);
+  } else if (nb) {
+    const uint64_t total = out_off[nb];
+    out.resize(total);
     SLATE_HIP(ctx->e_e.ensure(total + 16));
     SLATE_HIP(launch_pack(st, a, w, uint32_t(nb), w.block_size, ctx->e_e.as<uint8_t>(), ctx->num_cus));
     uint32_t status = 0;
@@ -222,7 +350,7 @@ slate_sst_builder* slate_sst_builder_new(slate_ctx* ctx, const slate_sst_config*
     *status = SLATE_E_INVALID_CODEC;
     return nullptr;
   }
-  if (cfg->codec != SLATE_CODEC_NONE) {  // GPU Snappy/Zstd/LZ4/Zlib encode: not yet
+  if (cfg->codec != SLATE_CODEC_NONE && cfg->codec != SLATE_CODEC_SNAPPY) {  // Zlib/LZ4/Zstd encode: not yet
     *status = SLATE_E_CODEC_UNSUPPORTED;
     return nullptr;
   }
@@ -329,26 +457,42 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
       SLATE_HIP(hipMemsetAsync(words, 0, (nb + 3) & ~uint64_t(3), ctx->stream));
       SLATE_HIP(launch_bloom_build(ctx->stream, b->d_hashes.as<uint64_t>(), b->n_hashes, np, uint32_t(nb * 8), words));
     }
-    // encoded filter = BE16 numProbes || bits || BE32 CRC (None codec)
+    // encoded filter = compress(BE16 numProbes || bits) || BE32 CRC (bloom.go:52-67)
     uint8_t hdr[2] = {uint8_t(np >> 8), uint8_t(np)};
     uint8_t* enc = ctx->e_g.as<uint8_t>();
     SLATE_HIP(hipMemcpyAsync(enc, hdr, 2, hipMemcpyHostToDevice, ctx->stream));
     if (nb) SLATE_HIP(hipMemcpyAsync(enc + 2, words, nb, hipMemcpyDeviceToDevice, ctx->stream));
-    uint32_t crc = 0;
-    st = ctx_crc32_device(ctx, enc, nb + 2, &crc);
-    if (st) { delete t; return st; }
     t->bloom_bits.resize(nb);
-    if (nb) SLATE_HIP(hipMemcpy(t->bloom_bits.data(), words, nb, hipMemcpyDeviceToHost));
+    if (nb) SLATE_HIP(hipMemcpyAsync(t->bloom_bits.data(), words, nb, hipMemcpyDeviceToHost, ctx->stream));
+    SLATE_HIP(hipStreamSynchronize(ctx->stream));
+    uint32_t crc = 0;
+    const size_t f0 = buf.size();
+    if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
+      std::vector<uint8_t> comp;
+      st = ctx_snappy_encode_device(ctx, enc, nb + 2, comp);
+      if (st) { delete t; return st; }
+      st = ctx_crc32_host_buffer(ctx, comp.data(), comp.size(), &crc);
+      if (st) { delete t; return st; }
+      buf.insert(buf.end(), comp.begin(), comp.end());
+    } else {
+      st = ctx_crc32_device(ctx, enc, nb + 2, &crc);
+      if (st) { delete t; return st; }
+      buf.push_back(hdr[0]);
+      buf.push_back(hdr[1]);
+      buf.insert(buf.end(), t->bloom_bits.begin(), t->bloom_bits.end());
+    }
     t->has_bloom = true;
     t->num_probes = np;
-    buf.push_back(hdr[0]);
-    buf.push_back(hdr[1]);
-    buf.insert(buf.end(), t->bloom_bits.begin(), t->bloom_bits.end());
     put_be32(buf, crc);
-    filter_len = nb + 6;
+    filter_len = buf.size() - f0;
   }
   // ---- index (builder.go:238-244, flatbuf.go:126-139)
-  std::vector<uint8_t> index = fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
+  std::vector<uint8_t> index;
+  {
+    std::vector<uint8_t> fb = fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
+    st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
+    if (st) { delete t; return st; }
+  }
   uint32_t icrc = 0;
   st = ctx_crc32_host_buffer(ctx, index.data(), index.size(), &icrc);
   if (st) { delete t; return st; }
@@ -507,9 +651,18 @@ int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   if (st) return st;
   if (crc != ld_be32(buf + ci)) return SLATE_E_INDEX_CHECKSUM;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;  // GPU stream decode of large buffers: next
+  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
   slate_index* x = new slate_index();
-  x->data.assign(buf, buf + ci);
+  if (codec == SLATE_CODEC_SNAPPY) {
+    int bst = 0;
+    st = ctx_snappy_decode_buffer(ctx, buf, len, x->data, &bst);
+    if (st || bst) {
+      delete x;
+      return st ? st : (bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_INDEX_CHECKSUM : bst);
+    }
+  } else {
+    x->data.assign(buf, buf + ci);
+  }
   if (!fb_decode_index(x->data.data(), x->data.size(), &x->offsets, &x->keys, &x->key_off)) {
     delete x;
     return SLATE_E_FLATBUF;
@@ -620,11 +773,13 @@ int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits,
                        uint8_t* out, size_t out_cap, size_t* out_len) {
   if (!ctx || (bits_len && !bits)) return SLATE_E_INVALID_ARG;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;
-  std::vector<uint8_t> buf(bits_len + 2);
-  buf[0] = uint8_t(num_probes >> 8);
-  buf[1] = uint8_t(num_probes);
-  if (bits_len) memcpy(buf.data() + 2, bits, bits_len);
+  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
+  std::vector<uint8_t> raw(bits_len + 2), buf;
+  raw[0] = uint8_t(num_probes >> 8);
+  raw[1] = uint8_t(num_probes);
+  if (bits_len) memcpy(raw.data() + 2, bits, bits_len);
+  int est = codec_encode_host(ctx, codec, raw.data(), raw.size(), buf);
+  if (est) return est;
   uint32_t crc = 0;
   int st = ctx_crc32_host_buffer(ctx, buf.data(), buf.size(), &crc);
   if (st) return st;
@@ -646,12 +801,23 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   if (st) return st;
   if (crc != ld_be32(buf + ci)) return SLATE_E_FILTER_CHECKSUM;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;
-  if (ci < 2) return SLATE_E_FILTER_PANIC;
-  if (num_probes) *num_probes = ld_be16(buf);
-  if (bits_len) *bits_len = ci - 2;
-  if (ci - 2 > bits_cap || (!bits && ci > 2)) return SLATE_E_CAPACITY;
-  if (ci > 2) memcpy(bits, buf + 2, ci - 2);
+  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
+  std::vector<uint8_t> dec;
+  const uint8_t* p = buf;
+  size_t pn = ci;
+  if (codec == SLATE_CODEC_SNAPPY) {
+    int bst = 0;
+    st = ctx_snappy_decode_buffer(ctx, buf, len, dec, &bst);
+    if (st) return st;
+    if (bst) return bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_FILTER_CHECKSUM : bst;
+    p = dec.data();
+    pn = dec.size();
+  }
+  if (pn < 2) return SLATE_E_FILTER_PANIC;
+  if (num_probes) *num_probes = ld_be16(p);
+  if (bits_len) *bits_len = pn - 2;
+  if (pn - 2 > bits_cap || (!bits && pn > 2)) return SLATE_E_CAPACITY;
+  if (pn > 2) memcpy(bits, p + 2, pn - 2);
   return SLATE_OK;
 }
 
@@ -683,11 +849,13 @@ int slate_block_encode(slate_ctx* ctx, int codec, const uint8_t* data, size_t da
                        size_t n_offsets, uint8_t* out, size_t out_cap, size_t* out_len) {
   if (!ctx || (data_len && !data) || (n_offsets && !offsets)) return SLATE_E_INVALID_ARG;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE) return SLATE_E_CODEC_UNSUPPORTED;
-  std::vector<uint8_t> buf(data_len + 2 * n_offsets + 2);
-  if (data_len) memcpy(buf.data(), data, data_len);
-  for (size_t i = 0; i < n_offsets; i++) st_be16(buf.data() + data_len + 2 * i, offsets[i]);
-  st_be16(buf.data() + data_len + 2 * n_offsets, uint16_t(n_offsets));
+  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
+  std::vector<uint8_t> raw(data_len + 2 * n_offsets + 2), buf;
+  if (data_len) memcpy(raw.data(), data, data_len);
+  for (size_t i = 0; i < n_offsets; i++) st_be16(raw.data() + data_len + 2 * i, offsets[i]);
+  st_be16(raw.data() + data_len + 2 * n_offsets, uint16_t(n_offsets));
+  int est = codec_encode_host(ctx, codec, raw.data(), raw.size(), buf);
+  if (est) return est;
   uint32_t crc = 0;
   int st = ctx_crc32_host_buffer(ctx, buf.data(), buf.size(), &crc);
   if (st) return st;

@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kLpbThreads) void decode_lpb_kernel(DecodeArgs a) {
     L.last_chunk = 0;
     if (have) {
       const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
-      if (len < 6) {
+      if (len < (a.raw ? 4u : 6u)) {
         m.status = SLATE_E_BLOCK_TOO_SMALL;
         a.meta[b] = m;
         have = false;
@@ -455,7 +455,9 @@ __global__ __launch_bounds__(kLpbThreads) void decode_lpb_kernel(DecodeArgs a) {
         }
         // let the row walker catch up on the block's last bytes (still in the ring)
         for (int i = 0; i < 16 && L.d >= L.rneed; i++) walk_rows(L, ring);
-        if (dn < 2) {
+        if (a.raw) {
+          m.data_len = dn;  // a decompressed index / filter buffer
+        } else if (dn < 2) {
           m.status = SLATE_E_BLOCK_UNCOMP_SMALL;
         } else {
           // block.go:101-134 over the decoded block, now in HBM (this lane's own stores)
@@ -513,12 +515,19 @@ __global__ __launch_bounds__(kLpbThreads) void decode_lpb_kernel(DecodeArgs a) {
                       if (walk_ok && end_last > uint32_t(osi)) walk_ok = false;
                     }
                     if (walk_ok) {
+                      // a row failing the prefix check keeps only its key lengths (row.go:203-206)
                       const uint32_t fk0 = L.grows[0].key_suffix_len;
                       const bool fk_nil = L.grows[0].key_prefix_len != 0;  // row 0 itself fails
-                      if (fk_nil) L.grows[0].status = SLATE_E_ROW_PREFIX;
-                      for (uint32_t i = 1; i < nr; i++) {
+                      for (uint32_t i = 0; i < nr; i++) {
                         const uint32_t pl = L.grows[i].key_prefix_len;
-                        if (fk_nil ? pl != 0 : pl > fk0) L.grows[i].status = SLATE_E_ROW_PREFIX;
+                        if (i == 0 ? fk_nil : (fk_nil ? pl != 0 : pl > fk0)) {
+                          slate_row r = L.grows[i];
+                          r.value_len = 0;
+                          r.flags = 0;
+                          r.meta_len = 0;
+                          r.status = SLATE_E_ROW_PREFIX;
+                          L.grows[i] = r;
+                        }
                       }
                     } else {
                       int fk = -1;

@@ -7,6 +7,10 @@ namespace slate {
 constexpr int kPackThreads = 256;        // 4 wavefronts, one block each
 constexpr uint32_t kPackCap = 8192;      // LDS bytes per wavefront for one encoded block
 constexpr uint32_t kPackBigCap = 155648; // one wavefront per workgroup
+constexpr int kSnapThreads = 128;        // Snappy pack: 2 wavefronts, ~21 KiB LDS each
+constexpr uint32_t kSnapRaw = 4096;      // raw block bytes handled in LDS (BlockSize 4096)
+constexpr uint64_t kSnapChunkSlot = 76544;  // >= MaxEncodedLen(64 KiB), 16-aligned
+constexpr uint64_t kSnapMaxChunk = 65536;   // golang/snappy maxBlockSize
 
 struct EncodeArgs {
   const uint8_t* keys;
@@ -48,6 +52,16 @@ hipError_t launch_bloom_build(hipStream_t st, const uint64_t* hashes, uint64_t n
                               uint32_t filter_bits, uint32_t* words);
 hipError_t launch_bloom_check(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
                               const uint8_t* bits, uint64_t bits_len, uint32_t num_probes, uint8_t* out);
+// Snappy (golang/snappy byte-exact) block and buffer encode
+size_t snappy_slots_bytes(uint64_t raw_total, uint64_t nblocks);
+hipError_t launch_pack_snappy(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, uint32_t nblocks,
+                              const uint64_t* raw_off, uint8_t* slots, uint64_t* csize, int num_cus);
+hipError_t launch_pack_snappy_big(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, const uint64_t* raw_off,
+                                  uint8_t* rawbuf, uint8_t* slots, uint64_t* csize, uint32_t big_count, int num_cus);
+hipError_t launch_compact(hipStream_t st, const uint8_t* slots, const uint64_t* raw_off, const uint64_t* final_off,
+                          uint32_t nblocks, uint8_t* out, int num_cus);
+hipError_t launch_snappy_chunks(hipStream_t st, const uint8_t* src, uint64_t n, uint8_t* dst, uint32_t* len,
+                                int num_cus);
 size_t crc_scratch_bytes(uint64_t n);
 hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out);
 // In-place exclusive scan of one u64 array of n+1 entries (the last becomes the total).

@@ -19,11 +19,13 @@
 //                      write into the SST byte stream
 //   bloom kernels      probes (enhanced double hashing) -> atomicOr bitset
 //   crc kernels        CRC32 of a large device buffer (filter / index)
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
 #include "encode.h"
 #include "wave_crc.h"
+#include "snappy_enc.h"
 
 namespace slate {
 
@@ -218,11 +220,12 @@ __device__ inline void write_bytes_from_lds(uint8_t* gdst, const uint8_t* lds, u
   for (uint32_t t = tail0 + lane; t < len; t += kWave) gdst[t] = lds[t];
 }
 
-template <bool kLds>
-__device__ void pack_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
-                           uint8_t* buf, const uint32_t* tab, uint8_t* gdst, uint64_t enc_len, int lane) {
+// rows ‖ BE16 offsets ‖ BE16 count of the block holding KVs [s, e) into buf
+// (block.go:162-182 Add, :54-64 Encode before compression); raw_len bytes.
+__device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
+                               uint8_t* buf, uint32_t raw_len, int lane) {
   const uint32_t nrows = e - s;
-  const uint32_t data_len = uint32_t(enc_len - 4 - 2 * uint64_t(nrows) - 2);
+  const uint32_t data_len = raw_len - 2 * nrows - 2;
   // rows, 64 at a time: prefix (running min of adjacent LCPs), row offset (scan)
   uint32_t carry_off = 0, carry_min = 0xFFFFFFFFu;
   for (uint32_t r0 = 0; r0 < nrows; r0 += kWave) {
@@ -272,7 +275,13 @@ __device__ void pack_block(const EncodeArgs& a, const uint32_t* adj, bool sorted
   if (lane == 0) st_be16(buf + data_len + 2 * nrows, uint16_t(nrows));
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_s_waitcnt(0);
-  uint32_t raw_len = uint32_t(enc_len - 4);
+}
+
+template <bool kLds>
+__device__ void pack_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
+                           uint8_t* buf, const uint32_t* tab, uint8_t* gdst, uint64_t enc_len, int lane) {
+  const uint32_t raw_len = uint32_t(enc_len - 4);
+  assemble_block(a, adj, sorted, s, e, buf, raw_len, lane);
   uint32_t crc = wave_crc32(tab, buf, 0, raw_len, lane);
   if (lane == 0) st_be32(buf + raw_len, crc);
   __builtin_amdgcn_wave_barrier();
@@ -333,6 +342,113 @@ __global__ __launch_bounds__(64) void enc_pack_big_kernel(EncodeArgs a, const ui
     }
     uint32_t s = block_start[b];
     pack_block<true>(a, adj, sorted, s, next[s], buf, tab, out + out_off[b], enc_len, lane);
+  }
+}
+
+// ----------------------------------------------------------- Snappy blocks
+// block.Encode with CodecSnappy (block.go:54-75): raw block assembled in LDS,
+// golang/snappy encoded in LDS (snappy_enc.h), CRC32 of the compressed bytes,
+// written to a per-block slot; a scan of the compressed sizes and a compaction
+// pass place the blocks back to back.
+__device__ inline uint64_t snap_slot_off(uint64_t raw_off, uint64_t b) { return align16(raw_off + raw_off / 6 + 48 * b); }
+
+constexpr uint32_t kSnapOut = uint32_t(((snappy_max_encoded_len(kSnapRaw) + 4 + 15) & ~15ull) + 16);
+constexpr uint32_t kSnapWaveBytes = kSnapRaw + 16 + kSnapOut + 2 * kSnapRaw + kSnapRaw;
+
+__global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
+    EncodeArgs a, const uint32_t* __restrict__ adj, const uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ block_start, const uint32_t* __restrict__ next, const uint64_t* __restrict__ raw_off,
+    uint32_t nblocks, uint8_t* __restrict__ slots, uint64_t* __restrict__ csize, uint32_t* __restrict__ big_list,
+    uint32_t* __restrict__ big_count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* raw = smem + kTabBytes + wave * kSnapWaveBytes;
+  uint8_t* out = raw + kSnapRaw + 16;
+  uint16_t* table = reinterpret_cast<uint16_t*>(out + kSnapOut);
+  uint8_t* owner = reinterpret_cast<uint8_t*>(table + kSnapRaw);
+  const bool sorted = (*flags & 1u) == 0;
+  const uint32_t waves = gridDim.x * (kSnapThreads / 64);
+  for (uint32_t b = blockIdx.x * (kSnapThreads / 64) + wave; b < nblocks; b += waves) {
+    const uint64_t raw_len = raw_off[b + 1] - raw_off[b] - 4;
+    if (raw_len > kSnapRaw) {
+      if (lane == 0) big_list[atomicAdd(big_count, 1u)] = b;
+      continue;
+    }
+    const uint32_t s = block_start[b];
+    assemble_block(a, adj, sorted, s, next[s], raw, uint32_t(raw_len), lane);
+    const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), out, table, owner, lane);
+    const uint32_t crc = wave_crc32(tab, out, 0, clen, lane);
+    if (lane == 0) st_be32(out + clen, crc);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0);
+    write_bytes_from_lds(slots + snap_slot_off(raw_off[b], b), out, clen + 4, lane);
+    if (lane == 0) csize[b] = clen + 4;
+  }
+}
+
+// Blocks above kSnapRaw bytes: one wave per workgroup, raw block staged in HBM,
+// full 16 Ki-slot table in LDS.
+__global__ __launch_bounds__(64) void enc_pack_snappy_big_kernel(
+    EncodeArgs a, const uint32_t* __restrict__ adj, const uint32_t* __restrict__ flags,
+    const uint32_t* __restrict__ block_start, const uint32_t* __restrict__ next, const uint64_t* __restrict__ raw_off,
+    uint8_t* __restrict__ rawbuf, uint8_t* __restrict__ slots, uint64_t* __restrict__ csize,
+    const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ big_count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63;
+  uint16_t* table = reinterpret_cast<uint16_t*>(smem + kTabBytes);
+  uint8_t* owner = reinterpret_cast<uint8_t*>(table + kSnapMaxTable);
+  const bool sorted = (*flags & 1u) == 0;
+  const uint32_t cnt = *big_count;
+  for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+    const uint32_t b = big_list[k];
+    const uint64_t raw_len = raw_off[b + 1] - raw_off[b] - 4;
+    uint8_t* rp = rawbuf + raw_off[b];
+    uint8_t* sp = slots + snap_slot_off(raw_off[b], b);
+    const uint32_t s = block_start[b];
+    assemble_block(a, adj, sorted, s, next[s], rp, uint32_t(raw_len), lane);
+    __threadfence();
+    const uint32_t clen = snappy_encode_wave(rp, uint32_t(raw_len), sp, table, owner, lane);
+    __threadfence();
+    const uint32_t crc = wave_crc32(tab, sp, 0, clen, lane);
+    if (lane == 0) {
+      st_be32(sp + clen, crc);
+      csize[b] = clen + 4;
+    }
+  }
+}
+
+// slots -> back-to-back blocks at final_off (exclusive scan of csize)
+__global__ void enc_compact_kernel(const uint8_t* __restrict__ slots, const uint64_t* __restrict__ raw_off,
+                                   const uint64_t* __restrict__ final_off, uint32_t nblocks, uint8_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t waves = gridDim.x * (blockDim.x / 64);
+  for (uint32_t b = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); b < nblocks; b += waves) {
+    write_bytes_from_lds(out + final_off[b], slots + snap_slot_off(raw_off[b], b),
+                         uint32_t(final_off[b + 1] - final_off[b]), lane);
+  }
+}
+
+// snappy.Encode of one large buffer (bloom filter, index): one wave per 64 KiB
+// chunk, chunk c's encoding at dst + c * kSnapChunkSlot, its length in len[c].
+__global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __restrict__ src, uint64_t n,
+                                                           uint8_t* __restrict__ dst, uint32_t* __restrict__ len) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  uint16_t* table = reinterpret_cast<uint16_t*>(smem);
+  uint8_t* owner = reinterpret_cast<uint8_t*>(table + kSnapMaxTable);
+  const uint64_t nchunks = (n + kSnapMaxBlock - 1) / kSnapMaxBlock;
+  for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const uint8_t* p = src + c * kSnapMaxBlock;
+    const uint32_t pn = uint32_t(min<uint64_t>(n - c * kSnapMaxBlock, kSnapMaxBlock));
+    uint8_t* o = dst + c * kSnapChunkSlot;
+    uint32_t d;
+    if (pn < kSnapMinNonLiteral) d = snap_emit_literal(o, 0, p, pn, lane);
+    else d = snappy_encode_block_wave(p, pn, o, table, owner, lane);
+    if (lane == 0) len[c] = d;
   }
 }
 
@@ -491,6 +607,46 @@ hipError_t launch_pack(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w,
                                                    w.big_list, w.big_count);
   enc_pack_big_kernel<<<uint32_t(num_cus), 64, kTabBytes + kPackBigCap, st>>>(
       a, w.adj, w.flags, w.block_start, w.next, out_off, out, w.big_list, w.big_count, w.status);
+  return hipGetLastError();
+}
+
+size_t snappy_slots_bytes(uint64_t raw_total, uint64_t nblocks) {
+  return align16(raw_total + raw_total / 6 + 48 * nblocks) + 64;
+}
+
+hipError_t launch_pack_snappy(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, uint32_t nblocks,
+                              const uint64_t* raw_off, uint8_t* slots, uint64_t* csize, int num_cus) {
+  if (nblocks == 0) return hipGetLastError();
+  const size_t lds = kTabBytes + (kSnapThreads / 64) * size_t(kSnapWaveBytes);
+  uint32_t grid = min(blocks_for(nblocks, kSnapThreads / 64), uint32_t(num_cus) * 3);
+  enc_pack_snappy_kernel<<<grid, kSnapThreads, lds, st>>>(a, w.adj, w.flags, w.block_start, w.next, raw_off, nblocks,
+                                                          slots, csize, w.big_list, w.big_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_snappy_big(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, const uint64_t* raw_off,
+                                  uint8_t* rawbuf, uint8_t* slots, uint64_t* csize, uint32_t big_count, int num_cus) {
+  if (big_count == 0) return hipGetLastError();
+  const size_t lds = kTabBytes + kSnapMaxTable * 3;
+  enc_pack_snappy_big_kernel<<<min(big_count, uint32_t(num_cus) * 2), 64, lds, st>>>(
+      a, w.adj, w.flags, w.block_start, w.next, raw_off, rawbuf, slots, csize, w.big_list, w.big_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(hipStream_t st, const uint8_t* slots, const uint64_t* raw_off, const uint64_t* final_off,
+                          uint32_t nblocks, uint8_t* out, int num_cus) {
+  if (nblocks == 0) return hipGetLastError();
+  enc_compact_kernel<<<min(blocks_for(nblocks, 4), uint32_t(num_cus) * 8), 256, 0, st>>>(slots, raw_off, final_off,
+                                                                                       nblocks, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_snappy_chunks(hipStream_t st, const uint8_t* src, uint64_t n, uint8_t* dst, uint32_t* len,
+                                int num_cus) {
+  const uint64_t nchunks = (n + kSnapMaxBlock - 1) / kSnapMaxBlock;
+  if (nchunks == 0) return hipGetLastError();
+  snappy_chunks_kernel<<<uint32_t(std::min<uint64_t>(nchunks, uint64_t(num_cus) * 2)), 64, kSnapMaxTable * 3, st>>>(
+      src, n, dst, len);
   return hipGetLastError();
 }
 

@@ -57,9 +57,11 @@ struct slate_ctx {
   DevBuf d_in, d_in_off, d_out, d_out_off, d_meta, d_rows, d_row_base, d_scratch;
   // encode / misc buffers
   DevBuf e_a, e_b, e_c, e_d, e_e, e_f, e_g, e_h, e_i, e_j;
+  // Snappy encode: per-block slots, raw staging for oversized blocks, snappy LDS-free scratch
+  DevBuf s_slots, s_raw, s_aux;
   void release_all() {
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
-                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j})
+                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &s_slots, &s_raw, &s_aux})
       b->release();
   }
 };

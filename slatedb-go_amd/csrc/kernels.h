@@ -30,6 +30,7 @@ struct DecodeArgs {
   uint32_t* large_list;   // filled by the launcher from scratch
   uint32_t* large_count;
   uint32_t debug;         // ablation switches for profiling only (SLATE_DEBUG_MODE); 0 in production
+  uint32_t raw = 0;       // LPB only: payload is not a block (index/filter buffer): CRC + decompress, no block checks
 };
 
 struct DecodeScratch {

@@ -1,0 +1,266 @@
+// golang/snappy v0.0.4 block-format encoder (encode.go Encode + encode_other.go
+// encodeBlock/emitLiteral/emitCopy), one wavefront per buffer, byte-exact.
+//
+// The match finder's probe loop is serial in Go: probe t at position s_t reads
+// table[hash(s_t)] and then writes s_t there.  The positions themselves do not
+// depend on the table: s_{t+1} = s_t + (skip_t >> 5) with skip starting at 32
+// (kProbe.cum).  So the wave evaluates 64 consecutive probes at once:
+//   * each lane hashes its position;
+//   * a lane's candidate is the table entry, or, when an earlier lane of the
+//     batch hashed to the same slot, that lane's position (positions increase, so
+//     the latest earlier writer is the one Go would see).  Collisions are
+//     detected through an LDS owner array; the rare colliding batch takes a
+//     64-step shuffle scan;
+//   * the first lane whose 4 bytes match ends the batch; only lanes up to it
+//     commit their table writes (the last writer per slot).
+// Match extension compares 64 bytes per step with a ballot; literals are copied
+// by all lanes.  Table bookkeeping after each copy is done by lane 0 in Go order.
+#pragma once
+#include "common.h"
+
+namespace slate {
+
+typedef uint32_t snap_u32u __attribute__((aligned(1)));
+
+constexpr uint32_t kSnapMaxBlock = 65536;    // encode.go maxBlockSize
+constexpr uint32_t kSnapMinNonLiteral = 17;  // 1 + 1 + inputMargin
+constexpr uint32_t kSnapInputMargin = 15;
+constexpr uint32_t kSnapMaxTable = 1u << 14;
+constexpr uint32_t kProbeSlots = 320;        // cum[] reaches past 65536 at t = 266
+
+struct SnapProbe {
+  uint32_t cum[kProbeSlots + 1];
+  constexpr SnapProbe() : cum{} {
+    uint32_t skip = 32, c = 0;
+    for (uint32_t t = 0; t <= kProbeSlots; t++) {
+      cum[t] = c;
+      c += skip >> 5;
+      skip += skip >> 5;
+      if (c > 0x7FFFFFFFu) c = 0x7FFFFFFFu;
+    }
+  }
+};
+static __constant__ SnapProbe g_snap_probe = SnapProbe();
+
+__host__ __device__ constexpr uint64_t snappy_max_encoded_len(uint64_t n) { return 32 + n + n / 6; }
+
+// table slots used for a chunk of n bytes (encode_other.go:206-210)
+__device__ inline uint32_t snappy_table_size(uint32_t n, uint32_t* shift) {
+  uint32_t sh = 24, ts = 256;
+  while (ts < kSnapMaxTable && ts < n) {
+    ts <<= 1;
+    sh--;
+  }
+  *shift = sh;
+  return ts;
+}
+
+__device__ inline uint32_t snap_ld32(const uint8_t* p) { return *reinterpret_cast<const snap_u32u*>(p); }
+__device__ inline uint32_t snap_hash(uint32_t u, uint32_t shift) { return (u * 0x1e35a7bdu) >> shift; }
+
+// emitLiteral (encode_other.go:12-38): header by lane 0, bytes by all lanes
+__device__ inline uint32_t snap_emit_literal(uint8_t* dst, uint32_t d, const uint8_t* lit, uint32_t len, int lane) {
+  const uint32_t n = len - 1;
+  uint32_t hl;
+  if (n < 60) {
+    hl = 1;
+    if (lane == 0) dst[d] = uint8_t(n << 2);
+  } else if (n < 256) {
+    hl = 2;
+    if (lane == 0) {
+      dst[d] = 60 << 2;
+      dst[d + 1] = uint8_t(n);
+    }
+  } else {
+    hl = 3;
+    if (lane == 0) {
+      dst[d] = 61 << 2;
+      dst[d + 1] = uint8_t(n);
+      dst[d + 2] = uint8_t(n >> 8);
+    }
+  }
+  uint8_t* o = dst + d + hl;
+  for (uint32_t k = lane; k < len; k += kWave) o[k] = lit[k];
+  return d + hl + len;
+}
+
+// emitCopy (encode_other.go:40-76)
+__device__ inline uint32_t snap_emit_copy(uint8_t* dst, uint32_t d, uint32_t offset, uint32_t length, int lane) {
+  while (length >= 68) {
+    if (lane == 0) {
+      dst[d] = 63 << 2 | 2;
+      dst[d + 1] = uint8_t(offset);
+      dst[d + 2] = uint8_t(offset >> 8);
+    }
+    d += 3;
+    length -= 64;
+  }
+  if (length > 64) {
+    if (lane == 0) {
+      dst[d] = 59 << 2 | 2;
+      dst[d + 1] = uint8_t(offset);
+      dst[d + 2] = uint8_t(offset >> 8);
+    }
+    d += 3;
+    length -= 60;
+  }
+  if (length >= 12 || offset >= 2048) {
+    if (lane == 0) {
+      dst[d] = uint8_t((length - 1) << 2 | 2);
+      dst[d + 1] = uint8_t(offset);
+      dst[d + 2] = uint8_t(offset >> 8);
+    }
+    return d + 3;
+  }
+  if (lane == 0) {
+    dst[d] = uint8_t((offset >> 8) << 5 | (length - 4) << 2 | 1);
+    dst[d + 1] = uint8_t(offset);
+  }
+  return d + 2;
+}
+
+// first s' >= s with src[i + (s'-s)] != src[s'] or s' == n (encode_other.go:176)
+__device__ inline uint32_t snap_extend(const uint8_t* src, uint32_t n, uint32_t i, uint32_t s, int lane) {
+  for (;;) {
+    const uint32_t p = s + lane;
+    const bool stop = p >= n || src[i + lane] != src[p];
+    const uint64_t m = __ballot(stop);
+    if (m) return s + uint32_t(__builtin_ctzll(m));
+    s += kWave;
+    i += kWave;
+  }
+}
+
+__device__ inline void snap_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// encodeBlock (encode_other.go:165-238) for kSnapMinNonLiteral <= n <= 65536.
+// table: kSnapMaxTable u16 slots (LDS); owner: kSnapMaxTable bytes (LDS).
+__device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table,
+                                             uint8_t* owner, int lane) {
+  uint32_t shift;
+  const uint32_t ts = snappy_table_size(n, &shift);
+  for (uint32_t i = lane; i < ts; i += kWave) table[i] = 0;
+  snap_sync();
+  const int32_t s_limit = int32_t(n) - int32_t(kSnapInputMargin);
+  uint32_t d = 0, next_emit = 0;
+  int32_t s = 1;
+  for (;;) {
+    // ---------------- probe loop, 64 probes per batch
+    int32_t cand = 0;
+    bool found = false;
+    for (uint32_t t0 = 0;; t0 += kWave) {
+      const uint32_t t = t0 + lane;
+      const bool in_sched = t + 1 <= kProbeSlots;
+      const int32_t st = in_sched ? s + int32_t(g_snap_probe.cum[t]) : 0x7FFFFFFF;
+      const int32_t snext = in_sched ? s + int32_t(g_snap_probe.cum[t + 1]) : 0x7FFFFFFF;
+      const bool valid = in_sched && snext <= s_limit;
+      uint32_t cur = 0, h = 0;
+      if (valid) {
+        cur = snap_ld32(src + st);
+        h = snap_hash(cur, shift);
+        owner[h] = uint8_t(lane);
+      }
+      snap_sync();
+      const bool dup = valid && owner[h] != uint8_t(lane);
+      const uint64_t dupmask = __ballot(dup);
+      const uint64_t validmask = __ballot(valid);
+      int32_t c = valid ? int32_t(table[h]) : 0;
+      if (dupmask) {  // latest earlier lane of this batch with the same slot
+        bool got = false;
+        for (int k = 1; k < kWave; k++) {
+          const uint32_t hp = __shfl(h, lane - k, 64);
+          const int32_t sp = __shfl(st, lane - k, 64);
+          const bool vp = (validmask >> ((lane - k) & 63)) & 1;
+          if (!got && lane >= k && vp && hp == h) {
+            c = sp;
+            got = true;
+          }
+        }
+      }
+      const bool match = valid && cur == snap_ld32(src + c);
+      const uint64_t mm = __ballot(match);
+      const uint32_t istar = mm ? uint32_t(__builtin_ctzll(mm)) : 64u;
+      const bool ran = valid && uint32_t(lane) <= istar;
+      bool last = true;
+      if (dupmask) {  // a later lane that also ran overwrites the same slot
+        for (int k = 1; k < kWave; k++) {
+          const uint32_t hn = __shfl(h, lane + k, 64);
+          const uint32_t ln = uint32_t(lane + k);
+          const bool vn = ln < 64 && ((validmask >> (ln & 63)) & 1) && ln <= istar;
+          if (vn && hn == h) last = false;
+        }
+      }
+      if (ran && last) table[h] = uint16_t(st);
+      snap_sync();
+      if (mm) {
+        s = __shfl(st, int(istar), 64);
+        cand = __shfl(c, int(istar), 64);
+        found = true;
+        break;
+      }
+      if (validmask != ~0ull) break;  // nextS > sLimit: emitRemainder
+    }
+    if (!found) break;
+    // ---------------- emit literal + copies (encode_other.go:194-235)
+    d = snap_emit_literal(dst, d, src + next_emit, uint32_t(s) - next_emit, lane);
+    bool done = false;
+    for (;;) {
+      const int32_t base = s;
+      s = int32_t(snap_extend(src, n, uint32_t(cand) + 4, uint32_t(s) + 4, lane));
+      d = snap_emit_copy(dst, d, uint32_t(base - cand), uint32_t(s - base), lane);
+      next_emit = uint32_t(s);
+      if (s >= s_limit) {
+        done = true;
+        break;
+      }
+      const uint32_t lo = snap_ld32(src + s - 1), hi = snap_ld32(src + s + 3);
+      const uint32_t prev_hash = snap_hash(lo, shift);
+      const uint32_t x1 = (lo >> 8) | (hi << 24);
+      const uint32_t curr_hash = snap_hash(x1, shift);
+      if (lane == 0) table[prev_hash] = uint16_t(s - 1);
+      snap_sync();
+      cand = int32_t(table[curr_hash]);
+      snap_sync();
+      if (lane == 0) table[curr_hash] = uint16_t(s);
+      snap_sync();
+      if (x1 != snap_ld32(src + cand)) {
+        s++;
+        break;
+      }
+    }
+    if (done) break;
+  }
+  if (next_emit < n) d = snap_emit_literal(dst, d, src + next_emit, n - next_emit, lane);
+  snap_sync();
+  return d;
+}
+
+// snappy.Encode (encode.go:17-42): uvarint length, then 64 KiB blocks.
+__device__ __forceinline__ uint32_t snappy_encode_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table, uint8_t* owner,
+                                       int lane) {
+  uint32_t d = 0;
+  {
+    uint64_t v = n;
+    while (v >= 0x80) {
+      if (lane == 0) dst[d] = uint8_t(v) | 0x80;
+      d++;
+      v >>= 7;
+    }
+    if (lane == 0) dst[d] = uint8_t(v);
+    d++;
+  }
+  for (uint32_t p = 0; p < n;) {
+    const uint32_t pn = min(n - p, kSnapMaxBlock);
+    if (pn < kSnapMinNonLiteral) d = snap_emit_literal(dst, d, src + p, pn, lane);
+    else d += snappy_encode_block_wave(src + p, pn, dst + d, table, owner, lane);
+    p += pn;
+  }
+  snap_sync();
+  return d;
+}
+
+}  // namespace slate

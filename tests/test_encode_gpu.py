@@ -23,9 +23,10 @@ def ctx(sc):
     return sc.Context(0)
 
 
-def _build_both(sc, ctx, kvs, block_size=4096, mfk=0, bpk=10, batch=False, next_every=0):
-    g = sc.SstBuilder(ctx, block_size, mfk, bpk, sc.NONE)
-    o = ob.SstBuilder(block_size, mfk, bpk, ob.NONE)
+def _build_both(sc, ctx, kvs, block_size=4096, mfk=0, bpk=10, batch=False, next_every=0, codec=None):
+    codec = ob.NONE if codec is None else codec
+    g = sc.SstBuilder(ctx, block_size, mfk, bpk, codec)
+    o = ob.SstBuilder(block_size, mfk, bpk, codec)
     g_blocks, o_blocks = [], []
     if batch:
         keys = [k for k, _ in kvs]
@@ -177,3 +178,67 @@ def test_vhalf_workload_batch(sc, ctx):
 def test_empty_builder(sc, ctx):
     t, o, _ = _build_both(sc, ctx, [], 4096, 0, 10)
     assert t.encode() == o.encode_table()
+
+
+# ------------------------------------------------------------------ Snappy
+# golang/snappy v0.0.4 encoded bytes: the oracle restates encode_other.go; it is
+# byte-identical to libsnappy on the probes in test_oracle (parity vs Go itself
+# unpinned).
+
+@pytest.mark.parametrize("seed", range(6))
+def test_snappy_sst_bytes(sc, ctx, seed):
+    rng = random.Random(100 + seed)
+    kvs = bg.random_kvs(rng, rng.randint(1, 1500), alphabet=rng.choice([3, 256]), tomb_p=0.15)
+    bs = rng.choice([40, 128, 1024, 4096, 16384])
+    t, o, _ = _build_both(sc, ctx, kvs, bs, rng.choice([0, 10]), rng.choice([1, 10]), batch=seed % 2 == 0,
+                          next_every=rng.choice([0, 7]), codec=ob.SNAPPY)
+    assert t.chunks() == o.chunks()
+    assert t.encode() == o.encode_table()
+    assert t.info() == o.info()
+
+
+def test_snappy_vhalf_and_read_back(sc, ctx):
+    kvs = bg.kv_synthetic(38 * 300, half=True, tomb_every=20)
+    t, o, _ = _build_both(sc, ctx, kvs, 4096, 0, 10, batch=True, codec=ob.SNAPPY)
+    sst = t.encode()
+    assert sst == o.encode_table()
+    st, info, fk = sc.read_info(sst)
+    assert st == 0 and info.codec == ob.SNAPPY
+    st, index = ctx.decode_index(sst[info.index_offset: info.index_offset + info.index_len], info.codec)
+    assert st == 0
+    n = len(index.block_metas())
+    st, failed, (out, out_off, meta, rows, rb) = ctx.read_blocks(info, index, 0, n, sst)
+    assert st == 0 and failed == 2**64 - 1
+    assert int(meta["n_rows"].astype(np.int64).sum()) == len(kvs)
+    # bloom filter read back through the Snappy path
+    filt = sst[info.filter_offset: info.filter_offset + info.filter_len]
+    st, k, bits = ctx.bloom_decode(filt, sc.SNAPPY)
+    assert st == 0 and (k, bits) == (t.bloom()[0], t.bloom()[1])
+
+
+def test_snappy_large_rows_and_blocks(sc, ctx):
+    rng = random.Random(5)
+    vals = [bytes(rng.randrange(256) for _ in range(n)) for n in (10, 9000, 30000, 5)]
+    vals += [b"ab" * 20000, bytes(70000), b"xyz" * 30000]
+    kvs = [(b"a%03d" % i, v) for i, v in enumerate(vals)]
+    t, o, _ = _build_both(sc, ctx, kvs, 4096, 0, 10, codec=ob.SNAPPY)
+    assert t.encode() == o.encode_table()
+
+
+def test_snappy_block_encode_and_bloom(sc, ctx, ref_vectors):
+    for c in ref_vectors["block_roundtrips"]:
+        bb = ob.BlockBuilder(c["block_size"])
+        for k, val in c["kvs"]:
+            bb.add_value(k.encode(), (val or "").encode())
+        data, offs, _ = bb.build()
+        st, enc = ctx.block_encode(data, offs, sc.SNAPPY)
+        assert st == 0 and enc == ob.block_encode(data, offs, ob.SNAPPY)[1]
+    rng = np.random.default_rng(3)
+    for nbytes in (0, 1, 15, 16, 17, 100, 65534, 65535, 65536, 65537, 200_000, 1_000_003):
+        bits = rng.integers(0, 4, nbytes, dtype=np.uint8).tobytes()  # compressible
+        st, enc = ctx.bloom_encode(6, bits, sc.SNAPPY)
+        assert st == 0 and enc == ob.bloom_encode(6, bits, ob.SNAPPY), nbytes
+        assert ctx.bloom_decode(enc, sc.SNAPPY) == (0, 6, bits)
+    bad = bytearray(ctx.bloom_encode(6, b"abc" * 100, sc.SNAPPY)[1])
+    bad[3] ^= 0x40
+    assert ctx.bloom_decode(bytes(bad), sc.SNAPPY)[0] == 31
