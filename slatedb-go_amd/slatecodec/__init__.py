@@ -256,6 +256,10 @@ class Context:
         npr = C.c_uint16()
         bl = C.c_size_t()
         st = lib().slate_bloom_decode(self._h, _ptr(b), len(buf), codec, C.byref(npr), _ptr(out), cap, C.byref(bl))
+        if st == E_CAPACITY:  # compressed filter: bits_len holds the decoded size
+            cap = bl.value + 16
+            out = np.zeros(cap, np.uint8)
+            st = lib().slate_bloom_decode(self._h, _ptr(b), len(buf), codec, C.byref(npr), _ptr(out), cap, C.byref(bl))
         return st, npr.value, (out[: bl.value].tobytes() if st == OK else b"")
 
     def decode_index(self, buf: bytes, codec: int):
