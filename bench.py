@@ -157,7 +157,7 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": "decode_lpb_kernel" if args.codec == "snappy" else "decode_fast_kernel", "kernel_ms": round(kern_ms, 4),
+                "kernel": "decode_lpb2_kernel" if args.codec == "snappy" else "decode_fast_kernel", "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg, "alg_read_bytes": alg_read, "alg_write_bytes": alg_write,
                 "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 

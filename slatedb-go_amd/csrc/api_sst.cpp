@@ -138,7 +138,7 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
                reinterpret_cast<slate_block_meta*>(u + 6), reinterpret_cast<slate_row*>(u + 8), u + 4,
                nullptr, reinterpret_cast<uint32_t*>(u + 10), 0};
   a.raw = 1;
-  SLATE_HIP(launch_decode_lpb(st, a, ctx->num_cus));
+  SLATE_HIP(launch_decode_lpb2(st, a, ctx->num_cus));
   slate_block_meta m;
   SLATE_HIP(hipMemcpyAsync(&m, u + 6, sizeof(m), hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));

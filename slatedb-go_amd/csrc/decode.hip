@@ -534,7 +534,9 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   if (a.n == 0) return hipGetLastError();
   // Snappy: lane-per-block streaming decoder (any block size); SLATE_DEBUG_MODE bit 16
   // selects the wave-per-block path instead (ablation only)
-  if (a.codec == SLATE_CODEC_SNAPPY && !(a.debug & 16)) return launch_decode_lpb(st, a, num_cus);
+  // (bit 32: the v1 lane-per-block kernel, A/B only)
+  if (a.codec == SLATE_CODEC_SNAPPY && !(a.debug & 16))
+    return (a.debug & 32) ? launch_decode_lpb(st, a, num_cus) : launch_decode_lpb2(st, a, num_cus);
   const size_t lds = kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap);
   uint32_t wgs_needed = (a.n + kDecodeThreads / 64 - 1) / (kDecodeThreads / 64);
   uint32_t grid = min(wgs_needed, uint32_t(num_cus) * kDecodeWgPerCu);

@@ -1,0 +1,669 @@
+// Lane-per-block Snappy block decode (the headline kernel).
+//
+// block.Decode (internal/sstable/block/block.go:78-134) with CodecSnappy:
+// CRC32 verify -> golang/snappy v0.0.4 decode (decode_other.go:19-110) ->
+// offset checks -> row descriptors (row.go:191-261 as block/iterator.go walks).
+//
+// One lane owns one block; the 64 lanes of a wave decode 64 consecutive blocks
+// in lockstep, so one wave instruction advances 64 independent Snappy tag
+// streams (the chain inside one block is serial).
+//
+// Memory pipeline.  Every step issues exactly four vector-memory instructions,
+// unconditionally: the next 16-byte input chunk (buffer_load nt), the source of a
+// pending long-distance copy (buffer_load nt), the completed 16-byte output chunk
+// (buffer_store) and the row descriptor finished this step (buffer_store).  A lane
+// with nothing to move gives an out-of-range offset: the hardware drops the access
+// (tools/buf_probe.hip).  The vmcnt bookkeeping is therefore static, and data loaded
+// in one step is consumed four steps later (rotating registers P0..P3, Q0..Q3) while
+// the loads of the three steps in between stay in flight.
+//
+// Per lane, LDS holds
+//   * an input ring of 8 x 16-byte chunks (+16-byte mirror).  The CRC32 is absorbed
+//     as each chunk is committed (slicing-by-4, tables shared by the workgroup).
+//     Bytes of a chunk outside the block are zeroed for the CRC: the register starts
+//     from a per-alignment state that reaches 0xFFFFFFFF after the leading zeros,
+//     and the trailing zeros are folded into the stored value (x^(8t) mod P);
+//   * an output ring of 128 bytes (+mirror and pads).
+// A step parses a tag if the previous one is used up (branch-free), then moves up
+// to 16 bytes with ONE unaligned ds_read_b128 (input ring for literals, output ring
+// for copies with offset <= 112, the far-load register for longer offsets) and ONE
+// unaligned ds_write_b128 (+ a mirror write near the ring ends).  gfx950 executes
+// unaligned b128 DS accesses correctly (tools/lds_probe2.hip).  Copies with offset
+// < 16 double their effective offset after every step (the output is periodic).
+// A row walker reads each row's header fields from the output ring as they are
+// produced; at block end the walk is compared with the block's offset array, and
+// on any mismatch rows are re-derived from HBM with the exact row.go decoder.
+#include "common.h"
+#include "kernels.h"
+#include "wave_crc.h"
+
+namespace slate {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+
+namespace {
+
+constexpr uint32_t kOR = 128;          // output ring bytes
+constexpr uint32_t kReach = kOR - 16;  // ring positions still valid behind d
+constexpr uint32_t kNS = 4;            // input ring slots
+constexpr uint32_t kIR = kNS * 16;
+// LDS per lane, 240 bytes: an output-ring record [pad 16][ring 128][mirror 16] (stride 160;
+// lane i's pad doubles as lane i-1's post-pad: both only ever write junk there) and an
+// input-ring record [ring 64][mirror 16] (stride 80) in a second array.
+constexpr uint32_t kOutStride = 16 + kOR + 16;
+constexpr uint32_t kInStride = kIR + 16;
+constexpr uint32_t kConstWords = 32;                  // crc_init[16] | tail_mul[16]
+constexpr uint32_t kOOB = 0xFFFFFFF0u;                // buffer offset that is always out of range
+#ifndef SLATE_IN_AUX
+#define SLATE_IN_AUX 0
+#endif
+constexpr int kInAux = SLATE_IN_AUX;
+
+// CRC register state that becomes 0xFFFFFFFF after `sh` zero bytes (sh < 16), and x^(8t) mod P.
+struct CrcLeadTail {
+  uint32_t init[16];
+  uint32_t tail[16];
+  constexpr CrcLeadTail() : init{}, tail{} {
+    for (uint32_t sh = 0; sh < 16; sh++) {
+      uint32_t s = 0xFFFFFFFFu;
+      for (uint32_t b = 0; b < 8 * sh; b++) s = (s & 0x80000000u) ? (((s ^ kCrcPoly) << 1) | 1u) : (s << 1);
+      init[sh] = s;
+      tail[sh] = x8n(sh);
+    }
+  }
+};
+static __constant__ CrcLeadTail g_crc_lt = CrcLeadTail();
+
+// Unaligned LDS b128/b64: gfx950 executes ds_read_b128 / ds_write_b128 / ds_read_b64 at any
+// byte address (tools/lds_probe2.hip).  The natural alignment of v4u/v2u is what makes the
+// compiler emit the single wide instruction instead of ds_read2_b32 pairs, whose behaviour
+// at unaligned addresses is not established.
+__device__ __forceinline__ v4u lds_rd16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
+__device__ __forceinline__ void lds_wr16(uint8_t* p, v4u v) { *reinterpret_cast<v4u*>(p) = v; }
+__device__ __forceinline__ v2u lds_rd8(const uint8_t* p) { return *reinterpret_cast<const v2u*>(p); }
+__device__ __forceinline__ uint32_t lds_rd4(const uint8_t* p) { return *reinterpret_cast<const u32_u*>(p); }
+__device__ __forceinline__ uint32_t be16_of(uint32_t w) { return ((w & 0xff) << 8) | ((w >> 8) & 0xff); }
+
+// Cache policy (gfx950 CPol bits): 0 = default (allocates in L2: a lane reads its block's 128-byte
+// lines 16 bytes at a time, so the line must stay for the next 7 accesses), 16 = sc1 (bypasses the
+// CU's L1, for reads of this kernel's own output), 2 = nt (streaming).
+template <int kAux>
+__device__ __forceinline__ v4u bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAux);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, v4u v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+// Resources must be in SGPRs (a VGPR resource turns every buffer op into a waterfall loop):
+// the inputs are wave-uniform, readfirstlane makes that visible to the compiler.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+  return (uint64_t(hi) << 32) | lo;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint64_t b = uniform64(reinterpret_cast<uint64_t>(base));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes < kOOB ? uint32_t(bytes) : kOOB);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0, int(n), 0x00020000);
+}
+
+// Reads of this kernel's own output go around the CU's L1 (nt): a line another wave
+// of this CU loaded earlier could be stale.
+__device__ __forceinline__ uint32_t out_u8(const uint8_t* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ uint32_t out_be16(const uint8_t* p) { return (out_u8(p) << 8) | out_u8(p + 1); }
+__device__ __forceinline__ uint32_t out_be32(const uint8_t* p) { return (out_be16(p) << 16) | out_be16(p + 2); }
+
+// byte mask of dword j (bytes 4j..4j+3 of a chunk) keeping chunk bytes [lo, hi)
+__device__ __forceinline__ uint32_t keep_mask(int32_t lo, int32_t hi, int32_t j) {
+  const int32_t a = min(max(lo - 4 * j, 0), 4), b = min(max(hi - 4 * j, 0), 4);
+  const uint64_t m = ((uint64_t(1) << (8 * b)) - 1) & ~((uint64_t(1) << (8 * a)) - 1);
+  return uint32_t(m);
+}
+
+__device__ __forceinline__ v4u pack_row(uint32_t off, uint32_t pl, uint32_t sl, uint32_t vl, uint32_t flags,
+                                        uint32_t meta_len, uint32_t status) {
+  v4u r;
+  r.x = off;
+  r.y = (pl & 0xffff) | (sl << 16);
+  r.z = vl;
+  r.w = (flags & 0xff) | ((meta_len & 0xff) << 8) | ((status & 0xffff) << 16);
+  return r;
+}
+
+// v0 row decode (row.go:191-261) reading the decoded block from HBM: the exact
+// fallback when the streaming walk does not match the offset array.
+__device__ v4u row_from_hbm(const uint8_t* data, uint32_t data_len, uint32_t off, int fk, uint32_t* sl_out) {
+  *sl_out = 0;
+  const uint8_t* p = data + off;
+  const uint32_t n = data_len - off;
+  uint32_t pl = 0, sl = 0;
+  if (n >= 4) {
+    pl = out_be16(p);
+    sl = out_be16(p + 2);
+  }
+  if (n < 13) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_TOO_SHORT));
+  if (pl > uint32_t(fk < 0 ? 0 : fk)) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_PREFIX));
+  uint32_t o = 4;
+  if (n - o < sl) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_SUFFIX));
+  o += sl;
+  if (n - o < 9) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_PANIC));
+  const uint32_t flags = out_u8(p + o + 8);
+  o += 9;
+  if (flags & 2) {
+    if (n - o < 8) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_EXPIRE));
+    o += 8;
+  }
+  if (flags & 4) {
+    if (n - o < 8) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_CREATE));
+    o += 8;
+  }
+  uint32_t vl = 0;
+  if ((flags & 1) == 0) {
+    if (n - o < 4) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_VALUE_LEN));
+    vl = out_be32(p + o);
+    o += 4;
+    if (n - o < vl) return pack_row(off, pl, sl, 0, 0, 0, uint32_t(SLATE_E_ROW_VALUE));
+  }
+  *sl_out = sl;
+  return pack_row(off, pl, sl, vl, flags & 7, o - 4 - sl, SLATE_OK);
+}
+
+struct Lane {
+  // block
+  uint32_t in_rel, out_rel, rows_rel;  // offsets of this block in the round's buffer resources
+  uint32_t sh, clen, dn, last_chunk, rcap;
+  int32_t crc_last;
+  uint32_t crc, crc_pos;
+  // decode
+  uint32_t s, d, rem, src, eff, lit, far, dd, err;
+  uint32_t c_issue, c_commit, pend, fpend, fready, fl;
+  // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
+  // follows them), 2 = value length after timestamps, 3 = stopped
+  uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
+};
+
+struct Rsrc {
+  __amdgpu_buffer_rsrc_t in, out, rows;
+};
+
+// CRC32 of the next committed input chunk (bytes outside the block zeroed).
+__device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint32_t* tab, bool go) {
+  const uint32_t k = L.crc_pos;
+  v4u v = *reinterpret_cast<const v4u*>(in + (k & (kNS - 1)) * 16);
+  const bool partial = go && (k == 0 || int32_t(k) == L.crc_last);
+  if (__builtin_amdgcn_ballot_w64(partial)) {  // wave-uniform branch: first/last chunks only
+    const int32_t lo = int32_t(L.sh) - int32_t(16 * k), hi = int32_t(L.sh + L.clen) - int32_t(16 * k);
+    v.x &= keep_mask(lo, hi, 0);
+    v.y &= keep_mask(lo, hi, 1);
+    v.z &= keep_mask(lo, hi, 2);
+    v.w &= keep_mask(lo, hi, 3);
+  }
+  uint32_t c = L.crc;
+  c = crc_word(tab, c, v.x);
+  c = crc_word(tab, c, v.y);
+  c = crc_word(tab, c, v.z);
+  c = crc_word(tab, c, v.w);
+  L.crc = go ? c : L.crc;
+  L.crc_pos += go ? 1u : 0u;
+}
+
+// Row walker, one action per call (row.go:191-261 field order), branch-free.
+// Returns true with `row`/`ridx` set when the action finished a row.
+__device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
+  const bool wa = act && L.rphase < 3 && L.d >= L.rneed;
+  const uint32_t fp = L.R + 4 + L.rsl + 8;
+  const uint32_t rpos = L.rphase == 0 ? L.R : (L.rphase == 1 ? fp : L.R + L.ro);
+  const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
+  const v2u q = lds_rd8(ring + (rpos & (kOR - 1)));
+  // phase 0: prefix / suffix lengths
+  const uint32_t pl0 = be16_of(q.x), sl0 = be16_of(q.x >> 16);
+  // phase 1: flags, and the value length right after them when there are no timestamps
+  const uint32_t fl1 = q.x & 0xff;
+  const uint32_t ts = ((fl1 & 2) ? 8u : 0u) + ((fl1 & 4) ? 8u : 0u);
+  const uint32_t ro1 = 4 + L.rsl + 9 + ts;
+  const bool tomb = (fl1 & 1) != 0;
+  const bool done1 = tomb || ts == 0;
+  const uint32_t vl1 = tomb ? 0u : __builtin_bswap32((q.x >> 8) | (q.y << 24));
+  // phase 2: value length after the timestamps
+  const uint32_t vl2 = __builtin_bswap32(q.x);
+  const bool p0 = L.rphase == 0, p1 = L.rphase == 1;
+  const bool done = wa && !lost && ((p1 && done1) || L.rphase == 2);
+  const uint32_t vl = p1 ? vl1 : vl2;
+  const uint32_t flags = p1 ? fl1 : L.rflags;
+  const uint32_t ro = p1 ? ro1 : L.ro;
+  const uint32_t rlen = (p1 && tomb) ? ro1 : ro + 4;
+  row = pack_row(L.R, L.rpl, L.rsl, vl, flags & 7, rlen - 4 - L.rsl, SLATE_OK);
+  ridx = L.nwalk;
+  const bool emit = done && L.nwalk < L.rcap;
+  const uint64_t next = uint64_t(L.R) + rlen + vl;
+  // state transitions
+  const bool to1 = wa && !lost && p0;
+  const bool to2 = wa && !lost && p1 && !done1;
+  L.rpl = to1 ? pl0 : L.rpl;
+  L.rsl = to1 ? sl0 : L.rsl;
+  L.rflags = (wa && p1) ? fl1 : L.rflags;
+  L.ro = (wa && p1) ? ro1 : L.ro;
+  L.nwalk += done ? 1u : 0u;
+  const bool stop = (wa && lost) || (done && next > L.dn);
+  const bool adv = done && next <= L.dn;
+  L.R = adv ? uint32_t(next) : L.R;
+  L.rphase = stop ? 3u : (adv ? 0u : (to1 ? 1u : (to2 ? 2u : L.rphase)));
+  L.rneed = stop ? 0xFFFFFFFFu
+            : adv ? uint32_t(next) + 4
+            : to1 ? L.R + 4 + sl0 + 13
+            : to2 ? L.R + ro1 + 4
+                  : L.rneed;
+  return emit;
+}
+
+// One pipeline step (slot `bit`): consume what the loads of four steps ago brought
+// (input chunk P, far-copy source Q), parse / copy, then issue this step's four
+// memory instructions.  Straight-line code: every lane executes every instruction
+// and conditions select values or junk addresses, because in lockstep some lane
+// always needs each part.
+template <bool kCrcSlot>
+__device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint32_t bit, bool act, uint8_t* ring,
+                                          uint8_t* in, uint8_t* junk, const uint32_t* tab, const Rsrc& R,
+                                          uint32_t dbg) {
+  // ---- commit the input chunk loaded four steps ago
+  {
+    const bool cm = (L.pend & bit) != 0;
+    const uint32_t k = L.c_commit;
+    lds_wr16(cm ? in + (k & (kNS - 1)) * 16 : junk, P);
+    lds_wr16((cm && (k & (kNS - 1)) == 0) ? in + kIR : junk, P);
+    L.c_commit += cm ? 1u : 0u;
+    L.pend &= cm ? ~bit : ~0u;
+  }
+  // ---- the far-copy source loaded four steps ago
+  {
+    const bool fc = (L.fpend & bit) != 0;
+    FD = fc ? Q : FD;
+    L.fready = fc ? 1u : L.fready;
+    L.fpend = fc ? 0u : L.fpend;
+  }
+  // ---- CRC32 of one committed chunk (two of the four steps)
+  if (kCrcSlot) {
+    const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
+    if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
+    else crc_chunk(L, in, tab, go);
+  }
+  const int32_t avail = int32_t(16 * L.c_commit) - int32_t(L.sh);  // committed payload bytes [0, avail)
+  const uint32_t sn = L.clen;
+  // ---- parse the next tag (golang/snappy decode_other.go:19-110)
+  {
+    const bool need = act && !L.dd && L.rem == 0;
+    const bool fin = need && L.s >= sn;
+    const bool can = need && L.s < sn && avail >= int32_t(min(L.s + 5, sn));
+    const v2u w = lds_rd8(in + ((L.sh + L.s) & (kIR - 1)));
+    const uint32_t c = w.x & 0xff, t = c & 3;
+    const uint32_t b14 = (w.x >> 8) | (w.y << 24);  // bytes s+1 .. s+4
+    const uint32_t xl = c >> 2;
+    const uint32_t nb = xl >= 60 ? xl - 59 : 0;
+    const uint32_t ext = nb >= 4 ? b14 : (b14 & ((1u << (8 * nb)) - 1));
+    const uint64_t lit_len = uint64_t(nb ? ext : xl) + 1;
+    const uint32_t cp_len = t == 1 ? 4 + ((c >> 2) & 7) : 1 + (c >> 2);
+    const uint32_t cp_off = t == 1 ? (((c & 0xe0) << 3) | (b14 & 0xff)) : (t == 2 ? (b14 & 0xffff) : b14);
+    const uint32_t hl = t == 0 ? 1 + nb : (t == 1 ? 2 : (t == 2 ? 3 : 5));
+    const uint32_t s1 = L.s + hl;
+    const bool bad_lit = lit_len > uint64_t(L.dn - L.d) || lit_len > uint64_t(sn - min(s1, sn));
+    const bool bad_cp = cp_off == 0 || L.d < cp_off || cp_len > L.dn - L.d;
+    const bool bad = s1 > sn || (t == 0 ? bad_lit : bad_cp);
+    const bool ok = can && !bad;
+    L.err |= (can && bad) ? 1u : 0u;
+    L.dd |= (fin || (can && bad)) ? 1u : 0u;
+    L.lit = ok ? uint32_t(t == 0) : L.lit;
+    L.rem = ok ? (t == 0 ? uint32_t(lit_len) : cp_len) : L.rem;
+    L.src = ok ? (t == 0 ? s1 : L.d - cp_off) : L.src;
+    L.eff = ok ? (t == 0 ? 16u : cp_off) : L.eff;
+    L.far = ok ? uint32_t(t != 0 && cp_off > kReach && !(dbg & 256)) : L.far;
+    L.s = ok ? (t == 0 ? s1 + uint32_t(lit_len) : s1) : L.s;
+  }
+  // ---- move up to 16 bytes of the current tag into the output ring
+  {
+    const bool cp = act && !L.dd && L.rem != 0;
+    uint32_t k = min(L.rem, 16u);
+    k = L.lit ? min(k, uint32_t(max(avail - int32_t(L.src), 0))) : (L.far ? (L.fready ? k : 0u) : min(k, L.eff));
+    k = cp ? k : 0u;
+    const v4u vl = lds_rd16(L.lit ? in + ((L.sh + L.src) & (kIR - 1)) : ring + (L.src & (kOR - 1)));
+    const v4u v = L.far ? FD : vl;
+    // bytes at [d, d+16) are not yet output: writing them when k == 0 is harmless
+    const uint32_t x = L.d & (kOR - 1);
+    lds_wr16(ring + x, v);
+    // mirror upkeep: ring[0..16) is duplicated at ring[128..144); a write crossing
+    // the end also lands at the start (pads absorb the overhang on both sides)
+    lds_wr16(x < 16 ? ring + x + kOR : (x > kOR - 16 ? ring + x - kOR : junk), v);
+    L.d += k;
+    L.rem -= k;
+    const bool step_cp = k != 0 && !L.lit && !L.far;
+    const uint32_t eff2 = (step_cp && L.eff < 16) ? 2 * L.eff : L.eff;  // periodic output: the pattern doubles
+    L.src = (L.lit || L.far) ? L.src + k : L.d - eff2;
+    L.eff = eff2;
+    L.fready = (L.far && k) ? 0u : L.fready;
+  }
+  // ---- the four memory instructions of this step (always issued)
+  {
+    // the ring keeps every chunk from the oldest byte still to be read or CRC'd
+    const uint32_t lo_pos = L.dd ? L.clen : ((L.rem && L.lit) ? L.src : L.s);
+    const uint32_t lo_chunk = min((L.sh + lo_pos) >> 4, L.crc_pos);
+    const bool room = act && L.c_issue <= L.last_chunk && L.c_issue < lo_chunk + kNS;
+    P = bload<kInAux>(R.in, room ? L.in_rel + 16 * L.c_issue : kOOB);
+    L.pend |= room ? bit : 0u;
+    L.c_issue += room ? 1u : 0u;
+    const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
+    Q = bload<16>(R.out, wantf ? L.out_rel + L.src : kOOB);
+    L.fpend = wantf ? bit : L.fpend;
+    const bool flush = act && (L.d >> 4) > L.fl;
+    const v4u o = *reinterpret_cast<const v4u*>(ring + ((L.fl * 16) & (kOR - 1)));
+    bstore(R.out, flush ? L.out_rel + 16 * L.fl : kOOB, o);
+    L.fl += flush ? 1u : 0u;
+    if (!kCrcSlot) {  // the row walker runs in the two steps without a CRC chunk
+      v4u row;
+      uint32_t ridx;
+      const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
+      bstore(R.rows, have_row ? L.rows_rel + 16 * ridx : kOOB, row);
+    }
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  {
+    const uint32_t* src = &g_crc_tables.t[0][0];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];
+    const uint32_t* lt = &g_crc_lt.init[0];
+    for (uint32_t i = threadIdx.x; i < kConstWords; i += blockDim.x) tab[1024 + i] = lt[i];
+    __syncthreads();
+  }
+  const uint32_t* crc_init = tab + 1024;
+  const uint32_t* crc_tail = tab + 1024 + 16;
+  uint8_t* outs = smem + kTabBytes + 4 * kConstWords;
+  uint8_t* ring = outs + threadIdx.x * kOutStride + 16;
+  uint8_t* junk = ring - 16;  // this lane's pad: write-only
+  uint8_t* in = outs + kLpb2Threads * kOutStride + 16 + threadIdx.x * kInStride;
+  const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
+  // wave-uniform by construction: the buffer resources derived from it must live in SGPRs
+  // (a VGPR resource turns every buffer op into a waterfall loop)
+  const uint32_t wave_g = blockIdx.x * (kLpb2Threads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+
+  for (uint32_t round0 = wave_g * 64; round0 < a.n; round0 += waves_total * 64) {
+    // ---- the round's buffer resources (wave-uniform)
+    const uint32_t rend = min(round0 + 64, a.n);
+    const uint8_t* in_lo = a.in + a.in_off[round0];
+    const uint8_t* in_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(in_lo) & ~uintptr_t(15));
+    const uint8_t* in_hi = a.in + a.in_off[rend];
+    Rsrc R;
+    R.in = make_rsrc(in_base, align16(uint64_t(in_hi - in_base)));
+    uint8_t* out_base = a.out + a.out_off[round0];
+    R.out = make_rsrc(out_base, a.out_off[rend] - a.out_off[round0]);
+    slate_row* rows_base = a.rows + a.row_base[round0];
+    R.rows = make_rsrc(rows_base, 16 * (a.row_base[rend] - a.row_base[round0]));
+
+    Lane L;
+    v4u P0 = {0, 0, 0, 0}, P1 = P0, P2 = P0, P3 = P0, Q0 = P0, Q1 = P0, Q2 = P0, Q3 = P0, FD = P0;
+    const uint32_t b = round0 + lane;
+    slate_block_meta m{};
+    bool have = b < a.n;
+    L.in_rel = L.out_rel = L.rows_rel = 0;
+    L.sh = L.clen = L.dn = L.last_chunk = L.rcap = 0;
+    L.crc_last = -1;
+    L.crc = 0xFFFFFFFFu;
+    L.crc_pos = 0;
+    L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = 0;
+    L.eff = 16;
+    L.dd = 1;
+    L.c_issue = L.c_commit = L.pend = L.fpend = L.fready = L.fl = 0;
+    L.R = 0;
+    L.rphase = 0;
+    L.rneed = 4;
+    L.rsl = L.rpl = L.rflags = L.ro = L.nwalk = 0;
+    if (have) {
+      const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
+      if (len < (a.raw ? 4u : 6u)) {
+        m.status = SLATE_E_BLOCK_TOO_SMALL;
+        a.meta[b] = m;
+        have = false;
+      } else {
+        const uint8_t* gin = a.in + s0;
+        L.sh = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
+        L.in_rel = uint32_t((gin - L.sh) - in_base);
+        L.clen = uint32_t(len - 4);
+        L.last_chunk = uint32_t((L.sh + len - 1) >> 4);
+        L.crc_last = L.clen ? int32_t((L.sh + L.clen - 1) >> 4) : -1;
+        L.crc = L.clen ? crc_init[L.sh] : 0xFFFFFFFFu;
+        L.out_rel = uint32_t(a.out_off[b] - a.out_off[round0]);
+        const uint64_t rb = a.row_base[b];
+        L.rows_rel = uint32_t(16 * (rb - a.row_base[round0]));
+        L.rcap = uint32_t(min<uint64_t>(a.row_base[b + 1] - rb, 0xFFFFFFFFull));
+      }
+    }
+    // ---- the block's first two chunks (aligned, inside the block's chunk range), then
+    // golang/snappy decodedLen (decode.go:20-31) over the committed ring
+    {
+      const v4u c0 = bload<kInAux>(R.in, have ? L.in_rel : kOOB);
+      const v4u c1 = bload<kInAux>(R.in, (have && L.last_chunk >= 1) ? L.in_rel + 16 : kOOB);
+      if (have) {
+        *reinterpret_cast<v4u*>(in) = c0;
+        *reinterpret_cast<v4u*>(in + kIR) = c0;
+        *reinterpret_cast<v4u*>(in + 16) = c1;
+        L.c_commit = L.last_chunk >= 1 ? 2u : 1u;
+        L.c_issue = L.c_commit;
+        uint64_t x = 0;
+        uint32_t sft = 0, hdr = 0;
+        bool ok = false, stop = false;
+        for (uint32_t i = 0; i < 10 && i < L.clen && !stop; i++) {
+          const uint32_t bt = in[L.sh + i];
+          if (bt < 0x80) {
+            if (!(i == 9 && bt > 1)) {
+              x |= uint64_t(bt) << sft;
+              ok = x <= 0xffffffffull;
+              hdr = i + 1;
+            }
+            stop = true;
+          } else {
+            x |= uint64_t(bt & 0x7f) << sft;
+            sft += 7;
+          }
+        }
+        if (!ok || x > kSnappyMaxExpansion * uint64_t(L.clen)) {
+          L.err = 1;
+        } else {
+          L.dn = uint32_t(x);
+          L.s = hdr;
+          L.dd = 0;
+        }
+      }
+    }
+
+    // ---------------- streaming decode, 64 blocks in lockstep, 4-deep memory pipeline
+    uint32_t iters = 0;
+    const uint64_t t_round = (a.debug & 512) ? __builtin_amdgcn_s_memtime() : 0;
+    // a lane is done when its decode is finished and every chunk is committed and in the CRC.
+    // Every step consumes input, produces output or waits on a load issued at most four steps
+    // earlier, so a block needs far fewer than `budget` iterations; the budget only guarantees
+    // that the loop ends (an exhausted lane reports SLATE_E_HIP, never a wrong result).
+    const uint32_t budget = have ? (L.clen + L.dn) / 2 + 1024 : 0u;
+    while (__ballot(have && !(L.dd && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
+                    iters < budget)) {
+      const bool act = have && !(L.dd && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
+                       iters < budget;
+      lane_step<true>(L, P0, Q0, FD, 1u, act, ring, in, junk, tab, R, a.debug);
+      lane_step<false>(L, P1, Q1, FD, 2u, act, ring, in, junk, tab, R, a.debug);
+      lane_step<true>(L, P2, Q2, FD, 4u, act, ring, in, junk, tab, R, a.debug);
+      lane_step<false>(L, P3, Q3, FD, 8u, act, ring, in, junk, tab, R, a.debug);
+      iters++;
+    }
+    const uint32_t round_cycles = (a.debug & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
+
+    // ---------------- finalise the round's blocks (SIMD across lanes)
+    if (have && iters >= budget) {
+      m.status = SLATE_E_HIP;  // step budget exhausted (see above): a kernel defect, reported loudly
+      a.meta[b] = m;
+      have = false;
+    }
+    if (have) {
+      uint8_t* gout = out_base + L.out_rel;
+      slate_row* grows = reinterpret_cast<slate_row*>(reinterpret_cast<uint8_t*>(rows_base) + L.rows_rel);
+      const uint32_t stored = __builtin_bswap32(lds_rd4(in + ((L.sh + L.clen) & (kIR - 1))));
+      // the register absorbed t zero bytes after the message: compare against stored * x^(8t)
+      const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
+      const bool crc_ok = gf2_mulmod(~stored, crc_tail[t]) == L.crc;
+      const bool snappy_ok = !L.err && L.d == L.dn && L.s == L.clen && L.rem == 0;
+      const uint32_t dn = L.dn;
+      if (!crc_ok) {
+        m.status = SLATE_E_BLOCK_CHECKSUM;
+      } else if (!snappy_ok) {
+        m.status = SLATE_E_SNAPPY_CORRUPT;
+      } else {
+        // remaining output chunks (the last one is padded inside its 16-byte slot)
+        while (L.fl * 16 < dn) {
+          const v4u o = *reinterpret_cast<const v4u*>(ring + ((L.fl * 16) & (kOR - 1)));
+          reinterpret_cast<v4u*>(gout)[L.fl] = o;
+          L.fl++;
+        }
+        // let the row walker catch up on the block's last bytes (still in the ring)
+        for (int i = 0; i < 16 && L.rphase < 3 && L.d >= L.rneed; i++) {
+          v4u row;
+          uint32_t ridx;
+          if (walk_step(L, ring, true, row, ridx)) reinterpret_cast<v4u*>(grows)[ridx] = row;
+        }
+        if (a.raw) {
+          m.data_len = dn;  // a decompressed index / filter buffer
+        } else if (dn < 2) {
+          m.status = SLATE_E_BLOCK_UNCOMP_SMALL;
+        } else {
+          // block.go:101-134 over the decoded block.  The tail (offsets, count) is read
+          // from the output ring when it is still there, else from HBM.
+          const uint32_t cnt = be16_of(lds_rd4(ring + ((dn - 2) & (kOR - 1))));
+          const int64_t osi = int64_t(dn) - 2 - 2 * int64_t(cnt);
+          if (osi <= 0) {
+            m.status = SLATE_E_BLOCK_INDEX_OFFSET;
+            m.detail = int32_t(osi);
+          } else {
+            const bool tail_in_ring = dn - uint32_t(osi) <= kReach;
+            auto off_at = [&](uint32_t i) -> uint32_t {
+              const uint32_t p = uint32_t(osi) + 2 * i;
+              if (tail_in_ring) return be16_of(lds_rd4(ring + (p & (kOR - 1))));
+              return out_be16(gout + p);
+            };
+            const uint16_t osi16 = uint16_t(osi);
+            uint32_t bad = 0xFFFFFFFFu;
+            const uint32_t nr = cnt < L.rcap ? cnt : L.rcap;
+            bool walk_ok = L.nwalk >= nr;
+            // batched: the loads of a batch are independent (no early exit inside it)
+            for (uint32_t i0 = 0; i0 < cnt && bad == 0xFFFFFFFFu; i0 += 8) {
+              uint32_t ofs[8], wr[8];
+#pragma unroll
+              for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t i = i0 + j;
+                ofs[j] = i < cnt ? off_at(i) : 0u;
+                wr[j] = (walk_ok && i < nr) ? __builtin_nontemporal_load(&grows[i].row_off) : 0u;
+              }
+#pragma unroll
+              for (uint32_t j = 0; j < 8; j++) {
+                const uint32_t i = i0 + j;
+                if (i < cnt && bad == 0xFFFFFFFFu) {
+                  if (ofs[j] > osi16) bad = i;
+                  else if (i < nr && wr[j] != ofs[j]) walk_ok = false;
+                }
+              }
+            }
+            if (bad != 0xFFFFFFFFu) {
+              m.status = SLATE_E_BLOCK_OFFSET_BOUNDS;
+              m.aux = uint16_t(bad);
+              m.detail = int32_t(off_at(bad));
+            } else {
+              m.data_len = uint32_t(osi);
+              m.n_rows = uint16_t(cnt);
+              if (cnt == 0) {
+                m.status = SLATE_E_BLOCK_NO_OFFSETS;
+              } else {
+                const uint32_t off0 = off_at(0);
+                if (uint64_t(osi) - off0 < 2) {
+                  m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
+                } else {
+                  const uint16_t kl = uint16_t(out_be16(gout + off0));
+                  const uint16_t lo = uint16_t(off0 + 2), hi = uint16_t(off0 + 2 + kl);
+                  if (lo > hi || hi > dn) {
+                    m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
+                  } else {
+                    m.aux = kl;
+                    if (cnt > L.rcap) m.flags |= SLATE_BLKF_ROWS_TRUNCATED;
+                    // walked rows are exact when they start where the offsets say and
+                    // the last one ends inside Data; prefixes are checked against row 0
+                    if (walk_ok) {
+                      uint32_t end_last = 0;
+                      if (L.nwalk > nr) {
+                        if (nr >= L.rcap) walk_ok = false;  // the next start was not recorded
+                        else end_last = __builtin_nontemporal_load(&grows[nr].row_off);
+                      } else {
+                        if (L.rphase == 3) walk_ok = false;
+                        end_last = L.R;
+                      }
+                      if (walk_ok && end_last > uint32_t(osi)) walk_ok = false;
+                    }
+                    if (walk_ok) {
+                      // a row failing the prefix check keeps only its key lengths (row.go:203-206)
+                      const uint32_t y0 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(grows) + 1);
+                      const uint32_t fk0 = y0 >> 16;
+                      const bool fk_nil = (y0 & 0xffff) != 0;  // row 0 itself fails
+                      for (uint32_t i = 0; i < nr; i++) {
+                        const uint32_t* rw = reinterpret_cast<const uint32_t*>(grows + i);
+                        const uint32_t y = __builtin_nontemporal_load(rw + 1);
+                        const uint32_t pl = y & 0xffff;
+                        if (i == 0 ? fk_nil : (fk_nil ? pl != 0 : pl > fk0)) {
+                          const uint32_t off = __builtin_nontemporal_load(rw);
+                          reinterpret_cast<v4u*>(grows)[i] =
+                              pack_row(off, pl, y >> 16, 0, 0, 0, uint32_t(SLATE_E_ROW_PREFIX));
+                        }
+                      }
+                    } else {
+                      int fk = -1;
+                      for (uint32_t i = 0; i < nr; i++) {
+                        uint32_t sl;
+                        const v4u r = row_from_hbm(gout, uint32_t(osi), off_at(i), fk, &sl);
+                        if (i == 0 && (r.w >> 16) == SLATE_OK) fk = int(sl);
+                        reinterpret_cast<v4u*>(grows)[i] = r;
+                      }
+                    }
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+      a.meta[b] = m;
+    }
+    if ((a.debug & 512) && lane == 0 && round0 + 1 < a.n) {
+      // profiling only: loop iterations and cycles of this round, in meta.detail of its first two blocks
+      a.meta[round0].detail = int32_t(iters);
+      a.meta[round0 + 1].detail = int32_t(round_cycles);
+    }
+  }
+}
+
+size_t lpb2_lds_bytes() {
+  return kTabBytes + 4 * kConstWords + size_t(kLpb2Threads) * (kOutStride + kInStride) + 16;
+}
+
+hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {
+  if (a.n == 0) return hipGetLastError();
+  const size_t lds = lpb2_lds_bytes();
+  const uint32_t waves_needed = (a.n + 63) / 64;
+  uint32_t grid = (waves_needed + kLpb2Threads / 64 - 1) / (kLpb2Threads / 64);
+  grid = min(grid, uint32_t(num_cus) * uint32_t(163840 / lds));
+  // one workgroup takes (nearly) the whole 160 KiB LDS of a CU
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_lpb2_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  decode_lpb2_kernel<<<grid, kLpb2Threads, lds, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace slate

@@ -16,6 +16,9 @@ constexpr uint32_t kLargeOutCap = 90112;
 // LDS per lane + 4 KiB CRC tables -> 5 workgroups (waves) per CU
 constexpr int kLpbThreads = 64;
 constexpr uint32_t kLpbWgPerCu = 5;
+// lane-per-block Snappy decode v2 (decode_lpb2.hip): 240 B of LDS per lane + 4.1 KiB of
+// CRC tables per workgroup -> one 10-wave workgroup per CU
+constexpr int kLpb2Threads = 640;
 
 struct DecodeArgs {
   int codec;
@@ -46,6 +49,7 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb(hipStream_t st, const DecodeArgs& a, int num_cus);
+hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
 // Validates that the code object loads on the current device.
 hipError_t decode_kernels_available();
 

@@ -1,5 +1,7 @@
 """Profiling aid: times the decode kernel with parts switched off
-(SLATE_DEBUG_MODE bits: 1 skip CRC, 2 skip Snappy, 4 skip rows, 8 skip write-back),
+(SLATE_DEBUG_MODE bits: wave-per-block kernel 1 skip CRC, 2 skip Snappy, 4 skip rows, 8 skip
+write-back, 16 use it for Snappy; lane-per-block kernel 32 v1 kernel, 64 skip CRC, 128 skip rows,
+256 far copies from the ring, 512 record per-round iterations/cycles),
 interleaved rounds in one process.  Results are wrong by design; timing only."""
 import json
 import os
@@ -48,9 +50,22 @@ def main():
                 if rnd:
                     res[m].append(a.elapsed_time(b))
     os.environ.pop("SLATE_DEBUG_MODE", None)
+    stats = None
+    if any(m & 512 for m in modes):  # per-round loop iterations and cycles (LPB kernel, last 512-mode run)
+        m512 = [m for m in modes if m & 512][-1]
+        os.environ["SLATE_DEBUG_MODE"] = str(m512)
+        ctx.decode_device(codec, d_in.data_ptr(), d_off.data_ptr(), n, d_out.data_ptr(), d_oo.data_ptr(),
+                          d_meta.data_ptr(), d_rows.data_ptr(), d_rb.data_ptr())
+        s.synchronize()
+        os.environ.pop("SLATE_DEBUG_MODE", None)
+        meta = np.frombuffer(d_meta.cpu().numpy().tobytes(), dtype=sc.META_DTYPE)
+        it = meta["detail"][0::64].astype(np.float64)
+        cyc = meta["detail"][1::64].astype(np.uint32).astype(np.float64)
+        stats = {"mode": m512, "iters_median": float(np.median(it)), "iters_max": float(it.max()),
+                 "cycles_median": float(np.median(cyc)), "cycles_per_iter": float(np.median(cyc / np.maximum(it, 1)))}
     out = {str(m): {"ms_median": float(np.median(v)), "ms_min": float(np.min(v)),
                     "GiBps": dec_bytes / (np.median(v) * 1e-3) / 2**30} for m, v in res.items()}
-    print(json.dumps({"blocks": n, "decoded_bytes": dec_bytes, "modes": out}, indent=1))
+    print(json.dumps({"blocks": n, "decoded_bytes": dec_bytes, "modes": out, "round_stats": stats}, indent=1))
 
 
 if __name__ == "__main__":

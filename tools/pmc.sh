@@ -12,8 +12,9 @@ timeout -k 10 180 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" \
-           "WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_WAIT_INST_LDS"; do
+           "WRITE_SIZE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH SQ_WAIT_INST_LDS" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $grp -f csv -d "$OUT/pmc$i" -o run -- python3 tools/ablate.py $ARGS > "$OUT/pmc$i.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $grp -f csv -d "$OUT/pmc$i" -o run -- python3 tools/ablate.py $ARGS > "$OUT/pmc$i.log" 2>&1 || echo "pass $i failed"
 done
 echo pmc done
