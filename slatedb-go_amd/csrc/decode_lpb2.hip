@@ -182,6 +182,8 @@ struct Lane {
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
   uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
+  int32_t fk;    // first key length for the prefix check (row.go:203-206), -1 before row 0 decodes
+  uint32_t pl0;  // row 0's prefix-length field: block.go's FirstKey length when offsets[0] == 0
 };
 
 struct Rsrc {
@@ -234,14 +236,20 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   const uint32_t flags = p1 ? fl1 : L.rflags;
   const uint32_t ro = p1 ? ro1 : L.ro;
   const uint32_t rlen = (p1 && tomb) ? ro1 : ro + 4;
-  row = pack_row(L.R, L.rpl, L.rsl, vl, flags & 7, rlen - 4 - L.rsl, SLATE_OK);
+  // row.go:203-206: a prefix longer than the block's first key fails the row, which then
+  // keeps only its key lengths; row 0 is decoded against an empty first key
+  const bool pfail = L.rpl > uint32_t(max(L.fk, 0));
+  row = pfail ? pack_row(L.R, L.rpl, L.rsl, 0, 0, 0, uint32_t(SLATE_E_ROW_PREFIX))
+              : pack_row(L.R, L.rpl, L.rsl, vl, flags & 7, rlen - 4 - L.rsl, SLATE_OK);
   ridx = L.nwalk;
+  L.fk = (done && L.nwalk == 0 && !pfail) ? int32_t(L.rsl) : L.fk;
   const bool emit = done && L.nwalk < L.rcap;
   const uint64_t next = uint64_t(L.R) + rlen + vl;
   // state transitions
   const bool to1 = wa && !lost && p0;
   const bool to2 = wa && !lost && p1 && !done1;
   L.rpl = to1 ? pl0 : L.rpl;
+  L.pl0 = (to1 && L.R == 0) ? pl0 : L.pl0;
   L.rsl = to1 ? sl0 : L.rsl;
   L.rflags = (wa && p1) ? fl1 : L.rflags;
   L.ro = (wa && p1) ? ro1 : L.ro;
@@ -259,20 +267,22 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
 }
 
 // One pipeline step (slot `bit`): consume what the loads of four steps ago brought
-// (input chunk P, far-copy source Q), parse / copy, then issue this step's four
-// memory instructions.  Straight-line code: every lane executes every instruction
+// (input chunk P, far-copy source Q), parse / copy, then issue this step's two loads.
+// Stores are batched at the end of each four-step iteration (flush_iteration): a load's
+// vmcnt wait covers every older memory instruction, so stores issued between loads would
+// put their write acknowledgements on the critical path.  Straight-line code: every lane executes every instruction
 // and conditions select values or junk addresses, because in lockstep some lane
 // always needs each part.
 template <bool kCrcSlot>
 __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint32_t bit, bool act, uint8_t* ring,
                                           uint8_t* in, uint8_t* junk, const uint32_t* tab, const Rsrc& R,
-                                          uint32_t dbg) {
+                                          uint32_t dbg, v4u& prow, uint32_t& prow_off) {
   // ---- commit the input chunk loaded four steps ago
   {
     const bool cm = (L.pend & bit) != 0;
     const uint32_t k = L.c_commit;
-    lds_wr16(cm ? in + (k & (kNS - 1)) * 16 : junk, P);
-    lds_wr16((cm && (k & (kNS - 1)) == 0) ? in + kIR : junk, P);
+    if (cm) lds_wr16(in + (k & (kNS - 1)) * 16, P);
+    if (cm && (k & (kNS - 1)) == 0) lds_wr16(in + kIR, P);
     L.c_commit += cm ? 1u : 0u;
     L.pend &= cm ? ~bit : ~0u;
   }
@@ -326,14 +336,15 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint
     uint32_t k = min(L.rem, 16u);
     k = L.lit ? min(k, uint32_t(max(avail - int32_t(L.src), 0))) : (L.far ? (L.fready ? k : 0u) : min(k, L.eff));
     k = cp ? k : 0u;
-    const v4u vl = lds_rd16(L.lit ? in + ((L.sh + L.src) & (kIR - 1)) : ring + (L.src & (kOR - 1)));
+    const v4u zero4 = {0, 0, 0, 0};
+    const v4u vl = (dbg & 4096) ? zero4 : lds_rd16(L.lit ? in + ((L.sh + L.src) & (kIR - 1)) : ring + (L.src & (kOR - 1)));
     const v4u v = L.far ? FD : vl;
     // bytes at [d, d+16) are not yet output: writing them when k == 0 is harmless
     const uint32_t x = L.d & (kOR - 1);
     lds_wr16(ring + x, v);
     // mirror upkeep: ring[0..16) is duplicated at ring[128..144); a write crossing
     // the end also lands at the start (pads absorb the overhang on both sides)
-    lds_wr16(x < 16 ? ring + x + kOR : (x > kOR - 16 ? ring + x - kOR : junk), v);
+    if (x < 16 || x > kOR - 16) lds_wr16(x < 16 ? ring + x + kOR : ring + x - kOR, v);
     L.d += k;
     L.rem -= k;
     const bool step_cp = k != 0 && !L.lit && !L.far;
@@ -342,7 +353,7 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint
     L.eff = eff2;
     L.fready = (L.far && k) ? 0u : L.fready;
   }
-  // ---- the four memory instructions of this step (always issued)
+  // ---- the two loads of this step (always issued)
   {
     // the ring keeps every chunk from the oldest byte still to be read or CRC'd
     const uint32_t lo_pos = L.dd ? L.clen : ((L.rem && L.lit) ? L.src : L.s);
@@ -354,17 +365,41 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint
     const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
     Q = bload<16>(R.out, wantf ? L.out_rel + L.src : kOOB);
     L.fpend = wantf ? bit : L.fpend;
-    const bool flush = act && (L.d >> 4) > L.fl;
-    const v4u o = *reinterpret_cast<const v4u*>(ring + ((L.fl * 16) & (kOR - 1)));
-    bstore(R.out, flush ? L.out_rel + 16 * L.fl : kOOB, o);
-    L.fl += flush ? 1u : 0u;
     if (!kCrcSlot) {  // the row walker runs in the two steps without a CRC chunk
       v4u row;
       uint32_t ridx;
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
-      bstore(R.rows, have_row ? L.rows_rel + 16 * ridx : kOOB, row);
+      prow = row;
+      prow_off = have_row ? L.rows_rel + 16 * ridx : kOOB;
     }
   }
+}
+
+// End of a four-step iteration: every completed aligned 16-byte output chunk (at most four:
+// a step adds at most 16 bytes; the ring keeps them, since unflushed bytes stay within 79 of
+// d and the ring holds 112) and the rows the walker finished, as always-issued stores.
+// The chunks are written transposed: in store j, lanes 4i..4i+3 write chunks 0..3 of the
+// block of lane 16j+i, so every store instruction writes 16 runs of 64 contiguous bytes
+// instead of 64 scattered 16-byte pieces (tools/scatter_probe.hip: ~3.5x cheaper).
+__device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
+                                                uint32_t dbg, const v4u& row_a, uint32_t off_a, const v4u& row_b,
+                                                uint32_t off_b) {
+  const uint32_t done = act ? (L.d >> 4) - L.fl : 0u;
+  const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
+  const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+    const uint32_t info_o = __shfl(info, int(o), 64);
+    const uint32_t base_o = __shfl(base, int(o), 64);
+    const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride + 16;
+    const v4u v = *reinterpret_cast<const v4u*>(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)));
+    bstore(R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, v);
+  }
+  L.fl += done;
+  bstore(R.rows, off_a, row_a);
+  bstore(R.rows, off_b, row_b);
 }
 
 }  // namespace
@@ -422,6 +457,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     L.rphase = 0;
     L.rneed = 4;
     L.rsl = L.rpl = L.rflags = L.ro = L.nwalk = 0;
+    L.fk = -1;
+    L.pl0 = 0xFFFFFFFFu;
     if (have) {
       const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
       if (len < (a.raw ? 4u : 6u)) {
@@ -492,10 +529,13 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
                     iters < budget)) {
       const bool act = have && !(L.dd && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                        iters < budget;
-      lane_step<true>(L, P0, Q0, FD, 1u, act, ring, in, junk, tab, R, a.debug);
-      lane_step<false>(L, P1, Q1, FD, 2u, act, ring, in, junk, tab, R, a.debug);
-      lane_step<true>(L, P2, Q2, FD, 4u, act, ring, in, junk, tab, R, a.debug);
-      lane_step<false>(L, P3, Q3, FD, 8u, act, ring, in, junk, tab, R, a.debug);
+      v4u row_a, row_b;
+      uint32_t off_a = kOOB, off_b = kOOB;
+      lane_step<true>(L, P0, Q0, FD, 1u, act, ring, in, junk, tab, R, a.debug, row_a, off_a);
+      lane_step<false>(L, P1, Q1, FD, 2u, act, ring, in, junk, tab, R, a.debug, row_a, off_a);
+      lane_step<true>(L, P2, Q2, FD, 4u, act, ring, in, junk, tab, R, a.debug, row_b, off_b);
+      lane_step<false>(L, P3, Q3, FD, 8u, act, ring, in, junk, tab, R, a.debug, row_b, off_b);
+      flush_iteration(L, act, outs, lane, R, a.debug, row_a, off_a, row_b, off_b);
       iters++;
     }
     const uint32_t round_cycles = (a.debug & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
@@ -506,9 +546,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       a.meta[b] = m;
       have = false;
     }
+    uint8_t* gout = out_base + L.out_rel;
+    slate_row* grows = reinterpret_cast<slate_row*>(reinterpret_cast<uint8_t*>(rows_base) + L.rows_rel);
+    // rows stage: 0 = no rows to produce, 1 = walked rows to verify, 2 = re-derive from HBM
+    uint32_t rows_stage = 0, nr = 0, osi_u = 0;
     if (have) {
-      uint8_t* gout = out_base + L.out_rel;
-      slate_row* grows = reinterpret_cast<slate_row*>(reinterpret_cast<uint8_t*>(rows_base) + L.rows_rel);
       const uint32_t stored = __builtin_bswap32(lds_rd4(in + ((L.sh + L.clen) & (kIR - 1))));
       // the register absorbed t zero bytes after the message: compare against stored * x^(8t)
       const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
@@ -553,24 +595,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
             };
             const uint16_t osi16 = uint16_t(osi);
             uint32_t bad = 0xFFFFFFFFu;
-            const uint32_t nr = cnt < L.rcap ? cnt : L.rcap;
-            bool walk_ok = L.nwalk >= nr;
-            // batched: the loads of a batch are independent (no early exit inside it)
-            for (uint32_t i0 = 0; i0 < cnt && bad == 0xFFFFFFFFu; i0 += 8) {
-              uint32_t ofs[8], wr[8];
-#pragma unroll
-              for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t i = i0 + j;
-                ofs[j] = i < cnt ? off_at(i) : 0u;
-                wr[j] = (walk_ok && i < nr) ? __builtin_nontemporal_load(&grows[i].row_off) : 0u;
-              }
-#pragma unroll
-              for (uint32_t j = 0; j < 8; j++) {
-                const uint32_t i = i0 + j;
-                if (i < cnt && bad == 0xFFFFFFFFu) {
-                  if (ofs[j] > osi16) bad = i;
-                  else if (i < nr && wr[j] != ofs[j]) walk_ok = false;
-                }
+            for (uint32_t i = 0; i < cnt; i++) {
+              if (off_at(i) > osi16) {
+                bad = i;
+                break;
               }
             }
             if (bad != 0xFFFFFFFFu) {
@@ -587,50 +615,25 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
                 if (uint64_t(osi) - off0 < 2) {
                   m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
                 } else {
-                  const uint16_t kl = uint16_t(out_be16(gout + off0));
+                  // FirstKey quirk (block.go:130-131): the BE16 at Data[off0]; the walker read
+                  // it already when off0 is the first row's start
+                  const uint16_t kl = uint16_t((off0 == 0 && L.pl0 != 0xFFFFFFFFu) ? L.pl0 : out_be16(gout + off0));
                   const uint16_t lo = uint16_t(off0 + 2), hi = uint16_t(off0 + 2 + kl);
                   if (lo > hi || hi > dn) {
                     m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
                   } else {
                     m.aux = kl;
                     if (cnt > L.rcap) m.flags |= SLATE_BLKF_ROWS_TRUNCATED;
-                    // walked rows are exact when they start where the offsets say and
-                    // the last one ends inside Data; prefixes are checked against row 0
+                    nr = cnt < L.rcap ? cnt : L.rcap;
+                    osi_u = uint32_t(osi);
+                    // walked rows are usable when at least nr rows were walked and the walk
+                    // stays inside Data; their starts are then compared with the offsets below
+                    bool walk_ok = L.nwalk >= nr;
                     if (walk_ok) {
-                      uint32_t end_last = 0;
-                      if (L.nwalk > nr) {
-                        if (nr >= L.rcap) walk_ok = false;  // the next start was not recorded
-                        else end_last = __builtin_nontemporal_load(&grows[nr].row_off);
-                      } else {
-                        if (L.rphase == 3) walk_ok = false;
-                        end_last = L.R;
-                      }
-                      if (walk_ok && end_last > uint32_t(osi)) walk_ok = false;
+                      if (L.nwalk > nr) walk_ok = nr < L.rcap;  // row nr's start is in the rows array
+                      else walk_ok = L.rphase != 3 && L.R <= osi_u;
                     }
-                    if (walk_ok) {
-                      // a row failing the prefix check keeps only its key lengths (row.go:203-206)
-                      const uint32_t y0 = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(grows) + 1);
-                      const uint32_t fk0 = y0 >> 16;
-                      const bool fk_nil = (y0 & 0xffff) != 0;  // row 0 itself fails
-                      for (uint32_t i = 0; i < nr; i++) {
-                        const uint32_t* rw = reinterpret_cast<const uint32_t*>(grows + i);
-                        const uint32_t y = __builtin_nontemporal_load(rw + 1);
-                        const uint32_t pl = y & 0xffff;
-                        if (i == 0 ? fk_nil : (fk_nil ? pl != 0 : pl > fk0)) {
-                          const uint32_t off = __builtin_nontemporal_load(rw);
-                          reinterpret_cast<v4u*>(grows)[i] =
-                              pack_row(off, pl, y >> 16, 0, 0, 0, uint32_t(SLATE_E_ROW_PREFIX));
-                        }
-                      }
-                    } else {
-                      int fk = -1;
-                      for (uint32_t i = 0; i < nr; i++) {
-                        uint32_t sl;
-                        const v4u r = row_from_hbm(gout, uint32_t(osi), off_at(i), fk, &sl);
-                        if (i == 0 && (r.w >> 16) == SLATE_OK) fk = int(sl);
-                        reinterpret_cast<v4u*>(grows)[i] = r;
-                      }
-                    }
+                    rows_stage = walk_ok ? 1u : 2u;
                   }
                 }
               }
@@ -638,8 +641,70 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
           }
         }
       }
-      a.meta[b] = m;
     }
+    // ---- wave-cooperative check of the walked row starts against offsets[] (block.go:107-118):
+    // per block, coalesced loads of its offsets and row descriptors; eight blocks per wait
+    {
+      uint64_t todo = __ballot(rows_stage == 1);
+      uint64_t mism = 0;
+      while (todo) {
+        uint32_t js[8], nrs[8], osis[8], outs[8], rws[8], nws[8], Rs[8], ends[8];
+        uint32_t ob[8], wr[8];
+        uint32_t nb = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+          const bool v = todo != 0;
+          const uint32_t j = v ? uint32_t(__builtin_ctzll(todo)) : 0u;
+          todo &= v ? todo - 1 : todo;
+          nb += v ? 1u : 0u;
+          js[q] = j;
+          nrs[q] = v ? __builtin_amdgcn_readlane(nr, j) : 0u;
+          osis[q] = __builtin_amdgcn_readlane(osi_u, j);
+          outs[q] = __builtin_amdgcn_readlane(L.out_rel, j);
+          rws[q] = __builtin_amdgcn_readlane(L.rows_rel, j);
+          nws[q] = __builtin_amdgcn_readlane(L.nwalk, j);
+          Rs[q] = __builtin_amdgcn_readlane(L.R, j);
+          const uint32_t i = lane;
+          const bool in = i < min(nrs[q], 64u);
+          ob[q] = __builtin_amdgcn_raw_buffer_load_b16(R.out, in ? outs[q] + osis[q] + 2 * i : kOOB, 0, 16);
+          wr[q] = __builtin_amdgcn_raw_buffer_load_b32(R.rows, in ? rws[q] + 16 * i : kOOB, 0, 16);
+          ends[q] = __builtin_amdgcn_raw_buffer_load_b32(
+              R.rows, (lane == 0 && nws[q] > nrs[q]) ? rws[q] + 16 * nrs[q] : kOOB, 0, 16);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+          if (q >= nb) break;
+          const uint32_t o = ((ob[q] & 0xff) << 8) | ((ob[q] >> 8) & 0xff);
+          bool bad = lane < min(nrs[q], 64u) && o != wr[q];
+          // blocks with more than 64 rows: the remaining rows, one group of 64 at a time
+          for (uint32_t i0 = 64; i0 < nrs[q]; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool in = i < nrs[q];
+            const uint32_t b2 = __builtin_amdgcn_raw_buffer_load_b16(R.out, in ? outs[q] + osis[q] + 2 * i : kOOB, 0, 16);
+            const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(R.rows, in ? rws[q] + 16 * i : kOOB, 0, 16);
+            bad = bad || (in && (((b2 & 0xff) << 8) | ((b2 >> 8) & 0xff)) != w2);
+          }
+          // the walk must also end inside Data: the start of row nr (recorded when more rows
+          // were walked) or the walker's position
+          const uint32_t end_last = nws[q] > nrs[q] ? __builtin_amdgcn_readfirstlane(ends[q]) : Rs[q];
+          bad = bad || end_last > osis[q];
+          if (__ballot(bad)) mism |= uint64_t(1) << js[q];
+        }
+      }
+      if (rows_stage == 1 && ((mism >> lane) & 1)) rows_stage = 2;
+    }
+    // ---- exact fallback: rows re-derived from HBM with the row.go decoder (corrupt blocks only)
+    if (rows_stage == 2) {
+      int fk = -1;
+      for (uint32_t i = 0; i < nr; i++) {
+        uint32_t sl;
+        const uint32_t off = out_be16(gout + osi_u + 2 * i);
+        const v4u r = row_from_hbm(gout, osi_u, off, fk, &sl);
+        if (i == 0 && (r.w >> 16) == SLATE_OK) fk = int(sl);
+        reinterpret_cast<v4u*>(grows)[i] = r;
+      }
+    }
+    if (have) a.meta[b] = m;
     if ((a.debug & 512) && lane == 0 && round0 + 1 < a.n) {
       // profiling only: loop iterations and cycles of this round, in meta.detail of its first two blocks
       a.meta[round0].detail = int32_t(iters);

@@ -1,7 +1,8 @@
 """Profiling aid: times the decode kernel with parts switched off
 (SLATE_DEBUG_MODE bits: wave-per-block kernel 1 skip CRC, 2 skip Snappy, 4 skip rows, 8 skip
 write-back, 16 use it for Snappy; lane-per-block kernel 32 v1 kernel, 64 skip CRC, 128 skip rows,
-256 far copies from the ring, 512 record per-round iterations/cycles),
+256 far copies from the ring, 512 record per-round iterations/cycles, 1024 drop output stores,
+2048 skip the flush LDS read, 4096 skip the copy-source LDS read),
 interleaved rounds in one process.  Results are wrong by design; timing only."""
 import json
 import os
