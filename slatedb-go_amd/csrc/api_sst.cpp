@@ -136,7 +136,7 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
   SLATE_HIP(hipMemcpyAsync(u, hv, sizeof(hv), hipMemcpyHostToDevice, st));
   DecodeArgs a{SLATE_CODEC_SNAPPY, ctx->d_in.as<uint8_t>(), u, 1, ctx->d_out.as<uint8_t>(), u + 2,
                reinterpret_cast<slate_block_meta*>(u + 6), reinterpret_cast<slate_row*>(u + 8), u + 4,
-               nullptr, reinterpret_cast<uint32_t*>(u + 10), 0};
+               reinterpret_cast<uint32_t*>(u + 11), reinterpret_cast<uint32_t*>(u + 10), 0};
   a.raw = 1;
   SLATE_HIP(launch_decode_lpb2(st, a, ctx->num_cus));
   slate_block_meta m;

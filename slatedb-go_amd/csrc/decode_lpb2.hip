@@ -4,35 +4,39 @@
 // CRC32 verify -> golang/snappy v0.0.4 decode (decode_other.go:19-110) ->
 // offset checks -> row descriptors (row.go:191-261 as block/iterator.go walks).
 //
-// One lane owns one block; the 64 lanes of a wave decode 64 consecutive blocks
-// in lockstep, so one wave instruction advances 64 independent Snappy tag
-// streams (the chain inside one block is serial).
+// One lane owns one block; the 64 lanes of a wave decode 64 consecutive blocks in
+// lockstep, so one wave instruction advances 64 independent Snappy tag streams (the
+// chain inside one block is serial).  A round (64 blocks) runs as iterations of four
+// steps; a step parses a tag if the previous one is used up and moves up to 16 bytes.
 //
-// Memory pipeline.  Every step issues exactly four vector-memory instructions,
-// unconditionally: the next 16-byte input chunk (buffer_load nt), the source of a
-// pending long-distance copy (buffer_load nt), the completed 16-byte output chunk
-// (buffer_store) and the row descriptor finished this step (buffer_store).  A lane
-// with nothing to move gives an out-of-range offset: the hardware drops the access
-// (tools/buf_probe.hip).  The vmcnt bookkeeping is therefore static, and data loaded
-// in one step is consumed four steps later (rotating registers P0..P3, Q0..Q3) while
-// the loads of the three steps in between stay in flight.
-//
-// Per lane, LDS holds
-//   * an input ring of 8 x 16-byte chunks (+16-byte mirror).  The CRC32 is absorbed
-//     as each chunk is committed (slicing-by-4, tables shared by the workgroup).
-//     Bytes of a chunk outside the block are zeroed for the CRC: the register starts
-//     from a per-alignment state that reaches 0xFFFFFFFF after the leading zeros,
-//     and the trailing zeros are folded into the stored value (x^(8t) mod P);
-//   * an output ring of 128 bytes (+mirror and pads).
-// A step parses a tag if the previous one is used up (branch-free), then moves up
-// to 16 bytes with ONE unaligned ds_read_b128 (input ring for literals, output ring
-// for copies with offset <= 112, the far-load register for longer offsets) and ONE
-// unaligned ds_write_b128 (+ a mirror write near the ring ends).  gfx950 executes
-// unaligned b128 DS accesses correctly (tools/lds_probe2.hip).  Copies with offset
-// < 16 double their effective offset after every step (the output is periodic).
-// A row walker reads each row's header fields from the output ring as they are
-// produced; at block end the walk is compared with the block's offset array, and
-// on any mismatch rows are re-derived from HBM with the exact row.go decoder.
+// Memory.  The decode is bound by the latency and the number of memory requests, not by
+// bytes, so every access is shaped for that (tools/scatter_probe.hip measured 16-byte
+// per-lane accesses at 3.5-8x the cost of 64-128-byte runs):
+//   * input: at the start of each iteration, four transposed loads fetch up to four new
+//     16-byte chunks per block: in load j, lanes 4i..4i+3 read four consecutive chunks
+//     (one 64-byte run) of block 16j+i.  They land in the block's LDS input ring (8
+//     chunks + mirror) at the start of the next iteration, so a load has a whole
+//     iteration to arrive, and the ring double-buffers a literal stream at full rate;
+//   * output: completed aligned 16-byte chunks are flushed at the end of each iteration
+//     by four transposed stores (lanes 4i..4i+3 write one block's four chunks);
+//   * all buffer loads/stores are always issued (an out-of-range offset drops a lane:
+//     tools/buf_probe.hip), so vmcnt bookkeeping is static, and stores come after the
+//     loads they could otherwise delay (a vmcnt wait covers every older access);
+//   * a copy with offset > 112 (beyond the 128-byte output ring) and length <= 16 becomes
+//     a "hole": its output bytes are reserved, its source is loaded from the flushed
+//     output, decoding continues, and the bytes are merged into the ring four steps
+//     later.  Flush, walker and ring copies wait for a hole that overlaps them.  Longer
+//     far copies stream 16 bytes per load.
+// CRC32 is absorbed from the input ring in two of the four steps (slicing-by-4 tables
+// shared by the workgroup).  Bytes of a chunk outside the block are zeroed: the register
+// starts from a per-alignment state that reaches 0xFFFFFFFF after the leading zeros, and
+// the trailing zeros are folded into the stored value (x^(8t) mod P).
+// LDS per lane: output ring 128 + mirror + pad (160 B), input ring 128 + mirror (144 B).
+// gfx950 executes unaligned ds_read_b128 / ds_write_b128 (tools/lds_probe2.hip).
+// A row walker reads each row's header from the output ring as it is produced and checks
+// the key prefix inline; at block end a wave-cooperative pass compares the walked row
+// starts with the block's offset array, and mismatches re-derive rows from HBM with the
+// exact row.go decoder.
 #include "common.h"
 #include "kernels.h"
 #include "wave_crc.h"
@@ -47,19 +51,17 @@ namespace {
 
 constexpr uint32_t kOR = 128;          // output ring bytes
 constexpr uint32_t kReach = kOR - 16;  // ring positions still valid behind d
-constexpr uint32_t kNS = 4;            // input ring slots
+constexpr uint32_t kUnflushed = 80;    // d - 16*fl before a step may advance d (see the throttle)
+constexpr uint32_t kNS = 8;            // input ring slots
 constexpr uint32_t kIR = kNS * 16;
-// LDS per lane, 240 bytes: an output-ring record [pad 16][ring 128][mirror 16] (stride 160;
-// lane i's pad doubles as lane i-1's post-pad: both only ever write junk there) and an
-// input-ring record [ring 64][mirror 16] (stride 80) in a second array.
+// output-ring records [pad 16][ring 128][mirror 16] (stride 160; lane i's pad doubles as
+// lane i-1's post-pad: both only ever write junk there), then input-ring records
+// [ring 128][mirror 16] (stride 144)
 constexpr uint32_t kOutStride = 16 + kOR + 16;
 constexpr uint32_t kInStride = kIR + 16;
-constexpr uint32_t kConstWords = 32;                  // crc_init[16] | tail_mul[16]
-constexpr uint32_t kOOB = 0xFFFFFFF0u;                // buffer offset that is always out of range
-#ifndef SLATE_IN_AUX
-#define SLATE_IN_AUX 0
-#endif
-constexpr int kInAux = SLATE_IN_AUX;
+constexpr uint32_t kConstWords = 32;    // crc_init[16] | crc_tail[16]
+constexpr uint32_t kOOB = 0xFFFFFFF0u;  // buffer offset that is always out of range
+constexpr uint32_t kMirrorBit = 1u << 20;  // refill slot tag: the chunk also goes to the ring mirror
 
 // CRC register state that becomes 0xFFFFFFFF after `sh` zero bytes (sh < 16), and x^(8t) mod P.
 struct CrcLeadTail {
@@ -178,7 +180,10 @@ struct Lane {
   uint32_t crc, crc_pos;
   // decode
   uint32_t s, d, rem, src, eff, lit, far, dd, err;
-  uint32_t c_issue, c_commit, pend, fpend, fready, fl;
+  uint32_t c_issue, c_commit, n_req, fpend, fready, fl;
+  // pending hole: a copy with offset > kReach and length <= 16 reserves output [hd, hd+hl)
+  // and decoding goes on; its source arrives four steps later and is merged into the ring
+  uint32_t hpend, hd, hl;
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
   uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
@@ -214,9 +219,10 @@ __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint
 // Row walker, one action per call (row.go:191-261 field order), branch-free.
 // Returns true with `row`/`ridx` set when the action finished a row.
 __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
-  const bool wa = act && L.rphase < 3 && L.d >= L.rneed;
   const uint32_t fp = L.R + 4 + L.rsl + 8;
   const uint32_t rpos = L.rphase == 0 ? L.R : (L.rphase == 1 ? fp : L.R + L.ro);
+  const bool in_hole = L.hpend && rpos < L.hd + L.hl && rpos + 8 > L.hd;
+  const bool wa = act && L.rphase < 3 && L.d >= L.rneed && !in_hole;
   const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
   const v2u q = lds_rd8(ring + (rpos & (kOR - 1)));
   // phase 0: prefix / suffix lengths
@@ -266,46 +272,88 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   return emit;
 }
 
-// One pipeline step (slot `bit`): consume what the loads of four steps ago brought
-// (input chunk P, far-copy source Q), parse / copy, then issue this step's two loads.
-// Stores are batched at the end of each four-step iteration (flush_iteration): a load's
-// vmcnt wait covers every older memory instruction, so stores issued between loads would
-// put their write acknowledgements on the critical path.  Straight-line code: every lane executes every instruction
-// and conditions select values or junk addresses, because in lockstep some lane
-// always needs each part.
-template <bool kCrcSlot>
-__device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint32_t bit, bool act, uint8_t* ring,
-                                          uint8_t* in, uint8_t* junk, const uint32_t* tab, const Rsrc& R,
-                                          uint32_t dbg, v4u& prow, uint32_t& prow_off) {
-  // ---- commit the input chunk loaded four steps ago
-  {
-    const bool cm = (L.pend & bit) != 0;
-    const uint32_t k = L.c_commit;
-    if (cm) lds_wr16(in + (k & (kNS - 1)) * 16, P);
-    if (cm && (k & (kNS - 1)) == 0) lds_wr16(in + kIR, P);
-    L.c_commit += cm ? 1u : 0u;
-    L.pend &= cm ? ~bit : ~0u;
-  }
-  // ---- the far-copy source loaded four steps ago
+// Start of an iteration: (1) the chunks loaded one iteration ago go into their blocks'
+// input rings (the loading lane writes them: transposed layout); (2) every block asks for
+// up to four more chunks (ring room and payload end permitting); (3) four transposed
+// loads fetch them: in load j, lanes 4i..4i+3 read chunks c_issue..c_issue+3 of block 16j+i.
+__device__ __forceinline__ void commit_one(uint8_t* ins, uint32_t slot, const v4u& v) {
+  // slot: LDS offset | kMirrorBit for ring slot 0 (the chunk also goes to the mirror)
+  if (slot != 0xFFFFFFFFu) *reinterpret_cast<v4u*>(ins + (slot & ~kMirrorBit)) = v;
+  if (slot != 0xFFFFFFFFu && (slot & kMirrorBit)) *reinterpret_cast<v4u*>(ins + (slot & ~kMirrorBit) + kIR) = v;
+}
+
+__device__ __forceinline__ void load_one(uint32_t j, uint32_t lane, uint32_t wave_lane0, uint32_t info,
+                                         uint32_t rel, const Rsrc& R, v4u& P, uint32_t& slot) {
+  const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+  const uint32_t info_o = __shfl(info, int(o), 64);
+  const uint32_t rel_o = __shfl(rel, int(o), 64);
+  const uint32_t ci = (info_o >> 3) + c;
+  const bool want = c < (info_o & 7);
+  P = __builtin_amdgcn_raw_buffer_load_b128(R.in, want ? rel_o + 16 * ci : kOOB, 0, 0);
+  slot = want ? ((wave_lane0 + o) * kInStride + (ci & (kNS - 1)) * 16) | ((ci & (kNS - 1)) ? 0u : kMirrorBit)
+              : 0xFFFFFFFFu;
+}
+
+// Start of an iteration, part 2: how many chunks this block asks for (ring room and
+// payload end permitting), then four transposed loads fetch them for the whole wave.
+__device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, uint32_t c_issue, uint32_t last_chunk) {
+  const uint32_t room = lo_chunk + kNS - c_issue;
+  const uint32_t left = last_chunk + 1 - c_issue;
+  return act ? min(min(room, left), 4u) : 0u;
+}
+
+// One step: the far-copy source loaded four steps ago, CRC (two of four steps), parse,
+// copy, the far-copy / hole load, and the row walker (the other two steps).
+template <bool kWalkSlot>
+__device__ __forceinline__ void lane_step(Lane& L, v4u& Q, v4u& FD, uint32_t bit, bool act, uint8_t* ring,
+                                          uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg,
+                                          v4u& prow, uint32_t& prow_off) {
+#ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
+  dbg = SLATE_FORCE_DBG;
+#endif
+  // ---- the far-copy source loaded four steps ago: fills the pending hole (read-modify-write
+  // of the 16 ring bytes at hd: the bytes after the hole were decoded meanwhile), or feeds
+  // a long far copy through FD
   {
     const bool fc = (L.fpend & bit) != 0;
-    FD = fc ? Q : FD;
-    L.fready = fc ? 1u : L.fready;
+    const bool fill = fc && L.hpend;
+    const uint32_t x = L.hd & (kOR - 1);
+    if (__builtin_amdgcn_ballot_w64(fill)) {
+      const v4u cur = lds_rd16(ring + x);
+      v4u m;
+      m.x = keep_mask(0, int32_t(L.hl), 0);
+      m.y = keep_mask(0, int32_t(L.hl), 1);
+      m.z = keep_mask(0, int32_t(L.hl), 2);
+      m.w = keep_mask(0, int32_t(L.hl), 3);
+      const v4u v = (Q & m) | (cur & ~m);
+      if (fill) {
+        lds_wr16(ring + x, v);
+        if (x < 16 || x > kOR - 16) lds_wr16(x < 16 ? ring + x + kOR : ring + x - kOR, v);
+      }
+    }
+    FD = (fc && !fill) ? Q : FD;
+    L.fready = (fc && !fill) ? 1u : L.fready;
+    L.hpend = fill ? 0u : L.hpend;
     L.fpend = fc ? 0u : L.fpend;
   }
-  // ---- CRC32 of one committed chunk (two of the four steps)
-  if (kCrcSlot) {
+  // ---- CRC32 of one committed chunk (the two steps without the walker)
+  if (!kWalkSlot) {
     const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
     if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
     else crc_chunk(L, in, tab, go);
   }
   const int32_t avail = int32_t(16 * L.c_commit) - int32_t(L.sh);  // committed payload bytes [0, avail)
   const uint32_t sn = L.clen;
+  bool hole_new = false;
+  uint32_t hole_src = 0;
   // ---- parse the next tag (golang/snappy decode_other.go:19-110)
   {
     const bool need = act && !L.dd && L.rem == 0;
     const bool fin = need && L.s >= sn;
-    const bool can = need && L.s < sn && avail >= int32_t(min(L.s + 5, sn));
+    // throttle (a hole delays the flush): after any step d - 16*fl <= 96, so the ring keeps
+    // every unflushed byte and every far source (offset > 112) is already flushed
+    const bool room_out = L.d - 16 * L.fl <= kUnflushed;
+    const bool can = need && L.s < sn && avail >= int32_t(min(L.s + 5, sn)) && room_out;
     const v2u w = lds_rd8(in + ((L.sh + L.s) & (kIR - 1)));
     const uint32_t c = w.x & 0xff, t = c & 3;
     const uint32_t b14 = (w.x >> 8) | (w.y << 24);  // bytes s+1 .. s+4
@@ -327,17 +375,29 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint
     L.rem = ok ? (t == 0 ? uint32_t(lit_len) : cp_len) : L.rem;
     L.src = ok ? (t == 0 ? s1 : L.d - cp_off) : L.src;
     L.eff = ok ? (t == 0 ? 16u : cp_off) : L.eff;
-    L.far = ok ? uint32_t(t != 0 && cp_off > kReach && !(dbg & 256)) : L.far;
+    const bool far = t != 0 && cp_off > kReach && !(dbg & 256);
+    L.far = ok ? uint32_t(far) : L.far;
     L.s = ok ? (t == 0 ? s1 + uint32_t(lit_len) : s1) : L.s;
+    // a short far copy becomes a hole: reserve its bytes, load its source, go on decoding
+    hole_new = ok && far && cp_len <= 16 && !L.hpend && !L.fpend && !(dbg & 8192);
+    hole_src = L.d - cp_off;
+    L.hd = hole_new ? L.d : L.hd;
+    L.hl = hole_new ? cp_len : L.hl;
+    L.hpend = hole_new ? 1u : L.hpend;
+    L.d += hole_new ? cp_len : 0u;
+    L.rem = hole_new ? 0u : L.rem;
+    L.far = hole_new ? 0u : L.far;
   }
   // ---- move up to 16 bytes of the current tag into the output ring
   {
     const bool cp = act && !L.dd && L.rem != 0;
     uint32_t k = min(L.rem, 16u);
     k = L.lit ? min(k, uint32_t(max(avail - int32_t(L.src), 0))) : (L.far ? (L.fready ? k : 0u) : min(k, L.eff));
-    k = cp ? k : 0u;
-    const v4u zero4 = {0, 0, 0, 0};
-    const v4u vl = (dbg & 4096) ? zero4 : lds_rd16(L.lit ? in + ((L.sh + L.src) & (kIR - 1)) : ring + (L.src & (kOR - 1)));
+    // a ring copy stops short of the pending hole's bytes
+    const bool near = !L.lit && !L.far;
+    if (near && L.hpend && L.src < L.hd + L.hl && L.src + k > L.hd) k = L.src < L.hd ? L.hd - L.src : 0u;
+    k = (cp && L.d - 16 * L.fl <= kUnflushed) ? k : 0u;
+    const v4u vl = lds_rd16(L.lit ? in + ((L.sh + L.src) & (kIR - 1)) : ring + (L.src & (kOR - 1)));
     const v4u v = L.far ? FD : vl;
     // bytes at [d, d+16) are not yet output: writing them when k == 0 is harmless
     const uint32_t x = L.d & (kOR - 1);
@@ -347,25 +407,20 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint
     if (x < 16 || x > kOR - 16) lds_wr16(x < 16 ? ring + x + kOR : ring + x - kOR, v);
     L.d += k;
     L.rem -= k;
-    const bool step_cp = k != 0 && !L.lit && !L.far;
-    const uint32_t eff2 = (step_cp && L.eff < 16) ? 2 * L.eff : L.eff;  // periodic output: the pattern doubles
+    // periodic output: once a whole period was copied, the pattern can be read twice as far back
+    const bool step_cp = k != 0 && k == L.eff && near;
+    const uint32_t eff2 = (step_cp && L.eff < 16) ? 2 * L.eff : L.eff;
     L.src = (L.lit || L.far) ? L.src + k : L.d - eff2;
     L.eff = eff2;
     L.fready = (L.far && k) ? 0u : L.fready;
   }
-  // ---- the two loads of this step (always issued)
+  // ---- the far-copy / hole source load of this step (always issued, sc1: L1 bypass)
   {
-    // the ring keeps every chunk from the oldest byte still to be read or CRC'd
-    const uint32_t lo_pos = L.dd ? L.clen : ((L.rem && L.lit) ? L.src : L.s);
-    const uint32_t lo_chunk = min((L.sh + lo_pos) >> 4, L.crc_pos);
-    const bool room = act && L.c_issue <= L.last_chunk && L.c_issue < lo_chunk + kNS;
-    P = bload<kInAux>(R.in, room ? L.in_rel + 16 * L.c_issue : kOOB);
-    L.pend |= room ? bit : 0u;
-    L.c_issue += room ? 1u : 0u;
     const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
-    Q = bload<16>(R.out, wantf ? L.out_rel + L.src : kOOB);
-    L.fpend = wantf ? bit : L.fpend;
-    if (!kCrcSlot) {  // the row walker runs in the two steps without a CRC chunk
+    Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : kOOB),
+                                              0, 16);
+    L.fpend = (wantf || hole_new) ? bit : L.fpend;
+    if (kWalkSlot) {
       v4u row;
       uint32_t ridx;
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
@@ -384,7 +439,7 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& P, v4u& Q, v4u& FD, uint
 __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
                                                 uint32_t dbg, const v4u& row_a, uint32_t off_a, const v4u& row_b,
                                                 uint32_t off_b) {
-  const uint32_t done = act ? (L.d >> 4) - L.fl : 0u;
+  const uint32_t done = act ? min(L.d >> 4, L.hpend ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
   const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
   const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
   const uint32_t wave_lane0 = threadIdx.x - lane;
@@ -397,7 +452,7 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
     const v4u v = *reinterpret_cast<const v4u*>(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)));
     bstore(R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, v);
   }
-  L.fl += done;
+  L.fl += min(done, 4u);
   bstore(R.rows, off_a, row_a);
   bstore(R.rows, off_b, row_b);
 }
@@ -417,12 +472,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
   const uint32_t* crc_init = tab + 1024;
   const uint32_t* crc_tail = tab + 1024 + 16;
   uint8_t* outs = smem + kTabBytes + 4 * kConstWords;
+  uint8_t* ins = outs + kLpb2Threads * kOutStride + 16;
   uint8_t* ring = outs + threadIdx.x * kOutStride + 16;
-  uint8_t* junk = ring - 16;  // this lane's pad: write-only
-  uint8_t* in = outs + kLpb2Threads * kOutStride + 16 + threadIdx.x * kInStride;
-  const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
+  uint8_t* in = ins + threadIdx.x * kInStride;
   // wave-uniform by construction: the buffer resources derived from it must live in SGPRs
-  // (a VGPR resource turns every buffer op into a waterfall loop)
+  const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
   const uint32_t wave_g = blockIdx.x * (kLpb2Threads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
 
@@ -440,7 +494,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     R.rows = make_rsrc(rows_base, 16 * (a.row_base[rend] - a.row_base[round0]));
 
     Lane L;
-    v4u P0 = {0, 0, 0, 0}, P1 = P0, P2 = P0, P3 = P0, Q0 = P0, Q1 = P0, Q2 = P0, Q3 = P0, FD = P0;
+    const v4u zero = {0, 0, 0, 0};
+    v4u Q0 = zero, Q1 = zero, Q2 = zero, Q3 = zero, FD = zero;
+    v4u P0 = zero, P1 = zero, P2 = zero, P3 = zero;
+    uint32_t S0 = 0xFFFFFFFFu, S1 = 0xFFFFFFFFu, S2 = 0xFFFFFFFFu, S3 = 0xFFFFFFFFu;
     const uint32_t b = round0 + lane;
     slate_block_meta m{};
     bool have = b < a.n;
@@ -452,7 +509,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = 0;
     L.eff = 16;
     L.dd = 1;
-    L.c_issue = L.c_commit = L.pend = L.fpend = L.fready = L.fl = 0;
+    L.c_issue = L.c_commit = L.n_req = L.fpend = L.fready = L.fl = 0;
+    L.hpend = L.hd = L.hl = 0;
     L.R = 0;
     L.rphase = 0;
     L.rneed = 4;
@@ -470,7 +528,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         L.sh = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
         L.in_rel = uint32_t((gin - L.sh) - in_base);
         L.clen = uint32_t(len - 4);
-        L.last_chunk = uint32_t((L.sh + len - 1) >> 4);
+        L.last_chunk = uint32_t((L.sh + len - 1) >> 4);  // includes the stored CRC
         L.crc_last = L.clen ? int32_t((L.sh + L.clen - 1) >> 4) : -1;
         L.crc = L.clen ? crc_init[L.sh] : 0xFFFFFFFFu;
         L.out_rel = uint32_t(a.out_off[b] - a.out_off[round0]);
@@ -482,8 +540,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     // ---- the block's first two chunks (aligned, inside the block's chunk range), then
     // golang/snappy decodedLen (decode.go:20-31) over the committed ring
     {
-      const v4u c0 = bload<kInAux>(R.in, have ? L.in_rel : kOOB);
-      const v4u c1 = bload<kInAux>(R.in, (have && L.last_chunk >= 1) ? L.in_rel + 16 : kOOB);
+      const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(R.in, have ? L.in_rel : kOOB, 0, 0);
+      const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && L.last_chunk >= 1) ? L.in_rel + 16 : kOOB, 0, 0);
       if (have) {
         *reinterpret_cast<v4u*>(in) = c0;
         *reinterpret_cast<v4u*>(in + kIR) = c0;
@@ -517,24 +575,45 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       }
     }
 
-    // ---------------- streaming decode, 64 blocks in lockstep, 4-deep memory pipeline
+    // ---------------- streaming decode, 64 blocks in lockstep
     uint32_t iters = 0;
     const uint64_t t_round = (a.debug & 512) ? __builtin_amdgcn_s_memtime() : 0;
-    // a lane is done when its decode is finished and every chunk is committed and in the CRC.
-    // Every step consumes input, produces output or waits on a load issued at most four steps
-    // earlier, so a block needs far fewer than `budget` iterations; the budget only guarantees
-    // that the loop ends (an exhausted lane reports SLATE_E_HIP, never a wrong result).
+    // a lane is done when its decode is finished, no hole is pending, and every chunk
+    // is committed and in the CRC.  Every step consumes input, produces output or waits
+    // on a load issued at most one iteration earlier, so a block needs far fewer than
+    // `budget` iterations; the budget only guarantees that the loop ends (an exhausted
+    // lane reports SLATE_E_HIP, never a wrong result).
     const uint32_t budget = have ? (L.clen + L.dn) / 2 + 1024 : 0u;
-    while (__ballot(have && !(L.dd && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
+    while (__ballot(have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                     iters < budget)) {
-      const bool act = have && !(L.dd && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
+      const bool act = have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                        iters < budget;
+      {
+        commit_one(ins, S0, P0);
+        commit_one(ins, S1, P1);
+        commit_one(ins, S2, P2);
+        commit_one(ins, S3, P3);
+        L.c_commit += L.n_req;
+        // the ring keeps every chunk from the oldest byte still to be read or CRC'd
+        const uint32_t lo_pos = L.dd ? L.clen : ((L.rem && L.lit) ? L.src : L.s);
+        const uint32_t lo_chunk = min((L.sh + lo_pos) >> 4, L.crc_pos);
+        const uint32_t n = refill_count(act, lo_chunk, L.c_issue, L.last_chunk);
+        const uint32_t info = (L.c_issue << 3) | n;
+        const uint32_t wave_lane0 = threadIdx.x - lane;
+        const uint32_t rel = L.in_rel;
+        load_one(0, lane, wave_lane0, info, rel, R, P0, S0);
+        load_one(1, lane, wave_lane0, info, rel, R, P1, S1);
+        load_one(2, lane, wave_lane0, info, rel, R, P2, S2);
+        load_one(3, lane, wave_lane0, info, rel, R, P3, S3);
+        L.c_issue += n;
+        L.n_req = n;
+      }
       v4u row_a, row_b;
       uint32_t off_a = kOOB, off_b = kOOB;
-      lane_step<true>(L, P0, Q0, FD, 1u, act, ring, in, junk, tab, R, a.debug, row_a, off_a);
-      lane_step<false>(L, P1, Q1, FD, 2u, act, ring, in, junk, tab, R, a.debug, row_a, off_a);
-      lane_step<true>(L, P2, Q2, FD, 4u, act, ring, in, junk, tab, R, a.debug, row_b, off_b);
-      lane_step<false>(L, P3, Q3, FD, 8u, act, ring, in, junk, tab, R, a.debug, row_b, off_b);
+      lane_step<false>(L, Q0, FD, 1u, act, ring, in, tab, R, a.debug, row_a, off_a);
+      lane_step<true>(L, Q1, FD, 2u, act, ring, in, tab, R, a.debug, row_a, off_a);
+      lane_step<false>(L, Q2, FD, 4u, act, ring, in, tab, R, a.debug, row_b, off_b);
+      lane_step<true>(L, Q3, FD, 8u, act, ring, in, tab, R, a.debug, row_b, off_b);
       flush_iteration(L, act, outs, lane, R, a.debug, row_a, off_a, row_b, off_b);
       iters++;
     }
@@ -552,7 +631,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     uint32_t rows_stage = 0, nr = 0, osi_u = 0;
     if (have) {
       const uint32_t stored = __builtin_bswap32(lds_rd4(in + ((L.sh + L.clen) & (kIR - 1))));
-      // the register absorbed t zero bytes after the message: compare against stored * x^(8t)
+      // the register absorbed t zero bytes after the payload: compare against stored * x^(8t)
       const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
       const bool crc_ok = gf2_mulmod(~stored, crc_tail[t]) == L.crc;
       const bool snappy_ok = !L.err && L.d == L.dn && L.s == L.clen && L.rem == 0;
@@ -673,7 +752,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         }
 #pragma unroll
         for (uint32_t q = 0; q < 8; q++) {
-          if (q >= nb) break;
+          if (q < nb) {
           const uint32_t o = ((ob[q] & 0xff) << 8) | ((ob[q] >> 8) & 0xff);
           bool bad = lane < min(nrs[q], 64u) && o != wr[q];
           // blocks with more than 64 rows: the remaining rows, one group of 64 at a time
@@ -689,6 +768,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
           const uint32_t end_last = nws[q] > nrs[q] ? __builtin_amdgcn_readfirstlane(ends[q]) : Rs[q];
           bad = bad || end_last > osis[q];
           if (__ballot(bad)) mism |= uint64_t(1) << js[q];
+          }
         }
       }
       if (rows_stage == 1 && ((mism >> lane) & 1)) rows_stage = 2;
@@ -712,6 +792,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     }
   }
 }
+
 
 size_t lpb2_lds_bytes() {
   return kTabBytes + 4 * kConstWords + size_t(kLpb2Threads) * (kOutStride + kInStride) + 16;

@@ -16,9 +16,9 @@ constexpr uint32_t kLargeOutCap = 90112;
 // LDS per lane + 4 KiB CRC tables -> 5 workgroups (waves) per CU
 constexpr int kLpbThreads = 64;
 constexpr uint32_t kLpbWgPerCu = 5;
-// lane-per-block Snappy decode v2 (decode_lpb2.hip): 240 B of LDS per lane + 4.1 KiB of
-// CRC tables per workgroup -> one 10-wave workgroup per CU
-constexpr int kLpb2Threads = 640;
+// lane-per-block Snappy decode v2 (decode_lpb2.hip): 304 B of LDS per lane + 4.1 KiB CRC
+// tables -> one 8-wave workgroup per CU
+constexpr int kLpb2Threads = 512;
 
 struct DecodeArgs {
   int codec;
