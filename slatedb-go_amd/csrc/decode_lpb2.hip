@@ -95,8 +95,11 @@ template <int kAux>
 __device__ __forceinline__ v4u bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAux);
 }
+// Stores are sc1 (write-through): the output is written in 64-byte runs, and default-policy
+// partial-line writes made the XCD L2 fill the rest of each 128-byte line from HBM first
+// (FETCH_SIZE 6.3 -> 4.3 KiB per block, tools/traffic_ablate.sh).
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, v4u v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
 // Resources must be in SGPRs (a VGPR resource turns every buffer op into a waterfall loop):
 // the inputs are wave-uniform, readfirstlane makes that visible to the compiler.
@@ -417,15 +420,15 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, v4u& FD, uint32_t bit
   // ---- the far-copy / hole source load of this step (always issued, sc1: L1 bypass)
   {
     const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
-    Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : kOOB),
-                                              0, 16);
+    const uint32_t qoff = hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : kOOB);
+    Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg & 32768) ? kOOB : qoff, 0, 16);
     L.fpend = (wantf || hole_new) ? bit : L.fpend;
     if (kWalkSlot) {
       v4u row;
       uint32_t ridx;
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
       prow = row;
-      prow_off = have_row ? L.rows_rel + 16 * ridx : kOOB;
+      prow_off = (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB;
     }
   }
 }
@@ -724,7 +727,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     // ---- wave-cooperative check of the walked row starts against offsets[] (block.go:107-118):
     // per block, coalesced loads of its offsets and row descriptors; eight blocks per wait
     {
-      uint64_t todo = __ballot(rows_stage == 1);
+      uint64_t todo = (a.debug & 65536) ? 0 : __ballot(rows_stage == 1);  // 65536: profiling only
       uint64_t mism = 0;
       while (todo) {
         uint32_t js[8], nrs[8], osis[8], outs[8], rws[8], nws[8], Rs[8], ends[8];

@@ -15,7 +15,7 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)  # slatedb-go_amd/
-LIB_PATH = os.path.join(ROOT, "lib", "libslatecodec.so")
+LIB_PATH = os.path.join(ROOT, "lib", os.environ.get("SLATE_LIB_VARIANT", "libslatecodec.so"))  # variant: profiling only
 HEADER = os.path.join(os.path.dirname(ROOT), "include", "slatecodec.h")
 
 NONE, SNAPPY, ZLIB, LZ4, ZSTD = 0, 1, 2, 3, 4

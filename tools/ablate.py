@@ -2,7 +2,8 @@
 (SLATE_DEBUG_MODE bits: wave-per-block kernel 1 skip CRC, 2 skip Snappy, 4 skip rows, 8 skip
 write-back, 16 use it for Snappy; lane-per-block kernel 32 v1 kernel, 64 skip CRC, 128 skip rows,
 256 far copies from the ring, 512 record per-round iterations/cycles, 1024 drop output stores,
-2048 skip the flush LDS read, 4096 skip the copy-source LDS read),
+2048 skip the flush LDS read, 4096 skip the copy-source LDS read, 8192 no holes, 16384 drop row
+stores, 32768 drop far-copy loads, 65536 skip the row verification),
 interleaved rounds in one process.  Results are wrong by design; timing only."""
 import json
 import os
