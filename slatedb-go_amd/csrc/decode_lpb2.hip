@@ -623,7 +623,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     const uint32_t round_cycles = (a.debug & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
 
     // ---------------- finalise the round's blocks (SIMD across lanes)
-    if (have && iters >= budget) {
+    // iters counts the wave's iterations: a lane that finished early is not exhausted
+    if (have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk)) {
       m.status = SLATE_E_HIP;  // step budget exhausted (see above): a kernel defect, reported loudly
       a.meta[b] = m;
       have = false;
