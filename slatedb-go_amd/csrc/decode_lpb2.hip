@@ -45,23 +45,26 @@ namespace slate {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-typedef uint32_t u32_u __attribute__((aligned(1)));
 
 namespace {
 
 constexpr uint32_t kOR = 128;          // output ring bytes
-constexpr uint32_t kReach = kOR - 16;  // ring positions still valid behind d
+// ring positions still valid behind d: a step's store reaches 20 bytes past d's dword
+// (five dwords), i.e. 109 bytes behind d modulo the ring
+constexpr uint32_t kReach = kOR - 20;
 constexpr uint32_t kUnflushed = 80;    // d - 16*fl before a step may advance d (see the throttle)
 constexpr uint32_t kNS = 8;            // input ring slots
 constexpr uint32_t kIR = kNS * 16;
-// output-ring records [pad 16][ring 128][mirror 16] (stride 160; lane i's pad doubles as
-// lane i-1's post-pad: both only ever write junk there), then input-ring records
-// [ring 128][mirror 16] (stride 144)
-constexpr uint32_t kOutStride = 16 + kOR + 16;
-constexpr uint32_t kInStride = kIR + 16;
+// LDS: output rings, then input rings, no mirrors: every access is naturally aligned and
+// wraps per element.  Lane records are 136 bytes apart (34 dwords): blocks of a round
+// progress alike, so lanes touch the same ring positions at the same time, and a stride of
+// 2 mod 32 dwords spreads them over the banks (a 128-byte stride put all 32 lanes of a
+// half-wave on one bank).  Records are therefore 8-byte aligned: 16-byte chunks move as
+// two b64 halves.
+constexpr uint32_t kOutStride = kOR + 8;
+constexpr uint32_t kInStride = kIR + 8;
 constexpr uint32_t kConstWords = 32;    // crc_init[16] | crc_tail[16]
 constexpr uint32_t kOOB = 0xFFFFFFF0u;  // buffer offset that is always out of range
-constexpr uint32_t kMirrorBit = 1u << 20;  // refill slot tag: the chunk also goes to the ring mirror
 
 // CRC register state that becomes 0xFFFFFFFF after `sh` zero bytes (sh < 16), and x^(8t) mod P.
 struct CrcLeadTail {
@@ -78,15 +81,103 @@ struct CrcLeadTail {
 };
 static __constant__ CrcLeadTail g_crc_lt = CrcLeadTail();
 
-// Unaligned LDS b128/b64: gfx950 executes ds_read_b128 / ds_write_b128 / ds_read_b64 at any
-// byte address (tools/lds_probe2.hip).  The natural alignment of v4u/v2u is what makes the
-// compiler emit the single wide instruction instead of ds_read2_b32 pairs, whose behaviour
-// at unaligned addresses is not established.
-__device__ __forceinline__ v4u lds_rd16(const uint8_t* p) { return *reinterpret_cast<const v4u*>(p); }
-__device__ __forceinline__ void lds_wr16(uint8_t* p, v4u v) { *reinterpret_cast<v4u*>(p) = v; }
-__device__ __forceinline__ v2u lds_rd8(const uint8_t* p) { return *reinterpret_cast<const v2u*>(p); }
-__device__ __forceinline__ uint32_t lds_rd4(const uint8_t* p) { return *reinterpret_cast<const u32_u*>(p); }
+// Rings and natural alignment.  gfx950 executes ds_read/ds_write of 8 or 16 bytes at any
+// byte address, but an access that is not naturally aligned is serialised lane by lane:
+// ~64 CU-cycles per wave-instruction against 2-9 aligned, for b32, b64 and b128 alike
+// (tools/lds_cost_probe.hip).  So every ring access here is naturally aligned: byte windows
+// are cut out of aligned 8-byte reads with v_alignbyte, and 16 output bytes at any position
+// are stored as five aligned dwords, the first merged with the bytes already in it (the
+// lane keeps that dword in a register, Lane::T).  Each element wraps on its own, so the
+// rings need no mirror copies.
 __device__ __forceinline__ uint32_t be16_of(uint32_t w) { return ((w & 0xff) << 8) | ((w >> 8) & 0xff); }
+__device__ __forceinline__ v2u rd64(const uint8_t* ring, uint32_t a) {
+  return *reinterpret_cast<const v2u*>(ring + (a & (kOR - 8)));
+}
+// An opaque zero keeps the compiler from fusing two b64 accesses 8 bytes apart into
+// ds_read2_b64 / ds_write2_b64, which cost ~55 CU-cycles per wave-instruction at these
+// addresses (tools/lds_cost_probe.hip) against ~3 for two ds_read_b64.
+__device__ __forceinline__ uint32_t opaque0() {
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+__device__ __forceinline__ v4u rd128(const uint8_t* p) {  // 8-byte aligned 16 bytes
+  const v2u a = *reinterpret_cast<const v2u*>(p), b = *reinterpret_cast<const v2u*>(p + 8 + opaque0());
+  v4u r;
+  r.x = a.x;
+  r.y = a.y;
+  r.z = b.x;
+  r.w = b.y;
+  return r;
+}
+__device__ __forceinline__ void wr128(uint8_t* p, const v4u& v) {
+  v2u a, b;
+  a.x = v.x;
+  a.y = v.y;
+  b.x = v.z;
+  b.y = v.w;
+  *reinterpret_cast<v2u*>(p) = a;
+  *reinterpret_cast<v2u*>(p + 8 + opaque0()) = b;
+}
+__device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t b) {
+  return __builtin_amdgcn_alignbyte(hi, lo, b);
+}
+// ring bytes [p, p+8) (ring of 128 bytes, any p)
+__device__ __forceinline__ v2u ring_rd8(const uint8_t* ring, uint32_t p) {
+  const uint32_t a = p & (kOR - 8);
+  const v2u A = rd64(ring, a), B = rd64(ring, a + 8);
+  const bool q = (p & 4) != 0;
+  const uint32_t d0 = q ? A.y : A.x, d1 = q ? B.x : A.y, d2 = q ? B.y : B.x;
+  const uint32_t b = p & 3;
+  v2u r;
+  r.x = alignb(d1, d0, b);
+  r.y = alignb(d2, d1, b);
+  return r;
+}
+// ring bytes [p, p+16)
+__device__ __forceinline__ v4u ring_rd16(const uint8_t* ring, uint32_t p) {
+  const uint32_t a = p & (kOR - 8);
+  const v2u A = rd64(ring, a), B = rd64(ring, a + 8), C = rd64(ring, a + 16);
+  const bool q = (p & 4) != 0;
+  const uint32_t e0 = q ? A.y : A.x, e1 = q ? B.x : A.y, e2 = q ? B.y : B.x, e3 = q ? C.x : B.y,
+                 e4 = q ? C.y : C.x;
+  const uint32_t b = p & 3;
+  v4u r;
+  r.x = alignb(e1, e0, b);
+  r.y = alignb(e2, e1, b);
+  r.z = alignb(e3, e2, b);
+  r.w = alignb(e4, e3, b);
+  return r;
+}
+// the five dwords that put v at byte b (0..3) of a 20-byte window whose first dword keeps
+// `head` below byte b
+struct Win5 {
+  uint32_t y0, y1, y2, y3, y4;
+};
+__device__ __forceinline__ Win5 shift_in(const v4u& v, uint32_t head, uint32_t b) {
+  const uint32_t sel = 0x07060504u - b * 0x01010101u;  // v_perm: byte i <- byte (4 - b + i) of {hi:lo}
+  const uint32_t keep = (1u << (8 * b)) - 1u;
+  Win5 w;
+  w.y0 = (head & keep) | (__builtin_amdgcn_perm(v.x, head, sel) & ~keep);
+  w.y1 = __builtin_amdgcn_perm(v.y, v.x, sel);
+  w.y2 = __builtin_amdgcn_perm(v.z, v.y, sel);
+  w.y3 = __builtin_amdgcn_perm(v.w, v.z, sel);
+  w.y4 = __builtin_amdgcn_perm(v.w, v.w, sel);
+  return w;
+}
+__device__ __forceinline__ void wr32(uint8_t* ring, uint32_t a, uint32_t v) {
+  *reinterpret_cast<uint32_t*>(ring + (a & (kOR - 4))) = v;
+}
+__device__ __forceinline__ void store_win(uint8_t* ring, uint32_t a4, const Win5& w) {
+  wr32(ring, a4, w.y0);
+  wr32(ring, a4 + 4, w.y1);
+  wr32(ring, a4 + 8, w.y2);
+  wr32(ring, a4 + 12, w.y3);
+  wr32(ring, a4 + 16, w.y4);
+}
+__device__ __forceinline__ uint32_t pick5(const Win5& w, uint32_t j) {
+  return j == 0 ? w.y0 : j == 1 ? w.y1 : j == 2 ? w.y2 : j == 3 ? w.y3 : w.y4;
+}
 
 // Cache policy (gfx950 CPol bits): 0 = default (allocates in L2: a lane reads its block's 128-byte
 // lines 16 bytes at a time, so the line must stay for the next 7 accesses), 16 = sc1 (bypasses the
@@ -183,6 +274,7 @@ struct Lane {
   uint32_t crc, crc_pos;
   // decode
   uint32_t s, d, rem, src, eff, lit, far, dd, err;
+  uint32_t T;  // the output ring's dword at d & ~3 (what the next store merges below d)
   uint32_t c_issue, c_commit, n_req, fpend, fready, fl;
   // pending hole: a copy with offset > kReach and length <= 16 reserves output [hd, hd+hl)
   // and decoding goes on; its source arrives four steps later and is merged into the ring
@@ -201,7 +293,7 @@ struct Rsrc {
 // CRC32 of the next committed input chunk (bytes outside the block zeroed).
 __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint32_t* tab, bool go) {
   const uint32_t k = L.crc_pos;
-  v4u v = *reinterpret_cast<const v4u*>(in + (k & (kNS - 1)) * 16);
+  v4u v = rd128(in + (k & (kNS - 1)) * 16);
   const bool partial = go && (k == 0 || int32_t(k) == L.crc_last);
   if (__builtin_amdgcn_ballot_w64(partial)) {  // wave-uniform branch: first/last chunks only
     const int32_t lo = int32_t(L.sh) - int32_t(16 * k), hi = int32_t(L.sh + L.clen) - int32_t(16 * k);
@@ -227,7 +319,7 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   const bool in_hole = L.hpend && rpos < L.hd + L.hl && rpos + 8 > L.hd;
   const bool wa = act && L.rphase < 3 && L.d >= L.rneed && !in_hole;
   const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
-  const v2u q = lds_rd8(ring + (rpos & (kOR - 1)));
+  const v2u q = ring_rd8(ring, rpos);
   // phase 0: prefix / suffix lengths
   const uint32_t pl0 = be16_of(q.x), sl0 = be16_of(q.x >> 16);
   // phase 1: flags, and the value length right after them when there are no timestamps
@@ -280,9 +372,7 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
 // up to four more chunks (ring room and payload end permitting); (3) four transposed
 // loads fetch them: in load j, lanes 4i..4i+3 read chunks c_issue..c_issue+3 of block 16j+i.
 __device__ __forceinline__ void commit_one(uint8_t* ins, uint32_t slot, const v4u& v) {
-  // slot: LDS offset | kMirrorBit for ring slot 0 (the chunk also goes to the mirror)
-  if (slot != 0xFFFFFFFFu) *reinterpret_cast<v4u*>(ins + (slot & ~kMirrorBit)) = v;
-  if (slot != 0xFFFFFFFFu && (slot & kMirrorBit)) *reinterpret_cast<v4u*>(ins + (slot & ~kMirrorBit) + kIR) = v;
+  if (slot != 0xFFFFFFFFu) wr128(ins + slot, v);  // slot: LDS offset of the ring slot
 }
 
 __device__ __forceinline__ void load_one(uint32_t j, uint32_t lane, uint32_t wave_lane0, uint32_t info,
@@ -293,8 +383,7 @@ __device__ __forceinline__ void load_one(uint32_t j, uint32_t lane, uint32_t wav
   const uint32_t ci = (info_o >> 3) + c;
   const bool want = c < (info_o & 7);
   P = __builtin_amdgcn_raw_buffer_load_b128(R.in, want ? rel_o + 16 * ci : kOOB, 0, 0);
-  slot = want ? ((wave_lane0 + o) * kInStride + (ci & (kNS - 1)) * 16) | ((ci & (kNS - 1)) ? 0u : kMirrorBit)
-              : 0xFFFFFFFFu;
+  slot = want ? (wave_lane0 + o) * kInStride + (ci & (kNS - 1)) * 16 : 0xFFFFFFFFu;
 }
 
 // Start of an iteration, part 2: how many chunks this block asks for (ring room and
@@ -305,40 +394,53 @@ __device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, ui
   return act ? min(min(room, left), 4u) : 0u;
 }
 
-// One step: the far-copy source loaded four steps ago, CRC (two of four steps), parse,
-// copy, the far-copy / hole load, and the row walker (the other two steps).
+// Start of an iteration, after the refill: the far-copy source loaded in the previous
+// iteration (at most one per lane) either fills the pending hole -- a read-modify-write of
+// the five ring dwords around [hd, hd+hl): the bytes after the hole were decoded meanwhile --
+// or feeds a long far copy through FD.
+__device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q0, const v4u& Q1, const v4u& Q2, const v4u& Q3,
+                                           v4u& FD, uint8_t* ring) {
+  const bool fc = L.fpend != 0;
+  const v4u Q = (L.fpend & 1) ? Q0 : ((L.fpend & 2) ? Q1 : ((L.fpend & 4) ? Q2 : Q3));
+  const bool fill = fc && L.hpend;
+  if (__builtin_amdgcn_ballot_w64(fill)) {
+    const uint32_t hd = L.hd, b = hd & 3, a4 = hd & ~3u, a = hd & ~7u;
+    const v2u A = rd64(ring, a), B = rd64(ring, a + 8), C = rd64(ring, a + 16);
+    const bool q = (hd & 4) != 0;
+    Win5 o;
+    o.y0 = q ? A.y : A.x;
+    o.y1 = q ? B.x : A.y;
+    o.y2 = q ? B.y : B.x;
+    o.y3 = q ? C.x : B.y;
+    o.y4 = q ? C.y : C.x;
+    const Win5 y = shift_in(Q, o.y0, b);
+    const int32_t lo = int32_t(b), hi = int32_t(b + L.hl);
+    Win5 n;
+    n.y0 = (y.y0 & keep_mask(lo, hi, 0)) | (o.y0 & ~keep_mask(lo, hi, 0));
+    n.y1 = (y.y1 & keep_mask(lo, hi, 1)) | (o.y1 & ~keep_mask(lo, hi, 1));
+    n.y2 = (y.y2 & keep_mask(lo, hi, 2)) | (o.y2 & ~keep_mask(lo, hi, 2));
+    n.y3 = (y.y3 & keep_mask(lo, hi, 3)) | (o.y3 & ~keep_mask(lo, hi, 3));
+    n.y4 = (y.y4 & keep_mask(lo, hi, 4)) | (o.y4 & ~keep_mask(lo, hi, 4));
+    if (fill) store_win(ring, a4, n);
+    // the register copy of d's dword follows a store into that dword
+    const uint32_t jd = (((L.d & ~3u) - a4) & (kOR - 1)) >> 2;
+    L.T = (fill && jd <= 4) ? pick5(n, jd) : L.T;
+  }
+  FD = (fc && !fill) ? Q : FD;
+  L.fready = (fc && !fill) ? 1u : L.fready;
+  L.hpend = fill ? 0u : L.hpend;
+  L.fpend = 0;
+}
+
+// One step: CRC (two of four steps), parse, copy, the far-copy / hole load, and the row
+// walker (the other two steps).
 template <bool kWalkSlot>
-__device__ __forceinline__ void lane_step(Lane& L, v4u& Q, v4u& FD, uint32_t bit, bool act, uint8_t* ring,
+__device__ __forceinline__ void lane_step(Lane& L, v4u& Q, const v4u& FD, uint32_t bit, bool act, uint8_t* ring,
                                           uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg,
                                           v4u& prow, uint32_t& prow_off) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
   dbg = SLATE_FORCE_DBG;
 #endif
-  // ---- the far-copy source loaded four steps ago: fills the pending hole (read-modify-write
-  // of the 16 ring bytes at hd: the bytes after the hole were decoded meanwhile), or feeds
-  // a long far copy through FD
-  {
-    const bool fc = (L.fpend & bit) != 0;
-    const bool fill = fc && L.hpend;
-    const uint32_t x = L.hd & (kOR - 1);
-    if (__builtin_amdgcn_ballot_w64(fill)) {
-      const v4u cur = lds_rd16(ring + x);
-      v4u m;
-      m.x = keep_mask(0, int32_t(L.hl), 0);
-      m.y = keep_mask(0, int32_t(L.hl), 1);
-      m.z = keep_mask(0, int32_t(L.hl), 2);
-      m.w = keep_mask(0, int32_t(L.hl), 3);
-      const v4u v = (Q & m) | (cur & ~m);
-      if (fill) {
-        lds_wr16(ring + x, v);
-        if (x < 16 || x > kOR - 16) lds_wr16(x < 16 ? ring + x + kOR : ring + x - kOR, v);
-      }
-    }
-    FD = (fc && !fill) ? Q : FD;
-    L.fready = (fc && !fill) ? 1u : L.fready;
-    L.hpend = fill ? 0u : L.hpend;
-    L.fpend = fc ? 0u : L.fpend;
-  }
   // ---- CRC32 of one committed chunk (the two steps without the walker)
   if (!kWalkSlot) {
     const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
@@ -357,7 +459,7 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, v4u& FD, uint32_t bit
     // every unflushed byte and every far source (offset > 112) is already flushed
     const bool room_out = L.d - 16 * L.fl <= kUnflushed;
     const bool can = need && L.s < sn && avail >= int32_t(min(L.s + 5, sn)) && room_out;
-    const v2u w = lds_rd8(in + ((L.sh + L.s) & (kIR - 1)));
+    const v2u w = ring_rd8(in, L.sh + L.s);
     const uint32_t c = w.x & 0xff, t = c & 3;
     const uint32_t b14 = (w.x >> 8) | (w.y << 24);  // bytes s+1 .. s+4
     const uint32_t xl = c >> 2;
@@ -400,14 +502,14 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, v4u& FD, uint32_t bit
     const bool near = !L.lit && !L.far;
     if (near && L.hpend && L.src < L.hd + L.hl && L.src + k > L.hd) k = L.src < L.hd ? L.hd - L.src : 0u;
     k = (cp && L.d - 16 * L.fl <= kUnflushed) ? k : 0u;
-    const v4u vl = lds_rd16(L.lit ? in + ((L.sh + L.src) & (kIR - 1)) : ring + (L.src & (kOR - 1)));
+    const v4u vl = ring_rd16(L.lit ? in : ring, L.lit ? L.sh + L.src : L.src);
     const v4u v = L.far ? FD : vl;
-    // bytes at [d, d+16) are not yet output: writing them when k == 0 is harmless
-    const uint32_t x = L.d & (kOR - 1);
-    lds_wr16(ring + x, v);
-    // mirror upkeep: ring[0..16) is duplicated at ring[128..144); a write crossing
-    // the end also lands at the start (pads absorb the overhang on both sides)
-    if (x < 16 || x > kOR - 16) lds_wr16(x < 16 ? ring + x + kOR : ring + x - kOR, v);
+    // bytes from d on are not yet output: storing them when k == 0 is harmless; the first
+    // dword keeps the bytes below d (L.T)
+    const uint32_t b = L.d & 3;
+    const Win5 y = shift_in(v, L.T, b);
+    store_win(ring, L.d & ~3u, y);
+    L.T = pick5(y, (b + k) >> 2);
     L.d += k;
     L.rem -= k;
     // periodic output: once a whole period was copied, the pattern can be read twice as far back
@@ -451,8 +553,8 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
     const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
     const uint32_t info_o = __shfl(info, int(o), 64);
     const uint32_t base_o = __shfl(base, int(o), 64);
-    const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride + 16;
-    const v4u v = *reinterpret_cast<const v4u*>(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)));
+    const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
+    const v4u v = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)));
     bstore(R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, v);
   }
   L.fl += min(done, 4u);
@@ -475,8 +577,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
   const uint32_t* crc_init = tab + 1024;
   const uint32_t* crc_tail = tab + 1024 + 16;
   uint8_t* outs = smem + kTabBytes + 4 * kConstWords;
-  uint8_t* ins = outs + kLpb2Threads * kOutStride + 16;
-  uint8_t* ring = outs + threadIdx.x * kOutStride + 16;
+  uint8_t* ins = outs + kLpb2Threads * kOutStride;
+  uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
   // wave-uniform by construction: the buffer resources derived from it must live in SGPRs
   const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
@@ -509,7 +611,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     L.crc_last = -1;
     L.crc = 0xFFFFFFFFu;
     L.crc_pos = 0;
-    L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = 0;
+    L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = L.T = 0;
     L.eff = 16;
     L.dd = 1;
     L.c_issue = L.c_commit = L.n_req = L.fpend = L.fready = L.fl = 0;
@@ -546,9 +648,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(R.in, have ? L.in_rel : kOOB, 0, 0);
       const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && L.last_chunk >= 1) ? L.in_rel + 16 : kOOB, 0, 0);
       if (have) {
-        *reinterpret_cast<v4u*>(in) = c0;
-        *reinterpret_cast<v4u*>(in + kIR) = c0;
-        *reinterpret_cast<v4u*>(in + 16) = c1;
+        wr128(in, c0);
+        wr128(in + 16, c1);
         L.c_commit = L.last_chunk >= 1 ? 2u : 1u;
         L.c_issue = L.c_commit;
         uint64_t x = 0;
@@ -611,6 +712,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         L.c_issue += n;
         L.n_req = n;
       }
+      absorb_far(L, Q0, Q1, Q2, Q3, FD, ring);
       v4u row_a, row_b;
       uint32_t off_a = kOOB, off_b = kOOB;
       lane_step<false>(L, Q0, FD, 1u, act, ring, in, tab, R, a.debug, row_a, off_a);
@@ -634,7 +736,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     // rows stage: 0 = no rows to produce, 1 = walked rows to verify, 2 = re-derive from HBM
     uint32_t rows_stage = 0, nr = 0, osi_u = 0;
     if (have) {
-      const uint32_t stored = __builtin_bswap32(lds_rd4(in + ((L.sh + L.clen) & (kIR - 1))));
+      const uint32_t stored = __builtin_bswap32(ring_rd8(in, L.sh + L.clen).x);
       // the register absorbed t zero bytes after the payload: compare against stored * x^(8t)
       const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
       const bool crc_ok = gf2_mulmod(~stored, crc_tail[t]) == L.crc;
@@ -647,7 +749,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       } else {
         // remaining output chunks (the last one is padded inside its 16-byte slot)
         while (L.fl * 16 < dn) {
-          const v4u o = *reinterpret_cast<const v4u*>(ring + ((L.fl * 16) & (kOR - 1)));
+          const v4u o = rd128(ring + ((L.fl * 16) & (kOR - 1)));
           reinterpret_cast<v4u*>(gout)[L.fl] = o;
           L.fl++;
         }
@@ -664,7 +766,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         } else {
           // block.go:101-134 over the decoded block.  The tail (offsets, count) is read
           // from the output ring when it is still there, else from HBM.
-          const uint32_t cnt = be16_of(lds_rd4(ring + ((dn - 2) & (kOR - 1))));
+          const uint32_t cnt = be16_of(ring_rd8(ring, dn - 2).x);
           const int64_t osi = int64_t(dn) - 2 - 2 * int64_t(cnt);
           if (osi <= 0) {
             m.status = SLATE_E_BLOCK_INDEX_OFFSET;
@@ -673,7 +775,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
             const bool tail_in_ring = dn - uint32_t(osi) <= kReach;
             auto off_at = [&](uint32_t i) -> uint32_t {
               const uint32_t p = uint32_t(osi) + 2 * i;
-              if (tail_in_ring) return be16_of(lds_rd4(ring + (p & (kOR - 1))));
+              if (tail_in_ring) return be16_of(ring_rd8(ring, p).x);
               return out_be16(gout + p);
             };
             const uint16_t osi16 = uint16_t(osi);
@@ -799,7 +901,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
 
 
 size_t lpb2_lds_bytes() {
-  return kTabBytes + 4 * kConstWords + size_t(kLpb2Threads) * (kOutStride + kInStride) + 16;
+  return kTabBytes + 4 * kConstWords + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {
