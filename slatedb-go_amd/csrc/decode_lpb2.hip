@@ -53,7 +53,10 @@ constexpr uint32_t kOR = 128;          // output ring bytes
 // (five dwords), i.e. 109 bytes behind d modulo the ring
 constexpr uint32_t kReach = kOR - 20;
 constexpr uint32_t kUnflushed = 80;    // d - 16*fl before a step may advance d (see the throttle)
-constexpr uint32_t kNS = 8;            // input ring slots
+#ifndef SLATE_LPB_NS
+#define SLATE_LPB_NS 8
+#endif
+constexpr uint32_t kNS = SLATE_LPB_NS;  // input ring slots (16 bytes each)
 constexpr uint32_t kIR = kNS * 16;
 // LDS: output rings, then input rings, no mirrors: every access is naturally aligned and
 // wraps per element.  Lane records are 136 bytes apart (34 dwords): blocks of a round
@@ -63,8 +66,8 @@ constexpr uint32_t kIR = kNS * 16;
 // two b64 halves.
 constexpr uint32_t kOutStride = kOR + 8;
 constexpr uint32_t kInStride = kIR + 8;
-constexpr uint32_t kConstWords = 32;    // crc_init[16] | crc_tail[16]
 constexpr uint32_t kOOB = 0xFFFFFFF0u;  // buffer offset that is always out of range
+constexpr uint32_t kVerifyBatch = 4;    // blocks per wait in the cooperative row check
 
 // CRC register state that becomes 0xFFFFFFFF after `sh` zero bytes (sh < 16), and x^(8t) mod P.
 struct CrcLeadTail {
@@ -90,19 +93,16 @@ static __constant__ CrcLeadTail g_crc_lt = CrcLeadTail();
 // lane keeps that dword in a register, Lane::T).  Each element wraps on its own, so the
 // rings need no mirror copies.
 __device__ __forceinline__ uint32_t be16_of(uint32_t w) { return ((w & 0xff) << 8) | ((w >> 8) & 0xff); }
-__device__ __forceinline__ v2u rd64(const uint8_t* ring, uint32_t a) {
-  return *reinterpret_cast<const v2u*>(ring + (a & (kOR - 8)));
+// m8 = ring size - 8 (both rings are powers of two)
+__device__ __forceinline__ v2u rd64(const uint8_t* ring, uint32_t a, uint32_t m8 = kOR - 8) {
+  return *reinterpret_cast<const v2u*>(ring + (a & m8));
 }
-// An opaque zero keeps the compiler from fusing two b64 accesses 8 bytes apart into
-// ds_read2_b64 / ds_write2_b64, which cost ~55 CU-cycles per wave-instruction at these
-// addresses (tools/lds_cost_probe.hip) against ~3 for two ds_read_b64.
-__device__ __forceinline__ uint32_t opaque0() {
-  uint32_t z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return z;
-}
-__device__ __forceinline__ v4u rd128(const uint8_t* p) {  // 8-byte aligned 16 bytes
-  const v2u a = *reinterpret_cast<const v2u*>(p), b = *reinterpret_cast<const v2u*>(p + 8 + opaque0());
+// z is a run-time zero (DecodeArgs::debug >> 31): it keeps the compiler from fusing two b64
+// accesses 8 bytes apart into ds_read2_b64 / ds_write2_b64, which cost ~55 CU-cycles per
+// wave-instruction at these addresses (tools/lds_cost_probe.hip) against ~3 for two
+// ds_read_b64.
+__device__ __forceinline__ v4u rd128(const uint8_t* p, uint32_t z) {  // 8-byte aligned 16 bytes
+  const v2u a = *reinterpret_cast<const v2u*>(p), b = *reinterpret_cast<const v2u*>(p + 8 + z);
   v4u r;
   r.x = a.x;
   r.y = a.y;
@@ -110,22 +110,22 @@ __device__ __forceinline__ v4u rd128(const uint8_t* p) {  // 8-byte aligned 16 b
   r.w = b.y;
   return r;
 }
-__device__ __forceinline__ void wr128(uint8_t* p, const v4u& v) {
+__device__ __forceinline__ void wr128(uint8_t* p, const v4u& v, uint32_t z) {
   v2u a, b;
   a.x = v.x;
   a.y = v.y;
   b.x = v.z;
   b.y = v.w;
   *reinterpret_cast<v2u*>(p) = a;
-  *reinterpret_cast<v2u*>(p + 8 + opaque0()) = b;
+  *reinterpret_cast<v2u*>(p + 8 + z) = b;
 }
 __device__ __forceinline__ uint32_t alignb(uint32_t hi, uint32_t lo, uint32_t b) {
   return __builtin_amdgcn_alignbyte(hi, lo, b);
 }
 // ring bytes [p, p+8) (ring of 128 bytes, any p)
-__device__ __forceinline__ v2u ring_rd8(const uint8_t* ring, uint32_t p) {
-  const uint32_t a = p & (kOR - 8);
-  const v2u A = rd64(ring, a), B = rd64(ring, a + 8);
+__device__ __forceinline__ v2u ring_rd8(const uint8_t* ring, uint32_t p, uint32_t m8 = kOR - 8) {
+  const uint32_t a = p & m8;
+  const v2u A = rd64(ring, a, m8), B = rd64(ring, a + 8, m8);
   const bool q = (p & 4) != 0;
   const uint32_t d0 = q ? A.y : A.x, d1 = q ? B.x : A.y, d2 = q ? B.y : B.x;
   const uint32_t b = p & 3;
@@ -135,9 +135,9 @@ __device__ __forceinline__ v2u ring_rd8(const uint8_t* ring, uint32_t p) {
   return r;
 }
 // ring bytes [p, p+16)
-__device__ __forceinline__ v4u ring_rd16(const uint8_t* ring, uint32_t p) {
-  const uint32_t a = p & (kOR - 8);
-  const v2u A = rd64(ring, a), B = rd64(ring, a + 8), C = rd64(ring, a + 16);
+__device__ __forceinline__ v4u ring_rd16(const uint8_t* ring, uint32_t p, uint32_t m8 = kOR - 8) {
+  const uint32_t a = p & m8;
+  const v2u A = rd64(ring, a, m8), B = rd64(ring, a + 8, m8), C = rd64(ring, a + 16, m8);
   const bool q = (p & 4) != 0;
   const uint32_t e0 = q ? A.y : A.x, e1 = q ? B.x : A.y, e2 = q ? B.y : B.x, e3 = q ? C.x : B.y,
                  e4 = q ? C.y : C.x;
@@ -275,7 +275,9 @@ struct Lane {
   // decode
   uint32_t s, d, rem, src, eff, lit, far, dd, err;
   uint32_t T;  // the output ring's dword at d & ~3 (what the next store merges below d)
+  uint32_t z;  // a run-time zero (see rd128)
   uint32_t c_issue, c_commit, n_req, fpend, fready, fl;
+  uint32_t qoff;  // far-copy / hole source requested this iteration (loaded once, before the flush)
   // pending hole: a copy with offset > kReach and length <= 16 reserves output [hd, hd+hl)
   // and decoding goes on; its source arrives four steps later and is merged into the ring
   uint32_t hpend, hd, hl;
@@ -293,7 +295,7 @@ struct Rsrc {
 // CRC32 of the next committed input chunk (bytes outside the block zeroed).
 __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint32_t* tab, bool go) {
   const uint32_t k = L.crc_pos;
-  v4u v = rd128(in + (k & (kNS - 1)) * 16);
+  v4u v = rd128(in + (k & (kNS - 1)) * 16, L.z);
   const bool partial = go && (k == 0 || int32_t(k) == L.crc_last);
   if (__builtin_amdgcn_ballot_w64(partial)) {  // wave-uniform branch: first/last chunks only
     const int32_t lo = int32_t(L.sh) - int32_t(16 * k), hi = int32_t(L.sh + L.clen) - int32_t(16 * k);
@@ -371,8 +373,8 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
 // input rings (the loading lane writes them: transposed layout); (2) every block asks for
 // up to four more chunks (ring room and payload end permitting); (3) four transposed
 // loads fetch them: in load j, lanes 4i..4i+3 read chunks c_issue..c_issue+3 of block 16j+i.
-__device__ __forceinline__ void commit_one(uint8_t* ins, uint32_t slot, const v4u& v) {
-  if (slot != 0xFFFFFFFFu) wr128(ins + slot, v);  // slot: LDS offset of the ring slot
+__device__ __forceinline__ void commit_one(uint8_t* ins, uint32_t slot, const v4u& v, uint32_t z) {
+  if (slot != 0xFFFFFFFFu) wr128(ins + slot, v, z);  // slot: LDS offset of the ring slot
 }
 
 __device__ __forceinline__ void load_one(uint32_t j, uint32_t lane, uint32_t wave_lane0, uint32_t info,
@@ -398,10 +400,8 @@ __device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, ui
 // iteration (at most one per lane) either fills the pending hole -- a read-modify-write of
 // the five ring dwords around [hd, hd+hl): the bytes after the hole were decoded meanwhile --
 // or feeds a long far copy through FD.
-__device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q0, const v4u& Q1, const v4u& Q2, const v4u& Q3,
-                                           v4u& FD, uint8_t* ring) {
+__device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q, v4u& FD, uint8_t* ring) {
   const bool fc = L.fpend != 0;
-  const v4u Q = (L.fpend & 1) ? Q0 : ((L.fpend & 2) ? Q1 : ((L.fpend & 4) ? Q2 : Q3));
   const bool fill = fc && L.hpend;
   if (__builtin_amdgcn_ballot_w64(fill)) {
     const uint32_t hd = L.hd, b = hd & 3, a4 = hd & ~3u, a = hd & ~7u;
@@ -435,9 +435,8 @@ __device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q0, const v4u& Q1
 // One step: CRC (two of four steps), parse, copy, the far-copy / hole load, and the row
 // walker (the other two steps).
 template <bool kWalkSlot>
-__device__ __forceinline__ void lane_step(Lane& L, v4u& Q, const v4u& FD, uint32_t bit, bool act, uint8_t* ring,
-                                          uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg,
-                                          v4u& prow, uint32_t& prow_off) {
+__device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint8_t* ring,
+                                          uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
   dbg = SLATE_FORCE_DBG;
 #endif
@@ -459,7 +458,7 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, const v4u& FD, uint32
     // every unflushed byte and every far source (offset > 112) is already flushed
     const bool room_out = L.d - 16 * L.fl <= kUnflushed;
     const bool can = need && L.s < sn && avail >= int32_t(min(L.s + 5, sn)) && room_out;
-    const v2u w = ring_rd8(in, L.sh + L.s);
+    const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
     const uint32_t c = w.x & 0xff, t = c & 3;
     const uint32_t b14 = (w.x >> 8) | (w.y << 24);  // bytes s+1 .. s+4
     const uint32_t xl = c >> 2;
@@ -502,7 +501,7 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, const v4u& FD, uint32
     const bool near = !L.lit && !L.far;
     if (near && L.hpend && L.src < L.hd + L.hl && L.src + k > L.hd) k = L.src < L.hd ? L.hd - L.src : 0u;
     k = (cp && L.d - 16 * L.fl <= kUnflushed) ? k : 0u;
-    const v4u vl = ring_rd16(L.lit ? in : ring, L.lit ? L.sh + L.src : L.src);
+    const v4u vl = ring_rd16(L.lit ? in : ring, L.lit ? L.sh + L.src : L.src, L.lit ? kIR - 8 : kOR - 8);
     const v4u v = L.far ? FD : vl;
     // bytes from d on are not yet output: storing them when k == 0 is harmless; the first
     // dword keeps the bytes below d (L.T)
@@ -519,18 +518,18 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, const v4u& FD, uint32
     L.eff = eff2;
     L.fready = (L.far && k) ? 0u : L.fready;
   }
-  // ---- the far-copy / hole source load of this step (always issued, sc1: L1 bypass)
+  // ---- the far-copy / hole source request of this step (loaded at the end of the iteration)
   {
     const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
-    const uint32_t qoff = hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : kOOB);
-    Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg & 32768) ? kOOB : qoff, 0, 16);
-    L.fpend = (wantf || hole_new) ? bit : L.fpend;
+    L.qoff = hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : L.qoff);
+    L.fpend = (wantf || hole_new) ? 1u : L.fpend;
     if (kWalkSlot) {
       v4u row;
       uint32_t ridx;
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
-      prow = row;
-      prow_off = (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB;
+      // stored right away: the loads waited on later were issued before it (refill) or are
+      // waited on an iteration later (far source), so its acknowledgement is off the path
+      bstore(R.rows, (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB, row);
     }
   }
 }
@@ -542,8 +541,7 @@ __device__ __forceinline__ void lane_step(Lane& L, v4u& Q, const v4u& FD, uint32
 // block of lane 16j+i, so every store instruction writes 16 runs of 64 contiguous bytes
 // instead of 64 scattered 16-byte pieces (tools/scatter_probe.hip: ~3.5x cheaper).
 __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
-                                                uint32_t dbg, const v4u& row_a, uint32_t off_a, const v4u& row_b,
-                                                uint32_t off_b) {
+                                                uint32_t dbg) {
   const uint32_t done = act ? min(L.d >> 4, L.hpend ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
   const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
   const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
@@ -554,12 +552,10 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
     const uint32_t info_o = __shfl(info, int(o), 64);
     const uint32_t base_o = __shfl(base, int(o), 64);
     const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
-    const v4u v = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)));
+    const v4u v = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)), L.z);
     bstore(R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, v);
   }
   L.fl += min(done, 4u);
-  bstore(R.rows, off_a, row_a);
-  bstore(R.rows, off_b, row_b);
 }
 
 }  // namespace
@@ -570,13 +566,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
   {
     const uint32_t* src = &g_crc_tables.t[0][0];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];
-    const uint32_t* lt = &g_crc_lt.init[0];
-    for (uint32_t i = threadIdx.x; i < kConstWords; i += blockDim.x) tab[1024 + i] = lt[i];
     __syncthreads();
   }
-  const uint32_t* crc_init = tab + 1024;
-  const uint32_t* crc_tail = tab + 1024 + 16;
-  uint8_t* outs = smem + kTabBytes + 4 * kConstWords;
+  const uint32_t* crc_init = g_crc_lt.init;  // used once per round: constant memory
+  const uint32_t* crc_tail = g_crc_lt.tail;
+  uint8_t* outs = smem + kTabBytes;
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
@@ -600,7 +594,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
 
     Lane L;
     const v4u zero = {0, 0, 0, 0};
-    v4u Q0 = zero, Q1 = zero, Q2 = zero, Q3 = zero, FD = zero;
+    v4u Q = zero, FD = zero;
     v4u P0 = zero, P1 = zero, P2 = zero, P3 = zero;
     uint32_t S0 = 0xFFFFFFFFu, S1 = 0xFFFFFFFFu, S2 = 0xFFFFFFFFu, S3 = 0xFFFFFFFFu;
     const uint32_t b = round0 + lane;
@@ -612,9 +606,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     L.crc = 0xFFFFFFFFu;
     L.crc_pos = 0;
     L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = L.T = 0;
+    L.z = a.debug >> 31;  // the host never sets bit 31
     L.eff = 16;
     L.dd = 1;
     L.c_issue = L.c_commit = L.n_req = L.fpend = L.fready = L.fl = 0;
+    L.qoff = kOOB;
     L.hpend = L.hd = L.hl = 0;
     L.R = 0;
     L.rphase = 0;
@@ -648,8 +644,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(R.in, have ? L.in_rel : kOOB, 0, 0);
       const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && L.last_chunk >= 1) ? L.in_rel + 16 : kOOB, 0, 0);
       if (have) {
-        wr128(in, c0);
-        wr128(in + 16, c1);
+        wr128(in, c0, L.z);
+        wr128(in + 16, c1, L.z);
         L.c_commit = L.last_chunk >= 1 ? 2u : 1u;
         L.c_issue = L.c_commit;
         uint64_t x = 0;
@@ -693,10 +689,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       const bool act = have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                        iters < budget;
       {
-        commit_one(ins, S0, P0);
-        commit_one(ins, S1, P1);
-        commit_one(ins, S2, P2);
-        commit_one(ins, S3, P3);
+        commit_one(ins, S0, P0, L.z);
+        commit_one(ins, S1, P1, L.z);
+        commit_one(ins, S2, P2, L.z);
+        commit_one(ins, S3, P3, L.z);
         L.c_commit += L.n_req;
         // the ring keeps every chunk from the oldest byte still to be read or CRC'd
         const uint32_t lo_pos = L.dd ? L.clen : ((L.rem && L.lit) ? L.src : L.s);
@@ -712,14 +708,17 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         L.c_issue += n;
         L.n_req = n;
       }
-      absorb_far(L, Q0, Q1, Q2, Q3, FD, ring);
-      v4u row_a, row_b;
-      uint32_t off_a = kOOB, off_b = kOOB;
-      lane_step<false>(L, Q0, FD, 1u, act, ring, in, tab, R, a.debug, row_a, off_a);
-      lane_step<true>(L, Q1, FD, 2u, act, ring, in, tab, R, a.debug, row_a, off_a);
-      lane_step<false>(L, Q2, FD, 4u, act, ring, in, tab, R, a.debug, row_b, off_b);
-      lane_step<true>(L, Q3, FD, 8u, act, ring, in, tab, R, a.debug, row_b, off_b);
-      flush_iteration(L, act, outs, lane, R, a.debug, row_a, off_a, row_b, off_b);
+      absorb_far(L, Q, FD, ring);
+      lane_step<false>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<true>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<false>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<true>(L, FD, act, ring, in, tab, R, a.debug);
+      // the far-copy / hole source requested in this iteration (at most one per lane; sc1:
+      // L1 bypass), before the flush stores so that vmcnt waits stay static; it is merged
+      // at the start of the next iteration
+      Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (a.debug & 32768) ? kOOB : L.qoff, 0, 16);
+      L.qoff = kOOB;
+      flush_iteration(L, act, outs, lane, R, a.debug);
       iters++;
     }
     const uint32_t round_cycles = (a.debug & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
@@ -736,7 +735,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     // rows stage: 0 = no rows to produce, 1 = walked rows to verify, 2 = re-derive from HBM
     uint32_t rows_stage = 0, nr = 0, osi_u = 0;
     if (have) {
-      const uint32_t stored = __builtin_bswap32(ring_rd8(in, L.sh + L.clen).x);
+      const uint32_t stored = __builtin_bswap32(ring_rd8(in, L.sh + L.clen, kIR - 8).x);
       // the register absorbed t zero bytes after the payload: compare against stored * x^(8t)
       const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
       const bool crc_ok = gf2_mulmod(~stored, crc_tail[t]) == L.crc;
@@ -749,7 +748,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       } else {
         // remaining output chunks (the last one is padded inside its 16-byte slot)
         while (L.fl * 16 < dn) {
-          const v4u o = rd128(ring + ((L.fl * 16) & (kOR - 1)));
+          const v4u o = rd128(ring + ((L.fl * 16) & (kOR - 1)), L.z);
           reinterpret_cast<v4u*>(gout)[L.fl] = o;
           L.fl++;
         }
@@ -833,11 +832,12 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       uint64_t todo = (a.debug & 65536) ? 0 : __ballot(rows_stage == 1);  // 65536: profiling only
       uint64_t mism = 0;
       while (todo) {
-        uint32_t js[8], nrs[8], osis[8], outs[8], rws[8], nws[8], Rs[8], ends[8];
-        uint32_t ob[8], wr[8];
+        uint32_t js[kVerifyBatch], nrs[kVerifyBatch], osis[kVerifyBatch], outs[kVerifyBatch], rws[kVerifyBatch],
+            nws[kVerifyBatch], Rs[kVerifyBatch], ends[kVerifyBatch];
+        uint32_t ob[kVerifyBatch], wr[kVerifyBatch];
         uint32_t nb = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < 8; q++) {
+        for (uint32_t q = 0; q < kVerifyBatch; q++) {
           const bool v = todo != 0;
           const uint32_t j = v ? uint32_t(__builtin_ctzll(todo)) : 0u;
           todo &= v ? todo - 1 : todo;
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
               R.rows, (lane == 0 && nws[q] > nrs[q]) ? rws[q] + 16 * nrs[q] : kOOB, 0, 16);
         }
 #pragma unroll
-        for (uint32_t q = 0; q < 8; q++) {
+        for (uint32_t q = 0; q < kVerifyBatch; q++) {
           if (q < nb) {
           const uint32_t o = ((ob[q] & 0xff) << 8) | ((ob[q] >> 8) & 0xff);
           bool bad = lane < min(nrs[q], 64u) && o != wr[q];
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
 
 
 size_t lpb2_lds_bytes() {
-  return kTabBytes + 4 * kConstWords + size_t(kLpb2Threads) * (kOutStride + kInStride);
+  return kTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {

@@ -16,9 +16,15 @@ constexpr uint32_t kLargeOutCap = 90112;
 // LDS per lane + 4 KiB CRC tables -> 5 workgroups (waves) per CU
 constexpr int kLpbThreads = 64;
 constexpr uint32_t kLpbWgPerCu = 5;
-// lane-per-block Snappy decode v2 (decode_lpb2.hip): 304 B of LDS per lane + 4.1 KiB CRC
-// tables -> one 8-wave workgroup per CU
-constexpr int kLpb2Threads = 512;
+// lane-per-block Snappy decode v2 (decode_lpb2.hip): 136 B output ring + 136 B input ring
+// per lane + 4 KiB CRC tables -> one 8-wave workgroup per CU.  (12 waves with a 4-slot
+// input ring fit LDS and 168 VGPRs but ran slower: the smaller ring costs 15 % more
+// iterations, and 3 waves per SIMD gained only 15 % per iteration.)  SLATE_LPB_THREADS /
+// SLATE_LPB_NS override them for experiments (tools/variant.sh).
+#ifndef SLATE_LPB_THREADS
+#define SLATE_LPB_THREADS 512
+#endif
+constexpr int kLpb2Threads = SLATE_LPB_THREADS;
 
 struct DecodeArgs {
   int codec;
