@@ -63,8 +63,11 @@ def main():
         meta = np.frombuffer(d_meta.cpu().numpy().tobytes(), dtype=sc.META_DTYPE)
         it = meta["detail"][0::64].astype(np.float64)
         cyc = meta["detail"][1::64].astype(np.uint32).astype(np.float64)
+        post = meta["detail"][2::64].astype(np.uint32).astype(np.float64)
+        waited = meta["detail"][3::64].astype(np.uint32).astype(np.float64)
         stats = {"mode": m512, "iters_median": float(np.median(it)), "iters_max": float(it.max()),
-                 "cycles_median": float(np.median(cyc)), "cycles_per_iter": float(np.median(cyc / np.maximum(it, 1)))}
+                 "cycles_median": float(np.median(cyc)), "cycles_per_iter": float(np.median(cyc / np.maximum(it, 1))),
+                 "final_cycles_median": float(np.median(post)), "rows_wait_median": float(np.median(waited))}
     out = {str(m): {"ms_median": float(np.median(v)), "ms_min": float(np.min(v)),
                     "GiBps": dec_bytes / (np.median(v) * 1e-3) / 2**30} for m, v in res.items()}
     print(json.dumps({"blocks": n, "decoded_bytes": dec_bytes, "modes": out, "round_stats": stats}, indent=1))

@@ -27,7 +27,8 @@ def mix(dbg):
             body = [x.strip() for x in lines[labels[m.group(2)]:i] if x.strip() and x.strip()[0] not in ";." and not x.strip().endswith(":")]
             nd = sum(1 for x in body if x.startswith("ds_"))
             nb = sum(1 for x in body if x.startswith("buffer_"))
-            if nb >= 10 and nd >= 20 and (best is None or len(body) < len(best)):
+            npm = sum(1 for x in body if x.startswith("ds_bpermute"))
+            if nb >= 8 and nd >= 20 and npm >= 8 and (best is None or len(body) < len(best)):
                 best = body
     c = collections.Counter(x.split()[0] for x in best)
     return {k: sum(v for op, v in c.items() if op.startswith(p)) for k, p in
