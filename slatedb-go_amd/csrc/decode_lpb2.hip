@@ -84,6 +84,37 @@ struct CrcLeadTail {
 };
 static __constant__ CrcLeadTail g_crc_lt = CrcLeadTail();
 
+// Slicing-by-16 tables: t[k][b] = the CRC of byte b followed by k zero bytes (t[0] is the
+// classic table).  A 16-byte chunk then costs 16 independent lookups and one dependent
+// step, instead of four dependent rounds of four.
+struct CrcTables16 {
+  uint32_t t[16][256];
+  constexpr CrcTables16() : t{} {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; i++)
+      for (int s = 1; s < 16; s++) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+  }
+};
+static __constant__ CrcTables16 g_crc16 = CrcTables16();
+constexpr uint32_t kTab16Bytes = 16 * 256 * 4;
+
+__device__ __forceinline__ uint32_t crc16_chunk(const uint32_t* tab, uint32_t c, const v4u& v) {
+  const uint32_t x = c ^ v.x;
+  uint32_t r = tab[15 * 256 + (x & 0xff)] ^ tab[14 * 256 + ((x >> 8) & 0xff)] ^ tab[13 * 256 + ((x >> 16) & 0xff)] ^
+               tab[12 * 256 + (x >> 24)];
+  r ^= tab[11 * 256 + (v.y & 0xff)] ^ tab[10 * 256 + ((v.y >> 8) & 0xff)] ^ tab[9 * 256 + ((v.y >> 16) & 0xff)] ^
+       tab[8 * 256 + (v.y >> 24)];
+  r ^= tab[7 * 256 + (v.z & 0xff)] ^ tab[6 * 256 + ((v.z >> 8) & 0xff)] ^ tab[5 * 256 + ((v.z >> 16) & 0xff)] ^
+       tab[4 * 256 + (v.z >> 24)];
+  r ^= tab[3 * 256 + (v.w & 0xff)] ^ tab[2 * 256 + ((v.w >> 8) & 0xff)] ^ tab[1 * 256 + ((v.w >> 16) & 0xff)] ^
+       tab[v.w >> 24];
+  return r;
+}
+
 // Rings and natural alignment.  gfx950 executes ds_read/ds_write of 8 or 16 bytes at any
 // byte address, but an access that is not naturally aligned is serialised lane by lane:
 // ~64 CU-cycles per wave-instruction against 2-9 aligned, for b32, b64 and b128 alike
@@ -305,10 +336,7 @@ __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint
     v.w &= keep_mask(lo, hi, 3);
   }
   uint32_t c = L.crc;
-  c = crc_word(tab, c, v.x);
-  c = crc_word(tab, c, v.y);
-  c = crc_word(tab, c, v.z);
-  c = crc_word(tab, c, v.w);
+  c = crc16_chunk(tab, c, v);
   L.crc = go ? c : L.crc;
   L.crc_pos += go ? 1u : 0u;
 }
@@ -564,13 +592,13 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   {
-    const uint32_t* src = &g_crc_tables.t[0][0];
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];
+    const uint32_t* src = &g_crc16.t[0][0];
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
     __syncthreads();
   }
   const uint32_t* crc_init = g_crc_lt.init;  // used once per round: constant memory
   const uint32_t* crc_tail = g_crc_lt.tail;
-  uint8_t* outs = smem + kTabBytes;
+  uint8_t* outs = smem + kTab16Bytes;
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
@@ -901,7 +929,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
 
 
 size_t lpb2_lds_bytes() {
-  return kTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
+  return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {
