@@ -397,6 +397,37 @@ int slate_sst_builder_add_value(slate_sst_builder* b, const uint8_t* key, size_t
 int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const uint64_t* key_off,
                                 const uint8_t* values, const uint64_t* value_off, const uint8_t* is_tomb, uint64_t n) {
   if (!b || (n && (!keys || !key_off || !value_off))) return SLATE_E_INVALID_ARG;
+  if (!is_tomb && n && !b->built) {
+    // bulk path (tombstone = empty value): the same effect as n calls of
+    // slate_sst_builder_add, up to the first empty key (block.go:163), which fails
+    uint64_t m = 0, lower = 0;
+    while (m < n && key_off[m + 1] > key_off[m]) {
+      const uint64_t vl = value_off[m + 1] - value_off[m];
+      lower += 2 + 13 + (vl ? 4 + vl : 0);
+      m++;
+    }
+    if (m) {
+      const uint64_t kb = b->keys.size(), vb = b->vals.size();
+      b->keys.insert(b->keys.end(), keys + key_off[0], keys + key_off[m]);
+      b->vals.insert(b->vals.end(), values + value_off[0], values + value_off[m]);
+      b->key_off.reserve(b->key_off.size() + m);
+      b->val_off.reserve(b->val_off.size() + m);
+      b->tomb.reserve(b->tomb.size() + m);
+      for (uint64_t i = 0; i < m; i++) {
+        b->key_off.push_back(kb + (key_off[i + 1] - key_off[0]));
+        b->val_off.push_back(vb + (value_off[i + 1] - value_off[0]));
+        b->tomb.push_back(value_off[i + 1] == value_off[i] ? 1 : 0);
+      }
+      b->num_keys += m;
+      b->pending_lower += lower;
+      b->dirty = true;
+      if (!b->has_first_key) {  // builder.go:178-180
+        b->first_key.assign(keys + key_off[0], keys + key_off[1]);
+        b->has_first_key = true;
+      }
+    }
+    return m == n ? SLATE_OK : SLATE_E_INVALID_ARG;
+  }
   for (uint64_t i = 0; i < n; i++) {
     uint64_t vl = value_off[i + 1] - value_off[i];
     int kind = is_tomb ? (is_tomb[i] ? 1 : 0) : (vl == 0 ? 1 : 0);
