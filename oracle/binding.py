@@ -77,6 +77,9 @@ def lib():
             "or_snappy_encode": (C.c_size_t, [u8p, C.c_size_t, u8p]),
             "or_snappy_decoded_len": (C.c_int, [u8p, C.c_size_t, u64p, C.POINTER(C.c_int)]),
             "or_snappy_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t]),
+            "or_xxh32": (C.c_uint32, [u8p, C.c_size_t, C.c_uint32]),
+            "or_lz4_frame_len": (C.c_int, [u8p, C.c_size_t, u64p]),
+            "or_lz4_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, szp]),
             "or_v0_size": (C.c_size_t, [C.POINTER(RowValue)]),
             "or_v0_encode": (C.c_size_t, [C.POINTER(RowValue), u8p]),
             "or_v0_decode": (C.c_int, [u8p, C.c_size_t, C.c_long, C.POINTER(RowValue)]),
@@ -183,6 +186,22 @@ def snappy_decode(src: bytes) -> tuple[int, bytes]:
     out = np.zeros(max(dl.value, 1), np.uint8)
     st = lib().or_snappy_decode(p, len(src), out.ctypes.data_as(u8p), dl.value)
     return st, (out[:dl.value].tobytes() if st == 0 else b"")
+
+
+def xxh32(src: bytes, seed: int = 0) -> int:
+    h, p = _buf(src)
+    return lib().or_xxh32(p, len(src), seed)
+
+
+def lz4_decode(src: bytes) -> tuple[int, bytes]:
+    """compress.Decode(CodecLz4): (status, decoded bytes) - the frame decoded in order."""
+    h, p = _buf(src)
+    dl = C.c_uint64()
+    lib().or_lz4_frame_len(p, len(src), C.byref(dl))
+    out = np.zeros(max(dl.value, 1), np.uint8)
+    n = C.c_size_t()
+    st = lib().or_lz4_decode(p, len(src), out.ctypes.data_as(u8p), dl.value, C.byref(n))
+    return st, (out[:n.value].tobytes() if st == 0 else b"")
 
 
 @dataclass

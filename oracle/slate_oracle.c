@@ -27,6 +27,11 @@ const char* or_status_string(int s) {
     case OR_E_SNAPPY_CORRUPT: return "snappy: corrupt input";
     case OR_E_SNAPPY_TOO_LARGE: return "snappy: decoded block is too large";
     case OR_E_CODEC_UNSUPPORTED: return "compression codec not supported by this backend";
+    case OR_E_LZ4_MAGIC: return "lz4: bad magic number";
+    case OR_E_LZ4_HEADER_CHECKSUM: return "lz4: invalid header checksum";
+    case OR_E_LZ4_BLOCK_CHECKSUM: return "lz4: invalid block checksum";
+    case OR_E_LZ4_FRAME_CHECKSUM: return "lz4: invalid frame checksum";
+    case OR_E_LZ4_CORRUPT: return "lz4: invalid source or destination buffer too short";
     case OR_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case OR_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case OR_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";
@@ -285,6 +290,152 @@ int or_snappy_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_len)
   return sn_decode(dst, (size_t)dl, src + hdr, n - (size_t)hdr) ? OR_E_SNAPPY_CORRUPT : OR_OK;
 }
 
+/* ============================================================ LZ4 frame decode
+ * compress.Decode CodecLz4 = io.ReadAll(lz4.NewReader(buf)) (compression.go:143-144) with
+ * github.com/pierrec/lz4/v4 v4.1.21 (go.mod:13), absent here: restated from the LZ4 frame
+ * format (v1.6.x) and block format specifications, which that reader implements, plus
+ * XXH32 (the frame's header / block / content checksums).  Parity is pinned by frames
+ * from liblz4 1.9.3 (tests/golden/lz4_frames.json, tests/golden/make_lz4_fixtures.py);
+ * pierrec's exact error strings and its handling of trailing data are unpinned: one frame
+ * per buffer, anything after it is corrupt. */
+static const uint32_t XP1 = 2654435761u, XP2 = 2246822519u, XP3 = 3266489917u, XP4 = 668265263u,
+                      XP5 = 374761393u;
+static uint32_t xrotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+uint32_t or_xxh32(const uint8_t* p, size_t n, uint32_t seed) {
+  size_t i = 0;
+  uint32_t h;
+  if (n >= 16) {
+    uint32_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+    for (; i + 16 <= n; i += 16) {
+      v1 = xrotl(v1 + le32(p + i) * XP2, 13) * XP1;
+      v2 = xrotl(v2 + le32(p + i + 4) * XP2, 13) * XP1;
+      v3 = xrotl(v3 + le32(p + i + 8) * XP2, 13) * XP1;
+      v4 = xrotl(v4 + le32(p + i + 12) * XP2, 13) * XP1;
+    }
+    h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+  } else {
+    h = seed + XP5;
+  }
+  h += (uint32_t)n;
+  for (; i + 4 <= n; i += 4) h = xrotl(h + le32(p + i) * XP3, 17) * XP4;
+  for (; i < n; i++) h = xrotl(h + p[i] * XP5, 11) * XP1;
+  h ^= h >> 15; h *= XP2; h ^= h >> 13; h *= XP3; h ^= h >> 16;
+  return h;
+}
+
+/* One LZ4 block (sequences) into out[d0..): matches may reach back to out[lo].  `limit`
+ * bounds the block's decoded size (the frame's max block size), `cap` the buffer.
+ * out == NULL: sizes only. */
+static int lz4_block(const uint8_t* src, size_t sn, uint8_t* out, size_t d0, size_t lo, size_t cap, size_t limit,
+                     size_t* d_end) {
+  size_t s = 0, d = d0;
+  for (;;) {
+    if (s >= sn) return OR_E_LZ4_CORRUPT;
+    uint32_t token = src[s++];
+    size_t ll = token >> 4;
+    if (ll == 15) {
+      uint32_t b;
+      do {
+        if (s >= sn) return OR_E_LZ4_CORRUPT;
+        b = src[s++];
+        ll += b;
+      } while (b == 255);
+    }
+    if (ll > sn - s || ll > limit - (d - d0) || ll > cap - d) return OR_E_LZ4_CORRUPT;
+    if (out) memcpy(out + d, src + s, ll);
+    s += ll;
+    d += ll;
+    if (s == sn) break; /* the last sequence has literals only */
+    if (sn - s < 2) return OR_E_LZ4_CORRUPT;
+    size_t off = src[s] | (size_t)src[s + 1] << 8;
+    s += 2;
+    if (off == 0 || off > d - lo) return OR_E_LZ4_CORRUPT;
+    size_t ml = token & 15;
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (s >= sn) return OR_E_LZ4_CORRUPT;
+        b = src[s++];
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (ml > limit - (d - d0) || ml > cap - d) return OR_E_LZ4_CORRUPT;
+    if (out)
+      for (size_t j = 0; j < ml; j++) out[d + j] = out[d - off + j]; /* overlapping copies repeat */
+    d += ml;
+  }
+  *d_end = d;
+  return OR_OK;
+}
+
+/* The frame, decoded in order.  out == NULL: structure only (no checksums), and *out_len is
+ * the decoded size of the blocks before the first structural error (what a sequential
+ * decoder writes before it can fail): the plan sizes buffers with it. */
+static int lz4_frame(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  *out_len = 0;
+  if (n < 4) return OR_E_LZ4_CORRUPT;
+  if (le32(in) != 0x184D2204u) return OR_E_LZ4_MAGIC;
+  if (n < 7) return OR_E_LZ4_CORRUPT;
+  const uint32_t flg = in[4], bd = in[5];
+  if ((flg >> 6) != 1 || (flg & 2) || (bd & 0x8F)) return OR_E_LZ4_CORRUPT;
+  const uint32_t bsid = (bd >> 4) & 7;
+  if (bsid < 4) return OR_E_LZ4_CORRUPT;
+  const size_t bmax = (size_t)1 << (8 + 2 * bsid); /* 4: 64 KiB ... 7: 4 MiB */
+  const int indep = (flg >> 5) & 1, bcheck = (flg >> 4) & 1, csize = (flg >> 3) & 1, ccheck = (flg >> 2) & 1,
+            dict = flg & 1;
+  const size_t hl = 2 + (csize ? 8 : 0) + (dict ? 4 : 0);
+  if (n < 4 + hl + 1) return OR_E_LZ4_CORRUPT;
+  if (out && in[4 + hl] != ((or_xxh32(in + 4, hl, 0) >> 8) & 0xFF)) return OR_E_LZ4_HEADER_CHECKSUM;
+  if (dict) return OR_E_LZ4_CORRUPT; /* no dictionaries are configured */
+  uint64_t content = 0;
+  if (csize)
+    for (int k = 7; k >= 0; k--) content = (content << 8) | in[6 + k];
+  size_t pos = 4 + hl + 1, d = 0;
+  for (;;) {
+    if (n - pos < 4) return OR_E_LZ4_CORRUPT;
+    const uint32_t bs = le32(in + pos);
+    pos += 4;
+    if (bs == 0) break;
+    const size_t sz = bs & 0x7FFFFFFFu;
+    if (sz > bmax || n - pos < sz + (bcheck ? 4 : 0)) return OR_E_LZ4_CORRUPT;
+    if (out && bcheck && or_xxh32(in + pos, sz, 0) != le32(in + pos + sz)) return OR_E_LZ4_BLOCK_CHECKSUM;
+    if (bs >> 31) {
+      if (sz > cap - d) return OR_E_LZ4_CORRUPT;
+      if (out) memcpy(out + d, in + pos, sz);
+      d += sz;
+    } else {
+      size_t e;
+      int st = lz4_block(in + pos, sz, out, d, indep ? d : 0, cap, bmax, &e);
+      if (st) return st;
+      d = e;
+    }
+    *out_len = d;
+    pos += sz + (bcheck ? 4 : 0);
+  }
+  if (ccheck) {
+    if (n - pos < 4) return OR_E_LZ4_CORRUPT;
+    if (out && or_xxh32(out, d, 0) != le32(in + pos)) return OR_E_LZ4_FRAME_CHECKSUM;
+    pos += 4;
+  }
+  if (csize && content != d) return OR_E_LZ4_CORRUPT;
+  if (pos != n) return OR_E_LZ4_CORRUPT;
+  return OR_OK;
+}
+
+int or_lz4_frame_len(const uint8_t* in, size_t n, uint64_t* dlen) {
+  size_t l;
+  int st = lz4_frame(in, n, NULL, (size_t)-1, &l);
+  *dlen = l;
+  return st;
+}
+
+int or_lz4_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  uint8_t dummy;
+  return lz4_frame(in, n, out ? out : &dummy, out ? cap : 0, out_len);
+}
+
 /* ================================================ compress (compression.go) */
 int or_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
   if (codec == OR_CODEC_NONE) {
@@ -302,11 +453,13 @@ int or_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap
 int or_decompress_len(int codec, const uint8_t* in, size_t n, uint64_t* dlen) {
   if (codec == OR_CODEC_NONE) { *dlen = n; return OR_OK; }
   if (codec == OR_CODEC_SNAPPY) { int hdr; return or_snappy_decoded_len(in, n, dlen, &hdr); }
+  if (codec == OR_CODEC_LZ4) return or_lz4_frame_len(in, n, dlen);
   if (codec >= OR_CODEC_ZLIB && codec <= OR_CODEC_ZSTD) return OR_E_CODEC_UNSUPPORTED;
   return OR_E_INVALID_CODEC;
 }
 
 int or_decompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  if (codec == OR_CODEC_LZ4) return or_lz4_decode(in, n, out, cap, out_len); /* sequential: first error wins */
   uint64_t dl;
   int st = or_decompress_len(codec, in, n, &dl);
   if (st) return st;
@@ -588,7 +741,7 @@ int or_block_decode_batch(int codec, const uint8_t* in, const uint64_t* in_off, 
   for (uint32_t i = 0; i < n; i++) {
     size_t len = in_off[i + 1] - in_off[i];
     uint64_t dl = 0;
-    if (len >= 6 && or_decompress_len(codec, in + in_off[i], len - 4, &dl) != OR_OK) dl = 0;
+    if (len >= 6 && or_decompress_len(codec, in + in_off[i], len - 4, &dl) != OR_OK && codec != OR_CODEC_LZ4) dl = 0;
     if (codec == OR_CODEC_SNAPPY && dl > 22ull * (len - 4)) dl = 0; /* provably corrupt (> 64/3 expansion) */
     out_off[i] = o; row_base[i] = r;
     o += (dl + 15) & ~15ull; r += or_row_capacity(dl); /* 16-byte aligned blocks, as the GPU plan */

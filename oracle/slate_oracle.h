@@ -35,6 +35,8 @@ enum {
   OR_E_BLOCK_FIRSTKEY_PANIC = 7, OR_E_BLOCK_EMPTY = 8,
   OR_E_INVALID_CODEC = 10, OR_E_SNAPPY_CORRUPT = 11, OR_E_SNAPPY_TOO_LARGE = 12,
   OR_E_CODEC_UNSUPPORTED = 13,
+  OR_E_LZ4_MAGIC = 14, OR_E_LZ4_HEADER_CHECKSUM = 15, OR_E_LZ4_BLOCK_CHECKSUM = 16,
+  OR_E_LZ4_FRAME_CHECKSUM = 17, OR_E_LZ4_CORRUPT = 18,
   OR_E_ROW_TOO_SHORT = 20, OR_E_ROW_PREFIX = 21, OR_E_ROW_SUFFIX = 22, OR_E_ROW_EXPIRE = 23,
   OR_E_ROW_CREATE = 24, OR_E_ROW_VALUE_LEN = 25, OR_E_ROW_VALUE = 26, OR_E_ROW_PANIC = 27,
   OR_E_ROW_PEEK_SHORT = 28, OR_E_ROW_OFFSET_RANGE = 29,
@@ -72,6 +74,9 @@ int or_snappy_decode(const uint8_t* src, size_t n, uint8_t* dst, size_t dst_len)
 /* compress.Encode/Decode (compression.go:80,126); out must hold the result.
  * Decode writes *out_len; for NONE it copies. */
 int or_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+uint32_t or_xxh32(const uint8_t* p, size_t n, uint32_t seed);
+int or_lz4_frame_len(const uint8_t* in, size_t n, uint64_t* dlen);
+int or_lz4_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 int or_decompress_len(int codec, const uint8_t* in, size_t n, uint64_t* dlen);
 int or_decompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 
