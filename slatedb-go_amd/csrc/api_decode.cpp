@@ -27,6 +27,11 @@ const char* slate_status_string(int s) {
     case SLATE_E_SNAPPY_CORRUPT: return "snappy: corrupt input";
     case SLATE_E_SNAPPY_TOO_LARGE: return "snappy: decoded block is too large";
     case SLATE_E_CODEC_UNSUPPORTED: return "compression codec not supported by this backend";
+    case SLATE_E_LZ4_MAGIC: return "lz4: bad magic number";
+    case SLATE_E_LZ4_HEADER_CHECKSUM: return "lz4: invalid header checksum";
+    case SLATE_E_LZ4_BLOCK_CHECKSUM: return "lz4: invalid block checksum";
+    case SLATE_E_LZ4_FRAME_CHECKSUM: return "lz4: invalid frame checksum";
+    case SLATE_E_LZ4_CORRUPT: return "lz4: invalid source or destination buffer too short";
     case SLATE_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case SLATE_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case SLATE_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";

@@ -51,6 +51,95 @@ __device__ inline bool snappy_header(const uint8_t* p, uint64_t n, uint64_t* dle
   return false;
 }
 
+// ------------------------------------------------------------------- LZ4
+// compress.Decode CodecLz4 = io.ReadAll(lz4.NewReader(buf)) (compression.go:143-144), the
+// LZ4 frame format read in order; oracle/slate_oracle.c lz4_frame is the restatement this
+// follows step for step (same checks, same order, same status codes).
+constexpr uint32_t kLz4Magic = 0x184D2204u;
+__device__ inline uint32_t ld_le32(const uint8_t* p) {
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+struct Lz4Hdr {
+  int status;
+  uint32_t flg, hl;  // FLG byte, descriptor length (FLG .. DictID)
+  uint64_t bmax, content;
+};
+__device__ inline Lz4Hdr lz4_header(const uint8_t* in, uint64_t n) {
+  Lz4Hdr h{SLATE_OK, 0, 0, 0, 0};
+  if (n < 4) { h.status = SLATE_E_LZ4_CORRUPT; return h; }
+  if (ld_le32(in) != kLz4Magic) { h.status = SLATE_E_LZ4_MAGIC; return h; }
+  if (n < 7) { h.status = SLATE_E_LZ4_CORRUPT; return h; }
+  const uint32_t flg = in[4], bd = in[5];
+  if ((flg >> 6) != 1 || (flg & 2) || (bd & 0x8F) || ((bd >> 4) & 7) < 4) { h.status = SLATE_E_LZ4_CORRUPT; return h; }
+  h.flg = flg;
+  h.bmax = uint64_t(1) << (8 + 2 * ((bd >> 4) & 7));
+  h.hl = 2 + ((flg & 8) ? 8 : 0) + ((flg & 1) ? 4 : 0);
+  if (n < 4 + h.hl + 1) { h.status = SLATE_E_LZ4_CORRUPT; return h; }
+  if (flg & 8)
+    for (int k = 7; k >= 0; k--) h.content = (h.content << 8) | in[6 + k];
+  return h;
+}
+// Structure-only pass (no checksums): the decoded size of the blocks before the first
+// structural error, which is what the in-order decoder can write before it fails.
+__device__ inline void lz4_frame_len(const uint8_t* in, uint64_t n, uint64_t* dl) {
+  *dl = 0;
+  const Lz4Hdr h = lz4_header(in, n);
+  if (h.status != SLATE_OK || (h.flg & 1)) return;
+  const bool indep = (h.flg >> 5) & 1, bcheck = (h.flg >> 4) & 1;
+  uint64_t pos = 4 + h.hl + 1, d = 0;
+  for (;;) {
+    if (n - pos < 4) return;
+    const uint32_t bs = ld_le32(in + pos);
+    pos += 4;
+    if (bs == 0) return;
+    const uint64_t sz = bs & 0x7FFFFFFFu;
+    if (sz > h.bmax || n - pos < sz + (bcheck ? 4 : 0)) return;
+    if (bs >> 31) {
+      d += sz;
+    } else {
+      const uint8_t* src = in + pos;
+      uint64_t s = 0, bd = 0;
+      const uint64_t lo = indep ? d : 0;
+      for (;;) {
+        if (s >= sz) return;
+        const uint32_t token = src[s++];
+        uint64_t ll = token >> 4;
+        if (ll == 15) {
+          uint32_t b;
+          do {
+            if (s >= sz) return;
+            b = src[s++];
+            ll += b;
+          } while (b == 255);
+        }
+        if (ll > sz - s || ll > h.bmax - bd) return;
+        s += ll;
+        bd += ll;
+        if (s == sz) break;
+        if (sz - s < 2) return;
+        const uint64_t off = src[s] | uint64_t(src[s + 1]) << 8;
+        s += 2;
+        if (off == 0 || off > d + bd - lo) return;
+        uint64_t ml = token & 15;
+        if (ml == 15) {
+          uint32_t b;
+          do {
+            if (s >= sz) return;
+            b = src[s++];
+            ml += b;
+          } while (b == 255);
+        }
+        ml += 4;
+        if (ml > h.bmax - bd) return;
+        bd += ml;
+      }
+      d += bd;
+    }
+    *dl = d;
+    pos += sz + (bcheck ? 4 : 0);
+  }
+}
+
 // Decoded length of a block: false when the block cannot decode (too small,
 // corrupt Snappy header, provably corrupt length, unsupported codec).
 __device__ inline bool decoded_len(int codec, const uint8_t* in, uint64_t len, uint64_t* dl, uint32_t* hdr) {
@@ -67,6 +156,10 @@ __device__ inline bool decoded_len(int codec, const uint8_t* in, uint64_t len, u
     if (!snappy_header(in, clen, &v, hdr)) return false;
     if (v > kSnappyMaxExpansion * clen) return false;
     *dl = v;
+    return true;
+  }
+  if (codec == SLATE_CODEC_LZ4) {  // the size the in-order decoder writes (even when it then fails)
+    lz4_frame_len(in, clen, dl);
     return true;
   }
   return false;
@@ -228,6 +321,126 @@ __device__ int wave_snappy_decode(const uint8_t* src, uint32_t sn, uint32_t s, u
   return d == dn ? SLATE_OK : SLATE_E_SNAPPY_CORRUPT;
 }
 
+// ------------------------------------------------------------- LZ4 decode
+// XXH32 (seed 0) of LDS bytes [off, off+n) of a 4-aligned buffer: lanes 0..3 run the four
+// stripe accumulators, the tail and the avalanche are wave-uniform.
+constexpr uint32_t kXP1 = 2654435761u, kXP2 = 2246822519u, kXP3 = 3266489917u, kXP4 = 668265263u,
+                   kXP5 = 374761393u;
+__device__ inline uint32_t xrotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ uint32_t wave_xxh32(const uint8_t* base, uint32_t off, uint32_t n, int lane) {
+  uint32_t h;
+  if (n >= 16) {
+    uint32_t v = lane == 0 ? kXP1 + kXP2 : (lane == 1 ? kXP2 : (lane == 2 ? 0u : 0u - kXP1));
+    const uint32_t stripes = n / 16;
+    if (lane < 4) {
+#pragma unroll 8
+      for (uint32_t i = 0; i < stripes; i++)
+        v = xrotl(v + lds_u32(base, int32_t(off + 16 * i + 4 * uint32_t(lane))) * kXP2, 13) * kXP1;
+    }
+    const uint32_t v1 = __builtin_amdgcn_readlane(v, 0), v2 = __builtin_amdgcn_readlane(v, 1),
+                   v3 = __builtin_amdgcn_readlane(v, 2), v4 = __builtin_amdgcn_readlane(v, 3);
+    h = xrotl(v1, 1) + xrotl(v2, 7) + xrotl(v3, 12) + xrotl(v4, 18);
+  } else {
+    h = kXP5;
+  }
+  h += n;
+  uint32_t i = n & ~15u;
+  for (; i + 4 <= n; i += 4) h = xrotl(h + __builtin_amdgcn_readfirstlane(lds_u32(base, int32_t(off + i))) * kXP3, 17) * kXP4;
+  for (; i < n; i++) h = xrotl(h + uint32_t(base[off + i]) * kXP5, 11) * kXP1;
+  h ^= h >> 15;
+  h *= kXP2;
+  h ^= h >> 13;
+  h *= kXP3;
+  h ^= h >> 16;
+  return __builtin_amdgcn_readfirstlane(h);
+}
+
+// The frame in LDS (in, n bytes; `base`/`off` address it for 4-aligned reads) decoded in
+// order into out[0, cap): wave-uniform parse, lane-parallel copies.  The checks and
+// their order are oracle/slate_oracle.c lz4_frame's.
+__device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, uint8_t* out, uint32_t cap, int lane,
+                               uint32_t* out_len) {
+  const uint8_t* in = base + off;
+  *out_len = 0;
+  const Lz4Hdr h = lz4_header(in, n);
+  if (h.status != SLATE_OK) return h.status;
+  if (in[4 + h.hl] != ((wave_xxh32(base, off + 4, h.hl, lane) >> 8) & 0xFF)) return SLATE_E_LZ4_HEADER_CHECKSUM;
+  if (h.flg & 1) return SLATE_E_LZ4_CORRUPT;  // no dictionaries are configured
+  const bool indep = (h.flg >> 5) & 1, bcheck = (h.flg >> 4) & 1, ccheck = (h.flg >> 2) & 1, csize = (h.flg >> 3) & 1;
+  uint32_t pos = 4 + h.hl + 1, d = 0;
+  for (;;) {
+    if (n - pos < 4) return SLATE_E_LZ4_CORRUPT;
+    const uint32_t bs = __builtin_amdgcn_readfirstlane(ld_le32(in + pos));
+    pos += 4;
+    if (bs == 0) break;
+    const uint32_t sz = bs & 0x7FFFFFFFu;
+    if (sz > h.bmax || n - pos < sz + (bcheck ? 4u : 0u)) return SLATE_E_LZ4_CORRUPT;
+    if (bcheck && wave_xxh32(base, off + pos, sz, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos + sz)))
+      return SLATE_E_LZ4_BLOCK_CHECKSUM;
+    const uint8_t* src = in + pos;
+    if (bs >> 31) {  // stored block
+      if (sz > cap - d) return SLATE_E_LZ4_CORRUPT;
+      for (uint32_t j = lane; j < sz; j += kWave) out[d + j] = src[j];
+      d += sz;
+    } else {
+      const uint32_t d0 = d, lo = indep ? d : 0u;
+      uint32_t s = 0;
+      for (;;) {
+        if (s >= sz) return SLATE_E_LZ4_CORRUPT;
+        const uint32_t token = __builtin_amdgcn_readfirstlane(src[s]);
+        s++;
+        uint32_t ll = token >> 4;
+        if (ll == 15) {
+          uint32_t b;
+          do {
+            if (s >= sz) return SLATE_E_LZ4_CORRUPT;
+            b = __builtin_amdgcn_readfirstlane(src[s]);
+            s++;
+            ll += b;
+          } while (b == 255);
+        }
+        if (ll > sz - s || ll > h.bmax - (d - d0) || ll > cap - d) return SLATE_E_LZ4_CORRUPT;
+        for (uint32_t j = lane; j < ll; j += kWave) out[d + j] = src[s + j];
+        s += ll;
+        d += ll;
+        if (s == sz) break;  // the last sequence has literals only
+        if (sz - s < 2) return SLATE_E_LZ4_CORRUPT;
+        const uint32_t mo = __builtin_amdgcn_readfirstlane(uint32_t(src[s]) | uint32_t(src[s + 1]) << 8);
+        s += 2;
+        if (mo == 0 || mo > d - lo) return SLATE_E_LZ4_CORRUPT;
+        uint32_t ml = token & 15;
+        if (ml == 15) {
+          uint32_t b;
+          do {
+            if (s >= sz) return SLATE_E_LZ4_CORRUPT;
+            b = __builtin_amdgcn_readfirstlane(src[s]);
+            s++;
+            ml += b;
+          } while (b == 255);
+        }
+        ml += 4;
+        if (ml > h.bmax - (d - d0) || ml > cap - d) return SLATE_E_LZ4_CORRUPT;
+        // byte j repeats the mo-byte pattern (overlapping copies); every read is below d
+        for (uint32_t j = lane; j < ml; j += kWave) out[d + j] = out[d - mo + (mo >= ml ? j : j % mo)];
+        d += ml;
+      }
+    }
+    *out_len = d;
+    pos += sz + (bcheck ? 4u : 0u);
+  }
+  if (ccheck) {
+    if (n - pos < 4) return SLATE_E_LZ4_CORRUPT;
+    __builtin_amdgcn_wave_barrier();
+    if (wave_xxh32(out, 0, d, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos)))
+      return SLATE_E_LZ4_FRAME_CHECKSUM;
+    pos += 4;
+  }
+  if (csize && h.content != d) return SLATE_E_LZ4_CORRUPT;
+  if (pos != n) return SLATE_E_LZ4_CORRUPT;
+  *out_len = d;
+  return SLATE_OK;
+}
+
 // ---------------------------------------------------------------- v0 rows
 // row.go:191-261 against firstKey of length fk (fk < 0: firstKey == nil).
 __device__ inline void decode_row(const uint8_t* data, uint32_t data_len, uint32_t off, int fk, slate_row& r,
@@ -299,7 +512,9 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   }
   uint32_t hdr = 0;
   uint64_t dl = 0;
-  const bool dl_ok = decoded_len(a.codec, gin, len, &dl, &hdr);
+  // LZ4: the plan's capacity (>= what the in-order decoder writes); others: the header
+  const bool dl_ok = a.codec == SLATE_CODEC_LZ4 ? (dl = a.out_off[b + 1] - a.out_off[b], true)
+                                                : decoded_len(a.codec, gin, len, &dl, &hdr);
   uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
   if (shift + len > w.in_cap || (a.codec != SLATE_CODEC_NONE && dl > w.out_cap)) {
     if (defer_large) return false;
@@ -344,8 +559,18 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     }
     buf = w.out;
     n = uint32_t(dl);
+  } else if (a.codec == SLATE_CODEC_LZ4) {
+    uint32_t outn = 0;
+    int st = wave_lz4_decode(w.in, shift, clen, w.out, uint32_t(dl), lane, &outn);
+    if (st != SLATE_OK) {
+      m.status = int16_t(st);
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    buf = w.out;
+    n = outn;
   } else {
-    m.status = (a.codec >= SLATE_CODEC_ZLIB && a.codec <= SLATE_CODEC_ZSTD) ? SLATE_E_CODEC_UNSUPPORTED
+    m.status = (a.codec == SLATE_CODEC_ZLIB || a.codec == SLATE_CODEC_ZSTD) ? SLATE_E_CODEC_UNSUPPORTED
                                                                                : SLATE_E_INVALID_CODEC;
     write_meta(&a.meta[b], m, lane);
     return true;

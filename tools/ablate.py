@@ -21,8 +21,8 @@ from tools import workload as wl  # noqa: E402
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000
     modes = [int(x, 0) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "4", "8", "15"])]
-    codec = sc.SNAPPY
-    blob, in_off, dec_bytes = wl.snappy_vhalf(n)
+    codec = int(os.environ.get("SLATE_ABLATE_CODEC", sc.SNAPPY))  # 3: LZ4 frames
+    blob, in_off, dec_bytes = wl.snappy_vhalf(n, codec=codec)
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
     ctx = sc.Context(0)

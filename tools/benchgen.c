@@ -1,7 +1,7 @@
 /* Bench input tooling (not product, not oracle): compress a batch of decoded
- * blocks with the C++ snappy library in /opt/conda (dlopen) and append the
- * block CRC32 trailer (block.go:54-75 layout), in parallel.  Used only to
- * synthesise encoded Snappy blocks for bench.py's workload. */
+ * blocks with the C++ snappy library or liblz4's frame API in /opt/conda (dlopen)
+ * and append the block CRC32 trailer (block.go:54-75 layout), in parallel.  Used
+ * only to synthesise encoded blocks for bench.py's and tools/ablate.py's workloads. */
 #include <dlfcn.h>
 #include <pthread.h>
 #include <stddef.h>
@@ -11,6 +11,27 @@
 
 typedef int (*compress_fn)(const char*, size_t, char*, size_t*);
 static compress_fn g_compress;
+/* LZ4F_preferences_t of lz4frame.h 1.9.x */
+typedef struct {
+  int blockSizeID, blockMode, contentChecksumFlag, frameType;
+  unsigned long long contentSize;
+  unsigned dictID;
+  int blockChecksumFlag, compressionLevel;
+  unsigned autoFlush, favorDecSpeed, reserved[3];
+} lz4f_prefs;
+typedef size_t (*lz4f_fn)(void*, size_t, const void*, size_t, const lz4f_prefs*);
+typedef unsigned (*lz4f_err_fn)(size_t);
+static lz4f_fn g_lz4f;
+static lz4f_err_fn g_lz4f_err;
+
+/* pierrec/lz4 v4 writer defaults: 4 MiB max blocks, independent blocks, content checksum */
+int bg_init_lz4(const char* liblz4) {
+  void* h = dlopen(liblz4, RTLD_NOW);
+  if (!h) return -1;
+  g_lz4f = (lz4f_fn)dlsym(h, "LZ4F_compressFrame");
+  g_lz4f_err = (lz4f_err_fn)dlsym(h, "LZ4F_isError");
+  return (g_lz4f && g_lz4f_err) ? 0 : -2;
+}
 static uint32_t g_tab[256];
 
 static uint32_t crc32(const uint8_t* p, size_t n) {
@@ -44,6 +65,15 @@ static void* work(void* arg) {
     uint8_t* d = j->dst + i * j->stride;
     size_t cl = j->stride - 4;
     if (j->codec == 0) { memcpy(d, s, n); cl = n; }
+    else if (j->codec == 3) {
+      lz4f_prefs p;
+      memset(&p, 0, sizeof p);
+      p.blockSizeID = 7;
+      p.contentChecksumFlag = 1;
+      size_t r = g_lz4f(d, j->stride - 4, s, n, &p);
+      if (g_lz4f_err(r)) { j->rc = -4; return NULL; }
+      cl = r;
+    }
     else if (g_compress((const char*)s, n, (char*)d, &cl) != 0) { j->rc = -3; return NULL; }
     uint32_t c = crc32(d, cl);
     d[cl] = (uint8_t)(c >> 24); d[cl + 1] = (uint8_t)(c >> 16); d[cl + 2] = (uint8_t)(c >> 8); d[cl + 3] = (uint8_t)c;

@@ -1,7 +1,7 @@
 """Synthetic SST-block workloads for bench.py, built with
 tools/benchgen.c: keys b"k%015d", 84-byte values (V-half r||r from
 numpy.random.default_rng(20250307), or V-rand), BlockSize 4096, then Snappy
-(C++ libsnappy from /opt/conda) or None, plus the block CRC32 trailer."""
+(C++ libsnappy from /opt/conda), LZ4 frames (liblz4) or None, plus the block CRC32 trailer."""
 from __future__ import annotations
 
 import ctypes as C
@@ -13,6 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libbenchgen.so")
 LIBSNAPPY = "/opt/conda/lib/libsnappy.so.1"
+LIBLZ4 = "/opt/conda/lib/liblz4.so.1"
 
 _lib = None
 
@@ -33,6 +34,8 @@ def lib():
         rc = L.bg_init(LIBSNAPPY.encode())
         if rc != 0:
             raise RuntimeError(f"benchgen: cannot load {LIBSNAPPY} ({rc})")
+        L.bg_init_lz4.argtypes = [C.c_char_p]
+        L.bg_init_lz4(LIBLZ4.encode())  # codec 3 (LZ4 frames) only: optional
         _lib = L
     return _lib
 
