@@ -206,8 +206,12 @@ __device__ __forceinline__ void store_win(uint8_t* ring, uint32_t a4, const Win5
   wr32(ring, a4 + 12, w.y3);
   wr32(ring, a4 + 16, w.y4);
 }
+// dword j (0..4) of the window, as bit-tested selects: an equality chain became a
+// branch tree of divergent if-blocks
 __device__ __forceinline__ uint32_t pick5(const Win5& w, uint32_t j) {
-  return j == 0 ? w.y0 : j == 1 ? w.y1 : j == 2 ? w.y2 : j == 3 ? w.y3 : w.y4;
+  const uint32_t a = (j & 1) ? w.y1 : w.y0, b = (j & 1) ? w.y3 : w.y2;
+  const uint32_t r = (j & 2) ? b : a;
+  return (j & 4) ? w.y4 : r;
 }
 
 // Cache policy (gfx950 CPol bits): 0 = default (allocates in L2: a lane reads its block's 128-byte
@@ -370,8 +374,8 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   // row.go:203-206: a prefix longer than the block's first key fails the row, which then
   // keeps only its key lengths; row 0 is decoded against an empty first key
   const bool pfail = L.rpl > uint32_t(max(L.fk, 0));
-  row = pfail ? pack_row(L.R, L.rpl, L.rsl, 0, 0, 0, uint32_t(SLATE_E_ROW_PREFIX))
-              : pack_row(L.R, L.rpl, L.rsl, vl, flags & 7, rlen - 4 - L.rsl, SLATE_OK);
+  row = pack_row(L.R, L.rpl, L.rsl, pfail ? 0u : vl, pfail ? 0u : flags & 7, pfail ? 0u : rlen - 4 - L.rsl,
+                 pfail ? uint32_t(SLATE_E_ROW_PREFIX) : uint32_t(SLATE_OK));
   ridx = L.nwalk;
   L.fk = (done && L.nwalk == 0 && !pfail) ? int32_t(L.rsl) : L.fk;
   const bool emit = done && L.nwalk < L.rcap;
@@ -388,12 +392,18 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   const bool stop = (wa && lost) || (done && next > L.dn);
   const bool adv = done && next <= L.dn;
   L.R = adv ? uint32_t(next) : L.R;
-  L.rphase = stop ? 3u : (adv ? 0u : (to1 ? 1u : (to2 ? 2u : L.rphase)));
-  L.rneed = stop ? 0xFFFFFFFFu
-            : adv ? uint32_t(next) + 4
-            : to1 ? L.R + 4 + sl0 + 13
-            : to2 ? L.R + ro1 + 4
-                  : L.rneed;
+  // priority stop > adv > to1 > to2, as plain selects (nested ternaries became branches)
+  uint32_t rph = L.rphase, rn = L.rneed;
+  rph = to2 ? 2u : rph;
+  rn = to2 ? L.R + ro1 + 4 : rn;
+  rph = to1 ? 1u : rph;
+  rn = to1 ? L.R + 4 + sl0 + 13 : rn;
+  rph = adv ? 0u : rph;
+  rn = adv ? uint32_t(next) + 4 : rn;
+  rph = stop ? 3u : rph;
+  rn = stop ? 0xFFFFFFFFu : rn;
+  L.rphase = rph;
+  L.rneed = rn;
   return emit;
 }
 
@@ -485,7 +495,7 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     // throttle (a hole delays the flush): after any step d - 16*fl <= 96, so the ring keeps
     // every unflushed byte and every far source (offset > 112) is already flushed
     const bool room_out = L.d - 16 * L.fl <= kUnflushed;
-    const bool can = need && L.s < sn && avail >= int32_t(min(L.s + 5, sn)) && room_out;
+    const bool can = need & (L.s < sn) & (avail >= int32_t(min(L.s + 5, sn))) & room_out;
     const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
     const uint32_t c = w.x & 0xff, t = c & 3;
     const uint32_t b14 = (w.x >> 8) | (w.y << 24);  // bytes s+1 .. s+4
@@ -493,9 +503,12 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     const uint32_t nb = xl >= 60 ? xl - 59 : 0;
     const uint32_t ext = nb >= 4 ? b14 : (b14 & ((1u << (8 * nb)) - 1));
     const uint64_t lit_len = uint64_t(nb ? ext : xl) + 1;
-    const uint32_t cp_len = t == 1 ? 4 + ((c >> 2) & 7) : 1 + (c >> 2);
-    const uint32_t cp_off = t == 1 ? (((c & 0xe0) << 3) | (b14 & 0xff)) : (t == 2 ? (b14 & 0xffff) : b14);
-    const uint32_t hl = t == 0 ? 1 + nb : (t == 1 ? 2 : (t == 2 ? 3 : 5));
+    // selects on the tag's bits (equality chains on t became branch trees)
+    const uint32_t cp_len = (t == 1) ? 4 + ((c >> 2) & 7) : 1 + (c >> 2);
+    const uint32_t off1 = ((c & 0xe0) << 3) | (b14 & 0xff), off2 = b14 & 0xffff;
+    const uint32_t cp_off = (t & 2) ? ((t & 1) ? b14 : off2) : off1;
+    const uint32_t hl_cp = (t & 2) ? ((t & 1) ? 5u : 3u) : 2u;
+    const uint32_t hl = (t == 0) ? 1 + nb : hl_cp;
     const uint32_t s1 = L.s + hl;
     const bool bad_lit = lit_len > uint64_t(L.dn - L.d) || lit_len > uint64_t(sn - min(s1, sn));
     const bool bad_cp = cp_off == 0 || L.d < cp_off || cp_len > L.dn - L.d;
@@ -524,7 +537,12 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
   {
     const bool cp = act && !L.dd && L.rem != 0;
     uint32_t k = min(L.rem, 16u);
-    k = L.lit ? min(k, uint32_t(max(avail - int32_t(L.src), 0))) : (L.far ? (L.fready ? k : 0u) : min(k, L.eff));
+    {
+      const uint32_t k_lit = min(k, uint32_t(max(avail - int32_t(L.src), 0)));
+      const uint32_t k_far = L.fready ? k : 0u, k_near = min(k, L.eff);
+      const uint32_t k_cp = L.far ? k_far : k_near;
+      k = L.lit ? k_lit : k_cp;
+    }
     // a ring copy stops short of the pending hole's bytes
     const bool near = !L.lit && !L.far;
     if (near && L.hpend && L.src < L.hd + L.hl && L.src + k > L.hd) k = L.src < L.hd ? L.hd - L.src : 0u;
