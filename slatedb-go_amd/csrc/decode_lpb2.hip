@@ -722,7 +722,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     }
 
     // ---------------- streaming decode, 64 blocks in lockstep
-    uint32_t iters = 0;
+    uint32_t iters = 0, fin_iter = 0;
     const uint64_t t_round = (a.debug & 512) ? __builtin_amdgcn_s_memtime() : 0;
     // a lane is done when its decode is finished, no hole is pending, and every chunk
     // is committed and in the CRC.  Every step consumes input, produces output or waits
@@ -766,6 +766,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
       L.qoff = kOOB;
       flush_iteration(L, act, outs, lane, R, a.debug);
       iters++;
+      fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
     }
     const uint32_t round_cycles = (a.debug & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
 
@@ -936,6 +937,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         reinterpret_cast<v4u*>(grows)[i] = r;
       }
     }
+    if (a.debug & 131072) m.detail = int32_t(fin_iter);  // profiling only: results are wrong by design
     if (have) a.meta[b] = m;
     if ((a.debug & 512) && lane == 0 && round0 + 1 < a.n) {
       // profiling only: loop iterations and cycles of this round, in meta.detail of its first two blocks

@@ -152,7 +152,10 @@ class Context:
             self._h = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (TypeError, AttributeError):  # interpreter shutdown: module globals already gone
+            pass
 
     @property
     def handle(self):
