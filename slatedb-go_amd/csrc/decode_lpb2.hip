@@ -345,61 +345,97 @@ __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint
   L.crc_pos += go ? 1u : 0u;
 }
 
-// Row walker, one action per call (row.go:191-261 field order), branch-free.
+// ring bytes [p, p+24)
+struct W6 {
+  uint32_t w[6];
+};
+__device__ __forceinline__ W6 ring_rd24(const uint8_t* ring, uint32_t p) {
+  const uint32_t a = p & (kOR - 8);
+  const v2u A = rd64(ring, a), B = rd64(ring, a + 8), C = rd64(ring, a + 16), D = rd64(ring, a + 24);
+  const bool q = (p & 4) != 0;
+  const uint32_t e[7] = {q ? A.y : A.x, q ? B.x : A.y, q ? B.y : B.x, q ? C.x : B.y,
+                         q ? C.y : C.x, q ? D.x : C.y, q ? D.y : D.x};
+  const uint32_t b = p & 3;
+  W6 r;
+#pragma unroll
+  for (int k = 0; k < 6; k++) r.w[k] = alignb(e[k + 1], e[k], b);
+  return r;
+}
+
+// Row walker, one action per call (row.go:191-261 field order), branch-free.  A row whose
+// header, flags and value length lie in its first 24 bytes (suffix <= 7 bytes, no
+// timestamps: every row of the bench's blocks) is decoded in one action; otherwise phase 0
+// reads the key lengths, phase 1 the flags (+ the value length when there are no
+// timestamps), phase 2 the value length after the timestamps.
 // Returns true with `row`/`ridx` set when the action finished a row.
 __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
   const uint32_t fp = L.R + 4 + L.rsl + 8;
-  const uint32_t rpos = L.rphase == 0 ? L.R : (L.rphase == 1 ? fp : L.R + L.ro);
+  const bool p0 = L.rphase == 0, p1 = L.rphase == 1;
+  const uint32_t rpos = p0 ? L.R : (p1 ? fp : L.R + L.ro);
   const bool in_hole = L.hpend && rpos < L.hd + L.hl && rpos + 8 > L.hd;
-  const bool wa = act && L.rphase < 3 && L.d >= L.rneed && !in_hole;
+  const bool wa = act & (L.rphase < 3) & (L.d >= L.rneed) & !in_hole;
   const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
-  const v2u q = ring_rd8(ring, rpos);
-  // phase 0: prefix / suffix lengths
-  const uint32_t pl0 = be16_of(q.x), sl0 = be16_of(q.x >> 16);
+  const W6 q = ring_rd24(ring, rpos);
+  // phase 0: prefix / suffix lengths, and the whole row when it fits the first 24 bytes
+  const uint32_t pl0 = be16_of(q.w[0]), sl0 = be16_of(q.w[0] >> 16);
+  const uint32_t f0 = 12 + sl0;  // flags byte (12..19 when sl0 <= 7)
+  const bool hi0 = (f0 & 16) != 0;  // f0 in 16..19 (one-shot rows have f0 in 12..19)
+  const uint32_t fw = hi0 ? q.w[4] : q.w[3], fw1 = hi0 ? q.w[5] : q.w[4];
+  const uint32_t fl0 = (fw >> (8 * (f0 & 3))) & 0xff;
+  const uint32_t vb = (f0 + 1) & 3;  // the value length is bytes f0+1 .. f0+4
+  const uint32_t vl0 = __builtin_bswap32(vb == 0 ? fw1 : alignb(fw1, fw, vb));
+  const bool tomb0 = (fl0 & 1) != 0;
+  const uint32_t rlen0 = 4 + sl0 + 9 + (tomb0 ? 0u : 4u);
+  const bool hole0 = L.hpend && rpos < L.hd + L.hl && rpos + rlen0 > L.hd;
+  const bool one = p0 & (sl0 <= 7) & !(fl0 & 6) & (L.d >= L.R + rlen0) & !hole0;
   // phase 1: flags, and the value length right after them when there are no timestamps
-  const uint32_t fl1 = q.x & 0xff;
+  const uint32_t fl1 = q.w[0] & 0xff;
   const uint32_t ts = ((fl1 & 2) ? 8u : 0u) + ((fl1 & 4) ? 8u : 0u);
   const uint32_t ro1 = 4 + L.rsl + 9 + ts;
   const bool tomb = (fl1 & 1) != 0;
-  const bool done1 = tomb || ts == 0;
-  const uint32_t vl1 = tomb ? 0u : __builtin_bswap32((q.x >> 8) | (q.y << 24));
+  const bool done1 = tomb | (ts == 0);
+  const uint32_t vl1 = tomb ? 0u : __builtin_bswap32((q.w[0] >> 8) | (q.w[1] << 24));
   // phase 2: value length after the timestamps
-  const uint32_t vl2 = __builtin_bswap32(q.x);
-  const bool p0 = L.rphase == 0, p1 = L.rphase == 1;
-  const bool done = wa && !lost && ((p1 && done1) || L.rphase == 2);
-  const uint32_t vl = p1 ? vl1 : vl2;
-  const uint32_t flags = p1 ? fl1 : L.rflags;
+  const uint32_t vl2 = __builtin_bswap32(q.w[0]);
+  const bool done = wa & !lost & ((p0 & one) | (p1 & done1) | (L.rphase == 2));
+  const uint32_t vl_p12 = p1 ? vl1 : vl2;
+  const uint32_t vl = p0 ? (tomb0 ? 0u : vl0) : vl_p12;
+  const uint32_t fl_p12 = p1 ? fl1 : L.rflags;
+  const uint32_t flags = p0 ? fl0 : fl_p12;
   const uint32_t ro = p1 ? ro1 : L.ro;
-  const uint32_t rlen = (p1 && tomb) ? ro1 : ro + 4;
+  const uint32_t rlen_p12 = (p1 & tomb) ? ro1 : ro + 4;
+  const uint32_t rlen = p0 ? rlen0 : rlen_p12;
+  const uint32_t rpl = p0 ? pl0 : L.rpl, rsl = p0 ? sl0 : L.rsl;
   // row.go:203-206: a prefix longer than the block's first key fails the row, which then
   // keeps only its key lengths; row 0 is decoded against an empty first key
-  const bool pfail = L.rpl > uint32_t(max(L.fk, 0));
-  row = pack_row(L.R, L.rpl, L.rsl, pfail ? 0u : vl, pfail ? 0u : flags & 7, pfail ? 0u : rlen - 4 - L.rsl,
+  const bool pfail = rpl > uint32_t(max(L.fk, 0));
+  row = pack_row(L.R, rpl, rsl, pfail ? 0u : vl, pfail ? 0u : flags & 7, pfail ? 0u : rlen - 4 - rsl,
                  pfail ? uint32_t(SLATE_E_ROW_PREFIX) : uint32_t(SLATE_OK));
   ridx = L.nwalk;
-  L.fk = (done && L.nwalk == 0 && !pfail) ? int32_t(L.rsl) : L.fk;
-  const bool emit = done && L.nwalk < L.rcap;
+  L.fk = (done & (L.nwalk == 0) & !pfail) ? int32_t(rsl) : L.fk;
+  const bool emit = done & (L.nwalk < L.rcap);
   const uint64_t next = uint64_t(L.R) + rlen + vl;
   // state transitions
-  const bool to1 = wa && !lost && p0;
-  const bool to2 = wa && !lost && p1 && !done1;
+  const bool to1 = wa & !lost & p0 & !one;
+  const bool to2 = wa & !lost & p1 & !done1;
   L.rpl = to1 ? pl0 : L.rpl;
-  L.pl0 = (to1 && L.R == 0) ? pl0 : L.pl0;
+  L.pl0 = (wa & !lost & p0 & (L.R == 0)) ? pl0 : L.pl0;
   L.rsl = to1 ? sl0 : L.rsl;
-  L.rflags = (wa && p1) ? fl1 : L.rflags;
-  L.ro = (wa && p1) ? ro1 : L.ro;
+  L.rflags = (wa & p1) ? fl1 : L.rflags;
+  L.ro = (wa & p1) ? ro1 : L.ro;
   L.nwalk += done ? 1u : 0u;
-  const bool stop = (wa && lost) || (done && next > L.dn);
-  const bool adv = done && next <= L.dn;
+  const bool stop = (wa & lost) | (done & (next > L.dn));
+  const bool adv = done & (next <= L.dn);
   L.R = adv ? uint32_t(next) : L.R;
-  // priority stop > adv > to1 > to2, as plain selects (nested ternaries became branches)
+  // priority stop > adv > to1 > to2, as plain selects (nested ternaries became branches);
+  // phase 0 waits for 24 bytes (or the end of the block) so that it can finish the row
   uint32_t rph = L.rphase, rn = L.rneed;
   rph = to2 ? 2u : rph;
   rn = to2 ? L.R + ro1 + 4 : rn;
   rph = to1 ? 1u : rph;
   rn = to1 ? L.R + 4 + sl0 + 13 : rn;
   rph = adv ? 0u : rph;
-  rn = adv ? uint32_t(next) + 4 : rn;
+  rn = adv ? min(uint32_t(next) + 24, L.dn) : rn;
   rph = stop ? 3u : rph;
   rn = stop ? 0xFFFFFFFFu : rn;
   L.rphase = rph;
@@ -472,14 +508,15 @@ __device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q, v4u& FD, uint8
 
 // One step: CRC (two of four steps), parse, copy, the far-copy / hole load, and the row
 // walker (the other two steps).
-template <bool kWalkSlot>
+// kSlot: 0 and 2 absorb a CRC chunk; 1 and (when needed) 3 run the walker
+template <int kSlot>
 __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint8_t* ring,
                                           uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
   dbg = SLATE_FORCE_DBG;
 #endif
   // ---- CRC32 of one committed chunk (the two steps without the walker)
-  if (!kWalkSlot) {
+  if (kSlot == 0 || kSlot == 2) {
     const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
     if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
     else crc_chunk(L, in, tab, go);
@@ -569,7 +606,10 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
     L.qoff = hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : L.qoff);
     L.fpend = (wantf || hole_new) ? 1u : L.fpend;
-    if (kWalkSlot) {
+    // the walker: every iteration once, and a second time only when some lane's walker has
+    // fallen more than 64 bytes behind (rows shorter than the iteration's output)
+    if (kSlot == 1 ||
+        (kSlot == 3 && __builtin_amdgcn_ballot_w64(act & (L.rphase < 3) & (L.d >= L.rneed) & (L.d - L.R > 64)))) {
       v4u row;
       uint32_t ridx;
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
@@ -755,10 +795,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         L.n_req = n;
       }
       absorb_far(L, Q, FD, ring);
-      lane_step<false>(L, FD, act, ring, in, tab, R, a.debug);
-      lane_step<true>(L, FD, act, ring, in, tab, R, a.debug);
-      lane_step<false>(L, FD, act, ring, in, tab, R, a.debug);
-      lane_step<true>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<0>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<1>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<2>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<3>(L, FD, act, ring, in, tab, R, a.debug);
       // the far-copy / hole source requested in this iteration (at most one per lane; sc1:
       // L1 bypass), before the flush stores so that vmcnt waits stay static; it is merged
       // at the start of the next iteration
