@@ -378,6 +378,17 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
     if (bcheck && wave_xxh32(base, off + pos, sz, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos + sz)))
       return SLATE_E_LZ4_BLOCK_CHECKSUM;
     const uint8_t* src = in + pos;
+    // sequence headers are read through a 64-byte window held one byte per lane
+    // (v_readlane with a uniform index): one LDS round trip per 64 input bytes instead
+    // of one per header byte
+    uint32_t wbase = 0x80000000u, win = 0;  // p - wbase >= 64 for every p < 2^31: the first read loads
+    auto byte_at = [&](uint32_t p) -> uint32_t {  // src[p], p < sz (wave-uniform)
+      if (p - wbase >= uint32_t(kWave)) {
+        wbase = p;
+        win = (p + uint32_t(lane) < sz) ? uint32_t(src[p + lane]) : 0u;
+      }
+      return __builtin_amdgcn_readlane(win, int(p - wbase));
+    };
     if (bs >> 31) {  // stored block
       if (sz > cap - d) return SLATE_E_LZ4_CORRUPT;
       for (uint32_t j = lane; j < sz; j += kWave) out[d + j] = src[j];
@@ -387,14 +398,14 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
       uint32_t s = 0;
       for (;;) {
         if (s >= sz) return SLATE_E_LZ4_CORRUPT;
-        const uint32_t token = __builtin_amdgcn_readfirstlane(src[s]);
+        const uint32_t token = byte_at(s);
         s++;
         uint32_t ll = token >> 4;
         if (ll == 15) {
           uint32_t b;
           do {
             if (s >= sz) return SLATE_E_LZ4_CORRUPT;
-            b = __builtin_amdgcn_readfirstlane(src[s]);
+            b = byte_at(s);
             s++;
             ll += b;
           } while (b == 255);
@@ -405,7 +416,7 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
         d += ll;
         if (s == sz) break;  // the last sequence has literals only
         if (sz - s < 2) return SLATE_E_LZ4_CORRUPT;
-        const uint32_t mo = __builtin_amdgcn_readfirstlane(uint32_t(src[s]) | uint32_t(src[s + 1]) << 8);
+        const uint32_t mo = byte_at(s) | (byte_at(s + 1) << 8);
         s += 2;
         if (mo == 0 || mo > d - lo) return SLATE_E_LZ4_CORRUPT;
         uint32_t ml = token & 15;
@@ -413,7 +424,7 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
           uint32_t b;
           do {
             if (s >= sz) return SLATE_E_LZ4_CORRUPT;
-            b = __builtin_amdgcn_readfirstlane(src[s]);
+            b = byte_at(s);
             s++;
             ml += b;
           } while (b == 255);
@@ -421,7 +432,12 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
         ml += 4;
         if (ml > h.bmax - (d - d0) || ml > cap - d) return SLATE_E_LZ4_CORRUPT;
         // byte j repeats the mo-byte pattern (overlapping copies); every read is below d
-        for (uint32_t j = lane; j < ml; j += kWave) out[d + j] = out[d - mo + (mo >= ml ? j : j % mo)];
+        if (mo >= ml) {  // wave-uniform: no overlap, no modulo
+          if (uint32_t(lane) < ml) out[d + lane] = out[d - mo + lane];
+          for (uint32_t j = lane + kWave; j < ml; j += kWave) out[d + j] = out[d - mo + j];
+        } else {
+          for (uint32_t j = lane; j < ml; j += kWave) out[d + j] = out[d - mo + (j % mo)];
+        }
         d += ml;
       }
     }
@@ -561,7 +577,8 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     n = uint32_t(dl);
   } else if (a.codec == SLATE_CODEC_LZ4) {
     uint32_t outn = 0;
-    int st = wave_lz4_decode(w.in, shift, clen, w.out, uint32_t(dl), lane, &outn);
+    int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)  // profiling: skip the decompression
+                           : wave_lz4_decode(w.in, shift, clen, w.out, uint32_t(dl), lane, &outn);
     if (st != SLATE_OK) {
       m.status = int16_t(st);
       write_meta(&a.meta[b], m, lane);
