@@ -9,30 +9,31 @@
 // chain inside one block is serial).  A round (64 blocks) runs as iterations of four
 // steps; a step parses a tag if the previous one is used up and moves up to 16 bytes.
 //
-// Memory.  The decode is bound by the latency and the number of memory requests, not by
-// bytes, so every access is shaped for that (tools/scatter_probe.hip measured 16-byte
-// per-lane accesses at 3.5-8x the cost of 64-128-byte runs):
+// Memory.  Every global access is shaped for the number of requests, not bytes
+// (tools/scatter_probe.hip measured 16-byte per-lane accesses at 3.5-8x the cost of
+// 64-128-byte runs):
 //   * input: at the start of each iteration, four transposed loads fetch up to four new
 //     16-byte chunks per block: in load j, lanes 4i..4i+3 read four consecutive chunks
 //     (one 64-byte run) of block 16j+i.  They land in the block's LDS input ring (8
-//     chunks + mirror) at the start of the next iteration, so a load has a whole
-//     iteration to arrive, and the ring double-buffers a literal stream at full rate;
+//     chunks) at the start of the next iteration, so a load has a whole iteration to
+//     arrive, and the ring double-buffers a literal stream at full rate;
 //   * output: completed aligned 16-byte chunks are flushed at the end of each iteration
 //     by four transposed stores (lanes 4i..4i+3 write one block's four chunks);
 //   * all buffer loads/stores are always issued (an out-of-range offset drops a lane:
 //     tools/buf_probe.hip), so vmcnt bookkeeping is static, and stores come after the
 //     loads they could otherwise delay (a vmcnt wait covers every older access);
-//   * a copy with offset > 112 (beyond the 128-byte output ring) and length <= 16 becomes
-//     a "hole": its output bytes are reserved, its source is loaded from the flushed
-//     output, decoding continues, and the bytes are merged into the ring four steps
-//     later.  Flush, walker and ring copies wait for a hole that overlaps them.  Longer
-//     far copies stream 16 bytes per load.
-// CRC32 is absorbed from the input ring in two of the four steps (slicing-by-4 tables
+//   * a copy with offset > 108 (beyond what the 128-byte output ring still holds) and
+//     length <= 16 becomes a "hole": its output bytes are reserved, its source is loaded
+//     from the flushed output at the end of the iteration, decoding continues, and the
+//     bytes are merged into the ring at the start of the next one.  Flush, walker and ring
+//     copies wait for a hole that overlaps them.  Longer far copies stream 16 bytes per
+//     iteration.
+// LDS: every access is naturally aligned (gfx950 serialises misaligned LDS accesses lane
+// by lane: tools/lds_cost_probe.hip), see "Rings and natural alignment" below.
+// CRC32 is absorbed from the input ring in two of the four steps (slicing-by-16 tables
 // shared by the workgroup).  Bytes of a chunk outside the block are zeroed: the register
 // starts from a per-alignment state that reaches 0xFFFFFFFF after the leading zeros, and
 // the trailing zeros are folded into the stored value (x^(8t) mod P).
-// LDS per lane: output ring 128 + mirror + pad (160 B), input ring 128 + mirror (144 B).
-// gfx950 executes unaligned ds_read_b128 / ds_write_b128 (tools/lds_probe2.hip).
 // A row walker reads each row's header from the output ring as it is produced and checks
 // the key prefix inline; at block end a wave-cooperative pass compares the walked row
 // starts with the block's offset array, and mismatches re-derive rows from HBM with the
@@ -314,7 +315,7 @@ struct Lane {
   uint32_t c_issue, c_commit, n_req, fpend, fready, fl;
   uint32_t qoff;  // far-copy / hole source requested this iteration (loaded once, before the flush)
   // pending hole: a copy with offset > kReach and length <= 16 reserves output [hd, hd+hl)
-  // and decoding goes on; its source arrives four steps later and is merged into the ring
+  // and decoding goes on; its source arrives at the start of the next iteration
   uint32_t hpend, hd, hl;
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
@@ -530,7 +531,7 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     const bool need = act && !L.dd && L.rem == 0;
     const bool fin = need && L.s >= sn;
     // throttle (a hole delays the flush): after any step d - 16*fl <= 96, so the ring keeps
-    // every unflushed byte and every far source (offset > 112) is already flushed
+    // every unflushed byte and every far source (offset > kReach) is already flushed
     const bool room_out = L.d - 16 * L.fl <= kUnflushed;
     const bool can = need & (L.s < sn) & (avail >= int32_t(min(L.s + 5, sn))) & room_out;
     const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
