@@ -80,6 +80,8 @@ def lib():
             "or_xxh32": (C.c_uint32, [u8p, C.c_size_t, C.c_uint32]),
             "or_lz4_frame_len": (C.c_int, [u8p, C.c_size_t, u64p]),
             "or_lz4_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, szp]),
+            "or_zlib_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, szp]),
+            "or_decompress_len": (C.c_int, [C.c_int, u8p, C.c_size_t, u64p]),
             "or_v0_size": (C.c_size_t, [C.POINTER(RowValue)]),
             "or_v0_encode": (C.c_size_t, [C.POINTER(RowValue), u8p]),
             "or_v0_decode": (C.c_int, [u8p, C.c_size_t, C.c_long, C.POINTER(RowValue)]),
@@ -201,6 +203,17 @@ def lz4_decode(src: bytes) -> tuple[int, bytes]:
     out = np.zeros(max(dl.value, 1), np.uint8)
     n = C.c_size_t()
     st = lib().or_lz4_decode(p, len(src), out.ctypes.data_as(u8p), dl.value, C.byref(n))
+    return st, (out[:n.value].tobytes() if st == 0 else b"")
+
+
+def zlib_decode(src: bytes) -> tuple[int, bytes]:
+    """compress.Decode(CodecZlib): (status, decoded bytes) - the stream decoded in order."""
+    h, p = _buf(src)
+    dl = C.c_uint64()
+    lib().or_decompress_len(ZLIB, p, len(src), C.byref(dl))
+    out = np.zeros(max(dl.value, 1), np.uint8)
+    n = C.c_size_t()
+    st = lib().or_zlib_decode(p, len(src), out.ctypes.data_as(u8p), dl.value, C.byref(n))
     return st, (out[:n.value].tobytes() if st == 0 else b"")
 
 

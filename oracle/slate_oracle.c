@@ -32,6 +32,12 @@ const char* or_status_string(int s) {
     case OR_E_LZ4_BLOCK_CHECKSUM: return "lz4: invalid block checksum";
     case OR_E_LZ4_FRAME_CHECKSUM: return "lz4: invalid frame checksum";
     case OR_E_LZ4_CORRUPT: return "lz4: invalid source or destination buffer too short";
+    case OR_E_ZLIB_HEADER: return "zlib: invalid header";
+    case OR_E_ZLIB_DICTIONARY: return "zlib: invalid dictionary";
+    case OR_E_ZLIB_CHECKSUM: return "zlib: invalid checksum";
+    case OR_E_FLATE_CORRUPT: return "flate: corrupt input before offset %d";
+    case OR_E_UNEXPECTED_EOF: return "unexpected EOF";
+    case OR_E_EOF: return "EOF";
     case OR_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case OR_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case OR_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";
@@ -436,6 +442,198 @@ int or_lz4_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t*
   return lz4_frame(in, n, out ? out : &dummy, out ? cap : 0, out_len);
 }
 
+/* ============================================================ Zlib (inflate)
+ * compress.Decode CodecZlib = io.ReadAll(zlib.NewReader(buf)) (compression.go:134-140),
+ * Go's compress/zlib + compress/flate, restated from RFC 1950 / RFC 1951 and the
+ * behaviour of those readers: the 2-byte header check (CM 8, CINFO <= 7, FCHECK; FDICT
+ * without a dictionary fails), blocks decoded in order, Huffman tables built as
+ * flate's huffmanDecoder.init accepts them (complete codes, an empty tree, or one code
+ * of length 1), then the big-endian Adler-32 of the output; bytes after it are not
+ * read.  Running out of input is io.ErrUnexpectedEOF (io.EOF on an empty buffer).
+ * Parity: decoded bytes pinned by zlib-written streams (tests/golden/zlib_streams.json);
+ * error precedence on damaged streams follows the readers' structure but is unpinned
+ * (no Go here), and flate's CorruptInputError offset is not reported. */
+typedef struct { const uint8_t* in; size_t n, pos; uint32_t bits, nb; } zbits;
+static int zneed(zbits* z, uint32_t k) { /* 0 ok, -1 out of input */
+  while (z->nb < k) {
+    if (z->pos >= z->n) return -1;
+    z->bits |= (uint32_t)z->in[z->pos++] << z->nb;
+    z->nb += 8;
+  }
+  return 0;
+}
+static uint32_t ztake(zbits* z, uint32_t k) {
+  uint32_t v = z->bits & ((1u << k) - 1u);
+  z->bits >>= k; z->nb -= k;
+  return v;
+}
+typedef struct { uint16_t count[16], sym[288]; int max; } zhuff;
+/* Canonical code from code lengths.  Returns 0 when flate's huffmanDecoder.init rejects
+ * it: accepted are complete codes, the empty tree and one code of length 1. */
+static int zhuff_build(zhuff* h, const uint8_t* len, int n) {
+  memset(h->count, 0, sizeof h->count);
+  int max = 0;
+  for (int i = 0; i < n; i++) { h->count[len[i]]++; if (len[i] > max) max = len[i]; }
+  h->count[0] = 0;
+  h->max = max;
+  int c = 0;
+  for (int l = 1; l <= max; l++) { c <<= 1; c += h->count[l]; }
+  uint16_t offs[17];
+  offs[1] = 0;
+  for (int l = 1; l < 16; l++) offs[l + 1] = (uint16_t)(offs[l] + h->count[l]);
+  for (int i = 0; i < n; i++) if (len[i]) h->sym[offs[len[i]]++] = (uint16_t)i;
+  if (max == 0) return 1;
+  return c == (1 << max) || (c == 1 && max == 1);
+}
+/* One symbol, MSB-first code bits: -1 out of input, -2 no code matches (an empty tree, or
+ * the unused half of a single-code tree) */
+static int zdecode(zbits* z, const zhuff* h) {
+  int code = 0, first = 0, index = 0;
+  for (int l = 1; l <= h->max; l++) {
+    if (zneed(z, 1)) return -1;
+    code |= (int)ztake(z, 1);
+    const int cnt = h->count[l];
+    if (code - first < cnt) return h->sym[index + (code - first)];
+    index += cnt; first += cnt; first <<= 1; code <<= 1;
+  }
+  return -2;
+}
+static const uint16_t zlen_base[29] = {3,4,5,6,7,8,9,10,11,13,15,17,19,23,27,31,35,43,51,59,67,83,99,115,131,163,195,227,258};
+static const uint8_t zlen_extra[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
+static const uint16_t zdist_base[30] = {1,2,3,4,5,7,9,13,17,25,33,49,65,97,129,193,257,385,513,769,1025,1537,2049,3073,
+                                        4097,6145,8193,12289,16385,24577};
+static const uint8_t zdist_extra[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
+
+/* out == NULL: sizes only (no Adler-32); *out_len = bytes the in-order decoder writes. */
+static int zlib_stream(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  *out_len = 0;
+  if (n == 0) return OR_E_EOF;
+  if (n < 2) return OR_E_UNEXPECTED_EOF;
+  const uint32_t h = ((uint32_t)in[0] << 8) | in[1];
+  if ((in[0] & 0x0f) != 8 || (in[0] >> 4) > 7 || h % 31 != 0) return OR_E_ZLIB_HEADER;
+  size_t start = 2;
+  if (in[1] & 0x20) { /* FDICT: the dictionary id must be Adler-32 of the (empty) dictionary, 1 */
+    if (n < 6) return OR_E_UNEXPECTED_EOF;
+    if (be32(in + 2) != 1) return OR_E_ZLIB_DICTIONARY;
+    start = 6;
+  }
+  zbits z = {in, n, start, 0, 0};
+  size_t d = 0;
+  zhuff fixed_l, fixed_d; /* RFC 1951 3.2.6 (built per call: the batch decoder is threaded) */
+  {
+    uint8_t l[288];
+    for (int i = 0; i < 144; i++) l[i] = 8;
+    for (int i = 144; i < 256; i++) l[i] = 9;
+    for (int i = 256; i < 280; i++) l[i] = 7;
+    for (int i = 280; i < 288; i++) l[i] = 8;
+    zhuff_build(&fixed_l, l, 288);
+    for (int i = 0; i < 30; i++) l[i] = 5;
+    zhuff_build(&fixed_d, l, 30);
+  }
+  int final = 0;
+  while (!final) {
+    if (zneed(&z, 3)) return OR_E_UNEXPECTED_EOF;
+    final = (int)ztake(&z, 1);
+    const uint32_t type = ztake(&z, 2);
+    if (type == 0) { /* stored */
+      z.bits = 0; z.nb = 0; /* to a byte boundary */
+      if (z.n - z.pos < 4) return OR_E_UNEXPECTED_EOF;
+      const uint32_t len = z.in[z.pos] | (uint32_t)z.in[z.pos + 1] << 8;
+      const uint32_t nlen = z.in[z.pos + 2] | (uint32_t)z.in[z.pos + 3] << 8;
+      z.pos += 4;
+      if (len != (~nlen & 0xffff)) return OR_E_FLATE_CORRUPT;
+      if (len > cap - d) return OR_E_FLATE_CORRUPT;
+      size_t avail = z.n - z.pos < len ? z.n - z.pos : len;
+      if (out) memcpy(out + d, z.in + z.pos, avail);
+      d += avail; z.pos += avail; *out_len = d;
+      if (avail < len) return OR_E_UNEXPECTED_EOF;
+      continue;
+    }
+    if (type == 3) return OR_E_FLATE_CORRUPT;
+    zhuff dl, dd;
+    const zhuff *hl = &fixed_l, *hd = &fixed_d;
+    if (type == 2) {
+      if (zneed(&z, 14)) return OR_E_UNEXPECTED_EOF;
+      const uint32_t nlit = ztake(&z, 5) + 257, ndist = ztake(&z, 5) + 1, nclen = ztake(&z, 4) + 4;
+      if (nlit > 286 || ndist > 30) return OR_E_FLATE_CORRUPT;
+      static const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+      uint8_t cl[19] = {0};
+      for (uint32_t i = 0; i < nclen; i++) {
+        if (zneed(&z, 3)) return OR_E_UNEXPECTED_EOF;
+        cl[order[i]] = (uint8_t)ztake(&z, 3);
+      }
+      zhuff hc;
+      if (!zhuff_build(&hc, cl, 19)) return OR_E_FLATE_CORRUPT;
+      uint8_t lens[316];
+      uint32_t i = 0;
+      while (i < nlit + ndist) {
+        int sym = zdecode(&z, &hc);
+        if (sym == -1) return OR_E_UNEXPECTED_EOF;
+        if (sym < 0) return OR_E_FLATE_CORRUPT;
+        if (sym < 16) { lens[i++] = (uint8_t)sym; continue; }
+        uint32_t rep, val = 0;
+        if (sym == 16) {
+          if (i == 0) return OR_E_FLATE_CORRUPT;
+          val = lens[i - 1];
+          if (zneed(&z, 2)) return OR_E_UNEXPECTED_EOF;
+          rep = 3 + ztake(&z, 2);
+        } else if (sym == 17) {
+          if (zneed(&z, 3)) return OR_E_UNEXPECTED_EOF;
+          rep = 3 + ztake(&z, 3);
+        } else {
+          if (zneed(&z, 7)) return OR_E_UNEXPECTED_EOF;
+          rep = 11 + ztake(&z, 7);
+        }
+        if (i + rep > nlit + ndist) return OR_E_FLATE_CORRUPT;
+        while (rep--) lens[i++] = (uint8_t)val;
+      }
+      if (!zhuff_build(&dl, lens, (int)nlit) || !zhuff_build(&dd, lens + nlit, (int)ndist)) return OR_E_FLATE_CORRUPT;
+      if (lens[256] == 0) return OR_E_FLATE_CORRUPT; /* every block ends with the end-of-block code */
+      hl = &dl; hd = &dd;
+    }
+    for (;;) {
+      int sym = zdecode(&z, hl);
+      if (sym == -1) return OR_E_UNEXPECTED_EOF;
+      if (sym < 0) return OR_E_FLATE_CORRUPT;
+      if (sym < 256) {
+        if (d >= cap) return OR_E_FLATE_CORRUPT;
+        if (out) out[d] = (uint8_t)sym;
+        d++; *out_len = d;
+        continue;
+      }
+      if (sym == 256) break;
+      sym -= 257;
+      if (sym >= 29) return OR_E_FLATE_CORRUPT;
+      if (zneed(&z, zlen_extra[sym])) return OR_E_UNEXPECTED_EOF;
+      const uint32_t len = zlen_base[sym] + ztake(&z, zlen_extra[sym]);
+      int ds = zdecode(&z, hd);
+      if (ds == -1) return OR_E_UNEXPECTED_EOF;
+      if (ds < 0 || ds >= 30) return OR_E_FLATE_CORRUPT;
+      if (zneed(&z, zdist_extra[ds])) return OR_E_UNEXPECTED_EOF;
+      const uint32_t dist = zdist_base[ds] + ztake(&z, zdist_extra[ds]);
+      if (dist > d || dist > 32768) return OR_E_FLATE_CORRUPT;
+      if (len > cap - d) return OR_E_FLATE_CORRUPT;
+      if (out) for (uint32_t j = 0; j < len; j++) out[d + j] = out[d - dist + j];
+      d += len; *out_len = d;
+    }
+  }
+  /* the Adler-32 trailer starts at the next byte boundary */
+  if (z.n - z.pos < 4) return OR_E_UNEXPECTED_EOF;
+  if (out) {
+    uint32_t a = 1, b = 0;
+    for (size_t i = 0; i < d; i++) { a = (a + out[i]) % 65521u; b = (b + a) % 65521u; }
+    const uint32_t want = ((uint32_t)z.in[z.pos] << 24) | ((uint32_t)z.in[z.pos + 1] << 16) |
+                          ((uint32_t)z.in[z.pos + 2] << 8) | z.in[z.pos + 3];
+    if (((b << 16) | a) != want) return OR_E_ZLIB_CHECKSUM;
+  }
+  return OR_OK;
+}
+
+int or_zlib_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
+  uint8_t dummy;
+  return zlib_stream(in, n, out ? out : &dummy, out ? cap : 0, out_len);
+}
+
 /* ================================================ compress (compression.go) */
 int or_compress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
   if (codec == OR_CODEC_NONE) {
@@ -454,12 +652,14 @@ int or_decompress_len(int codec, const uint8_t* in, size_t n, uint64_t* dlen) {
   if (codec == OR_CODEC_NONE) { *dlen = n; return OR_OK; }
   if (codec == OR_CODEC_SNAPPY) { int hdr; return or_snappy_decoded_len(in, n, dlen, &hdr); }
   if (codec == OR_CODEC_LZ4) return or_lz4_frame_len(in, n, dlen);
+  if (codec == OR_CODEC_ZLIB) { size_t l; int st = zlib_stream(in, n, NULL, (size_t)-1, &l); *dlen = l; return st; }
   if (codec >= OR_CODEC_ZLIB && codec <= OR_CODEC_ZSTD) return OR_E_CODEC_UNSUPPORTED;
   return OR_E_INVALID_CODEC;
 }
 
 int or_decompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
   if (codec == OR_CODEC_LZ4) return or_lz4_decode(in, n, out, cap, out_len); /* sequential: first error wins */
+  if (codec == OR_CODEC_ZLIB) return or_zlib_decode(in, n, out, cap, out_len);
   uint64_t dl;
   int st = or_decompress_len(codec, in, n, &dl);
   if (st) return st;
@@ -741,7 +941,9 @@ int or_block_decode_batch(int codec, const uint8_t* in, const uint64_t* in_off, 
   for (uint32_t i = 0; i < n; i++) {
     size_t len = in_off[i + 1] - in_off[i];
     uint64_t dl = 0;
-    if (len >= 6 && or_decompress_len(codec, in + in_off[i], len - 4, &dl) != OR_OK && codec != OR_CODEC_LZ4) dl = 0;
+    if (len >= 6 && or_decompress_len(codec, in + in_off[i], len - 4, &dl) != OR_OK && codec != OR_CODEC_LZ4 &&
+        codec != OR_CODEC_ZLIB)
+      dl = 0;
     if (codec == OR_CODEC_SNAPPY && dl > 22ull * (len - 4)) dl = 0; /* provably corrupt (> 64/3 expansion) */
     out_off[i] = o; row_base[i] = r;
     o += (dl + 15) & ~15ull; r += or_row_capacity(dl); /* 16-byte aligned blocks, as the GPU plan */
