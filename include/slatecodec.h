@@ -60,13 +60,20 @@ enum slate_status {
   SLATE_E_INVALID_CODEC = 10,       /* "corrupted; invalid compression codec" */
   SLATE_E_SNAPPY_CORRUPT = 11,      /* "snappy: corrupt input" */
   SLATE_E_SNAPPY_TOO_LARGE = 12,    /* "snappy: decoded block is too large" */
-  SLATE_E_CODEC_UNSUPPORTED = 13,   /* codec not yet implemented by this backend (zlib/zstd) */
+  SLATE_E_CODEC_UNSUPPORTED = 13,   /* codec not yet implemented by this backend (zstd) */
   /* CodecLz4 (compression.go:143-144, github.com/pierrec/lz4/v4 v4.1.21 errors; strings unpinned) */
   SLATE_E_LZ4_MAGIC = 14,           /* "lz4: bad magic number" */
   SLATE_E_LZ4_HEADER_CHECKSUM = 15, /* "lz4: invalid header checksum" */
   SLATE_E_LZ4_BLOCK_CHECKSUM = 16,  /* "lz4: invalid block checksum" */
   SLATE_E_LZ4_FRAME_CHECKSUM = 17,  /* "lz4: invalid frame checksum" */
   SLATE_E_LZ4_CORRUPT = 18,         /* "lz4: invalid source or destination buffer too short" */
+  /* CodecZlib (compression.go:134-140, Go compress/zlib + compress/flate errors) */
+  SLATE_E_ZLIB_HEADER = 50,         /* "zlib: invalid header" */
+  SLATE_E_ZLIB_DICTIONARY = 51,     /* "zlib: invalid dictionary" */
+  SLATE_E_ZLIB_CHECKSUM = 52,       /* "zlib: invalid checksum" */
+  SLATE_E_FLATE_CORRUPT = 53,       /* "flate: corrupt input before offset %d" (offset not reported) */
+  SLATE_E_UNEXPECTED_EOF = 54,      /* "unexpected EOF" (io.ErrUnexpectedEOF) */
+  SLATE_E_EOF = 55,                 /* "EOF" (io.EOF: empty zlib stream) */
   /* v0 row codec (row.go:191-288) — per-row status in slate_row.status */
   SLATE_E_ROW_TOO_SHORT = 20,       /* "corrupt v0 row: data length too short to decode a row" */
   SLATE_E_ROW_PREFIX = 21,          /* "corrupt v0 row: key prefix length exceeds length of first key in block" */

@@ -32,6 +32,12 @@ const char* slate_status_string(int s) {
     case SLATE_E_LZ4_BLOCK_CHECKSUM: return "lz4: invalid block checksum";
     case SLATE_E_LZ4_FRAME_CHECKSUM: return "lz4: invalid frame checksum";
     case SLATE_E_LZ4_CORRUPT: return "lz4: invalid source or destination buffer too short";
+    case SLATE_E_ZLIB_HEADER: return "zlib: invalid header";
+    case SLATE_E_ZLIB_DICTIONARY: return "zlib: invalid dictionary";
+    case SLATE_E_ZLIB_CHECKSUM: return "zlib: invalid checksum";
+    case SLATE_E_FLATE_CORRUPT: return "flate: corrupt input before offset %d";
+    case SLATE_E_UNEXPECTED_EOF: return "unexpected EOF";
+    case SLATE_E_EOF: return "EOF";
     case SLATE_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case SLATE_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case SLATE_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";

@@ -182,6 +182,12 @@ __global__ void plan_sizes_kernel(int codec, const uint8_t* __restrict__ in, con
   row_sz[i] = row_capacity(dl);
 }
 
+// CodecZlib sizes: the bytes the in-order inflater writes (also when it then fails;
+// oracle or_block_decode_batch), one wave per block reading the stream from HBM.
+__global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off, uint32_t n,
+                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz);
+
 // ------------------------------------------------ exclusive scan (2 arrays)
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 4;
@@ -457,6 +463,326 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
   return SLATE_OK;
 }
 
+// ------------------------------------------------------------ Zlib (inflate)
+// compress.Decode CodecZlib = io.ReadAll(zlib.NewReader(buf)) (compression.go:134-140):
+// oracle/slate_oracle.c zlib_stream is the restatement this follows check for check.  One
+// wave per stream: the bit reader is wave-uniform (bytes come through a 64-byte window
+// held one byte per lane), each Huffman symbol is found by lanes 1..15 testing the code of
+// their length at once (the shortest match wins, as in a bit-serial canonical decoder),
+// and copies are spread over the lanes.
+struct ZHuff {
+  uint32_t count[16], first[16], index[16];
+  uint16_t sym[288];
+  uint32_t max, ok;
+};
+struct ZScratch {  // per wave
+  ZHuff lit, dist, clen;
+  uint8_t lens[320];
+};
+constexpr uint32_t kZScratch = (sizeof(ZScratch) + 15) & ~15u;
+constexpr uint32_t kZFixed = (2 * sizeof(ZHuff) + 15) & ~15u;
+
+// Canonical tables from code lengths (flate huffmanDecoder.init's acceptance: complete
+// codes, the empty tree, or one code of length 1).  Symbols of a length are ranked in
+// symbol order with ballots, 64 symbols at a time.
+__device__ void zbuild(ZHuff* h, const uint8_t* lens, uint32_t n, int lane) {
+  uint32_t cnt = 0;  // lane l: number of codes of length l
+  for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
+    const uint32_t i = c0 + lane;
+    const uint32_t my = i < n ? lens[i] : 0u;
+    for (uint32_t l = 1; l < 16; l++) {
+      const uint32_t k = uint32_t(__builtin_popcountll(__ballot(my == l)));
+      cnt += (uint32_t(lane) == l) ? k : 0u;
+    }
+  }
+  // lane-uniform prefix over lengths
+  uint32_t max = 0, first = 0, idx = 0, c = 0;
+  for (uint32_t l = 1; l < 16; l++) {
+    const uint32_t k = __builtin_amdgcn_readlane(cnt, int(l));
+    if (uint32_t(lane) == l) {
+      h->count[l] = k;
+      h->first[l] = first;
+      h->index[l] = idx;
+    }
+    first = (first + k) << 1;
+    idx += k;
+    if (k) max = l;
+  }
+  for (uint32_t l = 1; l <= max; l++) c = (c << 1) + __builtin_amdgcn_readlane(cnt, int(l));
+  if (lane == 0) {
+    h->count[0] = 0;
+    h->max = max;
+    h->ok = (max == 0 || c == (1u << max) || (c == 1 && max == 1)) ? 1u : 0u;
+  }
+  // symbols of length l at index[l] + rank (rank = earlier symbols of that length)
+  uint32_t base = 0;  // lane l: symbols of length l placed so far
+  for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
+    const uint32_t i = c0 + lane;
+    const uint32_t my = i < n ? lens[i] : 0u;
+    uint32_t pos = 0;
+    for (uint32_t l = 1; l < 16; l++) {
+      const uint64_t m = __ballot(my == l);
+      const uint32_t before = __builtin_amdgcn_readlane(base, int(l));
+      if (my == l) pos = before + uint32_t(__builtin_popcountll(m & ((uint64_t(1) << lane) - 1)));
+      base += (uint32_t(lane) == l) ? uint32_t(__builtin_popcountll(m)) : 0u;
+    }
+    if (my) h->sym[h->index[my] + pos] = uint16_t(i);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+}
+
+struct ZBits {  // wave-uniform bit reader over src[0, n)
+  const uint8_t* src;
+  uint32_t n, pos, nb;
+  uint64_t bits;
+  uint32_t wbase, win;
+};
+__device__ inline uint32_t zbyte(ZBits& z, uint32_t p, int lane) {
+  if (p - z.wbase >= uint32_t(kWave)) {
+    z.wbase = p;
+    z.win = (p + uint32_t(lane) < z.n) ? uint32_t(z.src[p + lane]) : 0u;
+  }
+  return __builtin_amdgcn_readlane(z.win, int(p - z.wbase));
+}
+__device__ inline void zfill(ZBits& z, int lane) {  // as many whole bytes as fit (>= 56 bits when available)
+  while (z.nb <= 56 && z.pos < z.n) {
+    z.bits |= uint64_t(zbyte(z, z.pos, lane)) << z.nb;
+    z.pos++;
+    z.nb += 8;
+  }
+}
+// -1: out of input, -2: no code matches
+__device__ inline int zsym(ZBits& z, const ZHuff* h, int lane) {
+  zfill(z, lane);
+  const uint32_t l = uint32_t(lane);
+  const uint32_t mx = h->max;
+  const uint32_t peek = uint32_t(z.bits) & 0x7FFFu;
+  const bool test = l >= 1 && l <= mx && l <= z.nb && l < 16;
+  const uint32_t code = (l >= 1 && l < 16) ? (__builtin_bitreverse32(peek) >> (32 - l)) : 0u;
+  const uint32_t fi = l < 16 ? h->first[l] : 0u, ct = l < 16 ? h->count[l] : 0u;
+  const bool hit = test && code - fi < ct;
+  const uint64_t m = __ballot(hit);
+  if (m == 0) return (z.nb < mx) ? -1 : -2;
+  const int L = __builtin_ctzll(m);
+  const uint32_t at = __builtin_amdgcn_readlane((l < 16 ? h->index[l] : 0u) + code - fi, L);
+  z.bits >>= L;
+  z.nb -= uint32_t(L);
+  return int(h->sym[at]);
+}
+__device__ inline bool zneed(ZBits& z, uint32_t k, int lane) {
+  zfill(z, lane);
+  return z.nb >= k;
+}
+__device__ inline uint32_t ztake(ZBits& z, uint32_t k) {
+  const uint32_t v = uint32_t(z.bits) & ((1u << k) - 1u);
+  z.bits >>= k;
+  z.nb -= k;
+  return v;
+}
+
+__constant__ uint16_t kZLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kZLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kZDistBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,    65,    97,    129,
+                                        193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kZDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t kZClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// RFC 1951 3.2.6 fixed tables, built once per workgroup
+__device__ void zfixed_build(ZHuff* fl, ZHuff* fd, uint8_t* lens, int lane) {
+  for (uint32_t i = lane; i < 288; i += kWave) lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
+  __builtin_amdgcn_s_waitcnt(0);
+  zbuild(fl, lens, 288, lane);
+  for (uint32_t i = lane; i < 30; i += kWave) lens[i] = 5;
+  __builtin_amdgcn_s_waitcnt(0);
+  zbuild(fd, lens, 30, lane);
+}
+
+// The stream in[0, n) decoded in order into out[0, cap) (out == nullptr: sizes only, no
+// Adler-32).  *out_len: bytes written so far (also on failure).
+__device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap, ZScratch* zs,
+                            const ZHuff* fixl, const ZHuff* fixd, int lane, uint32_t* out_len) {
+  *out_len = 0;
+  if (n == 0) return SLATE_E_EOF;
+  if (n < 2) return SLATE_E_UNEXPECTED_EOF;
+  const uint32_t b0 = __builtin_amdgcn_readfirstlane(in[0]), b1 = __builtin_amdgcn_readfirstlane(in[1]);
+  if ((b0 & 0x0f) != 8 || (b0 >> 4) > 7 || ((b0 << 8) | b1) % 31 != 0) return SLATE_E_ZLIB_HEADER;
+  uint32_t start = 2;
+  if (b1 & 0x20) {
+    if (n < 6) return SLATE_E_UNEXPECTED_EOF;
+    const uint32_t id = __builtin_amdgcn_readfirstlane(ld_be32(in + 2));
+    if (id != 1) return SLATE_E_ZLIB_DICTIONARY;
+    start = 6;
+  }
+  ZBits z{in, n, start, 0, 0, 0x80000000u, 0};
+  uint32_t d = 0;
+  bool final = false;
+  while (!final) {
+    if (!zneed(z, 3, lane)) return SLATE_E_UNEXPECTED_EOF;
+    final = ztake(z, 1) != 0;
+    const uint32_t type = ztake(z, 2);
+    if (type == 0) {  // stored: to the byte boundary, LEN, NLEN, bytes
+      ztake(z, z.nb & 7);
+      const uint32_t p = z.pos - z.nb / 8;  // next unread byte
+      z.pos = p;
+      z.nb = 0;
+      z.bits = 0;
+      if (n - p < 4) return SLATE_E_UNEXPECTED_EOF;
+      const uint32_t len = zbyte(z, p, lane) | (zbyte(z, p + 1, lane) << 8);
+      const uint32_t nlen = zbyte(z, p + 2, lane) | (zbyte(z, p + 3, lane) << 8);
+      z.pos = p + 4;
+      if (len != (~nlen & 0xffffu)) return SLATE_E_FLATE_CORRUPT;
+      if (len > cap - d) return SLATE_E_FLATE_CORRUPT;
+      const uint32_t avail = min(n - z.pos, len);
+      if (out)
+        for (uint32_t j = lane; j < avail; j += kWave) out[d + j] = in[z.pos + j];
+      d += avail;
+      z.pos += avail;
+      *out_len = d;
+      if (avail < len) return SLATE_E_UNEXPECTED_EOF;
+      continue;
+    }
+    if (type == 3) return SLATE_E_FLATE_CORRUPT;
+    const ZHuff *hl = fixl, *hd = fixd;
+    if (type == 2) {
+      if (!zneed(z, 14, lane)) return SLATE_E_UNEXPECTED_EOF;
+      const uint32_t nlit = ztake(z, 5) + 257, ndist = ztake(z, 5) + 1, nclen = ztake(z, 4) + 4;
+      if (nlit > 286 || ndist > 30) return SLATE_E_FLATE_CORRUPT;
+      uint32_t cl = 0;  // lane i < 19: the code length of code-length symbol i
+      for (uint32_t i = 0; i < 19; i++) {
+        uint32_t v = 0;
+        if (i < nclen) {
+          if (!zneed(z, 3, lane)) return SLATE_E_UNEXPECTED_EOF;
+          v = ztake(z, 3);
+        }
+        if (uint32_t(lane) == kZClenOrder[i]) cl = v;
+      }
+      if (lane < 19) zs->lens[lane] = uint8_t(cl);
+      __builtin_amdgcn_s_waitcnt(0);
+      zbuild(&zs->clen, zs->lens, 19, lane);
+      if (!zs->clen.ok) return SLATE_E_FLATE_CORRUPT;
+      uint32_t i = 0, prev = 0;
+      while (i < nlit + ndist) {
+        const int sym = zsym(z, &zs->clen, lane);
+        if (sym == -1) return SLATE_E_UNEXPECTED_EOF;
+        if (sym < 0) return SLATE_E_FLATE_CORRUPT;
+        if (sym < 16) {
+          if (lane == 0) zs->lens[i] = uint8_t(sym);
+          prev = uint32_t(sym);
+          i++;
+          continue;
+        }
+        uint32_t rep, val = 0;
+        if (sym == 16) {
+          if (i == 0) return SLATE_E_FLATE_CORRUPT;
+          val = prev;
+          if (!zneed(z, 2, lane)) return SLATE_E_UNEXPECTED_EOF;
+          rep = 3 + ztake(z, 2);
+        } else if (sym == 17) {
+          if (!zneed(z, 3, lane)) return SLATE_E_UNEXPECTED_EOF;
+          rep = 3 + ztake(z, 3);
+        } else {
+          if (!zneed(z, 7, lane)) return SLATE_E_UNEXPECTED_EOF;
+          rep = 11 + ztake(z, 7);
+        }
+        if (i + rep > nlit + ndist) return SLATE_E_FLATE_CORRUPT;
+        for (uint32_t j = lane; j < rep; j += kWave) zs->lens[i + j] = uint8_t(val);
+        prev = val;
+        i += rep;
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      zbuild(&zs->lit, zs->lens, nlit, lane);
+      zbuild(&zs->dist, zs->lens + nlit, ndist, lane);
+      if (!zs->lit.ok || !zs->dist.ok) return SLATE_E_FLATE_CORRUPT;
+      if (__builtin_amdgcn_readfirstlane(zs->lens[256]) == 0) return SLATE_E_FLATE_CORRUPT;
+      hl = &zs->lit;
+      hd = &zs->dist;
+    }
+    for (;;) {
+      int sym = zsym(z, hl, lane);
+      if (sym == -1) return SLATE_E_UNEXPECTED_EOF;
+      if (sym < 0) return SLATE_E_FLATE_CORRUPT;
+      if (sym < 256) {
+        if (d >= cap) return SLATE_E_FLATE_CORRUPT;
+        if (out && lane == 0) out[d] = uint8_t(sym);
+        d++;
+        *out_len = d;
+        continue;
+      }
+      if (sym == 256) break;
+      sym -= 257;
+      if (sym >= 29) return SLATE_E_FLATE_CORRUPT;
+      const uint32_t le = kZLenExtra[sym];
+      if (!zneed(z, le, lane)) return SLATE_E_UNEXPECTED_EOF;
+      const uint32_t len = kZLenBase[sym] + ztake(z, le);
+      const int ds = zsym(z, hd, lane);
+      if (ds == -1) return SLATE_E_UNEXPECTED_EOF;
+      if (ds < 0 || ds >= 30) return SLATE_E_FLATE_CORRUPT;
+      const uint32_t de = kZDistExtra[ds];
+      if (!zneed(z, de, lane)) return SLATE_E_UNEXPECTED_EOF;
+      const uint32_t dist = kZDistBase[ds] + ztake(z, de);
+      if (dist > d || dist > 32768) return SLATE_E_FLATE_CORRUPT;
+      if (len > cap - d) return SLATE_E_FLATE_CORRUPT;
+      if (out) {
+        __builtin_amdgcn_wave_barrier();
+        if (dist >= len) {
+          for (uint32_t j = lane; j < len; j += kWave) out[d + j] = out[d - dist + j];
+        } else {
+          for (uint32_t j = lane; j < len; j += kWave) out[d + j] = out[d - dist + (j % dist)];
+        }
+      }
+      d += len;
+      *out_len = d;
+    }
+  }
+  // the Adler-32 trailer starts at the next byte boundary
+  ztake(z, z.nb & 7);
+  const uint32_t p = z.pos - z.nb / 8;
+  if (n - p < 4) return SLATE_E_UNEXPECTED_EOF;
+  if (out) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    uint64_t sa = 0, sb = 0;  // sum x_i and sum (d - i) x_i
+    for (uint32_t i = lane; i < d; i += kWave) {
+      const uint64_t x = out[i];
+      sa += x;
+      sb += uint64_t(d - i) * x;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      sa += __shfl_xor(sa, o, 64);
+      sb += __shfl_xor(sb, o, 64);
+    }
+    const uint32_t a = uint32_t((1 + sa) % 65521u), b = uint32_t((uint64_t(d) + sb) % 65521u);
+    const uint32_t want = __builtin_amdgcn_readfirstlane((zbyte(z, p, lane) << 24) | (zbyte(z, p + 1, lane) << 16) |
+                                                         (zbyte(z, p + 2, lane) << 8) | zbyte(z, p + 3, lane));
+    if (((b << 16) | a) != want) return SLATE_E_ZLIB_CHECKSUM;
+  }
+  *out_len = d;
+  return SLATE_OK;
+}
+
+__global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off, uint32_t n,
+                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kZFixed + 4 * kZScratch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ZHuff* fix = reinterpret_cast<ZHuff*>(smem);
+  ZScratch* zs = reinterpret_cast<ZScratch*>(smem + kZFixed + wave * kZScratch);
+  if (wave == 0) zfixed_build(fix, fix + 1, zs->lens, lane);
+  __syncthreads();
+  const uint32_t waves = gridDim.x * 4;
+  for (uint32_t b = blockIdx.x * 4 + wave; b < n; b += waves) {
+    const uint64_t s0 = in_off[b], len = in_off[b + 1] - s0;
+    uint32_t dl = 0;
+    if (len >= 6 && len - 4 < 0xFFFFFFFFull) wave_inflate(in + s0, uint32_t(len - 4), nullptr, 0xFFFFFFFFu, zs, fix, fix + 1, lane, &dl);
+    if (lane == 0) {
+      out_sz[b] = align16(dl);
+      row_sz[b] = row_capacity(dl);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- v0 rows
 // row.go:191-261 against firstKey of length fk (fk < 0: firstKey == nil).
 __device__ inline void decode_row(const uint8_t* data, uint32_t data_len, uint32_t off, int fk, slate_row& r,
@@ -510,6 +836,8 @@ struct WaveBufs {
   uint8_t* in;          // staging for the encoded block (in_cap bytes, 16-aligned)
   uint8_t* out;         // decoded block (out_cap bytes, 16-aligned)
   uint32_t in_cap, out_cap;
+  ZScratch* zs = nullptr;  // CodecZlib only: this wave's Huffman tables
+  const ZHuff* zfix = nullptr;  // CodecZlib only: the workgroup's fixed literal/length + distance tables
 };
 
 __device__ inline void write_meta(slate_block_meta* m, const slate_block_meta& v, int lane) {
@@ -528,9 +856,10 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   }
   uint32_t hdr = 0;
   uint64_t dl = 0;
-  // LZ4: the plan's capacity (>= what the in-order decoder writes); others: the header
-  const bool dl_ok = a.codec == SLATE_CODEC_LZ4 ? (dl = a.out_off[b + 1] - a.out_off[b], true)
-                                                : decoded_len(a.codec, gin, len, &dl, &hdr);
+  // LZ4/Zlib: the plan's capacity (>= what the in-order decoder writes); others: the header
+  const bool dl_ok = (a.codec == SLATE_CODEC_LZ4 || a.codec == SLATE_CODEC_ZLIB)
+                         ? (dl = a.out_off[b + 1] - a.out_off[b], true)
+                         : decoded_len(a.codec, gin, len, &dl, &hdr);
   uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
   if (shift + len > w.in_cap || (a.codec != SLATE_CODEC_NONE && dl > w.out_cap)) {
     if (defer_large) return false;
@@ -586,8 +915,19 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     }
     buf = w.out;
     n = outn;
+  } else if (a.codec == SLATE_CODEC_ZLIB) {
+    uint32_t outn = 0;
+    int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)
+                           : wave_inflate(w.in + shift, clen, w.out, uint32_t(dl), w.zs, w.zfix, w.zfix + 1, lane, &outn);
+    if (st != SLATE_OK) {
+      m.status = int16_t(st);
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    buf = w.out;
+    n = outn;
   } else {
-    m.status = (a.codec == SLATE_CODEC_ZLIB || a.codec == SLATE_CODEC_ZSTD) ? SLATE_E_CODEC_UNSUPPORTED
+    m.status = (a.codec == SLATE_CODEC_ZSTD) ? SLATE_E_CODEC_UNSUPPORTED
                                                                                : SLATE_E_INVALID_CODEC;
     write_meta(&a.meta[b], m, lane);
     return true;
@@ -691,6 +1031,17 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   return true;
 }
 
+// CodecZlib LDS after the per-wave buffers: fixed tables (one per workgroup), then a
+// ZScratch per wave; the fixed tables are built by wave 0.
+__device__ inline void zlib_lds(WaveBufs& w, uint8_t* zbase, int waves, int wave, int lane) {
+  ZHuff* fix = reinterpret_cast<ZHuff*>(zbase);
+  w.zfix = fix;
+  w.zs = reinterpret_cast<ZScratch*>(zbase + kZFixed + size_t(wave) * kZScratch);
+  if (wave == 0) zfixed_build(fix, fix + 1, w.zs->lens, lane);
+  (void)waves;
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
@@ -699,6 +1050,7 @@ __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs 
   const uint32_t per_wave = kFastInCap + kFastOutCap;
   WaveBufs w{tab, smem + kTabBytes + wave * per_wave, smem + kTabBytes + wave * per_wave + kFastInCap,
              kFastInCap, kFastOutCap};
+  if (a.codec == SLATE_CODEC_ZLIB) zlib_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, kDecodeThreads / 64, wave, lane);
   const uint32_t waves = gridDim.x * (kDecodeThreads / 64);
   for (uint32_t b = blockIdx.x * (kDecodeThreads / 64) + wave; b < a.n; b += waves) {
     if (!decode_block_wave(a, b, w, lane, true)) {
@@ -712,7 +1064,10 @@ __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   load_crc_tables(tab);
   const int lane = threadIdx.x & 63;
-  WaveBufs w{tab, smem + kTabBytes, smem + kTabBytes + kLargeInCap, kLargeInCap, kLargeOutCap};
+  // CodecZlib: its tables take the top of the input staging area
+  const uint32_t in_cap = a.codec == SLATE_CODEC_ZLIB ? kLargeInCap - kZFixed - kZScratch : kLargeInCap;
+  WaveBufs w{tab, smem + kTabBytes, smem + kTabBytes + kLargeInCap, in_cap, kLargeOutCap};
+  if (a.codec == SLATE_CODEC_ZLIB) zlib_lds(w, smem + kTabBytes + in_cap, 1, 0, lane);
   uint32_t count = *a.large_count;
   for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) decode_block_wave(a, a.large_list[k], w, lane, false);
 }
@@ -747,6 +1102,8 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
   DecodeScratch s = carve(scratch, n);
   uint32_t m = n + 1;
   plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
+  if (codec == SLATE_CODEC_ZLIB && n > 0)
+    plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
   scan_reduce_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
   scan_partials_kernel<<<1, kScanThreads, 0, st>>>(s.pa, s.pb, s.tiles);
   scan_apply_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
@@ -779,7 +1136,8 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   // (bit 32: the v1 lane-per-block kernel, A/B only)
   if (a.codec == SLATE_CODEC_SNAPPY && !(a.debug & 16))
     return (a.debug & 32) ? launch_decode_lpb(st, a, num_cus) : launch_decode_lpb2(st, a, num_cus);
-  const size_t lds = kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap);
+  const size_t lds = kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap) +
+                     (a.codec == SLATE_CODEC_ZLIB ? kZFixed + (kDecodeThreads / 64) * size_t(kZScratch) : 0);
   uint32_t wgs_needed = (a.n + kDecodeThreads / 64 - 1) / (kDecodeThreads / 64);
   uint32_t grid = min(wgs_needed, uint32_t(num_cus) * kDecodeWgPerCu);
   decode_fast_kernel<<<grid, kDecodeThreads, lds, st>>>(a);

@@ -1,0 +1,109 @@
+"""GPU parity for CodecZlib blocks (compress.Decode, compression.go:134-140) through the C ABI:
+block.Decode with zlib streams of every deflate strategy/level (stored, fixed and dynamic
+Huffman blocks), plus damaged streams with their status codes, bit-exact against the oracle
+(plan, meta, decoded bytes, rows).  The streams come from the zlib library (Python's zlib
+module), which the oracle's inflater is pinned to in tests/test_zlib_oracle.py."""
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+from tests import blockgen as bg
+
+pytestmark = pytest.mark.gpu
+STRATEGIES = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FILTERED]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import slatecodec as sc
+    return sc.Context(0)
+
+
+def _crc(stream: bytes) -> bytes:
+    return stream + struct.pack(">I", zlib.crc32(stream))
+
+
+def _z(data: bytes, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, wbits=15) -> bytes:
+    co = zlib.compressobj(level, zlib.DEFLATED, wbits, 8, strategy)
+    return co.compress(data) + co.flush()
+
+
+def _compare(ctx, blocks, misalign=0):
+    blob, off = bg.pack(blocks, misalign)
+    g_out, g_off, g_meta, g_rows, g_rb = ctx.decode_batch(ob.ZLIB, blob, off)
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(ob.ZLIB, blob, off)
+    assert np.array_equal(g_off, o_off), "plan: out_off"
+    assert np.array_equal(g_rb, o_rb), "plan: row_base"
+    for i, blk in enumerate(blocks):
+        gm, om = g_meta[i], o_meta[i]
+        assert gm.tobytes() == om.tobytes(), (i, gm, om)
+        st = int(om["status"])
+        if st == 0 or 3 <= st <= 7:
+            dec = ob.zlib_decode(blk[:-4])[1]
+            a = int(o_off[i])
+            assert g_out[a:a + len(dec)].tobytes() == dec == o_out[a:a + len(dec)].tobytes(), i
+        if st == 0:
+            r0 = int(o_rb[i])
+            nr = min(int(om["n_rows"]), int(o_rb[i + 1]) - r0)
+            assert g_rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+    return o_meta
+
+
+def _sst_plain(rng, n_kv, block_size):
+    kvs = bg.random_kvs(rng, n_kv, alphabet=rng.choice([4, 256]))
+    return [b[:-4] for b in bg.sst_blocks(kvs, block_size, ob.NONE)]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_zlib_ssts(ctx, seed):
+    rng = random.Random(seed)
+    blocks = [_crc(_z(dec, rng.choice([0, 1, 6, 9]), rng.choice(STRATEGIES), rng.choice([9, 15])))
+              for dec in _sst_plain(rng, rng.randint(300, 1500), rng.choice([512, 4096]))]
+    meta = _compare(ctx, blocks, misalign=rng.randrange(16))
+    assert (meta["status"] == 0).all()
+
+
+def test_vhalf_zlib_blocks(ctx):
+    kvs = bg.kv_synthetic(38 * 200, half=True, tomb_every=25)
+    blocks = [_crc(_z(b[:-4])) for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+    meta = _compare(ctx, blocks, misalign=7)
+    assert (meta["status"] == 0).all()
+
+
+def test_large_zlib_blocks(ctx):
+    """Blocks beyond the fast kernel's LDS budget go through the large-block kernel."""
+    rng = random.Random(11)
+    blocks = [_crc(_z(dec, rng.choice([1, 6]), rng.choice(STRATEGIES)))
+              for dec in _sst_plain(rng, 2500, 40000)]
+    blocks.append(_crc(_z(_sst_plain(rng, 600, 60000)[0], 0)))  # stored blocks, > 64 KiB cap? plan decides
+    _compare(ctx, blocks, misalign=5)
+
+
+def test_damaged_zlib_blocks(ctx):
+    rng = random.Random(9)
+    decs = _sst_plain(rng, 800, 1024)
+    blocks = []
+    for dec in decs:
+        f = bytearray(_z(dec, rng.choice([1, 6, 9]), rng.choice(STRATEGIES)))
+        kind = rng.randrange(6)
+        if kind == 0:
+            f[rng.randrange(len(f))] ^= 1 << rng.randrange(8)
+        elif kind == 1:
+            f = f[: rng.randrange(len(f))]
+        elif kind == 2:
+            f += bytes(rng.randrange(256) for _ in range(rng.randint(1, 5)))
+        elif kind == 3:
+            i = rng.randrange(2, len(f))
+            f[i:i + 2] = bytes([rng.randrange(256), rng.randrange(256)])
+        elif kind == 4:
+            f[rng.choice([0, 1])] ^= rng.choice([1, 2, 0x20, 0x80])
+        blocks.append(_crc(bytes(f)))
+    blocks += [_crc(b""), _crc(b"\x78"), _crc(b"\x78\x9c"), _crc(b"\x78\x9c\x07"),
+               _crc(bytes([0x78, 0x9c, 0x01, 0x05, 0x00, 0x00, 0x00]) + b"abcde" + b"\0" * 4)]
+    meta = _compare(ctx, blocks, misalign=1)
+    st = set(int(x) for x in meta["status"])
+    assert {0, 53, 54} <= st, st
