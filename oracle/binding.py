@@ -81,6 +81,9 @@ def lib():
             "or_lz4_frame_len": (C.c_int, [u8p, C.c_size_t, u64p]),
             "or_lz4_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, szp]),
             "or_zlib_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, szp]),
+            "or_xxh64": (C.c_uint64, [u8p, C.c_size_t, C.c_uint64]),
+            "or_zstd_plan": (C.c_int, [u8p, C.c_size_t, u64p]),
+            "or_zstd_decode": (C.c_int, [u8p, C.c_size_t, u8p, C.c_size_t, szp]),
             "or_decompress_len": (C.c_int, [C.c_int, u8p, C.c_size_t, u64p]),
             "or_v0_size": (C.c_size_t, [C.POINTER(RowValue)]),
             "or_v0_encode": (C.c_size_t, [C.POINTER(RowValue), u8p]),
@@ -215,6 +218,28 @@ def zlib_decode(src: bytes) -> tuple[int, bytes]:
     n = C.c_size_t()
     st = lib().or_zlib_decode(p, len(src), out.ctypes.data_as(u8p), dl.value, C.byref(n))
     return st, (out[:n.value].tobytes() if st == 0 else b"")
+
+
+def zstd_plan(src: bytes) -> int:
+    h, p = _buf(src)
+    dl = C.c_uint64()
+    lib().or_zstd_plan(p, len(src), C.byref(dl))
+    return dl.value
+
+
+def zstd_decode(src: bytes) -> tuple[int, bytes]:
+    """compress.Decode(CodecZstd): (status, decoded bytes) - frames decoded in order into the plan size."""
+    h, p = _buf(src)
+    cap = zstd_plan(src)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = C.c_size_t()
+    st = lib().or_zstd_decode(p, len(src), out.ctypes.data_as(u8p), cap, C.byref(n))
+    return st, (out[:n.value].tobytes() if st == 0 else b"")
+
+
+def xxh64(b: bytes, seed: int = 0) -> int:
+    h, p = _buf(b)
+    return lib().or_xxh64(p, len(b), seed)
 
 
 @dataclass

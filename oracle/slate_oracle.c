@@ -38,6 +38,12 @@ const char* or_status_string(int s) {
     case OR_E_FLATE_CORRUPT: return "flate: corrupt input before offset %d";
     case OR_E_UNEXPECTED_EOF: return "unexpected EOF";
     case OR_E_EOF: return "EOF";
+    case OR_E_ZSTD_MAGIC: return "invalid input: magic number mismatch";
+    case OR_E_ZSTD_CHECKSUM: return "CRC check failed";
+    case OR_E_ZSTD_CORRUPT: return "zstd: corrupt input";
+    case OR_E_ZSTD_FRAME_SIZE: return "frame size does not match size on stream";
+    case OR_E_ZSTD_DICT: return "unknown dictionary";
+    case OR_E_ZSTD_RESERVED_BLOCK: return "invalid input: reserved block type encountered";
     case OR_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case OR_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case OR_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";
@@ -653,13 +659,14 @@ int or_decompress_len(int codec, const uint8_t* in, size_t n, uint64_t* dlen) {
   if (codec == OR_CODEC_SNAPPY) { int hdr; return or_snappy_decoded_len(in, n, dlen, &hdr); }
   if (codec == OR_CODEC_LZ4) return or_lz4_frame_len(in, n, dlen);
   if (codec == OR_CODEC_ZLIB) { size_t l; int st = zlib_stream(in, n, NULL, (size_t)-1, &l); *dlen = l; return st; }
-  if (codec >= OR_CODEC_ZLIB && codec <= OR_CODEC_ZSTD) return OR_E_CODEC_UNSUPPORTED;
+  if (codec == OR_CODEC_ZSTD) return or_zstd_plan(in, n, dlen);
   return OR_E_INVALID_CODEC;
 }
 
 int or_decompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
   if (codec == OR_CODEC_LZ4) return or_lz4_decode(in, n, out, cap, out_len); /* sequential: first error wins */
   if (codec == OR_CODEC_ZLIB) return or_zlib_decode(in, n, out, cap, out_len);
+  if (codec == OR_CODEC_ZSTD) return or_zstd_decode(in, n, out, cap, out_len);
   uint64_t dl;
   int st = or_decompress_len(codec, in, n, &dl);
   if (st) return st;
@@ -942,7 +949,7 @@ int or_block_decode_batch(int codec, const uint8_t* in, const uint64_t* in_off, 
     size_t len = in_off[i + 1] - in_off[i];
     uint64_t dl = 0;
     if (len >= 6 && or_decompress_len(codec, in + in_off[i], len - 4, &dl) != OR_OK && codec != OR_CODEC_LZ4 &&
-        codec != OR_CODEC_ZLIB)
+        codec != OR_CODEC_ZLIB && codec != OR_CODEC_ZSTD)
       dl = 0;
     if (codec == OR_CODEC_SNAPPY && dl > 22ull * (len - 4)) dl = 0; /* provably corrupt (> 64/3 expansion) */
     out_off[i] = o; row_base[i] = r;

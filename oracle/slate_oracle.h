@@ -46,6 +46,8 @@ enum {
   OR_E_RANGE_START = 46, OR_E_RANGE_END = 47, OR_E_FLATBUF = 48,
   OR_E_ZLIB_HEADER = 50, OR_E_ZLIB_DICTIONARY = 51, OR_E_ZLIB_CHECKSUM = 52, OR_E_FLATE_CORRUPT = 53,
   OR_E_UNEXPECTED_EOF = 54, OR_E_EOF = 55,
+  OR_E_ZSTD_MAGIC = 56, OR_E_ZSTD_CHECKSUM = 57, OR_E_ZSTD_CORRUPT = 58, OR_E_ZSTD_FRAME_SIZE = 59,
+  OR_E_ZSTD_DICT = 60, OR_E_ZSTD_RESERVED_BLOCK = 61,
   OR_E_INVALID_ARG = 102, OR_E_CAPACITY = 103, OR_E_OOM = 104,
 };
 
@@ -80,6 +82,9 @@ uint32_t or_xxh32(const uint8_t* p, size_t n, uint32_t seed);
 int or_lz4_frame_len(const uint8_t* in, size_t n, uint64_t* dlen);
 int or_lz4_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 int or_zlib_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
+uint64_t or_xxh64(const uint8_t* p, size_t n, uint64_t seed);
+int or_zstd_plan(const uint8_t* in, size_t n, uint64_t* dlen);   /* zstd_oracle.c */
+int or_zstd_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 int or_decompress_len(int codec, const uint8_t* in, size_t n, uint64_t* dlen);
 int or_decompress(int codec, const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len);
 

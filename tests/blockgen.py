@@ -26,6 +26,33 @@ def kv_synthetic(n: int, seed: int = 20250307, half: bool = True, tomb_every: in
     return out
 
 
+def kv_mixed(n: int, seed: int = 20250307):
+    """SURVEY 8d config 5 KVs: ascending keys of 8-256 bytes sharing 3 + (Zipf(s=1.2) - 1) bytes
+    with the previous key (restart-scan stress; the 3-byte head absorbs carries so millions of
+    keys stay sorted), 1 KiB V-half values (r||r, 512 B halves)."""
+    rng = np.random.default_rng(seed)
+    keys, prev = [], None
+    for i in range(n):
+        ln = int(rng.integers(8, 257))
+        if prev is None:
+            head = bytearray(b"aaaa")
+        else:
+            p = min(3 + int(rng.zipf(1.2)) - 1, len(prev) - 1, ln - 1)
+            head = bytearray(prev[:p + 1])
+            while head[p] >= 0xFE:  # carry to the left
+                head = head[:p]
+                p -= 1
+                assert p >= 0, "kv_mixed: key space exhausted"
+            head[p] += 1 + int(rng.integers(0, 2))
+        tail = rng.integers(ord("a"), ord("z") + 1, max(ln - len(head), 0), dtype=np.uint8).tobytes()
+        k = bytes(head) + tail
+        assert prev is None or k > prev
+        keys.append(k)
+        prev = k
+    r = rng.integers(0, 256, (n, 512), dtype=np.uint8)
+    return [(keys[i], np.concatenate([r[i], r[i]]).tobytes()) for i in range(n)]
+
+
 def random_kvs(rng: random.Random, n: int, klen=(1, 24), vlen=(0, 120), tomb_p=0.1, alphabet=256):
     keys = sorted({bytes(rng.randrange(alphabet) for _ in range(rng.randint(*klen))) for _ in range(n)})
     return [(k, b"" if rng.random() < tomb_p else bytes(rng.randrange(alphabet) for _ in range(rng.randint(*vlen))))
