@@ -60,7 +60,7 @@ enum slate_status {
   SLATE_E_INVALID_CODEC = 10,       /* "corrupted; invalid compression codec" */
   SLATE_E_SNAPPY_CORRUPT = 11,      /* "snappy: corrupt input" */
   SLATE_E_SNAPPY_TOO_LARGE = 12,    /* "snappy: decoded block is too large" */
-  SLATE_E_CODEC_UNSUPPORTED = 13,   /* codec not yet implemented by this backend (zstd) */
+  SLATE_E_CODEC_UNSUPPORTED = 13,   /* codec not implemented by this backend (encode of Zlib/LZ4/Zstd) */
   /* CodecLz4 (compression.go:143-144, github.com/pierrec/lz4/v4 v4.1.21 errors; strings unpinned) */
   SLATE_E_LZ4_MAGIC = 14,           /* "lz4: bad magic number" */
   SLATE_E_LZ4_HEADER_CHECKSUM = 15, /* "lz4: invalid header checksum" */
@@ -74,6 +74,13 @@ enum slate_status {
   SLATE_E_FLATE_CORRUPT = 53,       /* "flate: corrupt input before offset %d" (offset not reported) */
   SLATE_E_UNEXPECTED_EOF = 54,      /* "unexpected EOF" (io.ErrUnexpectedEOF) */
   SLATE_E_EOF = 55,                 /* "EOF" (io.EOF: empty zlib stream) */
+  /* CodecZstd (compression.go:146-153, github.com/klauspost/compress v1.17.11 errors; strings unpinned) */
+  SLATE_E_ZSTD_MAGIC = 56,          /* "invalid input: magic number mismatch" */
+  SLATE_E_ZSTD_CHECKSUM = 57,       /* "CRC check failed" (XXH64 content checksum) */
+  SLATE_E_ZSTD_CORRUPT = 58,        /* malformed literals / sequences / tables / sizes */
+  SLATE_E_ZSTD_FRAME_SIZE = 59,     /* "frame size does not match size on stream" */
+  SLATE_E_ZSTD_DICT = 60,           /* "unknown dictionary" (no dictionaries are configured) */
+  SLATE_E_ZSTD_RESERVED_BLOCK = 61, /* "invalid input: reserved block type encountered" */
   /* v0 row codec (row.go:191-288) — per-row status in slate_row.status */
   SLATE_E_ROW_TOO_SHORT = 20,       /* "corrupt v0 row: data length too short to decode a row" */
   SLATE_E_ROW_PREFIX = 21,          /* "corrupt v0 row: key prefix length exceeds length of first key in block" */

@@ -576,3 +576,4 @@ int or_zstd_plan(const uint8_t* in, size_t n, uint64_t* dlen) {
 int or_zstd_decode(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* out_len) {
   return zs_frames(in, n, out, cap, out_len);
 }
+

@@ -38,6 +38,12 @@ const char* slate_status_string(int s) {
     case SLATE_E_FLATE_CORRUPT: return "flate: corrupt input before offset %d";
     case SLATE_E_UNEXPECTED_EOF: return "unexpected EOF";
     case SLATE_E_EOF: return "EOF";
+    case SLATE_E_ZSTD_MAGIC: return "invalid input: magic number mismatch";
+    case SLATE_E_ZSTD_CHECKSUM: return "CRC check failed";
+    case SLATE_E_ZSTD_CORRUPT: return "zstd: corrupt input";
+    case SLATE_E_ZSTD_FRAME_SIZE: return "frame size does not match size on stream";
+    case SLATE_E_ZSTD_DICT: return "unknown dictionary";
+    case SLATE_E_ZSTD_RESERVED_BLOCK: return "invalid input: reserved block type encountered";
     case SLATE_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case SLATE_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case SLATE_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";

@@ -25,6 +25,7 @@
 #include "kernels.h"
 #include "encode.h"
 #include "wave_crc.h"
+#include "zstd.h"
 
 namespace slate {
 
@@ -783,6 +784,31 @@ __global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restric
   }
 }
 
+// CodecZstd sizes (oracle or_zstd_plan): one wave per block reading the frames from HBM.
+__global__ __launch_bounds__(256) void plan_zstd_kernel(const uint8_t* __restrict__ in,
+                                                        const uint64_t* __restrict__ in_off, uint32_t n,
+                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kZsShared + 4 * kZsScratch];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  ZsShared* sh = reinterpret_cast<ZsShared*>(smem);
+  ZsScratch* sc = reinterpret_cast<ZsScratch*>(smem + kZsShared + wave * kZsScratch);
+  if (wave == 0) zs_shared_build(sh, sc, lane);
+  __syncthreads();
+  const uint32_t waves = gridDim.x * 4;
+  for (uint32_t b = blockIdx.x * 4 + wave; b < n; b += waves) {
+    const uint64_t s0 = in_off[b], len = in_off[b + 1] - s0;
+    uint64_t dl = 0;
+    if (len >= 6 && len - 4 < 0x7FFFFFFFull) {
+      const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(in + s0) & ~uintptr_t(3));
+      dl = wave_zstd_plan(base, int32_t((in + s0) - base), uint32_t(len - 4), sc, sh, lane);
+    }
+    if (lane == 0) {
+      out_sz[b] = align16(dl);
+      row_sz[b] = row_capacity(dl);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- v0 rows
 // row.go:191-261 against firstKey of length fk (fk < 0: firstKey == nil).
 __device__ inline void decode_row(const uint8_t* data, uint32_t data_len, uint32_t off, int fk, slate_row& r,
@@ -838,6 +864,8 @@ struct WaveBufs {
   uint32_t in_cap, out_cap;
   ZScratch* zs = nullptr;  // CodecZlib only: this wave's Huffman tables
   const ZHuff* zfix = nullptr;  // CodecZlib only: the workgroup's fixed literal/length + distance tables
+  ZsScratch* zss = nullptr;     // CodecZstd only: this wave's tables
+  const ZsShared* zsh = nullptr;  // CodecZstd only: the workgroup's predefined tables
 };
 
 __device__ inline void write_meta(slate_block_meta* m, const slate_block_meta& v, int lane) {
@@ -845,6 +873,9 @@ __device__ inline void write_meta(slate_block_meta* m, const slate_block_meta& v
 }
 
 // Returns false when the block does not fit this wave's LDS budget (caller defers it).
+// CK: the codec class compiled in (0: None/Snappy/LZ4, 1: Zlib, 2: Zstd), so each kernel
+// instance carries only its codec's registers.
+template <int CK>
 __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBufs& w, int lane, bool defer_large) {
   slate_block_meta m{};
   uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
@@ -857,7 +888,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   uint32_t hdr = 0;
   uint64_t dl = 0;
   // LZ4/Zlib: the plan's capacity (>= what the in-order decoder writes); others: the header
-  const bool dl_ok = (a.codec == SLATE_CODEC_LZ4 || a.codec == SLATE_CODEC_ZLIB)
+  const bool dl_ok = (a.codec == SLATE_CODEC_LZ4 || a.codec == SLATE_CODEC_ZLIB || a.codec == SLATE_CODEC_ZSTD)
                          ? (dl = a.out_off[b + 1] - a.out_off[b], true)
                          : decoded_len(a.codec, gin, len, &dl, &hdr);
   uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
@@ -890,7 +921,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   if (a.codec == SLATE_CODEC_NONE) {
     buf = w.in + shift;
     n = clen;
-  } else if (a.codec == SLATE_CODEC_SNAPPY) {
+  } else if (CK == 0 && a.codec == SLATE_CODEC_SNAPPY) {
     if (!dl_ok) {  // corrupt varint header or provably corrupt length
       m.status = SLATE_E_SNAPPY_CORRUPT;
       write_meta(&a.meta[b], m, lane);
@@ -904,7 +935,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     }
     buf = w.out;
     n = uint32_t(dl);
-  } else if (a.codec == SLATE_CODEC_LZ4) {
+  } else if (CK == 0 && a.codec == SLATE_CODEC_LZ4) {
     uint32_t outn = 0;
     int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)  // profiling: skip the decompression
                            : wave_lz4_decode(w.in, shift, clen, w.out, uint32_t(dl), lane, &outn);
@@ -915,7 +946,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     }
     buf = w.out;
     n = outn;
-  } else if (a.codec == SLATE_CODEC_ZLIB) {
+  } else if (CK == 1 && a.codec == SLATE_CODEC_ZLIB) {
     uint32_t outn = 0;
     int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)
                            : wave_inflate(w.in + shift, clen, w.out, uint32_t(dl), w.zs, w.zfix, w.zfix + 1, lane, &outn);
@@ -926,9 +957,19 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     }
     buf = w.out;
     n = outn;
+  } else if (CK == 2 && a.codec == SLATE_CODEC_ZSTD) {
+    uint32_t outn = 0;
+    int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)
+                           : wave_zstd_decode(w.in, int32_t(shift), clen, w.out, uint32_t(dl), w.zss, w.zsh, lane, &outn);
+    if (st != SLATE_OK) {
+      m.status = int16_t(st);
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    buf = w.out;
+    n = outn;
   } else {
-    m.status = (a.codec == SLATE_CODEC_ZSTD) ? SLATE_E_CODEC_UNSUPPORTED
-                                                                               : SLATE_E_INVALID_CODEC;
+    m.status = SLATE_E_INVALID_CODEC;
     write_meta(&a.meta[b], m, lane);
     return true;
   }
@@ -1042,6 +1083,17 @@ __device__ inline void zlib_lds(WaveBufs& w, uint8_t* zbase, int waves, int wave
   __syncthreads();
 }
 
+// CodecZstd LDS after the per-wave buffers: the predefined tables (one per workgroup, built
+// by wave 0), then a ZsScratch per wave.
+__device__ inline void zstd_lds(WaveBufs& w, uint8_t* zbase, int wave, int lane) {
+  ZsShared* sh = reinterpret_cast<ZsShared*>(zbase);
+  w.zsh = sh;
+  w.zss = reinterpret_cast<ZsScratch*>(zbase + kZsShared + size_t(wave) * kZsScratch);
+  if (wave == 0) zs_shared_build(sh, w.zss, lane);
+  __syncthreads();
+}
+
+template <int CK>
 __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
@@ -1050,32 +1102,37 @@ __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs 
   const uint32_t per_wave = kFastInCap + kFastOutCap;
   WaveBufs w{tab, smem + kTabBytes + wave * per_wave, smem + kTabBytes + wave * per_wave + kFastInCap,
              kFastInCap, kFastOutCap};
-  if (a.codec == SLATE_CODEC_ZLIB) zlib_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, kDecodeThreads / 64, wave, lane);
+  if (CK == 1) zlib_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, kDecodeThreads / 64, wave, lane);
+  if (CK == 2) zstd_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, wave, lane);
   const uint32_t waves = gridDim.x * (kDecodeThreads / 64);
   for (uint32_t b = blockIdx.x * (kDecodeThreads / 64) + wave; b < a.n; b += waves) {
-    if (!decode_block_wave(a, b, w, lane, true)) {
+    if (!decode_block_wave<CK>(a, b, w, lane, true)) {
       if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = b;
     }
   }
 }
 
+template <int CK>
 __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   load_crc_tables(tab);
   const int lane = threadIdx.x & 63;
   // CodecZlib: its tables take the top of the input staging area
-  const uint32_t in_cap = a.codec == SLATE_CODEC_ZLIB ? kLargeInCap - kZFixed - kZScratch : kLargeInCap;
+  const uint32_t in_cap = CK == 1 ? kLargeInCap - kZFixed - kZScratch
+                          : CK == 2 ? kLargeInCap - kZsShared - kZsScratch
+                                    : kLargeInCap;
   WaveBufs w{tab, smem + kTabBytes, smem + kTabBytes + kLargeInCap, in_cap, kLargeOutCap};
-  if (a.codec == SLATE_CODEC_ZLIB) zlib_lds(w, smem + kTabBytes + in_cap, 1, 0, lane);
+  if (CK == 1) zlib_lds(w, smem + kTabBytes + in_cap, 1, 0, lane);
+  if (CK == 2) zstd_lds(w, smem + kTabBytes + in_cap, 0, lane);
   uint32_t count = *a.large_count;
-  for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) decode_block_wave(a, a.large_list[k], w, lane, false);
+  for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) decode_block_wave<CK>(a, a.large_list[k], w, lane, false);
 }
 
 // --------------------------------------------------------------- launchers
 hipError_t decode_kernels_available() {
   hipFuncAttributes attr;
-  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&decode_fast_kernel));
+  return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&decode_fast_kernel<0>));
 }
 
 size_t decode_scratch_bytes(uint32_t n) {
@@ -1104,6 +1161,8 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
   plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
   if (codec == SLATE_CODEC_ZLIB && n > 0)
     plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
+  if (codec == SLATE_CODEC_ZSTD && n > 0)
+    plan_zstd_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
   scan_reduce_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
   scan_partials_kernel<<<1, kScanThreads, 0, st>>>(s.pa, s.pb, s.tiles);
   scan_apply_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
@@ -1137,13 +1196,23 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   if (a.codec == SLATE_CODEC_SNAPPY && !(a.debug & 16))
     return (a.debug & 32) ? launch_decode_lpb(st, a, num_cus) : launch_decode_lpb2(st, a, num_cus);
   const size_t lds = kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap) +
-                     (a.codec == SLATE_CODEC_ZLIB ? kZFixed + (kDecodeThreads / 64) * size_t(kZScratch) : 0);
+                     (a.codec == SLATE_CODEC_ZLIB ? kZFixed + (kDecodeThreads / 64) * size_t(kZScratch) : 0) +
+                     (a.codec == SLATE_CODEC_ZSTD ? kZsShared + (kDecodeThreads / 64) * size_t(kZsScratch) : 0);
   uint32_t wgs_needed = (a.n + kDecodeThreads / 64 - 1) / (kDecodeThreads / 64);
   uint32_t grid = min(wgs_needed, uint32_t(num_cus) * kDecodeWgPerCu);
-  decode_fast_kernel<<<grid, kDecodeThreads, lds, st>>>(a);
   const size_t lds_large = kTabBytes + size_t(kLargeInCap) + kLargeOutCap;
-  decode_large_kernel<<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  if (a.codec == SLATE_CODEC_ZLIB) {
+    decode_fast_kernel<1><<<grid, kDecodeThreads, lds, st>>>(a);
+    decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  } else if (a.codec == SLATE_CODEC_ZSTD) {
+    decode_fast_kernel<2><<<grid, kDecodeThreads, lds, st>>>(a);
+    decode_large_kernel<2><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  } else {
+    decode_fast_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a);
+    decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  }
   return hipGetLastError();
 }
 
 }  // namespace slate
+

@@ -1,0 +1,115 @@
+"""GPU parity for CodecZstd blocks (compress.Decode, compression.go:146-153) through the C ABI:
+block.Decode with Zstandard frames written by libzstd 1.4.9 (every level band and strategy,
+raw/RLE/compressed blocks, 1- and 4-stream Huffman literals, FSE/RLE/predefined/repeat tables,
+with and without content size and checksum, multi-block and concatenated frames), plus damaged
+frames with their status codes, bit-exact against the oracle (plan, meta, decoded bytes,
+rows).  tests/test_zstd_oracle.py pins the oracle to libzstd."""
+import random
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from tests import zstdgen
+
+from oracle import binding as ob
+from tests import blockgen as bg
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not zstdgen.available(), reason="libzstd not in this image")]
+LEVELS = [-5, -1, 1, 3, 6, 12, 19]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import slatecodec as sc
+    return sc.Context(0)
+
+
+def _crc(stream: bytes) -> bytes:
+    return stream + struct.pack(">I", zlib.crc32(stream))
+
+
+def _z(data: bytes, level=3, checksum=True, content_size=True, window_log=0, strategy=0) -> bytes:
+    return zstdgen.frame(data, level, checksum, content_size, window_log, strategy)
+
+
+def _compare(ctx, blocks, misalign=0):
+    blob, off = bg.pack(blocks, misalign)
+    g_out, g_off, g_meta, g_rows, g_rb = ctx.decode_batch(ob.ZSTD, blob, off)
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(ob.ZSTD, blob, off)
+    assert np.array_equal(g_off, o_off), "plan: out_off"
+    assert np.array_equal(g_rb, o_rb), "plan: row_base"
+    for i, blk in enumerate(blocks):
+        gm, om = g_meta[i], o_meta[i]
+        assert gm.tobytes() == om.tobytes(), (i, gm, om)
+        st = int(om["status"])
+        if st == 0 or 3 <= st <= 7:
+            dec = ob.zstd_decode(blk[:-4])[1]
+            a = int(o_off[i])
+            assert g_out[a:a + len(dec)].tobytes() == dec == o_out[a:a + len(dec)].tobytes(), i
+        if st == 0:
+            r0 = int(o_rb[i])
+            nr = min(int(om["n_rows"]), int(o_rb[i + 1]) - r0)
+            assert g_rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+    return o_meta
+
+
+def _sst_plain(rng, n_kv, block_size):
+    kvs = bg.random_kvs(rng, n_kv, alphabet=rng.choice([4, 256]))
+    return [b[:-4] for b in bg.sst_blocks(kvs, block_size, ob.NONE)]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_zstd_ssts(ctx, seed):
+    rng = random.Random(seed)
+    blocks = [_crc(_z(dec, rng.choice(LEVELS), rng.random() < 0.7, rng.random() < 0.7, rng.choice([0, 0, 10]),
+                      rng.choice([0, 0, 1, 5, 9])))
+              for dec in _sst_plain(rng, rng.randint(300, 1500), rng.choice([512, 4096]))]
+    meta = _compare(ctx, blocks, misalign=rng.randrange(16))
+    assert (meta["status"] == 0).all()
+
+
+def test_mixed_config_blocks(ctx):
+    """BASELINE configs[4]: 4 KiB blocks of 1 KiB V-half values and Zipf-prefixed 8-256 B keys, level 3 + checksum."""
+    kvs = bg.kv_mixed(2000)
+    blocks = [_crc(_z(b[:-4], 3, True)) for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+    meta = _compare(ctx, blocks, misalign=7)
+    assert (meta["status"] == 0).all()
+
+
+def test_large_and_concatenated_zstd_blocks(ctx):
+    """Blocks beyond the fast kernel's LDS budget (large-block kernel), multi-block frames
+    (small windows), concatenated and skippable frames."""
+    rng = random.Random(11)
+    blocks = [_crc(_z(dec, rng.choice([1, 3, 19]), True, rng.random() < 0.5, rng.choice([0, 10])))
+              for dec in _sst_plain(rng, 2500, 40000)]
+    decs = _sst_plain(rng, 400, 1024)
+    cat = b"".join(_z(d, rng.choice([1, 3]), rng.random() < 0.5, rng.random() < 0.5) for d in decs[:3])
+    blocks.append(_crc(cat[:0] + struct.pack("<II", 0x184D2A53, 3) + b"xyz" + cat))
+    _compare(ctx, blocks, misalign=5)
+
+
+def test_damaged_zstd_blocks(ctx):
+    rng = random.Random(9)
+    decs = _sst_plain(rng, 800, 1024)
+    blocks = []
+    for dec in decs:
+        f = bytearray(_z(dec, rng.choice([1, 3, 9]), rng.random() < 0.8, rng.random() < 0.8))
+        kind = rng.randrange(6)
+        if kind == 0:
+            f[rng.randrange(len(f))] ^= 1 << rng.randrange(8)
+        elif kind == 1:
+            f = f[: rng.randrange(len(f))]
+        elif kind == 2:
+            f += bytes(rng.randrange(256) for _ in range(rng.randint(1, 5)))
+        elif kind == 3:
+            i = rng.randrange(4, len(f))
+            f[i:i + 2] = bytes([rng.randrange(256), rng.randrange(256)])
+        elif kind == 4:
+            f[4] ^= rng.choice([1, 2, 8, 0x20, 0x80])
+        blocks.append(_crc(bytes(f)))
+    blocks += [_crc(b""), _crc(b"\x28\xb5"), _crc(b"\x28\xb5\x2f\xfd"), _crc(b"\x28\xb5\x2f\xfd\x00\x00\x07\x00\x00")]
+    meta = _compare(ctx, blocks, misalign=1)
+    st = set(int(x) for x in meta["status"])
+    assert {0, 58} <= st, st
