@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--blocks", type=int, default=1_000_000, help="blocks per GPU")
-    p.add_argument("--codec", choices=["snappy", "none", "lz4"], default="snappy")
+    p.add_argument("--codec", choices=["snappy", "none", "lz4", "zstd"], default="snappy",
+                   help="zstd runs BASELINE configs[4] (1 KiB values, Zipf-prefixed keys, libzstd level 3 + checksum)")
     p.add_argument("--values", choices=["half", "rand"], default="half")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="budget per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -65,11 +66,14 @@ def main():
     import slatecodec as sc
     from tools import workload as wl
 
-    codec = {"snappy": sc.SNAPPY, "none": sc.NONE, "lz4": sc.LZ4}[args.codec]
+    codec = {"snappy": sc.SNAPPY, "none": sc.NONE, "lz4": sc.LZ4, "zstd": sc.ZSTD}[args.codec]
     n = args.blocks
     t0 = time.time()
     spec = shard_spec(rank, n)
-    dec, dec_off = wl.decoded_blocks(n, seed=spec["seed"], half=(args.values == "half"), kv_begin=spec["kv_begin"])
+    if args.codec == "zstd":  # configs[4] "mixed"
+        dec, dec_off = wl.mixed_blocks(n, seed=spec["seed"])
+    else:
+        dec, dec_off = wl.decoded_blocks(n, seed=spec["seed"], half=(args.values == "half"), kv_begin=spec["kv_begin"])
     blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=min(16, os.cpu_count() or 4))
     gen_s = time.time() - t0
     dec_bytes = int(dec_off[-1])
@@ -157,18 +161,24 @@ def main():
             traffic = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": "decode_lpb2_kernel" if args.codec == "snappy" else "decode_fast_kernel", "kernel_ms": round(kern_ms, 4),
+                "kernel": {"snappy": "decode_lpb2_kernel", "zstd": "decode_fast_kernel<2>"}.get(args.codec, "decode_fast_kernel<0>"),
+                "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg, "alg_read_bytes": alg_read, "alg_write_bytes": alg_write,
                 "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
 
     result = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
               "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-              "data": "synthetic (SURVEY 8d keys k%015d, V-half values, " + {"snappy": "libsnappy-encoded)",
+              "data": ("synthetic (SURVEY 8d configs[4]: Zipf-prefixed 8-256 B keys, 1 KiB V-half values, libzstd "
+                       "level 3 + checksum frames)" if args.codec == "zstd" else
+                       "synthetic (SURVEY 8d keys k%015d, V-half values, " + {"snappy": "libsnappy-encoded)",
                                                                               "lz4": "liblz4 frames)",
-                                                                              "none": "CodecNone)"}[args.codec],
+                                                                              "none": "CodecNone)"}[args.codec]),
               "config": {"workload": ("configs[1]: 1 M x 4 KiB Snappy blocks, 100 B KV, device-resident decode"
                                       if args.codec == "snappy" and n == 1_000_000 and args.values == "half"
+                                      else f"configs[4] mixed: {n} x 4 KiB Zstd blocks, 1 KiB values, skewed key "
+                                      "prefixes, device-resident decode (not the headline config)"
+                                      if args.codec == "zstd"
                                       else f"{n} x 4 KiB {args.codec} blocks, 100 B KV ({args.values} values), "
                                       "device-resident decode (not the headline config)"),
                          "blocks_per_gpu": n, "codec": args.codec, "values": args.values, "block_size": 4096,

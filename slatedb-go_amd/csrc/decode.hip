@@ -960,7 +960,8 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   } else if (CK == 2 && a.codec == SLATE_CODEC_ZSTD) {
     uint32_t outn = 0;
     int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)
-                           : wave_zstd_decode(w.in, int32_t(shift), clen, w.out, uint32_t(dl), w.zss, w.zsh, lane, &outn);
+                           : wave_zstd_decode(w.in, int32_t(shift), clen, w.out, uint32_t(dl), w.zss, w.zsh, lane, &outn,
+                                              a.debug);
     if (st != SLATE_OK) {
       m.status = int16_t(st);
       write_meta(&a.meta[b], m, lane);
@@ -1099,9 +1100,11 @@ __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs 
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   load_crc_tables(tab);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t per_wave = kFastInCap + kFastOutCap;
-  WaveBufs w{tab, smem + kTabBytes + wave * per_wave, smem + kTabBytes + wave * per_wave + kFastInCap,
-             kFastInCap, kFastOutCap};
+  // CodecZstd: trimmed staging (two workgroups per CU with the tables); larger blocks
+  // take the large-block kernel
+  constexpr uint32_t in_cap = CK == 2 ? kZsFastInCap : kFastInCap, out_cap = CK == 2 ? kZsFastOutCap : kFastOutCap;
+  const uint32_t per_wave = in_cap + out_cap;
+  WaveBufs w{tab, smem + kTabBytes + wave * per_wave, smem + kTabBytes + wave * per_wave + in_cap, in_cap, out_cap};
   if (CK == 1) zlib_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, kDecodeThreads / 64, wave, lane);
   if (CK == 2) zstd_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, wave, lane);
   const uint32_t waves = gridDim.x * (kDecodeThreads / 64);
@@ -1195,9 +1198,10 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   // (bit 32: the v1 lane-per-block kernel, A/B only)
   if (a.codec == SLATE_CODEC_SNAPPY && !(a.debug & 16))
     return (a.debug & 32) ? launch_decode_lpb(st, a, num_cus) : launch_decode_lpb2(st, a, num_cus);
-  const size_t lds = kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap) +
-                     (a.codec == SLATE_CODEC_ZLIB ? kZFixed + (kDecodeThreads / 64) * size_t(kZScratch) : 0) +
-                     (a.codec == SLATE_CODEC_ZSTD ? kZsShared + (kDecodeThreads / 64) * size_t(kZsScratch) : 0);
+  const size_t lds = a.codec == SLATE_CODEC_ZSTD
+                         ? kTabBytes + (kDecodeThreads / 64) * size_t(kZsFastInCap + kZsFastOutCap + kZsScratch) + kZsShared
+                         : kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap) +
+                               (a.codec == SLATE_CODEC_ZLIB ? kZFixed + (kDecodeThreads / 64) * size_t(kZScratch) : 0);
   uint32_t wgs_needed = (a.n + kDecodeThreads / 64 - 1) / (kDecodeThreads / 64);
   uint32_t grid = min(wgs_needed, uint32_t(num_cus) * kDecodeWgPerCu);
   const size_t lds_large = kTabBytes + size_t(kLargeInCap) + kLargeOutCap;

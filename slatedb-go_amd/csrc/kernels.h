@@ -10,6 +10,8 @@ constexpr int kDecodeThreads = 256;          // 4 wavefronts, one block each at 
 constexpr uint32_t kDecodeWgPerCu = 4;       // LDS-limited residency (4 x 40 KiB)
 constexpr uint32_t kFastInCap = 4608;        // staged encoded block (incl. 16-byte misalignment)
 constexpr uint32_t kFastOutCap = 4608;       // decoded block
+constexpr uint32_t kZsFastInCap = 4224;      // CodecZstd fast-kernel staging: 2 x (4 waves + tables) per CU
+constexpr uint32_t kZsFastOutCap = 4112;
 constexpr uint32_t kLargeInCap = 65552;      // large-block kernel, one wave per workgroup
 constexpr uint32_t kLargeOutCap = 90112;
 // lane-per-block Snappy decode (decode_lpb.hip): one wave per workgroup, 432 B of

@@ -189,85 +189,69 @@ __device__ void zs_shared_build(ZsShared* sh, ZsScratch* sc, int lane) {
 }
 
 // ------------------------------------------------------------------ Huffman
-// FSE-compressed weights (lane 0): 0 / -1, *nw = number of decoded weights
-__device__ int zs_weights_fse(const uint8_t* base, int32_t off, uint32_t hb, ZsScratch* sc, int* nw_out) {
-  int al, last;
-  const int hs = zs_ncount(base, off, hb, sc->norm, 255, 6, &al, &last);
+// FSE-compressed weights (oracle zs_huf_read): the table description and build on lane 0,
+// then the two-state decode wave-uniform out of registers: lane u holds table cell u and
+// stream dword u (hb <= 127 bytes), so a symbol costs v_readlane + scalar bit arithmetic,
+// no LDS round trip.  0 / -1, *nw = the number of decoded weights.
+__device__ int zs_weights_fse(const uint8_t* base, int32_t off, uint32_t hb, ZsScratch* sc, int lane, int* nw_out) {
+  int hs = 0, al = 0, last = 0;
+  if (lane == 0) {
+    hs = zs_ncount(base, off, hb, sc->norm, 255, 6, &al, &last);
+    if (hs >= 0 && zs_fse_build(sc->wt, sc->norm, last, al, sc->next)) hs = -1;
+  }
+  hs = zrfl(hs);
+  al = zrfl(al);
   if (hs < 0) return -1;
-  if (zs_fse_build(sc->wt, sc->norm, last, al, sc->next)) return -1;
+  zs_sync();
   const int32_t so = off + hs;
-  int64_t pos = zs_bstart(base, so, hb - uint32_t(hs));
-  if (pos < 0) return -1;
-  const int64_t S = 8 * int64_t(so);
-  uint32_t s1 = uint32_t(zs_peek(base, S, pos, uint32_t(al)));
-  pos -= al;
-  uint32_t s2 = uint32_t(zs_peek(base, S, pos, uint32_t(al)));
-  pos -= al;
+  const uint32_t bn = hb - uint32_t(hs);
+  if (bn == 0) return -1;
+  const uint32_t tab = lane < (1 << al) ? *reinterpret_cast<const uint32_t*>(&sc->wt[lane]) : 0u;
+  const uint32_t win = uint32_t(lane) * 4 < bn ? lds_u32(base, so + 4 * lane) : 0u;
+  auto byte_at = [&](uint32_t i) -> uint32_t {
+    return (uint32_t(__builtin_amdgcn_readlane(win, int(i >> 2))) >> (8 * (i & 3))) & 0xFFu;
+  };
+  auto bits_at = [&](int64_t b, uint32_t k) -> uint32_t {  // k <= 24 bits at stream bit b >= 0
+    const uint32_t d = uint32_t(b >> 5);
+    const uint64_t v = uint64_t(uint32_t(__builtin_amdgcn_readlane(win, int(d)))) |
+                       (uint64_t(uint32_t(__builtin_amdgcn_readlane(win, int(d + 1 < 64 ? d + 1 : 63)))) << 32);
+    return uint32_t(v >> (b & 31)) & ((1u << k) - 1);
+  };
+  const uint32_t lastb = byte_at(bn - 1);
+  if (lastb == 0) return -1;
+  int64_t pos = 8 * int64_t(bn - 1) + (31 - __builtin_clz(lastb));
+  auto rd = [&](uint32_t k) -> uint32_t {
+    uint32_t v = 0;
+    if (k && pos > 0) v = pos >= int64_t(k) ? bits_at(pos - k, k) : bits_at(0, uint32_t(pos)) << (k - uint32_t(pos));
+    pos -= k;
+    return v;
+  };
+  uint32_t s1 = rd(uint32_t(al)), s2 = rd(uint32_t(al));
   int nw = 0;
-  for (;;) {  // two interleaved states until the stream overreads (oracle zs_huf_read)
+  for (;;) {  // two interleaved states until the stream overreads (FSE_decompress tail)
     if (nw > 253) return -1;
-    ZsFse e = sc->wt[s1];
-    sc->w[nw++] = e.sym;
-    s1 = e.base + uint32_t(zs_peek(base, S, pos, e.nb));
-    pos -= e.nb;
+    uint32_t e = uint32_t(__builtin_amdgcn_readlane(tab, int(s1)));
+    if (lane == 0) sc->w[nw] = uint8_t(e);
+    nw++;
+    s1 = (e >> 16) + rd((e >> 8) & 0xFF);
     if (pos < 0) {
-      sc->w[nw++] = sc->wt[s2].sym;
+      if (lane == 0) sc->w[nw] = uint8_t(__builtin_amdgcn_readlane(tab, int(s2)));
+      nw++;
       break;
     }
     if (nw > 253) return -1;
-    e = sc->wt[s2];
-    sc->w[nw++] = e.sym;
-    s2 = e.base + uint32_t(zs_peek(base, S, pos, e.nb));
-    pos -= e.nb;
+    e = uint32_t(__builtin_amdgcn_readlane(tab, int(s2)));
+    if (lane == 0) sc->w[nw] = uint8_t(e);
+    nw++;
+    s2 = (e >> 16) + rd((e >> 8) & 0xFF);
     if (pos < 0) {
-      sc->w[nw++] = sc->wt[s1].sym;
+      if (lane == 0) sc->w[nw] = uint8_t(__builtin_amdgcn_readlane(tab, int(s1)));
+      nw++;
       break;
     }
   }
   *nw_out = nw;
   return 0;
-}
-
-// Weight statistics (oracle zs_huf_read, lane 0): the implied last weight, the checks, and
-// each symbol's first slot in the weight-major table.  Returns tl, or -1.
-__device__ int zs_huf_stats(ZsScratch* sc, int nw) {
-  int16_t* rank = sc->norm;  // free once the weights are decoded
-  for (int k = 0; k < 12; k++) rank[k] = 0;
-  uint32_t total = 0;
-  for (int i = 0; i < nw; i++) {
-    const uint32_t k = sc->w[i];
-    if (k > 11) return -1;
-    rank[k]++;
-    total += (1u << k) >> 1;
-  }
-  if (total == 0) return -1;
-  const int tl = 32 - __builtin_clz(total);
-  if (tl > 11) return -1;
-  const uint32_t rest = (1u << tl) - total;
-  if (rest == 0 || (rest & (rest - 1))) return -1;
-  const uint32_t lastw = 32 - __builtin_clz(rest);
-  sc->w[nw] = uint8_t(lastw);
-  rank[lastw]++;
-  if (rank[1] < 2 || (rank[1] & 1)) return -1;
-  uint32_t cur[12];
-  uint32_t acc = 0;
-#pragma unroll
-  for (int k = 1; k < 12; k++) {
-    cur[k] = acc;
-    acc += uint32_t(k <= tl ? rank[k] : 0) << (k - 1);
-  }
-  for (int s2 = 0; s2 <= nw; s2++) {
-    const uint32_t k = sc->w[s2];
-    uint32_t p = 0;
-#pragma unroll
-    for (int j = 1; j < 12; j++)  // register-resident cursors (no dynamic indexing)
-      if (uint32_t(j) == k) {
-        p = cur[j];
-        cur[j] += 1u << (j - 1);
-      }
-    sc->next[s2] = uint16_t(p);
-  }
-  return tl;
 }
 
 // Huffman_Tree_Description at base[off, off+n): bytes used or -1; fills sc->huf, *tl
@@ -286,28 +270,60 @@ __device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScrat
     used = int(1 + nbytes);
   } else {
     if (1 + hb > n) return -1;
-    int r = 0, k = 0;
-    if (lane == 0) r = zs_weights_fse(base, off + 1, hb, sc, &k);
-    r = zrfl(r);
-    nw = zrfl(k);
-    if (r < 0) return -1;
+    int k = 0;
+    if (zs_weights_fse(base, off + 1, hb, sc, lane, &k) < 0) return -1;
+    nw = k;
     used = int(1 + hb);
   }
   zs_sync();
-  // weight statistics and each symbol's first table slot (oracle zs_huf_read), on lane 0:
-  // sc->norm[0..11] = symbols per weight, then sc->next[s] = symbol s's first slot
-  int tlv = 0;
-  if (lane == 0) tlv = zs_huf_stats(sc, nw);
-  tlv = zrfl(tlv);  // lane 0's result for every lane
-  if (tlv <= 0) return -1;
-  const uint32_t tl = uint32_t(tlv);
+  // weight statistics (oracle zs_huf_read), lane-parallel: lane k counts weight k
+  uint32_t cnt = 0, total = 0, bad = 0;
+  for (int c0 = 0; c0 < nw; c0 += kWave) {
+    const int i = c0 + lane;
+    const uint32_t my = i < nw ? uint32_t(sc->w[i]) : 0u;
+    bad |= my > 11 ? 1u : 0u;
+    total += my ? (1u << (my - 1)) : 0u;
+#pragma unroll
+    for (uint32_t k = 1; k <= 11; k++) {
+      const uint32_t c = uint32_t(__builtin_popcountll(__ballot(my == k)));
+      cnt += (uint32_t(lane) == k) ? c : 0u;
+    }
+  }
+  if (__ballot(bad != 0)) return -1;
+  for (int o = 32; o >= 1; o >>= 1) total += uint32_t(__shfl_xor(int(total), o, 64));
+  total = zrfl(total);
+  if (total == 0) return -1;
+  const uint32_t tl = 32 - __builtin_clz(total);  // highbit + 1
+  if (tl > 11) return -1;
+  const uint32_t rest = (1u << tl) - total;
+  if (rest & (rest - 1)) return -1;
+  const uint32_t lastw = 32 - __builtin_clz(rest);
+  if (lane == 0) sc->w[nw] = uint8_t(lastw);
+  cnt += (uint32_t(lane) == lastw) ? 1u : 0u;
+  const uint32_t r1 = uint32_t(__builtin_amdgcn_readlane(cnt, 1));
+  if (r1 < 2 || (r1 & 1)) return -1;
+  // weight-major table, symbol order within a weight: lane k holds weight k's next slot
+  uint32_t cur = 0, acc = 0;
+  for (uint32_t k = 1; k <= tl; k++) {
+    if (uint32_t(lane) == k) cur = acc;
+    acc += uint32_t(__builtin_amdgcn_readlane(cnt, int(k))) << (k - 1);
+  }
   zs_sync();
-  for (int s = lane; s <= nw; s += kWave) {
-    const uint32_t k = sc->w[s];
-    if (k) {
-      const uint16_t e = uint16_t(((tl + 1 - k) << 8) | uint32_t(s));
-      const uint32_t p0 = sc->next[s];
-      for (uint32_t i = 0; i < (1u << (k - 1)); i++) sc->huf[p0 + i] = e;
+  for (int c0 = 0; c0 <= nw; c0 += kWave) {
+    const int s = c0 + lane;
+    const uint32_t my = s <= nw ? uint32_t(sc->w[s]) : 0u;
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t k = 1; k <= 11; k++) {
+      const uint64_t m = __ballot(my == k);
+      const uint32_t before = uint32_t(__builtin_amdgcn_readlane(cur, int(k)));
+      const uint32_t rank = uint32_t(__builtin_popcountll(m & ((uint64_t(1) << lane) - 1)));
+      pos = (my == k) ? before + (rank << (k - 1)) : pos;
+      cur += (uint32_t(lane) == k) ? (uint32_t(__builtin_popcountll(m)) << (k - 1)) : 0u;
+    }
+    if (my) {
+      const uint16_t e = uint16_t(((tl + 1 - my) << 8) | uint32_t(s));
+      for (uint32_t i = 0; i < (1u << (my - 1)); i++) sc->huf[pos + i] = e;
     }
   }
   zs_sync();
@@ -364,8 +380,11 @@ __device__ int zs_table(uint32_t mode, const uint8_t* base, int32_t off, uint32_
 
 // A compressed block at base[off, off+n) appended to out at *d (out == nullptr: sizes
 // only).  fstart = the frame's first output byte.  Status codes as oracle zs_block.
+// dbg: profiling ablations only (SLATE_DEBUG_MODE bits 17 skip the Huffman streams, 19 skip
+// the sequence copies); 0 in production.
 __device__ int zs_block(const uint8_t* base, int32_t off, uint32_t n, uint8_t* out, uint32_t cap, uint32_t* d,
-                        uint32_t fstart, uint32_t bmax, ZsScratch* sc, const ZsShared* sh, ZsState& st, int lane) {
+                        uint32_t fstart, uint32_t bmax, ZsScratch* sc, const ZsShared* sh, ZsState& st, int lane,
+                        uint32_t dbg = 0) {
   if (n < 1) return SLATE_E_ZSTD_CORRUPT;
   const uint32_t b0 = zrfl(uint32_t(base[off]));
   const uint32_t type = b0 & 3, sf = (b0 >> 2) & 3;
@@ -459,7 +478,7 @@ __device__ int zs_block(const uint8_t* base, int32_t off, uint32_t n, uint8_t* o
       lo = seg * uint32_t(lane < 3 ? lane : 3);
     }
     bool badl = false;
-    if (uint32_t(lane) < streams) {
+    if (uint32_t(lane) < streams && !(dbg & (1u << 17))) {
       int64_t bp = zs_bstart(base, int32_t(sb), sl);
       if (bp < 0) {
         badl = true;
@@ -467,8 +486,27 @@ __device__ int zs_block(const uint8_t* base, int32_t off, uint32_t n, uint8_t* o
         const int64_t S = 8 * int64_t(sb);
         const uint32_t tl = st.tl;
         uint8_t* dst = out ? out + lbase + lo : nullptr;
+        // 56-bit register window over stream bits [clo, clo + 56): one LDS refill per ~5
+        // symbols instead of a bit fetch per symbol; the stream's first bits (an overread
+        // pads with zeros) go through zs_peek
+        const uint32_t tmask = (1u << tl) - 1;
+        int64_t clo = 0;
+        uint64_t cv = 0;
+        bool have = false;
         for (uint32_t i = 0; i < m; i++) {
-          const uint32_t e = sc->huf[zs_peek(base, S, bp, tl)];
+          const int64_t lo2 = bp - int64_t(tl);
+          uint32_t v;
+          if (have && lo2 >= clo) {
+            v = uint32_t(cv >> (lo2 - clo)) & tmask;
+          } else if (lo2 >= 0) {
+            clo = bp > 56 ? bp - 56 : 0;
+            cv = zs_bits(base, S + clo, 56);
+            have = true;
+            v = uint32_t(cv >> (lo2 - clo)) & tmask;
+          } else {
+            v = uint32_t(zs_peek(base, S, bp, tl));
+          }
+          const uint32_t e = sc->huf[v];
           if (dst) dst[i] = uint8_t(e);
           bp -= e >> 8;
         }
@@ -562,7 +600,7 @@ __device__ int zs_block(const uint8_t* base, int32_t off, uint32_t n, uint8_t* o
       if (uint64_t(o - d0) + ll + ml > bmax || uint64_t(o) + ll + ml > cap) return SLATE_E_ZSTD_CORRUPT;
       // the write cursor must stay below the unread literals (the oracle fails at the block end)
       if (uint64_t(o) + ll + ml > uint64_t(lbase) + lp + ll) return SLATE_E_ZSTD_CORRUPT;
-      if (out) {  // literals: dst <= src, 64 at a time, each chunk read before it is written
+      if (out && !(dbg & (1u << 19))) {  // literals: dst <= src, 64 at a time, each chunk read before it is written
         for (uint32_t c = 0; c < ll; c += kWave) {
           const uint32_t j = c + uint32_t(lane);
           const uint8_t v = j < ll ? out[lbase + lp + j] : 0;
@@ -573,7 +611,7 @@ __device__ int zs_block(const uint8_t* base, int32_t off, uint32_t n, uint8_t* o
       lp += ll;
       o += ll;
       if (offv > o - fstart) return SLATE_E_ZSTD_CORRUPT;
-      if (out) {
+      if (out && !(dbg & (1u << 19))) {
         const uint32_t off32 = uint32_t(offv);
         zs_sync();
         if (off32 >= ml) {
@@ -684,7 +722,7 @@ __device__ inline uint32_t zs_le24(const uint8_t* base, int32_t off) {
 // One frame at base[off + *pos] (magic included; the stream is base[off, off+n)) into
 // out at *d (oracle zs_frame).
 __device__ int zs_frame(const uint8_t* base, int32_t off, uint32_t n, uint32_t* posp, uint8_t* out, uint32_t cap,
-                        uint32_t* d, ZsScratch* sc, const ZsShared* sh, int lane) {
+                        uint32_t* d, ZsScratch* sc, const ZsShared* sh, int lane, uint32_t dbg = 0) {
   uint32_t p = *posp + 4;
   const ZsHdr h = zs_header(base, off + int32_t(p), n - p);
   if (h.status) return int(h.status);
@@ -716,7 +754,7 @@ __device__ int zs_frame(const uint8_t* base, int32_t off, uint32_t n, uint32_t* 
       p += 1;
     } else {
       if (n - p < bs) return SLATE_E_UNEXPECTED_EOF;
-      const int r = zs_block(base, off + int32_t(p), bs, out, cap, d, fstart, bmax, sc, sh, st, lane);
+      const int r = zs_block(base, off + int32_t(p), bs, out, cap, d, fstart, bmax, sc, sh, st, lane, dbg);
       if (r) return r;
       p += bs;
     }
@@ -725,7 +763,7 @@ __device__ int zs_frame(const uint8_t* base, int32_t off, uint32_t n, uint32_t* 
   if (h.has_fcs && uint64_t(*d - fstart) != h.fcs) return SLATE_E_ZSTD_FRAME_SIZE;
   if (h.checksum) {
     if (n - p < 4) return SLATE_E_UNEXPECTED_EOF;
-    if (out) {
+    if (out && !(dbg & (1u << 18))) {  // bit 18: skip the XXH64 (profiling only)
       zs_sync();
       const uint32_t want = zrfl(lds_u32(base, off + int32_t(p)));
       if (uint32_t(wave_xxh64(out, fstart, *d - fstart, lane)) != want) return SLATE_E_ZSTD_CHECKSUM;
@@ -739,7 +777,7 @@ __device__ int zs_frame(const uint8_t* base, int32_t off, uint32_t n, uint32_t* 
 // compress.Decode(CodecZstd) of base[off, off+n) into out[0, cap) (out == nullptr: sizes
 // only); *out_len = bytes produced (also on failure).  oracle zs_frames.
 __device__ int wave_zstd_decode(const uint8_t* base, int32_t off, uint32_t n, uint8_t* out, uint32_t cap, ZsScratch* sc,
-                                const ZsShared* sh, int lane, uint32_t* out_len) {
+                                const ZsShared* sh, int lane, uint32_t* out_len, uint32_t dbg = 0) {
   uint32_t pos = 0, d = 0;
   int st = SLATE_OK;
   while (pos < n) {
@@ -753,7 +791,7 @@ __device__ int wave_zstd_decode(const uint8_t* base, int32_t off, uint32_t n, ui
       continue;
     }
     if (magic != 0xFD2FB528u) { st = SLATE_E_ZSTD_MAGIC; break; }
-    st = zs_frame(base, off, n, &pos, out, cap, &d, sc, sh, lane);
+    st = zs_frame(base, off, n, &pos, out, cap, &d, sc, sh, lane, dbg);
     if (st != SLATE_OK) break;
   }
   *out_len = d;

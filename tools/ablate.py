@@ -22,7 +22,12 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 200_000
     modes = [int(x, 0) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "4", "8", "15"])]
     codec = int(os.environ.get("SLATE_ABLATE_CODEC", sc.SNAPPY))  # 3: LZ4 frames
-    blob, in_off, dec_bytes = wl.snappy_vhalf(n, codec=codec)
+    if codec == sc.ZSTD:  # configs[4] mixed; zstd bits: 2 skip decompression, 1<<17 Huffman streams,
+        dec, doff = wl.mixed_blocks(n)  # 1<<18 XXH64, 1<<19 sequence copies
+        blob, in_off = wl.encode_blocks(codec, dec, doff)
+        dec_bytes = int(doff[-1])
+    else:
+        blob, in_off, dec_bytes = wl.snappy_vhalf(n, codec=codec)
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
     ctx = sc.Context(0)

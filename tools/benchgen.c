@@ -32,6 +32,27 @@ int bg_init_lz4(const char* liblz4) {
   g_lz4f_err = (lz4f_err_fn)dlsym(h, "LZ4F_isError");
   return (g_lz4f && g_lz4f_err) ? 0 : -2;
 }
+/* libzstd 1.4.9 (dlopen): level 3 + content checksum + content size, one CCtx per call */
+typedef void* (*zcreate_fn)(void);
+typedef size_t (*zfree_fn)(void*);
+typedef size_t (*zsetp_fn)(void*, int, int);
+typedef size_t (*zc2_fn)(void*, void*, size_t, const void*, size_t);
+typedef unsigned (*zerr_fn)(size_t);
+static zcreate_fn g_zcreate;
+static zfree_fn g_zfree;
+static zsetp_fn g_zsetp;
+static zc2_fn g_zc2;
+static zerr_fn g_zerr;
+int bg_init_zstd(const char* libzstd) {
+  void* h = dlopen(libzstd, RTLD_NOW);
+  if (!h) return -1;
+  g_zcreate = (zcreate_fn)dlsym(h, "ZSTD_createCCtx");
+  g_zfree = (zfree_fn)dlsym(h, "ZSTD_freeCCtx");
+  g_zsetp = (zsetp_fn)dlsym(h, "ZSTD_CCtx_setParameter");
+  g_zc2 = (zc2_fn)dlsym(h, "ZSTD_compress2");
+  g_zerr = (zerr_fn)dlsym(h, "ZSTD_isError");
+  return (g_zcreate && g_zfree && g_zsetp && g_zc2 && g_zerr) ? 0 : -2;
+}
 static uint32_t g_tab[256];
 
 static uint32_t crc32(const uint8_t* p, size_t n) {
@@ -59,6 +80,13 @@ typedef struct {
 
 static void* work(void* arg) {
   job_t* j = (job_t*)arg;
+  void* zc = NULL;
+  if (j->codec == 4) {
+    zc = g_zcreate();
+    g_zsetp(zc, 100, 3);  /* ZSTD_c_compressionLevel */
+    g_zsetp(zc, 201, 1);  /* ZSTD_c_checksumFlag */
+    g_zsetp(zc, 200, 1);  /* ZSTD_c_contentSizeFlag */
+  }
   for (uint64_t i = j->lo; i < j->hi; i++) {
     const uint8_t* s = j->src + j->src_off[i];
     size_t n = j->src_off[i + 1] - j->src_off[i];
@@ -74,11 +102,17 @@ static void* work(void* arg) {
       if (g_lz4f_err(r)) { j->rc = -4; return NULL; }
       cl = r;
     }
+    else if (j->codec == 4) {
+      size_t r = g_zc2(zc, d, j->stride - 4, s, n);
+      if (g_zerr(r)) { j->rc = -5; g_zfree(zc); return NULL; }
+      cl = r;
+    }
     else if (g_compress((const char*)s, n, (char*)d, &cl) != 0) { j->rc = -3; return NULL; }
     uint32_t c = crc32(d, cl);
     d[cl] = (uint8_t)(c >> 24); d[cl + 1] = (uint8_t)(c >> 16); d[cl + 2] = (uint8_t)(c >> 8); d[cl + 3] = (uint8_t)c;
     j->dst_len[i] = cl + 4;
   }
+  if (zc) g_zfree(zc);
   return NULL;
 }
 
@@ -154,4 +188,83 @@ void bg_compact(const uint8_t* slots, uint64_t stride, const uint64_t* len, uint
     p += len[i];
   }
   blob_off[n] = p;
+}
+
+/* BASELINE configs[4] ("mixed") decoded blocks: ascending keys of 8-256 bytes sharing
+ * 3 + (Zipf(s=1.2) - 1) bytes with the previous key (the 3-byte head absorbs carries; same
+ * rule as tests/blockgen.py kv_mixed, with a splitmix64 stream and the Zipf law truncated at
+ * 256), 1 KiB V-half values (r||r, 512 B halves), greedy block fill (block.go:162-182). */
+static uint64_t sm64(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t bg_build_mixed(uint64_t seed, uint64_t n_kv, uint64_t block_size, uint8_t* out, uint64_t* out_off,
+                        uint64_t max_blocks) {
+  static double cdf[257];
+  double acc = 0;
+  for (int k = 1; k <= 256; k++) { acc += 1.0 / __builtin_pow(k, 1.2); cdf[k] = acc; }
+  uint64_t st = seed;
+  uint8_t prev[256], key[256], first[256], r[512];
+  uint32_t plen = 0, flen = 0;
+  uint64_t nb = 0, pos = 0, i = 0;
+  uint16_t offs[4096];
+  uint32_t n = 0, dlen = 0;
+  uint8_t* blk = out;
+  out_off[0] = 0;
+  while (i < n_kv && nb < max_blocks) {
+    /* next key */
+    uint32_t ln = 8 + (uint32_t)(sm64(&st) % 249), klen;
+    if (plen == 0) {
+      memcpy(key, "aaaa", 4); klen = 4;
+    } else {
+      double u = (double)(sm64(&st) >> 11) / 9007199254740992.0 * acc;
+      int z = 1;
+      while (z < 256 && cdf[z] < u) z++;
+      int p = 3 + z - 1;
+      if (p > (int)plen - 1) p = (int)plen - 1;
+      if (p > (int)ln - 1) p = (int)ln - 1;
+      memcpy(key, prev, (size_t)p + 1);
+      while (key[p] >= 0xFE) p--;  /* carry left (the head starts at "aaaa") */
+      key[p] = (uint8_t)(key[p] + 1 + (sm64(&st) & 1));
+      klen = (uint32_t)p + 1;
+    }
+    while (klen < ln) key[klen++] = (uint8_t)('a' + sm64(&st) % 26);
+    for (int b = 0; b < 512; b += 8) { uint64_t x = sm64(&st); memcpy(r + b, &x, 8); }
+    /* block.Builder.Add */
+    uint32_t p = 0;
+    if (n) while (p < flen && p < klen && first[p] == key[p]) p++;
+    uint32_t row = 4 + (klen - p) + 9 + 4 + 1024;
+    if ((uint64_t)2 + 2 * n + dlen + 2 + row > block_size && n) {  /* finish the block, retry the key */
+      for (uint32_t k = 0; k < n; k++) put16(blk + dlen + 2 * k, offs[k]);
+      put16(blk + dlen + 2 * n, n);
+      pos += dlen + 2 * n + 2;
+      out_off[++nb] = pos;
+      blk = out + pos;
+      n = 0; dlen = 0;
+      if (nb == max_blocks) break;
+      p = 0;
+      row = 4 + klen + 9 + 4 + 1024;
+    }
+    uint8_t* w = blk + dlen;
+    put16(w, p); put16(w + 2, klen - p);
+    memcpy(w + 4, key + p, klen - p);
+    memset(w + 4 + klen - p, 0, 9);
+    uint8_t* v = w + 4 + klen - p + 9;
+    v[0] = 0; v[1] = 0; v[2] = 4; v[3] = 0;  /* BE32 1024 */
+    memcpy(v + 4, r, 512); memcpy(v + 4 + 512, r, 512);
+    offs[n++] = (uint16_t)dlen;
+    dlen += row;
+    if (n == 1) { memcpy(first, key, klen); flen = klen; }
+    memcpy(prev, key, klen); plen = klen;
+    i++;
+  }
+  if (n && nb < max_blocks) {
+    for (uint32_t k = 0; k < n; k++) put16(blk + dlen + 2 * k, offs[k]);
+    put16(blk + dlen + 2 * n, n);
+    pos += dlen + 2 * n + 2;
+    out_off[++nb] = pos;
+  }
+  return nb;
 }

@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "libbenchgen.so")
 LIBSNAPPY = "/opt/conda/lib/libsnappy.so.1"
 LIBLZ4 = "/opt/conda/lib/liblz4.so.1"
+LIBZSTD = "/opt/conda/lib/libzstd.so.1"
 
 _lib = None
 
@@ -36,6 +37,10 @@ def lib():
             raise RuntimeError(f"benchgen: cannot load {LIBSNAPPY} ({rc})")
         L.bg_init_lz4.argtypes = [C.c_char_p]
         L.bg_init_lz4(LIBLZ4.encode())  # codec 3 (LZ4 frames) only: optional
+        L.bg_init_zstd.argtypes = [C.c_char_p]
+        L.bg_init_zstd(LIBZSTD.encode())  # codec 4 (Zstd level 3 + checksum) only: optional
+        L.bg_build_mixed.restype = C.c_uint64
+        L.bg_build_mixed.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64]
         _lib = L
     return _lib
 
@@ -51,6 +56,15 @@ def decoded_blocks(n_blocks: int, seed: int = 20250307, half: bool = True, block
     off = np.zeros(n_blocks + 1, np.uint64)
     nb = lib().bg_build_blocks(kv_begin, n_kv, rv.ctypes.data, rv.shape[1], int(half), block_size,
                                out.ctypes.data, off.ctypes.data, n_blocks)
+    assert nb == n_blocks, (nb, n_blocks)
+    return out[: int(off[nb])], off
+
+
+def mixed_blocks(n_blocks: int, seed: int = 20250307, block_size: int = 4096):
+    """BASELINE configs[4] decoded blocks (1 KiB V-half values, Zipf-prefixed 8-256 B keys)."""
+    out = np.empty(n_blocks * (block_size + 256), np.uint8)
+    off = np.zeros(n_blocks + 1, np.uint64)
+    nb = lib().bg_build_mixed(seed, n_blocks * 8 + 64, block_size, out.ctypes.data, off.ctypes.data, n_blocks)
     assert nb == n_blocks, (nb, n_blocks)
     return out[: int(off[nb])], off
 
