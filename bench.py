@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--values", choices=["half", "rand"], default="half")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="budget per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cache", default="", help="directory to reuse the generated workload from (profiling runs: "
+                   "the zstd generator's libzstd clashes with the profiler's own copy)")
     p.add_argument("--no-host-io", action="store_true")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_decode_latest.json"))
     return p.parse_args()
@@ -70,11 +72,21 @@ def main():
     n = args.blocks
     t0 = time.time()
     spec = shard_spec(rank, n)
-    if args.codec == "zstd":  # configs[4] "mixed"
-        dec, dec_off = wl.mixed_blocks(n, seed=spec["seed"])
+    cache = (os.path.join(args.cache, f"wl_{args.codec}_{args.values}_{n}_{spec['seed']}_{spec['kv_begin']}")
+             if args.cache else "")
+    if cache and os.path.exists(cache + "_blob.npy"):
+        dec, dec_off, blob, in_off = (np.load(cache + f"_{k}.npy") for k in ("dec", "dec_off", "blob", "in_off"))
     else:
-        dec, dec_off = wl.decoded_blocks(n, seed=spec["seed"], half=(args.values == "half"), kv_begin=spec["kv_begin"])
-    blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=min(16, os.cpu_count() or 4))
+        if args.codec == "zstd":  # configs[4] "mixed"
+            dec, dec_off = wl.mixed_blocks(n, seed=spec["seed"])
+        else:
+            dec, dec_off = wl.decoded_blocks(n, seed=spec["seed"], half=(args.values == "half"),
+                                             kv_begin=spec["kv_begin"])
+        blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=min(16, os.cpu_count() or 4))
+        if cache:
+            os.makedirs(args.cache, exist_ok=True)
+            for k, v in (("dec", dec), ("dec_off", dec_off), ("blob", blob), ("in_off", in_off)):
+                np.save(cache + f"_{k}.npy", v)
     gen_s = time.time() - t0
     dec_bytes = int(dec_off[-1])
     enc_bytes = int(in_off[-1])
@@ -306,6 +318,10 @@ def host_io_rate(torch, sc, ctx, codec, blob, in_off, dec_bytes, device):
             "path": "slate_block_decode_batch (pageable host buffers, one stream, plan sync)"}
 
 
+CODEC_RESTATEMENT = {0: "no codec", 1: "golang/snappy", 2: "compress/zlib+flate", 3: "LZ4 frame",
+                     4: "RFC 8878 zstd (oracle/zstd_oracle.c)"}
+
+
 def cpu_baseline(codec, blob, in_off, seconds):
     """The oracle (C restatement of the Go path) timed on this host: bounded sample."""
     from oracle import binding as ob
@@ -337,7 +353,8 @@ def cpu_baseline(codec, blob, in_off, seconds):
     mt = max(res)
     return {"value": round(res[mt][0], 3), "unit": "GiB/s", "cores": mt, "kind": "port",
             "sample": f"first {res[mt][1]} of the same blocks, oracle/slate_oracle.c block decode "
-                      f"(CRC32 + golang/snappy restatement + offsets + row walk), {mt} threads",
+                      f"(CRC32 + {CODEC_RESTATEMENT.get(codec, 'codec')} restatement + offsets + row walk), "
+                      f"{mt} threads",
             "single_thread": {"value": round(res[1][0], 3), "cores": 1, "blocks": res[1][1]},
             "cpu_model": cpu_model}
 
