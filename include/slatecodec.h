@@ -112,6 +112,7 @@ enum slate_status {
   SLATE_E_INVALID_ARG = 102,
   SLATE_E_CAPACITY = 103,           /* caller-provided output buffer too small */
   SLATE_E_OOM = 104,
+  SLATE_E_MERGE_UNSORTED = 105,     /* an iterator handed to the merge is not sorted (merge.go's precondition) */
 };
 
 /* ---- layouts ----------------------------------------------------------------- */
@@ -295,6 +296,25 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
 /* Filter.HasKey (bloom.go:19), batched on the GPU: out[i] = 1 if key i may be present. */
 int slate_bloom_has_keys(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len,
                          const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint8_t* out);
+
+/* ---- compaction merge (iter.MergeSort, internal/iter/merge.go:12-111) ----------------- */
+/* k sorted iterators, concatenated: key i = keys[key_off[i]..key_off[i+1]), iterator j holds
+ * elements [src_start[j], src_start[j+1]) (src_start: k+1 host values, src_start[0] = 0,
+ * n = src_start[k] < 2^32 - 1).  out_idx[0..*n_out) receives the element index of every entry
+ * MergeSort.Next (merge.go:54-76) returns, in order: keys ascending, on equal keys the entry of
+ * the lowest iterator index, later duplicates dropped, empty keys never returned (lastKey starts
+ * nil).  An unsorted iterator returns SLATE_E_MERGE_UNSORTED (Go does not check; its heap
+ * output for such input is unspecified).  Replaces NewMergeSort + the Next loop of
+ * executeCompaction (compaction/executor.go:92-151). */
+int slate_merge_sorted(slate_ctx* ctx, uint32_t k, const uint8_t* keys, const uint64_t* key_off,
+                       const uint64_t* src_start, uint32_t* out_idx, uint64_t* n_out);
+/* Device-resident variant on the context's stream: d_keys/d_key_off/d_out_idx/d_n_out/d_flags/
+ * d_scratch are device pointers, d_scratch holds slate_merge_scratch_bytes(n, k) bytes, and
+ * *d_flags bit 0 is set when an iterator is not sorted.  src_start stays a host array. */
+size_t slate_merge_scratch_bytes(uint64_t n, uint32_t k);
+int slate_merge_sorted_device(slate_ctx* ctx, uint32_t k, const uint8_t* d_keys, const uint64_t* d_key_off,
+                              const uint64_t* src_start, uint32_t* d_out_idx, uint64_t* d_n_out,
+                              uint32_t* d_flags, void* d_scratch);
 
 #ifdef __cplusplus
 }

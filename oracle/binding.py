@@ -131,6 +131,7 @@ def lib():
             "or_sst_table_info": (C.c_int, [C.c_void_p, C.POINTER(SstInfo), u8p, C.c_size_t]),
             "or_sst_table_bloom": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), u16p, u8p, C.c_size_t, szp]),
             "or_sst_read_info": (C.c_int, [u8p, C.c_size_t, C.POINTER(SstInfo), u8p, C.c_size_t]),
+            "or_merge_sort": (C.c_int, [C.c_uint32, u8p, u64p, u64p, u32p, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -572,3 +573,27 @@ def sst_read_info(sst: bytes) -> tuple[int, dict]:
     d = {f: getattr(info, f) for f, _ in SstInfo._fields_}
     d["first_key"] = fk[: info.first_key_len].tobytes()
     return st, d
+
+
+def merge_arrays(keys: np.ndarray, key_off: np.ndarray, src_start: np.ndarray) -> np.ndarray:
+    """iter.MergeSort (merge.go:12-111) over k concatenated sorted iterators: element indices
+    of the entries Next() returns, in order (u32)."""
+    keys = np.ascontiguousarray(keys, np.uint8) if len(keys) else np.zeros(1, np.uint8)
+    key_off = np.ascontiguousarray(key_off, np.uint64)
+    src_start = np.ascontiguousarray(src_start, np.uint64)
+    k = len(src_start) - 1
+    out = np.zeros(max(int(src_start[-1]), 1), np.uint32)
+    n = C.c_uint64(0)
+    st = lib().or_merge_sort(k, keys.ctypes.data_as(u8p), key_off.ctypes.data_as(u64p),
+                             src_start.ctypes.data_as(u64p), out.ctypes.data_as(u32p), C.byref(n))
+    assert st == 0, st
+    return out[: n.value]
+
+
+def merge_sort(sources: list[list[bytes]]) -> np.ndarray:
+    """merge_arrays over a list of per-iterator key lists."""
+    flat = [k for s in sources for k in s]
+    kd, ko = _arena(flat)
+    ss = np.zeros(len(sources) + 1, np.uint64)
+    ss[1:] = np.cumsum([len(s) for s in sources])
+    return merge_arrays(kd, ko, ss)

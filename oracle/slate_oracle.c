@@ -1559,3 +1559,98 @@ int or_sst_read_info(const uint8_t* sst, size_t n, or_sst_info* info, uint8_t* f
   if (mo > oi) return OR_E_BLOB_RANGE; /* bytesBlob.ReadRange bounds (blob.go:24) */
   return or_decode_info(sst + mo, (size_t)(oi - mo), info, fk, fk_cap);
 }
+
+/* ------------------------------------------------------------------ iter.MergeSort */
+/* merge.go:84-95 heapItem.Compare: bytes.Compare on keys, then the iterator index. */
+static int merge_item_cmp(const uint8_t* keys, const uint64_t* key_off, uint64_t ea, uint32_t ia, uint64_t eb,
+                          uint32_t ib) {
+  const uint64_t la = key_off[ea + 1] - key_off[ea], lb = key_off[eb + 1] - key_off[eb];
+  const uint64_t m = la < lb ? la : lb;
+  int c = m ? memcmp(keys + key_off[ea], keys + key_off[eb], m) : 0;
+  if (c == 0) c = la < lb ? -1 : (la > lb ? 1 : 0);
+  if (c == 0) c = ia < ib ? -1 : (ia > ib ? 1 : 0);
+  return c;
+}
+
+typedef struct {
+  uint64_t e;  /* element (global index) */
+  uint32_t it; /* iterator index */
+} or_heap_item;
+
+static void merge_sift_down(or_heap_item* h, size_t n, size_t i, const uint8_t* keys, const uint64_t* key_off) {
+  for (;;) {
+    size_t l = 2 * i + 1, s = i;
+    if (l < n && merge_item_cmp(keys, key_off, h[l].e, h[l].it, h[s].e, h[s].it) < 0) s = l;
+    if (l + 1 < n && merge_item_cmp(keys, key_off, h[l + 1].e, h[l + 1].it, h[s].e, h[s].it) < 0) s = l + 1;
+    if (s == i) return;
+    or_heap_item t = h[i];
+    h[i] = h[s];
+    h[s] = t;
+    i = s;
+  }
+}
+
+static void merge_sift_up(or_heap_item* h, size_t i, const uint8_t* keys, const uint64_t* key_off) {
+  while (i > 0) {
+    size_t p = (i - 1) / 2;
+    if (merge_item_cmp(keys, key_off, h[i].e, h[i].it, h[p].e, h[p].it) >= 0) return;
+    or_heap_item t = h[i];
+    h[i] = h[p];
+    h[p] = t;
+    i = p;
+  }
+}
+
+int or_merge_sort(uint32_t k, const uint8_t* keys, const uint64_t* key_off, const uint64_t* src_start,
+                  uint32_t* out_idx, uint64_t* n_out) {
+  *n_out = 0;
+  if (k == 0) return OR_OK;
+  or_heap_item* h = (or_heap_item*)malloc(sizeof(or_heap_item) * k);
+  uint64_t* next = (uint64_t*)malloc(sizeof(uint64_t) * k);
+  if (!h || !next) {
+    free(h);
+    free(next);
+    return OR_E_INVALID_ARG;
+  }
+  size_t hn = 0;
+  /* NewMergeSort (merge.go:30-50): the first entry of every iterator */
+  for (uint32_t i = 0; i < k; i++) {
+    next[i] = src_start[i];
+    if (next[i] < src_start[i + 1]) {
+      h[hn].e = next[i]++;
+      h[hn].it = i;
+      merge_sift_up(h, hn++, keys, key_off);
+    }
+  }
+  /* Next (merge.go:54-76) */
+  int have_last = 0; /* lastKey == nil */
+  uint64_t last = 0;
+  uint64_t n = 0;
+  while (hn > 0) {
+    or_heap_item it = h[0];
+    h[0] = h[--hn];
+    merge_sift_down(h, hn, 0, keys, key_off);
+    if (next[it.it] < src_start[it.it + 1]) {
+      h[hn].e = next[it.it]++;
+      h[hn].it = it.it;
+      merge_sift_up(h, hn++, keys, key_off);
+    }
+    const uint64_t len = key_off[it.e + 1] - key_off[it.e];
+    int equal;
+    if (!have_last) {
+      equal = len == 0; /* bytes.Equal(key, nil) */
+    } else {
+      const uint64_t ll = key_off[last + 1] - key_off[last];
+      equal = ll == len && (len == 0 || memcmp(keys + key_off[last], keys + key_off[it.e], len) == 0);
+    }
+    if (!equal) {
+      last = it.e;
+      have_last = 1;
+      out_idx[n++] = (uint32_t)it.e;
+    }
+  }
+  free(h);
+  free(next);
+  *n_out = n;
+  return OR_OK;
+}

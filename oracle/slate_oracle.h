@@ -190,6 +190,15 @@ int or_sst_table_bloom(const or_sst_builder* b, int* present, uint16_t* num_prob
 /* ReadInfo (decode.go:25) */
 int or_sst_read_info(const uint8_t* sst, size_t n, or_sst_info* info, uint8_t* fk, size_t fk_cap);
 
+/* iter.MergeSort (internal/iter/merge.go:12-111): k sorted iterators, concatenated.
+ * keys/key_off: n = src_start[k] keys (key i = keys[key_off[i]..key_off[i+1])); iterator j holds
+ * elements [src_start[j], src_start[j+1]).  out_idx receives the element index of every entry Next()
+ * returns, in order; *n_out their count.  Heap order is (bytes.Compare(key), iterator index)
+ * (merge.go:88-95); an entry is returned only when its key differs from the last returned key
+ * (merge.go:67-72), and lastKey starts nil, so empty keys are never returned. */
+int or_merge_sort(uint32_t k, const uint8_t* keys, const uint64_t* key_off, const uint64_t* src_start,
+                  uint32_t* out_idx, uint64_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

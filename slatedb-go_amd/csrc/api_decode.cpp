@@ -71,6 +71,7 @@ const char* slate_status_string(int s) {
     case SLATE_E_INVALID_ARG: return "invalid argument";
     case SLATE_E_CAPACITY: return "output buffer too small";
     case SLATE_E_OOM: return "out of memory";
+    case SLATE_E_MERGE_UNSORTED: return "merge input iterator is not sorted";
     default: return "unknown status";
   }
 }

@@ -58,6 +58,14 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb(hipStream_t st, const DecodeArgs& a, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
+// ---------------------------------------------------------------- merge (merge.hip)
+// iter.MergeSort over k concatenated sorted iterators (h_src_start: k+1 host element indices).
+// out_idx[0..*n_out) = element indices in return order; *d_flags bit 0 = some iterator unsorted.
+size_t merge_scratch_bytes(uint32_t n, uint32_t k);
+hipError_t launch_merge(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint32_t n,
+                        const uint32_t* h_src_start, uint32_t k, void* scratch, uint32_t* out_idx, uint64_t* n_out,
+                        uint32_t* d_flags);
+
 // Validates that the code object loads on the current device.
 hipError_t decode_kernels_available();
 

@@ -22,6 +22,7 @@ NONE, SNAPPY, ZLIB, LZ4, ZSTD = 0, 1, 2, 3, 4
 OK = 0
 E_NO_DEVICE = 100
 E_CAPACITY = 103
+E_MERGE_UNSORTED = 105
 
 u8p = C.POINTER(C.c_uint8)
 u16p = C.POINTER(C.c_uint16)
@@ -101,6 +102,9 @@ _SIGS = {
     "slate_bloom_encode": (C.c_int, [vp, C.c_uint16, vp, C.c_size_t, C.c_int, vp, C.c_size_t, szp]),
     "slate_bloom_decode": (C.c_int, [vp, vp, C.c_size_t, C.c_int, u16p, vp, C.c_size_t, szp]),
     "slate_bloom_has_keys": (C.c_int, [vp, C.c_uint16, vp, C.c_size_t, vp, vp, C.c_uint64, vp]),
+    "slate_merge_sorted": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, u64p]),
+    "slate_merge_scratch_bytes": (C.c_size_t, [C.c_uint64, C.c_uint32]),
+    "slate_merge_sorted_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp]),
 }
 
 _lib = None
@@ -235,6 +239,32 @@ class Context:
         _check(lib().slate_bloom_build(self._h, _ptr(kd), _ptr(ko), len(keys), bits_per_key, _ptr(out), cap,
                                        C.byref(bl), C.byref(npr)), "slate_bloom_build")
         return npr.value, out[: bl.value].tobytes()
+
+    def merge_arrays(self, keys: np.ndarray, key_off: np.ndarray, src_start: np.ndarray) -> np.ndarray:
+        """iter.MergeSort (merge.go:12-111) over k concatenated sorted iterators: the element
+        indices of the entries Next() returns, in order (u32).  Raises SlateError
+        (E_MERGE_UNSORTED) for an unsorted iterator."""
+        keys = np.ascontiguousarray(keys, np.uint8) if len(keys) else np.zeros(1, np.uint8)
+        key_off = np.ascontiguousarray(key_off, np.uint64)
+        src_start = np.ascontiguousarray(src_start, np.uint64)
+        out = np.zeros(max(int(src_start[-1]), 1), np.uint32)
+        n = C.c_uint64()
+        _check(lib().slate_merge_sorted(self._h, len(src_start) - 1, _ptr(keys), _ptr(key_off), _ptr(src_start),
+                                        _ptr(out), C.byref(n)), "slate_merge_sorted")
+        return out[: n.value]
+
+    def merge_sort(self, sources: list[list[bytes]]) -> np.ndarray:
+        """merge_arrays over per-iterator key lists."""
+        kd, ko = _arena([k for s in sources for k in s])
+        ss = np.zeros(len(sources) + 1, np.uint64)
+        ss[1:] = np.cumsum([len(s) for s in sources])
+        return self.merge_arrays(kd, ko, ss)
+
+    def merge_device(self, d_keys: int, d_key_off: int, src_start: np.ndarray, d_out_idx: int, d_n_out: int,
+                     d_flags: int, d_scratch: int) -> None:
+        src_start = np.ascontiguousarray(src_start, np.uint64)
+        _check(lib().slate_merge_sorted_device(self._h, len(src_start) - 1, d_keys, d_key_off, _ptr(src_start),
+                                               d_out_idx, d_n_out, d_flags, d_scratch), "slate_merge_sorted_device")
 
     def bloom_has_keys(self, num_probes: int, bits: bytes, keys: list[bytes]) -> list[bool]:
         kd, ko = _arena(keys)
