@@ -316,6 +316,36 @@ int slate_merge_sorted_device(slate_ctx* ctx, uint32_t k, const uint8_t* d_keys,
                               const uint64_t* src_start, uint32_t* d_out_idx, uint64_t* d_n_out,
                               uint32_t* d_flags, void* d_scratch);
 
+/* ---- compaction KV views (executeCompaction's iterators, compaction/executor.go:92-151) --
+ * Device-resident, on the context's stream, two phases each (lengths, then copy into buffers
+ * the caller sizes from the offsets' last element):
+ * rows -> KV: for decoded blocks (slate_block_decode_device outputs; n_rows = the row-slot
+ * count d_row_base[n_blocks]), the rows in block order (*d_n_kv of them), each with its full key
+ * (block.Iterator, block/iterator.go:84-107: row 0's key is its suffix and is the block's
+ * firstKey; row i's key = firstKey[:prefixLen] || suffix, row.go:72-79), value bytes (empty for
+ * tombstones) and tombstone flag.  *d_flags bit 1 = a block or row failed to decode (its rows
+ * contribute no KV).  d_key_off/d_val_off hold n_rows+1 entries (entries past *d_n_kv repeat the
+ * total).  d_scratch holds slate_kv_scratch_bytes(n_rows) and must be kept, unchanged, from the
+ * lengths call to the copy call (it carries the row-slot map).
+ * gather: the KV of every merge result index (slate_merge_sorted_device's d_out_idx), in order,
+ * ready for the SST builder (EncodedSSTableWriter.Add, table_store.go:221-266). */
+size_t slate_kv_scratch_bytes(uint64_t n);
+int slate_rows_kv_lengths_device(slate_ctx* ctx, uint32_t n_blocks, const uint64_t* d_row_base,
+                                 const slate_block_meta* d_meta, const slate_row* d_rows, uint64_t n_rows,
+                                 uint64_t* d_key_off, uint64_t* d_val_off, uint8_t* d_tomb, uint64_t* d_n_kv,
+                                 uint32_t* d_flags, void* d_scratch);
+int slate_rows_kv_copy_device(slate_ctx* ctx, uint32_t n_blocks, const uint8_t* d_data, const uint64_t* d_out_off,
+                              const uint64_t* d_row_base, const slate_row* d_rows, uint64_t n_rows,
+                              const uint64_t* d_n_kv, const void* d_scratch, const uint64_t* d_key_off,
+                              uint8_t* d_keys, const uint64_t* d_val_off, uint8_t* d_vals);
+int slate_kv_gather_lengths_device(slate_ctx* ctx, const uint32_t* d_idx, uint64_t n, const uint64_t* d_key_off,
+                                   const uint64_t* d_val_off, const uint8_t* d_tomb, uint64_t* d_okey_off,
+                                   uint64_t* d_oval_off, uint8_t* d_otomb, void* d_scratch);
+int slate_kv_gather_copy_device(slate_ctx* ctx, const uint32_t* d_idx, uint64_t n, const uint8_t* d_keys,
+                                const uint64_t* d_key_off, const uint8_t* d_vals, const uint64_t* d_val_off,
+                                uint8_t* d_okeys, const uint64_t* d_okey_off, uint8_t* d_ovals,
+                                const uint64_t* d_oval_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,4 +82,55 @@ int slate_merge_sorted(slate_ctx* ctx, uint32_t k, const uint8_t* keys, const ui
   return SLATE_OK;
 }
 
+size_t slate_kv_scratch_bytes(uint64_t n) { return kv_scratch_bytes(n); }
+
+int slate_rows_kv_lengths_device(slate_ctx* ctx, uint32_t n_blocks, const uint64_t* d_row_base,
+                                 const slate_block_meta* d_meta, const slate_row* d_rows, uint64_t n_rows,
+                                 uint64_t* d_key_off, uint64_t* d_val_off, uint8_t* d_tomb, uint64_t* d_n_kv,
+                                 uint32_t* d_flags, void* d_scratch) {
+  if (!ctx || !d_row_base || !d_meta || !d_key_off || !d_val_off || !d_n_kv || !d_flags || !d_scratch ||
+      n_blocks == 0 || n_rows >= 0xFFFFFFFFull)
+    return SLATE_E_INVALID_ARG;
+  if (n_rows && (!d_rows || !d_tomb)) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(launch_rows_lengths(ctx->stream, d_row_base, n_blocks, d_meta, d_rows, n_rows, d_key_off, d_val_off,
+                                d_tomb, d_n_kv, d_flags, d_scratch));
+  return SLATE_OK;
+}
+
+int slate_rows_kv_copy_device(slate_ctx* ctx, uint32_t n_blocks, const uint8_t* d_data, const uint64_t* d_out_off,
+                              const uint64_t* d_row_base, const slate_row* d_rows, uint64_t n_rows,
+                              const uint64_t* d_n_kv, const void* d_scratch, const uint64_t* d_key_off,
+                              uint8_t* d_keys, const uint64_t* d_val_off, uint8_t* d_vals) {
+  if (!ctx || !d_out_off || !d_row_base || !d_key_off || !d_val_off || !d_n_kv || !d_scratch || n_blocks == 0)
+    return SLATE_E_INVALID_ARG;
+  if (n_rows && (!d_data || !d_rows)) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(launch_rows_copy(ctx->stream, d_data, d_out_off, d_row_base, n_blocks, d_rows, n_rows, d_n_kv, d_scratch,
+                             d_key_off, d_keys, d_val_off, d_vals));
+  return SLATE_OK;
+}
+
+int slate_kv_gather_lengths_device(slate_ctx* ctx, const uint32_t* d_idx, uint64_t n, const uint64_t* d_key_off,
+                                   const uint64_t* d_val_off, const uint8_t* d_tomb, uint64_t* d_okey_off,
+                                   uint64_t* d_oval_off, uint8_t* d_otomb, void* d_scratch) {
+  if (!ctx || !d_key_off || !d_val_off || !d_okey_off || !d_oval_off || !d_scratch) return SLATE_E_INVALID_ARG;
+  if (n && (!d_idx || !d_tomb || !d_otomb)) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(launch_gather_lengths(ctx->stream, d_idx, n, d_key_off, d_val_off, d_tomb, d_okey_off, d_oval_off, d_otomb,
+                                  d_scratch));
+  return SLATE_OK;
+}
+
+int slate_kv_gather_copy_device(slate_ctx* ctx, const uint32_t* d_idx, uint64_t n, const uint8_t* d_keys,
+                                const uint64_t* d_key_off, const uint8_t* d_vals, const uint64_t* d_val_off,
+                                uint8_t* d_okeys, const uint64_t* d_okey_off, uint8_t* d_ovals,
+                                const uint64_t* d_oval_off) {
+  if (!ctx || (n && (!d_idx || !d_key_off || !d_val_off || !d_okey_off || !d_oval_off))) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(launch_gather_copy(ctx->stream, d_idx, n, d_keys, d_key_off, d_vals, d_val_off, d_okeys, d_okey_off,
+                               d_ovals, d_oval_off));
+  return SLATE_OK;
+}
+
 }  // extern "C"

@@ -108,6 +108,9 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
   if (len < 4) return SLATE_E_INVALID_ARG;
   const size_t clen = len - 4;
   uint64_t dl = 0;
+  uint32_t hdr_len = 0;
+  // above this decoded size the lane-per-block decoder would walk the stream on one lane
+  constexpr uint64_t kStreamMin = 16384;
   {
     uint64_t x = 0;
     uint32_t sft = 0;
@@ -123,10 +126,44 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
       x |= uint64_t(bt & 0x7f) << sft;
       sft += 7;
     }
-    if (ok && x <= kSnappyMaxExpansion * uint64_t(clen)) dl = x;  // else the kernel reports it
+    if (ok && x <= kSnappyMaxExpansion * uint64_t(clen)) {
+      dl = x;  // else the kernel reports it
+      hdr_len = 0;
+      while (buf[hdr_len] >= 0x80) hdr_len++;
+      hdr_len++;
+    }
   }
   SLATE_HIP(ctx_bind(ctx));
   hipStream_t st = ctx->stream;
+  if (dl > kStreamMin && dl <= 0xFFFFFFF0ull && clen <= 0xFFFFFFF0ull) {
+    // one long serial tag stream (an index or filter): the one-wave streaming decoder after
+    // a GPU CRC (block.go / bloom.go order: checksum first, then decode)
+    uint32_t crc = 0;
+    int cs = ctx_crc32_host_buffer(ctx, buf, clen, &crc);
+    if (cs != SLATE_OK) return cs;
+    const uint32_t want = (uint32_t(buf[clen]) << 24) | (uint32_t(buf[clen + 1]) << 16) |
+                          (uint32_t(buf[clen + 2]) << 8) | uint32_t(buf[clen + 3]);
+    if (crc != want) {
+      *bstatus = SLATE_E_BLOCK_CHECKSUM;
+      return SLATE_OK;
+    }
+    SLATE_HIP(ctx->d_in.ensure(len + 16));
+    SLATE_HIP(ctx->d_out.ensure(align16(dl) + 32));
+    SLATE_HIP(ctx->d_scratch.ensure(128));
+    int32_t* d_st = ctx->d_scratch.as<int32_t>();
+    SLATE_HIP(hipMemcpyAsync(ctx->d_in.p, buf, clen, hipMemcpyHostToDevice, st));
+    SLATE_HIP(launch_snappy_stream(st, ctx->d_in.as<uint8_t>(), uint32_t(clen), hdr_len, ctx->d_out.as<uint8_t>(),
+                                   uint32_t(dl), d_st));
+    int32_t h_st = 0;
+    SLATE_HIP(hipMemcpyAsync(&h_st, d_st, 4, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    *bstatus = h_st;
+    if (h_st == SLATE_OK) {
+      out.resize(dl);
+      SLATE_HIP(hipMemcpy(out.data(), ctx->d_out.p, dl, hipMemcpyDeviceToHost));
+    }
+    return SLATE_OK;
+  }
   SLATE_HIP(ctx->d_in.ensure(len + 16));
   SLATE_HIP(ctx->d_out.ensure(align16(dl) + 32));
   SLATE_HIP(ctx->d_scratch.ensure(128));

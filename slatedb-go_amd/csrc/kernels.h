@@ -66,6 +66,28 @@ hipError_t launch_merge(hipStream_t st, const uint8_t* keys, const uint64_t* key
                         const uint32_t* h_src_start, uint32_t k, void* scratch, uint32_t* out_idx, uint64_t* n_out,
                         uint32_t* d_flags);
 
+// Compaction KV views (merge.hip): full keys / values of decoded rows, and the merged gather.
+size_t kv_scratch_bytes(uint64_t n);
+hipError_t launch_rows_lengths(hipStream_t st, const uint64_t* row_base, uint32_t n_blocks,
+                               const slate_block_meta* meta, const slate_row* rows, uint64_t n_slots,
+                               uint64_t* key_off, uint64_t* val_off, uint8_t* tomb, uint64_t* n_kv, uint32_t* flags,
+                               void* scratch);
+hipError_t launch_rows_copy(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const uint64_t* row_base,
+                            uint32_t n_blocks, const slate_row* rows, uint64_t n_slots, const uint64_t* n_kv,
+                            const void* scratch, const uint64_t* key_off, uint8_t* keys, const uint64_t* val_off,
+                            uint8_t* vals);
+hipError_t launch_gather_lengths(hipStream_t st, const uint32_t* idx, uint64_t n, const uint64_t* key_off,
+                                 const uint64_t* val_off, const uint8_t* tomb, uint64_t* okey_off, uint64_t* oval_off,
+                                 uint8_t* otomb, void* scratch);
+hipError_t launch_gather_copy(hipStream_t st, const uint32_t* idx, uint64_t n, const uint8_t* keys,
+                              const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off, uint8_t* okeys,
+                              const uint64_t* okey_off, uint8_t* ovals, const uint64_t* oval_off);
+
+// Streaming one-wave Snappy decode of one large payload (snappy_stream.hip); *status = SLATE_OK or
+// SLATE_E_SNAPPY_CORRUPT.  hdr = varint header bytes, dn = decoded length from the header.
+hipError_t launch_snappy_stream(hipStream_t st, const uint8_t* in, uint32_t sn, uint32_t hdr, uint8_t* out,
+                                uint32_t dn, int32_t* status);
+
 // Validates that the code object loads on the current device.
 hipError_t decode_kernels_available();
 

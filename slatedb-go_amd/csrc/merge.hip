@@ -239,4 +239,269 @@ hipError_t launch_merge(hipStream_t st, const uint8_t* keys, const uint64_t* key
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- compaction rows (KV views)
+// Between block decode and the merge, executeCompaction's iterators (sstable.Iterator ->
+// block.Iterator, block/iterator.go:84-107) turn each row into (full key, value | tombstone):
+// row 0 of a block is decoded against firstKey = nil, so its key is its suffix and becomes the
+// block's firstKey; row i's key is firstKey[:prefixLen] || suffix (row.go:72-79).  Here every
+// row does that on its own: lengths -> exclusive scans -> a copy pass, 16 lanes per row.
+namespace {
+
+constexpr uint32_t kScanTile = 4096;  // elements per workgroup in the u64 scan
+
+// exclusive scan of n u32 lengths into n+1 u64 offsets: tile sums, one-workgroup scan of the
+// tile sums, tile-local scans
+__global__ __launch_bounds__(256) void scan_tile_sum_kernel(const uint32_t* len, uint64_t n, uint64_t* tile_sum) {
+  __shared__ uint64_t ws[4];
+  const uint64_t t0 = uint64_t(blockIdx.x) * kScanTile;
+  uint64_t s = 0;
+  for (uint64_t i = t0 + threadIdx.x; i < min(t0 + kScanTile, n); i += 256) s += len[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(1024) void scan_tiles_kernel(uint64_t* tile_sum, uint32_t tiles) {
+  __shared__ uint64_t ws[16];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < tiles; c0 += 1024) {
+    const uint32_t t = c0 + threadIdx.x;
+    const uint64_t v = t < tiles ? tile_sum[t] : 0;
+    uint64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if ((threadIdx.x & 63) >= uint32_t(o)) x += y;
+    }
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t wo = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) wo += ws[w];
+    const uint64_t base = carry;
+    if (t < tiles) tile_sum[t] = base + wo + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = base + wo + x;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void scan_local_kernel(const uint32_t* len, uint64_t n, const uint64_t* tile_off,
+                                                         uint64_t* off) {
+  __shared__ uint64_t ws[4];
+  __shared__ uint64_t carry;
+  const uint64_t t0 = uint64_t(blockIdx.x) * kScanTile;
+  if (threadIdx.x == 0) carry = tile_off[blockIdx.x];
+  __syncthreads();
+  for (uint64_t c0 = t0; c0 < min(t0 + kScanTile, n); c0 += 256) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint64_t v = i < n ? len[i] : 0;
+    uint64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if ((threadIdx.x & 63) >= uint32_t(o)) x += y;
+    }
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t wo = 0;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) wo += ws[w];
+    const uint64_t base = carry;
+    if (i < n) off[i] = base + wo + x - v;
+    if (i + 1 == n) off[n] = base + wo + x;
+    __syncthreads();
+    if (threadIdx.x == 255) carry = base + wo + x;
+    __syncthreads();
+  }
+}
+
+hipError_t scan_u32_to_u64(hipStream_t st, const uint32_t* len, uint64_t n, uint64_t* off, uint64_t* tile_scratch) {
+  if (n == 0) return hipMemsetAsync(off, 0, 8, st);
+  const uint32_t tiles = uint32_t((n + kScanTile - 1) / kScanTile);
+  hipLaunchKernelGGL(scan_tile_sum_kernel, dim3(tiles), dim3(256), 0, st, len, n, tile_scratch);
+  hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, st, tile_scratch, tiles);
+  hipLaunchKernelGGL(scan_local_kernel, dim3(tiles), dim3(256), 0, st, len, n, tile_scratch, off);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ uint32_t block_of_row(const uint64_t* row_base, uint32_t n_blocks, uint64_t r) {
+  uint32_t lo = 0, hi = n_blocks;  // row_base[lo] <= r < row_base[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (row_base[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// row slots are planned with a capacity per block (decoded_len + 13) / 15: slot j of block b holds a
+// row when j < n_rows.  valid[] marks them (a failed block or row sets flags bit 1 and keeps no rows)
+__global__ __launch_bounds__(256) void rows_valid_kernel(const uint64_t* row_base, uint32_t n_blocks,
+                                                         const slate_block_meta* meta, const slate_row* rows,
+                                                         uint64_t n_slots, uint32_t* valid, uint32_t* flags) {
+  const uint64_t r = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (r >= n_slots) return;
+  const uint32_t b = block_of_row(row_base, n_blocks, r);
+  const slate_block_meta m = meta[b];
+  const uint64_t j = r - row_base[b];
+  bool v = j < m.n_rows;
+  const bool bad_block = m.status != SLATE_OK || (m.flags & SLATE_BLKF_ROWS_TRUNCATED) != 0;
+  if (v && (bad_block || rows[r].status != SLATE_OK)) {
+    atomicOr(flags, 2u);
+    v = false;
+  }
+  if (bad_block && j == 0) atomicOr(flags, 2u);
+  valid[r] = v ? 1u : 0u;
+}
+
+// compacted row i -> its slot; lengths of row i (slots past the row count give zero lengths)
+__global__ __launch_bounds__(256) void rows_slot_kernel(const uint32_t* valid, const uint64_t* pos, uint64_t n_slots,
+                                                        uint32_t* slot) {
+  const uint64_t r = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (r < n_slots && valid[r]) slot[pos[r]] = uint32_t(r);
+}
+
+__global__ __launch_bounds__(256) void rows_len_kernel(const uint64_t* row_base, uint32_t n_blocks,
+                                                       const slate_row* rows, const uint32_t* slot,
+                                                       const uint64_t* pos, uint64_t n_slots, uint32_t* klen,
+                                                       uint32_t* vlen, uint8_t* tomb) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n_slots) return;
+  if (i >= pos[n_slots]) {
+    klen[i] = 0;
+    vlen[i] = 0;
+    return;
+  }
+  const uint32_t r = slot[i];
+  const uint32_t b = block_of_row(row_base, n_blocks, r);
+  const slate_row w = rows[r];
+  const bool first = r == row_base[b];
+  klen[i] = (first ? 0u : w.key_prefix_len) + w.key_suffix_len;
+  const bool t = (w.flags & 1) != 0;
+  vlen[i] = t ? 0u : w.value_len;
+  tomb[i] = t ? 1 : 0;
+}
+
+// 16 lanes per row: key = firstKey[:pl] || suffix, value bytes
+__global__ __launch_bounds__(256) void rows_copy_kernel(const uint8_t* data, const uint64_t* out_off,
+                                                        const uint64_t* row_base, uint32_t n_blocks,
+                                                        const slate_row* rows, const uint32_t* slot, const uint64_t* n_kv,
+                                                        uint64_t n_slots, const uint64_t* key_off, uint8_t* keys,
+                                                        const uint64_t* val_off, uint8_t* vals) {
+  const uint64_t i = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 4;
+  const uint32_t l = threadIdx.x & 15;
+  if (i >= n_slots || i >= *n_kv) return;
+  const uint32_t r = slot[i];
+  const uint32_t b = block_of_row(row_base, n_blocks, r);
+  const uint8_t* blk = data + out_off[b];
+  const slate_row w = rows[r];
+  const slate_row w0 = rows[row_base[b]];
+  const uint64_t ko = key_off[i], kn = key_off[i + 1] - ko;
+  const uint32_t pl = r == row_base[b] ? 0u : uint32_t(kn) - w.key_suffix_len;
+  const uint8_t* fk = blk + w0.row_off + 4;  // row 0's suffix is the block's first key
+  const uint8_t* sfx = blk + w.row_off + 4;
+  for (uint32_t i = l; i < kn; i += 16) keys[ko + i] = i < pl ? fk[i] : sfx[i - pl];
+  const uint64_t vo = val_off[i], vn = val_off[i + 1] - vo;
+  const uint8_t* v = blk + w.row_off + 4 + w.key_suffix_len + w.meta_len;
+  for (uint32_t i = l; i < vn; i += 16) vals[vo + i] = v[i];
+}
+
+// merged order: lengths of the returned entries
+__global__ __launch_bounds__(256) void gather_len_kernel(const uint32_t* idx, uint64_t n, const uint64_t* key_off,
+                                                         const uint64_t* val_off, const uint8_t* tomb,
+                                                         uint32_t* klen, uint32_t* vlen, uint8_t* tomb_out) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t e = idx[i];
+  klen[i] = uint32_t(key_off[e + 1] - key_off[e]);
+  vlen[i] = uint32_t(val_off[e + 1] - val_off[e]);
+  tomb_out[i] = tomb[e];
+}
+
+__global__ __launch_bounds__(256) void gather_copy_kernel(const uint32_t* idx, uint64_t n, const uint8_t* keys,
+                                                          const uint64_t* key_off, const uint8_t* vals,
+                                                          const uint64_t* val_off, uint8_t* okeys,
+                                                          const uint64_t* okey_off, uint8_t* ovals,
+                                                          const uint64_t* oval_off) {
+  const uint64_t i = (uint64_t(blockIdx.x) * 256 + threadIdx.x) >> 4;
+  const uint32_t l = threadIdx.x & 15;
+  if (i >= n) return;
+  const uint32_t e = idx[i];
+  const uint64_t ks = key_off[e], kd = okey_off[i], kn = okey_off[i + 1] - kd;
+  for (uint64_t j = l; j < kn; j += 16) okeys[kd + j] = keys[ks + j];
+  const uint64_t vs = val_off[e], vd = oval_off[i], vn = oval_off[i + 1] - vd;
+  for (uint64_t j = l; j < vn; j += 16) ovals[vd + j] = vals[vs + j];
+}
+
+}  // namespace
+
+// rows phase: klen, vlen, valid, slot (u32 each), pos (u64, n+1), tile sums
+size_t kv_scratch_bytes(uint64_t n) { return 16 * n + 8 * (n + 1) + 8 * ((n + kScanTile - 1) / kScanTile) + 256; }
+
+// scratch: klen | vlen | valid | slot (u32 x n_slots each) | pos (u64 x n_slots+1) | tile sums
+hipError_t launch_rows_lengths(hipStream_t st, const uint64_t* row_base, uint32_t n_blocks,
+                               const slate_block_meta* meta, const slate_row* rows, uint64_t n_slots,
+                               uint64_t* key_off, uint64_t* val_off, uint8_t* tomb, uint64_t* n_kv, uint32_t* flags,
+                               void* scratch) {
+  uint32_t* klen = static_cast<uint32_t*>(scratch);
+  uint32_t* vlen = klen + n_slots;
+  uint32_t* valid = vlen + n_slots;
+  uint32_t* slot = valid + n_slots;
+  uint64_t* pos = reinterpret_cast<uint64_t*>(slot + n_slots);
+  uint64_t* tiles = pos + n_slots + 1;
+  hipError_t e = hipMemsetAsync(flags, 0, 4, st);
+  if (e != hipSuccess) return e;
+  const dim3 g(uint32_t((n_slots + 255) / 256));
+  if (n_slots)
+    hipLaunchKernelGGL(rows_valid_kernel, g, dim3(256), 0, st, row_base, n_blocks, meta, rows, n_slots, valid, flags);
+  e = scan_u32_to_u64(st, valid, n_slots, pos, tiles);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(n_kv, pos + n_slots, 8, hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
+  if (n_slots) {
+    hipLaunchKernelGGL(rows_slot_kernel, g, dim3(256), 0, st, valid, pos, n_slots, slot);
+    hipLaunchKernelGGL(rows_len_kernel, g, dim3(256), 0, st, row_base, n_blocks, rows, slot, pos, n_slots, klen, vlen,
+                       tomb);
+  }
+  e = scan_u32_to_u64(st, klen, n_slots, key_off, tiles);
+  if (e != hipSuccess) return e;
+  return scan_u32_to_u64(st, vlen, n_slots, val_off, tiles);
+}
+
+// the slot map is read back from the scratch the lengths phase filled
+hipError_t launch_rows_copy(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const uint64_t* row_base,
+                            uint32_t n_blocks, const slate_row* rows, uint64_t n_slots, const uint64_t* n_kv,
+                            const void* scratch, const uint64_t* key_off, uint8_t* keys, const uint64_t* val_off,
+                            uint8_t* vals) {
+  if (n_slots == 0) return hipSuccess;
+  const uint32_t* slot = static_cast<const uint32_t*>(scratch) + 3 * n_slots;
+  hipLaunchKernelGGL(rows_copy_kernel, dim3(uint32_t((n_slots * 16 + 255) / 256)), dim3(256), 0, st, data, out_off,
+                     row_base, n_blocks, rows, slot, n_kv, n_slots, key_off, keys, val_off, vals);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_lengths(hipStream_t st, const uint32_t* idx, uint64_t n, const uint64_t* key_off,
+                                 const uint64_t* val_off, const uint8_t* tomb, uint64_t* okey_off, uint64_t* oval_off,
+                                 uint8_t* otomb, void* scratch) {
+  uint32_t* klen = static_cast<uint32_t*>(scratch);
+  uint32_t* vlen = klen + n;
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(vlen + n);
+  if (n) {
+    hipLaunchKernelGGL(gather_len_kernel, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, st, idx, n, key_off, val_off,
+                       tomb, klen, vlen, otomb);
+  }
+  hipError_t e = scan_u32_to_u64(st, klen, n, okey_off, tiles);
+  if (e != hipSuccess) return e;
+  return scan_u32_to_u64(st, vlen, n, oval_off, tiles);
+}
+
+hipError_t launch_gather_copy(hipStream_t st, const uint32_t* idx, uint64_t n, const uint8_t* keys,
+                              const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off, uint8_t* okeys,
+                              const uint64_t* okey_off, uint8_t* ovals, const uint64_t* oval_off) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_copy_kernel, dim3(uint32_t((n * 16 + 255) / 256)), dim3(256), 0, st, idx, n, keys,
+                     key_off, vals, val_off, okeys, okey_off, ovals, oval_off);
+  return hipGetLastError();
+}
+
 }  // namespace slate

@@ -105,6 +105,11 @@ _SIGS = {
     "slate_merge_sorted": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, u64p]),
     "slate_merge_scratch_bytes": (C.c_size_t, [C.c_uint64, C.c_uint32]),
     "slate_merge_sorted_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp]),
+    "slate_kv_scratch_bytes": (C.c_size_t, [C.c_uint64]),
+    "slate_rows_kv_lengths_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp]),
+    "slate_rows_kv_copy_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp]),
+    "slate_kv_gather_lengths_device": (C.c_int, [vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp]),
+    "slate_kv_gather_copy_device": (C.c_int, [vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp]),
 }
 
 _lib = None

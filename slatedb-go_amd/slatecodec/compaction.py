@@ -1,0 +1,190 @@
+"""executeCompaction (slatedb/compaction/executor.go:92-151) on the GPU, for the part of it that is
+the SST codec path: the input SSTs' data blocks are decoded in one device batch
+(block.Decode per block, as sstable.Iterator does it, internal/sstable/iterator.go:92-118), turned
+into (full key, value | tombstone) rows (block.Iterator, block/iterator.go:84-107), merged with
+first-iterator precedence (iter.MergeSort, internal/iter/merge.go:12-111), gathered in merged
+order, and re-encoded by the SST builder (EncodedSSTableWriter.Add/Close, table_store.go:221-266),
+cutting a new output SST whenever the running key+value size passes MaxSSTSize
+(executor.go:124-139).  Device memory and streams come from torch (plumbing); every byte
+operation runs in the HIP library through its C ABI.  Scheduling, manifests and object storage
+stay with the caller.
+
+`sources` are the merge's iterators in precedence order (executor.go:55-90: L0 SSTs, then sorted
+runs); each is a list of encoded SSTs read in order (a sorted run's SST list, or one L0 SST)."""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from . import (NONE, Context, SlateError, SstBuilder, _check, decode_scratch_bytes, lib, read_info, E_MERGE_UNSORTED,
+               META_DTYPE)
+
+
+def _blocks_of(ctx: Context, sst: bytes):
+    """Data-block byte ranges of one SST (ReadInfo + ReadIndex + getBlockRange, decode.go:25-103)."""
+    st, info, _ = read_info(sst)
+    _check(st, "read_info")
+    st, index = ctx.decode_index(sst[info.index_offset:info.index_offset + info.index_len], info.codec)
+    _check(st, "decode_index")
+    offs = [o for o, _ in index.block_metas()]
+    ends = offs[1:] + [info.filter_offset]
+    return info.codec, [(a, b) for a, b in zip(offs, ends)]
+
+
+def _mark(prof, label):
+    if prof is not None:
+        import torch
+        torch.cuda.synchronize()
+        prof.append((label, time.perf_counter()))
+
+
+def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list | None = None):
+    """Decode every data block of every input SST on the GPU and return the rows as a device KV view:
+    (keys, key_off, vals, val_off, tomb, n_kv, src_start) with src_start = per-source row ranges."""
+    import torch
+    _mark(prof, "start")
+    codec = None
+    pieces, in_off, src_blocks = [], [0], [0]
+    for run in sources:
+        for sst in run:
+            c, ranges = _blocks_of(ctx, sst)
+            if codec is None:
+                codec = c
+            if c != codec:
+                raise SlateError(102, "compaction inputs with different codecs")
+            for a, b in ranges:
+                pieces.append(np.frombuffer(sst, np.uint8, b - a, a))
+                in_off.append(in_off[-1] + (b - a))
+        src_blocks.append(len(in_off) - 1)
+    n = len(in_off) - 1
+    if n == 0:
+        z = torch.zeros(1, dtype=torch.int64, device=device)
+        return (torch.zeros(1, dtype=torch.uint8, device=device), z, torch.zeros(1, dtype=torch.uint8, device=device),
+                z, torch.zeros(1, dtype=torch.uint8, device=device), 0, np.zeros(len(sources) + 1, np.uint64))
+    _mark(prof, "index")
+    blob = np.concatenate(pieces)
+    _mark(prof, "gather_blocks")
+    d_in = torch.from_numpy(blob).to(device)
+    d_in_off = torch.from_numpy(np.array(in_off, np.int64)).to(device)
+    _mark(prof, "h2d")
+    d_out_off = torch.empty(n + 1, dtype=torch.int64, device=device)
+    d_row_base = torch.empty(n + 1, dtype=torch.int64, device=device)
+    d_scr = torch.empty(decode_scratch_bytes(n) + 64, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize(device)
+    ctx.decode_plan_device(codec, d_in.data_ptr(), d_in_off.data_ptr(), n, d_out_off.data_ptr(),
+                           d_row_base.data_ptr(), d_scr.data_ptr())
+    ctx.synchronize()
+    total_out = int(d_out_off[n].item())
+    slots = int(d_row_base[n].item())
+    d_out = torch.empty(total_out + 16, dtype=torch.uint8, device=device)
+    d_meta = torch.empty(n * 16, dtype=torch.uint8, device=device)
+    d_rows = torch.empty(max(slots, 1) * 16, dtype=torch.uint8, device=device)
+    ctx.decode_device(codec, d_in.data_ptr(), d_in_off.data_ptr(), n, d_out.data_ptr(), d_out_off.data_ptr(),
+                      d_meta.data_ptr(), d_rows.data_ptr(), d_row_base.data_ptr())
+    _mark(prof, "decode")
+    # rows -> KV view
+    d_key_off = torch.empty(slots + 1, dtype=torch.int64, device=device)
+    d_val_off = torch.empty(slots + 1, dtype=torch.int64, device=device)
+    d_tomb = torch.empty(max(slots, 1), dtype=torch.uint8, device=device)
+    d_nkv = torch.zeros(1, dtype=torch.int64, device=device)
+    d_flags = torch.zeros(1, dtype=torch.int32, device=device)
+    d_kvs = torch.empty(lib().slate_kv_scratch_bytes(slots), dtype=torch.uint8, device=device)
+    _check(lib().slate_rows_kv_lengths_device(ctx.handle, n, d_row_base.data_ptr(), d_meta.data_ptr(),
+                                              d_rows.data_ptr(), slots, d_key_off.data_ptr(), d_val_off.data_ptr(),
+                                              d_tomb.data_ptr(), d_nkv.data_ptr(), d_flags.data_ptr(),
+                                              d_kvs.data_ptr()), "slate_rows_kv_lengths_device")
+    ctx.synchronize()
+    meta = np.frombuffer(d_meta.cpu().numpy().tobytes(), dtype=META_DTYPE)
+    if int(d_flags.item()) & 2:
+        bad = np.nonzero(meta["status"] != 0)[0]
+        raise SlateError(int(meta["status"][bad[0]]) if len(bad) else 102, "compaction input block decode")
+    n_kv = int(d_nkv.item())
+    kb, vb = int(d_key_off[slots].item()), int(d_val_off[slots].item())
+    d_keys = torch.empty(max(kb, 1), dtype=torch.uint8, device=device)
+    d_vals = torch.empty(max(vb, 1), dtype=torch.uint8, device=device)
+    _check(lib().slate_rows_kv_copy_device(ctx.handle, n, d_out.data_ptr(), d_out_off.data_ptr(),
+                                           d_row_base.data_ptr(), d_rows.data_ptr(), slots, d_nkv.data_ptr(),
+                                           d_kvs.data_ptr(), d_key_off.data_ptr(), d_keys.data_ptr(),
+                                           d_val_off.data_ptr(), d_vals.data_ptr()), "slate_rows_kv_copy_device")
+    # per-source row ranges from the blocks' row counts
+    rows_per_block = np.concatenate([[0], np.cumsum(meta["n_rows"].astype(np.uint64))])
+    src_start = rows_per_block[np.array(src_blocks)].astype(np.uint64)
+    assert int(src_start[-1]) == n_kv
+    ctx.synchronize()
+    _mark(prof, "rows_kv")
+    return d_keys, d_key_off, d_vals, d_val_off, d_tomb, n_kv, src_start
+
+
+def merge_kv(ctx: Context, view, device, prof: list | None = None):
+    """iter.MergeSort over the sources of a KV view, gathered in merged order (device arrays)."""
+    import torch
+    d_keys, d_key_off, d_vals, d_val_off, d_tomb, n_kv, src_start = view
+    k = len(src_start) - 1
+    d_idx = torch.empty(max(n_kv, 1), dtype=torch.int32, device=device)
+    d_n = torch.zeros(1, dtype=torch.int64, device=device)
+    d_flags = torch.zeros(1, dtype=torch.int32, device=device)
+    d_ms = torch.empty(lib().slate_merge_scratch_bytes(n_kv, k), dtype=torch.uint8, device=device)
+    ctx.merge_device(d_keys.data_ptr(), d_key_off.data_ptr(), src_start, d_idx.data_ptr(), d_n.data_ptr(),
+                     d_flags.data_ptr(), d_ms.data_ptr())
+    if int(d_flags.item()) & 1:
+        raise SlateError(E_MERGE_UNSORTED, "compaction merge")
+    _mark(prof, "merge")
+    m = int(d_n.item())
+    d_okey_off = torch.empty(m + 1, dtype=torch.int64, device=device)
+    d_oval_off = torch.empty(m + 1, dtype=torch.int64, device=device)
+    d_otomb = torch.empty(max(m, 1), dtype=torch.uint8, device=device)
+    d_gs = torch.empty(lib().slate_kv_scratch_bytes(m), dtype=torch.uint8, device=device)
+    _check(lib().slate_kv_gather_lengths_device(ctx.handle, d_idx.data_ptr(), m, d_key_off.data_ptr(),
+                                                d_val_off.data_ptr(), d_tomb.data_ptr(), d_okey_off.data_ptr(),
+                                                d_oval_off.data_ptr(), d_otomb.data_ptr(), d_gs.data_ptr()),
+           "slate_kv_gather_lengths_device")
+    ctx.synchronize()
+    kb, vb = int(d_okey_off[m].item()), int(d_oval_off[m].item())
+    d_okeys = torch.empty(max(kb, 1), dtype=torch.uint8, device=device)
+    d_ovals = torch.empty(max(vb, 1), dtype=torch.uint8, device=device)
+    _check(lib().slate_kv_gather_copy_device(ctx.handle, d_idx.data_ptr(), m, d_keys.data_ptr(), d_key_off.data_ptr(),
+                                             d_vals.data_ptr(), d_val_off.data_ptr(), d_okeys.data_ptr(),
+                                             d_okey_off.data_ptr(), d_ovals.data_ptr(), d_oval_off.data_ptr()),
+           "slate_kv_gather_copy_device")
+    ctx.synchronize()
+    _mark(prof, "gather")
+    return d_okeys, d_okey_off, d_ovals, d_oval_off, d_otomb, m
+
+
+def split_points(key_off: np.ndarray, val_off: np.ndarray, max_sst_size: int) -> list[int]:
+    """executor.go:119-139: currentSize += len(key) + len(value); a writer closes right after the
+    entry that takes currentSize past MaxSSTSize.  Returns the entry index where each output SST ends."""
+    n = len(key_off) - 1
+    size = np.cumsum((np.diff(key_off.astype(np.int64)) + np.diff(val_off.astype(np.int64))))
+    ends, start, base = [], 0, 0
+    while start < n:
+        j = int(np.searchsorted(size, base + max_sst_size, side="right"))  # first entry with size > max
+        end = min(j + 1, n)
+        ends.append(end)
+        base = int(size[end - 1])
+        start = end
+    return ends
+
+
+def compact(ctx: Context, sources: list[list[bytes]], max_sst_size: int, block_size: int = 4096,
+            min_filter_keys: int = 0, filter_bits_per_key: int = 10, codec: int = NONE, device=None) -> list[bytes]:
+    """Returns the encoded output SSTs of the compaction, in order."""
+    import torch
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    view = decode_rows_kv(ctx, sources, device)
+    keys, key_off, vals, val_off, tomb, m = merge_kv(ctx, view, device)
+    h_keys, h_key_off = keys.cpu().numpy(), key_off.cpu().numpy().view(np.uint64)[: m + 1]
+    h_vals, h_val_off = vals.cpu().numpy(), val_off.cpu().numpy().view(np.uint64)[: m + 1]
+    h_tomb = tomb.cpu().numpy()[:m]
+    out, start = [], 0
+    for end in split_points(h_key_off, h_val_off, max_sst_size):
+        b = SstBuilder(ctx, block_size, min_filter_keys, filter_bits_per_key, codec)
+        ko = h_key_off[start:end + 1] - h_key_off[start]
+        vo = h_val_off[start:end + 1] - h_val_off[start]
+        _check(b.add_batch(h_keys[int(h_key_off[start]):int(h_key_off[end]) + 1], ko,
+                           h_vals[int(h_val_off[start]):int(h_val_off[end]) + 1], vo,
+                           None), "add_batch")  # AddValue: empty value => tombstone (table_store.go:221-223)
+        out.append(b.build().encode())
+        start = end
+    return out
