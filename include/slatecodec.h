@@ -271,6 +271,9 @@ void slate_index_free(slate_index* index);
 size_t slate_index_num_blocks(const slate_index* index); /* BlockMetaLength() */
 int slate_index_block_meta(const slate_index* index, size_t i, uint64_t* offset,
                            const uint8_t** first_key, size_t* first_key_len);
+/* Every BlockMeta's Offset at once (cap >= slate_index_num_blocks): what a batched reader or the
+ * compaction path needs to slice an SST's data blocks without per-block calls. */
+int slate_index_block_offsets(const slate_index* index, uint64_t* offsets, size_t cap);
 /* ReadBlocks (decode.go:107): data = the object's bytes [meta[start].Offset, end offset)
  * (slate_read_blocks_range gives that range).  Blocks are decoded as one GPU batch;
  * outputs as slate_block_decode_batch.  *failed_block receives the first failing

@@ -752,6 +752,13 @@ int slate_index_block_meta(const slate_index* index, size_t i, uint64_t* offset,
   return SLATE_OK;
 }
 
+int slate_index_block_offsets(const slate_index* index, uint64_t* offsets, size_t cap) {
+  if (!index || (index->offsets.size() && !offsets)) return SLATE_E_INVALID_ARG;
+  if (cap < index->offsets.size()) return SLATE_E_CAPACITY;
+  if (index->offsets.size()) memcpy(offsets, index->offsets.data(), 8 * index->offsets.size());
+  return SLATE_OK;
+}
+
 // getBlockRange (decode.go:93-103).
 int slate_read_blocks_range(const slate_sst_info* info, const slate_index* index, uint64_t start, uint64_t end,
                             uint64_t* range_start, uint64_t* range_end) {

@@ -106,6 +106,7 @@ _SIGS = {
     "slate_merge_scratch_bytes": (C.c_size_t, [C.c_uint64, C.c_uint32]),
     "slate_merge_sorted_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, vp, vp, vp]),
     "slate_kv_scratch_bytes": (C.c_size_t, [C.c_uint64]),
+    "slate_index_block_offsets": (C.c_int, [vp, vp, C.c_size_t]),
     "slate_rows_kv_lengths_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp]),
     "slate_rows_kv_copy_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp]),
     "slate_kv_gather_lengths_device": (C.c_int, [vp, vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp]),
@@ -341,6 +342,12 @@ class Index:
         if getattr(self, "_h", None):
             lib().slate_index_free(self._h)
             self._h = None
+
+    def block_offsets(self) -> np.ndarray:
+        n = lib().slate_index_num_blocks(self._h)
+        out = np.zeros(max(n, 1), np.uint64)
+        _check(lib().slate_index_block_offsets(self._h, _ptr(out), out.size), "slate_index_block_offsets")
+        return out[:n]
 
     def block_metas(self) -> list[tuple[int, bytes]]:
         out = []

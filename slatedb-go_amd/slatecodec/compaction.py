@@ -22,14 +22,14 @@ from . import (NONE, Context, SlateError, SstBuilder, _check, decode_scratch_byt
 
 
 def _blocks_of(ctx: Context, sst: bytes):
-    """Data-block byte ranges of one SST (ReadInfo + ReadIndex + getBlockRange, decode.go:25-103)."""
+    """Data-block offsets of one SST (ReadInfo + ReadIndex + getBlockRange, decode.go:25-103):
+    block i = sst[offs[i]:offs[i+1]], the last one ending at FilterOffset."""
     st, info, _ = read_info(sst)
     _check(st, "read_info")
     st, index = ctx.decode_index(sst[info.index_offset:info.index_offset + info.index_len], info.codec)
     _check(st, "decode_index")
-    offs = [o for o, _ in index.block_metas()]
-    ends = offs[1:] + [info.filter_offset]
-    return info.codec, [(a, b) for a, b in zip(offs, ends)]
+    offs = np.append(index.block_offsets(), np.uint64(info.filter_offset))
+    return info.codec, offs
 
 
 def _mark(prof, label):
@@ -45,18 +45,23 @@ def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list 
     import torch
     _mark(prof, "start")
     codec = None
-    pieces, in_off, src_blocks = [], [0], [0]
+    pieces, offs_parts, src_blocks = [], [np.zeros(1, np.uint64)], [0]
+    base, nblk = 0, 0  # encoded bytes and blocks gathered so far
     for run in sources:
         for sst in run:
-            c, ranges = _blocks_of(ctx, sst)
+            c, offs = _blocks_of(ctx, sst)
             if codec is None:
                 codec = c
             if c != codec:
                 raise SlateError(102, "compaction inputs with different codecs")
-            for a, b in ranges:
-                pieces.append(np.frombuffer(sst, np.uint8, b - a, a))
-                in_off.append(in_off[-1] + (b - a))
-        src_blocks.append(len(in_off) - 1)
+            if len(offs) > 1:  # the data blocks are contiguous: [offs[0], FilterOffset)
+                lo, hi = int(offs[0]), int(offs[-1])
+                pieces.append(np.frombuffer(sst, np.uint8, hi - lo, lo))
+                offs_parts.append(offs[1:] - np.uint64(lo) + np.uint64(base))
+                base += hi - lo
+                nblk += len(offs) - 1
+        src_blocks.append(nblk)
+    in_off = np.concatenate(offs_parts)
     n = len(in_off) - 1
     if n == 0:
         z = torch.zeros(1, dtype=torch.int64, device=device)
@@ -66,7 +71,7 @@ def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list 
     blob = np.concatenate(pieces)
     _mark(prof, "gather_blocks")
     d_in = torch.from_numpy(blob).to(device)
-    d_in_off = torch.from_numpy(np.array(in_off, np.int64)).to(device)
+    d_in_off = torch.from_numpy(in_off.view(np.int64)).to(device)
     _mark(prof, "h2d")
     d_out_off = torch.empty(n + 1, dtype=torch.int64, device=device)
     d_row_base = torch.empty(n + 1, dtype=torch.int64, device=device)
