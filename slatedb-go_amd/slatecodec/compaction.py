@@ -32,6 +32,28 @@ def _blocks_of(ctx: Context, sst: bytes):
     return info.codec, offs
 
 
+def _index_pool(ctx: Context, n: int) -> list[Context]:
+    """Extra contexts (one HIP stream each) so the input SSTs' indexes decode concurrently: each
+    index is one serial Snappy stream that occupies a single wavefront (snappy_stream.hip).  The
+    library is reentrant per context (one slate_ctx per goroutine in a Go port)."""
+    pool = getattr(ctx, "_index_pool", None)
+    if pool is None:
+        pool = ctx._index_pool = []
+    while len(pool) < n:
+        pool.append(Context(ctx.device))
+    return pool[:n]
+
+
+def _all_blocks(ctx: Context, ssts: list[bytes]):
+    if len(ssts) <= 1:
+        return [_blocks_of(ctx, s) for s in ssts]
+    from concurrent.futures import ThreadPoolExecutor
+    w = min(8, len(ssts))
+    pool = _index_pool(ctx, w)
+    with ThreadPoolExecutor(w) as ex:  # ctypes calls release the GIL
+        return list(ex.map(lambda i: _blocks_of(pool[i % w], ssts[i]), range(len(ssts))))
+
+
 def _mark(prof, label):
     if prof is not None:
         import torch
@@ -47,9 +69,10 @@ def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list 
     codec = None
     pieces, offs_parts, src_blocks = [], [np.zeros(1, np.uint64)], [0]
     base, nblk = 0, 0  # encoded bytes and blocks gathered so far
+    located = iter(_all_blocks(ctx, [sst for run in sources for sst in run]))
     for run in sources:
         for sst in run:
-            c, offs = _blocks_of(ctx, sst)
+            c, offs = next(located)
             if codec is None:
                 codec = c
             if c != codec:
