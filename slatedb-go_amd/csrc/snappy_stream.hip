@@ -57,10 +57,17 @@ __global__ __launch_bounds__(64) void snappy_stream_kernel(const uint8_t* in, ui
   uint32_t s = hdr, d = 0;
   refill(S, s, lane);
   int st = SLATE_OK;
+  // the tag and up to four more bytes, one LDS round trip: lane k reads byte s + k.  After a copy
+  // tag the next tag's bytes are read before the copy moves its bytes (both LDS round trips
+  // overlap); `have` says that `mine` already holds them.
+  uint32_t mine = 0;
+  bool have = false;
   while (s < sn) {
-    if (s + 5 > S.wb + kInWin) refill(S, s, lane);
-    // the tag and up to four more bytes, one LDS round trip: lane k reads byte s + k
-    const uint32_t mine = (uint32_t(lane) < 5 && s + lane < S.wb + kInWin) ? in_byte(S, s + lane) : 0u;
+    if (!have) {
+      if (s + 5 > S.wb + kInWin) refill(S, s, lane);
+      mine = (uint32_t(lane) < 5 && s + lane < S.wb + kInWin) ? in_byte(S, s + lane) : 0u;
+    }
+    have = false;
     const uint32_t c = __builtin_amdgcn_readlane(mine, 0);
     const uint32_t b1 = __builtin_amdgcn_readlane(mine, 1), b2 = __builtin_amdgcn_readlane(mine, 2),
                    b3 = __builtin_amdgcn_readlane(mine, 3), b4 = __builtin_amdgcn_readlane(mine, 4);
@@ -117,6 +124,10 @@ __global__ __launch_bounds__(64) void snappy_stream_kernel(const uint8_t* in, ui
     if (off == 0 || d < off || len > dn - d) {
       st = SLATE_E_SNAPPY_CORRUPT;
       break;
+    }
+    if (s < sn && s + 5 <= S.wb + kInWin) {
+      mine = (uint32_t(lane) < 5) ? in_byte(S, s + lane) : 0u;
+      have = true;
     }
     // len <= 64: one lane per byte; byte j repeats the off-byte pattern when off < len
     const uint32_t j = uint32_t(lane);

@@ -26,3 +26,19 @@ def oracle():
     from oracle import binding
     binding.build()
     return binding
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """torch ships its own HIP runtime next to the system one libslatecodec links.  When the
+    library's runtime opens the device first, torch's later init reports "No HIP GPUs are
+    available"; torch first, then the library, works (bench.py's order).  GPU sessions that use
+    torch device memory therefore initialise torch before any slate_ctx exists."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
+    yield
