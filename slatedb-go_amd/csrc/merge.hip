@@ -28,16 +28,31 @@ struct Head {
   uint64_t h0, h1;  // key bytes 0..7 and 8..15, big-endian, zero padded
 };
 
+// heads from aligned dword loads (a lane's key bytes [o, o+16) are covered by five aligned words;
+// a word that starts inside the key stays inside the allocation's last page)
 __global__ __launch_bounds__(kMergeThreads) void merge_heads_kernel(const uint8_t* keys, const uint64_t* key_off,
                                                                     uint32_t n, Head* heads, uint32_t* lens) {
   const uint32_t e = blockIdx.x * kMergeThreads + threadIdx.x;
   if (e >= n) return;
   const uint64_t o = key_off[e];
   const uint64_t len = key_off[e + 1] - o;
-  uint64_t h[2] = {0, 0};
   const uint32_t m = len < 16 ? uint32_t(len) : 16u;
-  for (uint32_t b = 0; b < m; b++) h[b >> 3] |= uint64_t(keys[o + b]) << (56 - 8 * (b & 7));
-  heads[e] = Head{h[0], h[1]};
+  const uint64_t base = o & ~uint64_t(3);
+  const uint32_t sh = uint32_t(o & 3);
+  uint32_t w[5];
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint64_t a = base + 4 * k;
+    w[k] = a < o + m ? *reinterpret_cast<const uint32_t*>(keys + a) : 0u;
+  }
+  uint32_t x[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int32_t keep = min(max(int32_t(m) - 4 * k, 0), 4);  // key bytes in this dword
+    const uint32_t mask = keep == 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+    x[k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[k + 1], w[k], sh) & mask);
+  }
+  heads[e] = Head{(uint64_t(x[0]) << 32) | x[1], (uint64_t(x[2]) << 32) | x[3]};
   lens[e] = len > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(len);
 }
 
@@ -79,19 +94,43 @@ __global__ __launch_bounds__(kMergeThreads) void merge_rank_kernel(const uint8_t
   if (e + 1 < src_start[i + 1] &&
       key_cmp(he, le, e, heads[e + 1], lens[e + 1], e + 1, keys, key_off) > 0)
     atomicOr(flags, 1u);
-  for (uint32_t j = 0; j < k; j++) {
-    if (j == i) continue;
-    // j < i: count keys <= e (upper bound); j > i: keys < e (lower bound)
-    const int lim = j < i ? 0 : -1;
-    uint32_t a = src_start[j], b = src_start[j + 1];
-    const uint32_t base = a;
-    while (a < b) {
-      const uint32_t mid = a + ((b - a) >> 1);
-      const int c = key_cmp(heads[mid], lens[mid], mid, he, le, e, keys, key_off);
-      if (c <= lim) a = mid + 1;
-      else b = mid;
+  // The (k-1) binary searches are independent: run up to four of them interleaved, so their
+  // dependent load chains overlap (the kernel is bound by load latency, not bandwidth; a
+  // wave-window variant that cut the loads 3x but lengthened the chain ran slower).
+  for (uint32_t j0 = 0; j0 < k; j0 += 4) {
+    uint32_t a[4], b[4], base[4];
+    int lim[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const uint32_t j = j0 + g;
+      const bool use = j < k && j != i;
+      base[g] = use ? src_start[j] : 0u;
+      a[g] = base[g];
+      b[g] = use ? src_start[j + 1] : 0u;
+      lim[g] = j < i ? 0 : -1;  // j < i: count keys <= e (upper bound); j > i: keys < e (lower bound)
     }
-    rank += a - base;
+    while ((a[0] < b[0]) | (a[1] < b[1]) | (a[2] < b[2]) | (a[3] < b[3])) {
+      uint32_t mid[4];
+      Head hm[4];
+      uint32_t lm[4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        mid[g] = a[g] + ((b[g] - a[g]) >> 1);
+        const bool live = a[g] < b[g];
+        hm[g] = live ? heads[mid[g]] : Head{0, 0};
+        lm[g] = live ? lens[mid[g]] : 0u;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; g++) {
+        if (a[g] < b[g]) {
+          const int c = key_cmp(hm[g], lm[g], mid[g], he, le, e, keys, key_off);
+          if (c <= lim[g]) a[g] = mid[g] + 1;
+          else b[g] = mid[g];
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; g++) rank += a[g] - base[g];
   }
   M[rank] = e;
 }
