@@ -440,14 +440,21 @@ __global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __rest
   const int lane = threadIdx.x & 63;
   uint16_t* table = reinterpret_cast<uint16_t*>(smem);
   uint8_t* owner = reinterpret_cast<uint8_t*>(table + kSnapMaxTable);
+  // the chunk itself is staged in LDS, so the match loop's dependent source reads come from LDS
+  // (measured neutral on its own: the cost was the duplicate-slot scans, see snap_slot_neighbours)
+  uint8_t* stage = smem + kSnapMaxTable * 3;
   const uint64_t nchunks = (n + kSnapMaxBlock - 1) / kSnapMaxBlock;
   for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const uint8_t* p = src + c * kSnapMaxBlock;
     const uint32_t pn = uint32_t(min<uint64_t>(n - c * kSnapMaxBlock, kSnapMaxBlock));
     uint8_t* o = dst + c * kSnapChunkSlot;
+    snap_sync();  // the previous chunk's reads of the stage are done
+    for (uint32_t i = uint32_t(lane); i < pn; i += kWave) stage[i] = p[i];
+    if (lane < 16) stage[pn + lane] = 0;  // bytes past the chunk (never part of a match)
+    snap_sync();
     uint32_t d;
-    if (pn < kSnapMinNonLiteral) d = snap_emit_literal(o, 0, p, pn, lane);
-    else d = snappy_encode_block_wave(p, pn, o, table, owner, lane);
+    if (pn < kSnapMinNonLiteral) d = snap_emit_literal(o, 0, stage, pn, lane);
+    else d = snappy_encode_block_wave(stage, pn, o, table, owner, lane);
     if (lane == 0) len[c] = d;
   }
 }
@@ -645,8 +652,11 @@ hipError_t launch_snappy_chunks(hipStream_t st, const uint8_t* src, uint64_t n, 
                                 int num_cus) {
   const uint64_t nchunks = (n + kSnapMaxBlock - 1) / kSnapMaxBlock;
   if (nchunks == 0) return hipGetLastError();
-  snappy_chunks_kernel<<<uint32_t(std::min<uint64_t>(nchunks, uint64_t(num_cus) * 2)), 64, kSnapMaxTable * 3, st>>>(
-      src, n, dst, len);
+  const size_t lds = kSnapMaxTable * 3 + kSnapMaxBlock + 64;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&snappy_chunks_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  snappy_chunks_kernel<<<uint32_t(std::min<uint64_t>(nchunks, uint64_t(num_cus))), 64, lds, st>>>(src, n, dst, len);
   return hipGetLastError();
 }
 

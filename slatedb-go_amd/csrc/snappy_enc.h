@@ -139,6 +139,28 @@ __device__ inline void snap_sync() {
 
 // encodeBlock (encode_other.go:165-238) for kSnapMinNonLiteral <= n <= 65536.
 // table: kSnapMaxTable u16 slots (LDS); owner: kSnapMaxTable bytes (LDS).
+// For each valid lane: the latest earlier (*prev) and the earliest later (*next) valid lane of the
+// wave with the same hash slot h (< 2^14), or 64.  Bitonic sort of (h, lane) keys across the wave;
+// invalid lanes get unique keys above every slot.  Results go back to their lanes by ds_permute.
+__device__ inline void snap_slot_neighbours(uint32_t h, bool valid, int lane, int32_t* prev, int32_t* next) {
+  uint32_t v = ((valid ? h : (1u << 14) + uint32_t(lane)) << 6) | uint32_t(lane);
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t o = uint32_t(__shfl_xor(int(v), int(j), 64));
+      const bool up = (uint32_t(lane) & k) == 0 || k == 64;
+      const bool lower = (uint32_t(lane) & j) == 0;
+      v = (lower == up) ? min(v, o) : max(v, o);
+    }
+  }
+  const uint32_t pv = uint32_t(__shfl_up(int(v), 1, 64)), nv = uint32_t(__shfl_down(int(v), 1, 64));
+  const bool vv = (v >> 6) < (1u << 14);
+  const uint32_t p_lane = (lane > 0 && vv && (pv >> 6) == (v >> 6)) ? (pv & 63) : 64u;
+  const uint32_t n_lane = (lane < 63 && vv && (nv >> 6) == (v >> 6)) ? (nv & 63) : 64u;
+  // sorted position `lane` holds original lane (v & 63): send the answers there
+  *prev = __builtin_amdgcn_ds_permute(int((v & 63) * 4), int(p_lane));
+  *next = __builtin_amdgcn_ds_permute(int((v & 63) * 4), int(n_lane));
+}
+
 __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table,
                                              uint8_t* owner, int lane) {
   uint32_t shift;
@@ -169,31 +191,20 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
       const uint64_t dupmask = __ballot(dup);
       const uint64_t validmask = __ballot(valid);
       int32_t c = valid ? int32_t(table[h]) : 0;
-      if (dupmask) {  // latest earlier lane of this batch with the same slot
-        bool got = false;
-        for (int k = 1; k < kWave; k++) {
-          const uint32_t hp = __shfl(h, lane - k, 64);
-          const int32_t sp = __shfl(st, lane - k, 64);
-          const bool vp = (validmask >> ((lane - k) & 63)) & 1;
-          if (!got && lane >= k && vp && hp == h) {
-            c = sp;
-            got = true;
-          }
-        }
-      }
+      // Lanes of this batch that share a table slot: each takes its candidate from the latest
+      // earlier lane with that slot (the serial encoder's table would hold that position), and
+      // only the latest lane that ran writes the slot.  The lanes are sorted by (slot, lane)
+      // with a 64-wide bitonic network, so the neighbours in sorted order are exactly those
+      // lanes (21 exchange steps, instead of two 63-step shuffle scans).
+      int32_t prev = 64, next = 64;
+      if (dupmask) snap_slot_neighbours(h, valid, lane, &prev, &next);
+      const int32_t sp = __shfl(st, prev < 64 ? prev : lane, 64);  // every lane takes part
+      if (valid && prev < 64) c = sp;
       const bool match = valid && cur == snap_ld32(src + c);
       const uint64_t mm = __ballot(match);
       const uint32_t istar = mm ? uint32_t(__builtin_ctzll(mm)) : 64u;
       const bool ran = valid && uint32_t(lane) <= istar;
-      bool last = true;
-      if (dupmask) {  // a later lane that also ran overwrites the same slot
-        for (int k = 1; k < kWave; k++) {
-          const uint32_t hn = __shfl(h, lane + k, 64);
-          const uint32_t ln = uint32_t(lane + k);
-          const bool vn = ln < 64 && ((validmask >> (ln & 63)) & 1) && ln <= istar;
-          if (vn && hn == h) last = false;
-        }
-      }
+      const bool last = !(next < 64 && uint32_t(next) <= istar);
       if (ran && last) table[h] = uint16_t(st);
       snap_sync();
       if (mm) {
