@@ -137,8 +137,6 @@ __device__ inline void snap_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// encodeBlock (encode_other.go:165-238) for kSnapMinNonLiteral <= n <= 65536.
-// table: kSnapMaxTable u16 slots (LDS); owner: kSnapMaxTable bytes (LDS).
 // For each valid lane: the latest earlier (*prev) and the earliest later (*next) valid lane of the
 // wave with the same hash slot h (< 2^14), or 64.  Bitonic sort of (h, lane) keys across the wave;
 // invalid lanes get unique keys above every slot.  Results go back to their lanes by ds_permute.
@@ -161,6 +159,8 @@ __device__ inline void snap_slot_neighbours(uint32_t h, bool valid, int lane, in
   *next = __builtin_amdgcn_ds_permute(int((v & 63) * 4), int(n_lane));
 }
 
+// encodeBlock (encode_other.go:165-238) for kSnapMinNonLiteral <= n <= 65536.
+// table: kSnapMaxTable u16 slots (LDS); owner: kSnapMaxTable bytes (LDS).
 __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table,
                                              uint8_t* owner, int lane) {
   uint32_t shift;
