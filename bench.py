@@ -1,22 +1,30 @@
 #!/usr/bin/env python
 """Headline benchmark: device-resident SST block decode GiB/s (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): 1 M encoded 4 KiB Snappy blocks
-per GPU, keys b"k%015d", 84-byte V-half values (r||r), BlockSize 4096 (38 rows of
-100-byte KVs per block), already resident in HBM.  One step = one pass of the
-decode path over the batch: plan (decoded sizes + scans) + decode (CRC32 verify,
-Snappy decompress, offset checks, row descriptors).  value = decoded bytes of all
-ranks per second (GiB = 2^30).  Multi-GPU: one process per GPU, every rank
-decodes its own shard (blocks are independent; no collective on the data path),
-so scaling is weak.
+Workloads (every block is generated on its own by tools/benchgen.c bg_build_set:
+keys b"k%015d", 84-byte V-half values r||r, BlockSize 4096 -> 38 rows of 100-byte KVs,
+Snappy-encoded by libsnappy + the block CRC32 trailer):
+  configs1 (default)  BASELINE configs[1]: 1 M blocks per GPU.  Under torchrun the set has
+                      N x 1 M blocks and block i belongs to rank i mod N (round-robin, no
+                      collective): weak scaling, N = 1 is exactly configs[1].
+  configs3            BASELINE configs[3]: ONE fixed set of 64 GiB of encoded blocks
+                      (32,505,856 blocks), block i on rank i mod N: strong scaling.  A rank
+                      holds what fits its HBM (outputs + row slots need ~10 KB per block),
+                      so N = 1 runs the largest single-GPU slice of the set.
+  --codec zstd        BASELINE configs[4] (1 KiB values, Zipf-prefixed keys, libzstd frames).
+Inputs are resident in HBM before timing.  One step = plan (decoded sizes + scans) + decode
+(CRC32 verify, decompress, offset checks, row descriptors) over the rank's whole shard.
+value = decoded bytes of all ranks per second (GiB = 2^30) over the slowest rank's time.
 
-Run: python bench.py [--gpus N --steps K --warmup W]
+Run: python bench.py [--gpus N --steps K --warmup W] [--workload configs3]
      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -30,6 +38,9 @@ for _p in (REPO, os.path.join(REPO, "slatedb-go_amd")):
 
 METRIC = "device-resident SST block decode GiB/s, 4 KiB blocks, at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SEED = 20250307
+CONFIG3_BLOCKS = 32_505_856  # 64 GiB of encoded Snappy V-half blocks (~2,114 B each)
+BYTES_PER_BLOCK_HBM = 2114 + 4016 + 268 * 16 + 16 + 24  # input, output slot, row slots, meta, offsets
 
 
 def parse():
@@ -37,21 +48,45 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--blocks", type=int, default=1_000_000, help="blocks per GPU")
+    p.add_argument("--workload", choices=["configs1", "configs3"], default="configs1")
+    p.add_argument("--blocks", type=int, default=1_000_000, help="configs1: blocks per GPU")
+    p.add_argument("--max-blocks-per-gpu", type=int, default=0, help="configs3: cap a rank's slice (0 = what fits)")
     p.add_argument("--codec", choices=["snappy", "none", "lz4", "zstd"], default="snappy",
                    help="zstd runs BASELINE configs[4] (1 KiB values, Zipf-prefixed keys, libzstd level 3 + checksum)")
     p.add_argument("--values", choices=["half", "rand"], default="half")
+    p.add_argument("--verify", choices=["all", "sample", "none"], default="",
+                   help="decoded bytes, meta and rows vs the generator (default: all for configs1, sample for configs3)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="budget per CPU-baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cache", default="", help="directory to reuse the generated workload from (profiling runs: "
-                   "the zstd generator's libzstd clashes with the profiler's own copy)")
+    p.add_argument("--cache", default="", help="configs[4]: directory to reuse the generated workload from")
     p.add_argument("--no-host-io", action="store_true")
+    p.add_argument("--allow-variant", action="store_true", help="profiling only: accept SLATE_LIB_VARIANT")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_decode_latest.json"))
     return p.parse_args()
 
 
+def lib_sha256() -> str:
+    import slatecodec as sc
+    with open(sc.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def host_cpus() -> int:
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def main():
     args = parse()
+    if (os.environ.get("SLATE_LIB_VARIANT") or os.environ.get("SLATE_DEBUG_MODE")) and not args.allow_variant:
+        sys.exit("bench.py: SLATE_LIB_VARIANT / SLATE_DEBUG_MODE set: profiling variants are not benchmarks")
     import torch
 
     rank = int(os.environ.get("RANK", "0"))
@@ -69,26 +104,39 @@ def main():
     from tools import workload as wl
 
     codec = {"snappy": sc.SNAPPY, "none": sc.NONE, "lz4": sc.LZ4, "zstd": sc.ZSTD}[args.codec]
-    n = args.blocks
+    if codec == sc.LZ4:
+        raise SystemExit("bench.py: LZ4 frames are timed by tools/ablate.py (liblz4), not the block set")
+    half = args.values == "half"
+    threads = max(1, min(16, host_cpus()))
     t0 = time.time()
-    spec = shard_spec(rank, n)
-    cache = (os.path.join(args.cache, f"wl_{args.codec}_{args.values}_{n}_{spec['seed']}_{spec['kv_begin']}")
-             if args.cache else "")
-    if cache and os.path.exists(cache + "_blob.npy"):
-        dec, dec_off, blob, in_off = (np.load(cache + f"_{k}.npy") for k in ("dec", "dec_off", "blob", "in_off"))
-    else:
-        if args.codec == "zstd":  # configs[4] "mixed"
-            dec, dec_off = wl.mixed_blocks(n, seed=spec["seed"])
+    shard = None  # (i_begin, stride, count) of the rank's blocks in the generated set
+    if args.codec == "zstd":  # configs[4] "mixed": its own sequential generator, one shard per rank
+        n = args.blocks
+        cache = os.path.join(args.cache, f"wl_zstd_{n}_{SEED + rank}") if args.cache else ""
+        if cache and os.path.exists(cache + "_blob.npy"):
+            blob, in_off = (np.load(cache + f"_{k}.npy") for k in ("blob", "in_off"))
         else:
-            dec, dec_off = wl.decoded_blocks(n, seed=spec["seed"], half=(args.values == "half"),
-                                             kv_begin=spec["kv_begin"])
-        blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=min(16, os.cpu_count() or 4))
-        if cache:
-            os.makedirs(args.cache, exist_ok=True)
-            for k, v in (("dec", dec), ("dec_off", dec_off), ("blob", blob), ("in_off", in_off)):
-                np.save(cache + f"_{k}.npy", v)
+            dec, dec_off = wl.mixed_blocks(n, seed=SEED + rank)
+            blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=threads)
+            del dec, dec_off
+            if cache:
+                os.makedirs(args.cache, exist_ok=True)
+                np.save(cache + "_blob.npy", blob)
+                np.save(cache + "_in_off.npy", in_off)
+        set_blocks, scaling = n * world, "weak"
+    else:
+        if args.workload == "configs1":
+            set_blocks, count, scaling = world * args.blocks, args.blocks, "weak"
+        else:
+            set_blocks, scaling = CONFIG3_BLOCKS, "strong"
+            count = sc.shard_blocks(set_blocks, world, rank)
+            free = torch.cuda.mem_get_info(device)[0]
+            fit = int(free * 0.92) // BYTES_PER_BLOCK_HBM
+            count = min(count, fit, args.max_blocks_per_gpu or count)
+        shard = (rank, world, count)
+        blob, in_off = wl.block_set(codec, rank, world, count, seed=SEED, half=half, threads=threads)
+        n = count
     gen_s = time.time() - t0
-    dec_bytes = int(dec_off[-1])
     enc_bytes = int(in_off[-1])
 
     ctx = sc.Context(local)
@@ -126,18 +174,33 @@ def main():
         step()
     torch.cuda.synchronize(device)
 
-    # ---- verify (size-independent properties + sampled bytes against the generator)
+    # ---- verify, outside the timed region: every block's status; decoded bytes, meta and row
+    # descriptors against the generator for every block (configs1) or evenly spread chunks (configs3)
     meta = np.frombuffer(d_meta.cpu().numpy().tobytes(), dtype=sc.META_DTYPE)
     assert (meta["status"] == 0).all(), np.unique(meta["status"], return_counts=True)
-    out_off = d_out_off.cpu().numpy().view(np.uint64)
-    sample = np.arange(0, n, max(1, n // 997))
-    out_h = d_out.cpu().numpy()
-    for i in sample:
-        a = int(out_off[i])
-        ln = int(dec_off[i + 1] - dec_off[i])
-        assert out_h[a:a + ln].tobytes() == dec[int(dec_off[i]):int(dec_off[i + 1])].tobytes(), f"block {i}"
+    dec_bytes = int(np.sum(meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2))
     n_rows = int(meta["n_rows"].astype(np.int64).sum())
-    del out_h
+    verify = args.verify or ("all" if args.workload == "configs1" else "sample")
+    verified = 0
+    if shard is not None and verify != "none":
+        out_off_h = d_out_off.cpu().numpy().view(np.uint64)
+        rb_h = d_row_base.cpu().numpy().view(np.uint64)
+        meta_u8 = d_meta.cpu().numpy()
+        chunk = 131072
+        starts = list(range(0, n, chunk))
+        if verify == "sample" and len(starts) > 16:
+            starts = [starts[int(j * (len(starts) - 1) / 15)] for j in range(16)]
+        for k0 in starts:
+            k1 = min(n, k0 + chunk)
+            oa, ob_ = int(out_off_h[k0]), int(out_off_h[k1])
+            ra, rb_ = int(rb_h[k0]), int(rb_h[k1])
+            out_c = d_out[oa:ob_].cpu().numpy()
+            rows_c = d_rows[16 * ra:16 * rb_].cpu().numpy()
+            bad = wl.verify_set(shard[0] + k0 * shard[1], shard[1], k1 - k0, out_c, out_off_h[k0:k1 + 1] - oa,
+                                rows_c, rb_h[k0:k1 + 1] - ra, meta_u8[16 * k0:16 * k1], seed=SEED, half=half,
+                                threads=threads)
+            assert bad == 0, f"{bad} blocks of [{k0}, {k1}) differ from the generator"
+            verified += k1 - k0
 
     # ---- timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -154,68 +217,89 @@ def main():
     elapsed = t_end - t_start
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     elapsed = max_over_ranks(dist, elapsed, device)
+    job_dec_bytes = sum_over_ranks(dist, dec_bytes, device)
 
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * dec_bytes * args.steps / elapsed / 2**30
+    value = job_dec_bytes * args.steps / elapsed / 2**30
 
-    # roofline of the dominant kernel (decode_lpb_kernel for Snappy): algorithmic bytes per launch
+    # roofline of the dominant kernel: algorithmic bytes per launch / its event time
     alg_read = enc_bytes + 8 * (n + 1) * 3  # encoded blocks incl. CRC + in_off/out_off/row_base
     alg_write = dec_bytes + 16 * n_rows + 16 * n  # decoded bytes + row descriptors + block meta
     alg = alg_read + alg_write
     achieved = alg / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.pmc_json):
-        try:
-            pm = json.load(open(args.pmc_json))
-            if pm.get("blocks") == n and pm.get("codec") == args.codec:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic(args.pmc_json, n, args.codec)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": {"snappy": "decode_lpb2_kernel", "zstd": "decode_fast_kernel<2>"}.get(args.codec, "decode_fast_kernel<0>"),
+                "kernel": {"snappy": "decode_lpb2_kernel", "zstd": "decode_fast_kernel<2>"}.get(args.codec,
+                                                                                           "decode_fast_kernel<0>"),
                 "kernel_ms": round(kern_ms, 4),
                 "alg_bytes_per_launch": alg, "alg_read_bytes": alg_read, "alg_write_bytes": alg_write,
-                "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+                "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "traffic_source": traffic_src}
 
+    if args.codec == "zstd":
+        workload = (f"configs[4] mixed: {n} x 4 KiB Zstd blocks per GPU, 1 KiB values, skewed key prefixes, "
+                    "device-resident decode")
+        data = ("synthetic (SURVEY 8d configs[4]: Zipf-prefixed 8-256 B keys, 1 KiB V-half values, libzstd "
+                "level 3 + checksum frames)")
+    else:
+        tag = f"{args.codec}, {args.values} values"
+        if args.workload == "configs1":
+            workload = (f"configs[1]: 1 M x 4 KiB Snappy blocks, 100 B KV, device-resident decode" if
+                        (n == 1_000_000 and args.codec == "snappy" and half) else
+                        f"{n} x 4 KiB blocks per GPU ({tag}), device-resident decode (not the headline config)")
+            if world > 1:
+                workload += f"; round-robin shards of one {set_blocks}-block set (block i on GPU i mod {world})"
+        else:
+            workload = (f"configs[3]: one set of {set_blocks} x 4 KiB Snappy blocks (64 GiB encoded), block i on GPU "
+                        f"i mod {world}; this rank decodes {n} of its {sc.shard_blocks(set_blocks, world, rank)}")
+        data = ("synthetic (SURVEY 8d keys k%015d, " + ("V-half" if half else "V-rand") + " values, " +
+                {"snappy": "libsnappy-encoded", "none": "CodecNone"}.get(args.codec, args.codec) +
+                ", every block generated on its own: tools/benchgen.c bg_build_set)")
     result = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-              "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-              "data": ("synthetic (SURVEY 8d configs[4]: Zipf-prefixed 8-256 B keys, 1 KiB V-half values, libzstd "
-                       "level 3 + checksum frames)" if args.codec == "zstd" else
-                       "synthetic (SURVEY 8d keys k%015d, V-half values, " + {"snappy": "libsnappy-encoded)",
-                                                                              "lz4": "liblz4 frames)",
-                                                                              "none": "CodecNone)"}[args.codec]),
-              "config": {"workload": ("configs[1]: 1 M x 4 KiB Snappy blocks, 100 B KV, device-resident decode"
-                                      if args.codec == "snappy" and n == 1_000_000 and args.values == "half"
-                                      else f"configs[4] mixed: {n} x 4 KiB Zstd blocks, 1 KiB values, skewed key "
-                                      "prefixes, device-resident decode (not the headline config)"
-                                      if args.codec == "zstd"
-                                      else f"{n} x 4 KiB {args.codec} blocks, 100 B KV ({args.values} values), "
-                                      "device-resident decode (not the headline config)"),
-                         "blocks_per_gpu": n, "codec": args.codec, "values": args.values, "block_size": 4096,
-                         "decoded_bytes_per_gpu": dec_bytes, "encoded_bytes_per_gpu": enc_bytes,
-                         "rows_per_gpu": n_rows, "parallelism": f"shard{world} (no collective)"},
-              "roofline": roofline}
+              "scaling": scaling, "vs_baseline": None, "dtype": "u8", "data": data,
+              "config": {"workload": workload, "blocks_per_gpu": n, "set_blocks": set_blocks, "codec": args.codec,
+                         "values": args.values, "block_size": 4096, "decoded_bytes_per_gpu": dec_bytes,
+                         "encoded_bytes_per_gpu": enc_bytes, "rows_per_gpu": n_rows,
+                         "parallelism": f"shard{world} round-robin (no collective)"},
+              "roofline": roofline,
+              "verified": {"blocks": verified, "mode": verify if shard is not None else "status only",
+                           "what": "every block's status; decoded bytes, meta and row descriptors vs the generator"}}
 
-    if rank == 0 and world == 1 and not args.no_host_io:
-        result["host_io"] = host_io_rate(torch, sc, ctx, codec, blob, in_off, dec_bytes, device)
-        result["host_io_pinned"] = host_io_pinned(torch, sc, codec, blob, in_off, device)
+    if rank == 0 and world == 1 and not args.no_host_io and shard is not None:
+        result["host_io"] = host_io_rate(sc, ctx, codec, blob, in_off)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(codec, blob, in_off, args.cpu_seconds)
 
     if rank == 0:
         result["gen_seconds"] = round(gen_s, 1)
+        result["lib_sha256"] = lib_sha256()[:16]
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
+def pmc_traffic(path: str, n: int, codec: str):
+    """HBM bytes per launch from the PMC passes (tools/traffic.sh), only when they were taken on
+    this very library build and workload."""
+    if not os.path.exists(path):
+        return None, "no PMC file"
+    try:
+        pm = json.load(open(path))
+    except (OSError, ValueError):
+        return None, "unreadable PMC file"
+    if pm.get("blocks") != n or pm.get("codec") != codec:
+        return None, "PMC file is for another workload"
+    if pm.get("lib_sha256") != lib_sha256():
+        return None, "PMC file is for another library build"
+    return pm.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+
+
 def shard_spec(rank: int, blocks_per_rank: int) -> dict:
-    """Rank r decodes its own blocks: a disjoint key range (38 keys per block, 40
-    reserved) and its own value seed, so every rank's shard is distinct data."""
-    return {"seed": 20250307 + rank, "kv_begin": rank * blocks_per_rank * 40}
+    """configs[4] (sequential generator): rank r gets its own seed and key range."""
+    return {"seed": SEED + rank, "kv_begin": rank * blocks_per_rank * 40}
 
 
 def max_over_ranks(dist, elapsed: float, device) -> float:
@@ -228,94 +312,54 @@ def max_over_ranks(dist, elapsed: float, device) -> float:
     return float(t.item())
 
 
-def host_io_pinned(torch, sc, codec, blob, in_off, device, n_streams=4, chunk=32768, max_blocks=262144):
-    """Host-in/host-out with pinned buffers: per chunk of blocks, H2D of the encoded
-    blocks + offsets, plan + decode, D2H of decoded bytes + block meta + row
-    descriptors; chunks round-robin over n_streams streams (one slate_ctx each) so
-    copies overlap kernels.  For DESIGN.md (PCIe-bound), never `value`."""
+def sum_over_ranks(dist, v: int, device) -> int:
+    if not dist:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+def host_io_rate(sc, ctx, codec, blob, in_off, max_blocks=262144):
+    """Host-in/host-out through the C-ABI itself (slate_block_decode_batch: page-locked staging,
+    chunks over two stream lanes), into caller buffers sized once from a plan-only call, and the
+    same batch sharded over two contexts (slate_block_decode_sharded).  PCIe-bound: for
+    DESIGN.md, never `value`."""
     n = min(len(in_off) - 1, max_blocks)
-    streams = [torch.cuda.Stream(device) for _ in range(n_streams)]
-    ctxs = []
-    for s in streams:
-        c = sc.Context(device.index)
-        c.set_stream(s.cuda_stream)
-        ctxs.append(c)
-    jobs = []
-    for a in range(0, n, chunk):
-        b = min(n, a + chunk)
-        m = b - a
-        lo, hi = int(in_off[a]), int(in_off[b])
-        h_in = torch.from_numpy(blob[lo:hi].copy()).pin_memory()
-        h_off = torch.from_numpy((in_off[a:b + 1] - in_off[a]).astype(np.int64)).pin_memory()
-        d_in = torch.empty(hi - lo, dtype=torch.uint8, device=device)
-        d_off = torch.empty(m + 1, dtype=torch.int64, device=device)
-        d_oo = torch.empty(m + 1, dtype=torch.int64, device=device)
-        d_rb = torch.empty(m + 1, dtype=torch.int64, device=device)
-        d_sc = torch.empty(sc.decode_scratch_bytes(m) + 64, dtype=torch.uint8, device=device)
-        d_in.copy_(h_in)
-        d_off.copy_(h_off)
-        ctxs[0].set_stream(torch.cuda.current_stream(device).cuda_stream)
-        ctxs[0].decode_plan_device(codec, d_in.data_ptr(), d_off.data_ptr(), m, d_oo.data_ptr(), d_rb.data_ptr(),
-                                   d_sc.data_ptr())
-        torch.cuda.synchronize(device)
-        ctxs[0].set_stream(streams[0].cuda_stream)
-        tot, rows = int(d_oo[m].item()), int(d_rb[m].item())
-        jobs.append(dict(m=m, h_in=h_in, h_off=h_off, d_in=d_in, d_off=d_off, d_oo=d_oo, d_rb=d_rb, d_sc=d_sc,
-                         d_out=torch.empty(tot + 16, dtype=torch.uint8, device=device),
-                         d_meta=torch.empty(m * 16, dtype=torch.uint8, device=device),
-                         d_rows=torch.empty(max(rows, 1) * 16, dtype=torch.uint8, device=device),
-                         h_out=torch.empty(tot + 16, dtype=torch.uint8).pin_memory(),
-                         h_meta=torch.empty(m * 16, dtype=torch.uint8).pin_memory(),
-                         h_rows=torch.empty(max(rows, 1) * 16, dtype=torch.uint8).pin_memory()))
-
-    def run():
-        for i, j in enumerate(jobs):
-            s, c = streams[i % n_streams], ctxs[i % n_streams]
-            with torch.cuda.stream(s):
-                j["d_in"].copy_(j["h_in"], non_blocking=True)
-                j["d_off"].copy_(j["h_off"], non_blocking=True)
-                c.decode_plan_device(codec, j["d_in"].data_ptr(), j["d_off"].data_ptr(), j["m"], j["d_oo"].data_ptr(),
-                                     j["d_rb"].data_ptr(), j["d_sc"].data_ptr())
-                c.decode_device(codec, j["d_in"].data_ptr(), j["d_off"].data_ptr(), j["m"], j["d_out"].data_ptr(),
-                                j["d_oo"].data_ptr(), j["d_meta"].data_ptr(), j["d_rows"].data_ptr(),
-                                j["d_rb"].data_ptr())
-                j["h_out"].copy_(j["d_out"], non_blocking=True)
-                j["h_meta"].copy_(j["d_meta"], non_blocking=True)
-                j["h_rows"].copy_(j["d_rows"], non_blocking=True)
-        torch.cuda.synchronize(device)
-
-    run()  # warm
-    t = time.perf_counter()
-    run()
-    el = time.perf_counter() - t
-    meta = np.concatenate([np.frombuffer(j["h_meta"].numpy().tobytes(), dtype=sc.META_DTYPE) for j in jobs])
-    assert (meta["status"] == 0).all()
+    sub_off = np.ascontiguousarray(in_off[: n + 1], np.uint64)
+    sub = np.ascontiguousarray(blob[: int(sub_off[n])])
+    ctx2 = sc.Context(ctx.device)
+    out_off = np.zeros(n + 1, np.uint64)
+    row_base = np.zeros(n + 1, np.uint64)
+    meta = np.zeros(n, sc.META_DTYPE)
+    st = ctx2.decode_batch_into(codec, sub, sub_off, np.zeros(1, np.uint8), np.zeros(1, sc.ROW_DTYPE), meta, out_off,
+                                row_base)
+    assert st == sc.E_CAPACITY, st
+    out = np.zeros(int(out_off[n]) + 16, np.uint8)
+    rows = np.zeros(int(row_base[n]) + 1, sc.ROW_DTYPE)
+    out.fill(0)
+    rows.fill(0)
+    for _ in range(2):  # the first call warms the context's staging and device buffers
+        t = time.perf_counter()
+        st = ctx2.decode_batch_into(codec, sub, sub_off, out, rows, meta, out_off, row_base)
+        el = time.perf_counter() - t
+        assert st == sc.OK and (meta["status"] == 0).all()
     dec = int(np.sum(meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2))
-    h2d = int(in_off[n]) + 8 * (n + len(jobs))
-    d2h = sum(j["h_out"].numel() + j["h_meta"].numel() + j["h_rows"].numel() for j in jobs)
-    for c in ctxs:
-        c.close()
-    return {"GiBps_decoded": round(dec / el / 2**30, 2), "blocks": n, "streams": n_streams, "chunk_blocks": chunk,
-            "h2d_GBps": round(h2d / el / 1e9, 2), "d2h_GBps": round(d2h / el / 1e9, 2),
-            "path": "pinned H2D + plan + decode + D2H (data, meta, rows), overlapped over streams"}
-
-
-def host_io_rate(torch, sc, ctx, codec, blob, in_off, dec_bytes, device):
-    """Host-in/host-out: pinned H2D of the encoded blocks + plan + decode + D2H of
-    the decoded blocks, through the C-ABI batch call (for DESIGN.md, never `value`)."""
-    n = len(in_off) - 1
-    m = min(n, 200_000)
-    sub_blob = blob[: int(in_off[m])]
-    sub_off = in_off[: m + 1]
-    ctx2 = sc.Context(device.index)
-    ctx2.decode_batch(codec, sub_blob, sub_off)  # warm (allocations)
+    res = {"GiBps_decoded": round(dec / el / 2**30, 2), "blocks": n,
+           "h2d_GBps": round(int(sub_off[n]) / el / 1e9, 2),
+           "d2h_GBps": round((int(out_off[n]) + 16 * int(row_base[n]) + 16 * n) / el / 1e9, 2),
+           "path": "slate_block_decode_batch: pageable caller buffers, page-locked staging, 2 stream lanes"}
+    ctx3 = sc.Context(ctx.device)
+    sc.decode_sharded([ctx2, ctx3], codec, sub[: int(sub_off[min(n, 4096)])], sub_off[: min(n, 4096) + 1])  # warm
     t = time.perf_counter()
-    out = ctx2.decode_batch(codec, sub_blob, sub_off)
+    o2 = sc.decode_sharded([ctx2, ctx3], codec, sub, sub_off)
     el = time.perf_counter() - t
+    assert (o2[2]["status"] == 0).all()
+    res["sharded_2ctx_GiBps_decoded"] = round(dec / el / 2**30, 2)
+    ctx3.close()
     ctx2.close()
-    sub_dec = int(out[1][-1])
-    return {"GiBps_decoded": round(sub_dec / el / 2**30, 2), "blocks": m,
-            "path": "slate_block_decode_batch (pageable host buffers, one stream, plan sync)"}
+    return res
 
 
 CODEC_RESTATEMENT = {0: "no codec", 1: "golang/snappy", 2: "compress/zlib+flate", 3: "LZ4 frame",
@@ -323,17 +367,18 @@ CODEC_RESTATEMENT = {0: "no codec", 1: "golang/snappy", 2: "compress/zlib+flate"
 
 
 def cpu_baseline(codec, blob, in_off, seconds):
-    """The oracle (C restatement of the Go path) timed on this host: bounded sample."""
+    """The oracle (C restatement of the Go path) timed on this host: bounded sample, on one
+    thread and on every CPU this process may use (affinity mask and cgroup quota)."""
     from oracle import binding as ob
     n = len(in_off) - 1
     chunk = 20_000
     res = {}
-    for threads in (1, min(16, os.cpu_count() or 1)):
+    for threads in sorted({1, min(64, host_cpus())}):
         done = 0
         dec = 0
         t = time.perf_counter()
         while time.perf_counter() - t < seconds / (1 if threads == 1 else 2) and done < n:
-            a, b = done, min(n, done + chunk)
+            a, b = done, min(n, done + chunk * max(1, threads // 8))
             sub_off = (in_off[a:b + 1] - in_off[a]).astype(np.uint64)
             out, o_off, meta, rows, rb = ob.block_decode_batch(codec, blob[int(in_off[a]):int(in_off[b])], sub_off,
                                                                nthreads=threads)
@@ -354,7 +399,8 @@ def cpu_baseline(codec, blob, in_off, seconds):
     return {"value": round(res[mt][0], 3), "unit": "GiB/s", "cores": mt, "kind": "port",
             "sample": f"first {res[mt][1]} of the same blocks, oracle/slate_oracle.c block decode "
                       f"(CRC32 + {CODEC_RESTATEMENT.get(codec, 'codec')} restatement + offsets + row walk), "
-                      f"{mt} threads",
+                      f"{mt} threads = every CPU this process may use, at most 64 (affinity/cgroup; os.cpu_count() = "
+                      f"{os.cpu_count()})",
             "single_thread": {"value": round(res[1][0], 3), "cores": 1, "blocks": res[1][1]},
             "cpu_model": cpu_model}
 

@@ -198,18 +198,39 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in,
                               const uint64_t* d_out_off, slate_block_meta* d_meta,
                               slate_row* d_rows, const uint64_t* d_row_base);
 
-/* Host-buffer convenience (object-store GET buffers in, caller buffers out):
- * stages through pinned memory, runs plan+decode, copies back, synchronises.
- * out_off/row_base are outputs (n+1 each); out_cap/rows_cap are capacities. */
+/* Host-buffer batch (object-store GET buffers in, caller buffers out; sstable.ReadBlocks,
+ * decode.go:107-149, and the compaction reads, compaction/executor.go:92-151): chunks of up to
+ * 64 K blocks go through page-locked staging on two stream lanes of the context (upload and plan
+ * of chunk c+1 overlap decode and download of chunk c); synchronous for the caller.
+ * out_off/row_base are outputs (n+1 each, always filled); out_cap/rows_cap are capacities:
+ * when the outputs do not fit (or out/meta are NULL) the call only plans and returns
+ * SLATE_E_CAPACITY with out_off[n] / row_base[n] the sizes needed. */
 int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off,
                              uint32_t n_blocks, uint8_t* out, uint64_t out_cap, uint64_t* out_off,
                              slate_block_meta* meta, slate_row* rows, uint64_t rows_cap,
                              uint64_t* row_base);
-/* Single block: block.Decode(&b, input, codec).  Data = out[0 .. meta.data_len);
+/* Single block: block.Decode(&b, input, codec) (block.go:78), the one-block-per-call pattern of
+ * sstable.Iterator.nextBlockIter (iterator.go:92-118).  Data = out[0 .. meta.data_len);
  * offsets[] receives Block.Offsets (meta.n_rows entries, capacity offsets_cap). */
 int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_len, uint8_t* out,
                        size_t out_cap, size_t* out_len, slate_block_meta* meta, uint16_t* offsets,
                        size_t offsets_cap);
+
+/* ---- round-robin sharding of one block set (BASELINE configs[3]) -------------
+ * Blocks are independent, so block i of a batch goes to shard i mod n_shards (one shard per
+ * GPU) with no collective.  slate_shard_blocks = blocks of one shard; slate_shard_pack copies
+ * them back to back (out_off: shard-local offsets, blocks+1 entries).  Host code: needs no GPU. */
+uint32_t slate_shard_blocks(uint32_t n_blocks, uint32_t n_shards, uint32_t shard);
+int slate_shard_pack(const uint8_t* in, const uint64_t* in_off, uint32_t n_blocks, uint32_t n_shards,
+                     uint32_t shard, uint8_t* out, uint64_t out_cap, uint64_t* out_off);
+/* One batch decoded by n_ctx contexts at once (one host thread each; contexts on different
+ * GPUs, or several on one): context g decodes shard g through the host pipeline, and the
+ * results come back in the original block order, laid out exactly as slate_block_decode_batch
+ * lays them out.  What a compactor process holding one slate_ctx per GPU calls. */
+int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec, const uint8_t* in,
+                               const uint64_t* in_off, uint32_t n_blocks, uint8_t* out,
+                               uint64_t out_cap, uint64_t* out_off, slate_block_meta* meta,
+                               slate_row* rows, uint64_t rows_cap, uint64_t* row_base);
 
 /* ---- block encode: block.Encode (block.go:54) ----------------------------------
  * Encodes one block (Data + Offsets) with codec: compress(Data || BE16 offsets ||

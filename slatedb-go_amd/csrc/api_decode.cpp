@@ -148,73 +148,6 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
   return SLATE_OK;
 }
 
-// Host-buffer batch: H2D, plan, (sync to size the outputs), decode, D2H.
-int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
-                             uint8_t* out, uint64_t out_cap, uint64_t* out_off, slate_block_meta* meta,
-                             slate_row* rows, uint64_t rows_cap, uint64_t* row_base) {
-  if (!ctx || !in_off || !out_off || !row_base || (n && (!meta || !in))) return SLATE_E_INVALID_ARG;
-  SLATE_HIP(ctx_bind(ctx));
-  hipStream_t st = ctx->stream;
-  const uint64_t total_in = in_off[n] - in_off[0];
-  // keep the device copy 16-byte aligned relative to the host layout
-  SLATE_HIP(ctx->d_in.ensure(total_in + 32));
-  SLATE_HIP(ctx->d_in_off.ensure((size_t(n) + 1) * 8));
-  SLATE_HIP(ctx->d_out_off.ensure((size_t(n) + 1) * 8));
-  SLATE_HIP(ctx->d_row_base.ensure((size_t(n) + 1) * 8));
-  SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes(n) + 64));
-  std::vector<uint64_t> rel(size_t(n) + 1);
-  for (uint32_t i = 0; i <= n; i++) rel[i] = in_off[i] - in_off[0];
-  if (total_in) SLATE_HIP(hipMemcpyAsync(ctx->d_in.p, in + in_off[0], total_in, hipMemcpyHostToDevice, st));
-  SLATE_HIP(hipMemcpyAsync(ctx->d_in_off.p, rel.data(), (size_t(n) + 1) * 8, hipMemcpyHostToDevice, st));
-  SLATE_HIP(launch_decode_plan(st, codec, ctx->d_in.as<uint8_t>(), ctx->d_in_off.as<uint64_t>(), n,
-                               ctx->d_out_off.as<uint64_t>(), ctx->d_row_base.as<uint64_t>(), ctx->d_scratch.p));
-  SLATE_HIP(hipMemcpyAsync(out_off, ctx->d_out_off.p, (size_t(n) + 1) * 8, hipMemcpyDeviceToHost, st));
-  SLATE_HIP(hipMemcpyAsync(row_base, ctx->d_row_base.p, (size_t(n) + 1) * 8, hipMemcpyDeviceToHost, st));
-  SLATE_HIP(hipStreamSynchronize(st));
-  const uint64_t total_out = out_off[n], total_rows = row_base[n];
-  if (total_out > out_cap || total_rows > rows_cap || (total_out && !out) || (total_rows && !rows))
-    return SLATE_E_CAPACITY;
-  if (n == 0) return SLATE_OK;
-  SLATE_HIP(ctx->d_out.ensure(total_out + 16));
-  SLATE_HIP(ctx->d_meta.ensure(size_t(n) * sizeof(slate_block_meta)));
-  SLATE_HIP(ctx->d_rows.ensure((total_rows + 1) * sizeof(slate_row)));
-  DecodeArgs a{codec, ctx->d_in.as<uint8_t>(), ctx->d_in_off.as<uint64_t>(), n, ctx->d_out.as<uint8_t>(),
-               ctx->d_out_off.as<uint64_t>(), ctx->d_meta.as<slate_block_meta>(), ctx->d_rows.as<slate_row>(),
-               ctx->d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
-  SLATE_HIP(launch_decode(st, a, ctx->d_scratch.p, ctx->num_cus));
-  if (total_out) SLATE_HIP(hipMemcpyAsync(out, ctx->d_out.p, total_out, hipMemcpyDeviceToHost, st));
-  SLATE_HIP(hipMemcpyAsync(meta, ctx->d_meta.p, size_t(n) * sizeof(slate_block_meta), hipMemcpyDeviceToHost, st));
-  if (total_rows)
-    SLATE_HIP(hipMemcpyAsync(rows, ctx->d_rows.p, total_rows * sizeof(slate_row), hipMemcpyDeviceToHost, st));
-  SLATE_HIP(hipStreamSynchronize(st));
-  return SLATE_OK;
-}
-
-int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_len, uint8_t* out, size_t out_cap,
-                       size_t* out_len, slate_block_meta* meta, uint16_t* offsets, size_t offsets_cap) {
-  if (!ctx || !meta || (in_len && !in)) return SLATE_E_INVALID_ARG;
-  uint64_t in_off[2] = {0, in_len}, out_off[2], row_base[2];
-  // decode into a scratch host vector (the batch output is 16-byte padded)
-  std::vector<uint8_t> tmp;
-  std::vector<slate_row> rows;
-  // size pass
-  int st = slate_block_decode_batch(ctx, codec, in, in_off, 1, nullptr, 0, out_off, meta, nullptr, 0, row_base);
-  if (st == SLATE_E_CAPACITY) {
-    tmp.resize(out_off[1] + 16);
-    rows.resize(row_base[1] + 1);
-    st = slate_block_decode_batch(ctx, codec, in, in_off, 1, tmp.data(), tmp.size(), out_off, meta, rows.data(),
-                                  rows.size(), row_base);
-  }
-  if (st != SLATE_OK) return st;
-  if (meta->status != SLATE_OK) return meta->status;
-  // Decoded length = data_len + 2 * n_rows + 2 for a successfully decoded block.
-  size_t dl = size_t(meta->data_len) + 2 * size_t(meta->n_rows) + 2;
-  if (out_len) *out_len = dl;
-  if (dl > out_cap || (offsets && meta->n_rows > offsets_cap)) return SLATE_E_CAPACITY;
-  if (out && dl) memcpy(out, tmp.data(), dl);
-  if (offsets)
-    for (uint32_t i = 0; i < meta->n_rows; i++) offsets[i] = ld_be16(tmp.data() + meta->data_len + 2 * i);
-  return SLATE_OK;
-}
+// slate_block_decode_batch / slate_block_decode / the sharded decode: api_host.cpp.
 
 }  // extern "C"

@@ -1,0 +1,374 @@
+// C-ABI: host-buffer block decode (object-store GET buffers in, caller buffers out) and the
+// round-robin sharding of one block set over several contexts / GPUs.
+//
+// Reference callers: sstable.ReadBlocks (internal/sstable/decode.go:107-149) and the
+// compaction executor's per-SST block reads (slatedb/compaction/executor.go:92-151,
+// internal/sstable/iterator.go:92-118).  Blocks are independent, so a batch is
+// decoded in chunks through page-locked staging on two stream lanes per context, and a batch
+// spread over G contexts sends block i to context i mod G with no collective.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "host_ctx.h"
+
+using namespace slate;
+
+namespace {
+
+constexpr uint32_t kChunkBlocks = 65536;
+constexpr uint64_t kChunkBytes = 96ull << 20;
+
+// memcpy split over threads for large copies between caller memory and page-locked staging
+// (one core copies ~10 GB/s, below what the PCIe link moves).
+void par_memcpy(void* dst, const void* src, size_t n) {
+  constexpr size_t kPiece = 8u << 20;
+  if (n < 2 * kPiece) {
+    if (n) memcpy(dst, src, n);
+    return;
+  }
+  const size_t t = std::min<size_t>(8, n / kPiece);
+  const size_t step = (n + t - 1) / t;
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < t; i++) {
+    const size_t a = i * step;
+    if (a >= n) break;
+    const size_t b = std::min(n, a + step);
+    th.emplace_back([=] { memcpy(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, b - a); });
+  }
+  memcpy(dst, src, std::min(n, step));
+  for (auto& x : th) x.join();
+}
+
+hipError_t lane_init(PipeLane& L) {
+  if (L.stream) return hipSuccess;
+  hipError_t e = hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  e = hipEventCreateWithFlags(&L.planned, hipEventDisableTiming);
+  if (e != hipSuccess) return e;
+  return hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
+}
+
+// Where decoded chunks go: the caller's arrays, or (sharded decode) vectors that grow per chunk.
+struct Sink {
+  uint8_t* out = nullptr;
+  uint64_t out_cap = 0;
+  uint64_t* out_off = nullptr;
+  slate_block_meta* meta = nullptr;
+  slate_row* rows = nullptr;
+  uint64_t rows_cap = 0;
+  uint64_t* row_base = nullptr;
+  // growable mode
+  std::vector<uint8_t>* v_out = nullptr;
+  std::vector<slate_row>* v_rows = nullptr;
+  std::vector<slate_block_meta>* v_meta = nullptr;
+  std::vector<uint64_t>* v_out_off = nullptr;
+  std::vector<uint64_t>* v_row_base = nullptr;
+};
+
+// The lane's chunk is decoded: copy its outputs into the sink.
+int lane_finish(PipeLane& L, Sink& o) {
+  if (!L.busy) return SLATE_OK;
+  L.busy = false;
+  SLATE_HIP(hipEventSynchronize(L.done));
+  if (!L.decoded) return SLATE_OK;
+  uint8_t* out = o.out;
+  slate_row* rows = o.rows;
+  slate_block_meta* meta = o.meta;
+  if (o.v_out) {
+    if (o.v_out->size() < L.out_base + L.out_total) o.v_out->resize(L.out_base + L.out_total);
+    if (o.v_rows->size() < L.row_base + L.rows_total) o.v_rows->resize(L.row_base + L.rows_total);
+    if (o.v_meta->size() < size_t(L.b0) + L.n) o.v_meta->resize(size_t(L.b0) + L.n);
+    out = o.v_out->data();
+    rows = o.v_rows->data();
+    meta = o.v_meta->data();
+  }
+  par_memcpy(out + L.out_base, L.h_out.p, L.out_total);
+  memcpy(meta + L.b0, L.h_meta.p, size_t(L.n) * sizeof(slate_block_meta));
+  par_memcpy(rows + L.row_base, L.h_rows.p, L.rows_total * sizeof(slate_row));
+  return SLATE_OK;
+}
+
+// Decode n host blocks: chunks of up to kChunkBlocks / kChunkBytes alternate between the two
+// lanes.  Per chunk: staging copy, H2D, plan, (wait for the plan: the chunk's place in the
+// outputs), decode, D2H into staging; the previous chunk's staging is copied out meanwhile.
+// out_off/row_base are always filled; when the outputs do not fit (or are absent) the
+// remaining chunks are only planned and SLATE_E_CAPACITY is returned.
+int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o) {
+  SLATE_HIP(ctx_bind(ctx));
+  // chunk size in blocks; SLATE_PIPE_CHUNK_BLOCKS lowers it so tests cover many chunks cheaply
+  static const uint32_t chunk_blocks = [] {
+    const char* e = getenv("SLATE_PIPE_CHUNK_BLOCKS");
+    const unsigned long v = e ? strtoul(e, nullptr, 0) : 0;
+    return v ? uint32_t(std::min<unsigned long>(v, kChunkBlocks)) : kChunkBlocks;
+  }();
+  uint64_t out_acc = 0, rows_acc = 0;
+  bool fits = o.v_out != nullptr || (o.meta != nullptr);
+  uint64_t* out_off = o.out_off;
+  uint64_t* row_base = o.row_base;
+  if (o.v_out_off) {
+    o.v_out_off->assign(size_t(n) + 1, 0);
+    o.v_row_base->assign(size_t(n) + 1, 0);
+    out_off = o.v_out_off->data();
+    row_base = o.v_row_base->data();
+  }
+  out_off[0] = 0;
+  row_base[0] = 0;
+  int li = 0;
+  for (uint32_t b = 0; b < n;) {
+    uint32_t e = b + 1;
+    while (e < n && e - b < chunk_blocks && in_off[e + 1] - in_off[b] <= kChunkBytes) e++;
+    const uint32_t m = e - b;
+    const uint64_t lo = in_off[b], bytes = in_off[e] - lo;
+    if (in_off[e] < lo) return SLATE_E_INVALID_ARG;
+    PipeLane& L = ctx->lanes[li];
+    li = (li + 1) % kPipeLanes;
+    SLATE_HIP(lane_init(L));
+    int st = lane_finish(L, o);
+    if (st) return st;
+    SLATE_HIP(L.h_in.ensure(bytes + 16));
+    SLATE_HIP(L.h_in_off.ensure((size_t(m) + 1) * 8));
+    SLATE_HIP(L.h_plan.ensure(2 * (size_t(m) + 1) * 8));
+    SLATE_HIP(L.d_in.ensure(bytes + 32));
+    SLATE_HIP(L.d_in_off.ensure((size_t(m) + 1) * 8));
+    SLATE_HIP(L.d_out_off.ensure((size_t(m) + 1) * 8));
+    SLATE_HIP(L.d_row_base.ensure((size_t(m) + 1) * 8));
+    SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes(m) + 64));
+    par_memcpy(L.h_in.p, in + lo, bytes);
+    uint64_t* ho = L.h_in_off.as<uint64_t>();
+    for (uint32_t i = 0; i <= m; i++) ho[i] = in_off[b + i] - lo;
+    hipStream_t s = L.stream;
+    if (bytes) SLATE_HIP(hipMemcpyAsync(L.d_in.p, L.h_in.p, bytes, hipMemcpyHostToDevice, s));
+    SLATE_HIP(hipMemcpyAsync(L.d_in_off.p, ho, (size_t(m) + 1) * 8, hipMemcpyHostToDevice, s));
+    SLATE_HIP(launch_decode_plan(s, codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), m,
+                                 L.d_out_off.as<uint64_t>(), L.d_row_base.as<uint64_t>(), L.d_scratch.p));
+    uint64_t* po = L.h_plan.as<uint64_t>();
+    uint64_t* pr = po + m + 1;
+    SLATE_HIP(hipMemcpyAsync(po, L.d_out_off.p, (size_t(m) + 1) * 8, hipMemcpyDeviceToHost, s));
+    SLATE_HIP(hipMemcpyAsync(pr, L.d_row_base.p, (size_t(m) + 1) * 8, hipMemcpyDeviceToHost, s));
+    SLATE_HIP(hipEventRecord(L.planned, s));
+    SLATE_HIP(hipEventSynchronize(L.planned));
+    for (uint32_t i = 1; i <= m; i++) {
+      out_off[b + i] = out_acc + po[i];
+      row_base[b + i] = rows_acc + pr[i];
+    }
+    L.b0 = b;
+    L.n = m;
+    L.out_base = out_acc;
+    L.row_base = rows_acc;
+    L.out_total = po[m];
+    L.rows_total = pr[m];
+    out_acc += po[m];
+    rows_acc += pr[m];
+    if (!o.v_out)
+      fits = fits && out_acc <= o.out_cap && rows_acc <= o.rows_cap && (out_acc == 0 || o.out) &&
+             (rows_acc == 0 || o.rows);
+    L.busy = true;
+    L.decoded = false;
+    if (fits) {
+      SLATE_HIP(L.d_out.ensure(L.out_total + 16));
+      SLATE_HIP(L.d_meta.ensure(size_t(m) * sizeof(slate_block_meta)));
+      SLATE_HIP(L.d_rows.ensure((L.rows_total + 1) * sizeof(slate_row)));
+      SLATE_HIP(L.h_out.ensure(L.out_total + 16));
+      SLATE_HIP(L.h_meta.ensure(size_t(m) * sizeof(slate_block_meta)));
+      SLATE_HIP(L.h_rows.ensure((L.rows_total + 1) * sizeof(slate_row)));
+      DecodeArgs a{codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), m, L.d_out.as<uint8_t>(),
+                   L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
+                   L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
+      SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
+      if (L.out_total) SLATE_HIP(hipMemcpyAsync(L.h_out.p, L.d_out.p, L.out_total, hipMemcpyDeviceToHost, s));
+      SLATE_HIP(hipMemcpyAsync(L.h_meta.p, L.d_meta.p, size_t(m) * sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
+      if (L.rows_total)
+        SLATE_HIP(hipMemcpyAsync(L.h_rows.p, L.d_rows.p, L.rows_total * sizeof(slate_row), hipMemcpyDeviceToHost, s));
+      L.decoded = true;
+    }
+    SLATE_HIP(hipEventRecord(L.done, s));
+    b = e;
+  }
+  for (PipeLane& L : ctx->lanes) {
+    int st = lane_finish(L, o);
+    if (st) return st;
+  }
+  if (o.v_out) {  // every chunk decoded: size the vectors exactly (zero-block shards included)
+    o.v_out->resize(out_acc);
+    o.v_rows->resize(rows_acc);
+    o.v_meta->resize(n);
+  }
+  return fits ? SLATE_OK : SLATE_E_CAPACITY;
+}
+
+uint32_t shard_count(uint32_t n, uint32_t g, uint32_t s) { return s < n ? (n - s + g - 1) / g : 0u; }
+
+}  // namespace
+
+extern "C" {
+
+int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
+                             uint8_t* out, uint64_t out_cap, uint64_t* out_off, slate_block_meta* meta,
+                             slate_row* rows, uint64_t rows_cap, uint64_t* row_base) {
+  if (!ctx || !in_off || !out_off || !row_base || (n && !in)) return SLATE_E_INVALID_ARG;
+  if (n == 0) {
+    out_off[0] = row_base[0] = 0;
+    return SLATE_OK;
+  }
+  Sink o;
+  o.out = out;
+  o.out_cap = out_cap;
+  o.out_off = out_off;
+  o.meta = meta;
+  o.rows = rows;
+  o.rows_cap = rows_cap;
+  o.row_base = row_base;
+  return host_decode(ctx, codec, in, in_off, n, o);
+}
+
+// One block, lowest latency: pinned staging, plan, decode, two synchronisations.
+int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_len, uint8_t* out, size_t out_cap,
+                       size_t* out_len, slate_block_meta* meta, uint16_t* offsets, size_t offsets_cap) {
+  if (!ctx || !meta || (in_len && !in)) return SLATE_E_INVALID_ARG;
+  if (in_len >= 0xFFFFFFF0ull) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  PipeLane& L = ctx->lanes[0];
+  SLATE_HIP(lane_init(L));
+  hipStream_t s = L.stream;
+  SLATE_HIP(ctx->h_small.ensure(in_len + 256));
+  uint8_t* h = ctx->h_small.as<uint8_t>();
+  uint64_t* hv = reinterpret_cast<uint64_t*>(h);  // in_off[2] | out_off[2] | row_base[2] | meta (16 B)
+  uint8_t* hin = h + 128;
+  hv[0] = 0;
+  hv[1] = in_len;
+  if (in_len) memcpy(hin, in, in_len);
+  SLATE_HIP(L.d_in.ensure(in_len + 32));
+  SLATE_HIP(L.d_in_off.ensure(64));
+  SLATE_HIP(L.d_out_off.ensure(64));
+  SLATE_HIP(L.d_row_base.ensure(64));
+  SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes(1) + 64));
+  SLATE_HIP(L.d_meta.ensure(64));
+  if (in_len) SLATE_HIP(hipMemcpyAsync(L.d_in.p, hin, in_len, hipMemcpyHostToDevice, s));
+  SLATE_HIP(hipMemcpyAsync(L.d_in_off.p, hv, 16, hipMemcpyHostToDevice, s));
+  SLATE_HIP(launch_decode_plan(s, codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), 1,
+                               L.d_out_off.as<uint64_t>(), L.d_row_base.as<uint64_t>(), L.d_scratch.p));
+  SLATE_HIP(hipMemcpyAsync(hv + 2, L.d_out_off.p, 16, hipMemcpyDeviceToHost, s));
+  SLATE_HIP(hipMemcpyAsync(hv + 4, L.d_row_base.p, 16, hipMemcpyDeviceToHost, s));
+  SLATE_HIP(hipStreamSynchronize(s));
+  const uint64_t cap = hv[3], slots = hv[5];
+  SLATE_HIP(L.d_out.ensure(cap + 16));
+  SLATE_HIP(L.d_rows.ensure((slots + 1) * sizeof(slate_row)));
+  SLATE_HIP(L.h_out.ensure(cap + 16));
+  DecodeArgs a{codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), 1, L.d_out.as<uint8_t>(),
+               L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
+               L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
+  SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
+  SLATE_HIP(hipMemcpyAsync(hv + 6, L.d_meta.p, sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
+  if (cap) SLATE_HIP(hipMemcpyAsync(L.h_out.p, L.d_out.p, cap, hipMemcpyDeviceToHost, s));
+  SLATE_HIP(hipStreamSynchronize(s));
+  memcpy(meta, hv + 6, sizeof(slate_block_meta));
+  if (meta->status != SLATE_OK) return meta->status;
+  // decoded length = data_len + 2 * n_rows + 2 for a successfully decoded block
+  const size_t dl = size_t(meta->data_len) + 2 * size_t(meta->n_rows) + 2;
+  if (out_len) *out_len = dl;
+  if (dl > out_cap || (offsets && meta->n_rows > offsets_cap)) return SLATE_E_CAPACITY;
+  const uint8_t* dec = L.h_out.as<uint8_t>();
+  if (out && dl) memcpy(out, dec, dl);
+  if (offsets)
+    for (uint32_t i = 0; i < meta->n_rows; i++) offsets[i] = ld_be16(dec + meta->data_len + 2 * i);
+  return SLATE_OK;
+}
+
+uint32_t slate_shard_blocks(uint32_t n_blocks, uint32_t n_shards, uint32_t shard) {
+  if (n_shards == 0 || shard >= n_shards) return 0;
+  return shard_count(n_blocks, n_shards, shard);
+}
+
+int slate_shard_pack(const uint8_t* in, const uint64_t* in_off, uint32_t n_blocks, uint32_t n_shards, uint32_t shard,
+                     uint8_t* out, uint64_t out_cap, uint64_t* out_off) {
+  if (!in_off || !out_off || n_shards == 0 || shard >= n_shards) return SLATE_E_INVALID_ARG;
+  const uint32_t m = shard_count(n_blocks, n_shards, shard);
+  uint64_t pos = 0;
+  out_off[0] = 0;
+  for (uint32_t j = 0; j < m; j++) {
+    const uint64_t i = uint64_t(shard) + uint64_t(j) * n_shards;
+    if (in_off[i + 1] < in_off[i]) return SLATE_E_INVALID_ARG;
+    pos += in_off[i + 1] - in_off[i];
+    out_off[j + 1] = pos;
+  }
+  if (pos > out_cap || (pos && (!out || !in))) return SLATE_E_CAPACITY;
+  for (uint32_t j = 0; j < m; j++) {
+    const uint64_t i = uint64_t(shard) + uint64_t(j) * n_shards;
+    if (out_off[j + 1] > out_off[j]) memcpy(out + out_off[j], in + in_off[i], out_off[j + 1] - out_off[j]);
+  }
+  return SLATE_OK;
+}
+
+int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec, const uint8_t* in,
+                               const uint64_t* in_off, uint32_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_off,
+                               slate_block_meta* meta, slate_row* rows, uint64_t rows_cap, uint64_t* row_base) {
+  if (!ctxs || n_ctx == 0 || !in_off || !out_off || !row_base || (n && !in)) return SLATE_E_INVALID_ARG;
+  for (uint32_t g = 0; g < n_ctx; g++)
+    if (!ctxs[g]) return SLATE_E_INVALID_ARG;
+  struct Shard {
+    std::vector<uint8_t> in, out;
+    std::vector<uint64_t> in_off, out_off, row_base;
+    std::vector<slate_block_meta> meta;
+    std::vector<slate_row> rows;
+    int st = SLATE_OK;
+  };
+  std::vector<Shard> sh(n_ctx);
+  auto work = [&](uint32_t g) {
+    Shard& S = sh[g];
+    const uint32_t m = shard_count(n, n_ctx, g);
+    S.in_off.assign(size_t(m) + 1, 0);
+    uint64_t bytes = 0;
+    for (uint32_t j = 0; j < m; j++) {
+      const uint64_t i = uint64_t(g) + uint64_t(j) * n_ctx;
+      bytes += in_off[i + 1] - in_off[i];
+    }
+    S.in.resize(bytes + 1);
+    S.st = slate_shard_pack(in, in_off, n, n_ctx, g, S.in.data(), bytes, S.in_off.data());
+    if (S.st || m == 0) return;
+    Sink o;
+    o.v_out = &S.out;
+    o.v_rows = &S.rows;
+    o.v_meta = &S.meta;
+    o.v_out_off = &S.out_off;
+    o.v_row_base = &S.row_base;
+    S.st = host_decode(ctxs[g], codec, S.in.data(), S.in_off.data(), m, o);
+  };
+  {
+    std::vector<std::thread> th;
+    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(work, g);
+    work(0);
+    for (auto& t : th) t.join();
+  }
+  for (uint32_t g = 0; g < n_ctx; g++)
+    if (sh[g].st) return sh[g].st;
+  // the outputs in the original block order
+  out_off[0] = row_base[0] = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const Shard& S = sh[i % n_ctx];
+    const uint32_t j = i / n_ctx;
+    out_off[i + 1] = out_off[i] + (S.out_off[j + 1] - S.out_off[j]);
+    row_base[i + 1] = row_base[i] + (S.row_base[j + 1] - S.row_base[j]);
+  }
+  if (n == 0) return SLATE_OK;
+  if (!meta || out_off[n] > out_cap || row_base[n] > rows_cap || (out_off[n] && !out) || (row_base[n] && !rows))
+    return SLATE_E_CAPACITY;
+  auto scatter = [&](uint32_t g) {
+    const Shard& S = sh[g];
+    for (uint32_t j = 0, i = g; i < n; j++, i += n_ctx) {
+      const uint64_t ob = S.out_off[j + 1] - S.out_off[j], rb = S.row_base[j + 1] - S.row_base[j];
+      if (ob) memcpy(out + out_off[i], S.out.data() + S.out_off[j], ob);
+      if (rb) memcpy(rows + row_base[i], S.rows.data() + S.row_base[j], rb * sizeof(slate_row));
+      meta[i] = S.meta[j];
+    }
+  };
+  std::vector<std::thread> th;
+  for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(scatter, g);
+  scatter(0);
+  for (auto& t : th) t.join();
+  return SLATE_OK;
+}
+
+}  // extern "C"

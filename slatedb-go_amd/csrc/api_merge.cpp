@@ -77,7 +77,10 @@ int slate_merge_sorted(slate_ctx* ctx, uint32_t k, const uint8_t* keys, const ui
   SLATE_HIP(hipMemcpyAsync(&flags, d_flags, 4, hipMemcpyDeviceToHost, s));
   SLATE_HIP(hipStreamSynchronize(s));
   if (flags & 1) return SLATE_E_MERGE_UNSORTED;
-  if (hn) SLATE_HIP(hipMemcpy(out_idx, d_out, 4 * hn, hipMemcpyDeviceToHost));
+  if (hn) {
+    SLATE_HIP(hipMemcpyAsync(out_idx, d_out, 4 * hn, hipMemcpyDeviceToHost, s));
+    SLATE_HIP(hipStreamSynchronize(s));
+  }
   *n_out = hn;
   return SLATE_OK;
 }

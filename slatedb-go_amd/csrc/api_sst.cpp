@@ -160,7 +160,8 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
     *bstatus = h_st;
     if (h_st == SLATE_OK) {
       out.resize(dl);
-      SLATE_HIP(hipMemcpy(out.data(), ctx->d_out.p, dl, hipMemcpyDeviceToHost));
+      SLATE_HIP(hipMemcpyAsync(out.data(), ctx->d_out.p, dl, hipMemcpyDeviceToHost, st));
+      SLATE_HIP(hipStreamSynchronize(st));
     }
     return SLATE_OK;
   }
@@ -182,7 +183,10 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
   *bstatus = m.status;
   if (m.status == SLATE_OK) {
     out.resize(m.data_len);
-    if (m.data_len) SLATE_HIP(hipMemcpy(out.data(), ctx->d_out.p, m.data_len, hipMemcpyDeviceToHost));
+    if (m.data_len) {
+      SLATE_HIP(hipMemcpyAsync(out.data(), ctx->d_out.p, m.data_len, hipMemcpyDeviceToHost, st));
+      SLATE_HIP(hipStreamSynchronize(st));
+    }
   }
   return SLATE_OK;
 }

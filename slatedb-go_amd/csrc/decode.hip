@@ -909,7 +909,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   __builtin_amdgcn_wave_barrier();
   uint32_t clen = uint32_t(len - 4);
   uint32_t stored = ld_be32(w.in + shift + clen);
-  uint32_t crc = (a.debug & 1) ? stored : wave_crc32(w.tab, w.in, int32_t(shift), clen, lane);
+  uint32_t crc = (dbg_bits(a) & 1) ? stored : wave_crc32(w.tab, w.in, int32_t(shift), clen, lane);
   if (stored != crc) {
     m.status = SLATE_E_BLOCK_CHECKSUM;
     write_meta(&a.meta[b], m, lane);
@@ -927,7 +927,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
       write_meta(&a.meta[b], m, lane);
       return true;
     }
-    int st = (a.debug & 2) ? SLATE_OK : wave_snappy_decode(w.in + shift, clen, hdr, w.out, uint32_t(dl), lane);
+    int st = (dbg_bits(a) & 2) ? SLATE_OK : wave_snappy_decode(w.in + shift, clen, hdr, w.out, uint32_t(dl), lane);
     if (st != SLATE_OK) {
       m.status = int16_t(st);
       write_meta(&a.meta[b], m, lane);
@@ -937,7 +937,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     n = uint32_t(dl);
   } else if (CK == 0 && a.codec == SLATE_CODEC_LZ4) {
     uint32_t outn = 0;
-    int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)  // profiling: skip the decompression
+    int st = (dbg_bits(a) & 2) ? (outn = uint32_t(dl), SLATE_OK)  // profiling: skip the decompression
                            : wave_lz4_decode(w.in, shift, clen, w.out, uint32_t(dl), lane, &outn);
     if (st != SLATE_OK) {
       m.status = int16_t(st);
@@ -948,7 +948,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     n = outn;
   } else if (CK == 1 && a.codec == SLATE_CODEC_ZLIB) {
     uint32_t outn = 0;
-    int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)
+    int st = (dbg_bits(a) & 2) ? (outn = uint32_t(dl), SLATE_OK)
                            : wave_inflate(w.in + shift, clen, w.out, uint32_t(dl), w.zs, w.zfix, w.zfix + 1, lane, &outn);
     if (st != SLATE_OK) {
       m.status = int16_t(st);
@@ -959,9 +959,9 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     n = outn;
   } else if (CK == 2 && a.codec == SLATE_CODEC_ZSTD) {
     uint32_t outn = 0;
-    int st = (a.debug & 2) ? (outn = uint32_t(dl), SLATE_OK)
+    int st = (dbg_bits(a) & 2) ? (outn = uint32_t(dl), SLATE_OK)
                            : wave_zstd_decode(w.in, int32_t(shift), clen, w.out, uint32_t(dl), w.zss, w.zsh, lane, &outn,
-                                              a.debug);
+                                              dbg_bits(a));
     if (st != SLATE_OK) {
       m.status = int16_t(st);
       write_meta(&a.meta[b], m, lane);
@@ -976,7 +976,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   }
   __builtin_amdgcn_wave_barrier();
   // ---- write the decoded buffer back (16-aligned destination)
-  if (!(a.debug & 8)) {
+  if (!(dbg_bits(a) & 8)) {
     uint8_t* gout = a.out + a.out_off[b];
     uint32_t chunks = (n + 15) / 16;
     if (buf == w.out) {
@@ -1062,7 +1062,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     if (r0.status == SLATE_OK) fk = int(sl0);
   }
   slate_row* grows = a.rows + rb;
-  if (a.debug & 4) nr = 0;
+  if (dbg_bits(a) & 4) nr = 0;
   for (uint32_t i = lane; i < nr; i += kWave) {
     slate_row r;
     uint32_t sl;
@@ -1186,18 +1186,21 @@ hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t m, void* scratc
 
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratch, int num_cus) {
   DecodeArgs a = args_in;
-  const char* dbg = getenv("SLATE_DEBUG_MODE");  // profiling ablations only
+#ifdef SLATE_PROFILING_BUILD
+  const char* dbg = getenv("SLATE_DEBUG_MODE");  // profiling variants only (tools/variant.sh)
   a.debug = dbg ? uint32_t(strtoul(dbg, nullptr, 0)) : 0u;
+#else
+  a.debug = 0;
+#endif
+  a.rt_zero = 0;
   DecodeScratch s = carve(scratch, a.n);
   a.large_list = s.large_list;
   a.large_count = s.large_count;
   (void)hipMemsetAsync(s.large_count, 0, sizeof(uint32_t), st);
   if (a.n == 0) return hipGetLastError();
-  // Snappy: lane-per-block streaming decoder (any block size); SLATE_DEBUG_MODE bit 16
-  // selects the wave-per-block path instead (ablation only)
-  // (bit 32: the v1 lane-per-block kernel, A/B only)
-  if (a.codec == SLATE_CODEC_SNAPPY && !(a.debug & 16))
-    return (a.debug & 32) ? launch_decode_lpb(st, a, num_cus) : launch_decode_lpb2(st, a, num_cus);
+  // Snappy: lane-per-block streaming decoder (any block size); ablation bit 16 (profiling
+  // variants only) selects the wave-per-block path instead
+  if (a.codec == SLATE_CODEC_SNAPPY && !(dbg_bits(a) & 16)) return launch_decode_lpb2(st, a, num_cus);
   const size_t lds = a.codec == SLATE_CODEC_ZSTD
                          ? kTabBytes + (kDecodeThreads / 64) * size_t(kZsFastInCap + kZsFastOutCap + kZsScratch) + kZsShared
                          : kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap) +

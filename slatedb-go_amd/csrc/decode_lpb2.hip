@@ -129,7 +129,7 @@ __device__ __forceinline__ uint32_t be16_of(uint32_t w) { return ((w & 0xff) << 
 __device__ __forceinline__ v2u rd64(const uint8_t* ring, uint32_t a, uint32_t m8 = kOR - 8) {
   return *reinterpret_cast<const v2u*>(ring + (a & m8));
 }
-// z is a run-time zero (DecodeArgs::debug >> 31): it keeps the compiler from fusing two b64
+// z is a run-time zero (DecodeArgs::rt_zero): it keeps the compiler from fusing two b64
 // accesses 8 bytes apart into ds_read2_b64 / ds_write2_b64, which cost ~55 CU-cycles per
 // wave-instruction at these addresses (tools/lds_cost_probe.hip) against ~3 for two
 // ds_read_b64.
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     L.crc = 0xFFFFFFFFu;
     L.crc_pos = 0;
     L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = L.T = 0;
-    L.z = a.debug >> 31;  // the host never sets bit 31
+    L.z = a.rt_zero;
     L.eff = 16;
     L.dd = 1;
     L.c_issue = L.c_commit = L.n_req = L.fpend = L.fready = L.fl = 0;
@@ -764,7 +764,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
 
     // ---------------- streaming decode, 64 blocks in lockstep
     uint32_t iters = 0, fin_iter = 0;
-    const uint64_t t_round = (a.debug & 512) ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t t_round = (dbg_bits(a) & 512) ? __builtin_amdgcn_s_memtime() : 0;
     // a lane is done when its decode is finished, no hole is pending, and every chunk
     // is committed and in the CRC.  Every step consumes input, produces output or waits
     // on a load issued at most one iteration earlier, so a block needs far fewer than
@@ -796,20 +796,20 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         L.n_req = n;
       }
       absorb_far(L, Q, FD, ring);
-      lane_step<0>(L, FD, act, ring, in, tab, R, a.debug);
-      lane_step<1>(L, FD, act, ring, in, tab, R, a.debug);
-      lane_step<2>(L, FD, act, ring, in, tab, R, a.debug);
-      lane_step<3>(L, FD, act, ring, in, tab, R, a.debug);
+      lane_step<0>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<1>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<2>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<3>(L, FD, act, ring, in, tab, R, dbg_bits(a));
       // the far-copy / hole source requested in this iteration (at most one per lane; sc1:
       // L1 bypass), before the flush stores so that vmcnt waits stay static; it is merged
       // at the start of the next iteration
-      Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (a.debug & 32768) ? kOOB : L.qoff, 0, 16);
+      Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg_bits(a) & 32768) ? kOOB : L.qoff, 0, 16);
       L.qoff = kOOB;
-      flush_iteration(L, act, outs, lane, R, a.debug);
+      flush_iteration(L, act, outs, lane, R, dbg_bits(a));
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
     }
-    const uint32_t round_cycles = (a.debug & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
+    const uint32_t round_cycles = (dbg_bits(a) & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
 
     // ---------------- finalise the round's blocks (SIMD across lanes)
     // iters counts the wave's iterations: a lane that finished early is not exhausted
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     // ---- wave-cooperative check of the walked row starts against offsets[] (block.go:107-118):
     // per block, coalesced loads of its offsets and row descriptors; eight blocks per wait
     {
-      uint64_t todo = (a.debug & 65536) ? 0 : __ballot(rows_stage == 1);  // 65536: profiling only
+      uint64_t todo = (dbg_bits(a) & 65536) ? 0 : __ballot(rows_stage == 1);  // 65536: profiling only
       uint64_t mism = 0;
       while (todo) {
         uint32_t js[kVerifyBatch], nrs[kVerifyBatch], osis[kVerifyBatch], outs[kVerifyBatch], rws[kVerifyBatch],
@@ -978,9 +978,9 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         reinterpret_cast<v4u*>(grows)[i] = r;
       }
     }
-    if (a.debug & 131072) m.detail = int32_t(fin_iter);  // profiling only: results are wrong by design
+    if (dbg_bits(a) & 131072) m.detail = int32_t(fin_iter);  // profiling only: results are wrong by design
     if (have) a.meta[b] = m;
-    if ((a.debug & 512) && lane == 0 && round0 + 1 < a.n) {
+    if ((dbg_bits(a) & 512) && lane == 0 && round0 + 1 < a.n) {
       // profiling only: loop iterations and cycles of this round, in meta.detail of its first two blocks
       a.meta[round0].detail = int32_t(iters);
       a.meta[round0 + 1].detail = int32_t(round_cycles);

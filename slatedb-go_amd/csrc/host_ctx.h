@@ -48,11 +48,60 @@ struct DevBuf {
   }
 };
 
+// Page-locked host staging (hipHostMalloc): DMA-able, so copies overlap kernels.
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = n < 65536 ? 65536 : n + n / 4;
+    hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    cap = c;
+    return hipSuccess;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// One lane of the host-buffer decode pipeline: its own stream, device buffers and pinned
+// staging, so chunk c+1's upload and plan overlap chunk c's decode and download.
+struct PipeLane {
+  hipStream_t stream = nullptr;
+  hipEvent_t planned = nullptr, done = nullptr;
+  DevBuf d_in, d_in_off, d_out_off, d_row_base, d_scratch, d_out, d_meta, d_rows;
+  PinBuf h_in, h_in_off, h_plan, h_out, h_meta, h_rows;
+  // the chunk in flight: blocks [b0, b0+n), its place in the caller's outputs
+  uint32_t b0 = 0, n = 0;
+  uint64_t out_base = 0, row_base = 0, out_total = 0, rows_total = 0;
+  bool busy = false, decoded = false;
+  void release() {
+    for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows}) b->release();
+    for (PinBuf* b : {&h_in, &h_in_off, &h_plan, &h_out, &h_meta, &h_rows}) b->release();
+    if (planned) (void)hipEventDestroy(planned);
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+    planned = done = nullptr;
+    stream = nullptr;
+  }
+};
+constexpr int kPipeLanes = 2;
+
 struct slate_ctx {
   int device = 0;
   int num_cus = 256;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+  PipeLane lanes[kPipeLanes];
+  PinBuf h_small;  // single-block staging (slate_block_decode)
   // decode batch buffers
   DevBuf d_in, d_in_off, d_out, d_out_off, d_meta, d_rows, d_row_base, d_scratch;
   // encode / misc buffers
@@ -63,6 +112,8 @@ struct slate_ctx {
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
                       &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &s_slots, &s_raw, &s_aux})
       b->release();
+    for (PipeLane& l : lanes) l.release();
+    h_small.release();
   }
 };
 

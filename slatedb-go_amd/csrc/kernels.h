@@ -14,10 +14,6 @@ constexpr uint32_t kZsFastInCap = 4224;      // CodecZstd fast-kernel staging: 2
 constexpr uint32_t kZsFastOutCap = 4112;
 constexpr uint32_t kLargeInCap = 65552;      // large-block kernel, one wave per workgroup
 constexpr uint32_t kLargeOutCap = 90112;
-// lane-per-block Snappy decode (decode_lpb.hip): one wave per workgroup, 432 B of
-// LDS per lane + 4 KiB CRC tables -> 5 workgroups (waves) per CU
-constexpr int kLpbThreads = 64;
-constexpr uint32_t kLpbWgPerCu = 5;
 // lane-per-block Snappy decode v2 (decode_lpb2.hip): 136 B output ring + 136 B input ring
 // per lane + 4 KiB CRC tables -> one 8-wave workgroup per CU.  (12 waves with a 4-slot
 // input ring fit LDS and 168 VGPRs but ran slower: the smaller ring costs 15 % more
@@ -40,9 +36,21 @@ struct DecodeArgs {
   const uint64_t* row_base;
   uint32_t* large_list;   // filled by the launcher from scratch
   uint32_t* large_count;
-  uint32_t debug;         // ablation switches for profiling only (SLATE_DEBUG_MODE); 0 in production
+  uint32_t debug;         // ablation switches (SLATE_DEBUG_MODE), read only by SLATE_PROFILING_BUILD variants
   uint32_t raw = 0;       // LPB only: payload is not a block (index/filter buffer): CRC + decompress, no block checks
+  uint32_t rt_zero = 0;   // always 0: a value the compiler cannot fold (see decode_lpb2.hip rd128)
 };
+
+// Ablation bits.  The shipped library is built without SLATE_PROFILING_BUILD, so every
+// ablation branch folds away at compile time; tools/variant.sh builds profiling variants.
+__host__ __device__ inline uint32_t dbg_bits(const DecodeArgs& a) {
+#ifdef SLATE_PROFILING_BUILD
+  return a.debug;
+#else
+  (void)a;
+  return 0u;
+#endif
+}
 
 struct DecodeScratch {
   uint64_t* pa;
@@ -56,7 +64,6 @@ size_t decode_scratch_bytes(uint32_t n);
 hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
-hipError_t launch_decode_lpb(hipStream_t st, const DecodeArgs& a, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
 // ---------------------------------------------------------------- merge (merge.hip)
 // iter.MergeSort over k concatenated sorted iterators (h_src_start: k+1 host element indices).

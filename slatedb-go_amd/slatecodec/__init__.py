@@ -73,6 +73,10 @@ _SIGS = {
     "slate_block_decode_batch": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, C.c_uint64, vp, vp, vp,
                                            C.c_uint64, vp]),
     "slate_block_decode": (C.c_int, [vp, C.c_int, vp, C.c_size_t, vp, C.c_size_t, szp, vp, vp, C.c_size_t]),
+    "slate_shard_blocks": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "slate_shard_pack": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint64, vp]),
+    "slate_block_decode_sharded": (C.c_int, [vp, C.c_uint32, C.c_int, vp, vp, C.c_uint32, vp, C.c_uint64, vp, vp,
+                                             vp, C.c_uint64, vp]),
     "slate_block_encode": (C.c_int, [vp, C.c_int, vp, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, szp]),
     "slate_sst_builder_new": (vp, [vp, C.POINTER(SstConfig), C.POINTER(C.c_int)]),
     "slate_sst_builder_free": (None, [vp]),
@@ -198,6 +202,14 @@ class Context:
                                         _ptr(out_off), _ptr(meta), _ptr(rows), rows.size, _ptr(row_base))
         _check(st, "slate_block_decode_batch")
         return out, out_off, meta[:n], rows, row_base
+
+    def decode_batch_into(self, codec: int, blob: np.ndarray, in_off: np.ndarray, out: np.ndarray,
+                          rows: np.ndarray, meta: np.ndarray, out_off: np.ndarray, row_base: np.ndarray) -> int:
+        """slate_block_decode_batch into caller-sized buffers (one pass; a caller that knows
+        capacity bounds, as an object-store reader does).  Returns the status."""
+        n = len(in_off) - 1
+        return lib().slate_block_decode_batch(self._h, codec, _ptr(blob), _ptr(in_off), n, _ptr(out), out.size,
+                                              _ptr(out_off), _ptr(meta), _ptr(rows), rows.size, _ptr(row_base))
 
     def block_decode(self, encoded: bytes, codec: int):
         """block.Decode(&b, input, codec) -> (status, meta, Data, Offsets)."""
@@ -328,6 +340,49 @@ class Context:
                                      re_.value - rs.value, _ptr(out), out_cap, _ptr(out_off), _ptr(meta), _ptr(rows),
                                      rows.size, _ptr(row_base), C.byref(failed))
         return st, failed.value, (out, out_off, meta, rows, row_base)
+
+
+def shard_blocks(n_blocks: int, n_shards: int, shard: int) -> int:
+    """Blocks of shard `shard` when block i goes to shard i mod n_shards."""
+    return int(lib().slate_shard_blocks(n_blocks, n_shards, shard))
+
+
+def shard_pack(blob: np.ndarray, in_off: np.ndarray, n_shards: int, shard: int):
+    """slate_shard_pack: shard `shard`'s blocks back to back -> (bytes, offsets)."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    in_off = np.ascontiguousarray(in_off, np.uint64)
+    n = len(in_off) - 1
+    m = shard_blocks(n, n_shards, shard)
+    idx = np.arange(shard, n, n_shards, dtype=np.int64)
+    nbytes = int((in_off[idx + 1] - in_off[idx]).sum()) if m else 0
+    out = np.zeros(max(nbytes, 1), np.uint8)
+    off = np.zeros(m + 1, np.uint64)
+    _check(lib().slate_shard_pack(_ptr(blob), _ptr(in_off), n, n_shards, shard, _ptr(out), nbytes, _ptr(off)),
+           "slate_shard_pack")
+    return out[:nbytes], off
+
+
+def decode_sharded(ctxs: list["Context"], codec: int, blob: np.ndarray, in_off: np.ndarray):
+    """slate_block_decode_sharded: block i decoded by ctxs[i % len(ctxs)], results in block order
+    -> (out, out_off, meta, rows, row_base) as Context.decode_batch."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    in_off = np.ascontiguousarray(in_off, np.uint64)
+    n = len(in_off) - 1
+    hs = (C.c_void_p * len(ctxs))(*[c.handle for c in ctxs])
+    out_off = np.zeros(n + 1, np.uint64)
+    row_base = np.zeros(n + 1, np.uint64)
+    meta = np.zeros(max(n, 1), META_DTYPE)
+    L = lib()
+    st = L.slate_block_decode_sharded(hs, len(ctxs), codec, _ptr(blob), _ptr(in_off), n, None, 0, _ptr(out_off),
+                                      _ptr(meta), None, 0, _ptr(row_base))
+    if st not in (OK, E_CAPACITY):
+        raise SlateError(st, "slate_block_decode_sharded")
+    out = np.zeros(max(int(out_off[n]), 1), np.uint8)
+    rows = np.zeros(max(int(row_base[n]), 1), ROW_DTYPE)
+    st = L.slate_block_decode_sharded(hs, len(ctxs), codec, _ptr(blob), _ptr(in_off), n, _ptr(out), out.size,
+                                      _ptr(out_off), _ptr(meta), _ptr(rows), rows.size, _ptr(row_base))
+    _check(st, "slate_block_decode_sharded")
+    return out, out_off, meta[:n], rows, row_base
 
 
 class Index:

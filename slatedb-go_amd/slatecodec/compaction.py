@@ -35,7 +35,8 @@ def _blocks_of(ctx: Context, sst: bytes):
 def _index_pool(ctx: Context, n: int) -> list[Context]:
     """Extra contexts (one HIP stream each) so the input SSTs' indexes decode concurrently: each
     index is one serial Snappy stream that occupies a single wavefront (snappy_stream.hip).  The
-    library is reentrant per context (one slate_ctx per goroutine in a Go port)."""
+    library is reentrant per context (one slate_ctx per goroutine in a Go port), and a context is
+    never used by two threads at once: each worker owns one context for its whole slice."""
     pool = getattr(ctx, "_index_pool", None)
     if pool is None:
         pool = ctx._index_pool = []
@@ -50,8 +51,14 @@ def _all_blocks(ctx: Context, ssts: list[bytes]):
     from concurrent.futures import ThreadPoolExecutor
     w = min(8, len(ssts))
     pool = _index_pool(ctx, w)
-    with ThreadPoolExecutor(w) as ex:  # ctypes calls release the GIL
-        return list(ex.map(lambda i: _blocks_of(pool[i % w], ssts[i]), range(len(ssts))))
+    # w contiguous slices, one per worker and context (ctypes calls release the GIL)
+    bounds = [len(ssts) * j // w for j in range(w + 1)]
+
+    def run(j):
+        return [_blocks_of(pool[j], ssts[i]) for i in range(bounds[j], bounds[j + 1])]
+
+    with ThreadPoolExecutor(w) as ex:
+        return [r for part in ex.map(run, range(w)) for r in part]
 
 
 def _mark(prof, label):
@@ -63,34 +70,75 @@ def _mark(prof, label):
 
 def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list | None = None):
     """Decode every data block of every input SST on the GPU and return the rows as a device KV view:
-    (keys, key_off, vals, val_off, tomb, n_kv, src_start) with src_start = per-source row ranges."""
+    (keys, key_off, vals, val_off, tomb, n_kv, src_start) with src_start = per-source row ranges.
+    Each SST carries its own codec (sstable.Info.CompressionCodec): consecutive SSTs that share one
+    are decoded as one batch, and the batches' views are concatenated in source order."""
     import torch
     _mark(prof, "start")
-    codec = None
-    pieces, offs_parts, src_blocks = [], [np.zeros(1, np.uint64)], [0]
+    flat = [sst for run in sources for sst in run]
+    located = _all_blocks(ctx, flat)
+    _mark(prof, "index")
+    groups, i = [], 0
+    while i < len(flat):
+        j = i
+        while j < len(flat) and located[j][0] == located[i][0]:
+            j += 1
+        groups.append((located[i][0], list(range(i, j))))
+        i = j
+    views = [_decode_group(ctx, codec, [(flat[k], located[k][1]) for k in idx], device, prof)
+             for codec, idx in groups]
+    rows_per_sst = [r for v in views for r in v[6]]
+    src_sst = np.cumsum([0] + [len(run) for run in sources])
+    row_cum = np.concatenate([[0], np.cumsum(np.asarray(rows_per_sst, np.uint64))]).astype(np.uint64)
+    src_start = row_cum[src_sst].astype(np.uint64) if len(flat) else np.zeros(len(sources) + 1, np.uint64)
+    if len(views) == 1:
+        v = views[0]
+        out = v[:6] + (src_start,)
+    elif not views:
+        z = torch.zeros(1, dtype=torch.int64, device=device)
+        u8 = torch.zeros(1, dtype=torch.uint8, device=device)
+        out = (u8, z, u8, z, u8, 0, src_start)
+    else:
+        keys, vals, koffs, voffs, tombs, kb, vb, n_kv = [], [], [], [], [], 0, 0, 0
+        for v in views:
+            d_keys, d_key_off, d_vals, d_val_off, d_tomb, m = v[:6]
+            k_end, v_end = int(d_key_off[m].item()), int(d_val_off[m].item())
+            keys.append(d_keys[:k_end])
+            vals.append(d_vals[:v_end])
+            koffs.append(d_key_off[:m] + kb)
+            voffs.append(d_val_off[:m] + vb)
+            tombs.append(d_tomb[:m])
+            kb, vb, n_kv = kb + k_end, vb + v_end, n_kv + m
+        one = torch.ones(1, dtype=torch.int64, device=device)
+        out = (torch.cat(keys + [torch.zeros(1, dtype=torch.uint8, device=device)]),
+               torch.cat(koffs + [one * kb]), torch.cat(vals + [torch.zeros(1, dtype=torch.uint8, device=device)]),
+               torch.cat(voffs + [one * vb]), torch.cat(tombs + [torch.zeros(1, dtype=torch.uint8, device=device)]),
+               n_kv, src_start)
+    assert int(src_start[-1]) == out[5]
+    _mark(prof, "rows_kv")
+    return out
+
+
+def _decode_group(ctx: Context, codec: int, ssts: list, device, prof):
+    """One device batch over the data blocks of SSTs that share a codec -> (keys, key_off, vals,
+    val_off, tomb, n_kv, rows per SST)."""
+    import torch
+    pieces, offs_parts, sst_blocks = [], [np.zeros(1, np.uint64)], [0]
     base, nblk = 0, 0  # encoded bytes and blocks gathered so far
-    located = iter(_all_blocks(ctx, [sst for run in sources for sst in run]))
-    for run in sources:
-        for sst in run:
-            c, offs = next(located)
-            if codec is None:
-                codec = c
-            if c != codec:
-                raise SlateError(102, "compaction inputs with different codecs")
-            if len(offs) > 1:  # the data blocks are contiguous: [offs[0], FilterOffset)
-                lo, hi = int(offs[0]), int(offs[-1])
-                pieces.append(np.frombuffer(sst, np.uint8, hi - lo, lo))
-                offs_parts.append(offs[1:] - np.uint64(lo) + np.uint64(base))
-                base += hi - lo
-                nblk += len(offs) - 1
-        src_blocks.append(nblk)
+    for sst, offs in ssts:
+        if len(offs) > 1:  # the data blocks are contiguous: [offs[0], FilterOffset)
+            lo, hi = int(offs[0]), int(offs[-1])
+            pieces.append(np.frombuffer(sst, np.uint8, hi - lo, lo))
+            offs_parts.append(offs[1:] - np.uint64(lo) + np.uint64(base))
+            base += hi - lo
+            nblk += len(offs) - 1
+        sst_blocks.append(nblk)
     in_off = np.concatenate(offs_parts)
     n = len(in_off) - 1
     if n == 0:
         z = torch.zeros(1, dtype=torch.int64, device=device)
-        return (torch.zeros(1, dtype=torch.uint8, device=device), z, torch.zeros(1, dtype=torch.uint8, device=device),
-                z, torch.zeros(1, dtype=torch.uint8, device=device), 0, np.zeros(len(sources) + 1, np.uint64))
-    _mark(prof, "index")
+        u8 = torch.zeros(1, dtype=torch.uint8, device=device)
+        return u8, z, u8, z, u8, 0, [0] * len(ssts)
     blob = np.concatenate(pieces)
     _mark(prof, "gather_blocks")
     d_in = torch.from_numpy(blob).to(device)
@@ -123,10 +171,17 @@ def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list 
                                               d_tomb.data_ptr(), d_nkv.data_ptr(), d_flags.data_ptr(),
                                               d_kvs.data_ptr()), "slate_rows_kv_lengths_device")
     ctx.synchronize()
+    # Every block's status is checked, whatever the row-slot flags say: a block that fails before
+    # its decoded length is known owns no row slot (sstable.Iterator stops on the error and
+    # executeCompaction returns it, iterator.go:62-68, executor.go:107-150).
     meta = np.frombuffer(d_meta.cpu().numpy().tobytes(), dtype=META_DTYPE)
+    bad = np.nonzero(meta["status"] != 0)[0]
+    if len(bad):
+        raise SlateError(int(meta["status"][bad[0]]), f"compaction input block {int(bad[0])} decode")
+    if (meta["flags"] & 1).any():  # SLATE_BLKF_ROWS_TRUNCATED: more offsets than row slots
+        raise SlateError(103, "compaction input block has more rows than row slots")
     if int(d_flags.item()) & 2:
-        bad = np.nonzero(meta["status"] != 0)[0]
-        raise SlateError(int(meta["status"][bad[0]]) if len(bad) else 102, "compaction input block decode")
+        raise SlateError(102, "compaction input row decode")
     n_kv = int(d_nkv.item())
     kb, vb = int(d_key_off[slots].item()), int(d_val_off[slots].item())
     d_keys = torch.empty(max(kb, 1), dtype=torch.uint8, device=device)
@@ -135,13 +190,12 @@ def decode_rows_kv(ctx: Context, sources: list[list[bytes]], device, prof: list 
                                            d_row_base.data_ptr(), d_rows.data_ptr(), slots, d_nkv.data_ptr(),
                                            d_kvs.data_ptr(), d_key_off.data_ptr(), d_keys.data_ptr(),
                                            d_val_off.data_ptr(), d_vals.data_ptr()), "slate_rows_kv_copy_device")
-    # per-source row ranges from the blocks' row counts
+    # rows per SST from the blocks' row counts
     rows_per_block = np.concatenate([[0], np.cumsum(meta["n_rows"].astype(np.uint64))])
-    src_start = rows_per_block[np.array(src_blocks)].astype(np.uint64)
-    assert int(src_start[-1]) == n_kv
+    per_sst = np.diff(rows_per_block[np.array(sst_blocks)].astype(np.int64)).tolist()
+    assert sum(per_sst) == n_kv
     ctx.synchronize()
-    _mark(prof, "rows_kv")
-    return d_keys, d_key_off, d_vals, d_val_off, d_tomb, n_kv, src_start
+    return d_keys, d_key_off, d_vals, d_val_off, d_tomb, n_kv, per_sst
 
 
 def merge_kv(ctx: Context, view, device, prof: list | None = None):

@@ -49,3 +49,61 @@ def test_compaction_skewed_prefixes(ctx):
     srcs = cg.random_sources(rng, 3, 600, 1500, key_fmt=key)
     got = compaction.compact(ctx, srcs, 20_000)
     assert got == cg.oracle_compact(srcs, 20_000)
+
+
+def test_compaction_many_snappy_ssts(ctx):
+    """More input SSTs than index-decode workers (8), all with Snappy indexes: each worker owns
+    its context for a contiguous slice of the SST list."""
+    from slatecodec import compaction
+    rng = random.Random(21)
+    srcs = cg.random_sources(rng, 4, 1200, 2500, codec=ob.SNAPPY, run_ssts=5)
+    assert sum(len(r) for r in srcs) > 8
+    got = compaction.compact(ctx, srcs, 30_000, codec=ob.SNAPPY)
+    assert got == cg.oracle_compact(srcs, 30_000, codec=ob.SNAPPY)
+
+
+def test_compaction_mixed_codecs(ctx):
+    """Each SST carries its own codec (sstable.Info.CompressionCodec): a DB whose compression
+    option changed has L0 SSTs and sorted runs in different codecs."""
+    from slatecodec import compaction
+    rng = random.Random(22)
+    srcs = []
+    for j, codec in enumerate((ob.NONE, ob.SNAPPY, ob.NONE, ob.SNAPPY)):
+        srcs += cg.random_sources(rng, 1, 700, 1600, codec=codec, run_ssts=1 + j % 3)
+    got = compaction.compact(ctx, srcs, 1 << 30, codec=ob.SNAPPY)
+    assert got == cg.oracle_compact(srcs, 1 << 30, codec=ob.SNAPPY)
+
+
+def _corrupt_first_block(sst: bytes, body: bytes) -> bytes:
+    """Replace the SST's first data block by `body` (padded to the block's length) + a valid CRC."""
+    import struct
+    import zlib
+    st, info = ob.sst_read_info(sst)
+    st, metas = ob.decode_index(sst[info["index_offset"]:info["index_offset"] + info["index_len"]], info["codec"])
+    a = metas[0][0]
+    b = metas[1][0] if len(metas) > 1 else info["filter_offset"]
+    body = (body + b"\0" * (b - a))[: b - a - 4]
+    return sst[:a] + body + struct.pack(">I", zlib.crc32(body)) + sst[b:]
+
+
+@pytest.mark.parametrize("body,status", [
+    (b"\x00", 11),       # Snappy header says 0 bytes, more input follows: snappy: corrupt input
+    (b"\x01\x00a", 11),  # decoded length 1 (no row slot) with trailing input
+    (None, 2),           # CRC mismatch
+])
+def test_compaction_bad_block_fails(ctx, body, status):
+    """A block that fails block.Decode stops the compaction (sstable.Iterator returns the error,
+    executeCompaction returns it: iterator.go:62-68, executor.go:107-150), also when the block
+    fails before it owns a row slot."""
+    from slatecodec import compaction, SlateError
+    rng = random.Random(23)
+    srcs = cg.random_sources(rng, 2, 600, 1200, codec=ob.SNAPPY)
+    if body is None:
+        s = bytearray(srcs[1][0])
+        s[20] ^= 0x40
+        srcs[1][0] = bytes(s)
+    else:
+        srcs[1][0] = _corrupt_first_block(srcs[1][0], body)
+    with pytest.raises(SlateError) as e:
+        compaction.compact(ctx, srcs, 1 << 30)
+    assert e.value.status == status

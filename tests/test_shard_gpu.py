@@ -1,0 +1,110 @@
+"""GPU parity of the host-buffer paths and the round-robin sharding (BASELINE configs[3],
+SURVEY 8e): slate_block_decode_batch through page-locked staging over many chunks, and
+slate_block_decode_sharded with G = 2..4 contexts on device 0 over one batch, against the
+oracle block by block, in the original order (plan layout, meta, decoded bytes, rows)."""
+import os
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import binding as ob
+from tests import blockgen as bg
+from tools import workload as wl
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_against_oracle(codec, blocks_blob, off, got):
+    g_out, g_off, g_meta, g_rows, g_rb = got
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(codec, blocks_blob, off)
+    assert np.array_equal(g_off, o_off) and np.array_equal(g_rb, o_rb)
+    assert g_meta.tobytes() == o_meta.tobytes()
+    n = len(off) - 1
+    for i in range(n):
+        st = int(o_meta["status"][i])
+        if st == 0:
+            a = int(o_off[i])
+            dl = int(o_meta["data_len"][i]) + 2 * int(o_meta["n_rows"][i]) + 2
+            assert g_out[a:a + dl].tobytes() == o_out[a:a + dl].tobytes(), i
+            r0 = int(o_rb[i])
+            nr = int(o_meta["n_rows"][i])
+            assert g_rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+
+
+def _mixed_batch(seed, n_good):
+    """Set blocks plus random, ragged and corrupt blocks, shuffled (statuses differ per shard)."""
+    rng = random.Random(seed)
+    blob, off = wl.block_set(ob.SNAPPY, seed, 3, n_good, threads=4)
+    blocks = [bytes(blob[int(off[i]):int(off[i + 1])]) for i in range(n_good)]
+    kvs = bg.random_kvs(rng, 300, klen=(1, 40), vlen=(0, 300))
+    blocks += bg.sst_blocks(kvs, 512, ob.SNAPPY)
+    blocks += [bg.mutate(rng, blocks[rng.randrange(n_good)], fix_crc=rng.random() < 0.5) for _ in range(40)]
+    blocks += [b"", b"\x01\x02\x03", bg.recrc(b"\x00")]
+    rng.shuffle(blocks)
+    return blocks
+
+
+@pytest.mark.parametrize("g", [2, 3, 4])
+def test_sharded_decode_matches_oracle(g):
+    import slatecodec as sc
+    ctxs = [sc.Context(0) for _ in range(g)]
+    blocks = _mixed_batch(g, 3000)
+    blob, off = bg.pack(blocks, misalign=5)
+    got = sc.decode_sharded(ctxs, sc.SNAPPY, blob, off)
+    _check_against_oracle(sc.SNAPPY, blob, off, got)
+    for c in ctxs:
+        c.close()
+
+
+def test_sharded_more_contexts_than_blocks():
+    import slatecodec as sc
+    ctxs = [sc.Context(0) for _ in range(4)]
+    blocks = _mixed_batch(7, 2)[:3]
+    blob, off = bg.pack(blocks)
+    got = sc.decode_sharded(ctxs, sc.SNAPPY, blob, off)
+    _check_against_oracle(sc.SNAPPY, blob, off, got)
+
+
+def test_host_pipeline_many_chunks():
+    """slate_block_decode_batch with 512-block chunks (two lanes alternate) in a child process
+    (the chunk size is read once per process), against the oracle."""
+    code = r"""
+import sys, numpy as np
+sys.path[:0] = [%r, %r]
+import torch; torch.cuda.init()
+import slatecodec as sc
+from tests.test_shard_gpu import _mixed_batch, _check_against_oracle
+from tests import blockgen as bg
+blocks = _mixed_batch(11, 5000)
+blob, off = bg.pack(blocks, misalign=3)
+ctx = sc.Context(0)
+got = ctx.decode_batch(sc.SNAPPY, blob, off)
+_check_against_oracle(sc.SNAPPY, blob, off, got)
+# one pass into caller-sized buffers, twice (reused staging)
+n = len(off) - 1
+out = np.zeros(int(got[1][n]) + 16, np.uint8); rows = np.zeros(int(got[4][n]) + 1, sc.ROW_DTYPE)
+meta = np.zeros(n, sc.META_DTYPE); oo = np.zeros(n + 1, np.uint64); rb = np.zeros(n + 1, np.uint64)
+for _ in range(2):
+    assert ctx.decode_batch_into(sc.SNAPPY, blob, off, out, rows, meta, oo, rb) == sc.OK
+    _check_against_oracle(sc.SNAPPY, blob, off, (out, oo, meta, rows, rb))
+print("ok")
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+       os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "slatedb-go_amd"))
+    env = dict(os.environ, SLATE_PIPE_CHUNK_BLOCKS="512")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_single_block_decode_matches_oracle():
+    import slatecodec as sc
+    ctx = sc.Context(0)
+    for blk in _mixed_batch(13, 50)[:80]:
+        st, m, data, offs = ctx.block_decode(blk, sc.SNAPPY)
+        om, odata, orows = ob.block_decode(blk, sc.SNAPPY)
+        assert int(m["status"]) == int(om["status"])
+        if st == 0:
+            assert data == odata[:int(om["data_len"])]
+            assert offs == [int(r["row_off"]) for r in orows][:len(offs)]

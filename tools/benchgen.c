@@ -268,3 +268,154 @@ uint64_t bg_build_mixed(uint64_t seed, uint64_t n_kv, uint64_t block_size, uint8
   }
   return nb;
 }
+
+/* ---- block sets for the round-robin multi-GPU bench (BASELINE configs[1] / configs[3]) ----
+ * Block i of a set is generated on its own: keys "k%015d" % (40 i + j), values r || r with r
+ * 42 bytes from a splitmix64 stream seeded by (seed, i) (V-half; or 84 random bytes), greedy
+ * fill of block.Builder.Add (block.go:162-182).  So a rank can build exactly its shard
+ * (blocks i = i_begin + k * stride) and check its decoded output block by block. */
+static uint32_t set_block(uint64_t seed, int half, uint64_t block_size, uint64_t i, uint8_t* blk, uint16_t* offs,
+                          uint32_t* nrows, uint32_t* pls) {
+  char first[17], key[17];
+  uint64_t st = seed * 0x9E3779B97F4A7C15ull ^ (i + 1) * 0xD1B54A32D192ED03ull;
+  const uint32_t rv_len = half ? 42 : 84, vlen = 84;
+  uint32_t n = 0, dlen = 0;
+  for (uint64_t j = 0;; j++) {
+    { /* "k%015llu" */
+      uint64_t x = 40 * i + j;
+      key[0] = 'k';
+      for (int d = 15; d >= 1; d--) { key[d] = (char)('0' + x % 10); x /= 10; }
+      key[16] = 0;
+    }
+    uint32_t p = 0;
+    if (n) while (p < 16 && first[p] == key[p]) p++;
+    uint32_t row = 4 + (16 - p) + 9 + 4 + vlen;
+    if ((uint64_t)2 + 2 * n + dlen + 2 + row > block_size && n) break;
+    uint8_t* r = blk + dlen;
+    put16(r, p); put16(r + 2, 16 - p);
+    memcpy(r + 4, key + p, 16 - p);
+    memset(r + 4 + 16 - p, 0, 9);
+    uint8_t* v = r + 4 + 16 - p + 9;
+    v[0] = 0; v[1] = 0; v[2] = 0; v[3] = (uint8_t)vlen;
+    uint8_t rv[88];
+    for (uint32_t b = 0; b < rv_len; b += 8) { uint64_t x = sm64(&st); memcpy(rv + b, &x, 8); }
+    memcpy(v + 4, rv, rv_len);
+    if (half) memcpy(v + 4 + rv_len, rv, rv_len);
+    if (pls) pls[n] = p;
+    offs[n++] = (uint16_t)dlen;
+    dlen += row;
+    if (n == 1) memcpy(first, key, 17);
+  }
+  for (uint32_t k = 0; k < n; k++) put16(blk + dlen + 2 * k, offs[k]);
+  put16(blk + dlen + 2 * n, n);
+  *nrows = n;
+  return dlen + 2 * n + 2;
+}
+
+typedef struct {
+  uint64_t seed; int half; uint64_t block_size, i_begin, stride, lo, hi; int codec;
+  uint8_t* enc; uint64_t enc_stride; uint64_t* enc_len;
+  const uint8_t* out; const uint64_t* out_off; const uint8_t* rows; const uint64_t* row_base; const uint8_t* meta;
+  int64_t bad; int rc;
+} set_job_t;
+
+static void* set_build_work(void* arg) {
+  set_job_t* j = (set_job_t*)arg;
+  uint8_t blk[8192];
+  uint16_t offs[4096];
+  void* zc = NULL;
+  if (j->codec == 4) {
+    zc = g_zcreate();
+    g_zsetp(zc, 100, 3);
+    g_zsetp(zc, 201, 1);
+    g_zsetp(zc, 200, 1);
+  }
+  for (uint64_t k = j->lo; k < j->hi; k++) {
+    uint32_t nr;
+    const uint32_t n = set_block(j->seed, j->half, j->block_size, j->i_begin + k * j->stride, blk, offs, &nr, NULL);
+    uint8_t* d = j->enc + k * j->enc_stride;
+    size_t cl = j->enc_stride - 4;
+    if (j->codec == 0) { memcpy(d, blk, n); cl = n; }
+    else if (j->codec == 4) {
+      size_t r = g_zc2(zc, d, j->enc_stride - 4, blk, n);
+      if (g_zerr(r)) { j->rc = -5; break; }
+      cl = r;
+    } else if (g_compress((const char*)blk, n, (char*)d, &cl) != 0) { j->rc = -3; break; }
+    uint32_t c = crc32(d, cl);
+    d[cl] = (uint8_t)(c >> 24); d[cl + 1] = (uint8_t)(c >> 16); d[cl + 2] = (uint8_t)(c >> 8); d[cl + 3] = (uint8_t)c;
+    j->enc_len[k] = cl + 4;
+  }
+  if (zc) g_zfree(zc);
+  return NULL;
+}
+
+/* Encoded blocks k = 0..count-1 of the set (global index i_begin + k * stride) into fixed slots
+ * of enc_stride bytes (codec 0 None, 1 Snappy via libsnappy, 4 Zstd), lengths in enc_len. */
+int bg_build_set(uint64_t seed, int half, uint64_t block_size, uint64_t i_begin, uint64_t stride, uint64_t count,
+                 int codec, uint8_t* enc, uint64_t enc_stride, uint64_t* enc_len, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  if (block_size > 8000) return -6;
+  pthread_t th[64];
+  set_job_t jobs[64];
+  for (int t = 0; t < nthreads; t++) {
+    set_job_t jb = {seed, half, block_size, i_begin, stride, count * t / nthreads, count * (t + 1) / nthreads, codec,
+                    enc, enc_stride, enc_len, NULL, NULL, NULL, NULL, NULL, 0, 0};
+    jobs[t] = jb;
+    pthread_create(&th[t], NULL, set_build_work, &jobs[t]);
+  }
+  int rc = 0;
+  for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
+  return rc;
+}
+
+static void* set_verify_work(void* arg) {
+  set_job_t* j = (set_job_t*)arg;
+  uint8_t blk[8192];
+  uint16_t offs[4096];
+  uint32_t pls[4096];
+  for (uint64_t k = j->lo; k < j->hi; k++) {
+    uint32_t nr;
+    const uint32_t n = set_block(j->seed, j->half, j->block_size, j->i_begin + k * j->stride, blk, offs, &nr, pls);
+    const uint32_t data_len = n - 2 * nr - 2;
+    int ok = j->out_off[k + 1] - j->out_off[k] >= n && memcmp(j->out + j->out_off[k], blk, n) == 0;
+    /* slate_block_meta {i16 status, u16 flags, i32 detail, u32 data_len, u16 n_rows, u16 aux} */
+    const uint8_t* m = j->meta + 16 * k;
+    uint32_t dl; uint16_t nrow, st, fl, aux; int32_t det;
+    memcpy(&st, m, 2); memcpy(&fl, m + 2, 2); memcpy(&det, m + 4, 4); memcpy(&dl, m + 8, 4);
+    memcpy(&nrow, m + 12, 2); memcpy(&aux, m + 14, 2);
+    ok = ok && st == 0 && fl == 0 && dl == data_len && nrow == nr && aux == 0;
+    /* slate_row {u32 row_off, u16 prefix, u16 suffix, u32 value_len, u8 flags, u8 meta_len, i16 status} */
+    ok = ok && j->row_base[k + 1] - j->row_base[k] >= nr;
+    for (uint32_t r = 0; ok && r < nr; r++) {
+      const uint8_t* d = j->rows + 16 * (j->row_base[k] + r);
+      uint32_t ro, vl; uint16_t pl, sl, rst;
+      memcpy(&ro, d, 4); memcpy(&pl, d + 4, 2); memcpy(&sl, d + 6, 2); memcpy(&vl, d + 8, 4); memcpy(&rst, d + 14, 2);
+      ok = ro == offs[r] && pl == pls[r] && sl == 16 - pls[r] && vl == 84 && d[12] == 0 && d[13] == 13 && rst == 0;
+    }
+    if (!ok) j->bad++;
+  }
+  return NULL;
+}
+
+/* Decoded outputs of blocks k = 0..count-1 (decode kernel layout: bytes at out + out_off[k],
+ * row descriptors at rows + 16 row_base[k], meta 16 B each) against the generator: returns
+ * the number of blocks whose bytes, meta or rows differ. */
+int64_t bg_verify_set(uint64_t seed, int half, uint64_t block_size, uint64_t i_begin, uint64_t stride, uint64_t count,
+                      const uint8_t* out, const uint64_t* out_off, const uint8_t* rows, const uint64_t* row_base,
+                      const uint8_t* meta, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  if (block_size > 8000) return -1;
+  pthread_t th[64];
+  set_job_t jobs[64];
+  for (int t = 0; t < nthreads; t++) {
+    set_job_t jb = {seed, half, block_size, i_begin, stride, count * t / nthreads, count * (t + 1) / nthreads, 0,
+                    NULL, 0, NULL, out, out_off, rows, row_base, meta, 0, 0};
+    jobs[t] = jb;
+    pthread_create(&th[t], NULL, set_verify_work, &jobs[t]);
+  }
+  int64_t bad = 0;
+  for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); bad += jobs[t].bad; }
+  return bad;
+}

@@ -32,7 +32,15 @@ def main():
     for line in open(log):
         if line.startswith("{"):
             bench = json.loads(line)
+    import hashlib
+    import subprocess
+    sha = hashlib.sha256(open(os.path.join(REPO, "slatedb-go_amd", "lib", "libslatecodec.so"), "rb").read()).hexdigest()
+    try:
+        commit = subprocess.run(["git", "-C", REPO, "rev-parse", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except OSError:
+        commit = ""
     res = {"kernel": kernel, "blocks": bench["config"]["blocks_per_gpu"], "codec": bench["config"]["codec"],
+           "lib_sha256": sha, "commit": commit or os.environ.get("SLATE_COMMIT", ""),
            "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
            "hbm_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024),
            "note": "2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md)"}

@@ -7,7 +7,7 @@ TAG=$1; FLAGS=$2
 cd "$(dirname "$0")/../slatedb-go_amd"
 make -s
 mkdir -p build/var_$TAG
-HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-parameter"
+HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-parameter -DSLATE_PROFILING_BUILD"
 objs=""
 for f in build/*.o; do
   b=$(basename $f)

@@ -39,6 +39,12 @@ def lib():
         L.bg_init_lz4(LIBLZ4.encode())  # codec 3 (LZ4 frames) only: optional
         L.bg_init_zstd.argtypes = [C.c_char_p]
         L.bg_init_zstd(LIBZSTD.encode())  # codec 4 (Zstd level 3 + checksum) only: optional
+        L.bg_build_set.restype = C.c_int
+        L.bg_build_set.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int,
+                                   C.c_void_p, C.c_uint64, C.c_void_p, C.c_int]
+        L.bg_verify_set.restype = C.c_int64
+        L.bg_verify_set.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.bg_build_mixed.restype = C.c_uint64
         L.bg_build_mixed.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64]
         _lib = L
@@ -89,3 +95,45 @@ def snappy_vhalf(n_blocks: int, codec: int = 1, seed: int = 20250307, half: bool
     dec, doff = decoded_blocks(n_blocks, seed=seed, half=half, kv_begin=kv_begin)
     blob, off = encode_blocks(codec, dec, doff, threads)
     return blob, off, int(doff[-1])
+
+
+def block_set(codec: int, i_begin: int, stride: int, count: int, seed: int = 20250307, half: bool = True,
+              block_size: int = 4096, threads: int = 16, chunk: int = 262144):
+    """Encoded blocks i_begin + k * stride (k < count) of the per-block synthetic set (tools/benchgen.c
+    bg_build_set): one rank's round-robin shard of a set that no rank holds whole -> (blob, in_off)."""
+    stride_e = block_size + block_size // 6 + 64
+    off = np.zeros(count + 1, np.uint64)
+    blob = None
+    pos = 0
+    for k0 in range(0, count, chunk):
+        m = min(chunk, count - k0)
+        slots = np.empty(m * stride_e, np.uint8)
+        elen = np.zeros(m, np.uint64)
+        rc = lib().bg_build_set(seed, int(half), block_size, i_begin + k0 * stride, stride, m, codec,
+                                slots.ctypes.data, stride_e, elen.ctypes.data, threads)
+        assert rc == 0, rc
+        part = np.empty(int(elen.sum()) + 16, np.uint8)
+        poff = np.zeros(m + 1, np.uint64)
+        lib().bg_compact(slots.ctypes.data, stride_e, elen.ctypes.data, m, part.ctypes.data, poff.ctypes.data)
+        del slots
+        nb = int(poff[m])
+        if blob is None:  # size the whole shard from the first chunk's average, grow if needed
+            blob = np.empty(int(nb / m * count * 1.02) + 4096, np.uint8)
+        if pos + nb + 16 > blob.size:
+            blob = np.resize(blob, int((pos + nb) * 1.1) + 4096)
+        blob[pos:pos + nb] = part[:nb]
+        off[k0:k0 + m + 1] = poff + np.uint64(pos)
+        pos += nb
+    if blob is None:
+        blob = np.zeros(16, np.uint8)
+    return blob[:pos + 16], off
+
+
+def verify_set(i_begin: int, stride: int, count: int, out: np.ndarray, out_off: np.ndarray, rows: np.ndarray,
+               row_base: np.ndarray, meta: np.ndarray, seed: int = 20250307, half: bool = True,
+               block_size: int = 4096, threads: int = 16) -> int:
+    """Blocks k < count decoded by the GPU (bytes at out[out_off[k]:], row descriptors from
+    rows[row_base[k]], 16-byte meta) against the generator: number of mismatching blocks."""
+    return int(lib().bg_verify_set(seed, int(half), block_size, i_begin, stride, count, out.ctypes.data,
+                                   out_off.ctypes.data, rows.ctypes.data, row_base.ctypes.data, meta.ctypes.data,
+                                   threads))
