@@ -51,7 +51,9 @@ hipError_t lane_init(PipeLane& L) {
   return hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
 }
 
-// Where decoded chunks go: the caller's arrays, or (sharded decode) vectors that grow per chunk.
+// Where decoded chunks go: the caller's arrays in chunk order, or (sharded decode, scatter
+// mode) block by block to the positions the whole batch's layout gives local block j of shard
+// g: global block i = g + j * G.
 struct Sink {
   uint8_t* out = nullptr;
   uint64_t out_cap = 0;
@@ -60,12 +62,10 @@ struct Sink {
   slate_row* rows = nullptr;
   uint64_t rows_cap = 0;
   uint64_t* row_base = nullptr;
-  // growable mode
-  std::vector<uint8_t>* v_out = nullptr;
-  std::vector<slate_row>* v_rows = nullptr;
-  std::vector<slate_block_meta>* v_meta = nullptr;
-  std::vector<uint64_t>* v_out_off = nullptr;
-  std::vector<uint64_t>* v_row_base = nullptr;
+  // scatter mode (G > 0): out_off/row_base above are the shard's own plan, these the batch's
+  uint32_t G = 0, g = 0;
+  const uint64_t* g_out_off = nullptr;
+  const uint64_t* g_row_base = nullptr;
 };
 
 // The lane's chunk is decoded: copy its outputs into the sink.
@@ -74,20 +74,23 @@ int lane_finish(PipeLane& L, Sink& o) {
   L.busy = false;
   SLATE_HIP(hipEventSynchronize(L.done));
   if (!L.decoded) return SLATE_OK;
-  uint8_t* out = o.out;
-  slate_row* rows = o.rows;
-  slate_block_meta* meta = o.meta;
-  if (o.v_out) {
-    if (o.v_out->size() < L.out_base + L.out_total) o.v_out->resize(L.out_base + L.out_total);
-    if (o.v_rows->size() < L.row_base + L.rows_total) o.v_rows->resize(L.row_base + L.rows_total);
-    if (o.v_meta->size() < size_t(L.b0) + L.n) o.v_meta->resize(size_t(L.b0) + L.n);
-    out = o.v_out->data();
-    rows = o.v_rows->data();
-    meta = o.v_meta->data();
+  const uint8_t* hout = L.h_out.as<uint8_t>();
+  const slate_row* hrows = L.h_rows.as<slate_row>();
+  const slate_block_meta* hmeta = L.h_meta.as<slate_block_meta>();
+  if (o.G) {
+    for (uint32_t k = 0; k < L.n; k++) {
+      const uint32_t j = L.b0 + k;
+      const uint64_t i = uint64_t(o.g) + uint64_t(j) * o.G;
+      const uint64_t ob = o.out_off[j + 1] - o.out_off[j], rb = o.row_base[j + 1] - o.row_base[j];
+      if (ob) memcpy(o.out + o.g_out_off[i], hout + (o.out_off[j] - L.out_base), ob);
+      if (rb) memcpy(o.rows + o.g_row_base[i], hrows + (o.row_base[j] - L.row_base), rb * sizeof(slate_row));
+      o.meta[i] = hmeta[k];
+    }
+    return SLATE_OK;
   }
-  par_memcpy(out + L.out_base, L.h_out.p, L.out_total);
-  memcpy(meta + L.b0, L.h_meta.p, size_t(L.n) * sizeof(slate_block_meta));
-  par_memcpy(rows + L.row_base, L.h_rows.p, L.rows_total * sizeof(slate_row));
+  par_memcpy(o.out + L.out_base, hout, L.out_total);
+  memcpy(o.meta + L.b0, hmeta, size_t(L.n) * sizeof(slate_block_meta));
+  par_memcpy(o.rows + L.row_base, hrows, L.rows_total * sizeof(slate_row));
   return SLATE_OK;
 }
 
@@ -105,15 +108,9 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
     return v ? uint32_t(std::min<unsigned long>(v, kChunkBlocks)) : kChunkBlocks;
   }();
   uint64_t out_acc = 0, rows_acc = 0;
-  bool fits = o.v_out != nullptr || (o.meta != nullptr);
+  bool fits = o.meta != nullptr;
   uint64_t* out_off = o.out_off;
   uint64_t* row_base = o.row_base;
-  if (o.v_out_off) {
-    o.v_out_off->assign(size_t(n) + 1, 0);
-    o.v_row_base->assign(size_t(n) + 1, 0);
-    out_off = o.v_out_off->data();
-    row_base = o.v_row_base->data();
-  }
   out_off[0] = 0;
   row_base[0] = 0;
   int li = 0;
@@ -162,7 +159,7 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
     L.rows_total = pr[m];
     out_acc += po[m];
     rows_acc += pr[m];
-    if (!o.v_out)
+    if (!o.G)
       fits = fits && out_acc <= o.out_cap && rows_acc <= o.rows_cap && (out_acc == 0 || o.out) &&
              (rows_acc == 0 || o.rows);
     L.busy = true;
@@ -190,11 +187,6 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
   for (PipeLane& L : ctx->lanes) {
     int st = lane_finish(L, o);
     if (st) return st;
-  }
-  if (o.v_out) {  // every chunk decoded: size the vectors exactly (zero-block shards included)
-    o.v_out->resize(out_acc);
-    o.v_rows->resize(rows_acc);
-    o.v_meta->resize(n);
   }
   return fits ? SLATE_OK : SLATE_E_CAPACITY;
 }
@@ -309,42 +301,44 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
   for (uint32_t g = 0; g < n_ctx; g++)
     if (!ctxs[g]) return SLATE_E_INVALID_ARG;
   struct Shard {
-    std::vector<uint8_t> in, out;
+    std::vector<uint8_t> in;
     std::vector<uint64_t> in_off, out_off, row_base;
-    std::vector<slate_block_meta> meta;
-    std::vector<slate_row> rows;
+    uint32_t m = 0;
     int st = SLATE_OK;
   };
   std::vector<Shard> sh(n_ctx);
-  auto work = [&](uint32_t g) {
+  auto run = [&](auto&& fn) {
+    std::vector<std::thread> th;
+    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(fn, g);
+    fn(0);
+    for (auto& t : th) t.join();
+    for (uint32_t g = 0; g < n_ctx; g++)
+      if (sh[g].st) return sh[g].st;
+    return int(SLATE_OK);
+  };
+  // phase 1: each context packs and plans its shard (block i -> context i mod n_ctx)
+  int st = run([&](uint32_t g) {
     Shard& S = sh[g];
-    const uint32_t m = shard_count(n, n_ctx, g);
-    S.in_off.assign(size_t(m) + 1, 0);
+    S.m = shard_count(n, n_ctx, g);
+    S.in_off.assign(size_t(S.m) + 1, 0);
+    S.out_off.assign(size_t(S.m) + 1, 0);
+    S.row_base.assign(size_t(S.m) + 1, 0);
     uint64_t bytes = 0;
-    for (uint32_t j = 0; j < m; j++) {
+    for (uint32_t j = 0; j < S.m; j++) {
       const uint64_t i = uint64_t(g) + uint64_t(j) * n_ctx;
       bytes += in_off[i + 1] - in_off[i];
     }
     S.in.resize(bytes + 1);
     S.st = slate_shard_pack(in, in_off, n, n_ctx, g, S.in.data(), bytes, S.in_off.data());
-    if (S.st || m == 0) return;
-    Sink o;
-    o.v_out = &S.out;
-    o.v_rows = &S.rows;
-    o.v_meta = &S.meta;
-    o.v_out_off = &S.out_off;
-    o.v_row_base = &S.row_base;
-    S.st = host_decode(ctxs[g], codec, S.in.data(), S.in_off.data(), m, o);
-  };
-  {
-    std::vector<std::thread> th;
-    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(work, g);
-    work(0);
-    for (auto& t : th) t.join();
-  }
-  for (uint32_t g = 0; g < n_ctx; g++)
-    if (sh[g].st) return sh[g].st;
-  // the outputs in the original block order
+    if (S.st || S.m == 0) return;
+    Sink o;  // no meta: plan only
+    o.out_off = S.out_off.data();
+    o.row_base = S.row_base.data();
+    const int r = host_decode(ctxs[g], codec, S.in.data(), S.in_off.data(), S.m, o);
+    S.st = r == SLATE_E_CAPACITY ? SLATE_OK : r;
+  });
+  if (st) return st;
+  // the batch's layout, in block order
   out_off[0] = row_base[0] = 0;
   for (uint32_t i = 0; i < n; i++) {
     const Shard& S = sh[i % n_ctx];
@@ -355,20 +349,22 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
   if (n == 0) return SLATE_OK;
   if (!meta || out_off[n] > out_cap || row_base[n] > rows_cap || (out_off[n] && !out) || (row_base[n] && !rows))
     return SLATE_E_CAPACITY;
-  auto scatter = [&](uint32_t g) {
-    const Shard& S = sh[g];
-    for (uint32_t j = 0, i = g; i < n; j++, i += n_ctx) {
-      const uint64_t ob = S.out_off[j + 1] - S.out_off[j], rb = S.row_base[j + 1] - S.row_base[j];
-      if (ob) memcpy(out + out_off[i], S.out.data() + S.out_off[j], ob);
-      if (rb) memcpy(rows + row_base[i], S.rows.data() + S.row_base[j], rb * sizeof(slate_row));
-      meta[i] = S.meta[j];
-    }
-  };
-  std::vector<std::thread> th;
-  for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(scatter, g);
-  scatter(0);
-  for (auto& t : th) t.join();
-  return SLATE_OK;
+  // phase 2: each context decodes its shard; chunks land block by block at their places
+  return run([&](uint32_t g) {
+    Shard& S = sh[g];
+    if (S.m == 0) return;
+    Sink o;
+    o.out = out;
+    o.meta = meta;
+    o.rows = rows;
+    o.out_off = S.out_off.data();
+    o.row_base = S.row_base.data();
+    o.G = n_ctx;
+    o.g = g;
+    o.g_out_off = out_off;
+    o.g_row_base = row_base;
+    S.st = host_decode(ctxs[g], codec, S.in.data(), S.in_off.data(), S.m, o);
+  });
 }
 
 }  // extern "C"
