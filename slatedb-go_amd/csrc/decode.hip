@@ -26,6 +26,7 @@
 #include "encode.h"
 #include "wave_crc.h"
 #include "zstd.h"
+#include "rows.h"
 
 namespace slate {
 
@@ -809,53 +810,6 @@ __global__ __launch_bounds__(256) void plan_zstd_kernel(const uint8_t* __restric
   }
 }
 
-// ---------------------------------------------------------------- v0 rows
-// row.go:191-261 against firstKey of length fk (fk < 0: firstKey == nil).
-__device__ inline void decode_row(const uint8_t* data, uint32_t data_len, uint32_t off, int fk, slate_row& r,
-                                  uint32_t* suffix_len_out) {
-  r.row_off = off;
-  r.key_prefix_len = 0;
-  r.key_suffix_len = 0;
-  r.value_len = 0;
-  r.flags = 0;
-  r.meta_len = 0;
-  const uint8_t* p = data + off;
-  uint32_t n = data_len - off;
-  *suffix_len_out = 0;
-  if (n >= 4) {
-    r.key_prefix_len = ld_be16(p);
-    r.key_suffix_len = ld_be16(p + 2);
-  }
-  if (n < 13) { r.status = SLATE_E_ROW_TOO_SHORT; return; }
-  uint16_t pl = r.key_prefix_len, sl = r.key_suffix_len;
-  if (pl > uint16_t(fk < 0 ? 0 : fk)) { r.status = SLATE_E_ROW_PREFIX; return; }
-  uint32_t o = 4;
-  if (n - o < sl) { r.status = SLATE_E_ROW_SUFFIX; return; }
-  o += sl;
-  if (n - o < 9) { r.status = SLATE_E_ROW_PANIC; return; }
-  uint8_t flags = p[o + 8];
-  o += 9;
-  if (flags & 2) {
-    if (n - o < 8) { r.status = SLATE_E_ROW_EXPIRE; return; }
-    o += 8;
-  }
-  if (flags & 4) {
-    if (n - o < 8) { r.status = SLATE_E_ROW_CREATE; return; }
-    o += 8;
-  }
-  if ((flags & 1) == 0) {
-    if (n - o < 4) { r.status = SLATE_E_ROW_VALUE_LEN; return; }
-    uint32_t vl = ld_be32(p + o);
-    o += 4;
-    if (n - o < vl) { r.status = SLATE_E_ROW_VALUE; return; }
-    r.value_len = vl;
-  }
-  r.flags = flags & 7;
-  r.meta_len = uint8_t(o - 4 - sl);
-  r.status = SLATE_OK;
-  *suffix_len_out = sl;
-}
-
 // ------------------------------------------------------------ one block
 struct WaveBufs {
   const uint32_t* tab;  // CRC tables in LDS (4 x 256)
@@ -1140,7 +1094,7 @@ hipError_t decode_kernels_available() {
 
 size_t decode_scratch_bytes(uint32_t n) {
   size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
-  return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t));
+  return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16;
 }
 
 static DecodeScratch carve(void* scratch, uint32_t n) {
@@ -1153,6 +1107,8 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   s.large_count = reinterpret_cast<uint32_t*>(p);
   p += 16;
   s.large_list = reinterpret_cast<uint32_t*>(p);
+  p += align16(size_t(n) * sizeof(uint32_t));
+  s.round_counter = reinterpret_cast<uint32_t*>(p);
   s.tiles = uint32_t(tiles);
   return s;
 }
@@ -1196,9 +1152,11 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   DecodeScratch s = carve(scratch, a.n);
   a.large_list = s.large_list;
   a.large_count = s.large_count;
+  a.round_counter = s.round_counter;
   (void)hipMemsetAsync(s.large_count, 0, sizeof(uint32_t), st);
+  (void)hipMemsetAsync(s.round_counter, 0, sizeof(uint32_t), st);
   if (a.n == 0) return hipGetLastError();
-  // Snappy: lane-per-block streaming decoder (any block size); ablation bit 16 (profiling
+  // Snappy: the lane-per-block streaming decoder (any block size); ablation bit 16 (profiling
   // variants only) selects the wave-per-block path instead
   if (a.codec == SLATE_CODEC_SNAPPY && !(dbg_bits(a) & 16)) return launch_decode_lpb2(st, a, num_cus);
   const size_t lds = a.codec == SLATE_CODEC_ZSTD

@@ -39,6 +39,7 @@ struct DecodeArgs {
   uint32_t debug;         // ablation switches (SLATE_DEBUG_MODE), read only by SLATE_PROFILING_BUILD variants
   uint32_t raw = 0;       // LPB only: payload is not a block (index/filter buffer): CRC + decompress, no block checks
   uint32_t rt_zero = 0;   // always 0: a value the compiler cannot fold (see decode_lpb2.hip rd128)
+  uint32_t* round_counter = nullptr;  // decode_lpb2: rounds handed out so far (launcher zeroes it)
 };
 
 // Ablation bits.  The shipped library is built without SLATE_PROFILING_BUILD, so every
@@ -57,6 +58,7 @@ struct DecodeScratch {
   uint64_t* pb;
   uint32_t* large_count;
   uint32_t* large_list;
+  uint32_t* round_counter;
   uint32_t tiles;
 };
 
