@@ -81,6 +81,10 @@ enum slate_status {
   SLATE_E_ZSTD_FRAME_SIZE = 59,     /* "frame size does not match size on stream" */
   SLATE_E_ZSTD_DICT = 60,           /* "unknown dictionary" (no dictionaries are configured) */
   SLATE_E_ZSTD_RESERVED_BLOCK = 61, /* "invalid input: reserved block type encountered" */
+  /* block.NewIteratorAtKey (block/iterator.go:31-82) */
+  SLATE_E_SEEK_NO_OFFSETS = 62,     /* "number of block.Offsets must be greater than zero" */
+  SLATE_E_SEEK_NO_FULL_KEY = 63,    /* "unable to locate uncorrupted first key in block; block is corrupt" */
+  SLATE_E_SEEK_PANIC = 64,          /* Go panics slicing block.Data[offset:] in firstFullKey */
   /* v0 row codec (row.go:191-288) — per-row status in slate_row.status */
   SLATE_E_ROW_TOO_SHORT = 20,       /* "corrupt v0 row: data length too short to decode a row" */
   SLATE_E_ROW_PREFIX = 21,          /* "corrupt v0 row: key prefix length exceeds length of first key in block" */
@@ -144,6 +148,19 @@ typedef struct slate_row {
   uint8_t meta_len;         /* seq(8)+flags(1)+[expire 8]+[create 8]+[value_len 4] */
   int16_t status;           /* SLATE_OK or SLATE_E_ROW_* */
 } slate_row;
+
+/* Result of block.NewIteratorAtKey (block/iterator.go:31-82) for one (block, key) query.
+ * The iterator starts at row `start` (its offsetIndex); its firstKey is the suffix of row
+ * `first_idx` (first_len bytes: firstFullKey's choice, row 0 unless that row is corrupt), and
+ * iterator.Next decodes row i >= start against it: key = firstKey[:prefixLen] || suffix.
+ * n_warn = warnings NewIteratorAtKey added (types.ErrWarn).  16 bytes. */
+typedef struct slate_seek {
+  uint32_t start;
+  int32_t first_idx;  /* -1 when no full key was found */
+  uint32_t n_warn;
+  int16_t status;     /* SLATE_OK, SLATE_E_SEEK_*, or the block's own decode status */
+  uint16_t first_len;
+} slate_seek;
 
 /* sstable.Config (builder.go:118-133); defaults in decode.go:16-23. */
 typedef struct slate_sst_config {
@@ -232,6 +249,19 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
                                uint64_t out_cap, uint64_t* out_off, slate_block_meta* meta,
                                slate_row* rows, uint64_t rows_cap, uint64_t* row_base);
 
+/* ---- seeks for the point-read path (slatedb/db.go:291-315) ---------------------------
+ * block.NewIteratorAtKey (block/iterator.go:31-82, firstFullKey :117-132) for n queries at
+ * once: query i seeks key i (keys[key_off[i]..key_off[i+1])) in block qblock[i] of a batch
+ * decoded by slate_block_decode_device / _batch (data, out_off, meta as those produce them).
+ * Device variant: device pointers, on the context stream.  Host variant: host buffers
+ * (the decode_batch layout, n_blocks blocks), synchronous. */
+int slate_block_seek_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_t* d_out_off,
+                            const slate_block_meta* d_meta, const uint32_t* d_qblock, const uint8_t* d_keys,
+                            const uint64_t* d_key_off, uint64_t n, slate_seek* d_res);
+int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                     uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
+                     uint64_t n, slate_seek* res);
+
 /* ---- block encode: block.Encode (block.go:54) ----------------------------------
  * Encodes one block (Data + Offsets) with codec: compress(Data || BE16 offsets ||
  * BE16 n) || BE32 CRC32-IEEE. */
@@ -292,6 +322,10 @@ void slate_index_free(slate_index* index);
 size_t slate_index_num_blocks(const slate_index* index); /* BlockMetaLength() */
 int slate_index_block_meta(const slate_index* index, size_t i, uint64_t* offset,
                            const uint8_t** first_key, size_t* first_key_len);
+/* sstable.Iterator.firstBlockIncludingOrAfterKey (iterator.go:123-153) for n keys: the block
+ * each NewIteratorAtKey (iterator.go:43-57) starts reading at, on the GPU. */
+int slate_index_seek(slate_ctx* ctx, const slate_index* index, const uint8_t* keys, const uint64_t* key_off,
+                     uint64_t n, uint64_t* block_out);
 /* Every BlockMeta's Offset at once (cap >= slate_index_num_blocks): what a batched reader or the
  * compaction path needs to slice an SST's data blocks without per-block calls. */
 int slate_index_block_offsets(const slate_index* index, uint64_t* offsets, size_t cap);

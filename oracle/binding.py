@@ -89,6 +89,10 @@ def lib():
             "or_v0_encode": (C.c_size_t, [C.POINTER(RowValue), u8p]),
             "or_v0_decode": (C.c_int, [u8p, C.c_size_t, C.c_long, C.POINTER(RowValue)]),
             "or_v0_peek": (C.c_int, [u8p, C.c_size_t, C.c_long, u16p, u16p]),
+            "or_block_seek": (C.c_int, [u8p, C.c_uint32, u16p, C.c_uint32, u8p, C.c_size_t,
+                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_uint32)]),
+            "or_index_seek": (C.c_uint64, [u8p, u64p, C.c_uint64, u8p, C.c_size_t]),
             "or_v0_estimate_block_size": (C.c_uint64, [u8p, u64p, u8p, u64p, C.c_size_t]),
             "or_block_builder_new": (C.c_void_p, [C.c_uint64]),
             "or_block_builder_free": (None, [C.c_void_p]),
@@ -285,6 +289,24 @@ def v0_peek(data: bytes, first_key_len: int | None) -> tuple[int, int, int]:
     pl, sl = C.c_uint16(), C.c_uint16()
     st = lib().or_v0_peek(p, len(data), -1 if first_key_len is None else first_key_len, C.byref(pl), C.byref(sl))
     return st, pl.value, sl.value
+
+
+def block_seek(data: bytes, offsets: list[int], key: bytes) -> tuple[int, int, int, int, int]:
+    """block.NewIteratorAtKey over a decoded block -> (status, start, first_idx, first_len, n_warn)."""
+    hd, pd = _buf(data)
+    offs = np.array(offsets or [0], dtype=np.uint16)
+    hk, pk = _buf(key)
+    st_, fi, fl, nw = C.c_uint32(), C.c_int32(), C.c_uint32(), C.c_uint32()
+    st = lib().or_block_seek(pd, len(data), offs.ctypes.data_as(u16p), len(offsets), pk, len(key), C.byref(st_),
+                             C.byref(fi), C.byref(fl), C.byref(nw))
+    return st, st_.value, fi.value, fl.value, nw.value
+
+
+def index_seek(first_keys: list[bytes], key: bytes) -> int:
+    """sstable.Iterator.firstBlockIncludingOrAfterKey over the index's first keys."""
+    kd, ko = _arena(first_keys)
+    hk, pk = _buf(key)
+    return int(lib().or_index_seek(kd.ctypes.data_as(u8p), ko.ctypes.data_as(u64p), len(first_keys), pk, len(key)))
 
 
 def _arena(items: list[bytes]):

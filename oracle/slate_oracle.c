@@ -53,6 +53,9 @@ const char* or_status_string(int s) {
     case OR_E_ROW_VALUE: return "corrupt v0 row: data length too short for for value";
     case OR_E_ROW_PANIC: return "runtime error: index out of range (v0 row seq/flags)";
     case OR_E_ROW_PEEK_SHORT: return "corrupt v0 row: data length too short to peek at row";
+    case OR_E_SEEK_NO_OFFSETS: return "number of block.Offsets must be greater than zero";
+    case OR_E_SEEK_NO_FULL_KEY: return "unable to locate uncorrupted first key in block; block is corrupt";
+    case OR_E_SEEK_PANIC: return "runtime error: slice bounds out of range (block.NewIteratorAtKey)";
     case OR_E_ROW_OFFSET_RANGE: return "block.Offset[%d] = %d is out of bounds";
     case OR_E_FILTER_TOO_SMALL: return "corrupt filter: filter is too small; must be at least 2 bytes";
     case OR_E_FILTER_CHECKSUM: return "corrupt filter: invalid checksum";
@@ -749,6 +752,80 @@ int or_v0_peek(const uint8_t* data, size_t n, long first_key_len, uint16_t* pl, 
   if (*pl > fk) return OR_E_ROW_PREFIX;
   if (n - 4 < *sl) return OR_E_ROW_SUFFIX;
   return OR_OK;
+}
+
+/* bytes.Compare */
+static int bytes_compare(const uint8_t* a, size_t an, const uint8_t* b, size_t bn) {
+  size_t m = an < bn ? an : bn;
+  int c = m ? memcmp(a, b, m) : 0;
+  if (c) return c < 0 ? -1 : 1;
+  return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+/* block/iterator.go:31-82 NewIteratorAtKey with firstFullKey (:117-132) and sort.Search
+ * (Go's binary search: i, j = 0, n; h = (i + j) / 2; !f(h) -> i = h + 1 else j = h). */
+int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
+                  size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn) {
+  *start = 0; *first_idx = -1; *first_len = 0; *n_warn = 0;
+  if (n == 0) return OR_E_SEEK_NO_OFFSETS;                         /* :32-34 */
+  /* firstFullKey: PeekAtKey(block.Data[offset:], nil); a full key has keyPrefixLen 0 */
+  int32_t idx = -1;
+  uint32_t fk_off = 0, fk_len = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (offsets[i] > data_len) return OR_E_SEEK_PANIC;              /* block.Data[offset:] */
+    uint16_t pl, sl;
+    int st = or_v0_peek(data + offsets[i], data_len - offsets[i], -1, &pl, &sl);
+    if (st) { (*n_warn)++; continue; }                              /* :120-123 */
+    if (pl == 0) { idx = (int32_t)i; fk_off = offsets[i] + 4; fk_len = sl; break; }
+  }
+  if (idx < 0) { (*n_warn)++; return OR_E_SEEK_NO_FULL_KEY; }       /* :130-131, :41-47 */
+  *first_idx = idx;
+  *first_len = fk_len;
+  const uint8_t* fk = data + fk_off;
+  if (bytes_compare(fk, fk_len, key, key_len) == 0) { *start = 0; return OR_OK; }  /* :51-58 */
+  uint32_t lo = 0, hi = n - (uint32_t)idx;
+  while (lo < hi) {
+    uint32_t h = (lo + hi) >> 1;
+    uint32_t o = offsets[h + (uint32_t)idx];
+    int ok = 0;
+    if (o > (uint16_t)data_len) {                                   /* :65-68 */
+      (*n_warn)++;
+    } else {
+      uint16_t pl, sl;
+      int st = or_v0_peek(data + o, data_len - o, (long)fk_len, &pl, &sl);
+      if (st) {
+        (*n_warn)++;                                                /* :70-73 */
+      } else {
+        /* v0FullKey(p, firstKey) = firstKey[:prefixLen] || suffix (row.go:72-79) */
+        size_t kl = (size_t)pl + sl;
+        size_t m = kl < key_len ? kl : key_len;
+        int c = 0;
+        for (size_t b = 0; b < m && !c; b++) {
+          uint8_t x = b < pl ? fk[b] : data[o + 4 + (b - pl)];
+          if (x != key[b]) c = x < key[b] ? -1 : 1;
+        }
+        if (!c) c = kl < key_len ? -1 : (kl > key_len ? 1 : 0);
+        ok = c >= 0;
+      }
+    }
+    if (!ok) lo = h + 1; else hi = h;
+  }
+  *start = lo + (uint32_t)idx;
+  return OR_OK;
+}
+
+/* sstable/iterator.go:123-153 firstBlockIncludingOrAfterKey */
+uint64_t or_index_seek(const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks, const uint8_t* key,
+                       size_t key_len) {
+  int64_t low = 0, high = (int64_t)n_blocks - 1, found = 0;
+  while (low <= high) {
+    int64_t mid = low + (high - low) / 2;
+    int c = bytes_compare(keys + key_off[mid], key_off[mid + 1] - key_off[mid], key, key_len);
+    if (c < 0) { low = mid + 1; found = mid; }
+    else if (c > 0) { if (mid > 0) high = mid - 1; else break; }
+    else return (uint64_t)mid;
+  }
+  return (uint64_t)found;
 }
 
 /* row.go:50-65 V0EstimateBlockSize: 2 + Σ(v0Size(suffix=key) + 2) + 4 */

@@ -48,6 +48,7 @@ enum {
   OR_E_UNEXPECTED_EOF = 54, OR_E_EOF = 55,
   OR_E_ZSTD_MAGIC = 56, OR_E_ZSTD_CHECKSUM = 57, OR_E_ZSTD_CORRUPT = 58, OR_E_ZSTD_FRAME_SIZE = 59,
   OR_E_ZSTD_DICT = 60, OR_E_ZSTD_RESERVED_BLOCK = 61,
+  OR_E_SEEK_NO_OFFSETS = 62, OR_E_SEEK_NO_FULL_KEY = 63, OR_E_SEEK_PANIC = 64,
   OR_E_INVALID_ARG = 102, OR_E_CAPACITY = 103, OR_E_OOM = 104,
 };
 
@@ -198,6 +199,16 @@ int or_sst_read_info(const uint8_t* sst, size_t n, or_sst_info* info, uint8_t* f
  * (merge.go:67-72), and lastKey starts nil, so empty keys are never returned. */
 int or_merge_sort(uint32_t k, const uint8_t* keys, const uint64_t* key_off, const uint64_t* src_start,
                   uint32_t* out_idx, uint64_t* n_out);
+
+/* block.NewIteratorAtKey (block/iterator.go:31-82) over a decoded block (Data, Offsets):
+ * *start = the iterator's offsetIndex, *first_idx = the row firstFullKey returned (its suffix
+ * is the iterator's firstKey, *first_len bytes), *n_warn = warnings added.  Returns OR_OK,
+ * OR_E_SEEK_NO_OFFSETS, OR_E_SEEK_NO_FULL_KEY or OR_E_SEEK_PANIC (Go slice panic). */
+int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
+                  size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn);
+/* sstable.Iterator.firstBlockIncludingOrAfterKey (iterator.go:123-153) over the index's first keys. */
+uint64_t or_index_seek(const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks, const uint8_t* key,
+                       size_t key_len);
 
 #ifdef __cplusplus
 }

@@ -2,6 +2,7 @@
 // ReadBlocks batches go through slate_block_decode_batch).
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "host_ctx.h"
 
@@ -44,6 +45,9 @@ const char* slate_status_string(int s) {
     case SLATE_E_ZSTD_FRAME_SIZE: return "frame size does not match size on stream";
     case SLATE_E_ZSTD_DICT: return "unknown dictionary";
     case SLATE_E_ZSTD_RESERVED_BLOCK: return "invalid input: reserved block type encountered";
+    case SLATE_E_SEEK_NO_OFFSETS: return "number of block.Offsets must be greater than zero";
+    case SLATE_E_SEEK_NO_FULL_KEY: return "unable to locate uncorrupted first key in block; block is corrupt";
+    case SLATE_E_SEEK_PANIC: return "runtime error: slice bounds out of range (block.NewIteratorAtKey)";
     case SLATE_E_ROW_TOO_SHORT: return "corrupt v0 row: data length too short to decode a row";
     case SLATE_E_ROW_PREFIX: return "corrupt v0 row: key prefix length exceeds length of first key in block";
     case SLATE_E_ROW_SUFFIX: return "corrupt v0 row: key suffix length exceeds length of block";
@@ -149,5 +153,54 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
 }
 
 // slate_block_decode_batch / slate_block_decode / the sharded decode: api_host.cpp.
+
+int slate_block_seek_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_t* d_out_off,
+                            const slate_block_meta* d_meta, const uint32_t* d_qblock, const uint8_t* d_keys,
+                            const uint64_t* d_key_off, uint64_t n, slate_seek* d_res) {
+  if (!ctx || (n && (!d_out_off || !d_meta || !d_qblock || !d_key_off || !d_res))) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(launch_block_seek(ctx->stream, d_data, d_out_off, d_meta, d_qblock, d_keys, d_key_off, n, d_res));
+  return SLATE_OK;
+}
+
+int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                     uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
+                     uint64_t n, slate_seek* res) {
+  if (!ctx || !out_off || (n_blocks && !meta) || (n && (!qblock || !key_off || !res))) return SLATE_E_INVALID_ARG;
+  if (n == 0) return SLATE_OK;
+  for (uint64_t i = 0; i < n; i++)
+    if (qblock[i] >= n_blocks) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  const uint64_t db = out_off[n_blocks], kb = key_off[n] - key_off[0];
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t o_data = carve(db + 16), o_off = carve((size_t(n_blocks) + 1) * 8),
+               o_meta = carve(size_t(n_blocks) * sizeof(slate_block_meta) + 16), o_q = carve(n * 4),
+               o_keys = carve(kb + 16), o_koff = carve((n + 1) * 8), o_res = carve(n * sizeof(slate_seek));
+  SLATE_HIP(ctx->e_g.ensure(off));
+  uint8_t* base = ctx->e_g.as<uint8_t>();
+  std::vector<uint64_t> rel(n + 1);
+  for (uint64_t i = 0; i <= n; i++) rel[i] = key_off[i] - key_off[0];
+  if (db) SLATE_HIP(hipMemcpyAsync(base + o_data, data, db, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(base + o_off, out_off, (size_t(n_blocks) + 1) * 8, hipMemcpyHostToDevice, st));
+  if (n_blocks)
+    SLATE_HIP(hipMemcpyAsync(base + o_meta, meta, size_t(n_blocks) * sizeof(slate_block_meta), hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(base + o_q, qblock, n * 4, hipMemcpyHostToDevice, st));
+  if (kb) SLATE_HIP(hipMemcpyAsync(base + o_keys, keys + key_off[0], kb, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(base + o_koff, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_block_seek(st, base + o_data, reinterpret_cast<const uint64_t*>(base + o_off),
+                              reinterpret_cast<const slate_block_meta*>(base + o_meta),
+                              reinterpret_cast<const uint32_t*>(base + o_q), base + o_keys,
+                              reinterpret_cast<const uint64_t*>(base + o_koff), n,
+                              reinterpret_cast<slate_seek*>(base + o_res)));
+  SLATE_HIP(hipMemcpyAsync(res, base + o_res, n * sizeof(slate_seek), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  return SLATE_OK;
+}
 
 }  // extern "C"

@@ -745,6 +745,36 @@ int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
 
 void slate_index_free(slate_index* index) { delete index; }
 
+int slate_index_seek(slate_ctx* ctx, const slate_index* index, const uint8_t* keys, const uint64_t* key_off,
+                     uint64_t n, uint64_t* block_out) {
+  if (!ctx || !index || (n && (!key_off || !block_out))) return SLATE_E_INVALID_ARG;
+  if (n == 0) return SLATE_OK;
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  const uint64_t nb = index->offsets.size(), ib = index->keys.size(), kb = key_off[n] - key_off[0];
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t o_ik = carve(ib + 16), o_iko = carve((nb + 1) * 8), o_q = carve(kb + 16), o_qo = carve((n + 1) * 8),
+               o_out = carve(n * 8);
+  SLATE_HIP(ctx->e_h.ensure(off));
+  uint8_t* base = ctx->e_h.as<uint8_t>();
+  std::vector<uint64_t> rel(n + 1);
+  for (uint64_t i = 0; i <= n; i++) rel[i] = key_off[i] - key_off[0];
+  if (ib) SLATE_HIP(hipMemcpyAsync(base + o_ik, index->keys.data(), ib, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(base + o_iko, index->key_off.data(), (nb + 1) * 8, hipMemcpyHostToDevice, st));
+  if (kb) SLATE_HIP(hipMemcpyAsync(base + o_q, keys + key_off[0], kb, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(base + o_qo, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_index_seek(st, base + o_ik, reinterpret_cast<const uint64_t*>(base + o_iko), nb, base + o_q,
+                              reinterpret_cast<const uint64_t*>(base + o_qo), n, reinterpret_cast<uint64_t*>(base + o_out)));
+  SLATE_HIP(hipMemcpyAsync(block_out, base + o_out, n * 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  return SLATE_OK;
+}
+
 size_t slate_index_num_blocks(const slate_index* index) { return index ? index->offsets.size() : 0; }
 
 int slate_index_block_meta(const slate_index* index, size_t i, uint64_t* offset, const uint8_t** first_key,

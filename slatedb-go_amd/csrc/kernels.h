@@ -97,6 +97,13 @@ hipError_t launch_gather_copy(hipStream_t st, const uint32_t* idx, uint64_t n, c
 hipError_t launch_snappy_stream(hipStream_t st, const uint8_t* in, uint32_t sn, uint32_t hdr, uint8_t* out,
                                 uint32_t dn, int32_t* status);
 
+// Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
+hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                             const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
+                             slate_seek* res);
+hipError_t launch_index_seek(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks,
+                             const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq, uint64_t* out);
+
 // Validates that the code object loads on the current device.
 hipError_t decode_kernels_available();
 

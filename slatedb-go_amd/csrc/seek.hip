@@ -1,0 +1,167 @@
+// Seeks for the point-read path (slatedb/db.go:291-315 reads through them):
+//   block_seek_kernel  block.NewIteratorAtKey (internal/sstable/block/iterator.go:31-82) with
+//                      firstFullKey's corrupted-first-key recovery (:117-132) and its warnings,
+//                      over blocks decoded by the block decode kernels;
+//   index_seek_kernel  sstable.Iterator.firstBlockIncludingOrAfterKey (iterator.go:123-153)
+//                      over an SST index's first keys.
+// One thread per query: each query is a short dependent chain (a binary search over a
+// block's rows or an index), and a batch of point reads supplies the parallelism.
+#include "common.h"
+#include "kernels.h"
+
+namespace slate {
+
+namespace {
+
+__device__ inline int cmp_bytes(const uint8_t* a, uint32_t an, const uint8_t* b, uint32_t bn) {
+  const uint32_t m = an < bn ? an : bn;
+  for (uint32_t i = 0; i < m; i++)
+    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+// row.go:265-288 PeekAtKey: status, prefix length, suffix length
+__device__ inline int peek(const uint8_t* p, uint32_t n, uint32_t fk_len, uint32_t* pl, uint32_t* sl) {
+  if (n < 4) return SLATE_E_ROW_PEEK_SHORT;
+  *pl = ld_be16(p);
+  *sl = ld_be16(p + 2);
+  if (*pl > fk_len) return SLATE_E_ROW_PREFIX;
+  if (n - 4 < *sl) return SLATE_E_ROW_SUFFIX;
+  return SLATE_OK;
+}
+
+}  // namespace
+
+__global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                                  const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
+                                  slate_seek* res) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  slate_seek r{};
+  r.first_idx = -1;
+  const uint32_t b = qblock[q];
+  const slate_block_meta m = meta[b];
+  const uint8_t* key = qkeys + qkey_off[q];
+  const uint32_t kl = uint32_t(qkey_off[q + 1] - qkey_off[q]);
+  if (m.status != SLATE_OK) {  // the block failed block.Decode: no iterator exists for it
+    r.status = m.status;
+    res[q] = r;
+    return;
+  }
+  const uint8_t* d = data + out_off[b];
+  const uint32_t dlen = m.data_len, n = m.n_rows;
+  const uint8_t* offs = d + dlen;  // BE16 Offsets after Data
+  if (n == 0) {
+    r.status = SLATE_E_SEEK_NO_OFFSETS;  // iterator.go:32-34
+    res[q] = r;
+    return;
+  }
+  // firstFullKey: the first row that PeekAtKey(Data[off:], nil) accepts has keyPrefixLen 0
+  int32_t idx = -1;
+  uint32_t fk_off = 0, fk_len = 0, warn = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t o = ld_be16(offs + 2 * i);
+    if (o > dlen) {  // block.Data[offset:] panics
+      r.status = SLATE_E_SEEK_PANIC;
+      r.n_warn = warn;
+      res[q] = r;
+      return;
+    }
+    uint32_t pl, sl;
+    if (peek(d + o, dlen - o, 0, &pl, &sl) != SLATE_OK) {
+      warn++;
+      continue;
+    }
+    if (pl == 0) {
+      idx = int32_t(i);
+      fk_off = o + 4;
+      fk_len = sl;
+      break;
+    }
+  }
+  if (idx < 0) {  // iterator.go:130-131 -> :41-47
+    r.status = SLATE_E_SEEK_NO_FULL_KEY;
+    r.n_warn = warn + 1;
+    res[q] = r;
+    return;
+  }
+  r.first_idx = idx;
+  r.first_len = uint16_t(fk_len);
+  const uint8_t* fk = d + fk_off;
+  if (cmp_bytes(fk, fk_len, key, kl) == 0) {  // iterator.go:51-58: offsetIndex 0
+    r.start = 0;
+    r.n_warn = warn;
+    res[q] = r;
+    return;
+  }
+  // sort.Search(len(Offsets) - idx, ...) over PeekAtKey + v0FullKey (iterator.go:62-74)
+  uint32_t lo = 0, hi = n - uint32_t(idx);
+  while (lo < hi) {
+    const uint32_t h = (lo + hi) >> 1;
+    const uint32_t o = ld_be16(offs + 2 * (h + uint32_t(idx)));
+    bool ok = false;
+    uint32_t pl, sl;
+    if (o > uint32_t(uint16_t(dlen))) {
+      warn++;
+    } else if (peek(d + o, dlen - o, fk_len, &pl, &sl) != SLATE_OK) {
+      warn++;
+    } else {
+      // v0FullKey = firstKey[:prefixLen] || suffix, compared with the sought key
+      const uint32_t fl = pl + sl, mm = fl < kl ? fl : kl;
+      int c = 0;
+      for (uint32_t i = 0; i < mm && !c; i++) {
+        const uint8_t x = i < pl ? fk[i] : d[o + 4 + (i - pl)];
+        if (x != key[i]) c = x < key[i] ? -1 : 1;
+      }
+      if (!c) c = fl < kl ? -1 : (fl > kl ? 1 : 0);
+      ok = c >= 0;
+    }
+    if (!ok) lo = h + 1;
+    else hi = h;
+  }
+  r.start = lo + uint32_t(idx);
+  r.n_warn = warn;
+  r.status = SLATE_OK;
+  res[q] = r;
+}
+
+__global__ void index_seek_kernel(const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks, const uint8_t* qkeys,
+                                  const uint64_t* qkey_off, uint64_t nq, uint64_t* out) {
+  const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const uint8_t* key = qkeys + qkey_off[q];
+  const uint32_t kl = uint32_t(qkey_off[q + 1] - qkey_off[q]);
+  int64_t low = 0, high = int64_t(n_blocks) - 1, found = 0;
+  while (low <= high) {
+    const int64_t mid = low + (high - low) / 2;
+    const int c = cmp_bytes(keys + key_off[mid], uint32_t(key_off[mid + 1] - key_off[mid]), key, kl);
+    if (c < 0) {
+      low = mid + 1;
+      found = mid;
+    } else if (c > 0) {
+      if (mid > 0) high = mid - 1;
+      else break;
+    } else {
+      found = mid;
+      break;
+    }
+  }
+  out[q] = uint64_t(found);
+}
+
+hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                             const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
+                             slate_seek* res) {
+  if (nq == 0) return hipSuccess;
+  block_seek_kernel<<<uint32_t((nq + 255) / 256), 256, 0, st>>>(data, out_off, meta, qblock, qkeys, qkey_off, nq, res);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_seek(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks,
+                             const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq, uint64_t* out) {
+  if (nq == 0) return hipSuccess;
+  index_seek_kernel<<<uint32_t((nq + 255) / 256), 256, 0, st>>>(keys, key_off, n_blocks, qkeys, qkey_off, nq, out);
+  return hipGetLastError();
+}
+
+}  // namespace slate

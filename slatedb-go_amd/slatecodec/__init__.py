@@ -30,6 +30,8 @@ u64p = C.POINTER(C.c_uint64)
 szp = C.POINTER(C.c_size_t)
 vp = C.c_void_p
 
+SEEK_DTYPE = np.dtype([("start", "<u4"), ("first_idx", "<i4"), ("n_warn", "<u4"), ("status", "<i2"),
+                       ("first_len", "<u2")])
 META_DTYPE = np.dtype([("status", "<i2"), ("flags", "<u2"), ("detail", "<i4"), ("data_len", "<u4"),
                        ("n_rows", "<u2"), ("aux", "<u2")])
 ROW_DTYPE = np.dtype([("row_off", "<u4"), ("key_prefix_len", "<u2"), ("key_suffix_len", "<u2"),
@@ -74,6 +76,9 @@ _SIGS = {
                                            C.c_uint64, vp]),
     "slate_block_decode": (C.c_int, [vp, C.c_int, vp, C.c_size_t, vp, C.c_size_t, szp, vp, vp, C.c_size_t]),
     "slate_shard_blocks": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "slate_block_seek_device": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, C.c_uint64, vp]),
+    "slate_block_seek": (C.c_int, [vp, vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint64, vp]),
+    "slate_index_seek": (C.c_int, [vp, vp, vp, vp, C.c_uint64, vp]),
     "slate_shard_pack": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint64, vp]),
     "slate_block_decode_sharded": (C.c_int, [vp, C.c_uint32, C.c_int, vp, vp, C.c_uint32, vp, C.c_uint64, vp, vp,
                                              vp, C.c_uint64, vp]),
@@ -210,6 +215,31 @@ class Context:
         n = len(in_off) - 1
         return lib().slate_block_decode_batch(self._h, codec, _ptr(blob), _ptr(in_off), n, _ptr(out), out.size,
                                               _ptr(out_off), _ptr(meta), _ptr(rows), rows.size, _ptr(row_base))
+
+    def block_seek(self, out: np.ndarray, out_off: np.ndarray, meta: np.ndarray, qblock: list[int],
+                   keys: list[bytes]) -> np.ndarray:
+        """block.NewIteratorAtKey for (block, key) queries over a decode_batch result -> SEEK_DTYPE."""
+        kd, ko = _arena(keys)
+        qb = np.ascontiguousarray(qblock, np.uint32)
+        res = np.zeros(max(len(keys), 1), SEEK_DTYPE)
+        out = np.ascontiguousarray(out, np.uint8)
+        _check(lib().slate_block_seek(self._h, _ptr(out), _ptr(np.ascontiguousarray(out_off, np.uint64)),
+                                      _ptr(np.ascontiguousarray(meta)), len(out_off) - 1, _ptr(qb), _ptr(kd), _ptr(ko),
+                                      len(keys), _ptr(res)), "slate_block_seek")
+        return res[: len(keys)]
+
+    def block_seek_device(self, d_data: int, d_out_off: int, d_meta: int, d_qblock: int, d_keys: int, d_key_off: int,
+                          n: int, d_res: int) -> None:
+        _check(lib().slate_block_seek_device(self._h, d_data, d_out_off, d_meta, d_qblock, d_keys, d_key_off, n, d_res),
+               "slate_block_seek_device")
+
+    def index_seek(self, index: "Index", keys: list[bytes]) -> np.ndarray:
+        """sstable.Iterator.firstBlockIncludingOrAfterKey for each key (u64 block indexes)."""
+        kd, ko = _arena(keys)
+        out = np.zeros(max(len(keys), 1), np.uint64)
+        _check(lib().slate_index_seek(self._h, index.handle, _ptr(kd), _ptr(ko), len(keys), _ptr(out)),
+               "slate_index_seek")
+        return out[: len(keys)]
 
     def block_decode(self, encoded: bytes, codec: int):
         """block.Decode(&b, input, codec) -> (status, meta, Data, Offsets)."""

@@ -120,6 +120,23 @@ V = {
     "iterator_seek": {"kvs": [["donkey", "kong"], ["kratos", "atreus"], ["super", "mario"]],
                       "cases": [{"key": "kratos", "start": 1}, {"key": "donkey", "start": 0},
                                 {"key": "ka", "start": 1}, {"key": "zzz", "start": 3}]},
+    # block_test.go:416-527 TestNewIteratorAtKeyWithCorruptedKeys: BlockSize 4096; "corrupt"
+    # lists the row indexes whose first Data byte is set to 0xFF ("data0" = Data[0]); either the
+    # error text or the keys Next() returns, and whether warnings were recorded
+    "iterator_seek_corrupt": [
+        {"name": "AllKeysCorrupted", "kvs": [["key1", "value1"], ["key2", "value2"]], "corrupt": [0, 1],
+         "key": "key1", "error": "unable to locate uncorrupted first key in block; block is corrupt"},
+        {"name": "AllKeysCorruptedFirstKeyCorrupt",
+         "kvs": [["key1", "value1"], ["key2", "value2"], ["key3", "value3"], ["key4", "value4"],
+                 ["key5", "value5"]], "corrupt": ["data0"], "key": "key4",
+         "error": "unable to locate uncorrupted first key in block; block is corrupt"},
+        {"name": "CorruptedFirstKey", "kvs": [["hello", "world"], ["rainbow", "dash"], ["wonderful", "day"]],
+         "corrupt": [0], "key": "key1", "next": [["rainbow", "dash"], ["wonderful", "day"]], "warnings": True},
+        {"name": "SomeKeysCorrupted",
+         "kvs": [["key1", "value1"], ["key2", "value2"], ["key3", "value3"], ["key4", "value4"],
+                 ["key5", "value5"]], "corrupt": [1, 2], "key": "key4",
+         "next": [["key4", "value4"], ["key5", "value5"]], "warnings": True},
+    ],
     # slatedb/store/table_store_test.go:69-97 TestBuilderShouldMakeBlocksAvailable (BlockSize 32)
     "make_blocks_available": {"block_size": 32,
                               "adds1": [["aaaaaaaa", "11111111"], ["bbbbbbbb", "22222222"], ["cccccccc", "33333333"]],

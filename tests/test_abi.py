@@ -18,7 +18,7 @@ def test_library_exports_every_header_symbol():
 
 def test_status_strings_match_oracle(oracle):
     import slatecodec as sc
-    for code in list(range(0, 50)):
+    for code in list(range(0, 70)):
         o = oracle.status_string(code)
         if o != "unknown status":
             assert sc.status_string(code) == o, code

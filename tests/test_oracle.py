@@ -383,21 +383,34 @@ def _libsnappy():
     return None
 
 
+# Inputs on which the restated golang/snappy v0.0.4 encoder and C++ libsnappy 1.1.8 may
+# legitimately differ (an explicit allow-list: none so far; golang/snappy emits the same bytes
+# as C++ snappy by design).  Any other difference fails the test.
+LIBSNAPPY_ALLOWED_DIFF: set[str] = set()
+
+
 def test_snappy_cross_libsnappy(oracle):
+    """Cross-check (not authority: golang/snappy itself is absent) of the restated encoder's
+    bytes against C++ libsnappy on row-shaped inputs, plus random and repetitive buffers."""
     L = _libsnappy()
     if L is None:
         pytest.skip("libsnappy not present")
     rng = np.random.default_rng(7)
-    same = 0
+    inputs = []
     for i in range(40):
         r = rng.integers(0, 256, 42, dtype=np.uint8).tobytes()
-        src = (b"\x00\x0e\x00\x02xy" + b"\x00" * 13 + b"\x54" + r + r) * (1 + i)
+        inputs.append((f"rows{i}", (b"\x00\x0e\x00\x02xy" + b"\x00" * 13 + b"\x54" + r + r) * (1 + i)))
+    for i, n in enumerate((0, 1, 16, 17, 100, 4096, 65536, 65537, 200_000)):
+        inputs.append((f"rand{i}", rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+        inputs.append((f"rep{i}", bytes(rng.integers(0, 4, n, dtype=np.uint8))))
+    diff = []
+    for name, src in inputs:
         out = ctypes.create_string_buffer(L.snappy_max_compressed_length(len(src)))
         ol = ctypes.c_size_t(len(out))
         assert L.snappy_compress(src, len(src), out, ctypes.byref(ol)) == 0
         lib_bytes = out.raw[: ol.value]
         st, d = oracle.snappy_decode(lib_bytes)
         assert st == 0 and d == src  # the restated golang decoder accepts C++ snappy output
-        same += lib_bytes == oracle.snappy_encode(src)
-    # informational: golang/snappy was designed to emit the same bytes as C++ snappy
-    print(f"libsnappy byte-identical on {same}/40 inputs")
+        if lib_bytes != oracle.snappy_encode(src) and name not in LIBSNAPPY_ALLOWED_DIFF:
+            diff.append(name)
+    assert not diff, f"restated golang/snappy encoder differs from libsnappy on {diff}"
