@@ -316,7 +316,8 @@ int slate_decode_info(const uint8_t* buf, size_t len, slate_sst_info* info, uint
                       size_t first_key_cap);
 int slate_encode_info(const slate_sst_info* info, const uint8_t* first_key, uint8_t* out,
                       size_t out_cap, size_t* out_len);
-/* DecodeIndex (flatbuf.go:83): CRC verify + decompress; index handle owns the bytes. */
+/* DecodeIndex (flatbuf.go:83): CRC verify + decompress (every codec: Snappy by the streaming
+ * decoder, LZ4 / Zlib / Zstd by one wave per payload in HBM); index handle owns the bytes. */
 int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, slate_index** index);
 void slate_index_free(slate_index* index);
 size_t slate_index_num_blocks(const slate_index* index); /* BlockMetaLength() */
@@ -346,7 +347,8 @@ int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_in
 int slate_bloom_build(slate_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
                       uint32_t bits_per_key, uint8_t* bits, size_t bits_cap, size_t* bits_len,
                       uint16_t* num_probes);
-/* Encode (bloom.go:52) / Decode (bloom.go:70).  Decode's bits alias nothing: copied out. */
+/* Encode (bloom.go:52; None and Snappy) / Decode (bloom.go:70; every codec).  Decode's bits alias
+ * nothing: copied out. */
 int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len,
                        int codec, uint8_t* out, size_t out_cap, size_t* out_len);
 int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec,

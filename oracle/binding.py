@@ -456,8 +456,8 @@ def bloom_encode(num_probes: int, bits: bytes, codec: int) -> bytes:
     return out[:ol.value].tobytes()
 
 
-def bloom_decode(buf: bytes, codec: int) -> tuple[int, int, bytes]:
-    cap = max(len(buf) * 24, 16)
+def bloom_decode(buf: bytes, codec: int, cap: int | None = None) -> tuple[int, int, bytes]:
+    cap = cap or max(len(buf) * 24, 16)
     out = np.zeros(cap, np.uint8)
     h, p = _buf(buf)
     np_ = C.c_uint16()
@@ -501,9 +501,9 @@ def encode_index(metas: list[tuple[int, bytes]], codec: int) -> bytes:
     return out[:ol.value].tobytes()
 
 
-def decode_index(buf: bytes, codec: int) -> tuple[int, list[tuple[int, bytes]]]:
+def decode_index(buf: bytes, codec: int, cap: int | None = None) -> tuple[int, list[tuple[int, bytes]]]:
     h, p = _buf(buf)
-    cap = max(len(buf) * 24, 64)
+    cap = cap or max(len(buf) * 24, 64)
     offs = np.zeros(cap, np.uint64)
     keys = np.zeros(cap, np.uint8)
     ko = np.zeros(cap + 1, np.uint64)

@@ -191,6 +191,48 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
   return SLATE_OK;
 }
 
+// Any codec: Snappy through the function above; LZ4 / Zlib / Zstd through the plan kernels
+// (decoded capacity) and one wave per payload reading and writing HBM (decode_payload_kernel).
+int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
+                              int* bstatus) {
+  if (codec == SLATE_CODEC_SNAPPY) return ctx_snappy_decode_buffer(ctx, buf, len, out, bstatus);
+  if (codec != SLATE_CODEC_LZ4 && codec != SLATE_CODEC_ZLIB && codec != SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+  if (len < 4 || len > 0xFFFFFF00ull) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  // in_off[2] | out_off[2] | row_base[2] | meta (16 B) | rows (16 B) | plan scratch
+  constexpr size_t kHead = 10 * sizeof(uint64_t);
+  SLATE_HIP(ctx->d_scratch.ensure(kHead + decode_scratch_bytes(1) + 64));
+  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  uint64_t* u = ctx->d_scratch.as<uint64_t>();
+  const uint64_t hv[2] = {0, len};
+  SLATE_HIP(hipMemcpyAsync(ctx->d_in.p, buf, len, hipMemcpyHostToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(u, hv, sizeof(hv), hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_decode_plan(st, codec, ctx->d_in.as<uint8_t>(), u, 1, u + 2, u + 4,
+                               reinterpret_cast<uint8_t*>(u) + kHead));
+  uint64_t cap[2] = {0, 0};
+  SLATE_HIP(hipMemcpyAsync(cap, u + 2, sizeof(cap), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  SLATE_HIP(ctx->d_out.ensure(cap[1] + 64));
+  DecodeArgs a{codec, ctx->d_in.as<uint8_t>(), u, 1, ctx->d_out.as<uint8_t>(), u + 2,
+               reinterpret_cast<slate_block_meta*>(u + 6), reinterpret_cast<slate_row*>(u + 8), u + 4, nullptr, nullptr,
+               0};
+  a.raw = 1;
+  SLATE_HIP(launch_decode_payload(st, a, ctx->num_cus));
+  slate_block_meta m;
+  SLATE_HIP(hipMemcpyAsync(&m, u + 6, sizeof(m), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  *bstatus = m.status;
+  if (m.status == SLATE_OK) {
+    out.resize(m.data_len);
+    if (m.data_len) {
+      SLATE_HIP(hipMemcpyAsync(out.data(), ctx->d_out.p, m.data_len, hipMemcpyDeviceToHost, st));
+      SLATE_HIP(hipStreamSynchronize(st));
+    }
+  }
+  return SLATE_OK;
+}
+
 // --------------------------------------------------------------- SST builder
 struct slate_sst_table {
   slate_sst_info info{};
@@ -723,11 +765,10 @@ int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   if (st) return st;
   if (crc != ld_be32(buf + ci)) return SLATE_E_INDEX_CHECKSUM;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
   slate_index* x = new slate_index();
-  if (codec == SLATE_CODEC_SNAPPY) {
+  if (codec != SLATE_CODEC_NONE) {
     int bst = 0;
-    st = ctx_snappy_decode_buffer(ctx, buf, len, x->data, &bst);
+    st = ctx_payload_decode_buffer(ctx, codec, buf, len, x->data, &bst);
     if (st || bst) {
       delete x;
       return st ? st : (bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_INDEX_CHECKSUM : bst);
@@ -910,13 +951,12 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   if (st) return st;
   if (crc != ld_be32(buf + ci)) return SLATE_E_FILTER_CHECKSUM;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
   std::vector<uint8_t> dec;
   const uint8_t* p = buf;
   size_t pn = ci;
-  if (codec == SLATE_CODEC_SNAPPY) {
+  if (codec != SLATE_CODEC_NONE) {
     int bst = 0;
-    st = ctx_snappy_decode_buffer(ctx, buf, len, dec, &bst);
+    st = ctx_payload_decode_buffer(ctx, codec, buf, len, dec, &bst);
     if (st) return st;
     if (bst) return bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_FILTER_CHECKSUM : bst;
     p = dec.data();

@@ -365,14 +365,15 @@ __device__ uint32_t wave_xxh32(const uint8_t* base, uint32_t off, uint32_t n, in
 
 // The frame in LDS (in, n bytes; `base`/`off` address it for 4-aligned reads) decoded in
 // order into out[0, cap): wave-uniform parse, lane-parallel copies.  The checks and
-// their order are oracle/slate_oracle.c lz4_frame's.
+// their order are oracle/slate_oracle.c lz4_frame's; out == nullptr is its sizes-only pass
+// (no writes, no checksums).
 __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, uint8_t* out, uint32_t cap, int lane,
                                uint32_t* out_len) {
   const uint8_t* in = base + off;
   *out_len = 0;
   const Lz4Hdr h = lz4_header(in, n);
   if (h.status != SLATE_OK) return h.status;
-  if (in[4 + h.hl] != ((wave_xxh32(base, off + 4, h.hl, lane) >> 8) & 0xFF)) return SLATE_E_LZ4_HEADER_CHECKSUM;
+  if (out && in[4 + h.hl] != ((wave_xxh32(base, off + 4, h.hl, lane) >> 8) & 0xFF)) return SLATE_E_LZ4_HEADER_CHECKSUM;
   if (h.flg & 1) return SLATE_E_LZ4_CORRUPT;  // no dictionaries are configured
   const bool indep = (h.flg >> 5) & 1, bcheck = (h.flg >> 4) & 1, ccheck = (h.flg >> 2) & 1, csize = (h.flg >> 3) & 1;
   uint32_t pos = 4 + h.hl + 1, d = 0;
@@ -383,7 +384,7 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
     if (bs == 0) break;
     const uint32_t sz = bs & 0x7FFFFFFFu;
     if (sz > h.bmax || n - pos < sz + (bcheck ? 4u : 0u)) return SLATE_E_LZ4_CORRUPT;
-    if (bcheck && wave_xxh32(base, off + pos, sz, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos + sz)))
+    if (out && bcheck && wave_xxh32(base, off + pos, sz, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos + sz)))
       return SLATE_E_LZ4_BLOCK_CHECKSUM;
     const uint8_t* src = in + pos;
     // sequence headers are read through a 64-byte window held one byte per lane
@@ -399,7 +400,8 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
     };
     if (bs >> 31) {  // stored block
       if (sz > cap - d) return SLATE_E_LZ4_CORRUPT;
-      for (uint32_t j = lane; j < sz; j += kWave) out[d + j] = src[j];
+      if (out)
+        for (uint32_t j = lane; j < sz; j += kWave) out[d + j] = src[j];
       d += sz;
     } else {
       const uint32_t d0 = d, lo = indep ? d : 0u;
@@ -419,7 +421,8 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
           } while (b == 255);
         }
         if (ll > sz - s || ll > h.bmax - (d - d0) || ll > cap - d) return SLATE_E_LZ4_CORRUPT;
-        for (uint32_t j = lane; j < ll; j += kWave) out[d + j] = src[s + j];
+        if (out)
+          for (uint32_t j = lane; j < ll; j += kWave) out[d + j] = src[s + j];
         s += ll;
         d += ll;
         if (s == sz) break;  // the last sequence has literals only
@@ -440,7 +443,8 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
         ml += 4;
         if (ml > h.bmax - (d - d0) || ml > cap - d) return SLATE_E_LZ4_CORRUPT;
         // byte j repeats the mo-byte pattern (overlapping copies); every read is below d
-        if (mo >= ml) {  // wave-uniform: no overlap, no modulo
+        if (!out) {
+        } else if (mo >= ml) {  // wave-uniform: no overlap, no modulo
           if (uint32_t(lane) < ml) out[d + lane] = out[d - mo + lane];
           for (uint32_t j = lane + kWave; j < ml; j += kWave) out[d + j] = out[d - mo + j];
         } else {
@@ -455,7 +459,7 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
   if (ccheck) {
     if (n - pos < 4) return SLATE_E_LZ4_CORRUPT;
     __builtin_amdgcn_wave_barrier();
-    if (wave_xxh32(out, 0, d, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos)))
+    if (out && wave_xxh32(out, 0, d, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos)))
       return SLATE_E_LZ4_FRAME_CHECKSUM;
     pos += 4;
   }
@@ -829,12 +833,22 @@ __device__ inline void write_meta(slate_block_meta* m, const slate_block_meta& v
 // Returns false when the block does not fit this wave's LDS budget (caller defers it).
 // CK: the codec class compiled in (0: None/Snappy/LZ4, 1: Zlib, 2: Zstd), so each kernel
 // instance carries only its codec's registers.
-template <int CK>
-__device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBufs& w, int lane, bool defer_large) {
+// G (decode_payload_kernel): no LDS staging; the decoders read the encoded bytes and write
+// the decoded ones in HBM (the lanes of one wave see each other's global stores in program
+// order, so the copies read back what earlier lanes wrote), for payloads of any size.
+// a.raw: the payload is an index or filter buffer, not a block: CRC + decompress only.
+template <int CK, bool G = false>
+__device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBufs& w0, int lane, bool defer_large) {
   slate_block_meta m{};
   uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
   const uint8_t* gin = a.in + s0;
-  if (len < 6) {
+  WaveBufs w = w0;
+  if (G) {
+    w.in = const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(gin) & ~uintptr_t(15)));
+    w.out = a.out + a.out_off[b];
+    w.in_cap = w.out_cap = 0xFFFFFFFFu;
+  }
+  if (len < (a.raw ? 4u : 6u)) {
     m.status = SLATE_E_BLOCK_TOO_SMALL;
     write_meta(&a.meta[b], m, lane);
     return true;
@@ -846,14 +860,14 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
                          ? (dl = a.out_off[b + 1] - a.out_off[b], true)
                          : decoded_len(a.codec, gin, len, &dl, &hdr);
   uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
-  if (shift + len > w.in_cap || (a.codec != SLATE_CODEC_NONE && dl > w.out_cap)) {
+  if (len > 0xFFFFFF00ull || shift + len > w.in_cap || (a.codec != SLATE_CODEC_NONE && dl > w.out_cap)) {
     if (defer_large) return false;
     m.status = SLATE_E_CAPACITY;  // beyond the large kernel's LDS budget
     write_meta(&a.meta[b], m, lane);
     return true;
   }
   // ---- stage the encoded block into LDS with aligned 16-byte loads
-  {
+  if (!G) {
     const uint4* src = reinterpret_cast<const uint4*>(gin - shift);
     uint4* dst = reinterpret_cast<uint4*>(w.in);
     uint32_t chunks = uint32_t((shift + len + 15) / 16);
@@ -868,6 +882,27 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     m.status = SLATE_E_BLOCK_CHECKSUM;
     write_meta(&a.meta[b], m, lane);
     return true;
+  }
+  // ---- an index / filter (DecodeIndex, ReadFilter): compress.Decode after the oracle's
+  // or_decompress_len, whose status comes first and whose size is the capacity
+  if (G && a.raw && (a.codec == SLATE_CODEC_LZ4 || a.codec == SLATE_CODEC_ZLIB || a.codec == SLATE_CODEC_ZSTD)) {
+    uint32_t pl = 0;
+    int pst = SLATE_OK;
+    if (CK == 0 && a.codec == SLATE_CODEC_LZ4) {
+      pst = wave_lz4_decode(w.in, shift, clen, nullptr, 0xFFFFFFFFu, lane, &pl);
+    } else if (CK == 1 && a.codec == SLATE_CODEC_ZLIB) {
+      pst = wave_inflate(w.in + shift, clen, nullptr, 0xFFFFFFFFu, w.zs, w.zfix, w.zfix + 1, lane, &pl);
+    } else if (CK == 2 && a.codec == SLATE_CODEC_ZSTD) {
+      const uint64_t z = wave_zstd_plan(w.in, int32_t(shift), clen, w.zss, w.zsh, lane);
+      if (z > a.out_off[b + 1] - a.out_off[b]) pst = SLATE_E_CAPACITY;  // cannot happen: the host planned with it
+      pl = uint32_t(z);
+    }
+    if (pst != SLATE_OK) {
+      m.status = int16_t(pst);
+      write_meta(&a.meta[b], m, lane);
+      return true;
+    }
+    dl = pl;
   }
   // ---- decompress (compress.Decode, compression.go:126-157)
   const uint8_t* buf;  // decoded buffer in LDS
@@ -930,7 +965,10 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   }
   __builtin_amdgcn_wave_barrier();
   // ---- write the decoded buffer back (16-aligned destination)
-  if (!(dbg_bits(a) & 8)) {
+  if (G) {
+    if (buf != w.out)
+      for (uint32_t c = lane; c < n; c += kWave) w.out[c] = buf[c];
+  } else if (!(dbg_bits(a) & 8)) {
     uint8_t* gout = a.out + a.out_off[b];
     uint32_t chunks = (n + 15) / 16;
     if (buf == w.out) {
@@ -948,6 +986,11 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
         reinterpret_cast<uint4*>(gout)[c] = v;
       }
     }
+  }
+  if (a.raw) {  // an index / filter payload: decoded length only
+    m.data_len = n;
+    write_meta(&a.meta[b], m, lane);
+    return true;
   }
   // ---- block.Decode structure checks (block.go:95-131)
   if (n < 2) {
@@ -1086,6 +1129,20 @@ __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) decode_block_wave<CK>(a, a.large_list[k], w, lane, false);
 }
 
+// Index / filter payloads of any size (LZ4 / Zlib / Zstd; raw mode): one wave per payload,
+// input and output in HBM (decode_block_wave<CK, true>), LDS for the CRC and codec tables only.
+template <int CK>
+__global__ __launch_bounds__(64) void decode_payload_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63;
+  WaveBufs w{tab, nullptr, nullptr, 0u, 0u};
+  if (CK == 1) zlib_lds(w, smem + kTabBytes, 1, 0, lane);
+  if (CK == 2) zstd_lds(w, smem + kTabBytes, 0, lane);
+  for (uint32_t b = blockIdx.x; b < a.n; b += gridDim.x) decode_block_wave<CK, true>(a, b, w, lane, false);
+}
+
 // --------------------------------------------------------------- launchers
 hipError_t decode_kernels_available() {
   hipFuncAttributes attr;
@@ -1137,6 +1194,22 @@ hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t m, void* scratc
   scan_reduce_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
   scan_partials_kernel<<<1, kScanThreads, 0, st>>>(pa, pb, tiles);
   scan_apply_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_payload(hipStream_t st, const DecodeArgs& args_in, int num_cus) {
+  DecodeArgs a = args_in;
+  a.debug = 0;
+  a.raw = 1;
+  if (a.n == 0) return hipGetLastError();
+  const uint32_t grid = min(a.n, uint32_t(num_cus) * 4u);
+  if (a.codec == SLATE_CODEC_ZLIB) {
+    decode_payload_kernel<1><<<grid, 64, kTabBytes + kZFixed + kZScratch, st>>>(a);
+  } else if (a.codec == SLATE_CODEC_ZSTD) {
+    decode_payload_kernel<2><<<grid, 64, kTabBytes + kZsShared + kZsScratch, st>>>(a);
+  } else {
+    decode_payload_kernel<0><<<grid, 64, kTabBytes, st>>>(a);
+  }
   return hipGetLastError();
 }
 

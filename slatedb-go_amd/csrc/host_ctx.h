@@ -134,6 +134,10 @@ inline int hip_status(hipError_t e) {
 inline hipError_t ctx_bind(slate_ctx* ctx) { return hipSetDevice(ctx->device); }
 
 // CRC32-IEEE of a host buffer computed on the context's GPU (stream-synchronous).
+// compress.Decode of one `payload || BE32 CRC` buffer (an index or filter) on the GPU, CRC
+// first: *bstatus = SLATE_OK, SLATE_E_BLOCK_CHECKSUM or the codec's status (api_sst.cpp).
+int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
+                              int* bstatus);
 int ctx_crc32_host_buffer(slate_ctx* ctx, const uint8_t* data, size_t n, uint32_t* crc);
 // CRC32-IEEE of a device buffer (stream-synchronous, result to host).
 int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* crc);

@@ -67,6 +67,9 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
+// Index / filter payloads (`payload || BE32 CRC`) of any size for LZ4 / Zlib / Zstd (raw mode;
+// out_off from launch_decode_plan): meta[i].status, meta[i].data_len = decoded length.
+hipError_t launch_decode_payload(hipStream_t st, const DecodeArgs& a, int num_cus);
 // ---------------------------------------------------------------- merge (merge.hip)
 // iter.MergeSort over k concatenated sorted iterators (h_src_start: k+1 host element indices).
 // out_idx[0..*n_out) = element indices in return order; *d_flags bit 0 = some iterator unsorted.
