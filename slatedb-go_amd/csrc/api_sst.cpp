@@ -147,13 +147,15 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
       *bstatus = SLATE_E_BLOCK_CHECKSUM;
       return SLATE_OK;
     }
-    SLATE_HIP(ctx->d_in.ensure(len + 16));
+    SLATE_HIP(ctx->d_in.ensure(len + 64));
     SLATE_HIP(ctx->d_out.ensure(align16(dl) + 32));
-    SLATE_HIP(ctx->d_scratch.ensure(128));
+    SLATE_HIP(ctx->d_scratch.ensure(256 + snappy_par_scratch_bytes(uint32_t(clen), uint32_t(dl))));
     int32_t* d_st = ctx->d_scratch.as<int32_t>();
     SLATE_HIP(hipMemcpyAsync(ctx->d_in.p, buf, clen, hipMemcpyHostToDevice, st));
-    SLATE_HIP(launch_snappy_stream(st, ctx->d_in.as<uint8_t>(), uint32_t(clen), hdr_len, ctx->d_out.as<uint8_t>(),
-                                   uint32_t(dl), d_st));
+    // the tag-parallel decoder; the serial streaming decoder runs instead (on the device, same
+    // launch sequence) when the stream fails one of its checks
+    SLATE_HIP(launch_snappy_decode_par(st, ctx->d_in.as<uint8_t>(), uint32_t(clen), hdr_len, ctx->d_out.as<uint8_t>(),
+                                       uint32_t(dl), ctx->d_scratch.as<uint8_t>() + 256, d_st));
     int32_t h_st = 0;
     SLATE_HIP(hipMemcpyAsync(&h_st, d_st, 4, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));

@@ -99,6 +99,12 @@ hipError_t launch_gather_copy(hipStream_t st, const uint32_t* idx, uint64_t n, c
 // SLATE_E_SNAPPY_CORRUPT.  hdr = varint header bytes, dn = decoded length from the header.
 hipError_t launch_snappy_stream(hipStream_t st, const uint8_t* in, uint32_t sn, uint32_t hdr, uint8_t* out,
                                 uint32_t dn, int32_t* status);
+// The same result through the tag-parallel path (snappy_stream.hip: chain strides, per-byte
+// pointer doubling), falling back to launch_snappy_stream's kernel on the device for a stream
+// that fails a check (so errors and their order are always the serial decoder's).
+size_t snappy_par_scratch_bytes(uint32_t sn, uint32_t dn);
+hipError_t launch_snappy_decode_par(hipStream_t st, const uint8_t* in, uint32_t sn, uint32_t hdr, uint8_t* out,
+                                    uint32_t dn, void* scratch, int32_t* status);
 
 // Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,

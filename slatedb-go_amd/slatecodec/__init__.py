@@ -333,6 +333,14 @@ class Context:
     def bloom_decode(self, buf: bytes, codec: int) -> tuple[int, int, bytes]:
         b = np.frombuffer(bytes(buf) or b"\0", dtype=np.uint8)
         cap = len(buf) + 64
+        if codec == SNAPPY:  # the decoded length is the payload's varint header
+            x, sh = 0, 0
+            for byte in bytes(buf[:10]):
+                x |= (byte & 0x7F) << sh
+                sh += 7
+                if byte < 0x80:
+                    break
+            cap = max(cap, min(x, 1 << 32) + 64)
         out = np.zeros(cap, np.uint8)
         npr = C.c_uint16()
         bl = C.c_size_t()

@@ -130,3 +130,38 @@ def test_large_index(ctx):
     bad = bytearray(ib)
     bad[len(bad) // 3] ^= 0x40
     assert ctx.decode_index(bytes(bad), sc.SNAPPY)[0] == ob.decode_index(bytes(bad), ob.SNAPPY)[0]
+
+
+@pytest.mark.parametrize("n", [65_536 * 2, 65_536 * 3 + 1, 65_536 * 5 - 7, 3_000_000])
+def test_golang_framed_sizes(ctx, n):
+    """golang/snappy-framed payloads (the tag-parallel path)
+    at and around fragment multiples, mixing literals, near copies and runs."""
+    rng = random.Random(n)
+    parts, size = [], 0
+    while size < n:
+        k = rng.random()
+        part = rng.randbytes(rng.randint(1, 3000)) if k < 0.4 else (
+            bytes([rng.randrange(256)]) * rng.randint(1, 5000) if k < 0.6 else
+            (parts[rng.randrange(len(parts))][:rng.randint(1, 2000)] if parts else b"x"))
+        parts.append(part)
+        size += len(part)
+    raw = (b"\x00\x06" + b"".join(parts))[:n]
+    _check(ctx, _filter_buf(ob.snappy_encode(raw)))
+
+
+def test_fragment_boundary_streams(ctx):
+    """Valid streams not split golang's way (copies across 64 KiB pieces, a literal across one): a copy
+    at a 64 KiB boundary reaching into the previous fragment, and a literal across a boundary."""
+    rng = random.Random(11)
+    a = b"\x00\x06" + rng.randbytes(65_534)
+    s1 = _lit(a[:60_000]) + _lit(a[60_000:]) + _copy4(1000, 64) + _lit(rng.randbytes(5000))
+    _check(ctx, _filter_buf(_varint(65_536 + 64 + 5000) + s1))
+    s2 = _lit(a[:30_000]) + _lit(a[30_000:] + rng.randbytes(40_000)) + _copy4(7, 20)
+    _check(ctx, _filter_buf(_varint(65_536 + 40_000 + 20) + s2))
+    # damage inside the third fragment of a golang-framed stream
+    raw = b"\x00\x06" + b"".join(rng.randbytes(300) * 3 for _ in range(300))
+    enc = bytearray(ob.snappy_encode(raw))
+    for pos in (len(enc) * 2 // 3, len(enc) - 10):
+        bad = bytearray(enc)
+        bad[pos] ^= 0x3C
+        _check(ctx, _filter_buf(bytes(bad)))
