@@ -7,6 +7,8 @@
 // decoded in chunks through page-locked staging on two stream lanes per context, and a batch
 // spread over G contexts sends block i to context i mod G with no collective.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -22,14 +24,16 @@ constexpr uint32_t kChunkBlocks = 65536;
 constexpr uint64_t kChunkBytes = 96ull << 20;
 
 // memcpy split over threads for large copies between caller memory and page-locked staging
-// (one core copies ~10 GB/s, below what the PCIe link moves).
+// (one core copies ~10 GB/s, below what the PCIe link moves).  16 threads: the CPU share one
+// GPU's process gets on the MI355X boxes.
+constexpr size_t kCopyThreads = 16;
 void par_memcpy(void* dst, const void* src, size_t n) {
-  constexpr size_t kPiece = 8u << 20;
+  constexpr size_t kPiece = 4u << 20;
   if (n < 2 * kPiece) {
     if (n) memcpy(dst, src, n);
     return;
   }
-  const size_t t = std::min<size_t>(8, n / kPiece);
+  const size_t t = std::min<size_t>(kCopyThreads, n / kPiece);
   const size_t step = (n + t - 1) / t;
   std::vector<std::thread> th;
   for (size_t i = 1; i < t; i++) {
@@ -68,39 +72,115 @@ struct Sink {
   const uint64_t* g_row_base = nullptr;
 };
 
-// The lane's chunk is decoded: copy its outputs into the sink.
+// SLATE_HOST_TRACE=1: per-chunk host phase times on stderr (diagnostics for DESIGN.md's
+// host pipeline numbers; read once per process)
+static bool host_trace() {
+  static const bool on = [] {
+    const char* e = getenv("SLATE_HOST_TRACE");
+    return e && *e == '1';
+  }();
+  return on;
+}
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// plan_sizes_kernel's decoded length for CodecNone / CodecSnappy on the host (decode.hip
+// decoded_len: the payload length, or golang/snappy decodedLen's varint header with the same
+// rejections), so that a chunk's place in the outputs needs no GPU round trip.
+bool host_plannable(int codec) { return codec == SLATE_CODEC_NONE || codec == SLATE_CODEC_SNAPPY; }
+uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len) {
+  if (len < 6) return 0;
+  const uint64_t clen = len - 4;
+  if (codec == SLATE_CODEC_NONE) return clen;
+  uint64_t x = 0;
+  uint32_t sh = 0;
+  for (uint64_t i = 0; i < clen; i++) {
+    if (i == 10) return 0;
+    const uint32_t b = p[i];
+    if (b < 0x80) {
+      if (i == 9 && b > 1) return 0;
+      x |= uint64_t(b) << sh;
+      if (x > 0xffffffffull || x > kSnappyMaxExpansion * clen) return 0;
+      return x;
+    }
+    x |= uint64_t(b & 0x7f) << sh;
+    sh += 7;
+  }
+  return 0;
+}
+
+// Run fn(lo, hi) over [0, n) split across up to kCopyThreads threads (pieces of >= grain).
+template <typename F>
+void par_for(size_t n, size_t grain, F fn) {
+  const size_t t = std::max<size_t>(1, std::min<size_t>(kCopyThreads, n / std::max<size_t>(grain, 1)));
+  if (t == 1) {
+    fn(size_t(0), n);
+    return;
+  }
+  const size_t step = (n + t - 1) / t;
+  std::vector<std::thread> th;
+  for (size_t k = 1; k < t; k++) {
+    const size_t a = k * step, b = std::min(n, a + step);
+    if (a < b) th.emplace_back(fn, a, b);
+  }
+  fn(size_t(0), std::min(n, step));
+  for (auto& x : th) x.join();
+}
+
+// The lane's chunk is decoded: copy its outputs into the sink.  Its rows arrive densely (the
+// rows of decoded blocks only, rows_pack): block j's come from the running count of the meta's.
 int lane_finish(PipeLane& L, Sink& o) {
   if (!L.busy) return SLATE_OK;
   L.busy = false;
+  const double t0 = host_trace() ? now_ms() : 0.0;
   SLATE_HIP(hipEventSynchronize(L.done));
+  if (host_trace()) fprintf(stderr, "[slate host]   wait decode+D2H %.2f ms\n", now_ms() - t0);
   if (!L.decoded) return SLATE_OK;
   const uint8_t* hout = L.h_out.as<uint8_t>();
   const slate_row* hrows = L.h_rows.as<slate_row>();
   const slate_block_meta* hmeta = L.h_meta.as<slate_block_meta>();
+  std::vector<uint64_t> doff(size_t(L.n) + 1, 0);
+  for (uint32_t k = 0; k < L.n; k++) {
+    const uint32_t j = L.b0 + k;
+    const uint64_t cap = o.row_base[j + 1] - o.row_base[j];
+    doff[k + 1] = doff[k] + (hmeta[k].status == SLATE_OK ? std::min<uint64_t>(hmeta[k].n_rows, cap) : 0);
+  }
   if (o.G) {
-    for (uint32_t k = 0; k < L.n; k++) {
-      const uint32_t j = L.b0 + k;
-      const uint64_t i = uint64_t(o.g) + uint64_t(j) * o.G;
-      const uint64_t ob = o.out_off[j + 1] - o.out_off[j], rb = o.row_base[j + 1] - o.row_base[j];
-      if (ob) memcpy(o.out + o.g_out_off[i], hout + (o.out_off[j] - L.out_base), ob);
-      if (rb) memcpy(o.rows + o.g_row_base[i], hrows + (o.row_base[j] - L.row_base), rb * sizeof(slate_row));
-      o.meta[i] = hmeta[k];
-    }
+    par_for(L.n, 2048, [&](size_t a, size_t b) {
+      for (size_t k = a; k < b; k++) {
+        const uint32_t j = L.b0 + uint32_t(k);
+        const uint64_t i = uint64_t(o.g) + uint64_t(j) * o.G;
+        const uint64_t ob = o.out_off[j + 1] - o.out_off[j], rb = doff[k + 1] - doff[k];
+        if (ob) memcpy(o.out + o.g_out_off[i], hout + (o.out_off[j] - L.out_base), ob);
+        if (rb) memcpy(o.rows + o.g_row_base[i], hrows + doff[k], rb * sizeof(slate_row));
+        o.meta[i] = hmeta[k];
+      }
+    });
     return SLATE_OK;
   }
   par_memcpy(o.out + L.out_base, hout, L.out_total);
   memcpy(o.meta + L.b0, hmeta, size_t(L.n) * sizeof(slate_block_meta));
-  par_memcpy(o.rows + L.row_base, hrows, L.rows_total * sizeof(slate_row));
+  par_for(L.n, 2048, [&](size_t a, size_t b) {
+    for (size_t k = a; k < b; k++) {
+      const uint64_t rb = doff[k + 1] - doff[k];
+      if (rb) memcpy(o.rows + o.row_base[L.b0 + k], hrows + doff[k], rb * sizeof(slate_row));
+    }
+  });
   return SLATE_OK;
 }
 
 // Decode n host blocks: chunks of up to kChunkBlocks / kChunkBytes alternate between the two
-// lanes.  Per chunk: staging copy, H2D, plan, (wait for the plan: the chunk's place in the
-// outputs), decode, D2H into staging; the previous chunk's staging is copied out meanwhile.
+// lanes.  Per chunk k: staging copy in, H2D and plan, chunk k's place in the outputs (computed
+// on the host for None / Snappy, else the plan read back), decode and D2H enqueued, and only
+// then chunk k-1 waited for and copied out of its staging -- so the copy engine always has the
+// next chunk queued and the host thread spends its time copying.
 // out_off/row_base are always filled; when the outputs do not fit (or are absent) the
 // remaining chunks are only planned and SLATE_E_CAPACITY is returned.
 int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o) {
   SLATE_HIP(ctx_bind(ctx));
+  const bool trace = host_trace();
+  const double t_start = trace ? now_ms() : 0.0;
   // chunk size in blocks; SLATE_PIPE_CHUNK_BLOCKS lowers it so tests cover many chunks cheaply
   static const uint32_t chunk_blocks = [] {
     const char* e = getenv("SLATE_PIPE_CHUNK_BLOCKS");
@@ -121,9 +201,10 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
     const uint64_t lo = in_off[b], bytes = in_off[e] - lo;
     if (in_off[e] < lo) return SLATE_E_INVALID_ARG;
     PipeLane& L = ctx->lanes[li];
+    PipeLane& prev = ctx->lanes[(li + kPipeLanes - 1) % kPipeLanes];
     li = (li + 1) % kPipeLanes;
     SLATE_HIP(lane_init(L));
-    int st = lane_finish(L, o);
+    int st = lane_finish(L, o);  // normally finished already (two chunks ago, below)
     if (st) return st;
     SLATE_HIP(L.h_in.ensure(bytes + 16));
     SLATE_HIP(L.h_in_off.ensure((size_t(m) + 1) * 8));
@@ -133,7 +214,9 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
     SLATE_HIP(L.d_out_off.ensure((size_t(m) + 1) * 8));
     SLATE_HIP(L.d_row_base.ensure((size_t(m) + 1) * 8));
     SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes(m) + 64));
+    const double t0 = trace ? now_ms() : 0.0;
     par_memcpy(L.h_in.p, in + lo, bytes);
+    const double t1 = trace ? now_ms() : 0.0;
     uint64_t* ho = L.h_in_off.as<uint64_t>();
     for (uint32_t i = 0; i <= m; i++) ho[i] = in_off[b + i] - lo;
     hipStream_t s = L.stream;
@@ -143,10 +226,27 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
                                  L.d_out_off.as<uint64_t>(), L.d_row_base.as<uint64_t>(), L.d_scratch.p));
     uint64_t* po = L.h_plan.as<uint64_t>();
     uint64_t* pr = po + m + 1;
-    SLATE_HIP(hipMemcpyAsync(po, L.d_out_off.p, (size_t(m) + 1) * 8, hipMemcpyDeviceToHost, s));
-    SLATE_HIP(hipMemcpyAsync(pr, L.d_row_base.p, (size_t(m) + 1) * 8, hipMemcpyDeviceToHost, s));
-    SLATE_HIP(hipEventRecord(L.planned, s));
-    SLATE_HIP(hipEventSynchronize(L.planned));
+    if (host_plannable(codec)) {
+      // the same sizes as the plan kernels, computed here: no wait for the GPU
+      po[0] = pr[0] = 0;
+      par_for(m, 4096, [&](size_t a, size_t e2) {
+        for (size_t i = a; i < e2; i++) {
+          const uint64_t dl = host_decoded_len(codec, in + in_off[b + i], in_off[b + i + 1] - in_off[b + i]);
+          po[i + 1] = align16(dl);
+          pr[i + 1] = row_capacity(dl);
+        }
+      });
+      for (uint32_t i = 0; i < m; i++) {
+        po[i + 1] += po[i];
+        pr[i + 1] += pr[i];
+      }
+    } else {
+      SLATE_HIP(hipMemcpyAsync(po, L.d_out_off.p, (size_t(m) + 1) * 8, hipMemcpyDeviceToHost, s));
+      SLATE_HIP(hipMemcpyAsync(pr, L.d_row_base.p, (size_t(m) + 1) * 8, hipMemcpyDeviceToHost, s));
+      SLATE_HIP(hipEventRecord(L.planned, s));
+      SLATE_HIP(hipEventSynchronize(L.planned));
+    }
+    const double t2 = trace ? now_ms() : 0.0;
     for (uint32_t i = 1; i <= m; i++) {
       out_off[b + i] = out_acc + po[i];
       row_base[b + i] = rows_acc + pr[i];
@@ -175,19 +275,34 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
                    L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
                    L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
       SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
+      // the rows, densely, written by the GPU straight into the page-locked staging
+      SLATE_HIP(L.d_dense.ensure((size_t(m) + 1) * 8 + rows_pack_scratch_bytes(m)));
+      void* hrows_dev = nullptr;
+      SLATE_HIP(hipHostGetDevicePointer(&hrows_dev, L.h_rows.p, 0));
+      SLATE_HIP(launch_rows_pack(s, L.d_meta.as<slate_block_meta>(), L.d_row_base.as<uint64_t>(), m,
+                                 L.d_rows.as<slate_row>(), L.d_dense.as<uint64_t>(),
+                                 L.d_dense.as<uint8_t>() + (size_t(m) + 1) * 8, static_cast<slate_row*>(hrows_dev)));
       if (L.out_total) SLATE_HIP(hipMemcpyAsync(L.h_out.p, L.d_out.p, L.out_total, hipMemcpyDeviceToHost, s));
       SLATE_HIP(hipMemcpyAsync(L.h_meta.p, L.d_meta.p, size_t(m) * sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
-      if (L.rows_total)
-        SLATE_HIP(hipMemcpyAsync(L.h_rows.p, L.d_rows.p, L.rows_total * sizeof(slate_row), hipMemcpyDeviceToHost, s));
       L.decoded = true;
     }
     SLATE_HIP(hipEventRecord(L.done, s));
+    // chunk k-1 out of its staging while chunk k decodes: the D2H engine has chunk k queued
+    // behind chunk k-1, and the lane chunk k+1 takes is free by then
+    if (&prev != &L) {
+      st = lane_finish(prev, o);
+      if (st) return st;
+    }
+    if (trace)
+      fprintf(stderr, "[slate host] chunk %u blocks %u in %.1f MB: copy-in %.2f ms, plan %.2f ms, prev out %.2f ms\n",
+              b, m, bytes / 1e6, t1 - t0, t2 - t1, now_ms() - t2);
     b = e;
   }
   for (PipeLane& L : ctx->lanes) {
     int st = lane_finish(L, o);
     if (st) return st;
   }
+  if (trace) fprintf(stderr, "[slate host] %u blocks: %.2f ms\n", n, now_ms() - t_start);
   return fits ? SLATE_OK : SLATE_E_CAPACITY;
 }
 

@@ -1197,6 +1197,44 @@ hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t m, void* scratc
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------- dense rows (host transfers)
+__global__ void rows_count_kernel(const slate_block_meta* __restrict__ meta, const uint64_t* __restrict__ row_base,
+                                  uint32_t n, uint64_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {
+    cnt[n] = 0;
+    return;
+  }
+  const uint64_t cap = row_base[i + 1] - row_base[i];
+  cnt[i] = meta[i].status == SLATE_OK ? min(uint64_t(meta[i].n_rows), cap) : 0;
+}
+
+// one wave per block: its rows as 16-byte stores, consecutive lanes consecutive rows
+__global__ __launch_bounds__(256) void rows_pack_kernel(const uint64_t* __restrict__ row_base, uint32_t n,
+                                                        const slate_row* __restrict__ rows,
+                                                        const uint64_t* __restrict__ dense_off,
+                                                        slate_row* __restrict__ dense) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {
+    const uint64_t d0 = dense_off[i], c = dense_off[i + 1] - d0, r0 = row_base[i];
+    for (uint64_t r = lane; r < c; r += 64)
+      reinterpret_cast<uint4*>(dense)[d0 + r] = reinterpret_cast<const uint4*>(rows)[r0 + r];
+  }
+}
+
+size_t rows_pack_scratch_bytes(uint32_t n) { return scan_scratch_bytes(n + 1) + 64; }
+
+hipError_t launch_rows_pack(hipStream_t st, const slate_block_meta* meta, const uint64_t* row_base, uint32_t n,
+                            const slate_row* rows, uint64_t* dense_off, void* scratch, slate_row* dense) {
+  if (n == 0) return hipSuccess;
+  rows_count_kernel<<<(n + 256) / 256, 256, 0, st>>>(meta, row_base, n, dense_off);
+  hipError_t e = launch_scan_u64(st, dense_off, n + 1, scratch);
+  if (e != hipSuccess) return e;
+  rows_pack_kernel<<<min((n + 3) / 4, 8192u), 256, 0, st>>>(row_base, n, rows, dense_off, dense);
+  return hipGetLastError();
+}
+
 hipError_t launch_decode_payload(hipStream_t st, const DecodeArgs& args_in, int num_cus) {
   DecodeArgs a = args_in;
   a.debug = 0;

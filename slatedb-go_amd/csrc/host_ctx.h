@@ -77,14 +77,15 @@ struct PinBuf {
 struct PipeLane {
   hipStream_t stream = nullptr;
   hipEvent_t planned = nullptr, done = nullptr;
-  DevBuf d_in, d_in_off, d_out_off, d_row_base, d_scratch, d_out, d_meta, d_rows;
-  PinBuf h_in, h_in_off, h_plan, h_out, h_meta, h_rows;
+  DevBuf d_in, d_in_off, d_out_off, d_row_base, d_scratch, d_out, d_meta, d_rows, d_dense;
+  PinBuf h_in, h_in_off, h_plan, h_out, h_meta, h_rows;  // h_rows: the chunk's rows, dense (rows_pack)
   // the chunk in flight: blocks [b0, b0+n), its place in the caller's outputs
   uint32_t b0 = 0, n = 0;
   uint64_t out_base = 0, row_base = 0, out_total = 0, rows_total = 0;
   bool busy = false, decoded = false;
   void release() {
-    for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows}) b->release();
+    for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows, &d_dense})
+      b->release();
     for (PinBuf* b : {&h_in, &h_in_off, &h_plan, &h_out, &h_meta, &h_rows}) b->release();
     if (planned) (void)hipEventDestroy(planned);
     if (done) (void)hipEventDestroy(done);
@@ -133,11 +134,11 @@ inline int hip_status(hipError_t e) {
 
 inline hipError_t ctx_bind(slate_ctx* ctx) { return hipSetDevice(ctx->device); }
 
-// CRC32-IEEE of a host buffer computed on the context's GPU (stream-synchronous).
 // compress.Decode of one `payload || BE32 CRC` buffer (an index or filter) on the GPU, CRC
 // first: *bstatus = SLATE_OK, SLATE_E_BLOCK_CHECKSUM or the codec's status (api_sst.cpp).
 int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
                               int* bstatus);
+// CRC32-IEEE of a host buffer computed on the context's GPU (stream-synchronous).
 int ctx_crc32_host_buffer(slate_ctx* ctx, const uint8_t* data, size_t n, uint32_t* crc);
 // CRC32-IEEE of a device buffer (stream-synchronous, result to host).
 int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* crc);

@@ -67,6 +67,14 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
+// The rows of a decoded batch, densely in block order, written to `dense` (device memory or
+// page-locked host memory mapped for the device): block i's min(n_rows, capacity) rows when it
+// decoded (status OK), none otherwise; dense_off (n+1 u64) gets the exclusive scan of those
+// counts.  For host transfers: the plan's row capacity is an upper bound several times the rows
+// a block holds.  scratch: rows_pack_scratch_bytes(n).
+size_t rows_pack_scratch_bytes(uint32_t n);
+hipError_t launch_rows_pack(hipStream_t st, const slate_block_meta* meta, const uint64_t* row_base, uint32_t n,
+                            const slate_row* rows, uint64_t* dense_off, void* scratch, slate_row* dense);
 // Index / filter payloads (`payload || BE32 CRC`) of any size for LZ4 / Zlib / Zstd (raw mode;
 // out_off from launch_decode_plan): meta[i].status, meta[i].data_len = decoded length.
 hipError_t launch_decode_payload(hipStream_t st, const DecodeArgs& a, int num_cus);
