@@ -288,6 +288,12 @@ int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const
 /* NextBlock (builder.go:185): *present = 0 when no finished block is queued.
  * The block is copied into out (capacity out_cap); *len receives its size
  * (also when it does not fit, with SLATE_E_CAPACITY). */
+/* The same as slate_sst_builder_add_batch for KVs already in device memory of the builder's
+ * context (compaction's merged output, slatedb/compaction/executor.go:100-146 writing through
+ * table_store.go:221-266): device pointers; d_is_tomb may be NULL (empty value = tombstone). */
+int slate_sst_builder_add_batch_device(slate_sst_builder* b, const uint8_t* d_keys, const uint64_t* d_key_off,
+                                       const uint8_t* d_values, const uint64_t* d_value_off,
+                                       const uint8_t* d_is_tomb, uint64_t n);
 int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_cap, size_t* len,
                                  int* present);
 /* Build (builder.go:215): consumes the builder's pending KVs; the table owns the

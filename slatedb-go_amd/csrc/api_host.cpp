@@ -18,15 +18,9 @@
 
 using namespace slate;
 
-namespace {
-
-constexpr uint32_t kChunkBlocks = 65536;
-constexpr uint64_t kChunkBytes = 96ull << 20;
-
 // memcpy split over threads for large copies between caller memory and page-locked staging
 // (one core copies ~10 GB/s, below what the PCIe link moves).  16 threads: the CPU share one
 // GPU's process gets on the MI355X boxes.
-constexpr size_t kCopyThreads = 16;
 void par_memcpy(void* dst, const void* src, size_t n) {
   constexpr size_t kPiece = 4u << 20;
   if (n < 2 * kPiece) {
@@ -54,6 +48,69 @@ hipError_t lane_init(PipeLane& L) {
   if (e != hipSuccess) return e;
   return hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
 }
+
+// ctx_h2d / ctx_d2h: 64 MiB pieces through the two lanes' page-locked input staging; the host
+// copy of piece i overlaps the DMA of piece i-1.
+constexpr size_t kXferPiece = 64u << 20;
+constexpr size_t kXferDirect = 8u << 20;
+
+int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st) {
+  if (n == 0) return SLATE_OK;
+  if (n <= kXferDirect) {
+    SLATE_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    return SLATE_OK;
+  }
+  bool used[kPipeLanes] = {};
+  size_t k = 0;
+  for (size_t o = 0; o < n; o += kXferPiece, k++) {
+    PipeLane& L = ctx->lanes[k % kPipeLanes];
+    SLATE_HIP(lane_init(L));
+    if (used[k % kPipeLanes]) SLATE_HIP(hipEventSynchronize(L.planned));  // its previous piece has left
+    const size_t len = std::min(kXferPiece, n - o);
+    SLATE_HIP(L.h_in.ensure(kXferPiece));
+    par_memcpy(L.h_in.p, static_cast<const uint8_t*>(src) + o, len);
+    SLATE_HIP(hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, L.h_in.p, len, hipMemcpyHostToDevice, st));
+    SLATE_HIP(hipEventRecord(L.planned, st));
+    used[k % kPipeLanes] = true;
+  }
+  SLATE_HIP(hipStreamSynchronize(st));
+  return SLATE_OK;
+}
+
+int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st) {
+  if (n == 0) return SLATE_OK;
+  if (n <= kXferDirect) {
+    SLATE_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    return SLATE_OK;
+  }
+  const size_t pieces = (n + kXferPiece - 1) / kXferPiece;
+  auto issue = [&](size_t k) -> hipError_t {
+    PipeLane& L = ctx->lanes[k % kPipeLanes];
+    hipError_t e = lane_init(L);
+    if (e == hipSuccess) e = L.h_in.ensure(kXferPiece);
+    const size_t o = k * kXferPiece, len = std::min(kXferPiece, n - o);
+    if (e == hipSuccess) e = hipMemcpyAsync(L.h_in.p, static_cast<const uint8_t*>(src) + o, len, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipEventRecord(L.planned, st);
+    return e;
+  };
+  SLATE_HIP(issue(0));
+  for (size_t k = 0; k < pieces; k++) {
+    if (k + 1 < pieces) SLATE_HIP(issue(k + 1));  // the next piece moves while this one is copied out
+    PipeLane& L = ctx->lanes[k % kPipeLanes];
+    SLATE_HIP(hipEventSynchronize(L.planned));
+    const size_t o = k * kXferPiece, len = std::min(kXferPiece, n - o);
+    par_memcpy(static_cast<uint8_t*>(dst) + o, L.h_in.p, len);
+  }
+  return SLATE_OK;
+}
+
+namespace {
+
+constexpr uint32_t kChunkBlocks = 65536;
+constexpr uint64_t kChunkBytes = 96ull << 20;
+
 
 // Where decoded chunks go: the caller's arrays in chunk order, or (sharded decode, scatter
 // mode) block by block to the positions the whole batch's layout gives local block j of shard

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <vector>
 
 #include "encode.h"
@@ -236,10 +237,26 @@ int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, siz
 }
 
 // --------------------------------------------------------------- SST builder
+// Encoded bytes on the host: one allocation per GPU pass (uninitialised), blocks are views into
+// it; the table keeps the allocations alive.
+struct HostBytes {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  explicit HostBytes(size_t len) : p(static_cast<uint8_t*>(malloc(len ? len : 1))), n(len) {}
+  ~HostBytes() { free(p); }
+  HostBytes(const HostBytes&) = delete;
+  HostBytes& operator=(const HostBytes&) = delete;
+};
+struct ByteView {
+  std::shared_ptr<HostBytes> seg;
+  size_t off = 0, len = 0;
+  const uint8_t* data() const { return seg ? seg->p + off : nullptr; }
+};
+
 struct slate_sst_table {
   slate_sst_info info{};
   std::vector<uint8_t> first_key;
-  std::deque<std::vector<uint8_t>> chunks;
+  std::vector<ByteView> chunks;  // Table.Blocks: one per finished block, then the final chunk
   bool has_bloom = false;
   uint16_t num_probes = 0;
   std::vector<uint8_t> bloom_bits;
@@ -248,12 +265,16 @@ struct slate_sst_table {
 struct slate_sst_builder {
   slate_ctx* ctx;
   slate_sst_config cfg;
-  // pending KVs (not yet in a finished block)
-  std::vector<uint8_t> keys, vals, tomb;
-  std::vector<uint64_t> key_off{0}, val_off{0};
+  // pending KVs (not yet in a finished block), on the device: key / value bytes, n+1 offsets
+  // into them, tombstone flags
+  DevBuf d_keys, d_vals, d_koff, d_voff, d_tomb, d_tmp;
+  uint64_t n_pend = 0, kbytes = 0, vbytes = 0;
+  // single-KV adds (slate_sst_builder_add) gathered on the host, moved to the device in one go
+  std::vector<uint8_t> hk, hv, ht;
+  std::vector<uint64_t> hko{0}, hvo{0};
   uint64_t pending_lower = 2;  // lower bound of the pending KVs' encoded size
   bool dirty = false;
-  std::deque<std::vector<uint8_t>> blocks;  // finished, not yet popped
+  std::deque<ByteView> blocks;  // finished, not yet popped
   std::vector<uint64_t> meta_off;
   std::vector<uint8_t> meta_keys;
   std::vector<uint64_t> meta_key_off{0};
@@ -263,34 +284,92 @@ struct slate_sst_builder {
   uint32_t num_keys = 0;  // builder.go:111 (uint32)
   DevBuf d_hashes;        // FNV-1 hashes of every key added (bloom input)
   uint64_t n_hashes = 0;
-  std::vector<uint8_t> last_block;  // the final block (Build keeps it in the last chunk)
+  ByteView last_block;    // the final block (Build keeps it in the last chunk)
   int sticky = SLATE_OK;
   bool built = false;
 };
 
+// Append n KVs (offsets relative to their byte arrays, key_off[0] / value_off[0] need not be 0)
+// to the device-resident pending set.  dev: the arrays are device pointers.  tomb may be null
+// (empty value = tombstone).
+static int pending_append(slate_sst_builder* b, const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals,
+                          const uint64_t* val_off, const uint8_t* tomb, uint64_t n, bool dev, uint64_t k0, uint64_t k1,
+                          uint64_t v0, uint64_t v1) {
+  if (n == 0) return SLATE_OK;
+  slate_ctx* ctx = b->ctx;
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx_bind(ctx));
+  const uint64_t kb = k1 - k0, vb = v1 - v0;
+  SLATE_HIP(b->d_keys.grow_keep(b->kbytes + kb + 16, b->kbytes, st));
+  SLATE_HIP(b->d_vals.grow_keep(b->vbytes + vb + 16, b->vbytes, st));
+  SLATE_HIP(b->d_koff.grow_keep((b->n_pend + n + 1) * 8, (b->n_pend + 1) * 8, st));
+  SLATE_HIP(b->d_voff.grow_keep((b->n_pend + n + 1) * 8, (b->n_pend + 1) * 8, st));
+  SLATE_HIP(b->d_tomb.grow_keep(b->n_pend + n + 16, b->n_pend, st));
+  uint8_t* dk = b->d_keys.as<uint8_t>() + b->kbytes;
+  uint8_t* dv = b->d_vals.as<uint8_t>() + b->vbytes;
+  uint64_t* dko = b->d_koff.as<uint64_t>() + b->n_pend;  // entry n_pend (== kbytes) is rewritten
+  uint64_t* dvo = b->d_voff.as<uint64_t>() + b->n_pend;
+  uint8_t* dt = b->d_tomb.as<uint8_t>() + b->n_pend;
+  if (dev) {
+    if (kb) SLATE_HIP(hipMemcpyAsync(dk, keys + k0, kb, hipMemcpyDeviceToDevice, st));
+    if (vb) SLATE_HIP(hipMemcpyAsync(dv, vals + v0, vb, hipMemcpyDeviceToDevice, st));
+    SLATE_HIP(launch_kv_rebase(st, key_off, n, dko, b->kbytes));
+    SLATE_HIP(launch_kv_rebase(st, val_off, n, dvo, b->vbytes));
+    if (tomb) SLATE_HIP(hipMemcpyAsync(dt, tomb, n, hipMemcpyDeviceToDevice, st));
+  } else {
+    int s = ctx_h2d(ctx, dk, keys + k0, kb, st);
+    if (!s) s = ctx_h2d(ctx, dv, vals + v0, vb, st);
+    // raw offsets to scratch, rebased on the device
+    SLATE_HIP(b->d_tmp.ensure((n + 1) * 16 + 16));
+    uint64_t* t0 = b->d_tmp.as<uint64_t>();
+    if (!s) s = ctx_h2d(ctx, t0, key_off, (n + 1) * 8, st);
+    if (!s) s = ctx_h2d(ctx, t0 + n + 1, val_off, (n + 1) * 8, st);
+    if (!s && tomb) s = ctx_h2d(ctx, dt, tomb, n, st);
+    if (s) return s;
+    SLATE_HIP(launch_kv_rebase(st, t0, n, dko, b->kbytes));
+    SLATE_HIP(launch_kv_rebase(st, t0 + n + 1, n, dvo, b->vbytes));
+  }
+  if (!tomb) SLATE_HIP(launch_kv_tomb_from_values(st, dvo, n, dt));
+  b->n_pend += n;
+  b->kbytes += kb;
+  b->vbytes += vb;
+  b->num_keys += uint32_t(n);
+  b->dirty = true;
+  return SLATE_OK;
+}
+
+// the single adds gathered on the host join the device-resident pending set
+static int pending_push_host(slate_sst_builder* b) {
+  const uint64_t n = b->hko.size() - 1;
+  if (n == 0) return SLATE_OK;
+  const uint32_t nk = b->num_keys;
+  int st = pending_append(b, b->hk.data(), b->hko.data(), b->hv.data(), b->hvo.data(), b->ht.data(), n, false, 0,
+                          b->hk.size(), 0, b->hv.size());
+  b->num_keys = nk;  // counted when they were added
+  b->hk.clear();
+  b->hv.clear();
+  b->ht.clear();
+  b->hko.assign(1, 0);
+  b->hvo.assign(1, 0);
+  return st;
+}
+
 static int builder_flush(slate_sst_builder* b, bool final) {
   slate_ctx* ctx = b->ctx;
   hipStream_t st = ctx->stream;
-  const uint64_t n64 = b->key_off.size() - 1;
+  int pst = pending_push_host(b);
+  if (pst) return pst;
+  const uint64_t n64 = b->n_pend;
   b->dirty = false;
   if (n64 == 0) return SLATE_OK;
   if (n64 >= 0xFFFFFFF0ull) return SLATE_E_INVALID_ARG;
   const uint32_t n = uint32_t(n64);
   SLATE_HIP(ctx_bind(ctx));
-  // ---- upload the pending KVs
-  SLATE_HIP(ctx->e_a.ensure(b->keys.size() + 16));
-  SLATE_HIP(ctx->e_b.ensure(b->vals.size() + 16));
-  SLATE_HIP(ctx->e_c.ensure((n64 + 1) * 16 + n64 + 16));
-  uint8_t* d_keys = ctx->e_a.as<uint8_t>();
-  uint8_t* d_vals = ctx->e_b.as<uint8_t>();
-  uint64_t* d_key_off = ctx->e_c.as<uint64_t>();
-  uint64_t* d_val_off = d_key_off + n64 + 1;
-  uint8_t* d_tomb = reinterpret_cast<uint8_t*>(d_val_off + n64 + 1);
-  if (!b->keys.empty()) SLATE_HIP(hipMemcpyAsync(d_keys, b->keys.data(), b->keys.size(), hipMemcpyHostToDevice, st));
-  if (!b->vals.empty()) SLATE_HIP(hipMemcpyAsync(d_vals, b->vals.data(), b->vals.size(), hipMemcpyHostToDevice, st));
-  SLATE_HIP(hipMemcpyAsync(d_key_off, b->key_off.data(), (n64 + 1) * 8, hipMemcpyHostToDevice, st));
-  SLATE_HIP(hipMemcpyAsync(d_val_off, b->val_off.data(), (n64 + 1) * 8, hipMemcpyHostToDevice, st));
-  SLATE_HIP(hipMemcpyAsync(d_tomb, b->tomb.data(), n64, hipMemcpyHostToDevice, st));
+  uint8_t* d_keys = b->d_keys.as<uint8_t>();
+  uint8_t* d_vals = b->d_vals.as<uint8_t>();
+  uint64_t* d_key_off = b->d_koff.as<uint64_t>();
+  uint64_t* d_val_off = b->d_voff.as<uint64_t>();
+  uint8_t* d_tomb = b->d_tomb.as<uint8_t>();
   SLATE_HIP(b->d_hashes.grow_keep((b->n_hashes + n64) * 8 + 64, b->n_hashes * 8, st));
   // ---- work buffers
   const uint64_t chunks = (n64 + 4095) / 4096;
@@ -303,7 +382,8 @@ static int builder_flush(slate_sst_builder* b, bool final) {
   size_t o_adj = carve(n64 * 4), o_next = carve(n64 * 4), o_bytes = carve(n64 * 8), o_exit = carve(n64 * 4),
          o_entry = carve(chunks * 4), o_starts = carve(n64 * 4), o_counts = carve((chunks + 1) * 8),
          o_bstart = carve(n64 * 4), o_bsize = carve((n64 + 1) * 8), o_big = carve(n64 * 4), o_flags = carve(64),
-         o_scan = carve(scan_scratch_bytes(uint32_t(n64 + 1)));
+         o_scan = carve(scan_scratch_bytes(uint32_t(n64 + 1))), o_fko = carve((n64 + 1) * 8),
+         o_pick = carve(kv_pick_scratch_bytes(n64));
   SLATE_HIP(ctx->e_d.ensure(off));
   uint8_t* base = ctx->e_d.as<uint8_t>();
   EncodeBufs w;
@@ -336,12 +416,24 @@ static int builder_flush(slate_sst_builder* b, bool final) {
   const uint64_t nb = final ? nb_total : nb_total - 1;
   std::vector<uint32_t> starts(nb_total);
   SLATE_HIP(hipMemcpyAsync(starts.data(), w.block_start, nb_total * 4, hipMemcpyDeviceToHost, st));
+  // the finished blocks' first keys (the index's BlockMeta keys), gathered on the device
+  uint64_t* fko = reinterpret_cast<uint64_t*>(base + o_fko);
+  SLATE_HIP(ctx->e_h.ensure(b->kbytes + 16));
+  SLATE_HIP(launch_kv_pick_keys(st, w.block_start, nb, d_keys, d_key_off, fko, base + o_pick, ctx->e_h.as<uint8_t>()));
+  std::vector<uint64_t> fk_off(nb + 1);
+  SLATE_HIP(hipMemcpyAsync(fk_off.data(), fko, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipMemsetAsync(w.block_size + nb, 0, 8, st));
   SLATE_HIP(launch_scan_u64(st, w.block_size, uint32_t(nb + 1), scan_scratch));
   std::vector<uint64_t> out_off(nb + 1);
   SLATE_HIP(hipMemcpyAsync(out_off.data(), w.block_size, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
-  std::vector<uint8_t> out;
+  {
+    const size_t mk = b->meta_keys.size();
+    b->meta_keys.resize(mk + fk_off[nb]);
+    int s = ctx_d2h(ctx, b->meta_keys.data() + mk, ctx->e_h.p, fk_off[nb], st);
+    if (s) return s;
+  }
+  std::shared_ptr<HostBytes> seg;
   if (nb && b->cfg.codec == SLATE_CODEC_SNAPPY) {
     // raw sizes -> per-block slots; golang/snappy + CRC per block; scan of the
     // compressed sizes; compaction into back-to-back blocks
@@ -366,59 +458,69 @@ static int builder_flush(slate_sst_builder* b, bool final) {
     SLATE_HIP(hipStreamSynchronize(st));
     SLATE_HIP(ctx->e_e.ensure(fin[nb] + 16));
     SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
-    out.resize(fin[nb]);
-    if (fin[nb]) SLATE_HIP(hipMemcpyAsync(out.data(), ctx->e_e.p, fin[nb], hipMemcpyDeviceToHost, st));
-    SLATE_HIP(hipStreamSynchronize(st));
+    seg = std::make_shared<HostBytes>(fin[nb]);
+    int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, fin[nb], st);
+    if (s) return s;
     out_off.swap(fin);
   } else if (nb) {
     const uint64_t total = out_off[nb];
-    out.resize(total);
     SLATE_HIP(ctx->e_e.ensure(total + 16));
     SLATE_HIP(launch_pack(st, a, w, uint32_t(nb), w.block_size, ctx->e_e.as<uint8_t>(), ctx->num_cus));
     uint32_t status = 0;
     SLATE_HIP(hipMemcpyAsync(&status, w.status, 4, hipMemcpyDeviceToHost, st));
-    if (total) SLATE_HIP(hipMemcpyAsync(out.data(), ctx->e_e.p, total, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
     if (status) return SLATE_E_CAPACITY;
+    seg = std::make_shared<HostBytes>(total);
+    int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, total, st);
+    if (s) return s;
   }
   // ---- queue the finished blocks (builder.go:169-176, finishBlock :192-213)
   for (uint64_t k = 0; k < nb; k++) {
-    uint32_t s = starts[k];
     b->meta_off.push_back(b->current_len);
-    b->meta_keys.insert(b->meta_keys.end(), b->keys.begin() + b->key_off[s], b->keys.begin() + b->key_off[s + 1]);
-    b->meta_key_off.push_back(b->meta_keys.size());
-    std::vector<uint8_t> blk(out.begin() + out_off[k], out.begin() + out_off[k + 1]);
+    b->meta_key_off.push_back(b->meta_key_off.back() + (fk_off[k + 1] - fk_off[k]));
+    ByteView v{seg, out_off[k], out_off[k + 1] - out_off[k]};
     if (final && k + 1 == nb) {
-      b->last_block.swap(blk);  // Build: the last block opens the final chunk
+      b->last_block = v;  // Build: the last block opens the final chunk
     } else {
-      b->current_len += blk.size();
-      b->blocks.push_back(std::move(blk));
+      b->current_len += v.len;
+      b->blocks.push_back(v);
     }
   }
-  uint64_t consumed = final ? n64 : starts[nb_total - 1];
+  const uint64_t consumed = final ? n64 : starts[nb_total - 1];
   b->n_hashes += consumed;
-  if (!final) {  // keep the open block's KVs pending
-    uint64_t k0 = b->key_off[consumed], v0 = b->val_off[consumed];
-    b->keys.erase(b->keys.begin(), b->keys.begin() + k0);
-    b->vals.erase(b->vals.begin(), b->vals.begin() + v0);
-    b->tomb.erase(b->tomb.begin(), b->tomb.begin() + consumed);
-    std::vector<uint64_t> ko(b->key_off.begin() + consumed, b->key_off.end());
-    std::vector<uint64_t> vo(b->val_off.begin() + consumed, b->val_off.end());
-    for (auto& x : ko) x -= k0;
-    for (auto& x : vo) x -= v0;
-    b->key_off.swap(ko);
-    b->val_off.swap(vo);
+  if (final || consumed == n64) {
+    b->n_pend = b->kbytes = b->vbytes = 0;
     b->pending_lower = 2;
-    for (size_t i = 0; i + 1 < b->key_off.size(); i++)
-      b->pending_lower += 2 + 13 + (b->tomb[i] ? 0 : 4 + (b->val_off[i + 1] - b->val_off[i]));
-  } else {
-    b->keys.clear();
-    b->vals.clear();
-    b->tomb.clear();
-    b->key_off.assign(1, 0);
-    b->val_off.assign(1, 0);
-    b->pending_lower = 2;
+    return SLATE_OK;
   }
+  if (consumed == 0) return SLATE_OK;  // nothing finished: the pending set stays as it is
+  // keep the open block's KVs pending: move them to the front (through scratch: may overlap)
+  uint64_t cut[2] = {0, 0};
+  SLATE_HIP(hipMemcpyAsync(&cut[0], d_key_off + consumed, 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipMemcpyAsync(&cut[1], d_val_off + consumed, 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  const uint64_t r = n64 - consumed, rk = b->kbytes - cut[0], rv = b->vbytes - cut[1];
+  SLATE_HIP(b->d_tmp.ensure(rk + rv + r + 2 * (r + 1) * 8 + 64));
+  uint8_t* t = b->d_tmp.as<uint8_t>();
+  uint64_t* to = reinterpret_cast<uint64_t*>(t);
+  uint8_t* tk = t + 2 * (r + 1) * 8;
+  uint8_t* tv = tk + rk;
+  uint8_t* tt = tv + rv;
+  SLATE_HIP(launch_kv_rebase(st, d_key_off + consumed, r, to, 0));
+  SLATE_HIP(launch_kv_rebase(st, d_val_off + consumed, r, to + r + 1, 0));
+  if (rk) SLATE_HIP(hipMemcpyAsync(tk, d_keys + cut[0], rk, hipMemcpyDeviceToDevice, st));
+  if (rv) SLATE_HIP(hipMemcpyAsync(tv, d_vals + cut[1], rv, hipMemcpyDeviceToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(tt, d_tomb + consumed, r, hipMemcpyDeviceToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_key_off, to, (r + 1) * 8, hipMemcpyDeviceToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_val_off, to + r + 1, (r + 1) * 8, hipMemcpyDeviceToDevice, st));
+  if (rk) SLATE_HIP(hipMemcpyAsync(d_keys, tk, rk, hipMemcpyDeviceToDevice, st));
+  if (rv) SLATE_HIP(hipMemcpyAsync(d_vals, tv, rv, hipMemcpyDeviceToDevice, st));
+  SLATE_HIP(hipMemcpyAsync(d_tomb, tt, r, hipMemcpyDeviceToDevice, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  b->n_pend = r;
+  b->kbytes = rk;
+  b->vbytes = rv;
+  b->pending_lower = 2 + 15 * r + rv;  // a lower bound (row.go:95-107 without the value lengths)
   return SLATE_OK;
 }
 
@@ -449,7 +551,8 @@ slate_sst_builder* slate_sst_builder_new(slate_ctx* ctx, const slate_sst_config*
 void slate_sst_builder_free(slate_sst_builder* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
-  b->d_hashes.release();
+  for (DevBuf* d : {&b->d_hashes, &b->d_keys, &b->d_vals, &b->d_koff, &b->d_voff, &b->d_tomb, &b->d_tmp})
+    d->release();
   delete b;
 }
 
@@ -460,11 +563,11 @@ int slate_sst_builder_add(slate_sst_builder* b, const uint8_t* key, size_t key_l
   if (key_len == 0) return SLATE_E_INVALID_ARG;  // block.go:163 assert (panic in Go)
   b->num_keys += 1;
   bool tomb = kind == 1;
-  b->keys.insert(b->keys.end(), key, key + key_len);
-  b->key_off.push_back(b->keys.size());
-  if (!tomb && value_len) b->vals.insert(b->vals.end(), value, value + value_len);
-  b->val_off.push_back(b->vals.size());
-  b->tomb.push_back(tomb ? 1 : 0);
+  b->hk.insert(b->hk.end(), key, key + key_len);
+  b->hko.push_back(b->hk.size());
+  if (!tomb && value_len) b->hv.insert(b->hv.end(), value, value + value_len);
+  b->hvo.push_back(b->hv.size());
+  b->ht.push_back(tomb ? 1 : 0);
   b->pending_lower += 2 + 13 + (tomb ? 0 : 4 + value_len);
   b->dirty = true;
   if (!b->has_first_key) {  // builder.go:178-180
@@ -482,44 +585,82 @@ int slate_sst_builder_add_value(slate_sst_builder* b, const uint8_t* key, size_t
 int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const uint64_t* key_off,
                                 const uint8_t* values, const uint64_t* value_off, const uint8_t* is_tomb, uint64_t n) {
   if (!b || (n && (!keys || !key_off || !value_off))) return SLATE_E_INVALID_ARG;
-  if (!is_tomb && n && !b->built) {
-    // bulk path (tombstone = empty value): the same effect as n calls of
-    // slate_sst_builder_add, up to the first empty key (block.go:163), which fails
-    uint64_t m = 0, lower = 0;
-    while (m < n && key_off[m + 1] > key_off[m]) {
-      const uint64_t vl = value_off[m + 1] - value_off[m];
-      lower += 2 + 13 + (vl ? 4 + vl : 0);
-      m++;
-    }
-    if (m) {
-      const uint64_t kb = b->keys.size(), vb = b->vals.size();
-      b->keys.insert(b->keys.end(), keys + key_off[0], keys + key_off[m]);
-      b->vals.insert(b->vals.end(), values + value_off[0], values + value_off[m]);
-      b->key_off.reserve(b->key_off.size() + m);
-      b->val_off.reserve(b->val_off.size() + m);
-      b->tomb.reserve(b->tomb.size() + m);
-      for (uint64_t i = 0; i < m; i++) {
-        b->key_off.push_back(kb + (key_off[i + 1] - key_off[0]));
-        b->val_off.push_back(vb + (value_off[i + 1] - value_off[0]));
-        b->tomb.push_back(value_off[i + 1] == value_off[i] ? 1 : 0);
-      }
-      b->num_keys += m;
-      b->pending_lower += lower;
-      b->dirty = true;
-      if (!b->has_first_key) {  // builder.go:178-180
-        b->first_key.assign(keys + key_off[0], keys + key_off[1]);
-        b->has_first_key = true;
+  if (b->built) return SLATE_E_INVALID_ARG;
+  if (n == 0) return SLATE_OK;
+  // the same effect as n calls of slate_sst_builder_add, up to the first empty key
+  // (block.go:163), which fails; a tombstone's value bytes are not kept
+  uint64_t m = 0, lower = 0;
+  while (m < n && key_off[m + 1] > key_off[m]) {
+    const bool tomb = is_tomb ? is_tomb[m] != 0 : value_off[m + 1] == value_off[m];
+    const uint64_t vl = value_off[m + 1] - value_off[m];
+    lower += 2 + 13 + (tomb ? 0 : 4 + vl);
+    m++;
+  }
+  if (m) {
+    int st = pending_push_host(b);  // keep the order of earlier single adds
+    if (st) return b->sticky = st;
+    if (is_tomb) {
+      // tombstones with value bytes: take the per-KV path so that those bytes are dropped
+      bool dropped = false;
+      for (uint64_t i = 0; i < m && !dropped; i++) dropped = is_tomb[i] && value_off[i + 1] > value_off[i];
+      if (dropped) {
+        for (uint64_t i = 0; i < m; i++) {
+          st = slate_sst_builder_add(b, keys + key_off[i], key_off[i + 1] - key_off[i], values + value_off[i],
+                                     value_off[i + 1] - value_off[i], is_tomb[i] ? 1 : 0);
+          if (st) return st;
+        }
+        return m == n ? SLATE_OK : SLATE_E_INVALID_ARG;
       }
     }
-    return m == n ? SLATE_OK : SLATE_E_INVALID_ARG;
+    if (!b->has_first_key) {  // builder.go:178-180
+      b->first_key.assign(keys + key_off[0], keys + key_off[1]);
+      b->has_first_key = true;
+    }
+    st = pending_append(b, keys, key_off, values, value_off, is_tomb, m, false, key_off[0], key_off[m], value_off[0],
+                        value_off[m]);
+    if (st) return b->sticky = st;
+    b->pending_lower += lower;
   }
-  for (uint64_t i = 0; i < n; i++) {
-    uint64_t vl = value_off[i + 1] - value_off[i];
-    int kind = is_tomb ? (is_tomb[i] ? 1 : 0) : (vl == 0 ? 1 : 0);
-    int st = slate_sst_builder_add(b, keys + key_off[i], key_off[i + 1] - key_off[i], values + value_off[i], vl, kind);
-    if (st) return st;
+  return m == n ? SLATE_OK : SLATE_E_INVALID_ARG;
+}
+
+// Device-resident KVs (compaction's merged output): keys / values / offsets / tombstones in
+// device memory of the builder's context, the same effect as slate_sst_builder_add_batch.
+int slate_sst_builder_add_batch_device(slate_sst_builder* b, const uint8_t* d_keys, const uint64_t* d_key_off,
+                                       const uint8_t* d_values, const uint64_t* d_value_off, const uint8_t* d_is_tomb,
+                                       uint64_t n) {
+  if (!b || (n && (!d_keys || !d_key_off || !d_value_off))) return SLATE_E_INVALID_ARG;
+  if (b->built) return SLATE_E_INVALID_ARG;
+  if (n == 0) return SLATE_OK;
+  slate_ctx* ctx = b->ctx;
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx_bind(ctx));
+  int s = pending_push_host(b);
+  if (s) return b->sticky = s;
+  // the first empty key ends the batch (block.go:163); the range and the first key
+  SLATE_HIP(b->d_tmp.ensure(64));
+  uint64_t* q = b->d_tmp.as<uint64_t>();
+  SLATE_HIP(launch_kv_first_empty(st, d_key_off, n, q));
+  uint64_t h[5];
+  SLATE_HIP(hipMemcpyAsync(&h[0], q, 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipMemcpyAsync(&h[1], d_key_off, 16, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipMemcpyAsync(&h[3], d_value_off, 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  const uint64_t m = std::min<uint64_t>(h[0], n);
+  if (m == 0) return SLATE_E_INVALID_ARG;
+  uint64_t ends[2];
+  SLATE_HIP(hipMemcpyAsync(&ends[0], d_key_off + m, 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipMemcpyAsync(&ends[1], d_value_off + m, 8, hipMemcpyDeviceToHost, st));
+  if (!b->has_first_key) {
+    b->first_key.resize(h[2] - h[1]);
+    SLATE_HIP(hipMemcpyAsync(b->first_key.data(), d_keys + h[1], h[2] - h[1], hipMemcpyDeviceToHost, st));
+    b->has_first_key = true;
   }
-  return SLATE_OK;
+  SLATE_HIP(hipStreamSynchronize(st));
+  s = pending_append(b, d_keys, d_key_off, d_values, d_value_off, d_is_tomb, m, true, h[1], ends[0], h[3], ends[1]);
+  if (s) return b->sticky = s;
+  b->pending_lower += 15 * m;  // a lower bound: every row is at least 15 bytes with its offset
+  return m == n ? SLATE_OK : SLATE_E_INVALID_ARG;
 }
 
 int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_cap, size_t* len, int* present) {
@@ -533,10 +674,10 @@ int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_
     if (st) return b->sticky = st;
   }
   if (b->blocks.empty()) return SLATE_OK;
-  std::vector<uint8_t>& blk = b->blocks.front();
-  if (len) *len = blk.size();
-  if (blk.size() > out_cap || (!out && blk.size())) return SLATE_E_CAPACITY;
-  if (!blk.empty()) memcpy(out, blk.data(), blk.size());
+  const ByteView& blk = b->blocks.front();
+  if (len) *len = blk.len;
+  if (blk.len > out_cap || (!out && blk.len)) return SLATE_E_CAPACITY;
+  if (blk.len) memcpy(out, blk.data(), blk.len);
   b->blocks.pop_front();
   *present = 1;
   return SLATE_OK;
@@ -550,7 +691,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   if (st) return st;
   b->built = true;
   slate_sst_table* t = new slate_sst_table();
-  std::vector<uint8_t> buf = b->last_block;
+  std::vector<uint8_t> buf(b->last_block.data(), b->last_block.data() + b->last_block.len);
   const uint64_t filter_off = b->current_len + buf.size();
   uint64_t filter_len = 0;
   // ---- bloom filter (builder.go:225-235, bloom.go:112-133 Build, :52-67 Encode)
@@ -639,8 +780,11 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   t->info.codec = b->cfg.codec;
   t->info.first_key_len = uint32_t(b->first_key.size());
   t->first_key = b->first_key;
-  t->chunks.swap(b->blocks);
-  t->chunks.push_back(std::move(buf));
+  t->chunks.assign(b->blocks.begin(), b->blocks.end());
+  b->blocks.clear();
+  auto fin = std::make_shared<HostBytes>(buf.size());
+  if (!buf.empty()) memcpy(fin->p, buf.data(), buf.size());
+  t->chunks.push_back(ByteView{fin, 0, buf.size()});
   *table = t;
   return SLATE_OK;
 }
@@ -660,24 +804,30 @@ size_t slate_sst_table_num_chunks(const slate_sst_table* t) { return t ? t->chun
 int slate_sst_table_chunk(const slate_sst_table* t, size_t i, const uint8_t** data, size_t* len) {
   if (!t || i >= t->chunks.size() || !data || !len) return SLATE_E_INVALID_ARG;
   *data = t->chunks[i].data();
-  *len = t->chunks[i].size();
+  *len = t->chunks[i].len;
   return SLATE_OK;
 }
 
 size_t slate_sst_table_encoded_len(const slate_sst_table* t) {
   size_t n = 0;
   if (t)
-    for (auto& c : t->chunks) n += c.size();
+    for (auto& c : t->chunks) n += c.len;
   return n;
 }
 
+// Runs of chunks adjacent in one host allocation are copied as one piece (the blocks of one
+// GPU pass are back to back), split over threads.
 int slate_sst_table_encode(const slate_sst_table* t, uint8_t* out, size_t out_cap) {
   if (!t) return SLATE_E_INVALID_ARG;
-  size_t o = 0;
-  for (auto& c : t->chunks) {
-    if (o + c.size() > out_cap) return SLATE_E_CAPACITY;
-    if (!c.empty()) memcpy(out + o, c.data(), c.size());
-    o += c.size();
+  if (slate_sst_table_encoded_len(t) > out_cap || (!out && slate_sst_table_encoded_len(t))) return SLATE_E_CAPACITY;
+  size_t o = 0, i = 0;
+  while (i < t->chunks.size()) {
+    const ByteView& c = t->chunks[i];
+    size_t j = i + 1, len = c.len;
+    while (j < t->chunks.size() && t->chunks[j].seg == c.seg && t->chunks[j].off == c.off + len) len += t->chunks[j++].len;
+    if (len) par_memcpy(out + o, c.data(), len);
+    o += len;
+    i = j;
   }
   return SLATE_OK;
 }

@@ -68,4 +68,14 @@ hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_
 hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t n_plus_1, void* scratch);
 size_t scan_scratch_bytes(uint32_t n_plus_1);
 
+// SST builder KV staging: dst[0..n] = base + (src[i] - src[0]); tomb[i] = empty value;
+// *out = index of the first empty key or ~0 (block.go:163); the keys at idx[0..m) gathered
+// back to back (out_off: m+1 u64, exclusive scan of their lengths; scratch kv_pick_scratch_bytes).
+hipError_t launch_kv_rebase(hipStream_t st, const uint64_t* src, uint64_t n, uint64_t* dst, uint64_t base);
+hipError_t launch_kv_tomb_from_values(hipStream_t st, const uint64_t* val_off, uint64_t n, uint8_t* tomb);
+hipError_t launch_kv_first_empty(hipStream_t st, const uint64_t* key_off, uint64_t n, uint64_t* out);
+size_t kv_pick_scratch_bytes(uint64_t m);
+hipError_t launch_kv_pick_keys(hipStream_t st, const uint32_t* idx, uint64_t m, const uint8_t* keys,
+                               const uint64_t* key_off, uint64_t* out_off, void* scratch, uint8_t* out);
+
 }  // namespace slate

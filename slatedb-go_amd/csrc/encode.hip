@@ -686,4 +686,71 @@ hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_
   return hipGetLastError();
 }
 
+// ------------------------------------------------------ builder KV staging (device side)
+// Pending KVs live in device arrays; appended batches are rebased onto them.
+__global__ void kv_rebase_kernel(const uint64_t* __restrict__ src, uint64_t n, uint64_t* __restrict__ dst,
+                                 uint64_t base) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i <= n) dst[i] = base + (src[i] - src[0]);
+}
+
+__global__ void kv_tomb_kernel(const uint64_t* __restrict__ val_off, uint64_t n, uint8_t* __restrict__ tomb) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) tomb[i] = val_off[i + 1] == val_off[i] ? 1 : 0;
+}
+
+// index of the first empty key (block.go:163 assert), or n
+__global__ void kv_first_empty_kernel(const uint64_t* __restrict__ key_off, uint64_t n, unsigned long long* out) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n && key_off[i + 1] == key_off[i]) atomicMin(out, static_cast<unsigned long long>(i));
+}
+
+__global__ void kv_pick_len_kernel(const uint32_t* __restrict__ idx, uint64_t m, const uint64_t* __restrict__ key_off,
+                                   uint64_t* __restrict__ len) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < m) len[i] = key_off[idx[i] + 1] - key_off[idx[i]];
+  if (i == m) len[m] = 0;
+}
+
+// one wave per picked key
+__global__ void kv_pick_copy_kernel(const uint32_t* __restrict__ idx, uint64_t m, const uint8_t* __restrict__ keys,
+                                    const uint64_t* __restrict__ key_off, const uint64_t* __restrict__ out_off,
+                                    uint8_t* __restrict__ out) {
+  const uint64_t w = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (w >= m) return;
+  const uint64_t s = key_off[idx[w]], l = key_off[idx[w] + 1] - s, o = out_off[w];
+  for (uint64_t k = lane; k < l; k += 64) out[o + k] = keys[s + k];
+}
+
+hipError_t launch_kv_rebase(hipStream_t st, const uint64_t* src, uint64_t n, uint64_t* dst, uint64_t base) {
+  kv_rebase_kernel<<<uint32_t((n + 256) / 256), 256, 0, st>>>(src, n, dst, base);
+  return hipGetLastError();
+}
+
+hipError_t launch_kv_tomb_from_values(hipStream_t st, const uint64_t* val_off, uint64_t n, uint8_t* tomb) {
+  if (n) kv_tomb_kernel<<<uint32_t((n + 255) / 256), 256, 0, st>>>(val_off, n, tomb);
+  return hipGetLastError();
+}
+
+hipError_t launch_kv_first_empty(hipStream_t st, const uint64_t* key_off, uint64_t n, uint64_t* out) {
+  hipError_t e = hipMemsetAsync(out, 0xFF, 8, st);
+  if (e != hipSuccess) return e;
+  if (n)
+    kv_first_empty_kernel<<<uint32_t((n + 255) / 256), 256, 0, st>>>(key_off, n,
+                                                                      reinterpret_cast<unsigned long long*>(out));
+  return hipGetLastError();
+}
+
+size_t kv_pick_scratch_bytes(uint64_t m) { return scan_scratch_bytes(uint32_t(m + 1)) + 64; }
+
+hipError_t launch_kv_pick_keys(hipStream_t st, const uint32_t* idx, uint64_t m, const uint8_t* keys,
+                               const uint64_t* key_off, uint64_t* out_off, void* scratch, uint8_t* out) {
+  kv_pick_len_kernel<<<uint32_t((m + 256) / 256), 256, 0, st>>>(idx, m, key_off, out_off);
+  hipError_t e = launch_scan_u64(st, out_off, uint32_t(m + 1), scratch);
+  if (e != hipSuccess) return e;
+  if (m) kv_pick_copy_kernel<<<uint32_t((m * 64 + 255) / 256), 256, 0, st>>>(idx, m, keys, key_off, out_off, out);
+  return hipGetLastError();
+}
+
 }  // namespace slate

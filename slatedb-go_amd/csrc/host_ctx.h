@@ -134,6 +134,17 @@ inline int hip_status(hipError_t e) {
 
 inline hipError_t ctx_bind(slate_ctx* ctx) { return hipSetDevice(ctx->device); }
 
+// Host copies split over up to kCopyThreads threads (16: the CPU share one GPU's process gets on
+// the MI355X boxes; one core copies ~10 GB/s, below the PCIe link) -- api_host.cpp.
+constexpr size_t kCopyThreads = 16;
+void par_memcpy(void* dst, const void* src, size_t n);
+// A pipeline lane's stream and events, created on first use.
+hipError_t lane_init(PipeLane& L);
+// Large host <-> device copies through the context's page-locked lane staging (64 MiB pieces,
+// two in flight; stream-ordered on st, synchronous on return); small ones go straight through.
+int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st);
+int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st);
+
 // compress.Decode of one `payload || BE32 CRC` buffer (an index or filter) on the GPU, CRC
 // first: *bstatus = SLATE_OK, SLATE_E_BLOCK_CHECKSUM or the codec's status (api_sst.cpp).
 int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,

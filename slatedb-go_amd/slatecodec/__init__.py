@@ -22,6 +22,7 @@ NONE, SNAPPY, ZLIB, LZ4, ZSTD = 0, 1, 2, 3, 4
 OK = 0
 E_NO_DEVICE = 100
 E_CAPACITY = 103
+E_INVALID_ARG = 102
 E_MERGE_UNSORTED = 105
 
 u8p = C.POINTER(C.c_uint8)
@@ -88,6 +89,7 @@ _SIGS = {
     "slate_sst_builder_add": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t, C.c_int]),
     "slate_sst_builder_add_value": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t]),
     "slate_sst_builder_add_batch": (C.c_int, [vp, vp, vp, vp, vp, vp, C.c_uint64]),
+    "slate_sst_builder_add_batch_device": (C.c_int, [vp, vp, vp, vp, vp, vp, C.c_uint64]),
     "slate_sst_builder_next_block": (C.c_int, [vp, vp, C.c_size_t, szp, C.POINTER(C.c_int)]),
     "slate_sst_builder_build": (C.c_int, [vp, C.POINTER(vp)]),
     "slate_sst_table_free": (None, [vp]),
@@ -481,6 +483,13 @@ class SstBuilder:
         return lib().slate_sst_builder_add_batch(self._h, _ptr(keys), _ptr(key_off), _ptr(vals), _ptr(val_off),
                                                  _ptr(is_tomb) if is_tomb is not None else None, len(key_off) - 1)
 
+    def add_batch_device(self, d_keys: int, d_key_off: int, d_vals: int, d_val_off: int, n: int,
+                         d_is_tomb: int | None = None) -> int:
+        """slate_sst_builder_add_batch_device: device pointers (e.g. tensor.data_ptr())."""
+        return lib().slate_sst_builder_add_batch_device(self._h, C.c_void_p(d_keys), C.c_void_p(d_key_off),
+                                                        C.c_void_p(d_vals), C.c_void_p(d_val_off),
+                                                        C.c_void_p(d_is_tomb) if d_is_tomb else None, n)
+
     def next_block(self) -> bytes | None:
         cap = 1 << 16
         while True:
@@ -519,10 +528,14 @@ class SstTable:
         return out
 
     def encode(self) -> bytes:
+        return self.encode_array().tobytes()
+
+    def encode_array(self) -> np.ndarray:
+        """The SST bytes (Table.Blocks concatenated) into a fresh uint8 array, no further copy."""
         n = lib().slate_sst_table_encoded_len(self._h)
-        out = np.zeros(max(n, 1), np.uint8)
+        out = np.empty(max(n, 1), np.uint8)
         _check(lib().slate_sst_table_encode(self._h, _ptr(out), out.size), "encode")
-        return out[:n].tobytes()
+        return out[:n]
 
     def info(self) -> dict:
         info = SstInfo()

@@ -256,17 +256,15 @@ def compact(ctx: Context, sources: list[list[bytes]], max_sst_size: int, block_s
     device = device or torch.device("cuda", torch.cuda.current_device())
     view = decode_rows_kv(ctx, sources, device)
     keys, key_off, vals, val_off, tomb, m = merge_kv(ctx, view, device)
-    h_keys, h_key_off = keys.cpu().numpy(), key_off.cpu().numpy().view(np.uint64)[: m + 1]
-    h_vals, h_val_off = vals.cpu().numpy(), val_off.cpu().numpy().view(np.uint64)[: m + 1]
-    h_tomb = tomb.cpu().numpy()[:m]
+    # the merged KVs stay on the device: only the offsets come back, for the output split
+    h_key_off = key_off.cpu().numpy().view(np.uint64)[: m + 1]
+    h_val_off = val_off.cpu().numpy().view(np.uint64)[: m + 1]
     out, start = [], 0
     for end in split_points(h_key_off, h_val_off, max_sst_size):
         b = SstBuilder(ctx, block_size, min_filter_keys, filter_bits_per_key, codec)
-        ko = h_key_off[start:end + 1] - h_key_off[start]
-        vo = h_val_off[start:end + 1] - h_val_off[start]
-        _check(b.add_batch(h_keys[int(h_key_off[start]):int(h_key_off[end]) + 1], ko,
-                           h_vals[int(h_val_off[start]):int(h_val_off[end]) + 1], vo,
-                           None), "add_batch")  # AddValue: empty value => tombstone (table_store.go:221-223)
+        # AddValue: empty value => tombstone (table_store.go:221-223)
+        _check(b.add_batch_device(keys.data_ptr(), key_off.data_ptr() + 8 * start, vals.data_ptr(),
+                                  val_off.data_ptr() + 8 * start, end - start), "add_batch_device")
         out.append(b.build().encode())
         start = end
     return out
