@@ -129,18 +129,6 @@ struct Sink {
   const uint64_t* g_row_base = nullptr;
 };
 
-// SLATE_HOST_TRACE=1: per-chunk host phase times on stderr (diagnostics for DESIGN.md's
-// host pipeline numbers; read once per process)
-static bool host_trace() {
-  static const bool on = [] {
-    const char* e = getenv("SLATE_HOST_TRACE");
-    return e && *e == '1';
-  }();
-  return on;
-}
-static double now_ms() {
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // plan_sizes_kernel's decoded length for CodecNone / CodecSnappy on the host (decode.hip
 // decoded_len: the payload length, or golang/snappy decodedLen's varint header with the same

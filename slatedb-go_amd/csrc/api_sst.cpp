@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
+#include <sys/mman.h>
 #include <memory>
 #include <vector>
 
@@ -237,13 +238,48 @@ int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, siz
 }
 
 // --------------------------------------------------------------- SST builder
+void SegPool::close() {
+  std::lock_guard<std::mutex> g(mu);
+  open = false;
+  for (auto& f : free_list) munmap(f.first, f.second);
+  free_list.clear();
+}
+
 // Encoded bytes on the host: one allocation per GPU pass (uninitialised), blocks are views into
 // it; the table keeps the allocations alive.
+// Large ones are 2 MiB-aligned anonymous mappings advised for transparent huge pages (a fresh
+// 1 GB buffer otherwise costs ~260 k page faults on first touch, more than its PCIe transfer),
+// and go back to the context's pool when released, so that repeated builds reuse them.
 struct HostBytes {
   uint8_t* p = nullptr;
-  size_t n = 0;
-  explicit HostBytes(size_t len) : p(static_cast<uint8_t*>(malloc(len ? len : 1))), n(len) {}
-  ~HostBytes() { free(p); }
+  size_t n = 0, cap = 0;
+  bool mapped = false;
+  std::shared_ptr<SegPool> pool;
+  explicit HostBytes(size_t len, std::shared_ptr<SegPool> pl = nullptr) : n(len), pool(std::move(pl)) {
+    if (pool && pool->take(len, &p, &cap)) {
+      mapped = true;
+      return;
+    }
+    if (len >= kSegHuge) {
+      cap = (len + kSegHuge - 1) & ~(kSegHuge - 1);
+      void* q = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (q != MAP_FAILED) {
+        (void)madvise(q, cap, MADV_HUGEPAGE);
+        p = static_cast<uint8_t*>(q);
+        mapped = true;
+        return;
+      }
+    }
+    cap = len ? len : 1;
+    p = static_cast<uint8_t*>(malloc(cap));
+  }
+  ~HostBytes() {
+    if (!mapped) {
+      free(p);
+    } else if (!pool || !pool->give(p, cap)) {
+      munmap(p, cap);
+    }
+  }
   HostBytes(const HostBytes&) = delete;
   HostBytes& operator=(const HostBytes&) = delete;
 };
@@ -405,6 +441,14 @@ static int builder_flush(slate_sst_builder* b, bool final) {
   w.status = w.flags + 3;
   void* scan_scratch = base + o_scan;
   EncodeArgs a{d_keys, d_key_off, d_vals, d_val_off, d_tomb, n, b->cfg.block_size, b->cfg.codec};
+  const bool trace = host_trace();
+  double tp = trace ? now_ms() : 0.0;
+  auto mark = [&](const char* what) {
+    if (!trace) return;
+    const double t = now_ms();
+    fprintf(stderr, "[slate build]   %s %.2f ms\n", what, t - tp);
+    tp = t;
+  };
   SLATE_HIP(launch_encode(st, a, w, ctx->num_cus));
   SLATE_HIP(hipMemsetAsync(w.counts + chunks, 0, 8, st));
   SLATE_HIP(launch_scan_u64(st, w.counts, uint32_t(chunks + 1), scan_scratch));
@@ -427,6 +471,7 @@ static int builder_flush(slate_sst_builder* b, bool final) {
   std::vector<uint64_t> out_off(nb + 1);
   SLATE_HIP(hipMemcpyAsync(out_off.data(), w.block_size, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
+  mark("segment + first keys");
   {
     const size_t mk = b->meta_keys.size();
     b->meta_keys.resize(mk + fk_off[nb]);
@@ -458,8 +503,10 @@ static int builder_flush(slate_sst_builder* b, bool final) {
     SLATE_HIP(hipStreamSynchronize(st));
     SLATE_HIP(ctx->e_e.ensure(fin[nb] + 16));
     SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
-    seg = std::make_shared<HostBytes>(fin[nb]);
+    mark("pack snappy");
+    seg = std::make_shared<HostBytes>(fin[nb], ctx->seg_pool);
     int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, fin[nb], st);
+    mark("blocks D2H");
     if (s) return s;
     out_off.swap(fin);
   } else if (nb) {
@@ -470,8 +517,10 @@ static int builder_flush(slate_sst_builder* b, bool final) {
     SLATE_HIP(hipMemcpyAsync(&status, w.status, 4, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
     if (status) return SLATE_E_CAPACITY;
-    seg = std::make_shared<HostBytes>(total);
+    mark("pack");
+    seg = std::make_shared<HostBytes>(total, ctx->seg_pool);
     int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, total, st);
+    mark("blocks D2H");
     if (s) return s;
   }
   // ---- queue the finished blocks (builder.go:169-176, finishBlock :192-213)
@@ -687,8 +736,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   if (!b || !table || b->built) return SLATE_E_INVALID_ARG;
   if (b->sticky) return b->sticky;
   slate_ctx* ctx = b->ctx;
+  const double t0 = host_trace() ? now_ms() : 0.0;
   int st = builder_flush(b, true);
   if (st) return st;
+  const double t1 = host_trace() ? now_ms() : 0.0;
   b->built = true;
   slate_sst_table* t = new slate_sst_table();
   std::vector<uint8_t> buf(b->last_block.data(), b->last_block.data() + b->last_block.len);
@@ -743,6 +794,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
     put_be32(buf, crc);
     filter_len = buf.size() - f0;
   }
+  const double t2 = host_trace() ? now_ms() : 0.0;
   // ---- index (builder.go:238-244, flatbuf.go:126-139)
   std::vector<uint8_t> index;
   {
@@ -786,6 +838,9 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   if (!buf.empty()) memcpy(fin->p, buf.data(), buf.size());
   t->chunks.push_back(ByteView{fin, 0, buf.size()});
   *table = t;
+  if (host_trace())
+    fprintf(stderr, "[slate build] flush %.2f ms, filter %.2f ms, index + info %.2f ms\n", t1 - t0, t2 - t1,
+            now_ms() - t2);
   return SLATE_OK;
 }
 

@@ -2,7 +2,13 @@
 // buffers.  Each slate_ctx is used by one caller thread at a time; the library
 // keeps no global mutable state (SURVEY 8b "Threading").
 #pragma once
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "kernels.h"
@@ -96,6 +102,37 @@ struct PipeLane {
 };
 constexpr int kPipeLanes = 2;
 
+// Released encoded-SST host buffers (api_sst.cpp HostBytes mappings) kept for reuse by the
+// context's next builds: a few, best fit.  Shared with the buffers, so it outlives whichever
+// of them and the context goes last.
+constexpr size_t kSegHuge = 2u << 20;
+struct SegPool {
+  std::mutex mu;
+  std::vector<std::pair<void*, size_t>> free_list;
+  bool open = true;
+  static constexpr size_t kKeep = 4;
+  bool take(size_t len, uint8_t** p, size_t* cap) {
+    std::lock_guard<std::mutex> g(mu);
+    size_t best = free_list.size();
+    for (size_t i = 0; i < free_list.size(); i++)
+      if (free_list[i].second >= len && free_list[i].second <= 2 * len + kSegHuge &&
+          (best == free_list.size() || free_list[i].second < free_list[best].second))
+        best = i;
+    if (best == free_list.size()) return false;
+    *p = static_cast<uint8_t*>(free_list[best].first);
+    *cap = free_list[best].second;
+    free_list.erase(free_list.begin() + long(best));
+    return true;
+  }
+  bool give(void* p, size_t cap) {  // false: the caller unmaps it
+    std::lock_guard<std::mutex> g(mu);
+    if (!open || free_list.size() >= kKeep) return false;
+    free_list.emplace_back(p, cap);
+    return true;
+  }
+  void close();  // unmaps the kept buffers (api_sst.cpp)
+};
+
 struct slate_ctx {
   int device = 0;
   int num_cus = 256;
@@ -109,7 +146,9 @@ struct slate_ctx {
   DevBuf e_a, e_b, e_c, e_d, e_e, e_f, e_g, e_h, e_i, e_j;
   // Snappy encode: per-block slots, raw staging for oversized blocks, snappy LDS-free scratch
   DevBuf s_slots, s_raw, s_aux;
+  std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
   void release_all() {
+    if (seg_pool) seg_pool->close();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
                       &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &s_slots, &s_raw, &s_aux})
       b->release();
@@ -133,6 +172,19 @@ inline int hip_status(hipError_t e) {
 }
 
 inline hipError_t ctx_bind(slate_ctx* ctx) { return hipSetDevice(ctx->device); }
+
+// SLATE_HOST_TRACE=1: host phase times of the host pipelines on stderr (diagnostics for the
+// numbers in DESIGN.md; read once per process).
+inline bool host_trace() {
+  static const bool on = [] {
+    const char* e = getenv("SLATE_HOST_TRACE");
+    return e && *e == '1';
+  }();
+  return on;
+}
+inline double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // Host copies split over up to kCopyThreads threads (16: the CPU share one GPU's process gets on
 // the MI355X boxes; one core copies ~10 GB/s, below the PCIe link) -- api_host.cpp.

@@ -530,10 +530,12 @@ class SstTable:
     def encode(self) -> bytes:
         return self.encode_array().tobytes()
 
-    def encode_array(self) -> np.ndarray:
-        """The SST bytes (Table.Blocks concatenated) into a fresh uint8 array, no further copy."""
+    def encode_array(self, out: np.ndarray | None = None) -> np.ndarray:
+        """The SST bytes (Table.Blocks concatenated) into `out` (reused when large enough) or a
+        fresh uint8 array; returns the filled prefix."""
         n = lib().slate_sst_table_encoded_len(self._h)
-        out = np.empty(max(n, 1), np.uint8)
+        if out is None or out.size < max(n, 1):
+            out = np.empty(max(n, 1), np.uint8)
         _check(lib().slate_sst_table_encode(self._h, _ptr(out), out.size), "encode")
         return out[:n]
 
