@@ -92,14 +92,121 @@ int ctx_snappy_encode_host(slate_ctx* ctx, const uint8_t* data, size_t n, std::v
   return ctx_snappy_encode_device(ctx, ctx->e_i.as<uint8_t>(), n, out);
 }
 
-// compress.Encode (compression.go:80-116) for the codecs the GPU implements.
+// compress.Encode (compression.go:80-116) with CodecLz4 / CodecZlib / CodecZstd of n payloads
+// already on the device (payload i: raw_len[i] bytes at d_raw + raw_start[i]): frames back to back
+// at codec_frames(ctx) (ctx->c_out after kFramePad bytes: the frame CRC reads the aligned dword
+// before a frame), each followed by its BE32 CRC32 when with_crc (block.Encode, bloom.Encode,
+// encodeIndex framing); out_off (n + 1) on the host.  encode_codecs.hip does the work.
+constexpr size_t kFramePad = 16;
+static uint8_t* codec_frames(slate_ctx* ctx) { return ctx->c_out.as<uint8_t>() + kFramePad; }
+static int ctx_codec_frames(slate_ctx* ctx, int codec, const uint8_t* d_raw, const uint64_t* raw_start,
+                            const uint64_t* raw_len, uint64_t n, bool with_crc, std::vector<uint64_t>& out_off) {
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx_bind(ctx));
+  std::vector<CodecPiece> pieces;
+  std::vector<CodecPayload> pay(n);
+  std::vector<uint32_t> small, big;
+  uint64_t tags = 0, bodies = 0, seqs = 0;
+  for (uint64_t p = 0; p < n; p++) {
+    const uint64_t len = raw_len[p];
+    if (len > 0xFFFFFF00ull) return SLATE_E_INVALID_ARG;
+    const uint32_t np = len ? uint32_t((len + kCodecPieceMax - 1) / kCodecPieceMax) : 1u;
+    pay[p] = CodecPayload{raw_start[p], uint32_t(len), uint32_t(pieces.size()), np, 0};
+    for (uint32_t k = 0; k < np; k++) {
+      const uint32_t l = uint32_t(std::min<uint64_t>(kCodecPieceMax, len - uint64_t(k) * kCodecPieceMax));
+      CodecPiece c{raw_start[p] + uint64_t(k) * kCodecPieceMax, tags, bodies, seqs, l,
+                   (k == 0 ? 1u : 0u) | (k + 1 == np ? 2u : 0u)};
+      tags += codec_piece_tags_bytes(l);
+      bodies += codec_piece_body_bytes(l);
+      if (l > kCodecSmallPiece) {
+        seqs += l / 3 + 2;
+        big.push_back(uint32_t(pieces.size()));
+      } else {
+        small.push_back(uint32_t(pieces.size()));
+      }
+      pieces.push_back(c);
+    }
+  }
+  const uint64_t np = pieces.size();
+  // device tables: pieces | payloads | small list | big list | tag_len | body_len | out_off
+  size_t off = 0;
+  auto carve = [&](size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const size_t o_pc = carve(np * sizeof(CodecPiece)), o_pay = carve(n * sizeof(CodecPayload)),
+               o_sl = carve(small.size() * 4 + 4), o_bl = carve(big.size() * 4 + 4), o_tl = carve(np * 4),
+               o_bo = carve(np * 4), o_oo = carve((n + 1) * 8);
+  SLATE_HIP(ctx->c_meta.ensure(off));
+  SLATE_HIP(ctx->c_tags.ensure(tags + 64));
+  SLATE_HIP(ctx->c_bodies.ensure(bodies + 64));
+  SLATE_HIP(ctx->c_seqs.ensure(seqs * kCodecSeqBytes + 64));
+  uint8_t* m = ctx->c_meta.as<uint8_t>();
+  auto* d_pc = reinterpret_cast<CodecPiece*>(m + o_pc);
+  auto* d_pay = reinterpret_cast<CodecPayload*>(m + o_pay);
+  auto* d_sl = reinterpret_cast<uint32_t*>(m + o_sl);
+  auto* d_bl = reinterpret_cast<uint32_t*>(m + o_bl);
+  auto* d_tl = reinterpret_cast<uint32_t*>(m + o_tl);
+  auto* d_bo = reinterpret_cast<uint32_t*>(m + o_bo);
+  auto* d_oo = reinterpret_cast<uint64_t*>(m + o_oo);
+  int s = ctx_h2d(ctx, d_pc, pieces.data(), np * sizeof(CodecPiece), st);
+  if (!s) s = ctx_h2d(ctx, d_pay, pay.data(), n * sizeof(CodecPayload), st);
+  if (!s && !small.empty()) s = ctx_h2d(ctx, d_sl, small.data(), small.size() * 4, st);
+  if (!s && !big.empty()) s = ctx_h2d(ctx, d_bl, big.data(), big.size() * 4, st);
+  if (s) return s;
+  SLATE_HIP(launch_codec_encode(st, codec, d_raw, d_pc, d_sl, uint32_t(small.size()), d_bl, uint32_t(big.size()),
+                                ctx->c_tags.as<uint8_t>(), d_tl, ctx->c_bodies.as<uint8_t>(), d_bo, ctx->c_seqs.p,
+                                ctx->num_cus));
+  std::vector<uint32_t> bl(np);
+  s = ctx_d2h(ctx, bl.data(), d_bo, np * 4, st);
+  if (s) return s;
+  // frame sizes (pc_frame_kernel's layout)
+  out_off.assign(n + 1, 0);
+  for (uint64_t p = 0; p < n; p++) {
+    uint64_t f = 0;
+    const uint32_t L = pay[p].len;
+    if (codec == SLATE_CODEC_LZ4) f = 7 + 8;
+    else if (codec == SLATE_CODEC_ZLIB) f = 2 + 4;
+    else f = 4 + 1 + (L < 256 ? 1 : (L < 65536 + 256 ? 2 : 4)) + 4;
+    for (uint32_t k = 0; k < pay[p].npieces; k++) {
+      const CodecPiece& c = pieces[pay[p].first + k];
+      const uint32_t b = bl[pay[p].first + k];
+      if (codec == SLATE_CODEC_ZLIB && b == kBodyRaw) return SLATE_E_HIP;  // deflate always fits its slot
+      const uint64_t body = b == kBodyRaw ? c.len : b;
+      if (codec == SLATE_CODEC_LZ4) f += c.len ? 4 + body : 0;
+      else if (codec == SLATE_CODEC_ZSTD) f += 3 + body;
+      else f += body;
+    }
+    out_off[p + 1] = out_off[p] + f + (with_crc ? 4 : 0);
+  }
+  SLATE_HIP(ctx->c_out.ensure(out_off[n] + kFramePad + 64));
+  s = ctx_h2d(ctx, d_oo, out_off.data(), (n + 1) * 8, st);
+  if (s) return s;
+  SLATE_HIP(launch_codec_frames(st, codec, d_raw, d_pay, uint32_t(n), d_pc, ctx->c_bodies.as<uint8_t>(), d_bo, d_oo,
+                                codec_frames(ctx), with_crc, ctx->num_cus));
+  SLATE_HIP(hipStreamSynchronize(st));
+  return SLATE_OK;
+}
+
+// compress.Encode (compression.go:80-116) of a host buffer.
 static int codec_encode_host(slate_ctx* ctx, int codec, const uint8_t* data, size_t n, std::vector<uint8_t>& out) {
   if (codec == SLATE_CODEC_NONE) {
     out.assign(data, data + n);
     return SLATE_OK;
   }
   if (codec == SLATE_CODEC_SNAPPY) return ctx_snappy_encode_host(ctx, data, n, out);
-  return SLATE_E_CODEC_UNSUPPORTED;
+  if (codec != SLATE_CODEC_LZ4 && codec != SLATE_CODEC_ZLIB && codec != SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(ctx->c_in.ensure(n + 64));
+  int s = ctx_h2d(ctx, ctx->c_in.p, data, n, ctx->stream);
+  if (s) return s;
+  const uint64_t start = 0, len = n;
+  std::vector<uint64_t> fo;
+  s = ctx_codec_frames(ctx, codec, ctx->c_in.as<uint8_t>(), &start, &len, 1, false, fo);
+  if (s) return s;
+  out.resize(fo[1]);
+  return ctx_d2h(ctx, out.data(), codec_frames(ctx), fo[1], ctx->stream);
 }
 
 // CRC32 verify + snappy.Decode of one `payload ‖ BE32 CRC` buffer (index,
@@ -207,10 +314,11 @@ int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, siz
   // in_off[2] | out_off[2] | row_base[2] | meta (16 B) | rows (16 B) | plan scratch
   constexpr size_t kHead = 10 * sizeof(uint64_t);
   SLATE_HIP(ctx->d_scratch.ensure(kHead + decode_scratch_bytes(1) + 64));
-  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  // 16 bytes of headroom: the payload kernel's CRC (wave_crc32) reads the aligned dword before it
+  SLATE_HIP(ctx->d_in.ensure(len + 16 + 64));
   uint64_t* u = ctx->d_scratch.as<uint64_t>();
-  const uint64_t hv[2] = {0, len};
-  SLATE_HIP(hipMemcpyAsync(ctx->d_in.p, buf, len, hipMemcpyHostToDevice, st));
+  const uint64_t hv[2] = {16, 16 + len};
+  SLATE_HIP(hipMemcpyAsync(ctx->d_in.as<uint8_t>() + 16, buf, len, hipMemcpyHostToDevice, st));
   SLATE_HIP(hipMemcpyAsync(u, hv, sizeof(hv), hipMemcpyHostToDevice, st));
   SLATE_HIP(launch_decode_plan(st, codec, ctx->d_in.as<uint8_t>(), u, 1, u + 2, u + 4,
                                reinterpret_cast<uint8_t*>(u) + kHead));
@@ -518,8 +626,22 @@ static int builder_flush(slate_sst_builder* b, bool final) {
     SLATE_HIP(hipStreamSynchronize(st));
     if (status) return SLATE_E_CAPACITY;
     mark("pack");
-    seg = std::make_shared<HostBytes>(total, ctx->seg_pool);
-    int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, total, st);
+    const uint8_t* src = ctx->e_e.as<uint8_t>();
+    if (b->cfg.codec != SLATE_CODEC_NONE) {
+      // LZ4 / Zlib / Zstd: the raw blocks (Data || offsets || count, before their CRC) framed
+      std::vector<uint64_t> rs(nb), rl(nb), fo;
+      for (uint64_t k = 0; k < nb; k++) {
+        rs[k] = out_off[k];
+        rl[k] = out_off[k + 1] - out_off[k] - 4;
+      }
+      int s = ctx_codec_frames(ctx, b->cfg.codec, src, rs.data(), rl.data(), nb, true, fo);
+      if (s) return s;
+      out_off.swap(fo);
+      src = codec_frames(ctx);
+      mark("codec frames");
+    }
+    seg = std::make_shared<HostBytes>(out_off[nb], ctx->seg_pool);
+    int s = ctx_d2h(ctx, seg->p, src, out_off[nb], st);
     mark("blocks D2H");
     if (s) return s;
   }
@@ -584,10 +706,6 @@ slate_sst_builder* slate_sst_builder_new(slate_ctx* ctx, const slate_sst_config*
   }
   if (cfg->codec < SLATE_CODEC_NONE || cfg->codec > SLATE_CODEC_ZSTD) {
     *status = SLATE_E_INVALID_CODEC;
-    return nullptr;
-  }
-  if (cfg->codec != SLATE_CODEC_NONE && cfg->codec != SLATE_CODEC_SNAPPY) {  // Zlib/LZ4/Zstd encode: not yet
-    *status = SLATE_E_CODEC_UNSUPPORTED;
     return nullptr;
   }
   slate_sst_builder* b = new slate_sst_builder();
@@ -782,6 +900,17 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
       st = ctx_crc32_host_buffer(ctx, comp.data(), comp.size(), &crc);
       if (st) { delete t; return st; }
       buf.insert(buf.end(), comp.begin(), comp.end());
+    } else if (b->cfg.codec != SLATE_CODEC_NONE) {
+      const uint64_t start = 0, len = nb + 2;
+      std::vector<uint64_t> fo;
+      st = ctx_codec_frames(ctx, b->cfg.codec, enc, &start, &len, 1, true, fo);
+      if (st) { delete t; return st; }
+      const size_t o = buf.size();
+      buf.resize(o + fo[1]);
+      st = ctx_d2h(ctx, buf.data() + o, codec_frames(ctx), fo[1], ctx->stream);
+      if (st) { delete t; return st; }
+      crc = ld_be32(buf.data() + buf.size() - 4);
+      buf.resize(buf.size() - 4);  // appended again below
     } else {
       st = ctx_crc32_device(ctx, enc, nb + 2, &crc);
       if (st) { delete t; return st; }
@@ -1130,7 +1259,6 @@ int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits,
                        uint8_t* out, size_t out_cap, size_t* out_len) {
   if (!ctx || (bits_len && !bits)) return SLATE_E_INVALID_ARG;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
   std::vector<uint8_t> raw(bits_len + 2), buf;
   raw[0] = uint8_t(num_probes >> 8);
   raw[1] = uint8_t(num_probes);
@@ -1205,7 +1333,6 @@ int slate_block_encode(slate_ctx* ctx, int codec, const uint8_t* data, size_t da
                        size_t n_offsets, uint8_t* out, size_t out_cap, size_t* out_len) {
   if (!ctx || (data_len && !data) || (n_offsets && !offsets)) return SLATE_E_INVALID_ARG;
   if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return SLATE_E_CODEC_UNSUPPORTED;
   std::vector<uint8_t> raw(data_len + 2 * n_offsets + 2), buf;
   if (data_len) memcpy(raw.data(), data, data_len);
   for (size_t i = 0; i < n_offsets; i++) st_be16(raw.data() + data_len + 2 * i, offsets[i]);

@@ -78,4 +78,39 @@ size_t kv_pick_scratch_bytes(uint64_t m);
 hipError_t launch_kv_pick_keys(hipStream_t st, const uint32_t* idx, uint64_t m, const uint8_t* keys,
                                const uint64_t* key_off, uint64_t* out_off, void* scratch, uint8_t* out);
 
+// compress.Encode for LZ4 / Zlib / Zstd (encode_codecs.hip).  A payload (a block, the filter, the
+// index) is cut into pieces of at most 64 KiB; pass 1 parses each piece with the golang/snappy
+// block encoder (tags into its slot), pass 2 transcodes the tags into the codec's body, pass 3
+// writes each payload's frame (+ BE32 CRC32 of the frame when asked).
+struct CodecPiece {
+  uint64_t raw;    // offset of the piece's bytes in the raw buffer
+  uint64_t tags;   // offset of its tag slot (codec_piece_tags_bytes(len))
+  uint64_t body;   // offset of its body slot (codec_piece_body_bytes(len))
+  uint64_t seqs;   // Zstd, pieces above 4 KiB: first Seq slot (len / 3 + 2 slots of 12 bytes)
+  uint32_t len;
+  uint32_t flags;  // bit 0: first piece of its payload, bit 1: last
+};
+struct CodecPayload {
+  uint64_t raw;     // offset of the payload in the raw buffer
+  uint32_t len;
+  uint32_t first;   // its first piece
+  uint32_t npieces;
+  uint32_t pad;
+};
+constexpr uint32_t kBodyRaw = 0xFFFFFFFFu;  // body_len: the piece goes out raw (LZ4 / Zstd) instead
+constexpr uint32_t kCodecPieceMax = 65536;
+constexpr uint32_t kCodecSmallPiece = 4096;
+__host__ __device__ inline uint32_t codec_body_cap(uint32_t len) { return len + len / 8 + 64; }
+size_t codec_piece_tags_bytes(uint32_t len);
+size_t codec_piece_body_bytes(uint32_t len);
+constexpr size_t kCodecSeqBytes = 12;
+hipError_t launch_codec_encode(hipStream_t st, int codec, const uint8_t* raw, const CodecPiece* pieces,
+                               const uint32_t* small_list, uint32_t n_small, const uint32_t* big_list, uint32_t n_big,
+                               uint8_t* tags, uint32_t* tag_len, uint8_t* bodies, uint32_t* body_len, void* big_seqs,
+                               int num_cus);
+// Frame sizes for out_off: header + pieces + trailer (+ 4 CRC), from the host's body_len copy.
+hipError_t launch_codec_frames(hipStream_t st, int codec, const uint8_t* raw, const CodecPayload* pay, uint32_t n,
+                               const CodecPiece* pieces, const uint8_t* bodies, const uint32_t* body_len,
+                               const uint64_t* out_off, uint8_t* out, bool with_crc, int num_cus);
+
 }  // namespace slate

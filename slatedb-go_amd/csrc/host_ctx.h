@@ -146,11 +146,14 @@ struct slate_ctx {
   DevBuf e_a, e_b, e_c, e_d, e_e, e_f, e_g, e_h, e_i, e_j;
   // Snappy encode: per-block slots, raw staging for oversized blocks, snappy LDS-free scratch
   DevBuf s_slots, s_raw, s_aux;
+  // LZ4 / Zlib / Zstd encode (encode_codecs.hip): piece tables, tag and body slots, sequences, frames
+  DevBuf c_meta, c_tags, c_bodies, c_seqs, c_out, c_in;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
   void release_all() {
     if (seg_pool) seg_pool->close();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
-                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &s_slots, &s_raw, &s_aux})
+                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &s_slots, &s_raw, &s_aux, &c_meta,
+                      &c_tags, &c_bodies, &c_seqs, &c_out, &c_in})
       b->release();
     for (PipeLane& l : lanes) l.release();
     h_small.release();
