@@ -20,6 +20,8 @@
 //   decode_large_kernel   same device code for blocks that exceed the fast
 //                         kernel's LDS budget (one wave per workgroup, ~150 KiB LDS)
 #include <cstdlib>
+#include <cstdio>
+#include <vector>
 
 #include "common.h"
 #include "kernels.h"
@@ -790,17 +792,22 @@ __global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restric
 }
 
 // CodecZstd sizes (oracle or_zstd_plan): one wave per block reading the frames from HBM.
+// list: the blocks to plan (list[0 .. *count)), or nullptr for all n.
 __global__ __launch_bounds__(256) void plan_zstd_kernel(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off, uint32_t n,
-                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz) {
+                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz,
+                                                        const uint32_t* list, const uint32_t* count) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kZsShared + 4 * kZsScratch];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t items = list ? *count : n;
+  if (blockIdx.x * 4 >= items) return;  // (workgroup-uniform) nothing to plan: skip the table build
   ZsShared* sh = reinterpret_cast<ZsShared*>(smem);
   ZsScratch* sc = reinterpret_cast<ZsScratch*>(smem + kZsShared + wave * kZsScratch);
   if (wave == 0) zs_shared_build(sh, sc, lane);
   __syncthreads();
   const uint32_t waves = gridDim.x * 4;
-  for (uint32_t b = blockIdx.x * 4 + wave; b < n; b += waves) {
+  for (uint32_t k = blockIdx.x * 4 + wave; k < items; k += waves) {
+    const uint32_t b = list ? list[k] : k;
     const uint64_t s0 = in_off[b], len = in_off[b + 1] - s0;
     uint64_t dl = 0;
     if (len >= 6 && len - 4 < 0x7FFFFFFFull) {
@@ -825,10 +832,6 @@ struct WaveBufs {
   ZsScratch* zss = nullptr;     // CodecZstd only: this wave's tables
   const ZsShared* zsh = nullptr;  // CodecZstd only: the workgroup's predefined tables
 };
-
-__device__ inline void write_meta(slate_block_meta* m, const slate_block_meta& v, int lane) {
-  if (lane == 0) *m = v;
-}
 
 // Returns false when the block does not fit this wave's LDS budget (caller defers it).
 // CK: the codec class compiled in (0: None/Snappy/LZ4, 1: Zlib, 2: Zstd), so each kernel
@@ -992,81 +995,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     write_meta(&a.meta[b], m, lane);
     return true;
   }
-  // ---- block.Decode structure checks (block.go:95-131)
-  if (n < 2) {
-    m.status = SLATE_E_BLOCK_UNCOMP_SMALL;
-    write_meta(&a.meta[b], m, lane);
-    return true;
-  }
-  uint32_t cnt = ld_be16(buf + n - 2);
-  int64_t osi = int64_t(n) - 2 - 2 * int64_t(cnt);
-  if (osi <= 0) {
-    m.status = SLATE_E_BLOCK_INDEX_OFFSET;
-    m.detail = int32_t(osi);
-    write_meta(&a.meta[b], m, lane);
-    return true;
-  }
-  uint16_t osi16 = uint16_t(osi);
-  uint32_t bad = 0xFFFFFFFFu;  // first offset index exceeding uint16(offsetStartIndex)
-  for (uint32_t i = lane; i < cnt; i += kWave) {
-    if (ld_be16(buf + osi + 2 * i) > osi16 && i < bad) bad = i;
-  }
-  for (int o = 32; o >= 1; o >>= 1) bad = min(bad, uint32_t(__shfl_xor(int(bad), o, 64)));
-  if (bad != 0xFFFFFFFFu) {
-    m.status = SLATE_E_BLOCK_OFFSET_BOUNDS;
-    m.aux = uint16_t(bad);
-    m.detail = ld_be16(buf + osi + 2 * bad);
-    write_meta(&a.meta[b], m, lane);
-    return true;
-  }
-  m.data_len = uint32_t(osi);
-  m.n_rows = uint16_t(cnt);
-  if (cnt == 0) {
-    m.status = SLATE_E_BLOCK_NO_OFFSETS;
-    write_meta(&a.meta[b], m, lane);
-    return true;
-  }
-  // FirstKey quirk (block.go:130-131): uint16 arithmetic, panics out of range
-  {
-    uint32_t off0 = ld_be16(buf + osi);
-    if (uint64_t(osi) - off0 < 2) {
-      m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
-      write_meta(&a.meta[b], m, lane);
-      return true;
-    }
-    uint16_t kl = ld_be16(buf + off0);
-    uint16_t lo = uint16_t(off0 + 2), hi = uint16_t(off0 + 2 + kl);
-    if (lo > hi || hi > n) {
-      m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
-      write_meta(&a.meta[b], m, lane);
-      return true;
-    }
-    m.aux = kl;
-  }
-  // ---- row descriptors
-  uint64_t rb = a.row_base[b];
-  uint32_t rcap = uint32_t(min(uint64_t(0xFFFFFFFFu), a.row_base[b + 1] - rb));
-  uint32_t nr = cnt;
-  if (nr > rcap) {
-    nr = rcap;
-    m.flags |= SLATE_BLKF_ROWS_TRUNCATED;
-  }
-  int fk = -1;
-  {
-    slate_row r0;
-    uint32_t sl0;
-    decode_row(buf, uint32_t(osi), ld_be16(buf + osi), -1, r0, &sl0);
-    if (r0.status == SLATE_OK) fk = int(sl0);
-  }
-  slate_row* grows = a.rows + rb;
-  if (dbg_bits(a) & 4) nr = 0;
-  for (uint32_t i = lane; i < nr; i += kWave) {
-    slate_row r;
-    uint32_t sl;
-    decode_row(buf, uint32_t(osi), ld_be16(buf + osi + 2 * i), i == 0 ? -1 : fk, r, &sl);
-    grows[i] = r;
-  }
-  write_meta(&a.meta[b], m, lane);
+  block_finish(a, b, buf, n, lane, m);
   return true;
 }
 
@@ -1112,6 +1041,31 @@ __global__ __launch_bounds__(kDecodeThreads) void decode_fast_kernel(DecodeArgs 
   }
 }
 
+// decode_fast_kernel over a list of blocks (list[0 .. *count)): the CodecZstd blocks the fast
+// path hands back (zstd_fast.hip).
+template <int CK>
+__global__ __launch_bounds__(kDecodeThreads) void decode_list_kernel(DecodeArgs a, const uint32_t* list,
+                                                                     const uint32_t* count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t items = *count;
+  if (blockIdx.x * (kDecodeThreads / 64) >= items) return;  // (workgroup-uniform) no block: skip the tables
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t in_cap = CK == 2 ? kZsFastInCap : kFastInCap, out_cap = CK == 2 ? kZsFastOutCap : kFastOutCap;
+  const uint32_t per_wave = in_cap + out_cap;
+  WaveBufs w{tab, smem + kTabBytes + wave * per_wave, smem + kTabBytes + wave * per_wave + in_cap, in_cap, out_cap};
+  if (CK == 1) zlib_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, kDecodeThreads / 64, wave, lane);
+  if (CK == 2) zstd_lds(w, smem + kTabBytes + (kDecodeThreads / 64) * per_wave, wave, lane);
+  const uint32_t waves = gridDim.x * (kDecodeThreads / 64);
+  for (uint32_t k = blockIdx.x * (kDecodeThreads / 64) + wave; k < items; k += waves) {
+    const uint32_t b = list[k];
+    if (!decode_block_wave<CK>(a, b, w, lane, true)) {
+      if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = b;
+    }
+  }
+}
+
 template <int CK>
 __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1151,7 +1105,10 @@ hipError_t decode_kernels_available() {
 
 size_t decode_scratch_bytes(uint32_t n) {
   size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
-  return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16;
+  return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16 +
+         // CodecZstd fast path: count, list, records, sequences
+         16 + align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
+         size_t(n) * kZsFastSeqs * sizeof(uint2);
 }
 
 static DecodeScratch carve(void* scratch, uint32_t n) {
@@ -1166,6 +1123,14 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   s.large_list = reinterpret_cast<uint32_t*>(p);
   p += align16(size_t(n) * sizeof(uint32_t));
   s.round_counter = reinterpret_cast<uint32_t*>(p);
+  p += 16;
+  s.zf.count = reinterpret_cast<uint32_t*>(p);
+  p += 16;
+  s.zf.list = reinterpret_cast<uint32_t*>(p);
+  p += align16(size_t(n) * sizeof(uint32_t));
+  s.zf.rec = reinterpret_cast<ZsFastRec*>(p);
+  p += size_t(n) * sizeof(ZsFastRec);
+  s.zf.seq = reinterpret_cast<uint2*>(p);
   s.tiles = uint32_t(tiles);
   return s;
 }
@@ -1177,8 +1142,13 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
   plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
   if (codec == SLATE_CODEC_ZLIB && n > 0)
     plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
-  if (codec == SLATE_CODEC_ZSTD && n > 0)
-    plan_zstd_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
+  if (codec == SLATE_CODEC_ZSTD && n > 0) {
+    // single-frame blocks with a content size: lane per block; the rest: the wave plan
+    (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
+    hipError_t e = launch_zstd_plan_fast(st, in, in_off, n, out_off, row_base, s.zf.list, s.zf.count);
+    if (e != hipSuccess) return e;
+    plan_zstd_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, s.zf.list, s.zf.count);
+  }
   scan_reduce_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
   scan_partials_kernel<<<1, kScanThreads, 0, st>>>(s.pa, s.pb, s.tiles);
   scan_apply_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
@@ -1281,8 +1251,32 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
     decode_fast_kernel<1><<<grid, kDecodeThreads, lds, st>>>(a);
     decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else if (a.codec == SLATE_CODEC_ZSTD) {
-    decode_fast_kernel<2><<<grid, kDecodeThreads, lds, st>>>(a);
+    // the fast path (zstd_fast.hip), then the exact path over the blocks it handed back
+    (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
+    hipError_t e = launch_zstd_fast(st, a, s.zf, num_cus);
+    if (e != hipSuccess) return e;
+    decode_list_kernel<2><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);
     decode_large_kernel<2><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+#ifdef SLATE_PROFILING_BUILD
+    if (getenv("SLATE_ZF_STATS")) {  // profiling variants only: how many blocks the fast path handed back
+      uint32_t cnt = 0;
+      std::vector<ZsFastRec> rec(a.n);
+      (void)hipMemcpyAsync(&cnt, s.zf.count, 4, hipMemcpyDeviceToHost, st);
+      (void)hipMemcpyAsync(rec.data(), s.zf.rec, a.n * sizeof(ZsFastRec), hipMemcpyDeviceToHost, st);
+      (void)hipStreamSynchronize(st);
+      std::vector<uint32_t> lst(cnt);
+      (void)hipMemcpy(lst.data(), s.zf.list, cnt * 4, hipMemcpyDeviceToHost);
+      uint32_t fast = 0, sum_fail = 0;
+      for (const ZsFastRec& r : rec) fast += (r.info >> 16) & kZfFast;
+      for (uint32_t b : lst) sum_fail += (rec[b].info >> 16) & kZfFast;
+      FILE* f = fopen(getenv("SLATE_ZF_STATS"), "w");  // the value names the output file
+      if (f) {
+        fprintf(f, "%u %u %u %u\n", a.n, fast, cnt, sum_fail);
+        for (uint32_t b : lst) fprintf(f, "%u %u\n", b, (rec[b].info >> 16) & kZfFast);
+        fclose(f);
+      }
+    }
+#endif
   } else {
     decode_fast_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a);
     decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);

@@ -53,6 +53,24 @@ __host__ __device__ inline uint32_t dbg_bits(const DecodeArgs& a) {
 #endif
 }
 
+// CodecZstd fast path (zstd_fast.hip): per block, what the lane-per-block parse found
+constexpr uint32_t kZsFastSeqs = 16;  // sequences per block on the fast path (more: exact path)
+constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4;
+struct ZsFastRec {
+  uint32_t lit;       // frame offset of the raw literals, or the RLE literal byte
+  uint32_t nlit;      // literal bytes
+  uint32_t produced;  // decoded bytes
+  uint32_t info;      // sequences | kZf* flags << 16 (kZfFast clear: the exact path decodes it)
+  uint32_t want;      // the frame's checksum (low 32 bits of XXH64) when kZfSum
+  uint32_t pad[3];
+};
+struct ZsFastArgs {
+  ZsFastRec* rec;   // n
+  uint2* seq;       // n * kZsFastSeqs: (ll | ml << 16, offset)
+  uint32_t* list;   // blocks for the exact path
+  uint32_t* count;
+};
+
 struct DecodeScratch {
   uint64_t* pa;
   uint64_t* pb;
@@ -60,6 +78,7 @@ struct DecodeScratch {
   uint32_t* large_list;
   uint32_t* round_counter;
   uint32_t tiles;
+  ZsFastArgs zf;
 };
 
 size_t decode_scratch_bytes(uint32_t n);
@@ -67,6 +86,11 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
+// CodecZstd fast path (zstd_fast.hip): plan sizes of single-frame blocks (the rest appended to
+// list for the wave plan); decode phases A-C (blocks for the exact path appended to z.list).
+hipError_t launch_zstd_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,
+                                 uint64_t* row_sz, uint32_t* list, uint32_t* count);
+hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
 // The rows of a decoded batch, densely in block order, written to `dense` (device memory or
 // page-locked host memory mapped for the device): block i's min(n_rows, capacity) rows when it
 // decoded (status OK), none otherwise; dense_off (n+1 u64) gets the exclusive scan of those

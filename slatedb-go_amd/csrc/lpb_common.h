@@ -31,35 +31,8 @@ struct CrcLeadTail {
 };
 static __constant__ CrcLeadTail g_crc_lt = CrcLeadTail();
 
-// Slicing-by-16 tables: t[k][b] = the CRC of byte b followed by k zero bytes (t[0] is the
-// classic table).  A 16-byte chunk then costs 16 independent lookups and one dependent
-// step, instead of four dependent rounds of four.
-struct CrcTables16 {
-  uint32_t t[16][256];
-  constexpr CrcTables16() : t{} {
-    for (uint32_t i = 0; i < 256; i++) {
-      uint32_t c = i;
-      for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
-      t[0][i] = c;
-    }
-    for (uint32_t i = 0; i < 256; i++)
-      for (int s = 1; s < 16; s++) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
-  }
-};
-static __constant__ CrcTables16 g_crc16 = CrcTables16();
-constexpr uint32_t kTab16Bytes = 16 * 256 * 4;
-
 __device__ __forceinline__ uint32_t crc16_chunk(const uint32_t* tab, uint32_t c, const v4u& v) {
-  const uint32_t x = c ^ v.x;
-  uint32_t r = tab[15 * 256 + (x & 0xff)] ^ tab[14 * 256 + ((x >> 8) & 0xff)] ^ tab[13 * 256 + ((x >> 16) & 0xff)] ^
-               tab[12 * 256 + (x >> 24)];
-  r ^= tab[11 * 256 + (v.y & 0xff)] ^ tab[10 * 256 + ((v.y >> 8) & 0xff)] ^ tab[9 * 256 + ((v.y >> 16) & 0xff)] ^
-       tab[8 * 256 + (v.y >> 24)];
-  r ^= tab[7 * 256 + (v.z & 0xff)] ^ tab[6 * 256 + ((v.z >> 8) & 0xff)] ^ tab[5 * 256 + ((v.z >> 16) & 0xff)] ^
-       tab[4 * 256 + (v.z >> 24)];
-  r ^= tab[3 * 256 + (v.w & 0xff)] ^ tab[2 * 256 + ((v.w >> 8) & 0xff)] ^ tab[1 * 256 + ((v.w >> 16) & 0xff)] ^
-       tab[v.w >> 24];
-  return r;
+  return crc16_step(tab, c, v.x, v.y, v.z, v.w);
 }
 
 // Rings and natural alignment.  gfx950 executes ds_read/ds_write of 8 or 16 bytes at any

@@ -10,6 +10,40 @@ static __constant__ CrcShift g_crc_shift = CrcShift();
 
 constexpr uint32_t kTabBytes = 4096;  // 4 x 256 u32 slicing tables in LDS
 
+// Slicing-by-16 tables: t[k][b] = the CRC of byte b followed by k zero bytes (t[0] is the
+// classic table).  A 16-byte chunk then costs 16 independent lookups and one dependent
+// step, instead of four dependent rounds of four.  Used by the lane-per-block kernels, one
+// block per lane (decode_lpb2.hip, zstd_fast.hip).
+struct CrcTables16 {
+  uint32_t t[16][256];
+  constexpr CrcTables16() : t{} {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; i++)
+      for (int s = 1; s < 16; s++) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+  }
+};
+static __constant__ CrcTables16 g_crc16 = CrcTables16();
+constexpr uint32_t kTab16Bytes = 16 * 256 * 4;
+
+// the CRC register after the 16 bytes (x, y, z, w) (little-endian dwords), tables in LDS
+__device__ __forceinline__ uint32_t crc16_step(const uint32_t* tab, uint32_t c, uint32_t vx, uint32_t vy, uint32_t vz,
+                                               uint32_t vw) {
+  const uint32_t x = c ^ vx;
+  uint32_t r = tab[15 * 256 + (x & 0xff)] ^ tab[14 * 256 + ((x >> 8) & 0xff)] ^ tab[13 * 256 + ((x >> 16) & 0xff)] ^
+               tab[12 * 256 + (x >> 24)];
+  r ^= tab[11 * 256 + (vy & 0xff)] ^ tab[10 * 256 + ((vy >> 8) & 0xff)] ^ tab[9 * 256 + ((vy >> 16) & 0xff)] ^
+       tab[8 * 256 + (vy >> 24)];
+  r ^= tab[7 * 256 + (vz & 0xff)] ^ tab[6 * 256 + ((vz >> 8) & 0xff)] ^ tab[5 * 256 + ((vz >> 16) & 0xff)] ^
+       tab[4 * 256 + (vz >> 24)];
+  r ^= tab[3 * 256 + (vw & 0xff)] ^ tab[2 * 256 + ((vw >> 8) & 0xff)] ^ tab[1 * 256 + ((vw >> 16) & 0xff)] ^
+       tab[vw >> 24];
+  return r;
+}
+
 __device__ inline void load_crc_tables(uint32_t* tab) {
   const uint32_t* src = &g_crc_tables.t[0][0];
   for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = src[i];

@@ -1,0 +1,784 @@
+// CodecZstd fast path: lane-per-block parse, wave-per-block build, lane-per-block checksum.
+//
+// compress.Decode(CodecZstd) (compression.go:146-153) is restated check for check by the
+// wave-per-block decoder (zstd.h, the exact path).  That path is latency-bound: one wave walks a
+// block's frame, FSE states and XXH64 as serial chains (20.6 ms per 1 M configs[4] blocks).
+// Most blocks an SST holds are one simple shape -- one frame, one compressed block, raw or RLE
+// literals, predefined or RLE sequence tables, a handful of sequences (configs[4]: 98.7 % of
+// blocks, ~7 sequences, ~1.9 KB of raw literals) -- and for that shape the work splits well:
+//
+//   A  zs_fast_parse_kernel  one LANE per block: the frame header, literal header and the whole
+//                            FSE sequence decode (64 blocks' state machines advance in one wave
+//                            instruction), every check of zs_frame/zs_block replicated; emits
+//                            the literal location and (ll, ml, offset) per sequence
+//   A2 zs_fast_crc_kernel    one LANE per block: the SST block's CRC32 over its encoded bytes,
+//                            streamed in 64-byte runs (slicing-by-16, 64 blocks per instruction)
+//   B  zs_fast_build_kernel  one WAVE per block (the next block's record in flight): stage the
+//                            frame in LDS, place all literal runs, then the matches in order (a
+//                            dword per lane), write the block back, block.Decode checks and rows
+//   C  zs_fast_sum_kernel    one LANE per block: the frame's XXH64 over the decoded block,
+//                            streamed in 64-byte runs (the four accumulators' serial chains of
+//                            64 blocks advance in one wave instruction)
+//
+// Anything outside the shape, or failing any check (A), or failing the frame checksum (C), is
+// appended to a list and decoded by the exact path afterwards (decode.hip decode_list_kernel),
+// which then writes that block's meta, bytes and rows; so every status and every byte of such a
+// block is the exact path's.  A CRC32 mismatch (A2) is reported directly: it is the first check
+// of both paths (block.go:83-89).
+// The plan (decoded sizes) has the same split: plan_zstd_fast_kernel (lane per block) for
+// single-frame blocks with a content size, the wave plan for the rest.
+#include "common.h"
+#include "kernels.h"
+#include "wave_crc.h"
+#include "zstd.h"
+#include "rows.h"
+
+namespace slate {
+
+namespace {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0xFFFFFFF0u;
+
+// per-lane LDS windows of phase A: the frame's first 32 bytes (three chunks: any alignment)
+// and 11 chunks around the sequences section (+16 bytes slack for 8-byte bit reads)
+constexpr uint32_t kZfHead = 48;
+constexpr uint32_t kZfTailChunks = 11;
+constexpr uint32_t kZfTail = 16 * kZfTailChunks + 16;
+constexpr uint32_t kZfLane = kZfHead + kZfTail;
+constexpr uint32_t kZfParseThreads = 256;
+// phase B: one wave per block, eight 4-wave workgroups per CU (64 VGPRs), the decoded block in LDS
+// with the frame staged around its tail (the bytes after the literals and the 16-byte phase: +256)
+constexpr uint32_t kZfBuildThreads = 256;
+constexpr uint32_t kZfIn = kZsFastInCap, kZfOut = kZsFastOutCap;
+constexpr uint32_t kZfOutLds = kZfOut + 256;
+// phase C: 64 bytes of LDS per lane; phase A2: the same + the slicing-by-16 CRC tables
+constexpr uint32_t kZfSumThreads = 256;
+constexpr uint32_t kZfCrcThreads = 512;
+
+struct ZfShared {
+  ZsShared fse;  // the predefined LL / ML / OF decoding tables
+  uint32_t ll_base[36], ml_base[53];
+  uint8_t ll_bits[36], ml_bits[53];
+};
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+  return (uint64_t(hi) << 32) | lo;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint64_t b = uniform64(reinterpret_cast<uint64_t>(base));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes < kOOB ? uint32_t(bytes) : kOOB);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0, int(n), 0x00020000);
+}
+__device__ __forceinline__ v4u bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void lds_put16(uint8_t* p, const v4u& v) { *reinterpret_cast<v4u*>(p) = v; }
+
+// wave-aggregated append of the lanes with `want` to list[*count ...]
+__device__ __forceinline__ void list_append(bool want, uint32_t item, uint32_t* list, uint32_t* count) {
+  const uint64_t m = __ballot(want);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == uint32_t(__builtin_ctzll(m))) base = atomicAdd(count, uint32_t(__builtin_popcountll(m)));
+  base = __shfl(base, __builtin_ctzll(m), 64);
+  if (want) list[base + uint32_t(__builtin_popcountll(m & ((uint64_t(1) << lane) - 1)))] = item;
+}
+
+// The frame head of one block (zs_header + the first block header, oracle zs_header /
+// zs_frame): bytes hb[i] = frame byte i for i < 32 (clen = frame bytes).  Fills the fields
+// and returns true when the frame has the fast shape's head: magic at 0, a valid header
+// without dictionary, exactly one block (last), the frame (and its checksum) ending at clen.
+struct ZfHead {
+  uint32_t body, bs, bt, checksum, has_fcs, bmax;
+  uint64_t fcs;
+};
+__device__ bool zf_head(const uint8_t* hb, uint32_t clen, ZfHead& h) {
+  if (clen < 4) return false;
+  const uint32_t magic = uint32_t(hb[0]) | (uint32_t(hb[1]) << 8) | (uint32_t(hb[2]) << 16) | (uint32_t(hb[3]) << 24);
+  if (magic != 0xFD2FB528u) return false;
+  const uint32_t n = clen - 4;  // zs_header(base, off + 4, n - 4)
+  if (n < 1) return false;
+  const uint32_t fhd = hb[4], fcsf = fhd >> 6, ss = (fhd >> 5) & 1, dif = fhd & 3;
+  if (fhd & 8) return false;
+  const uint32_t dsz = dif == 3 ? 4 : dif, fl = fcsf == 0 ? ss : (2u << (fcsf - 1));
+  const uint32_t hsize = 1 + (ss ? 0 : 1) + dsz + fl;
+  if (n < hsize) return false;
+  uint32_t q = 5;
+  uint64_t window = 0;
+  if (!ss) {
+    const uint32_t wd = hb[q++], wl = 10 + (wd >> 3);
+    window = (1ull << wl) + ((1ull << wl) >> 3) * (wd & 7);
+  }
+  uint32_t dict = 0;
+  for (uint32_t i = 0; i < dsz; i++) dict |= uint32_t(hb[q++]) << (8 * i);
+  if (dict != 0) return false;
+  uint64_t f = 0;
+  for (uint32_t i = 0; i < fl; i++) f |= uint64_t(hb[q + i]) << (8 * i);
+  if (fl == 2) f += 256;
+  if (ss) window = f;
+  if (window > kZsMaxWindow) return false;
+  h.has_fcs = fl != 0;
+  h.fcs = f;
+  h.checksum = (fhd >> 2) & 1;
+  h.bmax = uint32_t(window < kZsBlockMax ? window : kZsBlockMax);
+  uint32_t p = 4 + hsize;  // <= 18
+  if (clen - p < 3) return false;
+  const uint32_t bh = uint32_t(hb[p]) | (uint32_t(hb[p + 1]) << 8) | (uint32_t(hb[p + 2]) << 16);
+  p += 3;
+  h.bt = (bh >> 1) & 3;
+  h.bs = bh >> 3;
+  if (!(bh & 1) || h.bt == 3 || h.bs > h.bmax) return false;
+  const uint32_t adv = h.bt == 1 ? 1 : h.bs;
+  if (clen - p < adv) return false;
+  h.body = p;
+  p += adv;
+  if (h.checksum) {
+    if (clen - p < 4) return false;
+    p += 4;
+  }
+  return p == clen;
+}
+
+// --------------------------------------------------------------- bits of phase A
+// The sequences bitstream in a lane's tail window (zs_peek / zs_bits over LDS).
+struct ZfBits {
+  const uint8_t* buf;
+  int64_t S, bp;
+};
+__device__ __forceinline__ uint32_t zf_rd(ZfBits& z, uint32_t k) {
+  const uint32_t v = uint32_t(zs_peek(z.buf, z.S, z.bp, k));
+  z.bp -= k;
+  return v;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------- plan
+// Lane per block: single-frame blocks with a content size get or_zstd_plan's size here
+// (min(content size, the block's bound)); every other block goes to `list` for the wave plan.
+__global__ __launch_bounds__(kZfParseThreads) void plan_zstd_fast_kernel(const uint8_t* __restrict__ in,
+                                                                         const uint64_t* __restrict__ in_off, uint32_t n,
+                                                                         uint64_t* __restrict__ out_sz,
+                                                                         uint64_t* __restrict__ row_sz, uint32_t* list,
+                                                                         uint32_t* count) {
+  __shared__ __attribute__((aligned(16))) uint8_t heads[kZfParseThreads * kZfHead];
+  uint8_t* hb0 = heads + threadIdx.x * kZfHead;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); r0 < n; r0 += stride) {
+    const uint32_t b = r0 + (threadIdx.x & 63);
+    const uint32_t rend = min(r0 + 64, n);
+    const uint8_t* lo = in + in_off[r0];
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(lo) & ~uintptr_t(15));
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(base, align16(uint64_t((in + in_off[rend]) - base)));
+    bool fast = false;
+    uint64_t dl = 0;
+    uint32_t shift = 0, rel = kOOB;
+    uint64_t len = 0;
+    if (b < n) {
+      const uint64_t s0 = in_off[b];
+      len = in_off[b + 1] - s0;
+      shift = uint32_t(reinterpret_cast<uintptr_t>(in + s0) & 15);
+      if (len >= 6 && len - 4 < 0x7FFFFFFFull) rel = uint32_t(((in + s0) - shift) - base);
+    }
+    const v4u c0 = bload(R, rel), c1 = bload(R, rel == kOOB ? kOOB : rel + 16), c2 = bload(R, rel == kOOB ? kOOB : rel + 32);
+    lds_put16(hb0, c0);
+    lds_put16(hb0 + 16, c1);
+    lds_put16(hb0 + 32, c2);
+    if (rel != kOOB) {
+      ZfHead h;
+      if (zf_head(hb0 + shift, uint32_t(len - 4), h) && h.has_fcs) {
+        const uint64_t bound = h.bt == 2 ? h.bmax : h.bs;
+        dl = h.fcs < bound ? h.fcs : bound;
+        fast = true;
+      }
+    }
+    if (fast) {
+      out_sz[b] = align16(dl);
+      row_sz[b] = row_capacity(dl);
+    }
+    list_append(b < n && !fast, b, list, count);
+  }
+}
+
+// ------------------------------------------------------------------------------- phase A
+__global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  ZfShared* sh = reinterpret_cast<ZfShared*>(smem);
+  uint8_t* lanes = smem + ((sizeof(ZfShared) + 15) & ~size_t(15));
+  {
+    // the predefined tables (wave 0, lane 0), with a temporary ZsScratch over the lane windows
+    if (threadIdx.x < 64) zs_shared_build(&sh->fse, reinterpret_cast<ZsScratch*>(lanes), int(threadIdx.x));
+    for (uint32_t i = threadIdx.x; i < 36; i += blockDim.x) {
+      sh->ll_base[i] = kZsLLBase[i];
+      sh->ll_bits[i] = kZsLLBits[i];
+    }
+    for (uint32_t i = threadIdx.x; i < 53; i += blockDim.x) {
+      sh->ml_base[i] = kZsMLBase[i];
+      sh->ml_bits[i] = kZsMLBits[i];
+    }
+    __syncthreads();
+  }
+  uint8_t* hb0 = lanes + threadIdx.x * kZfLane;
+  uint8_t* tb0 = hb0 + kZfHead;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); r0 < a.n; r0 += stride) {
+    const uint32_t b = r0 + (threadIdx.x & 63);
+    const uint32_t rend = min(r0 + 64, a.n);
+    const uint8_t* lo = a.in + a.in_off[r0];
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(lo) & ~uintptr_t(15));
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(base, align16(uint64_t((a.in + a.in_off[rend]) - base)));
+    ZsFastRec rec{0, 0, 0, 0, 0, {0, 0, 0}};
+    bool ok = false;
+    uint32_t shift = 0, rel = kOOB, clen = 0, cap = 0;
+    if (b < a.n) {
+      const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
+      shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + s0) & 15);
+      const uint64_t cap64 = a.out_off[b + 1] - a.out_off[b];
+      // the exact path's staging limits (decode_block_wave): beyond them it is not this shape
+      if (len >= 6 && shift + len <= kZfIn && cap64 <= kZfOut) {
+        rel = uint32_t(((a.in + s0) - shift) - base);
+        clen = uint32_t(len - 4);
+        cap = uint32_t(cap64);
+        ok = true;
+      }
+    }
+    {
+      const v4u c0 = bload(R, rel), c1 = bload(R, ok ? rel + 16 : kOOB), c2 = bload(R, ok ? rel + 32 : kOOB);
+      lds_put16(hb0, c0);
+      lds_put16(hb0 + 16, c1);
+      lds_put16(hb0 + 32, c2);
+    }
+    const uint8_t* hb = hb0 + shift;
+    ZfHead h{};
+    ok = ok && zf_head(hb, clen, h) && h.bt == 2;
+    // ---- literals section header (zs_block), raw or RLE literals only
+    uint32_t nlit = 0, pos = 0, lit = 0, rle = 0;
+    const uint32_t nb = h.bs, body = h.body;
+    if (ok) {
+      const uint32_t b0 = hb[body], type = b0 & 3, sf = (b0 >> 2) & 3;
+      uint32_t hs;
+      if (type > 1) {
+        ok = false;
+        hs = 1;
+      } else if (sf == 1) {
+        hs = 2;
+        ok = nb >= 2;
+        nlit = (b0 >> 4) + (uint32_t(hb[body + 1]) << 4);
+      } else if (sf == 3) {
+        hs = 3;
+        ok = nb >= 3;
+        nlit = (b0 >> 4) + (uint32_t(hb[body + 1]) << 4) + (uint32_t(hb[body + 2]) << 12);
+      } else {
+        hs = 1;
+        nlit = b0 >> 3;
+      }
+      ok = ok && nb >= 1 && nlit <= h.bmax && (type == 0 ? nb - hs >= nlit : nb - hs >= 1) && nlit <= cap;
+      rle = type == 1;
+      lit = rle ? uint32_t(hb[body + hs]) : body + hs;
+      pos = hs + (type == 0 ? nlit : 1);
+      ok = ok && pos < nb;
+    }
+    // ---- the sequences section: 11 chunks from the one holding its first byte
+    const uint32_t s = body + pos;  // frame offset of the sequences section
+    const uint32_t c_lo = (shift + s) >> 4;
+    const uint32_t wend = 16 * (c_lo + kZfTailChunks) - shift;  // frame offset past the window
+    ok = ok && body + nb + (h.checksum ? 4u : 0u) <= wend;
+    {
+      v4u t[kZfTailChunks];
+#pragma unroll
+      for (uint32_t k = 0; k < kZfTailChunks; k++) t[k] = bload(R, ok ? rel + 16 * (c_lo + k) : kOOB);
+#pragma unroll
+      for (uint32_t k = 0; k < kZfTailChunks; k++) lds_put16(tb0 + 16 * k, t[k]);
+    }
+    const uint8_t* tb = tb0 + shift - 16 * c_lo;  // tb[i] = frame byte i for i in [s, wend)
+    uint32_t nseq = 0, produced = 0;
+    if (ok) {
+      const uint32_t sn = nb - pos;
+      const uint32_t c0 = tb[s];
+      uint32_t sp;
+      if (c0 < 128) {
+        nseq = c0;
+        sp = 1;
+      } else if (c0 < 255) {
+        ok = sn >= 2;
+        nseq = ((c0 - 128) << 8) + tb[s + 1];
+        sp = 2;
+      } else {
+        ok = sn >= 3;
+        nseq = uint32_t(tb[s + 1]) + (uint32_t(tb[s + 2]) << 8) + 0x7F00;
+        sp = 3;
+      }
+      ok = ok && nseq <= kZsFastSeqs;
+      uint32_t lp = 0, o = 0;
+      const uint32_t lbase = cap - nlit;
+      if (ok && nseq == 0) {
+        ok = sp == sn;
+      } else if (ok) {
+        ok = sp < sn;
+        const uint32_t modes = ok ? uint32_t(tb[s + sp++]) : 0u;
+        ok = ok && !(modes & 3);
+        // Symbol_Compression_Mode: predefined (0) or RLE (1) per table, in LL, OF, ML order
+        uint32_t m_ll = modes >> 6, m_of = (modes >> 4) & 3, m_ml = (modes >> 2) & 3;
+        ok = ok && m_ll <= 1 && m_of <= 1 && m_ml <= 1;
+        uint32_t r_ll = 0, r_of = 0, r_ml = 0;
+        if (ok && m_ll) {
+          ok = sn - sp >= 1 && tb[s + sp] <= 35;
+          r_ll = tb[s + sp++];
+        }
+        if (ok && m_of) {
+          ok = sn - sp >= 1 && tb[s + sp] <= 31;
+          r_of = tb[s + sp++];
+        }
+        if (ok && m_ml) {
+          ok = sn - sp >= 1 && tb[s + sp] <= 52;
+          r_ml = tb[s + sp++];
+        }
+        // zs_bstart
+        const uint32_t bn = sn - sp;
+        const uint32_t last = ok && bn ? uint32_t(tb[s + sn - 1]) : 0u;
+        ok = ok && last != 0;
+        ZfBits bits{tb0, 8 * int64_t(shift + s + sp - 16 * c_lo), ok ? 8 * int64_t(bn - 1) + (31 - __builtin_clz(last)) : 0};
+        uint32_t sll = 0, sof = 0, sml = 0;
+        if (ok) {
+          sll = zf_rd(bits, m_ll ? 0 : 6);
+          sof = zf_rd(bits, m_of ? 0 : 5);
+          sml = zf_rd(bits, m_ml ? 0 : 6);
+        }
+        uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+        uint2* seqs = z.seq + size_t(b) * kZsFastSeqs;
+        for (uint32_t i = 0; ok && i < nseq; i++) {
+          const ZsFse ell = m_ll ? ZsFse{uint8_t(r_ll), 0, 0} : sh->fse.ll[sll];
+          const ZsFse eof = m_of ? ZsFse{uint8_t(r_of), 0, 0} : sh->fse.of[sof];
+          const ZsFse eml = m_ml ? ZsFse{uint8_t(r_ml), 0, 0} : sh->fse.ml[sml];
+          const uint32_t ofc = eof.sym, llc = ell.sym, mlc = eml.sym;
+          if (ofc > 31) {
+            ok = false;
+            break;
+          }
+          uint64_t ofv = (1ull << ofc);
+          if (ofc > 24) {
+            const uint32_t hi = zf_rd(bits, ofc - 24);
+            ofv += (uint64_t(hi) << 24) + zf_rd(bits, 24);
+          } else {
+            ofv += zf_rd(bits, ofc);
+          }
+          const uint32_t ml = sh->ml_base[mlc] + zf_rd(bits, sh->ml_bits[mlc]);
+          const uint32_t ll = sh->ll_base[llc] + zf_rd(bits, sh->ll_bits[llc]);
+          uint64_t offv;
+          if (ofv > 3) {
+            offv = ofv - 3;
+            rep2 = rep1;
+            rep1 = rep0;
+            rep0 = uint32_t(offv);
+          } else {
+            const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1u : 0u);
+            offv = idx == 3 ? uint64_t(rep0) - 1 : (idx == 0 ? rep0 : idx == 1 ? rep1 : rep2);
+            if (offv == 0) offv = 1;
+            if (idx >= 2) rep2 = rep1;
+            if (idx >= 1) {
+              rep1 = rep0;
+              rep0 = uint32_t(offv);
+            }
+          }
+          if (i + 1 < nseq) {
+            sll = uint32_t(ell.base) + zf_rd(bits, ell.nb);
+            sml = uint32_t(eml.base) + zf_rd(bits, eml.nb);
+            sof = uint32_t(eof.base) + zf_rd(bits, eof.nb);
+          }
+          if (bits.bp < 0 || ll > nlit - lp || uint64_t(o) + ll + ml > h.bmax || uint64_t(o) + ll + ml > cap ||
+              uint64_t(o) + ll + ml > uint64_t(lbase) + lp + ll) {
+            ok = false;
+            break;
+          }
+          lp += ll;
+          o += ll;
+          if (offv > o) {  // fstart = 0: one frame
+            ok = false;
+            break;
+          }
+          seqs[i] = make_uint2(ll | (ml << 16), uint32_t(offv));
+          o += ml;
+        }
+        ok = ok && bits.bp == 0;
+      }
+      const uint32_t rest = nlit - lp;
+      ok = ok && uint64_t(o) + rest <= h.bmax && uint64_t(o) + rest <= cap;
+      produced = o + rest;
+      ok = ok && (!h.has_fcs || uint64_t(produced) == h.fcs);
+    }
+    if (ok) {
+      rec.lit = lit;
+      rec.nlit = nlit;
+      rec.produced = produced;
+      rec.info = nseq | ((kZfFast | (rle ? kZfRle : 0u) | (h.checksum ? kZfSum : 0u)) << 16);
+      const uint32_t q = body + nb;
+      rec.want = h.checksum ? uint32_t(tb[q]) | (uint32_t(tb[q + 1]) << 8) | (uint32_t(tb[q + 2]) << 16) |
+                                  (uint32_t(tb[q + 3]) << 24)
+                            : 0u;
+    }
+    if (b < a.n) z.rec[b] = rec;
+    list_append(b < a.n && !ok, b, z.list, z.count);
+  }
+}
+
+// ------------------------------------------------------------------------------- phase B
+namespace {
+struct ZfBlock {                      // what phase B needs of one block, loaded one block ahead
+  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle;
+  const uint8_t* gin;
+};
+__device__ __forceinline__ ZfBlock zf_block(const DecodeArgs& a, const ZsFastArgs& z, uint32_t b) {
+  ZfBlock k{};
+  k.b = b;
+  if (b >= a.n) return k;
+  const ZsFastRec rec = z.rec[b];
+  const uint32_t fl = __builtin_amdgcn_readfirstlane(rec.info >> 16);
+  k.fast = fl & kZfFast;
+  if (!k.fast) return k;
+  const uint64_t s0 = a.in_off[b];
+  k.gin = a.in + s0;
+  k.len = uint32_t(a.in_off[b + 1] - s0);
+  k.shift = uint32_t(reinterpret_cast<uintptr_t>(k.gin) & 15);
+  k.cap = uint32_t(a.out_off[b + 1] - a.out_off[b]);
+  k.nseq = __builtin_amdgcn_readfirstlane(rec.info & 0xFFFFu);
+  k.nlit = __builtin_amdgcn_readfirstlane(rec.nlit);
+  k.produced = __builtin_amdgcn_readfirstlane(rec.produced);
+  k.lit = __builtin_amdgcn_readfirstlane(rec.lit);
+  k.rle = fl & kZfRle;
+  return k;
+}
+// the block's sequences, lane i holding sequence i
+__device__ __forceinline__ uint2 zf_seqs(const ZsFastArgs& z, const ZfBlock& k, uint32_t lane) {
+  return (k.fast && lane < k.nseq) ? z.seq[size_t(k.b) * kZsFastSeqs + lane] : make_uint2(0, 0);
+}
+}  // namespace
+
+// One wave per block, the next block's record and sequences loaded while this one is built.  The frame is staged in the output buffer at the 16-byte phase of its address, placed
+// so that its raw literals start at lb >= cap - nlit: phase A checked zs_block's rule that the
+// write cursor never passes the unread literals (o + ml <= cap - nlit + lp before each literal
+// run), so the runs can be moved down in place, in order.
+__global__ __launch_bounds__(kZfBuildThreads, 8) void zs_fast_build_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = threadIdx.x >> 6;
+  uint8_t* wout = smem + wave * kZfOutLds;
+  const uint32_t waves = gridDim.x * (kZfBuildThreads / 64);
+  // profiling ablations (SLATE_DEBUG_MODE, profiling variants only): 1<<20 no block_finish,
+  // 1<<21 no matches, 1<<22 no literal runs, 1<<24 no XXH64 rounds, 1<<26 no hand-back from C
+  const uint32_t dbg = dbg_bits(a);
+  ZfBlock cur = zf_block(a, z, blockIdx.x * (kZfBuildThreads / 64) + wave);
+  uint2 sq = zf_seqs(z, cur, lane);
+  ZfBlock nxt = zf_block(a, z, cur.b + waves);
+  for (; cur.b < a.n; cur = nxt, nxt = zf_block(a, z, nxt.b + waves)) {
+    const uint2 seq = sq;
+    sq = zf_seqs(z, nxt, lane);  // in flight while this block is built
+    if (!cur.fast) continue;
+    const uint32_t lbase = cur.cap - cur.nlit, lit = cur.lit, shift = cur.shift;
+    // frame byte 0 at wout[F], F = 16-aligned base + shift, literals at lb = F + lit >= lbase
+    uint32_t base16 = 16;
+    if (!cur.rle && lbase > lit + shift + 16) base16 = (lbase - lit - shift + 15) & ~15u;
+    const uint32_t F = base16 + shift, lb = F + lit;
+    {
+      const uint32_t chunks = (shift + cur.len + 15) / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(cur.gin - shift);
+      uint4* dst = reinterpret_cast<uint4*>(wout + base16);
+      for (uint32_t c = lane; c < chunks; c += kWave) dst[c] = src[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    zs_sync();
+    slate_block_meta m{};  // (the block's CRC32 held: phase A2)
+    // sequence lane i: (ll, ml, offset); exclusive scans give each one's literal source and
+    // output position
+    const uint32_t nseq = cur.nseq, nlit = cur.nlit;
+    const uint32_t ll = seq.x & 0xFFFFu, ml = seq.x >> 16, off = seq.y;
+    uint32_t x_ll = ll, x_out = ll + ml;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y1 = __shfl_up(x_ll, d, 64), y2 = __shfl_up(x_out, d, 64);
+      if (int(lane) >= d) {
+        x_ll += y1;
+        x_out += y2;
+      }
+    }
+    const uint32_t lsrc = x_ll - ll, dpos = x_out - ll - ml;  // exclusive
+    const uint32_t tot_ll = __shfl(x_ll, 63, 64), tot_out = __shfl(x_out, 63, 64);
+    const uint32_t rle4 = (lit & 0xFF) * 0x01010101u;
+    // Literal runs of every sequence and the trailing run, in order, a dword per lane.  A run
+    // moves down (destination <= source: the cursor rule), so a lane reads its source dword
+    // before any lane writes over it; the (up to three) bytes a run's first or last dword
+    // spills over lie in the neighbouring match (>= 3 bytes), written afterwards, or past the
+    // block, and never reach the literals still to be moved (the cursor rule again, ml >= 3).
+    for (uint32_t i = 0; i <= nseq && !(dbg & (1u << 22)); i++) {
+      const uint32_t L = i < nseq ? __builtin_amdgcn_readlane(ll, i) : nlit - tot_ll;
+      if (L == 0) continue;
+      const uint32_t src = i < nseq ? __builtin_amdgcn_readlane(lsrc, i) : tot_ll;
+      const uint32_t dst = i < nseq ? __builtin_amdgcn_readlane(dpos, i) : tot_out;
+      const int32_t delta = int32_t(lb + src) - int32_t(dst);  // output byte p = wout[p + delta]
+      for (uint32_t w = (dst & ~3u) + 4 * lane; w < dst + L; w += 4 * kWave) {
+        const uint32_t v = cur.rle ? rle4 : lds_u32(wout, int32_t(w) + delta);
+        __builtin_amdgcn_wave_barrier();
+        *reinterpret_cast<uint32_t*>(wout + w) = v;
+      }
+    }
+    zs_sync();
+    // Matches in order: each reads only bytes before its own position.  Non-overlapping ones
+    // (offset >= length) a dword per lane, the edge dwords merged with the bytes around the
+    // match; overlapping ones a byte per lane.
+    for (uint32_t i = 0; i < nseq && !(dbg & (1u << 21)); i++) {
+      const uint32_t M = __builtin_amdgcn_readlane(ml, i), O = __builtin_amdgcn_readlane(off, i);
+      const uint32_t mp = __builtin_amdgcn_readlane(dpos, i) + __builtin_amdgcn_readlane(ll, i);
+      if (O >= M) {
+        const uint32_t me = mp + M;
+        const uint32_t lo_keep = (1u << (8 * (mp & 3))) - 1u, hi_keep = (me & 3) ? ~((1u << (8 * (me & 3))) - 1u) : 0u;
+        for (uint32_t w = (mp & ~3u) + 4 * lane; w < me; w += 4 * kWave) {
+          uint32_t v = lds_u32(wout, int32_t(w) - int32_t(O));
+          const uint32_t keep = (w < mp ? lo_keep : 0u) | (w + 4 > me ? hi_keep : 0u);
+          if (keep) v = (v & ~keep) | (*reinterpret_cast<const uint32_t*>(wout + w) & keep);
+          *reinterpret_cast<uint32_t*>(wout + w) = v;
+        }
+      } else {
+        for (uint32_t j = lane; j < M; j += kWave) wout[mp + j] = wout[mp - O + (j % O)];
+      }
+      zs_sync();
+    }
+    const uint32_t n = cur.produced;
+    {
+      uint8_t* gout = a.out + a.out_off[cur.b];
+      const uint32_t oc = (n + 15) / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(wout);
+      for (uint32_t c = lane; c < oc; c += kWave) reinterpret_cast<uint4*>(gout)[c] = src[c];
+    }
+    if (dbg & (1u << 20)) write_meta(&a.meta[cur.b], m, int(lane));
+    else block_finish(a, cur.b, wout, n, int(lane), m);
+  }
+}
+
+// ------------------------------------------------------------------------------- phase C
+// The frame checksum of each fast block whose CRC32 held (phase B), lane per block: XXH64 (seed
+// 0) of the decoded block, whose four accumulators' serial chains advance for 64 blocks in one
+// wave instruction.  A mismatch goes to the exact path, which reports it.  Round of 64 blocks:
+// each iteration brings the next 64 bytes of every block with transposed loads (in load j,
+// lanes 4i..4i+3 read one 64-byte run of block 16j+i) issued one iteration ahead into
+// registers; the loading lanes put them into the owner's LDS slot, and every lane runs two
+// 32-byte stripes.
+namespace {
+struct ZfGroup {
+  v4u p[4];
+};
+__device__ __forceinline__ ZfGroup zf_load_group(__amdgpu_buffer_rsrc_t R, uint32_t t, uint32_t rel, uint32_t groups,
+                                                 uint32_t lane) {
+  ZfGroup g;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+    const uint32_t g_o = __shfl(groups, int(o), 64), rel_o = __shfl(rel, int(o), 64);
+    g.p[j] = bload(R, t < g_o ? rel_o + 64 * t + 16 * c : kOOB);
+  }
+  return g;
+}
+__device__ __forceinline__ void zf_commit_group(const ZfGroup& g, uint8_t* slots0, uint32_t t, uint32_t groups,
+                                                uint32_t lane) {
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+    if (t < uint32_t(__shfl(groups, int(o), 64))) lds_put16(slots0 + o * 64 + 16 * c, g.p[j]);
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(kZfSumThreads) void zs_fast_sum_kernel(DecodeArgs a, ZsFastArgs z) {
+  __shared__ __attribute__((aligned(16))) uint8_t slots[kZfSumThreads * 64];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+  uint8_t* slots0 = slots + wave_lane0 * 64;
+  const uint8_t* mine = slots0 + lane * 64;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
+    const uint32_t b = r0 + lane;
+    const uint32_t rend = min(r0 + 64, a.n);
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(a.out + a.out_off[r0], a.out_off[rend] - a.out_off[r0]);
+    uint32_t orel = 0, len = 0, want = 0;
+    bool act = false;
+    if (b < a.n) {
+      const ZsFastRec rec = z.rec[b];
+      const uint32_t fl = rec.info >> 16;
+      act = (fl & kZfFast) && (fl & kZfSum) && a.meta[b].status != SLATE_E_BLOCK_CHECKSUM;
+      len = act ? rec.produced : 0u;
+      want = rec.want;
+      orel = uint32_t(a.out_off[b] - a.out_off[r0]);
+    }
+    const uint32_t groups = (len + 63) / 64, stripes = len / 32;
+    uint64_t v0 = kX64P1 + kX64P2, v1 = kX64P2, v2 = 0, v3 = 0ull - kX64P1;
+    ZfGroup g = zf_load_group(R, 0, orel, groups, lane);
+    for (uint32_t t = 0; __ballot(t < groups); t++) {
+      zf_commit_group(g, slots0, t, groups, lane);
+      g = zf_load_group(R, t + 1, orel, groups, lane);  // in flight during this iteration
+      zs_sync();
+#pragma unroll
+      for (uint32_t h = 0; h < 2; h++) {
+        if (2 * t + h < stripes && !(dbg_bits(a) & (1u << 24))) {
+          const uint64_t* w = reinterpret_cast<const uint64_t*>(mine + 32 * h);
+          v0 = x64round(v0, w[0]);
+          v1 = x64round(v1, w[1]);
+          v2 = x64round(v2, w[2]);
+          v3 = x64round(v3, w[3]);
+        }
+      }
+      zs_sync();
+    }
+    bool bad = false;
+    if (act) {
+      // the tail (< 32 bytes) lies in the last group, still in this lane's slot
+      uint64_t hh;
+      if (len >= 32) {
+        hh = x64rotl(v0, 1) + x64rotl(v1, 7) + x64rotl(v2, 12) + x64rotl(v3, 18);
+        hh = (hh ^ x64round(0, v0)) * kX64P1 + kX64P4;
+        hh = (hh ^ x64round(0, v1)) * kX64P1 + kX64P4;
+        hh = (hh ^ x64round(0, v2)) * kX64P1 + kX64P4;
+        hh = (hh ^ x64round(0, v3)) * kX64P1 + kX64P4;
+      } else {
+        hh = kX64P5;
+      }
+      hh += len;
+      uint32_t i = len & ~31u;
+      const uint8_t* tail = mine - 64 * ((len - 1) / 64);  // tail[i] = decoded byte i (len > 0)
+      for (; i + 8 <= len; i += 8)
+        hh = x64rotl(hh ^ x64round(0, *reinterpret_cast<const uint64_t*>(tail + i)), 27) * kX64P1 + kX64P4;
+      if (i + 4 <= len) {
+        hh = x64rotl(hh ^ uint64_t(*reinterpret_cast<const uint32_t*>(tail + i)) * kX64P1, 23) * kX64P2 + kX64P3;
+        i += 4;
+      }
+      for (; i < len; i++) hh = x64rotl(hh ^ uint64_t(tail[i]) * kX64P5, 11) * kX64P1;
+      hh ^= hh >> 33;
+      hh *= kX64P2;
+      hh ^= hh >> 29;
+      hh *= kX64P3;
+      hh ^= hh >> 32;
+      bad = uint32_t(hh) != want;
+    }
+    list_append(bad && !(dbg_bits(a) & (1u << 26)), b, z.list, z.count);
+  }
+}
+
+// ------------------------------------------------------------------------------- phase A2
+// The SST block CRC32 (block.go:83-89: the first check of block.Decode) of each block phase A
+// took, lane per block, before anything is built: slicing-by-16 over whole 16-byte chunks, the
+// payload's first and last chunk byte by byte, the encoded bytes streamed in 64-byte runs as in
+// phase C.  A mismatch is reported here, as the exact path would (status only), and the block
+// leaves the fast path.
+__global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  {
+    const uint32_t* src = &g_crc16.t[0][0];
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
+    __syncthreads();
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+  uint8_t* slots0 = smem + kTab16Bytes + wave_lane0 * 64;
+  const uint8_t* mine = slots0 + lane * 64;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
+    const uint32_t b = r0 + lane;
+    const uint32_t rend = min(r0 + 64, a.n);
+    const uint8_t* ilo = a.in + a.in_off[r0];
+    const uint8_t* ibase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(ilo) & ~uintptr_t(15));
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(ibase, align16(uint64_t((a.in + a.in_off[rend]) - ibase)));
+    // lane's block: payload bytes [shift, shift + clen) of its aligned run, the stored CRC after
+    uint32_t shift = 0, clen = 0, irel = 0, groups = 0;
+    bool act = false;
+    if (b < a.n) {
+      act = (z.rec[b].info >> 16) & kZfFast;
+      if (act) {
+        const uint64_t s0 = a.in_off[b];
+        shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + s0) & 15);
+        clen = uint32_t(a.in_off[b + 1] - s0) - 4;
+        irel = uint32_t(((a.in + s0) - shift) - ibase);
+        groups = (shift + clen + 63) / 64;
+      }
+    }
+    uint32_t stored = 0;
+    {
+      const uint32_t c = (shift + clen) >> 4;
+      const v4u s0 = bload(R, act ? irel + 16 * c : kOOB), s1 = bload(R, act ? irel + 16 * c + 16 : kOOB);
+      const uint32_t w[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const uint32_t p = (shift + clen) & 15;  // the stored CRC is bytes p..p+3 of the 32 loaded
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        lo = (p >> 2) == k ? w[k] : lo;
+        hi = (p >> 2) + 1 == k ? w[k] : hi;
+      }
+      stored = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
+    }
+    uint32_t crc = 0xFFFFFFFFu;
+    ZfGroup g = zf_load_group(R, 0, irel, groups, lane);
+    for (uint32_t t = 0; __ballot(t < groups); t++) {
+      zf_commit_group(g, slots0, t, groups, lane);
+      g = zf_load_group(R, t + 1, irel, groups, lane);  // in flight during this iteration
+      zs_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t c0 = 64 * t + 16 * k;  // aligned offset of the chunk
+        const v4u v = *reinterpret_cast<const v4u*>(mine + 16 * k);
+        const bool whole = t < groups && c0 >= shift && c0 + 16 <= shift + clen;
+        const bool part = t < groups && !whole && c0 < shift + clen && c0 + 16 > shift;
+        const uint32_t cw = crc16_step(tab, crc, v.x, v.y, v.z, v.w);
+        crc = whole ? cw : crc;
+        if (__ballot(part)) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t i = 0; i < 16; i++) {
+            const uint32_t pos = c0 + i;
+            const uint32_t byte = (w[i >> 2] >> (8 * (i & 3))) & 0xFF;
+            const uint32_t cb = tab[(crc ^ byte) & 0xFF] ^ (crc >> 8);
+            crc = (part && pos >= shift && pos < shift + clen) ? cb : crc;
+          }
+        }
+      }
+      zs_sync();
+    }
+    if (act && ~crc != stored) {
+      slate_block_meta m{};
+      m.status = SLATE_E_BLOCK_CHECKSUM;
+      a.meta[b] = m;
+      z.rec[b].info = 0;  // not built (B), not summed (C), not handed back
+    }
+  }
+}
+
+hipError_t launch_zstd_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,
+                                 uint64_t* row_sz, uint32_t* list, uint32_t* count) {
+  if (n == 0) return hipGetLastError();
+  const uint32_t grid = min((n + kZfParseThreads - 1) / kZfParseThreads, 8192u);
+  plan_zstd_fast_kernel<<<grid, kZfParseThreads, 0, st>>>(in, in_off, n, out_sz, row_sz, list, count);
+  return hipGetLastError();
+}
+
+size_t zstd_fast_parse_lds() { return ((sizeof(ZfShared) + 15) & ~size_t(15)) + size_t(kZfParseThreads) * kZfLane; }
+
+hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
+  if (a.n == 0) return hipGetLastError();
+  const size_t lds_a = zstd_fast_parse_lds();
+  const uint32_t grid_a = min((a.n + kZfParseThreads - 1) / kZfParseThreads, uint32_t(num_cus) * 2u);
+  zs_fast_parse_kernel<<<grid_a, kZfParseThreads, lds_a, st>>>(a, z);
+  const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
+  const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
+  zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
+  const size_t lds_b = size_t(kZfBuildThreads / 64) * kZfOutLds;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
+  if (attr != hipSuccess) return attr;
+  const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * 8u);
+  zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
+  const uint32_t grid_c = min((a.n + kZfSumThreads - 1) / kZfSumThreads, uint32_t(num_cus) * 4u);
+  zs_fast_sum_kernel<<<grid_c, kZfSumThreads, 0, st>>>(a, z);
+  return hipGetLastError();
+}
+
+}  // namespace slate

@@ -90,6 +90,32 @@ def test_large_and_concatenated_zstd_blocks(ctx):
     _compare(ctx, blocks, misalign=5)
 
 
+def test_fast_path_shapes_and_checksums(ctx):
+    """Blocks of the fast path's shape (one frame, one compressed block, raw literals, predefined
+    tables: zstd_fast.hip) mixed with ones it hands to the exact path, with: a wrong SST CRC32
+    (phase C's first check), a flipped literal byte with the CRC32 recomputed (the frame's
+    XXH64 no longer matches), frames without checksum or content size, RLE literals, and
+    blocks at every input alignment."""
+    rng = random.Random(5)
+    kvs = bg.kv_mixed(600)
+    decs = [b[:-4] for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+    blocks = []
+    for i, dec in enumerate(decs * 3):
+        f = bytearray(_z(dec, 3, checksum=i % 5 != 1, content_size=i % 7 != 2))
+        kind = i % 6
+        if kind == 3:  # literal byte flipped (raw literals start right after the headers)
+            f[len(f) // 3] ^= 0x10
+        blk = bytearray(_crc(bytes(f)))
+        if kind == 4:
+            blk[-1] ^= 0x01  # stored CRC32 wrong
+        blocks.append(bytes(blk))
+    blocks.append(_crc(_z(bytes(4000), 3)))  # RLE-heavy
+    blocks.append(_crc(_z(b"k" * 10 + bytes(range(256)) * 12, 3)))
+    meta = _compare(ctx, blocks, misalign=3)
+    st = set(int(x) for x in meta["status"])
+    assert 0 in st and 2 in st, st
+
+
 def test_damaged_zstd_blocks(ctx):
     rng = random.Random(9)
     decs = _sst_plain(rng, 800, 1024)
