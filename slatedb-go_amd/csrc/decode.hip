@@ -1107,7 +1107,7 @@ size_t decode_scratch_bytes(uint32_t n) {
   size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
   return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16 +
          // CodecZstd fast path: count, list, records, sequences
-         16 + align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
+         16 + 2 * align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
          size_t(n) * kZsFastSeqs * sizeof(uint2);
 }
 
@@ -1127,6 +1127,8 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   s.zf.count = reinterpret_cast<uint32_t*>(p);
   p += 16;
   s.zf.list = reinterpret_cast<uint32_t*>(p);
+  p += align16(size_t(n) * sizeof(uint32_t));
+  s.zf.hlist = reinterpret_cast<uint32_t*>(p);
   p += align16(size_t(n) * sizeof(uint32_t));
   s.zf.rec = reinterpret_cast<ZsFastRec*>(p);
   p += size_t(n) * sizeof(ZsFastRec);
@@ -1252,7 +1254,7 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
     decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else if (a.codec == SLATE_CODEC_ZSTD) {
     // the fast path (zstd_fast.hip), then the exact path over the blocks it handed back
-    (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
+    (void)hipMemsetAsync(s.zf.count, 0, 2 * sizeof(uint32_t), st);
     hipError_t e = launch_zstd_fast(st, a, s.zf, num_cus);
     if (e != hipSuccess) return e;
     decode_list_kernel<2><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);

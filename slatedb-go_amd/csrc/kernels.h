@@ -55,20 +55,22 @@ __host__ __device__ inline uint32_t dbg_bits(const DecodeArgs& a) {
 
 // CodecZstd fast path (zstd_fast.hip): per block, what the lane-per-block parse found
 constexpr uint32_t kZsFastSeqs = 16;  // sequences per block on the fast path (more: exact path)
-constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4;
+constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4, kZfHuf = 8, kZfHuf4 = 16;  // kZfHuf: Huffman literals
 struct ZsFastRec {
   uint32_t lit;       // frame offset of the raw literals, or the RLE literal byte
   uint32_t nlit;      // literal bytes
   uint32_t produced;  // decoded bytes
   uint32_t info;      // sequences | kZf* flags << 16 (kZfFast clear: the exact path decodes it)
   uint32_t want;      // the frame's checksum (low 32 bits of XXH64) when kZfSum
-  uint32_t pad[3];
+  uint32_t cs;        // kZfHuf: compressed literals bytes (tree description + streams) at lit
+  uint32_t pad[2];
 };
 struct ZsFastArgs {
   ZsFastRec* rec;   // n
   uint2* seq;       // n * kZsFastSeqs: (ll | ml << 16, offset)
   uint32_t* list;   // blocks for the exact path
-  uint32_t* count;
+  uint32_t* count;  // (count[1]: hlist entries)
+  uint32_t* hlist;  // kZfHuf blocks (phase B': Huffman literals)
 };
 
 struct DecodeScratch {

@@ -55,6 +55,9 @@ constexpr uint32_t kZfOutLds = kZfOut + 256;
 // phase C: 64 bytes of LDS per lane; phase A2: the same + the slicing-by-16 CRC tables
 constexpr uint32_t kZfSumThreads = 256;
 constexpr uint32_t kZfCrcThreads = 512;
+// phase B': per wave the frame, the decoded block and a ZsScratch (Huffman tables)
+constexpr uint32_t kZfHufThreads = 256;
+constexpr uint32_t kZfHufWave = kZsFastInCap + 16 + (kZsFastOutCap + 256) + kZsScratch;
 
 struct ZfShared {
   ZsShared fse;  // the predefined LL / ML / OF decoding tables
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
     const uint8_t* lo = a.in + a.in_off[r0];
     const uint8_t* base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(lo) & ~uintptr_t(15));
     const __amdgpu_buffer_rsrc_t R = make_rsrc(base, align16(uint64_t((a.in + a.in_off[rend]) - base)));
-    ZsFastRec rec{0, 0, 0, 0, 0, {0, 0, 0}};
+    ZsFastRec rec{0, 0, 0, 0, 0, 0, {0, 0}};
     bool ok = false;
     uint32_t shift = 0, rel = kOOB, clen = 0, cap = 0;
     if (b < a.n) {
@@ -255,15 +258,26 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
     const uint8_t* hb = hb0 + shift;
     ZfHead h{};
     ok = ok && zf_head(hb, clen, h) && h.bt == 2;
-    // ---- literals section header (zs_block), raw or RLE literals only
-    uint32_t nlit = 0, pos = 0, lit = 0, rle = 0;
+    // ---- literals section header (zs_block): raw, RLE, or Huffman-coded with a new tree
+    uint32_t nlit = 0, pos = 0, lit = 0, rle = 0, huf = 0, cs = 0;
     const uint32_t nb = h.bs, body = h.body;
     if (ok) {
       const uint32_t b0 = hb[body], type = b0 & 3, sf = (b0 >> 2) & 3;
       uint32_t hs;
-      if (type > 1) {
+      if (type == 3) {  // treeless: no earlier tree in a one-block frame (the exact path: corrupt)
         ok = false;
         hs = 1;
+      } else if (type == 2) {
+        huf = sf == 0 ? 1u : 4u;  // streams
+        const uint64_t hh = uint64_t(b0) | (uint64_t(hb[body + 1]) << 8) | (uint64_t(hb[body + 2]) << 16) |
+                            (uint64_t(hb[body + 3]) << 24) | (uint64_t(hb[body + 4]) << 32);
+        hs = sf <= 1 ? 3 : (sf == 2 ? 4 : 5);
+        ok = nb >= hs;
+        nlit = sf <= 1 ? uint32_t((hh >> 4) & 0x3FF) : (sf == 2 ? uint32_t((hh >> 4) & 0x3FFF) : uint32_t((hh >> 4) & 0x3FFFF));
+        cs = sf <= 1 ? uint32_t((hh >> 14) & 0x3FF) : (sf == 2 ? uint32_t((hh >> 18) & 0x3FFF) : uint32_t((hh >> 22) & 0x3FFFF));
+        ok = ok && nlit <= h.bmax && nb - hs >= cs && nlit <= cap;
+        lit = body + hs;
+        pos = hs + cs;
       } else if (sf == 1) {
         hs = 2;
         ok = nb >= 2;
@@ -276,10 +290,12 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
         hs = 1;
         nlit = b0 >> 3;
       }
-      ok = ok && nb >= 1 && nlit <= h.bmax && (type == 0 ? nb - hs >= nlit : nb - hs >= 1) && nlit <= cap;
-      rle = type == 1;
-      lit = rle ? uint32_t(hb[body + hs]) : body + hs;
-      pos = hs + (type == 0 ? nlit : 1);
+      if (type <= 1) {
+        ok = ok && nb >= 1 && nlit <= h.bmax && (type == 0 ? nb - hs >= nlit : nb - hs >= 1) && nlit <= cap;
+        rle = type == 1;
+        lit = rle ? uint32_t(hb[body + hs]) : body + hs;
+        pos = hs + (type == 0 ? nlit : 1);
+      }
       ok = ok && pos < nb;
     }
     // ---- the sequences section: 11 chunks from the one holding its first byte
@@ -414,7 +430,10 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
       rec.lit = lit;
       rec.nlit = nlit;
       rec.produced = produced;
-      rec.info = nseq | ((kZfFast | (rle ? kZfRle : 0u) | (h.checksum ? kZfSum : 0u)) << 16);
+      rec.info = nseq | ((kZfFast | (rle ? kZfRle : 0u) | (h.checksum ? kZfSum : 0u) | (huf ? kZfHuf : 0u) |
+                          (huf == 4 ? kZfHuf4 : 0u))
+                         << 16);
+      rec.cs = cs;
       const uint32_t q = body + nb;
       rec.want = h.checksum ? uint32_t(tb[q]) | (uint32_t(tb[q + 1]) << 8) | (uint32_t(tb[q + 2]) << 16) |
                                   (uint32_t(tb[q + 3]) << 24)
@@ -422,13 +441,14 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
     }
     if (b < a.n) z.rec[b] = rec;
     list_append(b < a.n && !ok, b, z.list, z.count);
+    list_append(b < a.n && ok && huf, b, z.hlist, z.count + 1);
   }
 }
 
 // ------------------------------------------------------------------------------- phase B
 namespace {
-struct ZfBlock {                      // what phase B needs of one block, loaded one block ahead
-  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle;
+struct ZfBlock {  // what phase B needs of one block, loaded one block ahead
+  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs;
   const uint8_t* gin;
 };
 __device__ __forceinline__ ZfBlock zf_block(const DecodeArgs& a, const ZsFastArgs& z, uint32_t b) {
@@ -449,6 +469,8 @@ __device__ __forceinline__ ZfBlock zf_block(const DecodeArgs& a, const ZsFastArg
   k.produced = __builtin_amdgcn_readfirstlane(rec.produced);
   k.lit = __builtin_amdgcn_readfirstlane(rec.lit);
   k.rle = fl & kZfRle;
+  k.huf = (fl & kZfHuf) ? ((fl & kZfHuf4) ? 4u : 1u) : 0u;
+  k.cs = __builtin_amdgcn_readfirstlane(rec.cs);
   return k;
 }
 // the block's sequences, lane i holding sequence i
@@ -456,6 +478,77 @@ __device__ __forceinline__ uint2 zf_seqs(const ZsFastArgs& z, const ZfBlock& k, 
   return (k.fast && lane < k.nseq) ? z.seq[size_t(k.b) * kZsFastSeqs + lane] : make_uint2(0, 0);
 }
 }  // namespace
+
+// Build one block in wout from its sequences (lane i: sequence i) and its literals at wout[lb...]
+// (or the RLE byte), write it back, then block.Decode's checks and rows (phases B and B').
+__device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur, uint2 seq, uint8_t* wout,
+                                         uint32_t lb, uint32_t lane, uint32_t dbg) {
+  const uint32_t lit = cur.lit;
+  slate_block_meta m{};
+  // sequence lane i: (ll, ml, offset); exclusive scans give each one's literal source and
+  // output position
+  const uint32_t nseq = cur.nseq, nlit = cur.nlit;
+  const uint32_t ll = seq.x & 0xFFFFu, ml = seq.x >> 16, off = seq.y;
+  uint32_t x_ll = ll, x_out = ll + ml;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y1 = __shfl_up(x_ll, d, 64), y2 = __shfl_up(x_out, d, 64);
+    if (int(lane) >= d) {
+      x_ll += y1;
+      x_out += y2;
+    }
+  }
+  const uint32_t lsrc = x_ll - ll, dpos = x_out - ll - ml;  // exclusive
+  const uint32_t tot_ll = __shfl(x_ll, 63, 64), tot_out = __shfl(x_out, 63, 64);
+  const uint32_t rle4 = (lit & 0xFF) * 0x01010101u;
+  // Literal runs of every sequence and the trailing run, in order, a dword per lane.  A run
+  // moves down (destination <= source: the cursor rule), so a lane reads its source dword
+  // before any lane writes over it; the (up to three) bytes a run's first or last dword
+  // spills over lie in the neighbouring match (>= 3 bytes), written afterwards, or past the
+  // block, and never reach the literals still to be moved (the cursor rule again, ml >= 3).
+  for (uint32_t i = 0; i <= nseq && !(dbg & (1u << 22)); i++) {
+    const uint32_t L = i < nseq ? __builtin_amdgcn_readlane(ll, i) : nlit - tot_ll;
+    if (L == 0) continue;
+    const uint32_t src = i < nseq ? __builtin_amdgcn_readlane(lsrc, i) : tot_ll;
+    const uint32_t dst = i < nseq ? __builtin_amdgcn_readlane(dpos, i) : tot_out;
+    const int32_t delta = int32_t(lb + src) - int32_t(dst);  // output byte p = wout[p + delta]
+    for (uint32_t w = (dst & ~3u) + 4 * lane; w < dst + L; w += 4 * kWave) {
+      const uint32_t v = cur.rle ? rle4 : lds_u32(wout, int32_t(w) + delta);
+      __builtin_amdgcn_wave_barrier();
+      *reinterpret_cast<uint32_t*>(wout + w) = v;
+    }
+  }
+  zs_sync();
+  // Matches in order: each reads only bytes before its own position.  Non-overlapping ones
+  // (offset >= length) a dword per lane, the edge dwords merged with the bytes around the
+  // match; overlapping ones a byte per lane.
+  for (uint32_t i = 0; i < nseq && !(dbg & (1u << 21)); i++) {
+    const uint32_t M = __builtin_amdgcn_readlane(ml, i), O = __builtin_amdgcn_readlane(off, i);
+    const uint32_t mp = __builtin_amdgcn_readlane(dpos, i) + __builtin_amdgcn_readlane(ll, i);
+    if (O >= M) {
+      const uint32_t me = mp + M;
+      const uint32_t lo_keep = (1u << (8 * (mp & 3))) - 1u, hi_keep = (me & 3) ? ~((1u << (8 * (me & 3))) - 1u) : 0u;
+      for (uint32_t w = (mp & ~3u) + 4 * lane; w < me; w += 4 * kWave) {
+        uint32_t v = lds_u32(wout, int32_t(w) - int32_t(O));
+        const uint32_t keep = (w < mp ? lo_keep : 0u) | (w + 4 > me ? hi_keep : 0u);
+        if (keep) v = (v & ~keep) | (*reinterpret_cast<const uint32_t*>(wout + w) & keep);
+        *reinterpret_cast<uint32_t*>(wout + w) = v;
+      }
+    } else {
+      for (uint32_t j = lane; j < M; j += kWave) wout[mp + j] = wout[mp - O + (j % O)];
+    }
+    zs_sync();
+  }
+  const uint32_t n = cur.produced;
+  {
+    uint8_t* gout = a.out + a.out_off[cur.b];
+    const uint32_t oc = (n + 15) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(wout);
+    for (uint32_t c = lane; c < oc; c += kWave) reinterpret_cast<uint4*>(gout)[c] = src[c];
+  }
+  if (dbg & (1u << 20)) write_meta(&a.meta[cur.b], m, int(lane));
+  else block_finish(a, cur.b, wout, n, int(lane), m);
+}
 
 // One wave per block, the next block's record and sequences loaded while this one is built.  The frame is staged in the output buffer at the 16-byte phase of its address, placed
 // so that its raw literals start at lb >= cap - nlit: phase A checked zs_block's rule that the
@@ -476,7 +569,7 @@ __global__ __launch_bounds__(kZfBuildThreads, 8) void zs_fast_build_kernel(Decod
   for (; cur.b < a.n; cur = nxt, nxt = zf_block(a, z, nxt.b + waves)) {
     const uint2 seq = sq;
     sq = zf_seqs(z, nxt, lane);  // in flight while this block is built
-    if (!cur.fast) continue;
+    if (!cur.fast || cur.huf) continue;  // (Huffman literals: phase B')
     const uint32_t lbase = cur.cap - cur.nlit, lit = cur.lit, shift = cur.shift;
     // frame byte 0 at wout[F], F = 16-aligned base + shift, literals at lb = F + lit >= lbase
     uint32_t base16 = 16;
@@ -490,70 +583,105 @@ __global__ __launch_bounds__(kZfBuildThreads, 8) void zs_fast_build_kernel(Decod
     }
     __builtin_amdgcn_s_waitcnt(0);
     zs_sync();
-    slate_block_meta m{};  // (the block's CRC32 held: phase A2)
-    // sequence lane i: (ll, ml, offset); exclusive scans give each one's literal source and
-    // output position
-    const uint32_t nseq = cur.nseq, nlit = cur.nlit;
-    const uint32_t ll = seq.x & 0xFFFFu, ml = seq.x >> 16, off = seq.y;
-    uint32_t x_ll = ll, x_out = ll + ml;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y1 = __shfl_up(x_ll, d, 64), y2 = __shfl_up(x_out, d, 64);
-      if (int(lane) >= d) {
-        x_ll += y1;
-        x_out += y2;
-      }
+    zf_build(a, cur, seq, wout, lb, lane, dbg);  // (the block's CRC32 held: phase A2)
+  }
+}
+
+// ------------------------------------------------------------------------------- phase B'
+// Blocks whose literals are Huffman-coded with a new tree (zs_block literal type 2; configs[4]:
+// ~1 %), one wave per block from phase A's list: the tree (zs_huf_read) and the one or four
+// streams decoded as zs_block does, into the tail of the output buffer, then built like phase B.
+// Any failed check hands the block to the exact path.
+__global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t items = z.count[1];
+  if (blockIdx.x * (kZfHufThreads / 64) >= items) return;  // (workgroup-uniform)
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* win = smem + wave * kZfHufWave;
+  uint8_t* wout = win + kZfIn + 16;
+  ZsScratch* sc = reinterpret_cast<ZsScratch*>(wout + kZfOutLds);
+  for (uint32_t k = blockIdx.x * (kZfHufThreads / 64) + wave; k < items; k += gridDim.x * (kZfHufThreads / 64)) {
+    const uint32_t b = z.hlist[k];
+    const ZfBlock cur = zf_block(a, z, b);
+    if (!cur.fast) continue;  // the CRC32 failed (phase A2)
+    const uint2 seq = zf_seqs(z, cur, lane);
+    const uint32_t shift = cur.shift;
+    {
+      const uint32_t chunks = (shift + cur.len + 15) / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(cur.gin - shift);
+      uint4* dst = reinterpret_cast<uint4*>(win);
+      for (uint32_t c = lane; c < chunks; c += kWave) dst[c] = src[c];
     }
-    const uint32_t lsrc = x_ll - ll, dpos = x_out - ll - ml;  // exclusive
-    const uint32_t tot_ll = __shfl(x_ll, 63, 64), tot_out = __shfl(x_out, 63, 64);
-    const uint32_t rle4 = (lit & 0xFF) * 0x01010101u;
-    // Literal runs of every sequence and the trailing run, in order, a dword per lane.  A run
-    // moves down (destination <= source: the cursor rule), so a lane reads its source dword
-    // before any lane writes over it; the (up to three) bytes a run's first or last dword
-    // spills over lie in the neighbouring match (>= 3 bytes), written afterwards, or past the
-    // block, and never reach the literals still to be moved (the cursor rule again, ml >= 3).
-    for (uint32_t i = 0; i <= nseq && !(dbg & (1u << 22)); i++) {
-      const uint32_t L = i < nseq ? __builtin_amdgcn_readlane(ll, i) : nlit - tot_ll;
-      if (L == 0) continue;
-      const uint32_t src = i < nseq ? __builtin_amdgcn_readlane(lsrc, i) : tot_ll;
-      const uint32_t dst = i < nseq ? __builtin_amdgcn_readlane(dpos, i) : tot_out;
-      const int32_t delta = int32_t(lb + src) - int32_t(dst);  // output byte p = wout[p + delta]
-      for (uint32_t w = (dst & ~3u) + 4 * lane; w < dst + L; w += 4 * kWave) {
-        const uint32_t v = cur.rle ? rle4 : lds_u32(wout, int32_t(w) + delta);
-        __builtin_amdgcn_wave_barrier();
-        *reinterpret_cast<uint32_t*>(wout + w) = v;
+    __builtin_amdgcn_s_waitcnt(0);
+    zs_sync();
+    const uint32_t nlit = cur.nlit, lbase = cur.cap - nlit;
+    uint32_t tl = 0;
+    const int t = zs_huf_read(win, int32_t(shift + cur.lit), cur.cs, sc, int(lane), &tl);
+    bool fail = t < 0;
+    if (!fail) {
+      const uint32_t q = shift + cur.lit + uint32_t(t), qn = cur.cs - uint32_t(t);
+      auto bN = [&](uint32_t i) -> uint32_t { return zrfl(uint32_t(win[q + i])); };
+      // stream l on lane l: bytes [sb, sb + sl) of win, m literals to wout[lbase + lo]
+      uint32_t sb = 0, sl = 0, m = 0, lo = 0;
+      if (cur.huf == 1) {
+        sb = q;
+        sl = qn;
+        m = nlit;
+      } else if (qn < 10) {
+        fail = true;
+      } else {
+        const uint32_t l1 = bN(0) | (bN(1) << 8), l2 = bN(2) | (bN(3) << 8), l3 = bN(4) | (bN(5) << 8);
+        const uint32_t seg = (nlit + 3) / 4;
+        fail = l1 + l2 + l3 + 6 > qn || 3 * seg > nlit;
+        const uint32_t l4 = qn - 6 - l1 - l2 - l3, s0 = q + 6;
+        sb = lane == 0 ? s0 : lane == 1 ? s0 + l1 : lane == 2 ? s0 + l1 + l2 : s0 + l1 + l2 + l3;
+        sl = lane == 0 ? l1 : lane == 1 ? l2 : lane == 2 ? l3 : l4;
+        m = lane < 3 ? seg : nlit - 3 * seg;
+        lo = seg * (lane < 3 ? lane : 3u);
       }
+      bool badl = false;
+      if (!fail && lane < cur.huf) {
+        int64_t bp = zs_bstart(win, int32_t(sb), sl);
+        if (bp < 0) {
+          badl = true;
+        } else {
+          const int64_t S = 8 * int64_t(sb);
+          const uint32_t tmask = (1u << tl) - 1;
+          uint8_t* dst = wout + lbase + lo;
+          int64_t clo = 0;
+          uint64_t cv = 0;
+          bool have = false;
+          for (uint32_t i = 0; i < m; i++) {  // a 56-bit register window, as zs_block
+            const int64_t lo2 = bp - int64_t(tl);
+            uint32_t v;
+            if (have && lo2 >= clo) {
+              v = uint32_t(cv >> (lo2 - clo)) & tmask;
+            } else if (lo2 >= 0) {
+              clo = bp > 56 ? bp - 56 : 0;
+              cv = zs_bits(win, S + clo, 56);
+              have = true;
+              v = uint32_t(cv >> (lo2 - clo)) & tmask;
+            } else {
+              v = uint32_t(zs_peek(win, S, bp, tl));
+            }
+            const uint32_t e = sc->huf[v];
+            dst[i] = uint8_t(e);
+            bp -= e >> 8;
+          }
+          badl = bp != 0;
+        }
+      }
+      fail = fail || __ballot(badl) != 0;
+    }
+    if (fail) {  // to the exact path: not summed (C), decoded and reported by D
+      if (lane == 0) {
+        z.rec[b].info = 0;
+        z.list[atomicAdd(z.count, 1u)] = b;
+      }
+      continue;
     }
     zs_sync();
-    // Matches in order: each reads only bytes before its own position.  Non-overlapping ones
-    // (offset >= length) a dword per lane, the edge dwords merged with the bytes around the
-    // match; overlapping ones a byte per lane.
-    for (uint32_t i = 0; i < nseq && !(dbg & (1u << 21)); i++) {
-      const uint32_t M = __builtin_amdgcn_readlane(ml, i), O = __builtin_amdgcn_readlane(off, i);
-      const uint32_t mp = __builtin_amdgcn_readlane(dpos, i) + __builtin_amdgcn_readlane(ll, i);
-      if (O >= M) {
-        const uint32_t me = mp + M;
-        const uint32_t lo_keep = (1u << (8 * (mp & 3))) - 1u, hi_keep = (me & 3) ? ~((1u << (8 * (me & 3))) - 1u) : 0u;
-        for (uint32_t w = (mp & ~3u) + 4 * lane; w < me; w += 4 * kWave) {
-          uint32_t v = lds_u32(wout, int32_t(w) - int32_t(O));
-          const uint32_t keep = (w < mp ? lo_keep : 0u) | (w + 4 > me ? hi_keep : 0u);
-          if (keep) v = (v & ~keep) | (*reinterpret_cast<const uint32_t*>(wout + w) & keep);
-          *reinterpret_cast<uint32_t*>(wout + w) = v;
-        }
-      } else {
-        for (uint32_t j = lane; j < M; j += kWave) wout[mp + j] = wout[mp - O + (j % O)];
-      }
-      zs_sync();
-    }
-    const uint32_t n = cur.produced;
-    {
-      uint8_t* gout = a.out + a.out_off[cur.b];
-      const uint32_t oc = (n + 15) / 16;
-      const uint4* src = reinterpret_cast<const uint4*>(wout);
-      for (uint32_t c = lane; c < oc; c += kWave) reinterpret_cast<uint4*>(gout)[c] = src[c];
-    }
-    if (dbg & (1u << 20)) write_meta(&a.meta[cur.b], m, int(lane));
-    else block_finish(a, cur.b, wout, n, int(lane), m);
+    zf_build(a, cur, seq, wout, lbase, lane, 0);
   }
 }
 
@@ -776,6 +904,11 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   if (attr != hipSuccess) return attr;
   const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * 8u);
   zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
+  const size_t lds_h = size_t(kZfHufThreads / 64) * kZfHufWave;
+  static const hipError_t attr_h = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_huf_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_h));
+  if (attr_h != hipSuccess) return attr_h;
+  zs_fast_huf_kernel<<<uint32_t(num_cus) * 2u, kZfHufThreads, lds_h, st>>>(a, z);
   const uint32_t grid_c = min((a.n + kZfSumThreads - 1) / kZfSumThreads, uint32_t(num_cus) * 4u);
   zs_fast_sum_kernel<<<grid_c, kZfSumThreads, 0, st>>>(a, z);
   return hipGetLastError();
