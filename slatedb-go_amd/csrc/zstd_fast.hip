@@ -51,13 +51,14 @@ constexpr uint32_t kZfParseThreads = 256;
 // with the frame staged around its tail (the bytes after the literals and the 16-byte phase: +256)
 constexpr uint32_t kZfBuildThreads = 256;
 constexpr uint32_t kZfIn = kZsFastInCap, kZfOut = kZsFastOutCap;
-constexpr uint32_t kZfOutLds = kZfOut + 256;
+constexpr uint32_t kZfJunk = kZfOut + 256;      // 64 junk dwords (lanes' discarded writes)
+constexpr uint32_t kZfOutLds = kZfJunk + 256;
 // phase C: 64 bytes of LDS per lane; phase A2: the same + the slicing-by-16 CRC tables
 constexpr uint32_t kZfSumThreads = 256;
 constexpr uint32_t kZfCrcThreads = 512;
 // phase B': per wave the frame, the decoded block and a ZsScratch (Huffman tables)
 constexpr uint32_t kZfHufThreads = 256;
-constexpr uint32_t kZfHufWave = kZsFastInCap + 16 + (kZsFastOutCap + 256) + kZsScratch;
+constexpr uint32_t kZfHufWave = kZsFastInCap + 16 + kZfOutLds + kZsScratch;
 
 struct ZfShared {
   ZsShared fse;  // the predefined LL / ML / OF decoding tables
@@ -447,42 +448,61 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
 
 // ------------------------------------------------------------------------------- phase B
 namespace {
-struct ZfBlock {  // what phase B needs of one block, loaded one block ahead
+// What phase B needs of one block: its record, offsets and sequences, loaded by independent
+// loads (no branch on their values) so that they can be issued one block ahead.
+struct ZfRaw {
+  ZsFastRec rec;
+  uint64_t i0, i1, o0, o1;
+  uint2 seq;  // lane i: sequence i (lanes < kZsFastSeqs)
+  uint32_t b;
+};
+__device__ __forceinline__ ZfRaw zf_load(const DecodeArgs& a, const ZsFastArgs& z, uint32_t b, uint32_t lane) {
+  ZfRaw r{};
+  r.b = b;
+  if (b < a.n) {
+    r.rec = z.rec[b];
+    r.i0 = a.in_off[b];
+    r.i1 = a.in_off[b + 1];
+    r.o0 = a.out_off[b];
+    r.o1 = a.out_off[b + 1];
+    r.seq = lane < kZsFastSeqs ? z.seq[size_t(b) * kZsFastSeqs + lane] : make_uint2(0, 0);
+  }
+  return r;
+}
+struct ZfBlock {
   uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs;
   const uint8_t* gin;
+  uint8_t* gout;
+  uint2 seq;  // lane i < nseq: sequence i, else 0
 };
-__device__ __forceinline__ ZfBlock zf_block(const DecodeArgs& a, const ZsFastArgs& z, uint32_t b) {
+__device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r, uint32_t lane) {
   ZfBlock k{};
-  k.b = b;
-  if (b >= a.n) return k;
-  const ZsFastRec rec = z.rec[b];
-  const uint32_t fl = __builtin_amdgcn_readfirstlane(rec.info >> 16);
+  k.b = r.b;
+  if (r.b >= a.n) return k;
+  const uint32_t fl = __builtin_amdgcn_readfirstlane(r.rec.info >> 16);
   k.fast = fl & kZfFast;
-  if (!k.fast) return k;
-  const uint64_t s0 = a.in_off[b];
-  k.gin = a.in + s0;
-  k.len = uint32_t(a.in_off[b + 1] - s0);
+  k.gin = a.in + r.i0;
+  k.gout = a.out + r.o0;
+  k.len = uint32_t(r.i1 - r.i0);
   k.shift = uint32_t(reinterpret_cast<uintptr_t>(k.gin) & 15);
-  k.cap = uint32_t(a.out_off[b + 1] - a.out_off[b]);
-  k.nseq = __builtin_amdgcn_readfirstlane(rec.info & 0xFFFFu);
-  k.nlit = __builtin_amdgcn_readfirstlane(rec.nlit);
-  k.produced = __builtin_amdgcn_readfirstlane(rec.produced);
-  k.lit = __builtin_amdgcn_readfirstlane(rec.lit);
+  k.cap = uint32_t(r.o1 - r.o0);
+  k.nseq = __builtin_amdgcn_readfirstlane(r.rec.info & 0xFFFFu);
+  k.nlit = __builtin_amdgcn_readfirstlane(r.rec.nlit);
+  k.produced = __builtin_amdgcn_readfirstlane(r.rec.produced);
+  k.lit = __builtin_amdgcn_readfirstlane(r.rec.lit);
   k.rle = fl & kZfRle;
   k.huf = (fl & kZfHuf) ? ((fl & kZfHuf4) ? 4u : 1u) : 0u;
-  k.cs = __builtin_amdgcn_readfirstlane(rec.cs);
+  k.cs = __builtin_amdgcn_readfirstlane(r.rec.cs);
+  k.seq = (k.fast && lane < k.nseq) ? r.seq : make_uint2(0, 0);
   return k;
-}
-// the block's sequences, lane i holding sequence i
-__device__ __forceinline__ uint2 zf_seqs(const ZsFastArgs& z, const ZfBlock& k, uint32_t lane) {
-  return (k.fast && lane < k.nseq) ? z.seq[size_t(k.b) * kZsFastSeqs + lane] : make_uint2(0, 0);
 }
 }  // namespace
 
 // Build one block in wout from its sequences (lane i: sequence i) and its literals at wout[lb...]
 // (or the RLE byte), write it back, then block.Decode's checks and rows (phases B and B').
-__device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur, uint2 seq, uint8_t* wout,
-                                         uint32_t lb, uint32_t lane, uint32_t dbg) {
+__device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur, uint8_t* wout, uint32_t lb,
+                                         uint32_t lane, uint32_t dbg) {
+  const uint2 seq = cur.seq;
   const uint32_t lit = cur.lit;
   slate_block_meta m{};
   // sequence lane i: (ll, ml, offset); exclusive scans give each one's literal source and
@@ -501,21 +521,38 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
   const uint32_t lsrc = x_ll - ll, dpos = x_out - ll - ml;  // exclusive
   const uint32_t tot_ll = __shfl(x_ll, 63, 64), tot_out = __shfl(x_out, 63, 64);
   const uint32_t rle4 = (lit & 0xFF) * 0x01010101u;
-  // Literal runs of every sequence and the trailing run, in order, a dword per lane.  A run
-  // moves down (destination <= source: the cursor rule), so a lane reads its source dword
-  // before any lane writes over it; the (up to three) bytes a run's first or last dword
+  // Literal runs of every sequence and the trailing run, in order, four dwords per lane.  A run
+  // moves down (destination <= source: the cursor rule), so a lane reads its source bytes
+  // before any lane writes over them.  Only the dwords that hold run bytes are written (the
+  // others go to the lane's junk dword); the (up to three) bytes the first or last of them
   // spills over lie in the neighbouring match (>= 3 bytes), written afterwards, or past the
   // block, and never reach the literals still to be moved (the cursor rule again, ml >= 3).
+  uint8_t* junk = wout + kZfJunk + 4 * lane;
   for (uint32_t i = 0; i <= nseq && !(dbg & (1u << 22)); i++) {
     const uint32_t L = i < nseq ? __builtin_amdgcn_readlane(ll, i) : nlit - tot_ll;
     if (L == 0) continue;
     const uint32_t src = i < nseq ? __builtin_amdgcn_readlane(lsrc, i) : tot_ll;
     const uint32_t dst = i < nseq ? __builtin_amdgcn_readlane(dpos, i) : tot_out;
     const int32_t delta = int32_t(lb + src) - int32_t(dst);  // output byte p = wout[p + delta]
-    for (uint32_t w = (dst & ~3u) + 4 * lane; w < dst + L; w += 4 * kWave) {
-      const uint32_t v = cur.rle ? rle4 : lds_u32(wout, int32_t(w) + delta);
+    const uint32_t end = dst + L;
+    for (uint32_t w = (dst & ~3u) + 16 * lane; w < end; w += 16 * kWave) {
+      uint32_t o[4];
+      if (cur.rle) {
+        o[0] = o[1] = o[2] = o[3] = rle4;
+      } else {
+        const int32_t sa = int32_t(w) + delta;
+        const uint32_t* sp = reinterpret_cast<const uint32_t*>(wout + (sa & ~3));
+        const uint32_t sh = uint32_t(sa) & 3;
+        const uint32_t d0 = sp[0], d1 = sp[1], d2 = sp[2], d3 = sp[3], d4 = sp[4];
+        o[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        o[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        o[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        o[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
+      }
       __builtin_amdgcn_wave_barrier();
-      *reinterpret_cast<uint32_t*>(wout + w) = v;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        *reinterpret_cast<uint32_t*>(w + 4 * k < end ? wout + w + 4 * k : junk) = o[k];
     }
   }
   zs_sync();
@@ -541,8 +578,8 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
   }
   const uint32_t n = cur.produced;
   {
-    uint8_t* gout = a.out + a.out_off[cur.b];
-    const uint32_t oc = (n + 15) / 16;
+    uint8_t* gout = cur.gout;
+    const uint32_t oc = (dbg & (1u << 27)) ? 0u : (n + 15) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(wout);
     for (uint32_t c = lane; c < oc; c += kWave) reinterpret_cast<uint4*>(gout)[c] = src[c];
   }
@@ -561,14 +598,15 @@ __global__ __launch_bounds__(kZfBuildThreads, 8) void zs_fast_build_kernel(Decod
   uint8_t* wout = smem + wave * kZfOutLds;
   const uint32_t waves = gridDim.x * (kZfBuildThreads / 64);
   // profiling ablations (SLATE_DEBUG_MODE, profiling variants only): 1<<20 no block_finish,
-  // 1<<21 no matches, 1<<22 no literal runs, 1<<24 no XXH64 rounds, 1<<26 no hand-back from C
+  // 1<<21 no matches, 1<<22 no literal runs, 1<<24 no XXH64 rounds, 1<<26 no hand-back from C,
+  // 1<<27 no output write, 1<<28 no frame staging
   const uint32_t dbg = dbg_bits(a);
-  ZfBlock cur = zf_block(a, z, blockIdx.x * (kZfBuildThreads / 64) + wave);
-  uint2 sq = zf_seqs(z, cur, lane);
-  ZfBlock nxt = zf_block(a, z, cur.b + waves);
-  for (; cur.b < a.n; cur = nxt, nxt = zf_block(a, z, nxt.b + waves)) {
-    const uint2 seq = sq;
-    sq = zf_seqs(z, nxt, lane);  // in flight while this block is built
+  const uint32_t first = blockIdx.x * (kZfBuildThreads / 64) + wave;
+  ZfRaw nr = zf_load(a, z, first, lane);
+  for (uint32_t b = first; b < a.n; b += waves) {
+    const ZfRaw cr = nr;
+    nr = zf_load(a, z, b + waves, lane);  // in flight while this block is built
+    const ZfBlock cur = zf_decode(a, cr, lane);
     if (!cur.fast || cur.huf) continue;  // (Huffman literals: phase B')
     const uint32_t lbase = cur.cap - cur.nlit, lit = cur.lit, shift = cur.shift;
     // frame byte 0 at wout[F], F = 16-aligned base + shift, literals at lb = F + lit >= lbase
@@ -576,14 +614,14 @@ __global__ __launch_bounds__(kZfBuildThreads, 8) void zs_fast_build_kernel(Decod
     if (!cur.rle && lbase > lit + shift + 16) base16 = (lbase - lit - shift + 15) & ~15u;
     const uint32_t F = base16 + shift, lb = F + lit;
     {
-      const uint32_t chunks = (shift + cur.len + 15) / 16;
+      const uint32_t chunks = (dbg & (1u << 28)) ? 0u : (shift + cur.len + 15) / 16;
       const uint4* src = reinterpret_cast<const uint4*>(cur.gin - shift);
       uint4* dst = reinterpret_cast<uint4*>(wout + base16);
       for (uint32_t c = lane; c < chunks; c += kWave) dst[c] = src[c];
     }
     __builtin_amdgcn_s_waitcnt(0);
     zs_sync();
-    zf_build(a, cur, seq, wout, lb, lane, dbg);  // (the block's CRC32 held: phase A2)
+    zf_build(a, cur, wout, lb, lane, dbg);  // (the block's CRC32 held: phase A2)
   }
 }
 
@@ -602,9 +640,8 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
   ZsScratch* sc = reinterpret_cast<ZsScratch*>(wout + kZfOutLds);
   for (uint32_t k = blockIdx.x * (kZfHufThreads / 64) + wave; k < items; k += gridDim.x * (kZfHufThreads / 64)) {
     const uint32_t b = z.hlist[k];
-    const ZfBlock cur = zf_block(a, z, b);
+    const ZfBlock cur = zf_decode(a, zf_load(a, z, b, lane), lane);
     if (!cur.fast) continue;  // the CRC32 failed (phase A2)
-    const uint2 seq = zf_seqs(z, cur, lane);
     const uint32_t shift = cur.shift;
     {
       const uint32_t chunks = (shift + cur.len + 15) / 16;
@@ -616,7 +653,8 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
     zs_sync();
     const uint32_t nlit = cur.nlit, lbase = cur.cap - nlit;
     uint32_t tl = 0;
-    const int t = zs_huf_read(win, int32_t(shift + cur.lit), cur.cs, sc, int(lane), &tl);
+    // 1<<30: profiling, no tree (a flat 8-bit table is assumed)
+    const int t = (dbg_bits(a) & (1u << 30)) ? (tl = 8, 1) : zs_huf_read(win, int32_t(shift + cur.lit), cur.cs, sc, int(lane), &tl);
     bool fail = t < 0;
     if (!fail) {
       const uint32_t q = shift + cur.lit + uint32_t(t), qn = cur.cs - uint32_t(t);
@@ -640,7 +678,7 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
         lo = seg * (lane < 3 ? lane : 3u);
       }
       bool badl = false;
-      if (!fail && lane < cur.huf) {
+      if (!fail && lane < cur.huf && !(dbg_bits(a) & (1u << 29))) {  // 1<<29: profiling, no streams
         int64_t bp = zs_bstart(win, int32_t(sb), sl);
         if (bp < 0) {
           badl = true;
@@ -681,7 +719,7 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
       continue;
     }
     zs_sync();
-    zf_build(a, cur, seq, wout, lbase, lane, 0);
+    zf_build(a, cur, wout, lbase, lane, 0);
   }
 }
 
