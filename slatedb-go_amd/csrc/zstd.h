@@ -24,17 +24,19 @@ struct ZsFse {
   uint8_t sym, nb;
   uint16_t base;
 };
-struct ZsScratch {     // per wave
+struct ZsScratch {     // per wave; the Huffman tree decode uses the fields before ll only
   uint16_t huf[2048];  // (nbits << 8) | symbol, indexed by the next tl stream bits
-  ZsFse ll[512], ml[512], of[256], wt[64];
+  ZsFse wt[64];
   int16_t norm[256];
   uint16_t next[256];
   uint8_t w[256];
+  ZsFse ll[512], ml[512], of[256];
 };
 struct ZsShared {  // per workgroup: the predefined distributions (RFC 8878 3.1.1.3.2.2)
   ZsFse ll[64], ml[64], of[32];
 };
 constexpr uint32_t kZsScratch = (sizeof(ZsScratch) + 15) & ~15u;
+constexpr uint32_t kZsHufScratch = (offsetof(ZsScratch, ll) + 15) & ~15u;  // zs_huf_read's part
 constexpr uint32_t kZsShared = (sizeof(ZsShared) + 15) & ~15u;
 
 __constant__ int16_t kZsLLDef[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,

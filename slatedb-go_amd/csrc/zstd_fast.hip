@@ -56,9 +56,10 @@ constexpr uint32_t kZfOutLds = kZfJunk + 256;
 // phase C: 64 bytes of LDS per lane; phase A2: the same + the slicing-by-16 CRC tables
 constexpr uint32_t kZfSumThreads = 256;
 constexpr uint32_t kZfCrcThreads = 512;
-// phase B': per wave the frame, the decoded block and a ZsScratch (Huffman tables)
+// phase B': per wave the frame, the decoded block and the Huffman part of a ZsScratch; two 4-wave
+// workgroups per CU (one-wave workgroups, eleven per CU, measured 18 % slower)
 constexpr uint32_t kZfHufThreads = 256;
-constexpr uint32_t kZfHufWave = kZsFastInCap + 16 + kZfOutLds + kZsScratch;
+constexpr uint32_t kZfHufWave = kZsFastInCap + 16 + kZfOutLds + kZsHufScratch;
 
 struct ZfShared {
   ZsShared fse;  // the predefined LL / ML / OF decoding tables
