@@ -18,6 +18,8 @@
 
 using namespace slate;
 
+thread_local size_t t_copy_threads = kCopyThreads;
+
 // memcpy split over threads for large copies between caller memory and page-locked staging
 // (one core copies ~10 GB/s, below what the PCIe link moves).  16 threads: the CPU share one
 // GPU's process gets on the MI355X boxes.
@@ -27,7 +29,7 @@ void par_memcpy(void* dst, const void* src, size_t n) {
     if (n) memcpy(dst, src, n);
     return;
   }
-  const size_t t = std::min<size_t>(kCopyThreads, n / kPiece);
+  const size_t t = std::max<size_t>(1, std::min<size_t>(t_copy_threads, n / kPiece));
   const size_t step = (n + t - 1) / t;
   std::vector<std::thread> th;
   for (size_t i = 1; i < t; i++) {
@@ -155,10 +157,10 @@ uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len) {
   return 0;
 }
 
-// Run fn(lo, hi) over [0, n) split across up to kCopyThreads threads (pieces of >= grain).
+// Run fn(lo, hi) over [0, n) split across up to t_copy_threads threads (pieces of >= grain).
 template <typename F>
 void par_for(size_t n, size_t grain, F fn) {
-  const size_t t = std::max<size_t>(1, std::min<size_t>(kCopyThreads, n / std::max<size_t>(grain, 1)));
+  const size_t t = std::max<size_t>(1, std::min<size_t>(t_copy_threads, n / std::max<size_t>(grain, 1)));
   if (t == 1) {
     fn(size_t(0), n);
     return;
@@ -222,7 +224,10 @@ int lane_finish(PipeLane& L, Sink& o) {
 // next chunk queued and the host thread spends its time copying.
 // out_off/row_base are always filled; when the outputs do not fit (or are absent) the
 // remaining chunks are only planned and SLATE_E_CAPACITY is returned.
-int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o) {
+// gsrc (sharded decode): local block j's bytes start at in + gsrc[j] (in_off then gives only
+// the local layout, i.e. the sizes); null = block j at in + in_off[j].
+int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o,
+                const uint64_t* gsrc = nullptr) {
   SLATE_HIP(ctx_bind(ctx));
   const bool trace = host_trace();
   const double t_start = trace ? now_ms() : 0.0;
@@ -260,7 +265,17 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
     SLATE_HIP(L.d_row_base.ensure((size_t(m) + 1) * 8));
     SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes(m) + 64));
     const double t0 = trace ? now_ms() : 0.0;
-    par_memcpy(L.h_in.p, in + lo, bytes);
+    if (gsrc) {
+      uint8_t* h = L.h_in.as<uint8_t>();
+      par_for(m, 2048, [&](size_t a, size_t e2) {
+        for (size_t i = a; i < e2; i++) {
+          const uint64_t len = in_off[b + i + 1] - in_off[b + i];
+          if (len) memcpy(h + (in_off[b + i] - lo), in + gsrc[b + i], len);
+        }
+      });
+    } else {
+      par_memcpy(L.h_in.p, in + lo, bytes);
+    }
     const double t1 = trace ? now_ms() : 0.0;
     uint64_t* ho = L.h_in_off.as<uint64_t>();
     for (uint32_t i = 0; i <= m; i++) ho[i] = in_off[b + i] - lo;
@@ -276,7 +291,8 @@ int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in
       po[0] = pr[0] = 0;
       par_for(m, 4096, [&](size_t a, size_t e2) {
         for (size_t i = a; i < e2; i++) {
-          const uint64_t dl = host_decoded_len(codec, in + in_off[b + i], in_off[b + i + 1] - in_off[b + i]);
+          const uint64_t src = gsrc ? gsrc[b + i] : in_off[b + i];
+          const uint64_t dl = host_decoded_len(codec, in + src, in_off[b + i + 1] - in_off[b + i]);
           po[i + 1] = align16(dl);
           pr[i + 1] = row_capacity(dl);
         }
@@ -460,41 +476,60 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
   if (!ctxs || n_ctx == 0 || !in_off || !out_off || !row_base || (n && !in)) return SLATE_E_INVALID_ARG;
   for (uint32_t g = 0; g < n_ctx; g++)
     if (!ctxs[g]) return SLATE_E_INVALID_ARG;
+  // No re-pack: each context's staging gathers its blocks straight from the caller's buffer.
   struct Shard {
-    std::vector<uint8_t> in;
-    std::vector<uint64_t> in_off, out_off, row_base;
+    std::vector<uint64_t> in_off, gsrc, out_off, row_base;
     uint32_t m = 0;
     int st = SLATE_OK;
   };
   std::vector<Shard> sh(n_ctx);
+  const size_t share = std::max<size_t>(1, kCopyThreads / n_ctx);
   auto run = [&](auto&& fn) {
     std::vector<std::thread> th;
-    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(fn, g);
-    fn(0);
+    auto body = [&](uint32_t g) {
+      t_copy_threads = share;
+      fn(g);
+    };
+    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(body, g);
+    const size_t keep = t_copy_threads;
+    body(0);
+    t_copy_threads = keep;
     for (auto& t : th) t.join();
     for (uint32_t g = 0; g < n_ctx; g++)
       if (sh[g].st) return sh[g].st;
     return int(SLATE_OK);
   };
-  // phase 1: each context packs and plans its shard (block i -> context i mod n_ctx)
+  // phase 1: each context's layout (block i -> context i mod n_ctx) and plan -- on the host for
+  // None / Snappy (the varint header), else by a plan-only pass on the context's GPU
   int st = run([&](uint32_t g) {
     Shard& S = sh[g];
     S.m = shard_count(n, n_ctx, g);
     S.in_off.assign(size_t(S.m) + 1, 0);
+    S.gsrc.assign(size_t(S.m) + 1, 0);
     S.out_off.assign(size_t(S.m) + 1, 0);
     S.row_base.assign(size_t(S.m) + 1, 0);
-    uint64_t bytes = 0;
     for (uint32_t j = 0; j < S.m; j++) {
       const uint64_t i = uint64_t(g) + uint64_t(j) * n_ctx;
-      bytes += in_off[i + 1] - in_off[i];
+      if (in_off[i + 1] < in_off[i]) {
+        S.st = SLATE_E_INVALID_ARG;
+        return;
+      }
+      S.gsrc[j] = in_off[i];
+      S.in_off[j + 1] = S.in_off[j] + (in_off[i + 1] - in_off[i]);
     }
-    S.in.resize(bytes + 1);
-    S.st = slate_shard_pack(in, in_off, n, n_ctx, g, S.in.data(), bytes, S.in_off.data());
-    if (S.st || S.m == 0) return;
+    if (S.m == 0) return;
+    if (host_plannable(codec)) {
+      for (uint32_t j = 0; j < S.m; j++) {
+        const uint64_t dl = host_decoded_len(codec, in + S.gsrc[j], S.in_off[j + 1] - S.in_off[j]);
+        S.out_off[j + 1] = S.out_off[j] + align16(dl);
+        S.row_base[j + 1] = S.row_base[j] + row_capacity(dl);
+      }
+      return;
+    }
     Sink o;  // no meta: plan only
     o.out_off = S.out_off.data();
     o.row_base = S.row_base.data();
-    const int r = host_decode(ctxs[g], codec, S.in.data(), S.in_off.data(), S.m, o);
+    const int r = host_decode(ctxs[g], codec, in, S.in_off.data(), S.m, o, S.gsrc.data());
     S.st = r == SLATE_E_CAPACITY ? SLATE_OK : r;
   });
   if (st) return st;
@@ -523,7 +558,7 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
     o.g = g;
     o.g_out_off = out_off;
     o.g_row_base = row_base;
-    S.st = host_decode(ctxs[g], codec, S.in.data(), S.in_off.data(), S.m, o);
+    S.st = host_decode(ctxs[g], codec, in, S.in_off.data(), S.m, o, S.gsrc.data());
   });
 }
 

@@ -192,6 +192,9 @@ inline double now_ms() {
 // Host copies split over up to kCopyThreads threads (16: the CPU share one GPU's process gets on
 // the MI355X boxes; one core copies ~10 GB/s, below the PCIe link) -- api_host.cpp.
 constexpr size_t kCopyThreads = 16;
+// The calling thread's share of those threads: a sharded decode runs one host thread per
+// context and gives each kCopyThreads / contexts of them (api_host.cpp).
+extern thread_local size_t t_copy_threads;
 void par_memcpy(void* dst, const void* src, size_t n);
 // A pipeline lane's stream and events, created on first use.
 hipError_t lane_init(PipeLane& L);

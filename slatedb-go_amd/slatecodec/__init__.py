@@ -425,6 +425,15 @@ def decode_sharded(ctxs: list["Context"], codec: int, blob: np.ndarray, in_off: 
     return out, out_off, meta[:n], rows, row_base
 
 
+def decode_sharded_into(ctxs: list["Context"], codec: int, blob: np.ndarray, in_off: np.ndarray, out: np.ndarray,
+                        rows: np.ndarray, meta: np.ndarray, out_off: np.ndarray, row_base: np.ndarray) -> int:
+    """slate_block_decode_sharded into caller-sized buffers (one pass). Returns the status."""
+    hs = (C.c_void_p * len(ctxs))(*[c.handle for c in ctxs])
+    return lib().slate_block_decode_sharded(hs, len(ctxs), codec, _ptr(blob), _ptr(in_off), len(in_off) - 1,
+                                            _ptr(out), out.size, _ptr(out_off), _ptr(meta), _ptr(rows), rows.size,
+                                            _ptr(row_base))
+
+
 class Index:
     def __init__(self, h):
         self._h = h
