@@ -1279,6 +1279,13 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
       }
     }
 #endif
+  } else if (a.codec == SLATE_CODEC_LZ4 && !a.raw && !(dbg_bits(a) & 16)) {
+    // one-block frames lane per block (decode_lpb2.hip), then the exact path over the hand-backs
+    (void)hipMemsetAsync(s.zf.count, 0, 2 * sizeof(uint32_t), st);
+    hipError_t e = launch_lz4_fast(st, a, s.zf, num_cus);
+    if (e != hipSuccess) return e;
+    decode_list_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);
+    decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else {
     decode_fast_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a);
     decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);

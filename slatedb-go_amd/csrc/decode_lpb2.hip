@@ -50,6 +50,11 @@ namespace {
 // ring positions still valid behind d: a step's store reaches 20 bytes past d's dword
 // (five dwords), i.e. 109 bytes behind d modulo the ring
 constexpr uint32_t kReach = kOR - 20;
+// CodecLz4 frame constants (LZ4 frame format; decode.hip has the exact path's copies)
+constexpr uint32_t kLz4Magic = 0x184D2204u;
+constexpr uint32_t kXP1 = 2654435761u, kXP2 = 2246822519u, kXP3 = 3266489917u, kXP4 = 668265263u,
+                   kXP5 = 374761393u;
+__device__ __forceinline__ uint32_t xrotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 constexpr uint32_t kUnflushed = 80;    // d - 16*fl before a step may advance d (see the throttle)
 #ifndef SLATE_LPB_NS
 #define SLATE_LPB_NS 8
@@ -64,7 +69,14 @@ constexpr uint32_t kIR = kNS * 16;
 // two b64 halves.
 constexpr uint32_t kOutStride = kOR + 8;
 constexpr uint32_t kInStride = kIR + 8;
-constexpr uint32_t kVerifyBatch = 4;    // blocks per wait in the cooperative row check
+#ifndef SLATE_VERIFY_BATCH
+#define SLATE_VERIFY_BATCH 4
+#endif
+constexpr uint32_t kVerifyBatch = SLATE_VERIFY_BATCH;
+#ifndef SLATE_WALK_LAG
+#define SLATE_WALK_LAG 64
+#endif
+constexpr uint32_t kWalkLag = SLATE_WALK_LAG;  // walker lag (bytes) that calls it a second time in an iteration  // blocks per wait in the cooperative row check
 
 __device__ __forceinline__ v4u pack_row(uint32_t off, uint32_t pl, uint32_t sl, uint32_t vl, uint32_t flags,
                                         uint32_t meta_len, uint32_t status) {
@@ -134,6 +146,10 @@ struct Lane {
   uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
   int32_t fk;    // first key length for the prefix check (row.go:203-206), -1 before row 0 decodes
   uint32_t pl0;  // row 0's prefix-length field: block.go's FirstKey length when offsets[0] == 0
+  // CodecLz4 (kLz4 instantiation only): the frame's one data block is payload bytes [s0, sn);
+  // lph = what the next parse reads (0 a token, 1 a match, 2 nothing: the last literals are
+  // out); mtok = the token's match nibble; hb = hand the block to the exact path
+  uint32_t sn, lph, mtok, hb;
 };
 
 struct Rsrc {
@@ -319,10 +335,83 @@ __device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q, v4u& FD, uint8
   L.fpend = 0;
 }
 
+// Appends item to list (wave-aggregated: one atomic per wave); every lane of the wave calls it.
+__device__ __forceinline__ void lpb_list_append(bool want, uint32_t item, uint32_t* list, uint32_t* count) {
+  const uint64_t m = __ballot(want);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == uint32_t(__builtin_ctzll(m))) base = atomicAdd(count, uint32_t(__builtin_popcountll(m)));
+  base = __shfl(base, __builtin_ctzll(m), 64);
+  if (want) list[base + uint32_t(__builtin_popcountll(m & ((uint64_t(1) << lane) - 1)))] = item;
+}
+
+// CodecLz4: the next sequence half of the frame's data block (LZ4 block format: token,
+// literal length extension bytes, literals, little-endian offset, match length extension
+// bytes), read from the input ring like a Snappy tag: a token starts a literal run, the
+// offset after the literals starts a match.  The checks are the exact path's
+// (decode.hip wave_lz4_decode) for one independent block; a run of extension bytes
+// longer than the 8-byte window, or any failed check, hands the block to the exact path
+// (L.hb), which then decodes and reports it.  A zero-length literal run costs one step.
+__device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, int32_t avail, bool& hole_new,
+                                          uint32_t& hole_src) {
+  const bool need = act && !L.dd && L.rem == 0;
+  const bool fin = need && L.lph == 2;
+  const bool room_out = L.d - 16 * L.fl <= kUnflushed;
+  const bool can = need & (L.lph < 2) & (avail >= int32_t(min(L.s + 8, L.clen))) & room_out;
+  const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
+  const bool tokp = L.lph == 0;
+  const uint32_t n4 = tokp ? (w.x >> 4) & 15 : L.mtok;  // the length nibble
+  // extension bytes: 7 after a token, 6 after an offset; k = how many 255s lead them
+  const uint64_t w64 = (uint64_t(w.y) << 32) | w.x;
+  const uint64_t ext = tokp ? w64 >> 8 : w64 >> 16;
+  const uint64_t nz = ~ext & (tokp ? 0x00FFFFFFFFFFFFFFull : 0x0000FFFFFFFFFFFFull);
+  const uint32_t k = uint32_t(__builtin_ctzll(nz | (uint64_t(1) << 63))) >> 3;
+  const uint32_t e = uint32_t(ext >> (8 * k)) & 0xff;
+  const bool lng = n4 == 15;
+  const uint32_t len = lng ? 15 + 255 * k + e : n4;
+  const uint32_t hl = (tokp ? 1u : 2u) + (lng ? k + 1 : 0u);
+  const uint32_t s1 = L.s + hl;
+  const bool ext_bad = lng && nz == 0;  // the run goes on past the window
+  const uint32_t room = L.dn - L.d;  // min(plan capacity, block maximum) left; the exact decoder's bounds
+  // token: literals [s1, s1 + len); the last sequence's literals end the block exactly
+  const uint32_t lit_end = s1 + len;
+  const bool bad_tok = lit_end > L.sn || len > room;
+  const bool last = lit_end == L.sn;
+  // match: offset, then the length (+4); a match may not end the block (a token must follow)
+  const uint32_t off = w.x & 0xffff, ml = len + 4;
+  const bool bad_m = L.s + 2 > L.sn || s1 >= L.sn || off == 0 || off > L.d || ml > room;
+  const bool bad = ext_bad || (tokp ? bad_tok : bad_m);
+  const bool ok = can && !bad;
+  L.hb |= (can && bad) ? 1u : 0u;
+  L.dd |= (fin || (can && bad)) ? 1u : 0u;
+  L.lit = ok ? uint32_t(tokp) : L.lit;
+  L.rem = ok ? (tokp ? len : ml) : L.rem;
+  L.src = ok ? (tokp ? s1 : L.d - off) : L.src;
+  L.eff = ok ? (tokp ? 16u : off) : L.eff;
+  const bool far = !tokp && off > kReach;
+  L.far = ok ? uint32_t(far) : L.far;
+  L.s = ok ? (tokp ? lit_end : s1) : L.s;
+  L.mtok = (ok && tokp) ? (w.x & 15) : L.mtok;
+  L.lph = ok ? (tokp ? (last ? 2u : 1u) : 0u) : L.lph;
+  // the decoded length is known once the last literals are parsed
+  const bool fix = ok && tokp && last;
+  L.dn = fix ? L.d + len : L.dn;
+  L.rneed = fix ? min(L.rneed, L.d + len) : L.rneed;
+  hole_new = ok && far && ml <= 16 && !L.hpend && !L.fpend;
+  hole_src = L.d - off;
+  L.hd = hole_new ? L.d : L.hd;
+  L.hl = hole_new ? ml : L.hl;
+  L.hpend = hole_new ? 1u : L.hpend;
+  L.d += hole_new ? ml : 0u;
+  L.rem = hole_new ? 0u : L.rem;
+  L.far = hole_new ? 0u : L.far;
+}
+
 // One step: CRC (two of four steps), parse, copy, the far-copy / hole load, and the row
 // walker (the other two steps).
 // kSlot: 0 and 2 absorb a CRC chunk; 1 and (when needed) 3 run the walker
-template <int kSlot>
+template <int kSlot, bool kLz4>
 __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint8_t* ring,
                                           uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
@@ -335,9 +424,12 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     else crc_chunk(L, in, tab, go);
   }
   const int32_t avail = int32_t(16 * L.c_commit) - int32_t(L.sh);  // committed payload bytes [0, avail)
-  const uint32_t sn = L.clen;
   bool hole_new = false;
   uint32_t hole_src = 0;
+  if constexpr (kLz4) {
+    lz4_parse(L, act, in, avail, hole_new, hole_src);
+  } else {
+  const uint32_t sn = L.clen;
   // ---- parse the next tag (golang/snappy decode_other.go:19-110)
   {
     const bool need = act && !L.dd && L.rem == 0;
@@ -383,6 +475,7 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     L.rem = hole_new ? 0u : L.rem;
     L.far = hole_new ? 0u : L.far;
   }
+  }
   // ---- move up to 16 bytes of the current tag into the output ring
   {
     const bool cp = act && !L.dd && L.rem != 0;
@@ -422,7 +515,7 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     // the walker: every iteration once, and a second time only when some lane's walker has
     // fallen more than 64 bytes behind (rows shorter than the iteration's output)
     if (kSlot == 1 ||
-        (kSlot == 3 && __builtin_amdgcn_ballot_w64(act & (L.rphase < 3) & (L.d >= L.rneed) & (L.d - L.R > 64)))) {
+        (kSlot == 3 && __builtin_amdgcn_ballot_w64(act & (L.rphase < 3) & (L.d >= L.rneed) & (L.d - L.R > kWalkLag)))) {
       v4u row;
       uint32_t ridx;
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
@@ -459,7 +552,53 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
 
 }  // namespace
 
-__global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a) {
+// The LZ4 frame descriptor check (HC = second byte of XXH32(FLG .. DictID), seed 0) for the two
+// descriptor lengths the fast path takes: 2 bytes (FLG, BD) or 10 (+ content size).
+__device__ __forceinline__ uint32_t lz4_xxh_avalanche(uint32_t h) {
+  h ^= h >> 15;
+  h *= kXP2;
+  h ^= h >> 13;
+  h *= kXP3;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t lz4_xxh_byte(uint32_t h, uint32_t b) { return xrotl(h + b * kXP5, 11) * kXP1; }
+__device__ __forceinline__ uint32_t lz4_xxh_word(uint32_t h, uint32_t w) { return xrotl(h + w * kXP3, 17) * kXP4; }
+
+// One LZ4 frame per block on the fast path: magic, FLG/BD as lz4_header, no dictionary, no block
+// checksums, the descriptor checksum, then exactly one compressed data block followed by the
+// EndMark and (FLG bit 2) the content checksum, ending the payload.  payload bytes 0..23 are
+// dwords d[0..5] (from the first three committed chunks).  On success the lane's parse state is
+// set and the function returns true; anything else goes to the exact path.
+__device__ __forceinline__ bool lz4_frame_head(Lane& L, const uint32_t* d, uint32_t cap, uint32_t& want_size) {
+  auto byte = [&](uint32_t i) { return (d[i >> 2] >> (8 * (i & 3))) & 0xffu; };
+  const uint32_t flg = byte(4), bd = byte(5);
+  const bool csize = (flg & 8) != 0;
+  bool ok = d[0] == kLz4Magic && (flg >> 6) == 1 && !(flg & 2) && !(bd & 0x8F) && ((bd >> 4) & 7) >= 4 &&
+            !(flg & 1) && !(flg & 0x10);
+  const uint32_t bmax = 1u << (8 + 2 * ((bd >> 4) & 7));
+  // descriptor checksum: XXH32 of bytes 4..5 or 4..13
+  uint32_t h2 = lz4_xxh_byte(lz4_xxh_byte(kXP5 + 2, flg), bd);
+  uint32_t h10 = lz4_xxh_word(lz4_xxh_word(kXP5 + 10, d[1]), d[2]);  // bytes 4..7, 8..11
+  h10 = lz4_xxh_byte(lz4_xxh_byte(h10, byte(12)), byte(13));
+  const uint32_t hc = csize ? byte(14) : byte(6);
+  ok = ok && hc == ((lz4_xxh_avalanche(csize ? h10 : h2) >> 8) & 0xff);
+  // the content size (8 bytes LE after BD) must fit 32 bits; compared with the output at the end
+  want_size = csize ? d[1] >> 16 | d[2] << 16 : 0xFFFFFFFFu;
+  ok = ok && (!csize || ((d[2] >> 16 | d[3] << 16) == 0 && want_size != 0xFFFFFFFFu));
+  const uint32_t p = csize ? 15u : 7u;  // the first block size
+  const uint32_t bs = csize ? (d[3] >> 24 | d[4] << 8) : (d[1] >> 24 | d[2] << 8);
+  const uint32_t tail = (flg & 4) ? 8u : 4u;  // EndMark (+ content checksum)
+  ok = ok && bs != 0 && !(bs >> 31) && bs <= bmax && uint64_t(p) + 4 + bs + tail == L.clen;
+  L.s = p + 4;
+  L.sn = p + 4 + bs;
+  L.lph = 0;
+  L.dn = min(cap, bmax);
+  return ok;
+}
+
+template <bool kLz4>
+__global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   {
@@ -527,6 +666,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     L.rsl = L.rpl = L.rflags = L.ro = L.nwalk = 0;
     L.fk = -1;
     L.pl0 = 0xFFFFFFFFu;
+    L.sn = L.lph = L.mtok = L.hb = 0;
+    uint32_t want_size = 0xFFFFFFFFu;  // CodecLz4: the frame's content size (0xFFFFFFFF: none)
     if (have) {
       const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
       if (len < (a.raw ? 4u : 6u)) {
@@ -552,7 +693,23 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     {
       const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(R.in, have ? L.in_rel : kOOB, 0, 0);
       const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && L.last_chunk >= 1) ? L.in_rel + 16 : kOOB, 0, 0);
-      if (have) {
+      if constexpr (kLz4) {
+        // CodecLz4: three chunks hold the frame head at any alignment (sh + 19 <= 34 bytes)
+        const v4u c2 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && L.last_chunk >= 2) ? L.in_rel + 32 : kOOB, 0, 0);
+        if (have) {
+          wr128(in, c0, L.z);
+          wr128(in + 16, c1, L.z);
+          wr128(in + 32, c2, L.z);
+          L.c_commit = min(L.last_chunk + 1, 3u);
+          L.c_issue = L.c_commit;
+          const v2u q0 = ring_rd8(in, L.sh, kIR - 8), q1 = ring_rd8(in, L.sh + 8, kIR - 8),
+                    q2 = ring_rd8(in, L.sh + 16, kIR - 8);
+          const uint32_t dw[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
+          const uint32_t cap = uint32_t(min<uint64_t>(a.out_off[b + 1] - a.out_off[b], 0xFFFFFFF0ull));
+          if (lz4_frame_head(L, dw, cap, want_size)) L.dd = 0;
+          else L.hb = 1;
+        }
+      } else if (have) {
         wr128(in, c0, L.z);
         wr128(in + 16, c1, L.z);
         L.c_commit = L.last_chunk >= 1 ? 2u : 1u;
@@ -618,10 +775,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         L.n_req = n;
       }
       absorb_far(L, Q, FD, ring);
-      lane_step<0>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      lane_step<1>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      lane_step<2>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      lane_step<3>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<0, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<1, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<2, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
+      lane_step<3, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
       // the far-copy / hole source requested in this iteration (at most one per lane; sc1:
       // L1 bypass), before the flush stores so that vmcnt waits stay static; it is merged
       // at the start of the next iteration
@@ -644,17 +801,30 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
     slate_row* grows = reinterpret_cast<slate_row*>(reinterpret_cast<uint8_t*>(rows_base) + L.rows_rel);
     // rows stage: 0 = no rows to produce, 1 = walked rows to verify, 2 = re-derive from HBM
     uint32_t rows_stage = 0, nr = 0, osi_u = 0;
+    bool hand_back = false;            // CodecLz4: the exact path decodes this block
+    uint32_t rec_info = 0, rec_want = 0;  // CodecLz4: what the content-checksum pass checks
     if (have) {
       const uint32_t stored = __builtin_bswap32(ring_rd8(in, L.sh + L.clen, kIR - 8).x);
       // the register absorbed t zero bytes after the payload: compare against stored * x^(8t)
       const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
       const bool crc_ok = gf2_mulmod(~stored, crc_tail[t]) == L.crc;
-      const bool snappy_ok = !L.err && L.d == L.dn && L.s == L.clen && L.rem == 0;
+      bool dec_ok;
+      if constexpr (kLz4) {
+        // the data block ended on its last literals, then the EndMark; the content size if any
+        const uint32_t endmark = ring_rd8(in, L.sh + L.sn, kIR - 8).x;
+        dec_ok = !L.hb && L.lph == 2 && L.rem == 0 && L.s == L.sn && L.d == L.dn && endmark == 0 &&
+                 (want_size == 0xFFFFFFFFu || want_size == L.d);
+        hand_back = crc_ok && !dec_ok;
+        rec_want = ring_rd8(in, L.sh + L.sn + 4, kIR - 8).x;
+        rec_info = (crc_ok && dec_ok && L.clen - L.sn == 8) ? (kZfFast | kZfSum) << 16 : 0u;
+      } else {
+        dec_ok = !L.err && L.d == L.dn && L.s == L.clen && L.rem == 0;
+      }
       const uint32_t dn = L.dn;
       if (!crc_ok) {
         m.status = SLATE_E_BLOCK_CHECKSUM;
-      } else if (!snappy_ok) {
-        m.status = SLATE_E_SNAPPY_CORRUPT;
+      } else if (!dec_ok) {
+        m.status = SLATE_E_SNAPPY_CORRUPT;  // (CodecLz4: handed back, not written)
       } else {
         // remaining output chunks (the last one is padded inside its 16-byte slot)
         while (L.fl * 16 < dn) {
@@ -736,6 +906,17 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a)
         }
       }
     }
+    if constexpr (kLz4) {
+      if (b < rend) {
+        ZsFastRec rc{};
+        rc.info = rec_info;
+        rc.produced = L.d;
+        rc.want = rec_want;
+        z.rec[b] = rc;
+      }
+      lpb_list_append(hand_back, b, z.list, z.count);
+      if (hand_back) have = false;
+    }
     // ---- wave-cooperative check of the walked row starts against offsets[] (block.go:107-118):
     // per block, coalesced loads of its offsets and row descriptors; eight blocks per wait
     {
@@ -815,17 +996,108 @@ size_t lpb2_lds_bytes() {
   return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
-hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {
-  if (a.n == 0) return hipGetLastError();
+// CodecLz4 content checksum of the fast path's blocks (FLG bit 2), lane per block: XXH32 (seed
+// 0) of the decoded block, its four stripe accumulators' chains advanced for 64 blocks per wave
+// instruction.  Each iteration brings the next 64 bytes of every block with transposed loads
+// (in load j, lanes 4i..4i+3 read one 64-byte run of block 16j+i) issued one iteration ahead;
+// the loading lanes put them into the owner's LDS slot.  A mismatch goes to the exact path.
+constexpr uint32_t kLz4SumThreads = 256;
+__global__ __launch_bounds__(kLz4SumThreads) void lz4_fast_sum_kernel(DecodeArgs a, ZsFastArgs z) {
+  __shared__ __attribute__((aligned(16))) uint8_t slots[kLz4SumThreads * 64];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+  uint8_t* slots0 = slots + wave_lane0 * 64;
+  const uint8_t* mine = slots0 + lane * 64;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
+    const uint32_t b = r0 + lane;
+    const uint32_t rend = min(r0 + 64, a.n);
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(a.out + a.out_off[r0], a.out_off[rend] - a.out_off[r0]);
+    uint32_t orel = 0, len = 0, want = 0;
+    bool act = false;
+    if (b < a.n) {
+      const ZsFastRec rec = z.rec[b];
+      act = ((rec.info >> 16) & kZfSum) != 0;
+      len = act ? rec.produced : 0u;
+      want = rec.want;
+      orel = uint32_t(a.out_off[b] - a.out_off[r0]);
+    }
+    const uint32_t groups = (len + 63) / 64, stripes = len / 16;
+    uint32_t v0 = kXP1 + kXP2, v1 = kXP2, v2 = 0, v3 = 0u - kXP1;
+    v4u g[4];
+    auto load = [&](uint32_t t) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+        const uint32_t g_o = __shfl(groups, int(o), 64), rel_o = __shfl(orel, int(o), 64);
+        g[j] = bload<0>(R, t < g_o ? rel_o + 64 * t + 16 * c : kOOB);
+      }
+    };
+    load(0);
+    for (uint32_t t = 0; __ballot(t < groups); t++) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+        if (t < uint32_t(__shfl(groups, int(o), 64))) *reinterpret_cast<v4u*>(slots0 + o * 64 + 16 * c) = g[j];
+      }
+      load(t + 1);  // in flight during this iteration
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (uint32_t h = 0; h < 4; h++) {
+        if (4 * t + h < stripes) {
+          const v4u w = *reinterpret_cast<const v4u*>(mine + 16 * h);
+          v0 = xrotl(v0 + w.x * kXP2, 13) * kXP1;
+          v1 = xrotl(v1 + w.y * kXP2, 13) * kXP1;
+          v2 = xrotl(v2 + w.z * kXP2, 13) * kXP1;
+          v3 = xrotl(v3 + w.w * kXP2, 13) * kXP1;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    bool bad = false;
+    if (act) {
+      uint32_t h = len >= 16 ? xrotl(v0, 1) + xrotl(v1, 7) + xrotl(v2, 12) + xrotl(v3, 18) : kXP5;
+      h += len;
+      // the tail (< 16 bytes) lies in the last group, still in this lane's slot
+      const uint8_t* tail = mine - 64 * ((len - 1) / 64);  // tail[i] = decoded byte i (len > 0)
+      uint32_t i = len & ~15u;
+      for (; i + 4 <= len; i += 4) h = lz4_xxh_word(h, *reinterpret_cast<const uint32_t*>(tail + i));
+      for (; i < len; i++) h = lz4_xxh_byte(h, tail[i]);
+      bad = lz4_xxh_avalanche(h) != want;
+    }
+    lpb_list_append(bad, b, z.list, z.count);
+  }
+}
+
+template <bool kLz4>
+hipError_t launch_lpb(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
   const size_t lds = lpb2_lds_bytes();
   const uint32_t waves_needed = (a.n + 63) / 64;
   uint32_t grid = (waves_needed + kLpb2Threads / 64 - 1) / (kLpb2Threads / 64);
   grid = min(grid, uint32_t(num_cus) * uint32_t(163840 / lds));
   // one workgroup takes (nearly) the whole 160 KiB LDS of a CU
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_lpb2_kernel),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_lpb2_kernel<kLz4>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
   if (attr != hipSuccess) return attr;
-  decode_lpb2_kernel<<<grid, kLpb2Threads, lds, st>>>(a);
+  decode_lpb2_kernel<kLz4><<<grid, kLpb2Threads, lds, st>>>(a, z);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {
+  if (a.n == 0) return hipGetLastError();
+  return launch_lpb<false>(st, a, ZsFastArgs{}, num_cus);
+}
+
+hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
+  if (a.n == 0) return hipGetLastError();
+  hipError_t e = launch_lpb<true>(st, a, z, num_cus);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = min((a.n + kLz4SumThreads - 1) / kLz4SumThreads, uint32_t(num_cus) * 4u);
+  lz4_fast_sum_kernel<<<grid, kLz4SumThreads, 0, st>>>(a, z);
   return hipGetLastError();
 }
 

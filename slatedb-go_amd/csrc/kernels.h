@@ -88,6 +88,9 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
+// CodecLz4 blocks: the lane-per-block decoder for one-block frames, then their XXH32 content
+// checksums; every other shape and any failed check is appended to z.list for the exact path.
+hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
 // CodecZstd fast path (zstd_fast.hip): plan sizes of single-frame blocks (the rest appended to
 // list for the wave plan); decode phases A-C (blocks for the exact path appended to z.list).
 hipError_t launch_zstd_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,

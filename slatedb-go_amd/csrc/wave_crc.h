@@ -29,10 +29,30 @@ struct CrcTables16 {
 static __constant__ CrcTables16 g_crc16 = CrcTables16();
 constexpr uint32_t kTab16Bytes = 16 * 256 * 4;
 
+// v_bitop3_b32 with the truth table of a ^ b ^ c (the compiler re-chains plain XORs)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // the CRC register after the 16 bytes (x, y, z, w) (little-endian dwords), tables in LDS
 __device__ __forceinline__ uint32_t crc16_step(const uint32_t* tab, uint32_t c, uint32_t vx, uint32_t vy, uint32_t vz,
                                                uint32_t vw) {
   const uint32_t x = c ^ vx;
+#ifdef SLATE_CRC_TREE
+  // the 16 lookups folded as a balanced tree of three-input XORs (4 levels instead of a
+  // 15-deep chain)
+  const uint32_t a0 = tab[15 * 256 + (x & 0xff)], a1 = tab[14 * 256 + ((x >> 8) & 0xff)],
+                 a2 = tab[13 * 256 + ((x >> 16) & 0xff)], a3 = tab[12 * 256 + (x >> 24)];
+  const uint32_t b0 = tab[11 * 256 + (vy & 0xff)], b1 = tab[10 * 256 + ((vy >> 8) & 0xff)],
+                 b2 = tab[9 * 256 + ((vy >> 16) & 0xff)], b3 = tab[8 * 256 + (vy >> 24)];
+  const uint32_t c0 = tab[7 * 256 + (vz & 0xff)], c1 = tab[6 * 256 + ((vz >> 8) & 0xff)],
+                 c2 = tab[5 * 256 + ((vz >> 16) & 0xff)], c3 = tab[4 * 256 + (vz >> 24)];
+  const uint32_t d0 = tab[3 * 256 + (vw & 0xff)], d1 = tab[2 * 256 + ((vw >> 8) & 0xff)],
+                 d2 = tab[1 * 256 + ((vw >> 16) & 0xff)], d3 = tab[vw >> 24];
+  const uint32_t e0 = xor3(a0, a1, a2), e1 = xor3(a3, b0, b1), e2 = xor3(b2, b3, c0), e3 = xor3(c1, c2, c3),
+                 e4 = xor3(d0, d1, d2);
+  const uint32_t r = xor3(xor3(e0, e1, e2), xor3(e3, e4, d3), 0u);
+#else
   uint32_t r = tab[15 * 256 + (x & 0xff)] ^ tab[14 * 256 + ((x >> 8) & 0xff)] ^ tab[13 * 256 + ((x >> 16) & 0xff)] ^
                tab[12 * 256 + (x >> 24)];
   r ^= tab[11 * 256 + (vy & 0xff)] ^ tab[10 * 256 + ((vy >> 8) & 0xff)] ^ tab[9 * 256 + ((vy >> 16) & 0xff)] ^
@@ -41,6 +61,7 @@ __device__ __forceinline__ uint32_t crc16_step(const uint32_t* tab, uint32_t c, 
        tab[4 * 256 + (vz >> 24)];
   r ^= tab[3 * 256 + (vw & 0xff)] ^ tab[2 * 256 + ((vw >> 8) & 0xff)] ^ tab[1 * 256 + ((vw >> 16) & 0xff)] ^
        tab[vw >> 24];
+#endif
   return r;
 }
 

@@ -104,3 +104,44 @@ def test_damaged_lz4_blocks(ctx):
     meta = _compare(ctx, blocks, misalign=1)
     st = set(int(x) for x in meta["status"])
     assert {0, 18} <= st, st
+
+
+def _recrc(block: bytes) -> bytes:
+    return _crc(block[:-4])
+
+
+def test_lz4_fast_path_shapes(ctx):
+    """The lane-per-block path (one-block frames: decode_lpb2.hip lz4_parse) and its hand-backs to
+    the exact path: every alignment, content size / checksum options, literal and match length
+    extensions inside and beyond the 8-byte window, far and overlapping matches, damaged content
+    checksums under a valid CRC, multi-block frames and trailing bytes."""
+    rng = random.Random(11)
+    kvs = bg.kv_synthetic(38 * 64, half=True, tomb_every=9)
+    plain = [b[:-4] for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+    blocks = []
+    for i, dec in enumerate(plain):
+        blocks.append(_crc(lz4gen.frame(dec, content_size=i % 3 == 0, content_checksum=i % 4 != 1, rng=rng)))
+    # long literal runs (1, 2 and 7+ extension bytes) and long matches (several extension bytes)
+    for n_lit in (20, 300, 700, 1600, 2200):
+        kv = [(b"key%06d" % j, bytes(rng.randrange(256) for _ in range(n_lit)) + b"x" * 600) for j in range(3)]
+        for dec in (b[:-4] for b in bg.sst_blocks(kv, 1 << 16, ob.NONE)):
+            blocks.append(_crc(lz4gen.frame(dec, rng=rng)))
+    # damaged content checksums and flipped literal bytes under a valid CRC -> LZ4_FRAME_CHECKSUM
+    for dec in plain[:6]:
+        f = bytearray(lz4gen.frame(dec, rng=rng))
+        f[-1] ^= 0x40
+        blocks.append(_crc(bytes(f)))
+        g = bytearray(lz4gen.frame(dec, rng=rng))
+        g[40] ^= 0x01  # inside the first literal run (the header is 7 + 4 bytes)
+        blocks.append(_crc(bytes(g)))
+    # shapes the lane path hands back: two data blocks, trailing bytes, stored, block checksums
+    for dec in plain[6:10]:
+        blocks.append(_crc(lz4gen.frame(dec, block_split=1500, rng=rng)))
+        blocks.append(_crc(lz4gen.frame(dec, rng=rng) + b"\x00\x01"))
+        blocks.append(_crc(lz4gen.frame(dec, stored_p=1.0, rng=rng)))
+        blocks.append(_crc(lz4gen.frame(dec, block_checksum=True, rng=rng)))
+    for mis in (0, 5, 13):
+        meta = _compare(ctx, blocks, misalign=mis)
+        st = [int(x) for x in meta["status"]]
+        assert st.count(0) >= len(plain) + 5, st
+        assert 18 in st or 17 in st, st  # the damaged content checksums
