@@ -186,6 +186,23 @@ __global__ void plan_sizes_kernel(int codec, const uint8_t* __restrict__ in, con
   row_sz[i] = row_capacity(dl);
 }
 
+// plan_sizes_kernel over a list of blocks (list[0 .. *count)): the CodecLz4 frames the lane plan
+// hands back (decode_lpb2.hip plan_lz4_lane_kernel).
+__global__ void plan_list_kernel(int codec, const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                 const uint32_t* list, const uint32_t* count, uint64_t* __restrict__ out_sz,
+                                 uint64_t* __restrict__ row_sz) {
+  const uint32_t items = *count;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < items; k += gridDim.x * blockDim.x) {
+    const uint32_t i = list[k];
+    const uint64_t s0 = in_off[i];
+    uint32_t hdr;
+    uint64_t dl;
+    decoded_len(codec, in + s0, in_off[i + 1] - s0, &dl, &hdr);
+    out_sz[i] = align16(dl);
+    row_sz[i] = row_capacity(dl);
+  }
+}
+
 // CodecZlib sizes: the bytes the in-order inflater writes (also when it then fails;
 // oracle or_block_decode_batch), one wave per block reading the stream from HBM.
 __global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restrict__ in,
@@ -1141,7 +1158,17 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch) {
   DecodeScratch s = carve(scratch, n);
   uint32_t m = n + 1;
-  plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
+  if (codec == SLATE_CODEC_LZ4 && n >= 64) {
+    // one-block frames lane per block; the rest by the serial structure walk over a list (small
+    // batches, e.g. one index or filter payload, take the serial walk directly)
+    (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
+    hipError_t e = launch_lz4_plan(st, in, in_off, n, out_off, row_base, s.zf.list, s.zf.count);
+    if (e != hipSuccess) return e;
+    if (n > 0) plan_list_kernel<<<min((n + 255) / 256, 1024u), 256, 0, st>>>(codec, in, in_off, s.zf.list, s.zf.count,
+                                                                            out_off, row_base);
+  } else {
+    plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
+  }
   if (codec == SLATE_CODEC_ZLIB && n > 0)
     plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
   if (codec == SLATE_CODEC_ZSTD && n > 0) {

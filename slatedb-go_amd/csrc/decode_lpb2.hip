@@ -1073,6 +1073,145 @@ __global__ __launch_bounds__(kLz4SumThreads) void lz4_fast_sum_kernel(DecodeArgs
   }
 }
 
+// CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order
+// decoder writes before its first structural error; decode.hip lz4_frame_len) for frames whose
+// first data block is followed by the EndMark or by nothing: the header checks, then the
+// token / match structure of that block walked without copying (literals are skipped).  The
+// block streams through the lane's 128-byte input ring by the decoder's transposed refills (64
+// bytes per block per iteration), and up to eight sequence halves are parsed per iteration.  A
+// frame with a second data block, or a length extension longer than the 8-byte window, is
+// appended to `list` for the serial plan.
+constexpr uint32_t kLz4PlanThreads = 256;
+constexpr uint32_t kLz4PlanSteps = 8;
+__global__ __launch_bounds__(kLz4PlanThreads) void plan_lz4_lane_kernel(const uint8_t* __restrict__ gin,
+                                                                        const uint64_t* __restrict__ in_off, uint32_t n,
+                                                                        uint64_t* __restrict__ out_sz,
+                                                                        uint64_t* __restrict__ row_sz, uint32_t* list,
+                                                                        uint32_t* count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+  uint8_t* in = smem + threadIdx.x * kInStride;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the scans turn the trailing zero into the totals
+    out_sz[n] = 0;
+    row_sz[n] = 0;
+  }
+  for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < n; r0 += stride) {
+    const uint32_t b = r0 + lane;
+    const uint32_t rend = min(r0 + 64, n);
+    const uint8_t* in_lo = gin + in_off[r0];
+    const uint8_t* in_base = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(in_lo) & ~uintptr_t(15));
+    Rsrc R;
+    R.in = make_rsrc(in_base, align16(uint64_t((gin + in_off[rend]) - in_base)));
+    const uint32_t z = 0;
+    uint32_t sh = 0, rel = 0, clen = 0, last_chunk = 0;
+    bool have = b < rend, fb = false;
+    if (have) {
+      const uint64_t s0 = in_off[b], len = in_off[b + 1] - s0;
+      const uint8_t* p = gin + s0;
+      sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 15);
+      rel = uint32_t((p - sh) - in_base);
+      have = len >= 6;  // decoded_len: a shorter block decodes nothing
+      clen = have ? uint32_t(len - 4) : 0u;
+      last_chunk = have ? uint32_t((sh + clen - 1) >> 4) : 0u;  // the frame's chunks (not the CRC)
+    }
+    // the frame head: three chunks
+    const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(R.in, have ? rel : kOOB, 0, 0);
+    const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && last_chunk >= 1) ? rel + 16 : kOOB, 0, 0);
+    const v4u c2 = __builtin_amdgcn_raw_buffer_load_b128(R.in, (have && last_chunk >= 2) ? rel + 32 : kOOB, 0, 0);
+    wr128(in, c0, z);
+    wr128(in + 16, c1, z);
+    wr128(in + 32, c2, z);
+    uint32_t c_commit = min(last_chunk + 1, 3u), c_issue = c_commit, n_req = 0;
+    // lz4_header: magic, FLG / BD, the descriptor in the buffer; no dictionary
+    const v2u q0 = ring_rd8(in, sh, kIR - 8), q1 = ring_rd8(in, sh + 8, kIR - 8), q2 = ring_rd8(in, sh + 16, kIR - 8);
+    const uint32_t flg = q0.y & 0xff, bd = (q0.y >> 8) & 0xff;
+    const bool csize = (flg & 8) != 0, bcheck = (flg & 0x10) != 0;
+    const uint32_t pos = csize ? 15u : 7u;  // the first block size word (after HC)
+    const bool hdr_ok = have && clen >= 7 && q0.x == kLz4Magic && (flg >> 6) == 1 && !(flg & 2) && !(bd & 0x8F) &&
+                        ((bd >> 4) & 7) >= 4 && clen >= pos && !(flg & 1);
+    const uint32_t bmax = 1u << (8 + 2 * ((bd >> 4) & 7));
+    const uint32_t bs = csize ? (q1.y >> 24 | q2.x << 8) : (q0.y >> 24 | q1.x << 8);
+    const uint32_t sz = bs & 0x7FFFFFFFu;
+    // a block size word, not the EndMark, the block (and its checksum) inside the frame
+    const bool blk = hdr_ok && clen >= pos + 4 && bs != 0 && sz <= bmax &&
+                     uint64_t(clen) - pos - 4 >= uint64_t(sz) + (bcheck ? 4u : 0u);
+    const bool stored = (bs >> 31) != 0;
+    const uint32_t sn = pos + 4 + sz, tail = sn + (bcheck ? 4u : 0u);  // the next block size word
+    uint32_t s = stored ? sn : pos + 4;  // a stored block is not walked
+    uint32_t dl = blk && stored ? sz : 0u, lph = 0, mtok = 0;
+    // ph: 0 walking the block, 1 waiting for the word after it, 2 done
+    uint32_t ph = !blk ? 2u : (stored ? 1u : 0u);
+    v4u P0 = c0, P1 = c0, P2 = c0, P3 = c0;
+    uint32_t S0 = 0xFFFFFFFFu, S1 = 0xFFFFFFFFu, S2 = 0xFFFFFFFFu, S3 = 0xFFFFFFFFu;
+    const uint32_t budget = (clen + 63) / 64 + (clen + 3) / 4 + 8;  // > chunks / 4 + halves / 8: never hit
+    uint32_t it = 0;
+    for (; __ballot(ph < 2 && it < budget); it++) {
+      const bool act = ph < 2 && it < budget;
+      commit_one(smem, S0, P0, z);
+      commit_one(smem, S1, P1, z);
+      commit_one(smem, S2, P2, z);
+      commit_one(smem, S3, P3, z);
+      c_commit += n_req;
+      const uint32_t lo_chunk = (sh + min(s, tail)) >> 4;
+      const uint32_t nq = refill_count(act, lo_chunk, c_issue, last_chunk);
+      const uint32_t info = (c_issue << 3) | nq;
+      load_one(0, lane, wave_lane0, info, rel, R, P0, S0);
+      load_one(1, lane, wave_lane0, info, rel, R, P1, S1);
+      load_one(2, lane, wave_lane0, info, rel, R, P2, S2);
+      load_one(3, lane, wave_lane0, info, rel, R, P3, S3);
+      c_issue += nq;
+      n_req = nq;
+      const int32_t avail = int32_t(16 * c_commit) - int32_t(sh);
+#pragma unroll
+      for (uint32_t k = 0; k < kLz4PlanSteps; k++) {
+        const bool can = act && ph == 0 && avail >= int32_t(min(s + 8, clen));
+        const v2u w = ring_rd8(in, sh + s, kIR - 8);
+        const bool tokp = lph == 0;
+        const uint32_t n4 = tokp ? (w.x >> 4) & 15 : mtok;
+        const uint64_t w64 = (uint64_t(w.y) << 32) | w.x;
+        const uint64_t ext = tokp ? w64 >> 8 : w64 >> 16;
+        const uint64_t nz = ~ext & (tokp ? 0x00FFFFFFFFFFFFFFull : 0x0000FFFFFFFFFFFFull);
+        const uint32_t kk = uint32_t(__builtin_ctzll(nz | (uint64_t(1) << 63))) >> 3;
+        const bool lng = n4 == 15;
+        const uint32_t len = lng ? 15 + 255 * kk + (uint32_t(ext >> (8 * kk)) & 0xff) : n4;
+        const uint32_t s1 = s + (tokp ? 1u : 2u) + (lng ? kk + 1 : 0u);
+        const bool to_list = lng && nz == 0;  // the run goes on past the window
+        // lz4_frame_len: the token at s < sz, its literals inside the block and the block maximum
+        const uint32_t lit_end = s1 + len;
+        const bool err_t = s >= sn || lit_end > sn || len > bmax - dl;
+        // the offset (2 bytes), 0 < offset <= output so far, the length, and a token after it
+        const uint32_t off = w.x & 0xffff, ml = len + 4;
+        const bool err_m = s + 2 > sn || s1 >= sn || off == 0 || off > dl || ml > bmax - dl;
+        const bool err = tokp ? err_t : err_m;
+        const bool good = can && !to_list && !err;
+        fb = fb || (can && to_list);
+        const bool last = tokp && lit_end == sn;
+        // an error leaves the bytes of the blocks before this one: none
+        dl = (can && !to_list && err) ? 0u : (good ? dl + (tokp ? len : ml) : dl);
+        ph = (can && (to_list || err)) ? 2u : ((good && last) ? 1u : ph);
+        s = good ? (tokp ? lit_end : s1) : s;
+        mtok = (good && tokp) ? (w.x & 15) : mtok;
+        lph = good ? (tokp ? 1u : 0u) : lph;
+      }
+      // the word after the block: a second data block goes to the serial plan
+      const bool tail_in = act && ph == 1 && avail >= int32_t(min(tail + 4, clen));
+      if (tail_in) {
+        const uint32_t next = tail + 4 <= clen ? ring_rd8(in, sh + tail, kIR - 8).x : 0u;
+        fb = fb || next != 0;
+        ph = 2;
+      }
+    }
+    fb = fb || (have && ph < 2);  // (budget: never reached)
+    if (b < rend && !fb) {
+      out_sz[b] = align16(dl);
+      row_sz[b] = row_capacity(dl);
+    }
+    lpb_list_append(b < rend && fb, b, list, count);
+  }
+}
+
 template <bool kLz4>
 hipError_t launch_lpb(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
   const size_t lds = lpb2_lds_bytes();
@@ -1090,6 +1229,19 @@ hipError_t launch_lpb(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, 
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus) {
   if (a.n == 0) return hipGetLastError();
   return launch_lpb<false>(st, a, ZsFastArgs{}, num_cus);
+}
+
+hipError_t launch_lz4_plan(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,
+                           uint64_t* row_sz, uint32_t* list, uint32_t* count) {
+  if (n == 0) {
+    (void)hipMemsetAsync(out_sz, 0, 8, st);
+    (void)hipMemsetAsync(row_sz, 0, 8, st);
+    return hipGetLastError();
+  }
+  const uint32_t grid = min((n + kLz4PlanThreads - 1) / kLz4PlanThreads, 8192u);
+  plan_lz4_lane_kernel<<<grid, kLz4PlanThreads, size_t(kLz4PlanThreads) * kInStride, st>>>(in, in_off, n, out_sz,
+                                                                                            row_sz, list, count);
+  return hipGetLastError();
 }
 
 hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {

@@ -91,6 +91,10 @@ hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
 // CodecLz4 blocks: the lane-per-block decoder for one-block frames, then their XXH32 content
 // checksums; every other shape and any failed check is appended to z.list for the exact path.
 hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
+// CodecLz4 plan sizes lane per block for frames of one data block (out_sz[n] = row_sz[n] = 0 too);
+// the rest appended to list (*count) for the serial plan.
+hipError_t launch_lz4_plan(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,
+                           uint64_t* row_sz, uint32_t* list, uint32_t* count);
 // CodecZstd fast path (zstd_fast.hip): plan sizes of single-frame blocks (the rest appended to
 // list for the wave plan); decode phases A-C (blocks for the exact path appended to z.list).
 hipError_t launch_zstd_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,

@@ -140,6 +140,22 @@ def test_lz4_fast_path_shapes(ctx):
         blocks.append(_crc(lz4gen.frame(dec, rng=rng) + b"\x00\x01"))
         blocks.append(_crc(lz4gen.frame(dec, stored_p=1.0, rng=rng)))
         blocks.append(_crc(lz4gen.frame(dec, block_checksum=True, rng=rng)))
+    # structural damage under a valid CRC in one-block frames: the lane plan's and the lane
+    # decoder's checks (truncation, flipped bytes in tokens / offsets / lengths, trailing bytes)
+    for dec in plain[10:50]:
+        f = bytearray(lz4gen.frame(dec, content_checksum=rng.random() < 0.5, rng=rng))
+        kind = rng.randrange(4)
+        if kind == 0:
+            f = f[: rng.randrange(7, len(f))]
+        elif kind == 1:
+            i = rng.randrange(11, len(f) - 8)
+            f[i] ^= 1 << rng.randrange(8)
+        elif kind == 2:
+            i = rng.randrange(11, len(f) - 10)
+            f[i:i + 2] = bytes([rng.randrange(256), rng.randrange(256)])
+        else:
+            f[7:11] = struct.pack("<I", struct.unpack("<I", bytes(f[7:11]))[0] + rng.choice([-3, -1, 1, 2]))
+        blocks.append(_crc(bytes(f)))
     for mis in (0, 5, 13):
         meta = _compare(ctx, blocks, misalign=mis)
         st = [int(x) for x in meta["status"]]
