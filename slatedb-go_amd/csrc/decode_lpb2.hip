@@ -352,7 +352,7 @@ __device__ __forceinline__ void lpb_list_append(bool want, uint32_t item, uint32
 // offset after the literals starts a match.  The checks are the exact path's
 // (decode.hip wave_lz4_decode) for one independent block; a run of extension bytes
 // longer than the 8-byte window, or any failed check, hands the block to the exact path
-// (L.hb), which then decodes and reports it.  A zero-length literal run costs one step.
+// (L.hb), which then decodes and reports it.  A token without literals is parsed with its match.
 __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, int32_t avail, bool& hole_new,
                                           uint32_t& hole_src) {
   const bool need = act && !L.dd && L.rem == 0;
@@ -360,18 +360,25 @@ __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, 
   const bool room_out = L.d - 16 * L.fl <= kUnflushed;
   const bool can = need & (L.lph < 2) & (avail >= int32_t(min(L.s + 8, L.clen))) & room_out;
   const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
-  const bool tokp = L.lph == 0;
-  const uint32_t n4 = tokp ? (w.x >> 4) & 15 : L.mtok;  // the length nibble
-  // extension bytes: 7 after a token, 6 after an offset; k = how many 255s lead them
   const uint64_t w64 = (uint64_t(w.y) << 32) | w.x;
-  const uint64_t ext = tokp ? w64 >> 8 : w64 >> 16;
-  const uint64_t nz = ~ext & (tokp ? 0x00FFFFFFFFFFFFFFull : 0x0000FFFFFFFFFFFFull);
+  const uint32_t tok = w.x & 0xff;
+  const bool tokp = L.lph == 0;
+  // a token without literals (half of V-half's sequences) is parsed together with its match, so
+  // it costs no step of its own; unless it ends the block
+  const bool z0 = tokp && (tok >> 4) == 0 && L.s + 1 < L.sn;
+  const bool mph = !tokp || z0;           // this step starts a match
+  const uint64_t wm = z0 ? w64 >> 8 : w64;  // the window from the match's offset
+  const uint32_t n4 = mph ? (tokp ? tok & 15 : L.mtok) : tok >> 4;  // the length nibble
+  // extension bytes: 7 after a token, 6 after an offset (5 after a literal-less token's offset);
+  // k = how many 255s lead them
+  const uint64_t ext = mph ? wm >> 16 : w64 >> 8;
+  const uint64_t nz = ~ext & (mph ? (z0 ? 0x000000FFFFFFFFFFull : 0x0000FFFFFFFFFFFFull) : 0x00FFFFFFFFFFFFFFull);
   const uint32_t k = uint32_t(__builtin_ctzll(nz | (uint64_t(1) << 63))) >> 3;
   const uint32_t e = uint32_t(ext >> (8 * k)) & 0xff;
   const bool lng = n4 == 15;
   const uint32_t len = lng ? 15 + 255 * k + e : n4;
-  const uint32_t hl = (tokp ? 1u : 2u) + (lng ? k + 1 : 0u);
-  const uint32_t s1 = L.s + hl;
+  const uint32_t ms = L.s + (z0 ? 1u : 0u);  // where the match's offset starts
+  const uint32_t s1 = (mph ? ms + 2 : L.s + 1) + (lng ? k + 1 : 0u);
   const bool ext_bad = lng && nz == 0;  // the run goes on past the window
   const uint32_t room = L.dn - L.d;  // min(plan capacity, block maximum) left; the exact decoder's bounds
   // token: literals [s1, s1 + len); the last sequence's literals end the block exactly
@@ -379,23 +386,23 @@ __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, 
   const bool bad_tok = lit_end > L.sn || len > room;
   const bool last = lit_end == L.sn;
   // match: offset, then the length (+4); a match may not end the block (a token must follow)
-  const uint32_t off = w.x & 0xffff, ml = len + 4;
-  const bool bad_m = L.s + 2 > L.sn || s1 >= L.sn || off == 0 || off > L.d || ml > room;
-  const bool bad = ext_bad || (tokp ? bad_tok : bad_m);
+  const uint32_t off = uint32_t(wm) & 0xffff, ml = len + 4;
+  const bool bad_m = ms + 2 > L.sn || s1 >= L.sn || off == 0 || off > L.d || ml > room;
+  const bool bad = ext_bad || (mph ? bad_m : bad_tok);
   const bool ok = can && !bad;
   L.hb |= (can && bad) ? 1u : 0u;
   L.dd |= (fin || (can && bad)) ? 1u : 0u;
-  L.lit = ok ? uint32_t(tokp) : L.lit;
-  L.rem = ok ? (tokp ? len : ml) : L.rem;
-  L.src = ok ? (tokp ? s1 : L.d - off) : L.src;
-  L.eff = ok ? (tokp ? 16u : off) : L.eff;
-  const bool far = !tokp && off > kReach;
+  L.lit = ok ? uint32_t(!mph) : L.lit;
+  L.rem = ok ? (mph ? ml : len) : L.rem;
+  L.src = ok ? (mph ? L.d - off : s1) : L.src;
+  L.eff = ok ? (mph ? off : 16u) : L.eff;
+  const bool far = mph && off > kReach;
   L.far = ok ? uint32_t(far) : L.far;
-  L.s = ok ? (tokp ? lit_end : s1) : L.s;
-  L.mtok = (ok && tokp) ? (w.x & 15) : L.mtok;
-  L.lph = ok ? (tokp ? (last ? 2u : 1u) : 0u) : L.lph;
+  L.s = ok ? (mph ? s1 : lit_end) : L.s;
+  L.mtok = (ok && !mph) ? (tok & 15) : L.mtok;
+  L.lph = ok ? (mph ? 0u : (last ? 2u : 1u)) : L.lph;
   // the decoded length is known once the last literals are parsed
-  const bool fix = ok && tokp && last;
+  const bool fix = ok && !mph && last;
   L.dn = fix ? L.d + len : L.dn;
   L.rneed = fix ? min(L.rneed, L.d + len) : L.rneed;
   hole_new = ok && far && ml <= 16 && !L.hpend && !L.fpend;
