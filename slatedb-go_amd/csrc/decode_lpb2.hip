@@ -150,6 +150,8 @@ struct Lane {
   // lph = what the next parse reads (0 a token, 1 a match, 2 nothing: the last literals are
   // out); mtok = the token's match nibble; hb = hand the block to the exact path
   uint32_t sn, lph, mtok, hb;
+  // CodecLz4 content checksum: XXH32's four stripe accumulators over output chunks [0, xp)
+  uint32_t xp, x0, x1, x2, x3;
 };
 
 struct Rsrc {
@@ -344,6 +346,16 @@ __device__ __forceinline__ void lpb_list_append(bool want, uint32_t item, uint32
   if (lane == uint32_t(__builtin_ctzll(m))) base = atomicAdd(count, uint32_t(__builtin_popcountll(m)));
   base = __shfl(base, __builtin_ctzll(m), 64);
   if (want) list[base + uint32_t(__builtin_popcountll(m & ((uint64_t(1) << lane) - 1)))] = item;
+}
+
+// CodecLz4 content checksum: one XXH32 stripe (output chunk xp, still in the ring) when go.
+__device__ __forceinline__ void xxh_absorb(Lane& L, const uint8_t* ring, bool go) {
+  const v4u v = rd128(ring + ((L.xp * 16) & (kOR - 1)), L.z);
+  L.x0 = go ? xrotl(L.x0 + v.x * kXP2, 13) * kXP1 : L.x0;
+  L.x1 = go ? xrotl(L.x1 + v.y * kXP2, 13) * kXP1 : L.x1;
+  L.x2 = go ? xrotl(L.x2 + v.z * kXP2, 13) * kXP1 : L.x2;
+  L.x3 = go ? xrotl(L.x3 + v.w * kXP2, 13) * kXP1 : L.x3;
+  L.xp += go ? 1u : 0u;
 }
 
 // CodecLz4: the next sequence half of the frame's data block (LZ4 block format: token,
@@ -674,6 +686,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     L.fk = -1;
     L.pl0 = 0xFFFFFFFFu;
     L.sn = L.lph = L.mtok = L.hb = 0;
+    L.xp = 0;
+    L.x0 = kXP1 + kXP2;
+    L.x1 = kXP2;
+    L.x2 = 0;
+    L.x3 = 0u - kXP1;
     uint32_t want_size = 0xFFFFFFFFu;  // CodecLz4: the frame's content size (0xFFFFFFFF: none)
     if (have) {
       const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
@@ -792,6 +809,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg_bits(a) & 32768) ? kOOB : L.qoff, 0, 16);
       L.qoff = kOOB;
       flush_iteration(L, act, outs, lane, R, dbg_bits(a));
+      if constexpr (kLz4) {
+        // the content checksum's stripes: the chunks just completed (at most four), still in the ring
+#pragma unroll
+        for (int j = 0; j < 4; j++) xxh_absorb(L, ring, L.xp < L.fl);
+      }
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
     }
@@ -808,8 +830,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     slate_row* grows = reinterpret_cast<slate_row*>(reinterpret_cast<uint8_t*>(rows_base) + L.rows_rel);
     // rows stage: 0 = no rows to produce, 1 = walked rows to verify, 2 = re-derive from HBM
     uint32_t rows_stage = 0, nr = 0, osi_u = 0;
-    bool hand_back = false;            // CodecLz4: the exact path decodes this block
-    uint32_t rec_info = 0, rec_want = 0;  // CodecLz4: what the content-checksum pass checks
+    bool hand_back = false;  // CodecLz4: the exact path decodes this block
     if (have) {
       const uint32_t stored = __builtin_bswap32(ring_rd8(in, L.sh + L.clen, kIR - 8).x);
       // the register absorbed t zero bytes after the payload: compare against stored * x^(8t)
@@ -822,8 +843,19 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         dec_ok = !L.hb && L.lph == 2 && L.rem == 0 && L.s == L.sn && L.d == L.dn && endmark == 0 &&
                  (want_size == 0xFFFFFFFFu || want_size == L.d);
         hand_back = crc_ok && !dec_ok;
-        rec_want = ring_rd8(in, L.sh + L.sn + 4, kIR - 8).x;
-        rec_info = (crc_ok && dec_ok && L.clen - L.sn == 8) ? (kZfFast | kZfSum) << 16 : 0u;
+        if (crc_ok && dec_ok && L.clen - L.sn == 8) {
+          // FLG bit 2: XXH32 of the decoded block, the rest of its stripes and its tail from the ring
+          const uint32_t dn = L.dn;
+          while (L.xp < dn / 16) xxh_absorb(L, ring, true);
+          uint32_t h = dn >= 16 ? xrotl(L.x0, 1) + xrotl(L.x1, 7) + xrotl(L.x2, 12) + xrotl(L.x3, 18) : kXP5;
+          h += dn;
+          const v4u tv = rd128(ring + ((dn & ~15u) & (kOR - 1)), L.z);
+          const uint32_t tb = dn & 15, tw[4] = {tv.x, tv.y, tv.z, tv.w};
+          for (uint32_t i = 0; 4 * (i + 1) <= tb; i++) h = lz4_xxh_word(h, tw[i]);
+          for (uint32_t i = tb & ~3u; i < tb; i++) h = lz4_xxh_byte(h, (tw[i >> 2] >> (8 * (i & 3))) & 0xff);
+          hand_back = lz4_xxh_avalanche(h) != ring_rd8(in, L.sh + L.sn + 4, kIR - 8).x;
+          dec_ok = !hand_back;  // a mismatch: the exact path reports it
+        }
       } else {
         dec_ok = !L.err && L.d == L.dn && L.s == L.clen && L.rem == 0;
       }
@@ -914,15 +946,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       }
     }
     if constexpr (kLz4) {
-      if (b < rend) {
-        ZsFastRec rc{};
-        rc.info = rec_info;
-        rc.produced = L.d;
-        rc.want = rec_want;
-        z.rec[b] = rc;
-      }
       lpb_list_append(hand_back, b, z.list, z.count);
-      if (hand_back) have = false;
+      if (hand_back) {
+        have = false;
+        rows_stage = 0;
+      }
     }
     // ---- wave-cooperative check of the walked row starts against offsets[] (block.go:107-118):
     // per block, coalesced loads of its offsets and row descriptors; eight blocks per wait
@@ -1001,83 +1029,6 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
 size_t lpb2_lds_bytes() {
   return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
-}
-
-// CodecLz4 content checksum of the fast path's blocks (FLG bit 2), lane per block: XXH32 (seed
-// 0) of the decoded block, its four stripe accumulators' chains advanced for 64 blocks per wave
-// instruction.  Each iteration brings the next 64 bytes of every block with transposed loads
-// (in load j, lanes 4i..4i+3 read one 64-byte run of block 16j+i) issued one iteration ahead;
-// the loading lanes put them into the owner's LDS slot.  A mismatch goes to the exact path.
-constexpr uint32_t kLz4SumThreads = 256;
-__global__ __launch_bounds__(kLz4SumThreads) void lz4_fast_sum_kernel(DecodeArgs a, ZsFastArgs z) {
-  __shared__ __attribute__((aligned(16))) uint8_t slots[kLz4SumThreads * 64];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave_lane0 = threadIdx.x - lane;
-  uint8_t* slots0 = slots + wave_lane0 * 64;
-  const uint8_t* mine = slots0 + lane * 64;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
-    const uint32_t b = r0 + lane;
-    const uint32_t rend = min(r0 + 64, a.n);
-    const __amdgpu_buffer_rsrc_t R = make_rsrc(a.out + a.out_off[r0], a.out_off[rend] - a.out_off[r0]);
-    uint32_t orel = 0, len = 0, want = 0;
-    bool act = false;
-    if (b < a.n) {
-      const ZsFastRec rec = z.rec[b];
-      act = ((rec.info >> 16) & kZfSum) != 0;
-      len = act ? rec.produced : 0u;
-      want = rec.want;
-      orel = uint32_t(a.out_off[b] - a.out_off[r0]);
-    }
-    const uint32_t groups = (len + 63) / 64, stripes = len / 16;
-    uint32_t v0 = kXP1 + kXP2, v1 = kXP2, v2 = 0, v3 = 0u - kXP1;
-    v4u g[4];
-    auto load = [&](uint32_t t) {
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
-        const uint32_t g_o = __shfl(groups, int(o), 64), rel_o = __shfl(orel, int(o), 64);
-        g[j] = bload<0>(R, t < g_o ? rel_o + 64 * t + 16 * c : kOOB);
-      }
-    };
-    load(0);
-    for (uint32_t t = 0; __ballot(t < groups); t++) {
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) {
-        const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
-        if (t < uint32_t(__shfl(groups, int(o), 64))) *reinterpret_cast<v4u*>(slots0 + o * 64 + 16 * c) = g[j];
-      }
-      load(t + 1);  // in flight during this iteration
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (uint32_t h = 0; h < 4; h++) {
-        if (4 * t + h < stripes) {
-          const v4u w = *reinterpret_cast<const v4u*>(mine + 16 * h);
-          v0 = xrotl(v0 + w.x * kXP2, 13) * kXP1;
-          v1 = xrotl(v1 + w.y * kXP2, 13) * kXP1;
-          v2 = xrotl(v2 + w.z * kXP2, 13) * kXP1;
-          v3 = xrotl(v3 + w.w * kXP2, 13) * kXP1;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    bool bad = false;
-    if (act) {
-      uint32_t h = len >= 16 ? xrotl(v0, 1) + xrotl(v1, 7) + xrotl(v2, 12) + xrotl(v3, 18) : kXP5;
-      h += len;
-      // the tail (< 16 bytes) lies in the last group, still in this lane's slot
-      const uint8_t* tail = mine - 64 * ((len - 1) / 64);  // tail[i] = decoded byte i (len > 0)
-      uint32_t i = len & ~15u;
-      for (; i + 4 <= len; i += 4) h = lz4_xxh_word(h, *reinterpret_cast<const uint32_t*>(tail + i));
-      for (; i < len; i++) h = lz4_xxh_byte(h, tail[i]);
-      bad = lz4_xxh_avalanche(h) != want;
-    }
-    lpb_list_append(bad, b, z.list, z.count);
-  }
 }
 
 // CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order
@@ -1175,32 +1126,39 @@ __global__ __launch_bounds__(kLz4PlanThreads) void plan_lz4_lane_kernel(const ui
       for (uint32_t k = 0; k < kLz4PlanSteps; k++) {
         const bool can = act && ph == 0 && avail >= int32_t(min(s + 8, clen));
         const v2u w = ring_rd8(in, sh + s, kIR - 8);
-        const bool tokp = lph == 0;
-        const uint32_t n4 = tokp ? (w.x >> 4) & 15 : mtok;
         const uint64_t w64 = (uint64_t(w.y) << 32) | w.x;
-        const uint64_t ext = tokp ? w64 >> 8 : w64 >> 16;
-        const uint64_t nz = ~ext & (tokp ? 0x00FFFFFFFFFFFFFFull : 0x0000FFFFFFFFFFFFull);
+        const uint32_t tok = w.x & 0xff;
+        const bool tokp = lph == 0;
+        // a token without literals is walked together with its match (as lz4_parse)
+        const bool z0 = tokp && (tok >> 4) == 0 && s + 1 < sn;
+        const bool mph = !tokp || z0;
+        const uint64_t wm = z0 ? w64 >> 8 : w64;
+        const uint32_t n4 = mph ? (tokp ? tok & 15 : mtok) : tok >> 4;
+        const uint64_t ext = mph ? wm >> 16 : w64 >> 8;
+        const uint64_t nz =
+            ~ext & (mph ? (z0 ? 0x000000FFFFFFFFFFull : 0x0000FFFFFFFFFFFFull) : 0x00FFFFFFFFFFFFFFull);
         const uint32_t kk = uint32_t(__builtin_ctzll(nz | (uint64_t(1) << 63))) >> 3;
         const bool lng = n4 == 15;
         const uint32_t len = lng ? 15 + 255 * kk + (uint32_t(ext >> (8 * kk)) & 0xff) : n4;
-        const uint32_t s1 = s + (tokp ? 1u : 2u) + (lng ? kk + 1 : 0u);
+        const uint32_t ms = s + (z0 ? 1u : 0u);
+        const uint32_t s1 = (mph ? ms + 2 : s + 1) + (lng ? kk + 1 : 0u);
         const bool to_list = lng && nz == 0;  // the run goes on past the window
         // lz4_frame_len: the token at s < sz, its literals inside the block and the block maximum
         const uint32_t lit_end = s1 + len;
         const bool err_t = s >= sn || lit_end > sn || len > bmax - dl;
         // the offset (2 bytes), 0 < offset <= output so far, the length, and a token after it
-        const uint32_t off = w.x & 0xffff, ml = len + 4;
-        const bool err_m = s + 2 > sn || s1 >= sn || off == 0 || off > dl || ml > bmax - dl;
-        const bool err = tokp ? err_t : err_m;
+        const uint32_t off = uint32_t(wm) & 0xffff, ml = len + 4;
+        const bool err_m = ms + 2 > sn || s1 >= sn || off == 0 || off > dl || ml > bmax - dl;
+        const bool err = mph ? err_m : err_t;
         const bool good = can && !to_list && !err;
         fb = fb || (can && to_list);
-        const bool last = tokp && lit_end == sn;
+        const bool last = !mph && lit_end == sn;
         // an error leaves the bytes of the blocks before this one: none
-        dl = (can && !to_list && err) ? 0u : (good ? dl + (tokp ? len : ml) : dl);
+        dl = (can && !to_list && err) ? 0u : (good ? dl + (mph ? ml : len) : dl);
         ph = (can && (to_list || err)) ? 2u : ((good && last) ? 1u : ph);
-        s = good ? (tokp ? lit_end : s1) : s;
-        mtok = (good && tokp) ? (w.x & 15) : mtok;
-        lph = good ? (tokp ? 1u : 0u) : lph;
+        s = good ? (mph ? s1 : lit_end) : s;
+        mtok = (good && !mph) ? (tok & 15) : mtok;
+        lph = good ? (mph ? 0u : 1u) : lph;
       }
       // the word after the block: a second data block goes to the serial plan
       const bool tail_in = act && ph == 1 && avail >= int32_t(min(tail + 4, clen));
@@ -1253,11 +1211,7 @@ hipError_t launch_lz4_plan(hipStream_t st, const uint8_t* in, const uint64_t* in
 
 hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
   if (a.n == 0) return hipGetLastError();
-  hipError_t e = launch_lpb<true>(st, a, z, num_cus);
-  if (e != hipSuccess) return e;
-  const uint32_t grid = min((a.n + kLz4SumThreads - 1) / kLz4SumThreads, uint32_t(num_cus) * 4u);
-  lz4_fast_sum_kernel<<<grid, kLz4SumThreads, 0, st>>>(a, z);
-  return hipGetLastError();
+  return launch_lpb<true>(st, a, z, num_cus);
 }
 
 }  // namespace slate

@@ -88,8 +88,8 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
-// CodecLz4 blocks: the lane-per-block decoder for one-block frames, then their XXH32 content
-// checksums; every other shape and any failed check is appended to z.list for the exact path.
+// CodecLz4 blocks: the lane-per-block decoder for one-block frames (XXH32 content checksum in its
+// loop); every other shape and any failed check is appended to z.list for the exact path.
 hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
 // CodecLz4 plan sizes lane per block for frames of one data block (out_sz[n] = row_sz[n] = 0 too);
 // the rest appended to list (*count) for the serial plan.
