@@ -73,6 +73,14 @@ constexpr uint32_t kInStride = kIR + 8;
 #define SLATE_VERIFY_BATCH 4
 #endif
 constexpr uint32_t kVerifyBatch = SLATE_VERIFY_BATCH;
+// cache policy of the flush and row-descriptor stores (lpb_common.h bstore: sc1 = 16)
+#ifndef SLATE_OUT_CPOL
+#define SLATE_OUT_CPOL 16
+#endif
+#ifndef SLATE_ROW_CPOL
+#define SLATE_ROW_CPOL 16
+#endif
+constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
 #endif
@@ -540,7 +548,8 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
       const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
       // stored right away: the loads waited on later were issued before it (refill) or are
       // waited on an iteration later (far source), so its acknowledgement is off the path
-      bstore(R.rows, (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB, row);
+      __builtin_amdgcn_raw_buffer_store_b128(row, R.rows, (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB,
+                                             0, kRowCpol);
     }
   }
 }
@@ -564,7 +573,8 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
     const uint32_t base_o = __shfl(base, int(o), 64);
     const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
     const v4u v = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)), L.z);
-    bstore(R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, v);
+    __builtin_amdgcn_raw_buffer_store_b128(v, R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, 0,
+                                           kOutCpol);
   }
   L.fl += min(done, 4u);
 }
