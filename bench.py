@@ -104,8 +104,6 @@ def main():
     from tools import workload as wl
 
     codec = {"snappy": sc.SNAPPY, "none": sc.NONE, "lz4": sc.LZ4, "zstd": sc.ZSTD}[args.codec]
-    if codec == sc.LZ4:
-        raise SystemExit("bench.py: LZ4 frames are timed by tools/ablate.py (liblz4), not the block set")
     half = args.values == "half"
     threads = max(1, min(16, host_cpus()))
     t0 = time.time()
@@ -230,7 +228,7 @@ def main():
     traffic, traffic_src = pmc_traffic(args.pmc_json, n, args.codec)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": {"snappy": "decode_lpb2_kernel",
+                "kernel": {"snappy": "decode_lpb2_kernel", "lz4": "decode_lpb2_kernel<true> (+ decode_list_kernel<0>)",
                            "zstd": "zstd decode: zs_fast_parse/crc/build/sum + decode_list_kernel<2> "
                                    "(HIP events around the whole decode)"}.get(args.codec, "decode_fast_kernel<0>"),
                 "kernel_ms": round(kern_ms, 4),
@@ -255,7 +253,8 @@ def main():
             workload = (f"configs[3]: one set of {set_blocks} x 4 KiB Snappy blocks (64 GiB encoded), block i on GPU "
                         f"i mod {world}; this rank decodes {n} of its {sc.shard_blocks(set_blocks, world, rank)}")
         data = ("synthetic (SURVEY 8d keys k%015d, " + ("V-half" if half else "V-rand") + " values, " +
-                {"snappy": "libsnappy-encoded", "none": "CodecNone"}.get(args.codec, args.codec) +
+                {"snappy": "libsnappy-encoded", "none": "CodecNone",
+                 "lz4": "liblz4 frames as pierrec/lz4's writer defaults"}.get(args.codec, args.codec) +
                 ", every block generated on its own: tools/benchgen.c bg_build_set)")
     result = {"metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -267,6 +266,12 @@ def main():
               "roofline": roofline,
               "verified": {"blocks": verified, "mode": verify if shard is not None else "status only",
                            "what": "every block's status; decoded bytes, meta and row descriptors vs the generator"}}
+
+    if rank == 0 and world == 1:
+        # the kernel's rate against a device-to-device copy measured on this box too
+        copy = measured_copy_gbps(device)
+        roofline["measured_copy_GBps"] = round(copy, 1)
+        roofline["frac_of_measured_copy"] = round(achieved / copy, 4)
 
     if rank == 0 and world == 1 and not args.no_host_io and shard is not None:
         result["host_io"] = host_io_rate(sc, ctx, codec, blob, in_off)
@@ -280,6 +285,25 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def measured_copy_gbps(device, nbytes: int = 2 << 30, reps: int = 10) -> float:
+    """Read + write bytes per second of a large device-to-device copy (torch copy_, the same
+    stream as the decode), outside the timed region."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        b.copy_(a)
+    ev[1].record()
+    ev[1].synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def pmc_traffic(path: str, n: int, codec: str):

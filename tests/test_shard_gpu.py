@@ -108,3 +108,27 @@ def test_single_block_decode_matches_oracle():
         if st == 0:
             assert data == odata[:int(om["data_len"])]
             assert offs == [int(r["row_off"]) for r in orows][:len(offs)]
+
+
+@pytest.mark.parametrize("codec", ["lz4", "zstd", "none"])
+def test_sharded_decode_other_codecs(codec):
+    """slate_block_decode_sharded for codecs the host cannot plan (LZ4 / Zstd: a plan-only GPU
+    pass per context over its gathered shard) and for CodecNone, against the oracle."""
+    import slatecodec as sc
+    c = {"lz4": sc.LZ4, "zstd": sc.ZSTD, "none": sc.NONE}[codec]
+    rng = random.Random(17)
+    kvs = bg.kv_synthetic(38 * 300, half=True, tomb_every=11)
+    plain = [b[:-4] for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+    dec = np.frombuffer(b"".join(plain), np.uint8)
+    doff = np.cumsum([0] + [len(b) for b in plain]).astype(np.uint64)
+    eblob, eoff = wl.encode_blocks(c, dec, doff, threads=4)  # liblz4 / libzstd frames + CRC
+    blocks = [bytes(eblob[int(eoff[i]):int(eoff[i + 1])]) for i in range(len(plain))]
+    blocks += [bg.mutate(rng, blocks[rng.randrange(len(blocks))], fix_crc=rng.random() < 0.5) for _ in range(20)]
+    blocks += [b"", bg.recrc(b"\x00\x01")]
+    rng.shuffle(blocks)
+    blob, off = bg.pack(blocks, misalign=3)
+    ctxs = [sc.Context(0) for _ in range(3)]
+    got = sc.decode_sharded(ctxs, c, blob, off)
+    _check_against_oracle(c, blob, off, got)
+    for x in ctxs:
+        x.close()

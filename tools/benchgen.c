@@ -336,6 +336,15 @@ static void* set_build_work(void* arg) {
     uint8_t* d = j->enc + k * j->enc_stride;
     size_t cl = j->enc_stride - 4;
     if (j->codec == 0) { memcpy(d, blk, n); cl = n; }
+    else if (j->codec == 3) {  /* pierrec/lz4 v4 writer defaults: 4 MiB blocks, content checksum */
+      lz4f_prefs p;
+      memset(&p, 0, sizeof p);
+      p.blockSizeID = 7;
+      p.contentChecksumFlag = 1;
+      size_t r = g_lz4f(d, j->enc_stride - 4, blk, n, &p);
+      if (g_lz4f_err(r)) { j->rc = -4; break; }
+      cl = r;
+    }
     else if (j->codec == 4) {
       size_t r = g_zc2(zc, d, j->enc_stride - 4, blk, n);
       if (g_zerr(r)) { j->rc = -5; break; }
@@ -350,7 +359,7 @@ static void* set_build_work(void* arg) {
 }
 
 /* Encoded blocks k = 0..count-1 of the set (global index i_begin + k * stride) into fixed slots
- * of enc_stride bytes (codec 0 None, 1 Snappy via libsnappy, 4 Zstd), lengths in enc_len. */
+ * of enc_stride bytes (codec 0 None, 1 Snappy via libsnappy, 3 LZ4 frames via liblz4, 4 Zstd), lengths in enc_len. */
 int bg_build_set(uint64_t seed, int half, uint64_t block_size, uint64_t i_begin, uint64_t stride, uint64_t count,
                  int codec, uint8_t* enc, uint64_t enc_stride, uint64_t* enc_len, int nthreads) {
   if (nthreads < 1) nthreads = 1;
