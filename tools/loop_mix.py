@@ -17,7 +17,7 @@ def mix(dbg):
                f"-DSLATE_FORCE_DBG={dbg}", SRC, "-o", os.path.join(d, "k.s")]
         subprocess.run(cmd, check=True, capture_output=True)
         text = open(os.path.join(d, "k.s")).read()
-    start = text.index("_ZN5slate18decode_lpb2_kernel")
+    start = text.index("_ZN5slate18decode_lpb2_kernelILb0E")
     lines = text[start:].split("\n")
     labels = {m.group(1): i for i, l in enumerate(lines) for m in [re.match(r"^(\.LBB\d+_\d+):", l)] if m}
     best = None
