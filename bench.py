@@ -93,10 +93,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal of the N-rank path on a one-GPU box only (every rank on cuda:0, gloo); the driver's
+    # multi-GPU runs leave both unset: one rank per GPU over RCCL
+    if os.environ.get("SLATE_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("SLATE_BENCH_BACKEND", "nccl"))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
