@@ -85,6 +85,50 @@ int ctx_snappy_encode_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std
   return SLATE_OK;
 }
 
+// The same encoding assembled on the device: varint header and the chunks' encodings back to back
+// at ctx->e_k (device-to-device copies on the context's stream), then its CRC32 on the device, so
+// the encoded payload crosses the link once (into `out` after `out`'s current bytes), with its
+// BE32 CRC appended (bloom.Encode / encodeIndex framing).
+int ctx_snappy_encode_crc_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std::vector<uint8_t>& out) {
+  SLATE_HIP(ctx_bind(ctx));
+  const uint64_t nch = (uint64_t(n) + kSnapMaxChunk - 1) / kSnapMaxChunk;
+  SLATE_HIP(ctx->e_h.ensure(nch * kSnapChunkSlot + nch * 4 + 64));
+  uint8_t* slots = ctx->e_h.as<uint8_t>();
+  uint32_t* lens = reinterpret_cast<uint32_t*>(slots + nch * kSnapChunkSlot);
+  SLATE_HIP(launch_snappy_chunks(ctx->stream, d_src, n, slots, lens, ctx->num_cus));
+  std::vector<uint32_t> hl(nch);
+  if (nch) SLATE_HIP(hipMemcpyAsync(hl.data(), lens, nch * 4, hipMemcpyDeviceToHost, ctx->stream));
+  SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  uint8_t hdr[10];
+  size_t hn = 0;
+  for (uint64_t v = n; ; v >>= 7) {
+    hdr[hn++] = uint8_t(v & 0x7f) | (v >= 0x80 ? 0x80 : 0);
+    if (v < 0x80) break;
+  }
+  size_t total = hn;
+  for (uint64_t c = 0; c < nch; c++) total += hl[c];
+  SLATE_HIP(ctx->e_k.ensure(total + 64));
+  uint8_t* d = ctx->e_k.as<uint8_t>();
+  SLATE_HIP(hipMemcpyAsync(d, hdr, hn, hipMemcpyHostToDevice, ctx->stream));
+  size_t o = hn;
+  for (uint64_t c = 0; c < nch; c++) {
+    if (hl[c]) SLATE_HIP(hipMemcpyAsync(d + o, slots + c * kSnapChunkSlot, hl[c], hipMemcpyDeviceToDevice, ctx->stream));
+    o += hl[c];
+  }
+  uint32_t crc = 0;
+  const int st = ctx_crc32_device(ctx, d, total, &crc);  // stream-synchronous
+  if (st) return st;
+  const size_t base = out.size();
+  out.resize(base + total + 4);
+  const int s2 = ctx_d2h(ctx, out.data() + base, d, total, ctx->stream);
+  if (s2) return s2;
+  out[base + total] = uint8_t(crc >> 24);
+  out[base + total + 1] = uint8_t(crc >> 16);
+  out[base + total + 2] = uint8_t(crc >> 8);
+  out[base + total + 3] = uint8_t(crc);
+  return SLATE_OK;
+}
+
 int ctx_snappy_encode_host(slate_ctx* ctx, const uint8_t* data, size_t n, std::vector<uint8_t>& out) {
   SLATE_HIP(ctx_bind(ctx));
   SLATE_HIP(ctx->e_i.ensure(n + 16));
@@ -894,12 +938,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
     uint32_t crc = 0;
     const size_t f0 = buf.size();
     if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
-      std::vector<uint8_t> comp;
-      st = ctx_snappy_encode_device(ctx, enc, nb + 2, comp);
+      st = ctx_snappy_encode_crc_device(ctx, enc, nb + 2, buf);  // payload || BE32 CRC
       if (st) { delete t; return st; }
-      st = ctx_crc32_host_buffer(ctx, comp.data(), comp.size(), &crc);
-      if (st) { delete t; return st; }
-      buf.insert(buf.end(), comp.begin(), comp.end());
+      crc = ld_be32(buf.data() + buf.size() - 4);
+      buf.resize(buf.size() - 4);  // appended again below
     } else if (b->cfg.codec != SLATE_CODEC_NONE) {
       const uint64_t start = 0, len = nb + 2;
       std::vector<uint64_t> fo;
@@ -928,13 +970,22 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   std::vector<uint8_t> index;
   {
     std::vector<uint8_t> fb = fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
-    st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
-    if (st) { delete t; return st; }
+    if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
+      // encoded and CRC'd on the device: the payload comes back once, with its CRC
+      SLATE_HIP(ctx_bind(ctx));
+      SLATE_HIP(ctx->e_i.ensure(fb.size() + 16));
+      st = ctx_h2d(ctx, ctx->e_i.p, fb.data(), fb.size(), ctx->stream);
+      if (!st) st = ctx_snappy_encode_crc_device(ctx, ctx->e_i.as<uint8_t>(), fb.size(), index);
+      if (st) { delete t; return st; }
+    } else {
+      st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
+      if (st) { delete t; return st; }
+      uint32_t icrc = 0;
+      st = ctx_crc32_host_buffer(ctx, index.data(), index.size(), &icrc);
+      if (st) { delete t; return st; }
+      put_be32(index, icrc);
+    }
   }
-  uint32_t icrc = 0;
-  st = ctx_crc32_host_buffer(ctx, index.data(), index.size(), &icrc);
-  if (st) { delete t; return st; }
-  put_be32(index, icrc);
   const uint64_t index_off = b->current_len + buf.size();
   buf.insert(buf.end(), index.begin(), index.end());
   const uint64_t meta_off = b->current_len + buf.size();

@@ -143,7 +143,7 @@ struct slate_ctx {
   // decode batch buffers
   DevBuf d_in, d_in_off, d_out, d_out_off, d_meta, d_rows, d_row_base, d_scratch;
   // encode / misc buffers
-  DevBuf e_a, e_b, e_c, e_d, e_e, e_f, e_g, e_h, e_i, e_j;
+  DevBuf e_a, e_b, e_c, e_d, e_e, e_f, e_g, e_h, e_i, e_j, e_k;
   // Snappy encode: per-block slots, raw staging for oversized blocks, snappy LDS-free scratch
   DevBuf s_slots, s_raw, s_aux;
   // LZ4 / Zlib / Zstd encode (encode_codecs.hip): piece tables, tag and body slots, sequences, frames
@@ -152,7 +152,7 @@ struct slate_ctx {
   void release_all() {
     if (seg_pool) seg_pool->close();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
-                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &s_slots, &s_raw, &s_aux, &c_meta,
+                      &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &e_k, &s_slots, &s_raw, &s_aux, &c_meta,
                       &c_tags, &c_bodies, &c_seqs, &c_out, &c_in})
       b->release();
     for (PipeLane& l : lanes) l.release();
