@@ -232,12 +232,17 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
       const uint32_t prev_hash = snap_hash(lo, shift);
       const uint32_t x1 = (lo >> 8) | (hi << 24);
       const uint32_t curr_hash = snap_hash(x1, shift);
-      if (lane == 0) table[prev_hash] = uint16_t(s - 1);
+      // table[prevHash] = s-1; candidate = table[currHash]; table[currHash] = s (encode_other.go:
+      // 226-231) with one wave barrier instead of three: the read is taken before either write,
+      // and the write of prevHash is forwarded when the two slots coincide
+      const int32_t old = int32_t(table[curr_hash]);
       snap_sync();
-      cand = int32_t(table[curr_hash]);
-      snap_sync();
-      if (lane == 0) table[curr_hash] = uint16_t(s);
-      snap_sync();
+      cand = prev_hash == curr_hash ? s - 1 : old;
+      if (lane == 0) {
+        table[prev_hash] = uint16_t(s - 1);
+        table[curr_hash] = uint16_t(s);
+      }
+      // (the next table reads come after the probe batch's barrier, or after this one's)
       if (x1 != snap_ld32(src + cand)) {
         s++;
         break;
