@@ -348,9 +348,138 @@ int ctx_snappy_decode_buffer(slate_ctx* ctx, const uint8_t* buf, size_t len, std
 
 // Any codec: Snappy through the function above; LZ4 / Zlib / Zstd through the plan kernels
 // (decoded capacity) and one wave per payload reading and writing HBM (decode_payload_kernel).
+// payloads from this size on take the split paths (smaller ones: one wave, no set-up)
+constexpr size_t kSplitMin = 32 * 1024;
+
+// XXH32 (seed 0) of a few host bytes (the LZ4 frame descriptor's checksum byte).
+static uint32_t xxh32_small(const uint8_t* p, size_t n) {
+  constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u, P5 = 374761393u;
+  auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+  uint32_t h = P5 + uint32_t(n);  // n < 16
+  size_t i = 0;
+  for (; i + 4 <= n; i += 4) h = rotl(h + (uint32_t(p[i]) | uint32_t(p[i + 1]) << 8 | uint32_t(p[i + 2]) << 16 |
+                                           uint32_t(p[i + 3]) << 24) * P3, 17) * P4;
+  for (; i < n; i++) h = rotl(h + uint32_t(p[i]) * P5, 11) * P1;
+  h ^= h >> 15;
+  h *= P2;
+  h ^= h >> 13;
+  h *= P3;
+  h ^= h >> 16;
+  return h;
+}
+
+// A large CodecLz4 index / filter (`frame || BE32 CRC`) decoded block by block in parallel when
+// its frame has the shape this builder writes: independent data blocks (FLG bit 5), no block
+// checksums, no dictionary, every block decoding to at most 64 KiB.  The frame header and the
+// block list are read here (structure only, as the plan does); the CRC, the blocks and the
+// content checksum are computed on the GPU.  Returns 1 with *bstatus and `out` set, or 0 when
+// the serial path must decode the payload (another shape, or any check failing: that path then
+// reports it exactly); < 0 never (HIP errors are returned as their status).
+static int lz4_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
+                             int* bstatus, int* handled) {
+  *handled = 0;
+  const size_t clen = len - 4;
+  const uint8_t* f = buf;
+  auto le32 = [&](size_t i) {
+    return uint32_t(f[i]) | uint32_t(f[i + 1]) << 8 | uint32_t(f[i + 2]) << 16 | uint32_t(f[i + 3]) << 24;
+  };
+  if (clen < 7 || le32(0) != 0x184D2204u) return SLATE_OK;
+  const uint32_t flg = f[4], bd = f[5];
+  if ((flg >> 6) != 1 || (flg & 2) || (bd & 0x8F) || ((bd >> 4) & 7) < 4 || (flg & 1) || !(flg & 0x20) ||
+      (flg & 0x10))
+    return SLATE_OK;
+  const uint32_t bmax = 1u << (8 + 2 * ((bd >> 4) & 7));
+  const size_t hl = 2 + ((flg & 8) ? 8 : 0);
+  if (clen < 4 + hl + 1 || f[4 + hl] != ((xxh32_small(f + 4, hl) >> 8) & 0xFF)) return SLATE_OK;
+  uint64_t content = 0;
+  if (flg & 8)
+    for (int k = 7; k >= 0; k--) content = (content << 8) | f[6 + k];
+  std::vector<uint32_t> blk;
+  size_t pos = 4 + hl + 1;
+  for (;;) {
+    if (clen - pos < 4) return SLATE_OK;
+    const uint32_t bs = le32(pos);
+    if (bs == 0) {
+      pos += 4;
+      break;
+    }
+    const uint32_t sz = bs & 0x7FFFFFFFu;
+    if (sz > bmax || clen - pos - 4 < sz || pos + 4 > 0xFFFFFFFFull) return SLATE_OK;
+    blk.push_back(uint32_t(pos + 4));
+    blk.push_back(bs);
+    pos += 4 + sz;
+  }
+  uint32_t want = 0;
+  const bool ccheck = (flg & 4) != 0;
+  if (ccheck) {
+    if (clen - pos < 4) return SLATE_OK;
+    want = le32(pos);
+    pos += 4;
+  }
+  if (pos != clen) return SLATE_OK;
+  const uint32_t nblk = uint32_t(blk.size() / 2);
+  // ---- on the GPU: the payload's CRC, then the blocks, then the content checksum
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  int s = ctx_h2d(ctx, ctx->d_in.p, buf, len, st);
+  if (s) return s;
+  uint32_t crc = 0;
+  s = ctx_crc32_device(ctx, ctx->d_in.as<uint8_t>(), clen, &crc);
+  if (s) return s;
+  if (crc != ld_be32(buf + clen)) {
+    *bstatus = SLATE_E_BLOCK_CHECKSUM;  // block.Decode / bloom.Decode / DecodeIndex check it first
+    *handled = 1;
+    return SLATE_OK;
+  }
+  SLATE_HIP(ctx->d_scratch.ensure(size_t(nblk) * 12 + 64));
+  uint32_t* d_blk = ctx->d_scratch.as<uint32_t>();
+  uint32_t* d_sizes = d_blk + 2 * size_t(nblk);
+  SLATE_HIP(ctx->d_rows.ensure(size_t(nblk) * kLz4PayloadSlot + 64));  // the blocks' output slots
+  if (nblk) SLATE_HIP(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_lz4_payload_blocks(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, bmax, ctx->d_rows.as<uint8_t>(),
+                                      d_sizes, ctx->num_cus));
+  std::vector<uint32_t> sizes(nblk);
+  if (nblk) SLATE_HIP(hipMemcpyAsync(sizes.data(), d_sizes, size_t(nblk) * 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    if (sizes[k] == ~0u) return SLATE_OK;  // the serial path decodes (and reports) it
+    total += sizes[k];
+  }
+  if (total > 0xFFFFFF00ull || ((flg & 8) && content != total)) return SLATE_OK;
+  SLATE_HIP(ctx->d_out.ensure(total + 64));
+  uint8_t* d_out = ctx->d_out.as<uint8_t>();
+  uint64_t o = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    if (sizes[k])
+      SLATE_HIP(hipMemcpyAsync(d_out + o, ctx->d_rows.as<uint8_t>() + size_t(k) * kLz4PayloadSlot, sizes[k],
+                               hipMemcpyDeviceToDevice, st));
+    o += sizes[k];
+  }
+  if (ccheck) {
+    SLATE_HIP(launch_xxh32(st, d_out, uint32_t(total), d_sizes));
+    uint32_t got = 0;
+    SLATE_HIP(hipMemcpyAsync(&got, d_sizes, 4, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (got != want) return SLATE_OK;  // the serial path reports the frame checksum
+  }
+  out.resize(total);
+  s = ctx_d2h(ctx, out.data(), d_out, total, st);
+  if (s) return s;
+  *bstatus = SLATE_OK;
+  *handled = 1;
+  return SLATE_OK;
+}
+
 int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
                               int* bstatus) {
   if (codec == SLATE_CODEC_SNAPPY) return ctx_snappy_decode_buffer(ctx, buf, len, out, bstatus);
+  if (codec == SLATE_CODEC_LZ4 && len >= kSplitMin && len <= 0xFFFFFF00ull) {
+    int handled = 0;
+    const int s = lz4_payload_split(ctx, buf, len, out, bstatus, &handled);
+    if (s || handled) return s;
+  }
   if (codec != SLATE_CODEC_LZ4 && codec != SLATE_CODEC_ZLIB && codec != SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
   if (len < 4 || len > 0xFFFFFF00ull) return SLATE_E_INVALID_ARG;
   SLATE_HIP(ctx_bind(ctx));

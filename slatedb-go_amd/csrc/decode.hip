@@ -478,7 +478,11 @@ __device__ int wave_lz4_decode(const uint8_t* base, uint32_t off, uint32_t n, ui
   if (ccheck) {
     if (n - pos < 4) return SLATE_E_LZ4_CORRUPT;
     __builtin_amdgcn_wave_barrier();
+#ifdef SLATE_NO_CONTENT_XXH  // profiling variants only (tools/payload_probe.py): the check skipped
+    if (false)
+#else
     if (out && wave_xxh32(out, 0, d, lane) != __builtin_amdgcn_readfirstlane(ld_le32(in + pos)))
+#endif
       return SLATE_E_LZ4_FRAME_CHECKSUM;
     pos += 4;
   }
@@ -1112,6 +1116,172 @@ __global__ __launch_bounds__(64) void decode_payload_kernel(DecodeArgs a) {
   if (CK == 1) zlib_lds(w, smem + kTabBytes, 1, 0, lane);
   if (CK == 2) zstd_lds(w, smem + kTabBytes, 0, lane);
   for (uint32_t b = blockIdx.x; b < a.n; b += gridDim.x) decode_block_wave<CK, true>(a, b, w, lane, false);
+}
+
+// ------------------------------------------- CodecLz4 payloads split by data block
+// An index or filter written as an LZ4 frame of independent data blocks (this builder's frames:
+// one block per 64 KiB piece) decodes block by block in parallel: one wave per data block, the
+// compressed block and its output in LDS.  sizes[k] = the decoded bytes (the output at
+// slots + k * kLz4PaySlot), or ~0u when block k needs the serial path (an output above 64 KiB, or
+// any check of wave_lz4_decode's failing).  Frame header, block list, content size and checksum
+// are the host's and lz4_payload_xxh32_kernel's (api_sst.cpp lz4_payload_split).
+constexpr uint32_t kLz4PayIn = 65536 + 32, kLz4PayOut = 65536, kLz4PaySlot = 65536;
+__global__ __launch_bounds__(64) void lz4_payload_blocks_kernel(const uint8_t* __restrict__ in,
+                                                                const uint32_t* __restrict__ blk, uint32_t nblk,
+                                                                uint32_t bmax, uint8_t* __restrict__ slots,
+                                                                uint32_t* __restrict__ sizes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* lin = smem;
+  uint8_t* lout = smem + kLz4PayIn;
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t k = blockIdx.x; k < nblk; k += gridDim.x) {
+    const uint32_t pos = blk[2 * k], bs = blk[2 * k + 1];
+    const uint32_t sz = bs & 0x7FFFFFFFu;
+    const bool stored = (bs >> 31) != 0;
+    const uint8_t* g = in + pos;
+    const uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(g) & 15);
+    if (shift + sz + 16 > kLz4PayIn || (stored && sz > kLz4PayOut) || sz > bmax) {
+      if (lane == 0) sizes[k] = ~0u;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const uint4* src4 = reinterpret_cast<const uint4*>(g - shift);
+      uint4* dst4 = reinterpret_cast<uint4*>(lin);
+      const uint32_t chunks = (shift + sz + 15) / 16;
+      for (uint32_t c = lane; c < chunks; c += kWave) dst4[c] = src4[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* src = lin + shift;
+    uint32_t d = 0;
+    bool ok = true;
+    if (stored) {
+      for (uint32_t j = lane; j < sz; j += kWave) lout[j] = src[j];
+      d = sz;
+    } else {
+      // wave_lz4_decode's sequence loop for one independent block (lo = d0 = 0), cap = 64 KiB
+      uint32_t wbase = 0x80000000u, win = 0;
+      auto byte_at = [&](uint32_t p) -> uint32_t {
+        if (p - wbase >= uint32_t(kWave)) {
+          wbase = p;
+          win = (p + lane < sz) ? uint32_t(src[p + lane]) : 0u;
+        }
+        return __builtin_amdgcn_readlane(win, int(p - wbase));
+      };
+      const uint32_t cap = min(kLz4PayOut, bmax);
+      uint32_t s = 0;
+      for (;;) {
+        if (s >= sz) { ok = false; break; }
+        const uint32_t token = byte_at(s);
+        s++;
+        uint32_t ll = token >> 4;
+        if (ll == 15) {
+          uint32_t b;
+          do {
+            if (s >= sz) { ok = false; break; }
+            b = byte_at(s);
+            s++;
+            ll += b;
+          } while (b == 255);
+          if (!ok) break;
+        }
+        if (ll > sz - s || ll > cap - d) { ok = false; break; }
+        for (uint32_t j = lane; j < ll; j += kWave) lout[d + j] = src[s + j];
+        s += ll;
+        d += ll;
+        if (s == sz) break;  // the last sequence has literals only
+        if (sz - s < 2) { ok = false; break; }
+        const uint32_t mo = byte_at(s) | (byte_at(s + 1) << 8);
+        s += 2;
+        if (mo == 0 || mo > d) { ok = false; break; }
+        uint32_t ml = token & 15;
+        if (ml == 15) {
+          uint32_t b;
+          do {
+            if (s >= sz) { ok = false; break; }
+            b = byte_at(s);
+            s++;
+            ml += b;
+          } while (b == 255);
+          if (!ok) break;
+        }
+        ml += 4;
+        if (ml > cap - d) { ok = false; break; }
+        __builtin_amdgcn_wave_barrier();  // the literals / earlier matches are in LDS
+        if (mo >= ml) {
+          for (uint32_t j = lane; j < ml; j += kWave) lout[d + j] = lout[d - mo + j];
+        } else {
+          for (uint32_t j = lane; j < ml; j += kWave) lout[d + j] = lout[d - mo + (j % mo)];
+        }
+        __builtin_amdgcn_wave_barrier();
+        d += ml;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+      uint4* o4 = reinterpret_cast<uint4*>(slots + size_t(k) * kLz4PaySlot);
+      const uint4* l4 = reinterpret_cast<const uint4*>(lout);
+      for (uint32_t c = lane; c < (d + 15) / 16; c += kWave) o4[c] = l4[c];
+    }
+    if (lane == 0) sizes[k] = ok ? d : ~0u;
+  }
+}
+
+// XXH32 (seed 0) of a device buffer by one wave: 1 KiB of stripes per step staged in LDS
+// (loaded one step ahead), the four accumulators on lanes 0-3; *out = the hash.
+__global__ __launch_bounds__(64) void lz4_payload_xxh32_kernel(const uint8_t* __restrict__ p, uint32_t n,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 buf[2][64];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t stripes = n / 16, steps = (stripes + 63) / 64;
+  uint32_t v = lane == 0 ? kXP1 + kXP2 : (lane == 1 ? kXP2 : (lane == 2 ? 0u : 0u - kXP1));
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);  // (a 16-byte aligned device buffer)
+  uint4 nxt = (steps && lane < stripes) ? p4[lane] : make_uint4(0, 0, 0, 0);
+  for (uint32_t t = 0; t < steps; t++) {
+    buf[t & 1][lane] = nxt;
+    const uint32_t q = 64 * (t + 1) + lane;
+    nxt = q < stripes ? p4[q] : make_uint4(0, 0, 0, 0);  // in flight during this step
+    __builtin_amdgcn_s_waitcnt(0xc07f);                   // lgkmcnt(0): the LDS store landed
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane < 4) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(buf[t & 1]);
+      const uint32_t m = min(64u, stripes - 64 * t);
+      for (uint32_t i = 0; i < m; i++) v = xrotl(v + w[4 * i + lane] * kXP2, 13) * kXP1;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  uint32_t h = n >= 16 ? xrotl(__builtin_amdgcn_readlane(v, 0), 1) + xrotl(__builtin_amdgcn_readlane(v, 1), 7) +
+                             xrotl(__builtin_amdgcn_readlane(v, 2), 12) + xrotl(__builtin_amdgcn_readlane(v, 3), 18)
+                       : kXP5;
+  h += n;
+  uint32_t i = n & ~15u;
+  for (; i + 4 <= n; i += 4) h = xrotl(h + ld_le32(p + i) * kXP3, 17) * kXP4;
+  for (; i < n; i++) h = xrotl(h + uint32_t(p[i]) * kXP5, 11) * kXP1;
+  h ^= h >> 15;
+  h *= kXP2;
+  h ^= h >> 13;
+  h *= kXP3;
+  h ^= h >> 16;
+  if (lane == 0) *out = h;
+}
+
+hipError_t launch_lz4_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
+                                     uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus) {
+  if (nblk == 0) return hipGetLastError();
+  const size_t lds = size_t(kLz4PayIn) + kLz4PayOut;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&lz4_payload_blocks_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  lz4_payload_blocks_kernel<<<min(nblk, uint32_t(num_cus)), 64, lds, st>>>(in, blk, nblk, bmax, slots, sizes);
+  return hipGetLastError();
+}
+
+hipError_t launch_xxh32(hipStream_t st, const uint8_t* p, uint32_t n, uint32_t* out) {
+  lz4_payload_xxh32_kernel<<<1, 64, 0, st>>>(p, n, out);
+  return hipGetLastError();
 }
 
 // --------------------------------------------------------------- launchers

@@ -154,6 +154,15 @@ hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t
 hipError_t launch_index_seek(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks,
                              const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq, uint64_t* out);
 
+// CodecLz4 index / filter payloads split by (independent) data block: blk = nblk x (frame offset,
+// block size word); one wave per block in LDS; sizes[k] = decoded bytes at slots + k * 64 KiB, or
+// ~0u for a block the serial path must decode (decode.hip).
+constexpr uint32_t kLz4PayloadSlot = 65536;
+hipError_t launch_lz4_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
+                                     uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus);
+// XXH32 (seed 0) of n bytes of a 16-byte aligned device buffer into *out (one wave).
+hipError_t launch_xxh32(hipStream_t st, const uint8_t* p, uint32_t n, uint32_t* out);
+
 // Validates that the code object loads on the current device.
 hipError_t decode_kernels_available();
 
