@@ -368,6 +368,72 @@ static uint32_t xxh32_small(const uint8_t* p, size_t n) {
   return h;
 }
 
+// The GPU part of the split payload paths: the payload's CRC, then its blocks (blk = offset /
+// header word pairs) one wave each into 64 KiB slots, their outputs concatenated, the content size
+// and checksum (LZ4: XXH32; Zstd: XXH64's low half), and the decoded bytes back into `out`.
+static int payload_split_run(slate_ctx* ctx, const uint8_t* buf, size_t len, const std::vector<uint32_t>& blk,
+                             uint32_t bmax, int codec, bool has_size, uint64_t content, bool has_sum, uint32_t want,
+                             std::vector<uint8_t>& out, int* bstatus, int* handled) {
+  const size_t clen = len - 4;
+  const uint32_t nblk = uint32_t(blk.size() / 2);
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  int s = ctx_h2d(ctx, ctx->d_in.p, buf, len, st);
+  if (s) return s;
+  uint32_t crc = 0;
+  s = ctx_crc32_device(ctx, ctx->d_in.as<uint8_t>(), clen, &crc);
+  if (s) return s;
+  if (crc != ld_be32(buf + clen)) {
+    *bstatus = SLATE_E_BLOCK_CHECKSUM;  // block.Decode / bloom.Decode / DecodeIndex check it first
+    *handled = 1;
+    return SLATE_OK;
+  }
+  SLATE_HIP(ctx->d_scratch.ensure(size_t(nblk) * 12 + 64));
+  uint32_t* d_blk = ctx->d_scratch.as<uint32_t>();
+  uint32_t* d_sizes = d_blk + 2 * size_t(nblk);
+  SLATE_HIP(ctx->d_rows.ensure(size_t(nblk) * kLz4PayloadSlot + 64));  // the blocks' output slots
+  if (nblk) SLATE_HIP(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
+  if (codec == SLATE_CODEC_LZ4)
+    SLATE_HIP(launch_lz4_payload_blocks(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, bmax, ctx->d_rows.as<uint8_t>(),
+                                        d_sizes, ctx->num_cus));
+  else
+    SLATE_HIP(launch_zstd_payload_blocks(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, bmax, ctx->d_rows.as<uint8_t>(),
+                                         d_sizes, ctx->num_cus));
+  std::vector<uint32_t> sizes(nblk);
+  if (nblk) SLATE_HIP(hipMemcpyAsync(sizes.data(), d_sizes, size_t(nblk) * 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    if (sizes[k] == ~0u) return SLATE_OK;  // the serial path decodes (and reports) it
+    total += sizes[k];
+  }
+  if (total > 0xFFFFFF00ull || (has_size && content != total)) return SLATE_OK;
+  SLATE_HIP(ctx->d_out.ensure(total + 64));
+  uint8_t* d_out = ctx->d_out.as<uint8_t>();
+  uint64_t o = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    if (sizes[k])
+      SLATE_HIP(hipMemcpyAsync(d_out + o, ctx->d_rows.as<uint8_t>() + size_t(k) * kLz4PayloadSlot, sizes[k],
+                               hipMemcpyDeviceToDevice, st));
+    o += sizes[k];
+  }
+  if (has_sum) {
+    if (codec == SLATE_CODEC_LZ4) SLATE_HIP(launch_xxh32(st, d_out, uint32_t(total), d_sizes));
+    else SLATE_HIP(launch_xxh64_lo(st, d_out, uint32_t(total), d_sizes));
+    uint32_t got = 0;
+    SLATE_HIP(hipMemcpyAsync(&got, d_sizes, 4, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (got != want) return SLATE_OK;  // the serial path reports the checksum
+  }
+  out.resize(total);
+  s = ctx_d2h(ctx, out.data(), d_out, total, st);
+  if (s) return s;
+  *bstatus = SLATE_OK;
+  *handled = 1;
+  return SLATE_OK;
+}
+
 // A large CodecLz4 index / filter (`frame || BE32 CRC`) decoded block by block in parallel when
 // its frame has the shape this builder writes: independent data blocks (FLG bit 5), no block
 // checksums, no dictionary, every block decoding to at most 64 KiB.  The frame header and the
@@ -417,67 +483,75 @@ static int lz4_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std
     pos += 4;
   }
   if (pos != clen) return SLATE_OK;
-  const uint32_t nblk = uint32_t(blk.size() / 2);
-  // ---- on the GPU: the payload's CRC, then the blocks, then the content checksum
-  SLATE_HIP(ctx_bind(ctx));
-  hipStream_t st = ctx->stream;
-  SLATE_HIP(ctx->d_in.ensure(len + 64));
-  int s = ctx_h2d(ctx, ctx->d_in.p, buf, len, st);
-  if (s) return s;
-  uint32_t crc = 0;
-  s = ctx_crc32_device(ctx, ctx->d_in.as<uint8_t>(), clen, &crc);
-  if (s) return s;
-  if (crc != ld_be32(buf + clen)) {
-    *bstatus = SLATE_E_BLOCK_CHECKSUM;  // block.Decode / bloom.Decode / DecodeIndex check it first
-    *handled = 1;
-    return SLATE_OK;
+  return payload_split_run(ctx, buf, len, blk, bmax, SLATE_CODEC_LZ4, (flg & 8) != 0, content, ccheck, want, out,
+                           bstatus, handled);
+}
+
+// A large CodecZstd index / filter decoded block by block in parallel when it is one frame whose
+// compressed blocks decode on their own (the frames this builder writes; decode.hip
+// zstd_payload_blocks_kernel checks it block by block).  Same contract as lz4_payload_split.
+static int zstd_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
+                              int* bstatus, int* handled) {
+  *handled = 0;
+  const size_t clen = len - 4;
+  const uint8_t* f = buf;
+  auto le32 = [&](size_t i) {
+    return uint32_t(f[i]) | uint32_t(f[i + 1]) << 8 | uint32_t(f[i + 2]) << 16 | uint32_t(f[i + 3]) << 24;
+  };
+  if (clen < 6 || le32(0) != 0xFD2FB528u) return SLATE_OK;
+  const uint32_t fhd = f[4], fcsf = fhd >> 6, ss = (fhd >> 5) & 1, dif = fhd & 3;
+  if (fhd & 8) return SLATE_OK;
+  const uint32_t dsz = dif == 3 ? 4 : dif, fl = fcsf == 0 ? ss : (2u << (fcsf - 1));
+  const size_t hsize = 1 + (ss ? 0 : 1) + dsz + fl;
+  if (clen < 4 + hsize) return SLATE_OK;
+  size_t q = 5;
+  uint64_t window = 0;
+  if (!ss) {
+    const uint32_t wd = f[q++], wl = 10 + (wd >> 3);
+    window = (1ull << wl) + ((1ull << wl) >> 3) * (wd & 7);
   }
-  SLATE_HIP(ctx->d_scratch.ensure(size_t(nblk) * 12 + 64));
-  uint32_t* d_blk = ctx->d_scratch.as<uint32_t>();
-  uint32_t* d_sizes = d_blk + 2 * size_t(nblk);
-  SLATE_HIP(ctx->d_rows.ensure(size_t(nblk) * kLz4PayloadSlot + 64));  // the blocks' output slots
-  if (nblk) SLATE_HIP(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
-  SLATE_HIP(launch_lz4_payload_blocks(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, bmax, ctx->d_rows.as<uint8_t>(),
-                                      d_sizes, ctx->num_cus));
-  std::vector<uint32_t> sizes(nblk);
-  if (nblk) SLATE_HIP(hipMemcpyAsync(sizes.data(), d_sizes, size_t(nblk) * 4, hipMemcpyDeviceToHost, st));
-  SLATE_HIP(hipStreamSynchronize(st));
-  uint64_t total = 0;
-  for (uint32_t k = 0; k < nblk; k++) {
-    if (sizes[k] == ~0u) return SLATE_OK;  // the serial path decodes (and reports) it
-    total += sizes[k];
+  uint32_t dict = 0;
+  for (uint32_t i = 0; i < dsz; i++) dict |= uint32_t(f[q++]) << (8 * i);
+  if (dict) return SLATE_OK;
+  uint64_t fcs = 0;
+  for (uint32_t i = 0; i < fl; i++) fcs |= uint64_t(f[q + i]) << (8 * i);
+  if (fl == 2) fcs += 256;
+  if (ss) window = fcs;
+  if (window > (1ull << 29)) return SLATE_OK;
+  const uint32_t bmax = uint32_t(window < 128 * 1024 ? window : 128 * 1024);
+  std::vector<uint32_t> blk;
+  size_t pos = 4 + hsize;
+  for (;;) {
+    if (clen - pos < 3) return SLATE_OK;
+    const uint32_t bh = uint32_t(f[pos]) | uint32_t(f[pos + 1]) << 8 | uint32_t(f[pos + 2]) << 16;
+    const uint32_t bt = (bh >> 1) & 3, bs = bh >> 3;
+    if (bt == 3 || bs > bmax) return SLATE_OK;
+    const size_t body = bt == 1 ? 1 : bs;
+    if (clen - pos - 3 < body || pos + 3 > 0xFFFFFFFFull) return SLATE_OK;
+    blk.push_back(uint32_t(pos + 3));
+    blk.push_back(bh);
+    pos += 3 + body;
+    if (bh & 1) break;
   }
-  if (total > 0xFFFFFF00ull || ((flg & 8) && content != total)) return SLATE_OK;
-  SLATE_HIP(ctx->d_out.ensure(total + 64));
-  uint8_t* d_out = ctx->d_out.as<uint8_t>();
-  uint64_t o = 0;
-  for (uint32_t k = 0; k < nblk; k++) {
-    if (sizes[k])
-      SLATE_HIP(hipMemcpyAsync(d_out + o, ctx->d_rows.as<uint8_t>() + size_t(k) * kLz4PayloadSlot, sizes[k],
-                               hipMemcpyDeviceToDevice, st));
-    o += sizes[k];
+  const bool has_sum = (fhd >> 2) & 1;
+  uint32_t want = 0;
+  if (has_sum) {
+    if (clen - pos < 4) return SLATE_OK;
+    want = le32(pos);
+    pos += 4;
   }
-  if (ccheck) {
-    SLATE_HIP(launch_xxh32(st, d_out, uint32_t(total), d_sizes));
-    uint32_t got = 0;
-    SLATE_HIP(hipMemcpyAsync(&got, d_sizes, 4, hipMemcpyDeviceToHost, st));
-    SLATE_HIP(hipStreamSynchronize(st));
-    if (got != want) return SLATE_OK;  // the serial path reports the frame checksum
-  }
-  out.resize(total);
-  s = ctx_d2h(ctx, out.data(), d_out, total, st);
-  if (s) return s;
-  *bstatus = SLATE_OK;
-  *handled = 1;
-  return SLATE_OK;
+  if (pos != clen) return SLATE_OK;  // one frame, nothing after it
+  return payload_split_run(ctx, buf, len, blk, bmax, SLATE_CODEC_ZSTD, fl != 0, fcs, has_sum, want, out, bstatus,
+                           handled);
 }
 
 int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
                               int* bstatus) {
   if (codec == SLATE_CODEC_SNAPPY) return ctx_snappy_decode_buffer(ctx, buf, len, out, bstatus);
-  if (codec == SLATE_CODEC_LZ4 && len >= kSplitMin && len <= 0xFFFFFF00ull) {
+  if ((codec == SLATE_CODEC_LZ4 || codec == SLATE_CODEC_ZSTD) && len >= kSplitMin && len <= 0xFFFFFF00ull) {
     int handled = 0;
-    const int s = lz4_payload_split(ctx, buf, len, out, bstatus, &handled);
+    const int s = codec == SLATE_CODEC_LZ4 ? lz4_payload_split(ctx, buf, len, out, bstatus, &handled)
+                                           : zstd_payload_split(ctx, buf, len, out, bstatus, &handled);
     if (s || handled) return s;
   }
   if (codec != SLATE_CODEC_LZ4 && codec != SLATE_CODEC_ZLIB && codec != SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;

@@ -1268,6 +1268,144 @@ __global__ __launch_bounds__(64) void lz4_payload_xxh32_kernel(const uint8_t* __
   if (lane == 0) *out = h;
 }
 
+// CodecZstd payloads split by block: a frame whose compressed blocks decode on their own (fresh
+// state: predefined or own tables, no treeless literals, no repeat offsets, no match reaching
+// before the block) -- the frames this builder writes: one block per 64 KiB piece.  blk = nblk x
+// (frame offset, block header); one wave per block with the block, its output and the tables in
+// LDS; sizes[k] = decoded bytes at slots + k * 64 KiB, or ~0u for the serial path.
+constexpr uint32_t kZsPayIn = 65536 + 32, kZsPayOut = 65536;
+__global__ __launch_bounds__(64) void zstd_payload_blocks_kernel(const uint8_t* __restrict__ in,
+                                                                 const uint32_t* __restrict__ blk, uint32_t nblk,
+                                                                 uint32_t bmax, uint8_t* __restrict__ slots,
+                                                                 uint32_t* __restrict__ sizes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* lin = smem;
+  uint8_t* lout = smem + kZsPayIn;
+  ZsShared* sh = reinterpret_cast<ZsShared*>(lout + kZsPayOut);
+  ZsScratch* sc = reinterpret_cast<ZsScratch*>(reinterpret_cast<uint8_t*>(sh) + kZsShared);
+  const int lane = int(threadIdx.x);
+  zs_shared_build(sh, sc, lane);
+  zs_sync();
+  for (uint32_t k = blockIdx.x; k < nblk; k += gridDim.x) {
+    const uint32_t pos = blk[2 * k], bh = blk[2 * k + 1];
+    const uint32_t bt = (bh >> 1) & 3, bs = bh >> 3;
+    const uint8_t* g = in + pos;
+    const uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(g) & 15);
+    const uint32_t clen = bt == 1 ? 1u : bs;  // bytes of the block body
+    if (bt == 3 || shift + clen + 16 > kZsPayIn || bs > bmax || (bt != 2 && bs > kZsPayOut)) {
+      if (lane == 0) sizes[k] = ~0u;
+      continue;
+    }
+    zs_sync();
+    {
+      const uint4* src4 = reinterpret_cast<const uint4*>(g - shift);
+      uint4* dst4 = reinterpret_cast<uint4*>(lin);
+      const uint32_t chunks = (shift + clen + 15) / 16;
+      for (uint32_t c = uint32_t(lane); c < chunks; c += kWave) dst4[c] = src4[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    zs_sync();
+    uint32_t d = 0;
+    bool ok = true;
+    if (bt == 0) {
+      for (uint32_t j = uint32_t(lane); j < bs; j += kWave) lout[j] = lin[shift + j];
+      d = bs;
+    } else if (bt == 1) {
+      const uint8_t v = lin[shift];
+      for (uint32_t j = uint32_t(lane); j < bs; j += kWave) lout[j] = v;
+      d = bs;
+    } else {
+      ZsState st{nullptr, nullptr, nullptr, 0, 0, 0, 0, 0, {1, 4, 8}, 0};
+      const int r = zs_block(lin, int32_t(shift), bs, lout, kZsPayOut, &d, 0u, bmax, sc, sh, st, lane);
+      ok = r == SLATE_OK && !st.rep_used;
+    }
+    zs_sync();
+    __builtin_amdgcn_s_waitcnt(0);
+    if (ok) {
+      uint4* o4 = reinterpret_cast<uint4*>(slots + size_t(k) * kZsPayOut);
+      const uint4* l4 = reinterpret_cast<const uint4*>(lout);
+      for (uint32_t c = uint32_t(lane); c < (d + 15) / 16; c += kWave) o4[c] = l4[c];
+    }
+    if (lane == 0) sizes[k] = ok ? d : ~0u;
+  }
+}
+
+// XXH64 (seed 0) of a 16-byte aligned device buffer by one wave (2 KiB of 32-byte stripes per
+// step staged in LDS, loaded one step ahead; accumulators on lanes 0-3); out = the low 32 bits
+// as the frame stores them.
+__global__ __launch_bounds__(64) void zstd_payload_xxh64_kernel(const uint8_t* __restrict__ p, uint32_t n,
+                                                                uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 buf[2][128];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t stripes = n / 32, steps = (stripes + 63) / 64;
+  uint64_t v = lane == 0 ? kX64P1 + kX64P2 : (lane == 1 ? kX64P2 : (lane == 2 ? 0ull : 0ull - kX64P1));
+  const uint4* p4 = reinterpret_cast<const uint4*>(p);
+  const uint32_t q16 = 2 * stripes;  // 16-byte chunks in whole stripes
+  uint4 n0 = lane < q16 ? p4[lane] : make_uint4(0, 0, 0, 0), n1 = 64 + lane < q16 ? p4[64 + lane] : make_uint4(0, 0, 0, 0);
+  for (uint32_t t = 0; t < steps; t++) {
+    buf[t & 1][lane] = n0;
+    buf[t & 1][64 + lane] = n1;
+    const uint32_t q = 128 * (t + 1) + lane;
+    n0 = q < q16 ? p4[q] : make_uint4(0, 0, 0, 0);
+    n1 = q + 64 < q16 ? p4[q + 64] : make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    if (lane < 4) {
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(buf[t & 1]);
+      const uint32_t m = min(64u, stripes - 64 * t);
+      for (uint32_t i = 0; i < m; i++) v = x64round(v, w[4 * i + lane]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  uint64_t vv[4];
+  for (int l = 0; l < 4; l++)
+    vv[l] = uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(v), l))) |
+            (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(v >> 32), l))) << 32);
+  uint64_t h;
+  if (n >= 32) {
+    h = x64rotl(vv[0], 1) + x64rotl(vv[1], 7) + x64rotl(vv[2], 12) + x64rotl(vv[3], 18);
+    for (int l = 0; l < 4; l++) h = (h ^ x64round(0, vv[l])) * kX64P1 + kX64P4;
+  } else {
+    h = kX64P5;
+  }
+  h += n;
+  uint32_t i = n & ~31u;
+  auto le64 = [&](uint32_t o) {
+    uint64_t x = 0;
+    for (int b = 7; b >= 0; b--) x = (x << 8) | p[o + b];
+    return x;
+  };
+  for (; i + 8 <= n; i += 8) h = x64rotl(h ^ x64round(0, le64(i)), 27) * kX64P1 + kX64P4;
+  if (i + 4 <= n) {
+    h = x64rotl(h ^ uint64_t(ld_le32(p + i)) * kX64P1, 23) * kX64P2 + kX64P3;
+    i += 4;
+  }
+  for (; i < n; i++) h = x64rotl(h ^ uint64_t(p[i]) * kX64P5, 11) * kX64P1;
+  h ^= h >> 33;
+  h *= kX64P2;
+  h ^= h >> 29;
+  h *= kX64P3;
+  h ^= h >> 32;
+  if (lane == 0) *out = uint32_t(h);
+}
+
+hipError_t launch_zstd_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
+                                      uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus) {
+  if (nblk == 0) return hipGetLastError();
+  const size_t lds = size_t(kZsPayIn) + kZsPayOut + kZsShared + kZsScratch;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zstd_payload_blocks_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  zstd_payload_blocks_kernel<<<min(nblk, uint32_t(num_cus)), 64, lds, st>>>(in, blk, nblk, bmax, slots, sizes);
+  return hipGetLastError();
+}
+
+hipError_t launch_xxh64_lo(hipStream_t st, const uint8_t* p, uint32_t n, uint32_t* out) {
+  zstd_payload_xxh64_kernel<<<1, 64, 0, st>>>(p, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_lz4_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
                                      uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus) {
   if (nblk == 0) return hipGetLastError();

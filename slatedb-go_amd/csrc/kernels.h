@@ -160,6 +160,12 @@ hipError_t launch_index_seek(hipStream_t st, const uint8_t* keys, const uint64_t
 constexpr uint32_t kLz4PayloadSlot = 65536;
 hipError_t launch_lz4_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
                                      uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus);
+// CodecZstd index / filter payloads split by block (blk = nblk x (frame offset, block header)),
+// the same contract for blocks that decode on their own (decode.hip).
+hipError_t launch_zstd_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
+                                      uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus);
+// The low 32 bits of XXH64 (seed 0) of a 16-byte aligned device buffer into *out (one wave).
+hipError_t launch_xxh64_lo(hipStream_t st, const uint8_t* p, uint32_t n, uint32_t* out);
 // XXH32 (seed 0) of n bytes of a 16-byte aligned device buffer into *out (one wave).
 hipError_t launch_xxh32(hipStream_t st, const uint8_t* p, uint32_t n, uint32_t* out);
 

@@ -339,6 +339,7 @@ struct ZsState {
   uint32_t ll_al, of_al, ml_al;
   uint32_t huf_valid, tl;
   uint32_t rep[3];
+  uint32_t rep_used;  // a sequence took a repeat offset (the split payload path needs none)
 };
 
 // Symbol_Compression_Mode for one table type: bytes used or -1 (oracle zs_table).
@@ -583,6 +584,7 @@ __device__ int zs_block(const uint8_t* base, int32_t off, uint32_t n, uint8_t* o
         st.rep[1] = st.rep[0];
         st.rep[0] = uint32_t(offv);
       } else {
+        st.rep_used = 1;
         const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1u : 0u);
         offv = idx == 3 ? uint64_t(st.rep[0]) - 1 : (idx == 0 ? st.rep[0] : idx == 1 ? st.rep[1] : st.rep[2]);
         if (offv == 0) offv = 1;

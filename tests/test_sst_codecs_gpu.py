@@ -113,26 +113,27 @@ def test_damaged_index_and_filter(ctx, codec):
     assert ctx.decode_index(bad, codec)[0] == ob.decode_index(bad, codec)[0] != 0
 
 
-def test_lz4_split_payloads(ctx):
-    """Index and filter payloads of this builder's LZ4 frames (independent 64 KiB data blocks, more
-    than 32 KiB: api_sst.cpp lz4_payload_split, one wave per data block) decoded like the oracle;
-    damaged ones (flipped bytes under a valid CRC, a wrong content checksum, a wrong CRC) reach the
-    serial path or the CRC check with the oracle's statuses."""
+@pytest.mark.parametrize("codec", [ob.LZ4, ob.ZSTD])
+def test_split_payloads(ctx, codec):
+    """Index and filter payloads of this builder's LZ4 / Zstd frames (independent 64 KiB blocks,
+    more than 32 KiB: api_sst.cpp lz4_payload_split / zstd_payload_split, one wave per block)
+    decoded like the oracle; damaged ones (flipped bytes under a valid CRC, a wrong content
+    checksum, a wrong CRC) reach the serial path or the CRC check with the oracle's statuses."""
     import slatecodec as sc
     from tools.bench_encode import kv_arrays
     keys, key_off, vals, val_off = kv_arrays(1_200_000)
-    b = sc.SstBuilder(ctx, 4096, 0, 10, ob.LZ4)
+    b = sc.SstBuilder(ctx, 4096, 0, 10, codec)
     assert b.add_batch(keys, key_off, vals, val_off) == 0
     sst = b.build().encode()
     st, info, _ = sc.read_info(sst)
     ib = sst[info.index_offset:info.index_offset + info.index_len]
     fb = sst[info.filter_offset:info.filter_offset + info.filter_len]
     assert len(ib) > 256 * 1024 and len(fb) > 1024 * 1024
-    st, index = ctx.decode_index(ib, ob.LZ4)
-    ost, ometas = ob.decode_index(ib, ob.LZ4, cap=1 << 24)
+    st, index = ctx.decode_index(ib, codec)
+    ost, ometas = ob.decode_index(ib, codec, cap=1 << 24)
     assert st == ost == 0 and index.block_metas() == ometas
-    g = ctx.bloom_decode(fb, ob.LZ4)
-    o = ob.bloom_decode(fb, ob.LZ4, cap=1 << 24)
+    g = ctx.bloom_decode(fb, codec)
+    o = ob.bloom_decode(fb, codec, cap=1 << 24)
     assert g[0] == o[0] == 0 and g[1:] == o[1:]
     rng = random.Random(5)
     for trial in range(12):
@@ -145,11 +146,11 @@ def test_lz4_split_payloads(ctx):
                 body[rng.randrange(11, len(body) - 8)] ^= 1 << rng.randrange(8)
         buf = sstgen.crc(bytes(body))
         if trial % 2 == 0:
-            st, _ = ctx.decode_index(buf, ob.LZ4)
-            ost, _ = ob.decode_index(buf, ob.LZ4, cap=1 << 24)
+            st, _ = ctx.decode_index(buf, codec)
+            ost, _ = ob.decode_index(buf, codec, cap=1 << 24)
         else:
-            st = ctx.bloom_decode(buf, ob.LZ4)[0]
-            ost = ob.bloom_decode(buf, ob.LZ4, cap=1 << 24)[0]
+            st = ctx.bloom_decode(buf, codec)[0]
+            ost = ob.bloom_decode(buf, codec, cap=1 << 24)[0]
         assert st == ost, (trial, st, ost)
     bad = fb[:-1] + bytes([fb[-1] ^ 1])
-    assert ctx.bloom_decode(bad, ob.LZ4)[0] == ob.bloom_decode(bad, ob.LZ4, cap=1 << 24)[0] != 0
+    assert ctx.bloom_decode(bad, codec)[0] == ob.bloom_decode(bad, codec, cap=1 << 24)[0] != 0

@@ -1,8 +1,8 @@
 #!/bin/bash
-# r3s: LZ4 index / filter payloads split by data block: SST codec suite, LZ4 suite, open times.
+# r3t: LZ4 and Zstd payloads split by block: SST codec suite, LZ4 suite, open times.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-OUT=gpurun_out/r3s
+OUT=gpurun_out/r3t
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_sst_codecs_gpu.py tests/test_lz4_gpu.py -x -v --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { echo TESTS_FAILED; tail -60 $OUT/tests.log; exit 1; }
 tail -3 $OUT/tests.log
