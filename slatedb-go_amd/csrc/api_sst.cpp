@@ -397,9 +397,12 @@ static int payload_split_run(slate_ctx* ctx, const uint8_t* buf, size_t len, con
   if (codec == SLATE_CODEC_LZ4)
     SLATE_HIP(launch_lz4_payload_blocks(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, bmax, ctx->d_rows.as<uint8_t>(),
                                         d_sizes, ctx->num_cus));
-  else
+  else if (codec == SLATE_CODEC_ZSTD)
     SLATE_HIP(launch_zstd_payload_blocks(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, bmax, ctx->d_rows.as<uint8_t>(),
                                          d_sizes, ctx->num_cus));
+  else
+    SLATE_HIP(launch_zlib_payload_segs(st, ctx->d_in.as<uint8_t>(), d_blk, nblk, ctx->d_rows.as<uint8_t>(), d_sizes,
+                                       ctx->num_cus));
   std::vector<uint32_t> sizes(nblk);
   if (nblk) SLATE_HIP(hipMemcpyAsync(sizes.data(), d_sizes, size_t(nblk) * 4, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
@@ -418,7 +421,22 @@ static int payload_split_run(slate_ctx* ctx, const uint8_t* buf, size_t len, con
                                hipMemcpyDeviceToDevice, st));
     o += sizes[k];
   }
-  if (has_sum) {
+  if (has_sum && codec == SLATE_CODEC_ZLIB) {
+    // Adler-32 (RFC 1950): a = 1 + sum x, b = n + sum (n - j) x, from 4 KiB slices' partial sums
+    const uint32_t nsl = uint32_t((total + 4095) / 4096);
+    SLATE_HIP(ctx->e_k.ensure(size_t(nsl) * 16 + 64));
+    SLATE_HIP(launch_adler_slices(st, d_out, uint32_t(total), ctx->e_k.as<uint64_t>()));
+    std::vector<uint64_t> part(2 * size_t(nsl));
+    if (nsl) SLATE_HIP(hipMemcpyAsync(part.data(), ctx->e_k.p, part.size() * 8, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    uint64_t a = 1, b = total % 65521;
+    for (uint32_t t = 0; t < nsl; t++) {
+      const uint64_t end = std::min<uint64_t>(total, 4096ull * (t + 1));
+      a = (a + part[2 * t]) % 65521;
+      b = (b + part[2 * t + 1] % 65521 + (part[2 * t] % 65521) * ((total - end) % 65521)) % 65521;
+    }
+    if (((b << 16) | a) != want) return SLATE_OK;  // the serial path reports the checksum
+  } else if (has_sum) {
     if (codec == SLATE_CODEC_LZ4) SLATE_HIP(launch_xxh32(st, d_out, uint32_t(total), d_sizes));
     else SLATE_HIP(launch_xxh64_lo(st, d_out, uint32_t(total), d_sizes));
     uint32_t got = 0;
@@ -545,13 +563,45 @@ static int zstd_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, st
                            handled);
 }
 
+// A large CodecZlib index / filter (`zlib stream || BE32 CRC`) inflated piece by piece in parallel:
+// this builder ends every piece but the last with an empty stored block, so the stream is cut
+// after each `00 00 FF FF` (decode.hip zlib_payload_segs_kernel checks that every segment is a
+// whole piece).  Same contract as lz4_payload_split.
+static int zlib_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
+                              int* bstatus, int* handled) {
+  *handled = 0;
+  const size_t clen = len - 4;
+  const uint8_t* f = buf;
+  if (clen < 2 + 4) return SLATE_OK;
+  const uint32_t b0 = f[0], b1 = f[1];
+  if ((b0 & 0x0f) != 8 || (b0 >> 4) > 7 || ((b0 << 8) | b1) % 31 != 0 || (b1 & 0x20)) return SLATE_OK;
+  const size_t dend = clen - 4;  // the Adler-32 trailer (big-endian) follows the deflate stream
+  const uint32_t want = uint32_t(f[dend]) << 24 | uint32_t(f[dend + 1]) << 16 | uint32_t(f[dend + 2]) << 8 | f[dend + 3];
+  std::vector<uint32_t> seg;
+  size_t s0 = 2;
+  for (size_t i = 2; i + 4 <= dend; i++) {
+    if (f[i] == 0 && f[i + 1] == 0 && f[i + 2] == 0xFF && f[i + 3] == 0xFF) {
+      seg.push_back(uint32_t(s0));
+      seg.push_back(uint32_t(i + 4 - s0));
+      s0 = i + 4;
+      i += 3;
+    }
+  }
+  if (s0 >= dend || dend > 0xFFFFFFFFull) return SLATE_OK;
+  seg.push_back(uint32_t(s0));
+  seg.push_back(uint32_t(dend - s0));
+  return payload_split_run(ctx, buf, len, seg, 0, SLATE_CODEC_ZLIB, false, 0, true, want, out, bstatus, handled);
+}
+
 int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,
                               int* bstatus) {
   if (codec == SLATE_CODEC_SNAPPY) return ctx_snappy_decode_buffer(ctx, buf, len, out, bstatus);
-  if ((codec == SLATE_CODEC_LZ4 || codec == SLATE_CODEC_ZSTD) && len >= kSplitMin && len <= 0xFFFFFF00ull) {
+  if ((codec == SLATE_CODEC_LZ4 || codec == SLATE_CODEC_ZSTD || codec == SLATE_CODEC_ZLIB) && len >= kSplitMin &&
+      len <= 0xFFFFFF00ull) {
     int handled = 0;
-    const int s = codec == SLATE_CODEC_LZ4 ? lz4_payload_split(ctx, buf, len, out, bstatus, &handled)
-                                           : zstd_payload_split(ctx, buf, len, out, bstatus, &handled);
+    const int s = codec == SLATE_CODEC_LZ4    ? lz4_payload_split(ctx, buf, len, out, bstatus, &handled)
+                  : codec == SLATE_CODEC_ZSTD ? zstd_payload_split(ctx, buf, len, out, bstatus, &handled)
+                                              : zlib_payload_split(ctx, buf, len, out, bstatus, &handled);
     if (s || handled) return s;
   }
   if (codec != SLATE_CODEC_LZ4 && codec != SLATE_CODEC_ZLIB && codec != SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;

@@ -630,15 +630,20 @@ __device__ void zfixed_build(ZHuff* fl, ZHuff* fd, uint8_t* lens, int lane) {
 
 // The stream in[0, n) decoded in order into out[0, cap) (out == nullptr: sizes only, no
 // Adler-32).  *out_len: bytes written so far (also on failure).
+// kSeg (zlib_payload_segs_kernel): in[0, n) is a raw deflate segment of a larger stream that
+// starts with a block header and ends either after an empty non-final stored block whose bytes
+// end exactly at n (a piece of this builder's streams) or after the final block at the byte
+// boundary n; no zlib header, no Adler-32; distances may not reach before the segment.
+template <bool kSeg = false>
 __device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap, ZScratch* zs,
                             const ZHuff* fixl, const ZHuff* fixd, int lane, uint32_t* out_len) {
   *out_len = 0;
   if (n == 0) return SLATE_E_EOF;
   if (n < 2) return SLATE_E_UNEXPECTED_EOF;
   const uint32_t b0 = __builtin_amdgcn_readfirstlane(in[0]), b1 = __builtin_amdgcn_readfirstlane(in[1]);
-  if ((b0 & 0x0f) != 8 || (b0 >> 4) > 7 || ((b0 << 8) | b1) % 31 != 0) return SLATE_E_ZLIB_HEADER;
-  uint32_t start = 2;
-  if (b1 & 0x20) {
+  if (!kSeg && ((b0 & 0x0f) != 8 || (b0 >> 4) > 7 || ((b0 << 8) | b1) % 31 != 0)) return SLATE_E_ZLIB_HEADER;
+  uint32_t start = kSeg ? 0u : 2u;
+  if (!kSeg && (b1 & 0x20)) {
     if (n < 6) return SLATE_E_UNEXPECTED_EOF;
     const uint32_t id = __builtin_amdgcn_readfirstlane(ld_be32(in + 2));
     if (id != 1) return SLATE_E_ZLIB_DICTIONARY;
@@ -670,6 +675,7 @@ __device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_
       z.pos += avail;
       *out_len = d;
       if (avail < len) return SLATE_E_UNEXPECTED_EOF;
+      if (kSeg && !final && len == 0 && z.pos == n) return SLATE_OK;  // the piece's byte-aligning end
       continue;
     }
     if (type == 3) return SLATE_E_FLATE_CORRUPT;
@@ -768,6 +774,7 @@ __device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_
   // the Adler-32 trailer starts at the next byte boundary
   ztake(z, z.nb & 7);
   const uint32_t p = z.pos - z.nb / 8;
+  if (kSeg) return p == n ? SLATE_OK : SLATE_E_FLATE_CORRUPT;  // the last segment ends the stream
   if (n - p < 4) return SLATE_E_UNEXPECTED_EOF;
   if (out) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -1116,6 +1123,97 @@ __global__ __launch_bounds__(64) void decode_payload_kernel(DecodeArgs a) {
   if (CK == 1) zlib_lds(w, smem + kTabBytes, 1, 0, lane);
   if (CK == 2) zstd_lds(w, smem + kTabBytes, 0, lane);
   for (uint32_t b = blockIdx.x; b < a.n; b += gridDim.x) decode_block_wave<CK, true>(a, b, w, lane, false);
+}
+
+// ---------------------------------------------- CodecZlib payloads split by piece
+// An index or filter written by this builder is one deflate stream whose pieces each end with an
+// empty stored block, so piece k starts byte-aligned right after the k-th `00 00 FF FF`.  The host
+// cuts the stream at those markers (a marker inside a piece's data makes that piece fail here, and
+// the serial path takes over); one wave per segment inflates it in LDS (wave_inflate<true>).
+// seg = nseg x (stream offset, length); sizes[k] = decoded bytes at slots + k * 64 KiB, or ~0u.
+constexpr uint32_t kZPayIn = 66 * 1024 + 32, kZPayOut = 65536;
+__global__ __launch_bounds__(64) void zlib_payload_segs_kernel(const uint8_t* __restrict__ in,
+                                                               const uint32_t* __restrict__ seg, uint32_t nseg,
+                                                               uint8_t* __restrict__ slots,
+                                                               uint32_t* __restrict__ sizes) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* lin = smem;
+  uint8_t* lout = smem + kZPayIn;
+  ZHuff* fix = reinterpret_cast<ZHuff*>(lout + kZPayOut);
+  ZScratch* zs = reinterpret_cast<ZScratch*>(reinterpret_cast<uint8_t*>(fix) + kZFixed);
+  const int lane = int(threadIdx.x);
+  zfixed_build(fix, fix + 1, zs->lens, lane);
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t k = blockIdx.x; k < nseg; k += gridDim.x) {
+    const uint32_t pos = seg[2 * k], n = seg[2 * k + 1];
+    const uint8_t* g = in + pos;
+    const uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(g) & 15);
+    if (shift + n + 16 > kZPayIn) {
+      if (lane == 0) sizes[k] = ~0u;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const uint4* src4 = reinterpret_cast<const uint4*>(g - shift);
+      uint4* dst4 = reinterpret_cast<uint4*>(lin);
+      for (uint32_t c = uint32_t(lane); c < (shift + n + 15) / 16; c += kWave) dst4[c] = src4[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t d = 0;
+    const bool ok = wave_inflate<true>(lin + shift, n, lout, kZPayOut, zs, fix, fix + 1, lane, &d) == SLATE_OK;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+      uint4* o4 = reinterpret_cast<uint4*>(slots + size_t(k) * kZPayOut);
+      const uint4* l4 = reinterpret_cast<const uint4*>(lout);
+      for (uint32_t c = uint32_t(lane); c < (d + 15) / 16; c += kWave) o4[c] = l4[c];
+    }
+    if (lane == 0) sizes[k] = ok ? d : ~0u;
+  }
+}
+
+// Adler-32 partial sums of a device buffer: slice t = bytes [4096 t, 4096 t + 4096) (the last one
+// shorter): part[t] = (sum x_j, sum (end_t - j) x_j); the host folds them (api_sst.cpp).
+__global__ __launch_bounds__(256) void adler_slices_kernel(const uint8_t* __restrict__ p, uint32_t n,
+                                                           uint64_t* __restrict__ part) {
+  const uint32_t nsl = (n + 4095) / 4096;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nsl; t += gridDim.x * 4) {
+    const uint32_t s0 = 4096 * t, e = min(n, s0 + 4096);
+    uint64_t sa = 0, sb = 0;
+    for (uint32_t j = s0 + lane; j < e; j += kWave) {
+      const uint64_t x = p[j];
+      sa += x;
+      sb += uint64_t(e - j) * x;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      sa += __shfl_xor(sa, o, 64);
+      sb += __shfl_xor(sb, o, 64);
+    }
+    if (lane == 0) {
+      part[2 * t] = sa;
+      part[2 * t + 1] = sb;
+    }
+  }
+}
+
+hipError_t launch_zlib_payload_segs(hipStream_t st, const uint8_t* in, const uint32_t* seg, uint32_t nseg,
+                                    uint8_t* slots, uint32_t* sizes, int num_cus) {
+  if (nseg == 0) return hipGetLastError();
+  const size_t lds = size_t(kZPayIn) + kZPayOut + kZFixed + kZScratch;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zlib_payload_segs_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  zlib_payload_segs_kernel<<<min(nseg, uint32_t(num_cus)), 64, lds, st>>>(in, seg, nseg, slots, sizes);
+  return hipGetLastError();
+}
+
+hipError_t launch_adler_slices(hipStream_t st, const uint8_t* p, uint32_t n, uint64_t* part) {
+  const uint32_t nsl = (n + 4095) / 4096;
+  if (nsl) adler_slices_kernel<<<min((nsl + 3) / 4, 4096u), 256, 0, st>>>(p, n, part);
+  return hipGetLastError();
 }
 
 // ------------------------------------------- CodecLz4 payloads split by data block

@@ -164,6 +164,12 @@ hipError_t launch_lz4_payload_blocks(hipStream_t st, const uint8_t* in, const ui
 // the same contract for blocks that decode on their own (decode.hip).
 hipError_t launch_zstd_payload_blocks(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
                                       uint32_t bmax, uint8_t* slots, uint32_t* sizes, int num_cus);
+// CodecZlib index / filter payloads split at this builder's piece ends (seg = nseg x (stream
+// offset, length) of raw deflate segments), the same contract (decode.hip); Adler-32 partial sums
+// per 4 KiB slice (part = 2 u64 per slice: sum x, sum (slice end - j) x).
+hipError_t launch_zlib_payload_segs(hipStream_t st, const uint8_t* in, const uint32_t* seg, uint32_t nseg,
+                                    uint8_t* slots, uint32_t* sizes, int num_cus);
+hipError_t launch_adler_slices(hipStream_t st, const uint8_t* p, uint32_t n, uint64_t* part);
 // The low 32 bits of XXH64 (seed 0) of a 16-byte aligned device buffer into *out (one wave).
 hipError_t launch_xxh64_lo(hipStream_t st, const uint8_t* p, uint32_t n, uint32_t* out);
 // XXH32 (seed 0) of n bytes of a 16-byte aligned device buffer into *out (one wave).

@@ -113,10 +113,10 @@ def test_damaged_index_and_filter(ctx, codec):
     assert ctx.decode_index(bad, codec)[0] == ob.decode_index(bad, codec)[0] != 0
 
 
-@pytest.mark.parametrize("codec", [ob.LZ4, ob.ZSTD])
+@pytest.mark.parametrize("codec", [ob.LZ4, ob.ZSTD, ob.ZLIB])
 def test_split_payloads(ctx, codec):
-    """Index and filter payloads of this builder's LZ4 / Zstd frames (independent 64 KiB blocks,
-    more than 32 KiB: api_sst.cpp lz4_payload_split / zstd_payload_split, one wave per block)
+    """Index and filter payloads of this builder's LZ4 / Zstd frames and Zlib streams (independent
+    64 KiB pieces, more than 32 KiB: api_sst.cpp lz4_ / zstd_ / zlib_payload_split, one wave per piece)
     decoded like the oracle; damaged ones (flipped bytes under a valid CRC, a wrong content
     checksum, a wrong CRC) reach the serial path or the CRC check with the oracle's statuses."""
     import slatecodec as sc
