@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
+#include <future>
 #include <sys/mman.h>
 #include <memory>
 #include <vector>
@@ -1158,6 +1159,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   b->built = true;
   slate_sst_table* t = new slate_sst_table();
   std::vector<uint8_t> buf(b->last_block.data(), b->last_block.data() + b->last_block.len);
+  // the index flatbuffer (host work) is built while the filter is encoded on the GPU
+  std::future<std::vector<uint8_t>> fb_job = std::async(std::launch::async, [b] {
+    return fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
+  });
   const uint64_t filter_off = b->current_len + buf.size();
   uint64_t filter_len = 0;
   // ---- bloom filter (builder.go:225-235, bloom.go:112-133 Build, :52-67 Encode)
@@ -1168,6 +1173,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
       np = bloom_num_probes(b->cfg.filter_bits_per_key);
       nb = bloom_filter_bytes(b->num_keys, b->cfg.filter_bits_per_key);
       if (nb * 8 == 0 || nb * 8 > 0xFFFFFFFFull) {  // Go: divide by zero panic / uint32 bits
+        fb_job.wait();
         delete t;
         return SLATE_E_INVALID_ARG;
       }
@@ -1222,7 +1228,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   // ---- index (builder.go:238-244, flatbuf.go:126-139)
   std::vector<uint8_t> index;
   {
-    std::vector<uint8_t> fb = fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
+    std::vector<uint8_t> fb = fb_job.get();
     if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
       // encoded and CRC'd on the device: the payload comes back once, with its CRC
       SLATE_HIP(ctx_bind(ctx));
