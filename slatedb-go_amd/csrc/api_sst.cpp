@@ -453,9 +453,80 @@ static int payload_split_run(slate_ctx* ctx, const uint8_t* buf, size_t len, con
   return SLATE_OK;
 }
 
+// LZ4 frames with larger data blocks -- pierrec/lz4 v4's writer defaults: 4 MiB blocks, a content
+// checksum -- or linked blocks have each compressed block decoded by the tag-parallel passes
+// (snappy_stream.hip launch_lz4_par_chain / _bytes) over the whole GPU, one block after another
+// (a linked block's matches may reach into the blocks before it); stored blocks are copied.  Same
+// contract as lz4_payload_split.
+static int lz4_payload_par_run(slate_ctx* ctx, const uint8_t* buf, size_t len, const std::vector<uint32_t>& blk,
+                               uint32_t bmax, bool indep, bool has_size, uint64_t content, bool has_sum, uint32_t want,
+                               std::vector<uint8_t>& out, int* bstatus, int* handled) {
+  const size_t clen = len - 4;
+  const uint32_t nblk = uint32_t(blk.size() / 2);
+  if (uint64_t(nblk) * bmax > (1ull << 31)) return SLATE_OK;  // the output bound (every block at bmax)
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  int s = ctx_h2d(ctx, ctx->d_in.p, buf, len, st);
+  if (s) return s;
+  uint32_t crc = 0;
+  s = ctx_crc32_device(ctx, ctx->d_in.as<uint8_t>(), clen, &crc);
+  if (s) return s;
+  if (crc != ld_be32(buf + clen)) {
+    *bstatus = SLATE_E_BLOCK_CHECKSUM;  // block.Decode / bloom.Decode / DecodeIndex check it first
+    *handled = 1;
+    return SLATE_OK;
+  }
+  uint32_t smax = 0;
+  for (uint32_t k = 0; k < nblk; k++) smax = std::max(smax, blk[2 * k + 1] & 0x7FFFFFFFu);
+  SLATE_HIP(ctx->d_scratch.ensure(lz4_par_scratch_bytes(smax, bmax) + 64));
+  SLATE_HIP(ctx->d_out.ensure(uint64_t(nblk) * bmax + 64));
+  SLATE_HIP(ctx->e_k.ensure(64));
+  uint8_t* d_in = ctx->d_in.as<uint8_t>();
+  uint8_t* d_out = ctx->d_out.as<uint8_t>();
+  void* scratch = ctx->d_scratch.p;
+  uint64_t total = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    const uint32_t off = blk[2 * k], bs = blk[2 * k + 1], sz = bs & 0x7FFFFFFFu;
+    if (bs >> 31) {  // stored
+      if (sz) SLATE_HIP(hipMemcpyAsync(d_out + total, d_in + off, sz, hipMemcpyDeviceToDevice, st));
+      total += sz;
+      continue;
+    }
+    uint32_t res[5] = {1, 0, 0, 0, 0};
+    const uint32_t* d_res = lz4_par_result(scratch, sz, bmax);
+    SLATE_HIP(launch_lz4_par_chain(st, d_in + off, sz, bmax, scratch));
+    SLATE_HIP(hipMemcpyAsync(res, d_res, sizeof(res), hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (res[0]) return SLATE_OK;  // the serial path decodes (and reports) it
+    const uint32_t dn = res[4];
+    SLATE_HIP(launch_lz4_par_bytes(st, d_in + off, sz, bmax, dn, indep ? 0u : uint32_t(total), scratch,
+                                   d_out + total));
+    SLATE_HIP(hipMemcpyAsync(res, d_res, 4, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (res[0]) return SLATE_OK;
+    total += dn;
+  }
+  if (total > 0xFFFFFF00ull || (has_size && content != total)) return SLATE_OK;
+  if (has_sum) {
+    SLATE_HIP(launch_xxh32(st, d_out, uint32_t(total), ctx->e_k.as<uint32_t>()));
+    uint32_t got = 0;
+    SLATE_HIP(hipMemcpyAsync(&got, ctx->e_k.p, 4, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+    if (got != want) return SLATE_OK;  // the serial path reports the checksum
+  }
+  out.resize(total);
+  s = ctx_d2h(ctx, out.data(), d_out, total, st);
+  if (s) return s;
+  *bstatus = SLATE_OK;
+  *handled = 1;
+  return SLATE_OK;
+}
+
 // A large CodecLz4 index / filter (`frame || BE32 CRC`) decoded block by block in parallel when
-// its frame has the shape this builder writes: independent data blocks (FLG bit 5), no block
-// checksums, no dictionary, every block decoding to at most 64 KiB.  The frame header and the
+// its frame has no block checksums and no dictionary: independent blocks of at most 64 KiB (the
+// shape this builder writes) one wave each, larger or linked ones (pierrec's 4 MiB blocks)
+// through lz4_payload_par_run.  The frame header and the
 // block list are read here (structure only, as the plan does); the CRC, the blocks and the
 // content checksum are computed on the GPU.  Returns 1 with *bstatus and `out` set, or 0 when
 // the serial path must decode the payload (another shape, or any check failing: that path then
@@ -470,9 +541,9 @@ static int lz4_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std
   };
   if (clen < 7 || le32(0) != 0x184D2204u) return SLATE_OK;
   const uint32_t flg = f[4], bd = f[5];
-  if ((flg >> 6) != 1 || (flg & 2) || (bd & 0x8F) || ((bd >> 4) & 7) < 4 || (flg & 1) || !(flg & 0x20) ||
-      (flg & 0x10))
+  if ((flg >> 6) != 1 || (flg & 2) || (bd & 0x8F) || ((bd >> 4) & 7) < 4 || (flg & 1) || (flg & 0x10))
     return SLATE_OK;
+  const bool indep = (flg & 0x20) != 0;
   const uint32_t bmax = 1u << (8 + 2 * ((bd >> 4) & 7));
   const size_t hl = 2 + ((flg & 8) ? 8 : 0);
   if (clen < 4 + hl + 1 || f[4 + hl] != ((xxh32_small(f + 4, hl) >> 8) & 0xFF)) return SLATE_OK;
@@ -502,6 +573,8 @@ static int lz4_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std
     pos += 4;
   }
   if (pos != clen) return SLATE_OK;
+  if (bmax > kLz4PayloadSlot || !indep)
+    return lz4_payload_par_run(ctx, buf, len, blk, bmax, indep, (flg & 8) != 0, content, ccheck, want, out, bstatus, handled);
   return payload_split_run(ctx, buf, len, blk, bmax, SLATE_CODEC_LZ4, (flg & 8) != 0, content, ccheck, want, out,
                            bstatus, handled);
 }

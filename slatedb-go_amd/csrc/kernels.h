@@ -147,6 +147,17 @@ size_t snappy_par_scratch_bytes(uint32_t sn, uint32_t dn);
 hipError_t launch_snappy_decode_par(hipStream_t st, const uint8_t* in, uint32_t sn, uint32_t hdr, uint8_t* out,
                                     uint32_t dn, void* scratch, int32_t* status);
 
+// One independent LZ4 data block (sz bytes, decoding to at most cap) through the same passes:
+// the chain pass, then (the host having read lz4_par_result's words: [0] != 0 = hand the
+// payload to the exact decoder, [4] = decoded length) the bytes pass into out; [0] is checked
+// again after it.  prior: how far before out a match may reach (0: independent blocks; linked
+// blocks: the frame's bytes already decoded there).
+size_t lz4_par_scratch_bytes(uint32_t sz, uint32_t cap);
+const uint32_t* lz4_par_result(const void* scratch, uint32_t sz, uint32_t cap);
+hipError_t launch_lz4_par_chain(hipStream_t st, const uint8_t* in, uint32_t sz, uint32_t cap, void* scratch);
+hipError_t launch_lz4_par_bytes(hipStream_t st, const uint8_t* in, uint32_t sz, uint32_t cap, uint32_t dn,
+                                uint32_t prior, void* scratch, uint8_t* out);
+
 // Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                              const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,

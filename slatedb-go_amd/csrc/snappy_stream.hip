@@ -230,7 +230,7 @@ __host__ __device__ inline ParScratch par_carve(void* base, uint32_t sn, uint32_
   p.td = take(p.n_tags_cap);
   p.pa = take(size_t(dn) + 1);
   p.pb = take(size_t(dn) + 1);
-  p.flag = take(4);  // [0] give up, [1] small strides, [2] tags, [3] large hops
+  p.flag = take(8);  // [0] give up, [1] small strides, [2] tags, [3] large hops, [4] LZ4: decoded length
   p.changed = take(64);
   p.val = reinterpret_cast<uint8_t*>(q);
   q += al256(size_t(dn) + 16);
@@ -407,7 +407,199 @@ __global__ void sp_gather_kernel(const ParScratch P, const uint32_t* __restrict_
   if (x >= P.dn || P.flag[0]) return;
   out[x] = P.val[ps[x]];
 }
+
+// ----------------------------------------------------------------- LZ4 blocks, same passes
+// One LZ4 data block (the lz4 block format: sequences of literals then a match, the last one
+// literals only) decoded with the passes above, a "tag" being one sequence.  The exact decoder
+// is decode.hip wave_lz4_decode's sequence loop (oracle/slate_oracle.c lz4_frame, pierrec/lz4
+// v4 decoder): every check it makes on a block is made here on the same values, and any that
+// fails sets flag[0], so the caller hands the payload to it.  `cap` (the frame's block maximum)
+// bounds the decoded length, which the chain pass finds (flag[4]).  A match reaches back at most
+// `prior` bytes before the block: 0 for independent blocks, the frame's bytes decoded so far for
+// linked ones (whose earlier blocks are final in out[-prior, 0) by then).
+//
+// the sequence at p: next sequence, decoded length, literals [lit, lit + ll), match offset;
+// last = the literals end the block (no match).  false when it runs past the block.
+__device__ __forceinline__ bool lz_seq_at(const uint8_t* in, uint32_t sz, uint32_t p, uint32_t* next, uint32_t* len,
+                                          uint32_t* lit, uint32_t* ll_out, uint32_t* mo, bool* last) {
+  uint32_t s = p + 1;
+  const uint32_t tok = in[p];
+  uint32_t ll = tok >> 4;  // sz <= 4 MiB: the 255-runs cannot overflow
+  if (ll == 15) {
+    uint32_t b;
+    do {
+      if (s >= sz) return false;
+      b = in[s++];
+      ll += b;
+    } while (b == 255);
+  }
+  if (ll > sz - s) return false;
+  *lit = s;
+  *ll_out = ll;
+  s += ll;
+  *mo = 0;
+  *last = s == sz;
+  if (s == sz) {
+    *next = sz;
+    *len = ll;
+    return true;
+  }
+  if (sz - s < 2) return false;
+  *mo = uint32_t(in[s]) | uint32_t(in[s + 1]) << 8;
+  s += 2;
+  uint32_t ml = tok & 15;
+  if (ml == 15) {
+    uint32_t b;
+    do {
+      if (s >= sz) return false;
+      b = in[s++];
+      ml += b;
+    } while (b == 255);
+  }
+  *next = s;
+  *len = ll + ml + 4;
+  return true;
+}
+
+__global__ void lz_next_kernel(const uint8_t* __restrict__ in, uint32_t sz, ParScratch P) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.n_pos) return;
+  uint32_t nx = sz + 1, dl = 0;  // ERR
+  if (p >= sz) {
+    nx = p;  // END and ERR stay where they are
+  } else {
+    uint32_t n, l, lt, ll, o;
+    bool last;
+    if (lz_seq_at(in, sz, p, &n, &l, &lt, &ll, &o, &last)) {
+      nx = n;
+      dl = l;
+    }
+  }
+  P.j0[p] = nx;
+  P.d0[p] = dl;
+  P.ja[p] = nx;
+  P.da[p] = dl;
+}
+
+// sp_hops_kernel for a block of unknown decoded length: the chain must end at the block's end
+// with at most P.dn (the cap) bytes decoded; the length goes to flag[4]
+__global__ void lz_hops_kernel(uint32_t sz, ParScratch P, const uint32_t* __restrict__ jk,
+                               const uint32_t* __restrict__ dk) {
+  if (threadIdx.x != 0) return;
+  uint32_t p = 0, i = 0;
+  uint64_t d = 0;
+  bool bad = sz == 0;  // a compressed block holds at least one sequence
+  while (!bad) {
+    if (i >= P.n_big) {
+      bad = true;
+      break;
+    }
+    P.Hp[i] = p;
+    P.Hd[i] = uint32_t(d > 0xFFFFFFFFull ? 0xFFFFFFFFull : d);
+    i++;
+    if (p >= sz) break;
+    d += dk[p];
+    p = jk[p];
+  }
+  if (bad || p != sz || d > P.dn) P.flag[0] = 1;
+  P.flag[3] = i;
+  P.flag[4] = uint32_t(d > P.dn ? 0 : d);
+}
+
+// the exact decoder's per-sequence checks: a match offset of 0 or reaching before the frame's
+// window, and a sequence with a match ending the block (the decoder then wants another token)
+__global__ void lz_check_kernel(const uint8_t* __restrict__ in, uint32_t sz, uint32_t prior, ParScratch P) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (P.flag[0] || t >= P.flag[2]) return;
+  uint32_t n, l, lt, ll, o;
+  bool last;
+  const bool ok = lz_seq_at(in, sz, P.tp[t], &n, &l, &lt, &ll, &o, &last);
+  if (!ok || (!last && (o == 0 || uint64_t(o) > uint64_t(P.td[t]) + ll + prior || n >= sz))) atomicOr(P.flag, 1u);
+}
+
+// decoded byte x: its sequence, then its literal value or the byte its match copies
+__global__ void lz_bytes_kernel(const uint8_t* __restrict__ in, uint32_t sz, ParScratch P,
+                                const uint8_t* __restrict__ out) {
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= P.dn || P.flag[0]) return;
+  uint32_t lo = 0, hi = P.flag[2];  // last sequence with td <= x
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (P.td[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  uint32_t n, l, lt, ll, o;
+  bool last;
+  lz_seq_at(in, sz, P.tp[lo], &n, &l, &lt, &ll, &o, &last);
+  const uint32_t k = x - P.td[lo];
+  if (k < ll) {
+    P.val[x] = in[lt + k];
+    P.pa[x] = x;
+  } else if (x < o) {  // a linked block's match into the blocks before it (checked: o <= x + prior)
+    P.val[x] = out[int64_t(x) - int64_t(o)];
+    P.pa[x] = x;
+  } else {
+    P.pa[x] = x - o;
+  }
+}
 }  // namespace
+
+size_t lz4_par_scratch_bytes(uint32_t sz, uint32_t cap) {
+  size_t bytes = 0;
+  par_carve(nullptr, sz, cap, &bytes);
+  return bytes + 256;
+}
+
+const uint32_t* lz4_par_result(const void* scratch, uint32_t sz, uint32_t cap) {
+  return par_carve(const_cast<void*>(scratch), sz, cap, nullptr).flag;
+}
+
+hipError_t launch_lz4_par_chain(hipStream_t st, const uint8_t* in, uint32_t sz, uint32_t cap, void* scratch) {
+  if (sz >= 0xFFFFFF00u || cap >= 0xFFFFFF00u) return hipErrorInvalidValue;
+  const ParScratch P = par_carve(scratch, sz, cap, nullptr);
+  hipError_t e = hipMemsetAsync(P.flag, 0, 32, st);
+  if (e != hipSuccess) return e;
+  const uint32_t g = (P.n_pos + 255) / 256;
+  lz_next_kernel<<<g, 256, 0, st>>>(in, sz, P);
+  uint32_t* bj[2] = {P.ja, P.jb};
+  uint32_t* bd[2] = {P.da, P.db};
+  uint32_t *js = P.ja, *ds = P.da;
+  int nxt = 1;
+  for (uint32_t k = 0; k < 2 * kLog; k++) {
+    const bool keep = k + 1 == kLog;
+    uint32_t* jt = keep ? P.j1 : bj[nxt];
+    uint32_t* dt = keep ? P.d1 : bd[nxt];
+    sp_jump_kernel<<<g, 256, 0, st>>>(P.n_pos, js, ds, jt, dt);
+    if (!keep) nxt ^= 1;
+    js = jt;
+    ds = dt;
+  }
+  lz_hops_kernel<<<1, 64, 0, st>>>(sz, P, js, ds);
+  return hipGetLastError();
+}
+
+hipError_t launch_lz4_par_bytes(hipStream_t st, const uint8_t* in, uint32_t sz, uint32_t cap, uint32_t dn,
+                                uint32_t prior, void* scratch, uint8_t* out) {
+  if (dn > cap) return hipErrorInvalidValue;
+  ParScratch P = par_carve(scratch, sz, cap, nullptr);  // the chain pass's layout
+  P.dn = dn;
+  sp_subhops_kernel<<<(P.n_big + 63) / 64, 64, 0, st>>>(sz, P);
+  sp_walk_kernel<<<(P.n_hops + 63) / 64, 64, 0, st>>>(sz, P);
+  lz_check_kernel<<<(P.n_tags_cap + 255) / 256, 256, 0, st>>>(in, sz, prior, P);
+  if (dn) {
+    const uint32_t gb = (dn + 255) / 256;
+    lz_bytes_kernel<<<gb, 256, 0, st>>>(in, sz, P, out);
+    uint32_t *ps = P.pa, *pd = P.pb;
+    hipError_t e = hipMemsetAsync(P.changed, 0, 64 * 4, st);
+    if (e != hipSuccess) return e;
+    for (uint32_t r = 0; (1ull << r) < uint64_t(dn); r++) {
+      sp_ptr_kernel<<<gb, 256, 0, st>>>(dn, ps, pd, P.flag, P.changed, r);
+      std::swap(ps, pd);
+    }
+    sp_gather_kernel<<<gb, 256, 0, st>>>(P, ps, out);
+  }
+  return hipGetLastError();
+}
 
 size_t snappy_par_scratch_bytes(uint32_t sn, uint32_t dn) {
   size_t bytes = 0;
