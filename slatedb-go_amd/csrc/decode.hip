@@ -1674,31 +1674,6 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   if (a.n == 0) return hipGetLastError();
   // Snappy: the lane-per-block streaming decoder (any block size); ablation bit 16 (profiling
   // variants only) selects the wave-per-block path instead
-#ifdef SLATE_CRC_SPLIT
-  if (a.codec == SLATE_CODEC_SNAPPY && !(dbg_bits(a) & 16) && !a.raw) {
-    // experiment: the CRC on an auxiliary stream beside the decoder (one per thread and device)
-    static thread_local hipStream_t aux[64];
-    static thread_local hipEvent_t ev[64][2];
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (!aux[dev]) {
-      (void)hipStreamCreateWithFlags(&aux[dev], hipStreamNonBlocking);
-      (void)hipEventCreateWithFlags(&ev[dev][0], hipEventDisableTiming);
-      (void)hipEventCreateWithFlags(&ev[dev][1], hipEventDisableTiming);
-    }
-    (void)hipMemsetAsync(s.zf.count, 0, 2 * sizeof(uint32_t), st);
-    (void)hipEventRecord(ev[dev][0], st);
-    // the decoder's persistent workgroups first; the CRC's small ones fill what they leave
-    hipError_t e = launch_decode_lpb2(st, a, num_cus);
-    if (e != hipSuccess) return e;
-    (void)hipStreamWaitEvent(aux[dev], ev[dev][0], 0);
-    e = launch_block_crc_list(aux[dev], a, s.zf);
-    if (e != hipSuccess) return e;
-    (void)hipEventRecord(ev[dev][1], aux[dev]);
-    (void)hipStreamWaitEvent(st, ev[dev][1], 0);
-    return launch_crc_fix(st, s.zf, a.meta);
-  }
-#endif
   if (a.codec == SLATE_CODEC_SNAPPY && !(dbg_bits(a) & 16)) return launch_decode_lpb2(st, a, num_cus);
   const size_t lds = a.codec == SLATE_CODEC_ZSTD
                          ? kTabBytes + (kDecodeThreads / 64) * size_t(kZsFastInCap + kZsFastOutCap + kZsScratch) + kZsShared

@@ -81,11 +81,6 @@ constexpr uint32_t kVerifyBatch = SLATE_VERIFY_BATCH;
 #define SLATE_ROW_CPOL 16
 #endif
 constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
-#ifdef SLATE_CRC_SPLIT  // experiment: CodecSnappy's CRC32 in a kernel of its own beside this one
-constexpr bool kCrcSplit = true;
-#else
-constexpr bool kCrcSplit = false;
-#endif
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
 #endif
@@ -450,14 +445,10 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
   dbg = SLATE_FORCE_DBG;
 #endif
   // ---- CRC32 of one committed chunk (the two steps without the walker)
-  if (kLz4 || !kCrcSplit) {
-    if (kSlot == 0 || kSlot == 2) {
-      const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
-      if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
-      else crc_chunk(L, in, tab, go);
-    }
-  } else if (kSlot == 0) {
-    L.crc_pos = L.c_commit;  // SLATE_CRC_SPLIT: the CRC runs beside (zstd_fast.hip); no chunk is held for it
+  if (kSlot == 0 || kSlot == 2) {
+    const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
+    if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
+    else crc_chunk(L, in, tab, go);
   }
   const int32_t avail = int32_t(16 * L.c_commit) - int32_t(L.sh);  // committed payload bytes [0, avail)
   bool hole_new = false;
@@ -638,16 +629,15 @@ __device__ __forceinline__ bool lz4_frame_head(Lane& L, const uint32_t* d, uint3
 template <bool kLz4>
 __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr bool kCrcIn = kLz4 || !kCrcSplit;
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
-  if constexpr (kCrcIn) {
+  {
     const uint32_t* src = &g_crc16.t[0][0];
     for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
     __syncthreads();
   }
   const uint32_t* crc_init = g_crc_lt.init;  // used once per round: constant memory
   const uint32_t* crc_tail = g_crc_lt.tail;
-  uint8_t* outs = smem + (kCrcIn ? kTab16Bytes : 0);
+  uint8_t* outs = smem + kTab16Bytes;
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
@@ -855,7 +845,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       const uint32_t stored = __builtin_bswap32(ring_rd8(in, L.sh + L.clen, kIR - 8).x);
       // the register absorbed t zero bytes after the payload: compare against stored * x^(8t)
       const uint32_t t = L.clen ? uint32_t(16 * (L.crc_last + 1)) - (L.sh + L.clen) : 0u;
-      const bool crc_ok = !kCrcIn || gf2_mulmod(~stored, crc_tail[t]) == L.crc;
+      const bool crc_ok = gf2_mulmod(~stored, crc_tail[t]) == L.crc;
       bool dec_ok;
       if constexpr (kLz4) {
         // the data block ended on its last literals, then the EndMark; the content size if any
@@ -1047,8 +1037,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 }
 
 
-size_t lpb2_lds_bytes(bool crc_in) {
-  return (crc_in ? kTab16Bytes : 0) + size_t(kLpb2Threads) * (kOutStride + kInStride);
+size_t lpb2_lds_bytes() {
+  return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
 // CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order
@@ -1199,7 +1189,7 @@ __global__ __launch_bounds__(kLz4PlanThreads) void plan_lz4_lane_kernel(const ui
 
 template <bool kLz4>
 hipError_t launch_lpb(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
-  const size_t lds = lpb2_lds_bytes(kLz4 || !kCrcSplit);
+  const size_t lds = lpb2_lds_bytes();
   const uint32_t waves_needed = (a.n + 63) / 64;
   uint32_t grid = (waves_needed + kLpb2Threads / 64 - 1) / (kLpb2Threads / 64);
   grid = min(grid, uint32_t(num_cus) * uint32_t(163840 / lds));

@@ -158,11 +158,6 @@ hipError_t launch_lz4_par_chain(hipStream_t st, const uint8_t* in, uint32_t sz, 
 hipError_t launch_lz4_par_bytes(hipStream_t st, const uint8_t* in, uint32_t sz, uint32_t cap, uint32_t dn,
                                 uint32_t prior, void* scratch, uint8_t* out);
 
-// SLATE_CRC_SPLIT experiment (CodecSnappy): the blocks' CRC32 lane per block on another stream,
-// mismatches listed in z.list / z.count; launch_crc_fix then writes their status.
-hipError_t launch_block_crc_list(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z);
-hipError_t launch_crc_fix(hipStream_t st, const ZsFastArgs& z, slate_block_meta* meta);
-
 // Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                              const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,

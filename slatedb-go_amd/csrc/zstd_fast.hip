@@ -837,10 +837,6 @@ __global__ __launch_bounds__(kZfSumThreads) void zs_fast_sum_kernel(DecodeArgs a
 // payload's first and last chunk byte by byte, the encoded bytes streamed in 64-byte runs as in
 // phase C.  A mismatch is reported here, as the exact path would (status only), and the block
 // leaves the fast path.
-// kAll (SLATE_CRC_SPLIT, CodecSnappy): every block of at least 6 bytes, on a stream of its own
-// beside the lane-per-block decoder; a mismatch is listed (z.list), and crc_fix_kernel writes the
-// block's status once both kernels are done.
-template <bool kAll>
 __global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
@@ -864,7 +860,7 @@ __global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a
     uint32_t shift = 0, clen = 0, irel = 0, groups = 0;
     bool act = false;
     if (b < a.n) {
-      act = kAll ? a.in_off[b + 1] - a.in_off[b] >= 6 : ((z.rec[b].info >> 16) & kZfFast) != 0;
+      act = (z.rec[b].info >> 16) & kZfFast;
       if (act) {
         const uint64_t s0 = a.in_off[b];
         shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + s0) & 15);
@@ -914,35 +910,13 @@ __global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a
       }
       zs_sync();
     }
-    if constexpr (kAll) {
-      list_append(act && ~crc != stored, b, z.list, z.count);
-    } else if (act && ~crc != stored) {
+    if (act && ~crc != stored) {
       slate_block_meta m{};
       m.status = SLATE_E_BLOCK_CHECKSUM;
       a.meta[b] = m;
       z.rec[b].info = 0;  // not built (B), not summed (C), not handed back
     }
   }
-}
-
-__global__ void crc_fix_kernel(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                               slate_block_meta* __restrict__ meta) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < *count; i += gridDim.x * blockDim.x) {
-    slate_block_meta m{};
-    m.status = SLATE_E_BLOCK_CHECKSUM;  // block.go:83-89 comes first, whatever the decoder found
-    meta[list[i]] = m;
-  }
-}
-
-hipError_t launch_block_crc_list(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z) {
-  if (a.n == 0) return hipGetLastError();
-  zs_fast_crc_kernel<true><<<(a.n + 63) / 64, 64, kTab16Bytes + 64 * 64, st>>>(a, z);
-  return hipGetLastError();
-}
-
-hipError_t launch_crc_fix(hipStream_t st, const ZsFastArgs& z, slate_block_meta* meta) {
-  crc_fix_kernel<<<64, 256, 0, st>>>(z.list, z.count, meta);
-  return hipGetLastError();
 }
 
 hipError_t launch_zstd_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,
@@ -962,7 +936,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   zs_fast_parse_kernel<<<grid_a, kZfParseThreads, lds_a, st>>>(a, z);
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
-  zs_fast_crc_kernel<false><<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
+  zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
   const size_t lds_b = size_t(kZfBuildThreads / 64) * kZfOutLds;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
