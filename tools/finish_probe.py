@@ -20,5 +20,13 @@ with torch.cuda.stream(s):
     ctx.decode_device(1,d_in.data_ptr(),d_off.data_ptr(),n,d_out.data_ptr(),d_oo.data_ptr(),d_meta.data_ptr(),d_rows.data_ptr(),d_rb.data_ptr()); s.synchronize()
 meta=np.frombuffer(d_meta.cpu().numpy().tobytes(),dtype=sc.META_DTYPE)
 f=meta['detail'].astype(np.float64).reshape(-1,64)
+# what grouping similar blocks into rounds could give: rounds formed after sorting by the block's
+# own finish (the bound) or by its encoded length (known before decoding)
+fl=f.reshape(-1)
+clen=np.diff(in_off.astype(np.int64))
+by_fin=np.sort(fl).reshape(-1,64).max(axis=1).mean()
+by_len=fl[np.argsort(clen,kind="stable")].reshape(-1,64).max(axis=1).mean()
 print(json.dumps({"mean_block_finish":float(f.mean()),"mean_round_max":float(f.max(axis=1).mean()),"median_block":float(np.median(f)),
- "p90_block":float(np.percentile(f,90)),"mean_round_min":float(f.min(axis=1).mean())}))
+ "p90_block":float(np.percentile(f,90)),"mean_round_min":float(f.min(axis=1).mean()),
+ "round_max_if_sorted_by_finish":float(by_fin),"round_max_if_sorted_by_len":float(by_len),
+ "corr_len_finish":float(np.corrcoef(clen,fl)[0,1])}))
