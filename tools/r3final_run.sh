@@ -3,7 +3,7 @@
 # default bench line, and the kernel trace of the same bench command (default steps).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-OUT=gpurun_out/r3final
+OUT=${OUT:-gpurun_out/r3final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 $OUT/gpu_tests.log; exit 1; }
