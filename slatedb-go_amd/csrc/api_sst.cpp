@@ -463,7 +463,20 @@ static int lz4_payload_par_run(slate_ctx* ctx, const uint8_t* buf, size_t len, c
                                std::vector<uint8_t>& out, int* bstatus, int* handled) {
   const size_t clen = len - 4;
   const uint32_t nblk = uint32_t(blk.size() / 2);
-  if (uint64_t(nblk) * bmax > (1ull << 31)) return SLATE_OK;  // the output bound (every block at bmax)
+  // a block decodes to at most bmax bytes, and to at most 255 per encoded byte (+ the last
+  // literals): cap[k] bounds block k, their sum the output buffer
+  auto cap_of = [&](uint32_t k) -> uint32_t {
+    const uint32_t bs = blk[2 * k + 1], sz = bs & 0x7FFFFFFFu;
+    return (bs >> 31) ? sz : uint32_t(std::min<uint64_t>(bmax, 256ull * sz + 64));
+  };
+  uint64_t out_bound = 0;
+  uint32_t smax = 0, cmax = 0;
+  for (uint32_t k = 0; k < nblk; k++) {
+    out_bound += cap_of(k);
+    smax = std::max(smax, blk[2 * k + 1] & 0x7FFFFFFFu);
+    cmax = std::max(cmax, cap_of(k));
+  }
+  if (out_bound > (1ull << 31)) return SLATE_OK;
   SLATE_HIP(ctx_bind(ctx));
   hipStream_t st = ctx->stream;
   SLATE_HIP(ctx->d_in.ensure(len + 64));
@@ -477,10 +490,8 @@ static int lz4_payload_par_run(slate_ctx* ctx, const uint8_t* buf, size_t len, c
     *handled = 1;
     return SLATE_OK;
   }
-  uint32_t smax = 0;
-  for (uint32_t k = 0; k < nblk; k++) smax = std::max(smax, blk[2 * k + 1] & 0x7FFFFFFFu);
-  SLATE_HIP(ctx->d_scratch.ensure(lz4_par_scratch_bytes(smax, bmax) + 64));
-  SLATE_HIP(ctx->d_out.ensure(uint64_t(nblk) * bmax + 64));
+  SLATE_HIP(ctx->d_scratch.ensure(lz4_par_scratch_bytes(smax, cmax) + 64));
+  SLATE_HIP(ctx->d_out.ensure(out_bound + 64));
   SLATE_HIP(ctx->e_k.ensure(64));
   uint8_t* d_in = ctx->d_in.as<uint8_t>();
   uint8_t* d_out = ctx->d_out.as<uint8_t>();
@@ -494,13 +505,14 @@ static int lz4_payload_par_run(slate_ctx* ctx, const uint8_t* buf, size_t len, c
       continue;
     }
     uint32_t res[5] = {1, 0, 0, 0, 0};
-    const uint32_t* d_res = lz4_par_result(scratch, sz, bmax);
-    SLATE_HIP(launch_lz4_par_chain(st, d_in + off, sz, bmax, scratch));
+    const uint32_t cap = cap_of(k);  // = bmax whenever a block could reach it
+    const uint32_t* d_res = lz4_par_result(scratch, sz, cap);
+    SLATE_HIP(launch_lz4_par_chain(st, d_in + off, sz, cap, scratch));
     SLATE_HIP(hipMemcpyAsync(res, d_res, sizeof(res), hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
     if (res[0]) return SLATE_OK;  // the serial path decodes (and reports) it
     const uint32_t dn = res[4];
-    SLATE_HIP(launch_lz4_par_bytes(st, d_in + off, sz, bmax, dn, indep ? 0u : uint32_t(total), scratch,
+    SLATE_HIP(launch_lz4_par_bytes(st, d_in + off, sz, cap, dn, indep ? 0u : uint32_t(total), scratch,
                                    d_out + total));
     SLATE_HIP(hipMemcpyAsync(res, d_res, 4, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
