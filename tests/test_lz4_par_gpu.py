@@ -138,3 +138,19 @@ def test_lz4_large_blocks_generated_and_damaged(ctx):
             for _ in range(rng.randint(1, 3)):
                 body[rng.randrange(11, len(body) - 8)] ^= 1 << rng.randrange(8)
         _check_filter(ctx, sstgen.crc(bytes(body)))
+
+
+def test_lz4_large_blocks_cross_block_matches(ctx):
+    """Linked blocks whose matches reach into the block before decode like the oracle; the same
+    frame declared independent (FLG bit 5 set, header checksum redone) has matches reaching before
+    their block, which the parallel passes must reject so the exact path reports the corruption."""
+    rng = random.Random(9)
+    unit = np.random.default_rng(9).integers(0, 256, 30_000, dtype=np.uint8).tobytes()
+    raw = b"".join(unit[i * 7:] + unit[: i * 7] for i in range(12))
+    f = lz4gen.frame(raw, bsid=5, indep=False, block_split=100_000, content_checksum=True, rng=rng)
+    assert not (f[4] & 0x20) and len(_block_sizes(f)[1]) >= 3
+    assert _check_filter(ctx, sstgen.crc(f)) == 0
+    g = bytearray(f)
+    g[4] |= 0x20
+    g[6] = (lz4gen.xxh32(bytes(g[4:6])) >> 8) & 0xFF
+    assert _check_filter(ctx, sstgen.crc(bytes(g))) != 0
