@@ -582,23 +582,36 @@ __device__ inline void zfill(ZBits& z, int lane) {  // as many whole bytes as fi
   }
 }
 // -1: out of input, -2: no code matches
-__device__ inline int zsym(ZBits& z, const ZHuff* h, int lane) {
+// A table's per-length values, lane l holding length l's (1 <= l < 16): read from LDS once per
+// table instead of once per symbol.
+struct ZLane {
+  const ZHuff* h;
+  uint32_t first, count, index, max;
+};
+__device__ inline ZLane zlane(const ZHuff* h, int lane) {
+  const uint32_t l = uint32_t(lane);
+  return ZLane{h, l < 16 ? h->first[l] : 0u, l < 16 ? h->count[l] : 0u, l < 16 ? h->index[l] : 0u,
+               uint32_t(__builtin_amdgcn_readfirstlane(h->max))};
+}
+// The next symbol: lanes 1..15 test the code of their length at once, the shortest match wins
+// (a bit-serial canonical decoder's result); -1: the input ends first, -2: no code matches.
+__device__ inline int zsym(ZBits& z, const ZLane& t, int lane) {
   zfill(z, lane);
   const uint32_t l = uint32_t(lane);
-  const uint32_t mx = h->max;
+  const uint32_t mx = t.max;
   const uint32_t peek = uint32_t(z.bits) & 0x7FFFu;
   const bool test = l >= 1 && l <= mx && l <= z.nb && l < 16;
   const uint32_t code = (l >= 1 && l < 16) ? (__builtin_bitreverse32(peek) >> (32 - l)) : 0u;
-  const uint32_t fi = l < 16 ? h->first[l] : 0u, ct = l < 16 ? h->count[l] : 0u;
-  const bool hit = test && code - fi < ct;
+  const bool hit = test && code - t.first < t.count;
   const uint64_t m = __ballot(hit);
   if (m == 0) return (z.nb < mx) ? -1 : -2;
   const int L = __builtin_ctzll(m);
-  const uint32_t at = __builtin_amdgcn_readlane((l < 16 ? h->index[l] : 0u) + code - fi, L);
+  const uint32_t at = __builtin_amdgcn_readlane(t.index + code - t.first, L);
   z.bits >>= L;
   z.nb -= uint32_t(L);
-  return int(h->sym[at]);
+  return int(t.h->sym[at]);
 }
+__device__ inline int zsym(ZBits& z, const ZHuff* h, int lane) { return zsym(z, zlane(h, lane), lane); }
 __device__ inline bool zneed(ZBits& z, uint32_t k, int lane) {
   zfill(z, lane);
   return z.nb >= k;
@@ -734,8 +747,9 @@ __device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_
       hl = &zs->lit;
       hd = &zs->dist;
     }
+    const ZLane tl = zlane(hl, lane), td = zlane(hd, lane);
     for (;;) {
-      int sym = zsym(z, hl, lane);
+      int sym = zsym(z, tl, lane);
       if (sym == -1) return SLATE_E_UNEXPECTED_EOF;
       if (sym < 0) return SLATE_E_FLATE_CORRUPT;
       if (sym < 256) {
@@ -751,7 +765,7 @@ __device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_
       const uint32_t le = kZLenExtra[sym];
       if (!zneed(z, le, lane)) return SLATE_E_UNEXPECTED_EOF;
       const uint32_t len = kZLenBase[sym] + ztake(z, le);
-      const int ds = zsym(z, hd, lane);
+      const int ds = zsym(z, td, lane);
       if (ds == -1) return SLATE_E_UNEXPECTED_EOF;
       if (ds < 0 || ds >= 30) return SLATE_E_FLATE_CORRUPT;
       const uint32_t de = kZDistExtra[ds];
