@@ -1676,26 +1676,43 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   if (len < 2) return SLATE_E_FILTER_TOO_SMALL;
   if (len < 4) return SLATE_E_FILTER_PANIC;
   size_t ci = len - 4;
-  uint32_t crc = 0;
-  int st = ctx_crc32_host_buffer(ctx, buf, ci, &crc);
-  if (st) return st;
-  if (crc != ld_be32(buf + ci)) return SLATE_E_FILTER_CHECKSUM;
-  if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
   std::vector<uint8_t> dec;
   const uint8_t* p = buf;
   size_t pn = ci;
-  if (codec != SLATE_CODEC_NONE) {
-    int bst = 0;
-    st = ctx_payload_decode_buffer(ctx, codec, buf, len, dec, &bst);
-    if (st) return st;
-    if (bst) return bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_FILTER_CHECKSUM : bst;
+  const bool cached = codec != SLATE_CODEC_NONE && codec == ctx->bloom_codec && len == ctx->bloom_in.size() &&
+                      memcmp(buf, ctx->bloom_in.data(), len) == 0;
+  if (cached) {  // the same bytes decoded (and checked) by the call that reported SLATE_E_CAPACITY
+    dec.swap(ctx->bloom_dec);
+    ctx->bloom_in.clear();
+    ctx->bloom_codec = -1;
     p = dec.data();
     pn = dec.size();
+  } else {
+    uint32_t crc = 0;
+    int st = ctx_crc32_host_buffer(ctx, buf, ci, &crc);
+    if (st) return st;
+    if (crc != ld_be32(buf + ci)) return SLATE_E_FILTER_CHECKSUM;
+    if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
+    if (codec != SLATE_CODEC_NONE) {
+      int bst = 0;
+      st = ctx_payload_decode_buffer(ctx, codec, buf, len, dec, &bst);
+      if (st) return st;
+      if (bst) return bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_FILTER_CHECKSUM : bst;
+      p = dec.data();
+      pn = dec.size();
+    }
   }
   if (pn < 2) return SLATE_E_FILTER_PANIC;
   if (num_probes) *num_probes = ld_be16(p);
   if (bits_len) *bits_len = pn - 2;
-  if (pn - 2 > bits_cap || (!bits && pn > 2)) return SLATE_E_CAPACITY;
+  if (pn - 2 > bits_cap || (!bits && pn > 2)) {
+    if (codec != SLATE_CODEC_NONE) {  // keep it for the retry with a buffer of *bits_len bytes
+      ctx->bloom_in.assign(buf, buf + len);
+      ctx->bloom_dec.swap(dec);
+      ctx->bloom_codec = codec;
+    }
+    return SLATE_E_CAPACITY;
+  }
   if (pn > 2) memcpy(bits, p + 2, pn - 2);
   return SLATE_OK;
 }
