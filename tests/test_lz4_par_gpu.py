@@ -154,3 +154,37 @@ def test_lz4_large_blocks_cross_block_matches(ctx):
     g[4] |= 0x20
     g[6] = (lz4gen.xxh32(bytes(g[4:6])) >> 8) & 0xFF
     assert _check_filter(ctx, sstgen.crc(bytes(g))) != 0
+
+
+def test_bloom_decode_capacity_retry(sc, ctx):
+    """slate_bloom_decode keeps a compressed filter that did not fit the caller's buffer for the retry
+    with the reported length: the retry returns the same bytes as the oracle, and a different
+    payload of the same length (or another codec) is decoded afresh, never served from that copy."""
+    import ctypes as C
+    rng = np.random.default_rng(5)
+    raw1 = b"\x00\x06" + rng.integers(0, 4, 300_000, dtype=np.uint8).tobytes()
+    raw2 = b"\x00\x07" + rng.integers(0, 4, 300_000, dtype=np.uint8).tobytes()
+    f1, f2 = _liblz4_frame(raw1), _liblz4_frame(raw2)
+    if len(f2) != len(f1):  # same length, different bytes: pad the shorter frame's source
+        f2 = f1[:-5] + bytes([f1[-5] ^ 1]) + f1[-4:]  # a damaged copy (CRC now wrong)
+    L = sc.lib()
+
+    def call(buf: bytes, cap: int, codec: int = ob.LZ4):
+        b = np.frombuffer(buf, np.uint8)
+        out = np.zeros(max(cap, 1), np.uint8)
+        k, n = C.c_uint16(), C.c_size_t()
+        st = L.slate_bloom_decode(ctx._h, sc._ptr(b), len(buf), codec, C.byref(k), sc._ptr(out), cap, C.byref(n))
+        return st, k.value, n.value, out[: n.value].tobytes()
+
+    st, k, n, _ = call(f1, 16)
+    assert st == sc.E_CAPACITY and n == len(raw1) - 2
+    o2 = ob.bloom_decode(f2, ob.LZ4, cap=1 << 22)
+    st2, k2, n2, bits2 = call(f2, n + 64)  # not the kept filter
+    assert st2 == o2[0] and (st2 != 0 or (k2, bits2) == (o2[1], o2[2]))
+    st, k, n, _ = call(f1, 16)
+    assert st == sc.E_CAPACITY
+    assert call(f1, n + 64, ob.ZSTD)[0] != 0  # same bytes, another codec: decoded (and rejected) afresh
+    st, k, n, _ = call(f1, 16)
+    st, k, n1, bits = call(f1, n)  # the retry
+    o1 = ob.bloom_decode(f1, ob.LZ4, cap=1 << 22)
+    assert st == o1[0] == 0 and (k, bits) == (o1[1], o1[2])
