@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cache", default="", help="configs[4]: directory to reuse the generated workload from")
     p.add_argument("--no-host-io", action="store_true")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the extra legs (codec_none, configs4_zstd, configs2_encode; N=1 only)")
+    p.add_argument("--extra-steps", type=int, default=10, help="timed steps of each extra leg")
     p.add_argument("--allow-variant", action="store_true", help="profiling only: accept SLATE_LIB_VARIANT")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_decode_latest.json"))
     return p.parse_args()
@@ -115,12 +118,13 @@ def main():
     if args.codec == "zstd":  # configs[4] "mixed": its own sequential generator, one shard per rank
         n = args.blocks
         cache = os.path.join(args.cache, f"wl_zstd_{n}_{SEED + rank}") if args.cache else ""
+        dec_ref = None
         if cache and os.path.exists(cache + "_blob.npy"):
             blob, in_off = (np.load(cache + f"_{k}.npy") for k in ("blob", "in_off"))
         else:
             dec, dec_off = wl.mixed_blocks(n, seed=SEED + rank)
             blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=threads)
-            del dec, dec_off
+            dec_ref = (dec, dec_off)
             if cache:
                 os.makedirs(args.cache, exist_ok=True)
                 np.save(cache + "_blob.npy", blob)
@@ -148,62 +152,27 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
-    d_in = torch.from_numpy(blob).to(device)
-    d_in_off = torch.from_numpy(in_off.view(np.int64)).to(device)
-    d_out_off = torch.empty(n + 1, dtype=torch.int64, device=device)
-    d_row_base = torch.empty(n + 1, dtype=torch.int64, device=device)
-    d_scratch = torch.empty(sc.decode_scratch_bytes(n) + 64, dtype=torch.uint8, device=device)
-    ctx.decode_plan_device(codec, d_in.data_ptr(), d_in_off.data_ptr(), n, d_out_off.data_ptr(),
-                           d_row_base.data_ptr(), d_scratch.data_ptr())
-    torch.cuda.synchronize(device)
-    total_out = int(d_out_off[n].item())
-    total_rows = int(d_row_base[n].item())
-    d_out = torch.empty(total_out + 16, dtype=torch.uint8, device=device)
-    d_meta = torch.empty(n * 16, dtype=torch.uint8, device=device)
-    d_rows = torch.empty(max(total_rows, 1) * 16, dtype=torch.uint8, device=device)
-
-    def step(ev=None):
-        ctx.decode_plan_device(codec, d_in.data_ptr(), d_in_off.data_ptr(), n, d_out_off.data_ptr(),
-                               d_row_base.data_ptr(), d_scratch.data_ptr())
-        if ev is not None:
-            ev[0].record(stream)
-        ctx.decode_device(codec, d_in.data_ptr(), d_in_off.data_ptr(), n, d_out.data_ptr(), d_out_off.data_ptr(),
-                          d_meta.data_ptr(), d_rows.data_ptr(), d_row_base.data_ptr())
-        if ev is not None:
-            ev[1].record(stream)
+    # Every device buffer is library-owned HBM (slate_devbuf, include/slatecodec.h): the path timed
+    # here is the one a cgo caller reaches (slate_devbuf_ptr -> the *_device entry points).
+    leg = DecodeLeg(sc, ctx, codec, blob, in_off)
+    n = leg.n
 
     for _ in range(args.warmup):
-        step()
+        leg.step()
     torch.cuda.synchronize(device)
 
     # ---- verify, outside the timed region: every block's status; decoded bytes, meta and row
     # descriptors against the generator for every block (configs1) or evenly spread chunks (configs3)
-    meta = np.frombuffer(d_meta.cpu().numpy().tobytes(), dtype=sc.META_DTYPE)
+    meta = leg.d_meta.download().view(sc.META_DTYPE)
     assert (meta["status"] == 0).all(), np.unique(meta["status"], return_counts=True)
     dec_bytes = int(np.sum(meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2))
     n_rows = int(meta["n_rows"].astype(np.int64).sum())
     verify = args.verify or ("all" if args.workload == "configs1" else "sample")
     verified = 0
     if shard is not None and verify != "none":
-        out_off_h = d_out_off.cpu().numpy().view(np.uint64)
-        rb_h = d_row_base.cpu().numpy().view(np.uint64)
-        meta_u8 = d_meta.cpu().numpy()
-        chunk = 131072
-        starts = list(range(0, n, chunk))
-        if verify == "sample" and len(starts) > 16:
-            starts = [starts[int(j * (len(starts) - 1) / 15)] for j in range(16)]
-        for k0 in starts:
-            k1 = min(n, k0 + chunk)
-            oa, ob_ = int(out_off_h[k0]), int(out_off_h[k1])
-            ra, rb_ = int(rb_h[k0]), int(rb_h[k1])
-            out_c = d_out[oa:ob_].cpu().numpy()
-            rows_c = d_rows[16 * ra:16 * rb_].cpu().numpy()
-            bad = wl.verify_set(shard[0] + k0 * shard[1], shard[1], k1 - k0, out_c, out_off_h[k0:k1 + 1] - oa,
-                                rows_c, rb_h[k0:k1 + 1] - ra, meta_u8[16 * k0:16 * k1], seed=SEED, half=half,
-                                threads=threads)
-            assert bad == 0, f"{bad} blocks of [{k0}, {k1}) differ from the generator"
-            verified += k1 - k0
-
+        verified = leg.verify_against_generator(wl, shard, verify, meta, threads, half)
+    elif args.codec == "zstd" and verify != "none":
+        verified = leg.verify_against_decoded(dec_ref, meta)
     # ---- timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -211,7 +180,7 @@ def main():
     torch.cuda.synchronize(device)
     t_start = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        leg.step(evs[k], stream)
     torch.cuda.synchronize(device)
     t_end = time.perf_counter()
     if dist:
@@ -225,20 +194,13 @@ def main():
     value = job_dec_bytes * args.steps / elapsed / 2**30
 
     # roofline of the dominant kernel: algorithmic bytes per launch / its event time
-    alg_read = enc_bytes + 8 * (n + 1) * 3  # encoded blocks incl. CRC + in_off/out_off/row_base
-    alg_write = dec_bytes + 16 * n_rows + 16 * n  # decoded bytes + row descriptors + block meta
-    alg = alg_read + alg_write
-    achieved = alg / (kern_ms * 1e-3) / 1e9
+    roofline = decode_roofline(enc_bytes, n, dec_bytes, n_rows, kern_ms)
     traffic, traffic_src = pmc_traffic(args.pmc_json, n, args.codec)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": {"snappy": "decode_lpb2_kernel", "lz4": "decode_lpb2_kernel<true> (+ decode_list_kernel<0>)",
-                           "zstd": "zstd decode: zs_fast_parse/crc/build/sum + decode_list_kernel<2> "
-                                   "(HIP events around the whole decode)"}.get(args.codec, "decode_fast_kernel<0>"),
-                "kernel_ms": round(kern_ms, 4),
-                "alg_bytes_per_launch": alg, "alg_read_bytes": alg_read, "alg_write_bytes": alg_write,
-                "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                "traffic_source": traffic_src}
+    roofline["traffic"] = traffic
+    roofline["traffic_source"] = traffic_src
+    roofline["kernel"] = {"snappy": "decode_lpb2_kernel", "lz4": "decode_lpb2_kernel<true> (+ decode_list_kernel<0>)",
+                          "zstd": "zstd decode: zs_fast_parse/crc/build/sum + decode_list_kernel<2> "
+                                  "(HIP events around the whole decode)"}.get(args.codec, "decode_fast_kernel<0>")
 
     if args.codec == "zstd":
         workload = (f"configs[4] mixed: {n} x 4 KiB Zstd blocks per GPU, 1 KiB values, skewed key prefixes, "
@@ -280,6 +242,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_host_io and shard is not None:
         result["host_io"] = host_io_rate(sc, ctx, codec, blob, in_off)
 
+    if rank == 0 and world == 1 and not args.no_extras and args.codec == "snappy" and args.workload == "configs1":
+        del leg  # the extra legs get the HBM back
+        result["codec_none"] = codec_none_leg(sc, ctx, stream, wl, args, threads)
+        result["configs4_zstd"] = zstd_leg(sc, ctx, stream, wl, args, threads)
+        result["configs2_encode"] = encode_leg(sc, ctx, args)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(codec, blob, in_off, args.cpu_seconds)
 
@@ -289,6 +257,220 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+class DecodeLeg:
+    """One device-resident decode workload on library-owned HBM (slate_devbuf): inputs uploaded
+    once, a step = plan + decode (slate_block_decode_plan_device + slate_block_decode_device)."""
+
+    def __init__(self, sc, ctx, codec, blob, in_off):
+        self.sc, self.ctx, self.codec = sc, ctx, codec
+        self.n = n = len(in_off) - 1
+        self.d_in = sc.devbuf_from(ctx, blob)
+        self.d_in_off = sc.devbuf_from(ctx, np.ascontiguousarray(in_off, np.uint64))
+        self.d_out_off, self.d_row_base = sc.DevBuf(ctx, 8 * (n + 1)), sc.DevBuf(ctx, 8 * (n + 1))
+        self.d_scratch = sc.DevBuf(ctx, sc.decode_scratch_bytes(n) + 64)
+        ctx.decode_plan_device(codec, self.d_in.ptr, self.d_in_off.ptr, n, self.d_out_off.ptr, self.d_row_base.ptr,
+                               self.d_scratch.ptr)
+        self.total_out, self.total_rows = self.d_out_off.u64(n), self.d_row_base.u64(n)
+        self.d_out = sc.DevBuf(ctx, self.total_out + 16)
+        self.d_meta = sc.DevBuf(ctx, 16 * n)
+        self.d_rows = sc.DevBuf(ctx, 16 * max(self.total_rows, 1))
+
+    def step(self, ev=None, stream=None):
+        c = self.ctx
+        c.decode_plan_device(self.codec, self.d_in.ptr, self.d_in_off.ptr, self.n, self.d_out_off.ptr,
+                             self.d_row_base.ptr, self.d_scratch.ptr)
+        if ev is not None:
+            ev[0].record(stream)
+        c.decode_device(self.codec, self.d_in.ptr, self.d_in_off.ptr, self.n, self.d_out.ptr, self.d_out_off.ptr,
+                        self.d_meta.ptr, self.d_rows.ptr, self.d_row_base.ptr)
+        if ev is not None:
+            ev[1].record(stream)
+
+    def timed(self, torch, stream, steps, warmup):
+        """Mean decode-kernel ms (HIP events on the context's stream) and wall ms per step."""
+        for _ in range(warmup):
+            self.step()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(steps):
+            self.step(evs[k], stream)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t) * 1e3 / steps
+        return float(np.mean([a.elapsed_time(b) for a, b in evs])), wall
+
+    def verify_against_generator(self, wl, shard, verify, meta, threads, half):
+        """Decoded bytes, meta and rows of every block (or 16 evenly spread chunks) against the
+        per-block generator (tools/benchgen.c): returns the blocks verified."""
+        n = self.n
+        out_off_h = self.d_out_off.download(dtype=np.uint64)
+        rb_h = self.d_row_base.download(dtype=np.uint64)
+        meta_u8 = meta.view(np.uint8)
+        chunk = 131072
+        starts = list(range(0, n, chunk))
+        if verify == "sample" and len(starts) > 16:
+            starts = [starts[int(j * (len(starts) - 1) / 15)] for j in range(16)]
+        verified = 0
+        for k0 in starts:
+            k1 = min(n, k0 + chunk)
+            oa, ob_ = int(out_off_h[k0]), int(out_off_h[k1])
+            ra, rb_ = int(rb_h[k0]), int(rb_h[k1])
+            out_c = self.d_out.download(ob_ - oa, oa)
+            rows_c = self.d_rows.download(16 * (rb_ - ra), 16 * ra)
+            bad = wl.verify_set(shard[0] + k0 * shard[1], shard[1], k1 - k0, out_c, out_off_h[k0:k1 + 1] - oa,
+                                rows_c, rb_h[k0:k1 + 1] - ra, meta_u8[16 * k0:16 * k1], seed=SEED, half=half,
+                                threads=threads)
+            assert bad == 0, f"{bad} blocks of [{k0}, {k1}) differ from the generator"
+            verified += k1 - k0
+        return verified
+
+    def verify_against_decoded(self, dec_ref, meta):
+        """configs[4]: every block's decoded bytes against the blocks before encoding."""
+        if dec_ref is None:
+            return 0
+        from tools import workload as wl
+        dec, dec_off = dec_ref
+        dl = (meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2)
+        assert np.array_equal(dl, np.diff(dec_off.astype(np.int64))), "decoded lengths differ"
+        bad = wl.compare_blocks(self.d_out.download(), self.d_out_off.download(dtype=np.uint64), dec, dec_off)
+        assert bad == 0, f"{bad} blocks differ from the blocks before encoding"
+        return self.n
+
+    def free(self):
+        for b in (self.d_in, self.d_in_off, self.d_out_off, self.d_row_base, self.d_scratch, self.d_out, self.d_meta,
+                  self.d_rows):
+            b.free()
+
+
+def decode_roofline(enc_bytes, n, dec_bytes, n_rows, kern_ms):
+    """SURVEY 8d algorithmic bytes of one decode launch: R = encoded blocks incl. CRC + in_off /
+    out_off / row_base reads, W = decoded bytes + 16 B per row descriptor + 16 B per block meta."""
+    alg_read = enc_bytes + 8 * (n + 1) * 3
+    alg_write = dec_bytes + 16 * n_rows + 16 * n
+    alg = alg_read + alg_write
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel_ms": round(kern_ms, 4),
+            "alg_bytes_per_launch": alg, "alg_read_bytes": alg_read, "alg_write_bytes": alg_write,
+            "read_only_frac": round(alg_read / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+def _decode_leg_result(sc, leg, torch, stream, steps, warmup, enc_bytes):
+    kern_ms, wall_ms = leg.timed(torch, stream, steps, warmup)
+    meta = leg.d_meta.download().view(sc.META_DTYPE)
+    assert (meta["status"] == 0).all(), np.unique(meta["status"], return_counts=True)
+    dec_bytes = int(np.sum(meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2))
+    n_rows = int(meta["n_rows"].astype(np.int64).sum())
+    return meta, {"value": round(dec_bytes / (wall_ms * 1e-3) / 2**30, 2), "unit": "GiB/s",
+                  "ms_per_step": round(wall_ms, 4), "steps": steps,
+                  "roofline": decode_roofline(enc_bytes, leg.n, dec_bytes, n_rows, kern_ms),
+                  "blocks": leg.n, "decoded_bytes": dec_bytes, "encoded_bytes": enc_bytes, "rows": n_rows}
+
+
+def codec_none_leg(sc, ctx, stream, wl, args, threads):
+    """CodecNone decode (the DB's default codec, slatedb/config/config.go:85) of the configs[1] keys
+    and values: 1 M blocks, every block verified against the generator outside the timed region."""
+    import torch
+    n = args.blocks
+    blob, in_off = wl.block_set(sc.NONE, 0, 1, n, seed=SEED, half=True, threads=threads)
+    leg = DecodeLeg(sc, ctx, sc.NONE, blob, in_off)
+    meta, res = _decode_leg_result(sc, leg, torch, stream, args.extra_steps, 2, int(in_off[-1]))
+    res["roofline"]["kernel"] = "decode_fast_kernel<0> (+ plan)"
+    res["verified"] = leg.verify_against_generator(wl, (0, 1, n), "all", meta, threads, True)
+    res["workload"] = f"{n} x 4 KiB CodecNone blocks (configs[1] keys and V-half values), device-resident decode"
+    leg.free()
+    return res
+
+
+def zstd_leg(sc, ctx, stream, wl, args, threads):
+    """BASELINE configs[4]: Zstd 4 KiB blocks (libzstd level 3 + checksum frames), 1 KiB values,
+    Zipf-prefixed 8-256 B keys; every block's decoded bytes checked against the blocks before
+    encoding, and the first 4096 blocks' metas and rows against the oracle."""
+    import torch
+    from oracle import binding as ob
+    n = args.blocks
+    t0 = time.time()
+    dec, dec_off = wl.mixed_blocks(n, seed=SEED)
+    blob, in_off = wl.encode_blocks(sc.ZSTD, dec, dec_off, threads=threads)
+    gen_s = time.time() - t0
+    leg = DecodeLeg(sc, ctx, sc.ZSTD, blob, in_off)
+    meta, res = _decode_leg_result(sc, leg, torch, stream, args.extra_steps, 2, int(in_off[-1]))
+    res["roofline"]["kernel"] = "zs_fast_parse/crc/build/sum + decode_list_kernel<2> (+ plan)"
+    res["verified"] = leg.verify_against_decoded((dec, dec_off), meta)
+    m = min(4096, n)
+    sub_off = np.ascontiguousarray(in_off[:m + 1], np.uint64)
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(ob.ZSTD, blob[:int(sub_off[m])], sub_off, nthreads=threads)
+    assert o_meta.tobytes() == meta[:m].tobytes(), "configs4 metas differ from the oracle"
+    rows = leg.d_rows.download(16 * int(o_rb[m])).view(sc.ROW_DTYPE)
+    used = np.concatenate([np.arange(int(o_rb[i]), int(o_rb[i]) + int(o_meta["n_rows"][i])) for i in range(m)])
+    assert rows[used].tobytes() == o_rows[used].tobytes(), "configs4 rows differ from the oracle"
+    res["oracle_checked_blocks"] = m
+    res["gen_seconds"] = round(gen_s, 1)
+    res["workload"] = f"configs[4] mixed: {n} x 4 KiB Zstd blocks, 1 KiB values, skewed key prefixes"
+    leg.free()
+    return res
+
+
+def encode_leg(sc, ctx, args):
+    """BASELINE configs[2]: 10 M x 100 B KV through the GPU sstable.Builder from HBM-resident KVs
+    (slate_sst_builder_add_batch_device, compaction's re-encode path; flush's host-array path too),
+    SST bytes compared with the oracle's C restatement of the Go builder at full size once.
+    roofline: SURVEY 8d encode bytes (R = 100 B KV + 16 B descriptor per KV, W = encoded SST bytes +
+    6 bloom-bit byte RMWs of 2 B per key) over the device-input build's wall time (kernels plus the
+    D2H of the finished SST: an upper bound on the kernel time, so the fraction is a lower bound)."""
+    from oracle import binding as ob
+    from tools import bench_encode as be
+    n = 10_000_000
+    keys, key_off, vals, val_off = be.kv_arrays(n)
+    d_keys, d_vals = sc.devbuf_from(ctx, keys), sc.devbuf_from(ctx, vals)
+    d_ko, d_vo = sc.devbuf_from(ctx, key_off), sc.devbuf_from(ctx, val_off)
+    sink = np.empty(int(n * 110), np.uint8)
+    sink.fill(0)
+    res = {}
+    for codec, name in ((sc.NONE, "none"), (sc.SNAPPY, "snappy")):
+        times, enc = [], None
+        for k in range(4):  # the first warms the context
+            t0 = time.perf_counter()
+            b = sc.SstBuilder(ctx, 4096, 0, 10, codec)
+            assert b.add_batch_device(d_keys.ptr, d_ko.ptr, d_vals.ptr, d_vo.ptr, n) == 0
+            t = b.build()
+            t1 = time.perf_counter()
+            enc = t.encode_array(sink)
+            if k:
+                times.append(t1 - t0)
+            del t, b
+        th = []
+        for k in range(3):  # flush's path: host arrays in (staging + PCIe included)
+            t0 = time.perf_counter()
+            b = sc.SstBuilder(ctx, 4096, 0, 10, codec)
+            assert b.add_batch(keys, key_off, vals, val_off) == 0
+            t = b.build()
+            host = t.encode_array()
+            th.append(time.perf_counter() - t0)
+            del t, b
+        t0 = time.perf_counter()
+        o = ob.SstBuilder(4096, 0, 10, ob.NONE if codec == sc.NONE else ob.SNAPPY)
+        assert o.add_batch(keys, key_off, vals, val_off) == 0
+        assert o.build() == 0
+        ref = o.encode_table()
+        oracle_s = time.perf_counter() - t0
+        exact = ref == enc.tobytes() and ref == host.tobytes()
+        assert exact, f"configs[2] {name}: SST bytes differ from the oracle"
+        s_dev = float(np.median(times))
+        alg = n * (100 + 16) + len(ref) + n * 6 * 2
+        res[name] = {"value": round(n / s_dev, 1), "unit": "KV/s", "s_device_input": round(s_dev, 4),
+                     "s_host_input": round(float(np.median(th)), 4), "sst_bytes": len(ref), "bit_exact": exact,
+                     "roofline": {"bound": "hbm", "achieved": round(alg / s_dev / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                                  "unit": "GB/s", "frac": round(alg / s_dev / 1e9 / HBM_PEAK_GBPS, 5),
+                                  "alg_bytes": alg, "time": "device-input build wall (kernels + D2H of the SST)"},
+                     "cpu_baseline": {"value": round(n / oracle_s, 1), "unit": "KV/s", "cores": 1, "kind": "port",
+                                      "sample": "the same 10 M KV through oracle/slate_oracle.c's sstable.Builder"}}
+    for x in (d_keys, d_vals, d_ko, d_vo):
+        x.free()
+    res["workload"] = "configs[2]: 10 M x 100 B KV (keys k%015d, V-half values) -> SST blocks + bloom, BlockSize 4096"
+    return res
 
 
 def measured_copy_gbps(device, nbytes: int = 2 << 30, reps: int = 10) -> float:
@@ -377,7 +559,10 @@ def host_io_rate(sc, ctx, codec, blob, in_off, max_blocks=262144):
     dec = int(np.sum(meta["data_len"].astype(np.int64) + 2 * meta["n_rows"].astype(np.int64) + 2))
     res = {"GiBps_decoded": round(dec / el / 2**30, 2), "blocks": n,
            "h2d_GBps": round(int(sub_off[n]) / el / 1e9, 2),
-           "d2h_GBps": round((int(out_off[n]) + 16 * int(row_base[n]) + 16 * n) / el / 1e9, 2),
+           # what crosses the link back: decoded bytes, the rows densely (slate_row, 16 B, of decoded
+           # blocks only: rows_pack) and the metas
+           "d2h_GBps": round((dec + 16 * int(np.sum(np.where(meta["status"] == 0, meta["n_rows"], 0).astype(np.int64)))
+                              + 16 * n) / el / 1e9, 2),
            "path": "slate_block_decode_batch: pageable caller buffers, page-locked staging, 2 stream lanes"}
     ctx3 = sc.Context(ctx.device)
     for _ in range(2):  # the same caller buffers; the first call warms the second context

@@ -60,7 +60,7 @@ enum slate_status {
   SLATE_E_INVALID_CODEC = 10,       /* "corrupted; invalid compression codec" */
   SLATE_E_SNAPPY_CORRUPT = 11,      /* "snappy: corrupt input" */
   SLATE_E_SNAPPY_TOO_LARGE = 12,    /* "snappy: decoded block is too large" */
-  SLATE_E_CODEC_UNSUPPORTED = 13,   /* codec not implemented by this backend (encode of Zlib/LZ4/Zstd) */
+  SLATE_E_CODEC_UNSUPPORTED = 13,   /* reserved: every codec decodes and encodes, no entry point returns it */
   /* CodecLz4 (compression.go:143-144, github.com/pierrec/lz4/v4 v4.1.21 errors; strings unpinned) */
   SLATE_E_LZ4_MAGIC = 14,           /* "lz4: bad magic number" */
   SLATE_E_LZ4_HEADER_CHECKSUM = 15, /* "lz4: invalid header checksum" */
@@ -162,6 +162,26 @@ typedef struct slate_seek {
   uint16_t first_len;
 } slate_seek;
 
+/* One warning NewIteratorAtKey added to its types.ErrWarn, in the order Go adds them, so a shim can
+ * rebuild the ErrWarn text (err: a SLATE_E_ROW_* status, slate_status_string gives its text).  16 bytes.
+ *   SLATE_WARN_PEEK_FIRST_KEY  "while peeking at key at offset %d: %v"  (a = offset, err)  iterator.go:121
+ *   SLATE_WARN_NO_FULL_KEY     "unable to locate uncorrupted first key in block; block is corrupt"  :130
+ *   SLATE_WARN_OFFSET_BOUNDS   "block.Offset[%d] = %d is out of bounds"  (a = index, b = offset)  :65
+ *   SLATE_WARN_PEEK_ROW        "while peeking at block.Offset[%d]: %s"   (a = index, err)  :70        */
+enum slate_seek_warn_kind {
+  SLATE_WARN_PEEK_FIRST_KEY = 1,
+  SLATE_WARN_NO_FULL_KEY = 2,
+  SLATE_WARN_OFFSET_BOUNDS = 3,
+  SLATE_WARN_PEEK_ROW = 4,
+};
+typedef struct slate_seek_warn {
+  uint16_t kind;
+  int16_t err;
+  uint32_t a;
+  uint32_t b;
+  uint32_t reserved;
+} slate_seek_warn;
+
 /* sstable.Config (builder.go:118-133); defaults in decode.go:16-23. */
 typedef struct slate_sst_config {
   uint64_t block_size;
@@ -181,6 +201,8 @@ typedef struct slate_sst_info {
 } slate_sst_info;
 
 typedef struct slate_ctx slate_ctx;
+typedef struct slate_devbuf slate_devbuf;
+typedef struct slate_hostbuf slate_hostbuf;
 typedef struct slate_sst_builder slate_sst_builder;
 typedef struct slate_sst_table slate_sst_table;
 typedef struct slate_index slate_index;
@@ -197,6 +219,35 @@ void slate_ctx_destroy(slate_ctx* ctx);
  * calls; NULL restores the context's own stream. */
 int slate_ctx_set_stream(slate_ctx* ctx, void* hip_stream);
 int slate_ctx_synchronize(slate_ctx* ctx);
+
+/* ---- library-owned memory (SURVEY 8b "Ownership": device-resident mode uses opaque handles
+ * owned by the C side) ----------------------------------------------------------------------
+ * cgo lets C keep no Go pointer once a call returns, and the *_device entry points only enqueue
+ * work on the context's stream.  So a Go caller gives them memory the library owns:
+ *   slate_devbuf   HBM of the context's GPU; every *_device entry point takes
+ *                  slate_devbuf_ptr(b) (plus a byte offset) wherever it takes a device pointer;
+ *   slate_hostbuf  page-locked host memory, the endpoint of the asynchronous copies (the DMA may
+ *                  run after the call returns, so it must not be Go memory).
+ * upload / download are synchronous (any host memory, large copies through the context's
+ * page-locked staging); copy, memset and the _async copies are ordered on the context's stream
+ * (slate_ctx_synchronize waits for them).  A buffer is used with contexts of its own device only. */
+slate_devbuf* slate_devbuf_alloc(slate_ctx* ctx, uint64_t bytes, int* status);
+void slate_devbuf_free(slate_devbuf* b); /* waits for the device first */
+void* slate_devbuf_ptr(const slate_devbuf* b);
+uint64_t slate_devbuf_size(const slate_devbuf* b);
+int slate_devbuf_upload(slate_ctx* ctx, slate_devbuf* dst, uint64_t dst_off, const void* src, uint64_t n);
+int slate_devbuf_download(slate_ctx* ctx, void* dst, const slate_devbuf* src, uint64_t src_off, uint64_t n);
+int slate_devbuf_copy(slate_ctx* ctx, slate_devbuf* dst, uint64_t dst_off, const slate_devbuf* src, uint64_t src_off,
+                      uint64_t n);
+int slate_devbuf_memset(slate_ctx* ctx, slate_devbuf* b, uint64_t off, int value, uint64_t n);
+slate_hostbuf* slate_hostbuf_alloc(slate_ctx* ctx, uint64_t bytes, int* status);
+void slate_hostbuf_free(slate_hostbuf* b);
+void* slate_hostbuf_ptr(const slate_hostbuf* b);
+uint64_t slate_hostbuf_size(const slate_hostbuf* b);
+int slate_devbuf_upload_async(slate_ctx* ctx, slate_devbuf* dst, uint64_t dst_off, const slate_hostbuf* src,
+                              uint64_t src_off, uint64_t n);
+int slate_devbuf_download_async(slate_ctx* ctx, slate_hostbuf* dst, uint64_t dst_off, const slate_devbuf* src,
+                                uint64_t src_off, uint64_t n);
 
 /* ---- block decode: block.Decode (block.go:78) ----------------------------------
  * Device-resident batch.  Block i's encoded bytes are d_in[d_in_off[i] .. d_in_off[i+1]).
@@ -261,6 +312,16 @@ int slate_block_seek_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_
 int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                      uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
                      uint64_t n, slate_seek* res);
+/* The same, also returning the warnings: query i's first warn_cap warnings at warn[i * warn_cap ..]
+ * (res[i].n_warn counts all of them; firstFullKey adds one per corrupt row before the first full key,
+ * the binary search at most log2(n_rows) + 1). */
+int slate_block_seek_warn_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_t* d_out_off,
+                                 const slate_block_meta* d_meta, const uint32_t* d_qblock, const uint8_t* d_keys,
+                                 const uint64_t* d_key_off, uint64_t n, slate_seek* d_res, slate_seek_warn* d_warn,
+                                 uint32_t warn_cap);
+int slate_block_seek_warn(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                          uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
+                          uint64_t n, slate_seek* res, slate_seek_warn* warn, uint32_t warn_cap);
 
 /* ---- block encode: block.Encode (block.go:54) ----------------------------------
  * Encodes one block (Data + Offsets) with codec: compress(Data || BE16 offsets ||
@@ -353,8 +414,10 @@ int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_in
 int slate_bloom_build(slate_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
                       uint32_t bits_per_key, uint8_t* bits, size_t bits_cap, size_t* bits_len,
                       uint16_t* num_probes);
-/* Encode (bloom.go:52; None and Snappy) / Decode (bloom.go:70; every codec).  Decode's bits alias
- * nothing: copied out. */
+/* Encode (bloom.go:52) / Decode (bloom.go:70), every codec.  Decode's bits alias nothing: copied out.
+ * When bits_cap is too small, Decode returns SLATE_E_CAPACITY with *bits_len set; a compressed filter
+ * of at most 64 MiB (input + decoded) is kept on the context until the next bloom_decode call, so
+ * the retry with the same bytes and a large enough buffer does not decompress it again. */
 int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len,
                        int codec, uint8_t* out, size_t out_cap, size_t* out_len);
 int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec,
@@ -411,6 +474,26 @@ int slate_kv_gather_copy_device(slate_ctx* ctx, const uint32_t* d_idx, uint64_t 
                                 const uint64_t* d_key_off, const uint8_t* d_vals, const uint64_t* d_val_off,
                                 uint8_t* d_okeys, const uint64_t* d_okey_off, uint8_t* d_ovals,
                                 const uint64_t* d_oval_off);
+
+/* ---- executeCompaction's codec path (slatedb/compaction/executor.go:92-151) ----------------
+ * One call for what executeCompaction does between reading its input SSTs and uploading its
+ * outputs: every data block of every input SST decoded on the GPU (block.Decode as
+ * sstable.Iterator applies it, internal/sstable/iterator.go:92-118), each row's full key and
+ * value (block.Iterator, block/iterator.go:84-107), iter.MergeSort over the sources
+ * (internal/iter/merge.go:12-111: keys ascending, the lowest source wins a duplicate key), and the
+ * merged entries written through one SST builder per output (EncodedSSTableWriter.Add,
+ * table_store.go:221-266: AddValue, an empty value is a tombstone), a new output starting after
+ * the entry that takes the running key + value size past max_sst_size (executor.go:119-139).
+ * Inputs: n_sst encoded SSTs, sst i = ssts[sst_off[i] .. sst_off[i+1]); n_src sources in
+ * precedence order (executor.go:55-90: L0 SSTs, then sorted runs), source j = SSTs
+ * [src_sst[j], src_sst[j+1]) read in order (src_sst: n_src + 1 entries, 0 .. n_sst).
+ * Outputs: *n_out tables in out_tables (the caller frees them with slate_sst_table_free); with
+ * out_cap too small, SLATE_E_CAPACITY and *n_out = the number needed.  The first failing input
+ * block's status is returned as executeCompaction returns its iterator's error; a row that fails
+ * to decode returns SLATE_E_INVALID_ARG.  Every intermediate stays in library-owned HBM. */
+int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst, const uint32_t* src_sst,
+                  uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size, slate_sst_table** out_tables,
+                  uint32_t out_cap, uint32_t* n_out);
 
 #ifdef __cplusplus
 }

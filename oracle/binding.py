@@ -92,6 +92,9 @@ def lib():
             "or_block_seek": (C.c_int, [u8p, C.c_uint32, u16p, C.c_uint32, u8p, C.c_size_t,
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
                                         C.POINTER(C.c_uint32)]),
+            "or_block_seek_w": (C.c_int, [u8p, C.c_uint32, u16p, C.c_uint32, u8p, C.c_size_t,
+                                          C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32]),
             "or_index_seek": (C.c_uint64, [u8p, u64p, C.c_uint64, u8p, C.c_size_t]),
             "or_v0_estimate_block_size": (C.c_uint64, [u8p, u64p, u8p, u64p, C.c_size_t]),
             "or_block_builder_new": (C.c_void_p, [C.c_uint64]),
@@ -300,6 +303,21 @@ def block_seek(data: bytes, offsets: list[int], key: bytes) -> tuple[int, int, i
     st = lib().or_block_seek(pd, len(data), offs.ctypes.data_as(u16p), len(offsets), pk, len(key), C.byref(st_),
                              C.byref(fi), C.byref(fl), C.byref(nw))
     return st, st_.value, fi.value, fl.value, nw.value
+
+
+def block_seek_warnings(data: bytes, offsets: list[int], key: bytes, cap: int = 64):
+    """block_seek plus the warnings NewIteratorAtKey adds, in order: [(kind, err, a, b), ...]
+    (the first `cap` of them; n_warn in the result counts all)."""
+    hd, pd = _buf(data)
+    offs = np.array(offsets or [0], dtype=np.uint16)
+    hk, pk = _buf(key)
+    st_, fi, fl, nw = C.c_uint32(), C.c_int32(), C.c_uint32(), C.c_uint32()
+    w = np.zeros(4 * max(cap, 1), np.uint32)
+    st = lib().or_block_seek_w(pd, len(data), offs.ctypes.data_as(u16p), len(offsets), pk, len(key), C.byref(st_),
+                               C.byref(fi), C.byref(fl), C.byref(nw), w.ctypes.data_as(C.POINTER(C.c_uint32)), cap)
+    warns = [(int(w[4 * k]), int(np.int32(w[4 * k + 1])), int(w[4 * k + 2]), int(w[4 * k + 3]))
+             for k in range(min(nw.value, cap))]
+    return (st, st_.value, fi.value, fl.value, nw.value), warns
 
 
 def index_seek(first_keys: list[bytes], key: bytes) -> int:

@@ -763,9 +763,22 @@ static int bytes_compare(const uint8_t* a, size_t an, const uint8_t* b, size_t b
 }
 
 /* block/iterator.go:31-82 NewIteratorAtKey with firstFullKey (:117-132) and sort.Search
- * (Go's binary search: i, j = 0, n; h = (i + j) / 2; !f(h) -> i = h + 1 else j = h). */
-int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
-                  size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn) {
+ * (Go's binary search: i, j = 0, n; h = (i + j) / 2; !f(h) -> i = h + 1 else j = h).
+ * Every warning types.ErrWarn.Add receives is recorded, in order, as (kind, err, a, b) in
+ * warn[4 * k ..] for the first cap of them: kind 1 "while peeking at key at offset %d: %v" (:121),
+ * 2 "unable to locate uncorrupted first key in block; block is corrupt" (:130),
+ * 3 "block.Offset[%d] = %d is out of bounds" (:65), 4 "while peeking at block.Offset[%d]: %s" (:70). */
+static void seek_warn(uint32_t* warn, uint32_t cap, uint32_t* n_warn, uint32_t kind, int err, uint32_t a, uint32_t b) {
+  if (warn && *n_warn < cap) {
+    uint32_t* w = warn + 4 * (size_t)*n_warn;
+    w[0] = kind; w[1] = (uint32_t)err; w[2] = a; w[3] = b;
+  }
+  (*n_warn)++;
+}
+
+int or_block_seek_w(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
+                    size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn,
+                    uint32_t* warn, uint32_t cap) {
   *start = 0; *first_idx = -1; *first_len = 0; *n_warn = 0;
   if (n == 0) return OR_E_SEEK_NO_OFFSETS;                         /* :32-34 */
   /* firstFullKey: PeekAtKey(block.Data[offset:], nil); a full key has keyPrefixLen 0 */
@@ -775,10 +788,10 @@ int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offset
     if (offsets[i] > data_len) return OR_E_SEEK_PANIC;              /* block.Data[offset:] */
     uint16_t pl, sl;
     int st = or_v0_peek(data + offsets[i], data_len - offsets[i], -1, &pl, &sl);
-    if (st) { (*n_warn)++; continue; }                              /* :120-123 */
+    if (st) { seek_warn(warn, cap, n_warn, 1, st, offsets[i], 0); continue; }  /* :120-123 */
     if (pl == 0) { idx = (int32_t)i; fk_off = offsets[i] + 4; fk_len = sl; break; }
   }
-  if (idx < 0) { (*n_warn)++; return OR_E_SEEK_NO_FULL_KEY; }       /* :130-131, :41-47 */
+  if (idx < 0) { seek_warn(warn, cap, n_warn, 2, OR_OK, 0, 0); return OR_E_SEEK_NO_FULL_KEY; }  /* :130-131, :41-47 */
   *first_idx = idx;
   *first_len = fk_len;
   const uint8_t* fk = data + fk_off;
@@ -789,12 +802,12 @@ int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offset
     uint32_t o = offsets[h + (uint32_t)idx];
     int ok = 0;
     if (o > (uint16_t)data_len) {                                   /* :65-68 */
-      (*n_warn)++;
+      seek_warn(warn, cap, n_warn, 3, OR_OK, h + (uint32_t)idx, o);
     } else {
       uint16_t pl, sl;
       int st = or_v0_peek(data + o, data_len - o, (long)fk_len, &pl, &sl);
       if (st) {
-        (*n_warn)++;                                                /* :70-73 */
+        seek_warn(warn, cap, n_warn, 4, st, h + (uint32_t)idx, 0);  /* :70-73 */
       } else {
         /* v0FullKey(p, firstKey) = firstKey[:prefixLen] || suffix (row.go:72-79) */
         size_t kl = (size_t)pl + sl;
@@ -812,6 +825,11 @@ int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offset
   }
   *start = lo + (uint32_t)idx;
   return OR_OK;
+}
+
+int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
+                  size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn) {
+  return or_block_seek_w(data, data_len, offsets, n, key, key_len, start, first_idx, first_len, n_warn, NULL, 0);
 }
 
 /* sstable/iterator.go:123-153 firstBlockIncludingOrAfterKey */

@@ -206,6 +206,9 @@ int or_merge_sort(uint32_t k, const uint8_t* keys, const uint64_t* key_off, cons
  * OR_E_SEEK_NO_OFFSETS, OR_E_SEEK_NO_FULL_KEY or OR_E_SEEK_PANIC (Go slice panic). */
 int or_block_seek(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
                   size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn);
+int or_block_seek_w(const uint8_t* data, uint32_t data_len, const uint16_t* offsets, uint32_t n, const uint8_t* key,
+                    size_t key_len, uint32_t* start, int32_t* first_idx, uint32_t* first_len, uint32_t* n_warn,
+                    uint32_t* warn, uint32_t cap);
 /* sstable.Iterator.firstBlockIncludingOrAfterKey (iterator.go:123-153) over the index's first keys. */
 uint64_t or_index_seek(const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks, const uint8_t* key,
                        size_t key_len);

@@ -154,19 +154,30 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
 
 // slate_block_decode_batch / slate_block_decode / the sharded decode: api_host.cpp.
 
-int slate_block_seek_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_t* d_out_off,
-                            const slate_block_meta* d_meta, const uint32_t* d_qblock, const uint8_t* d_keys,
-                            const uint64_t* d_key_off, uint64_t n, slate_seek* d_res) {
+int slate_block_seek_warn_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_t* d_out_off,
+                                 const slate_block_meta* d_meta, const uint32_t* d_qblock, const uint8_t* d_keys,
+                                 const uint64_t* d_key_off, uint64_t n, slate_seek* d_res, slate_seek_warn* d_warn,
+                                 uint32_t warn_cap) {
   if (!ctx || (n && (!d_out_off || !d_meta || !d_qblock || !d_key_off || !d_res))) return SLATE_E_INVALID_ARG;
+  if (warn_cap && !d_warn) return SLATE_E_INVALID_ARG;
   SLATE_HIP(ctx_bind(ctx));
-  SLATE_HIP(launch_block_seek(ctx->stream, d_data, d_out_off, d_meta, d_qblock, d_keys, d_key_off, n, d_res));
+  SLATE_HIP(launch_block_seek(ctx->stream, d_data, d_out_off, d_meta, d_qblock, d_keys, d_key_off, n, d_res,
+                              warn_cap ? d_warn : nullptr, warn_cap));
   return SLATE_OK;
 }
 
-int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
-                     uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
-                     uint64_t n, slate_seek* res) {
+int slate_block_seek_device(slate_ctx* ctx, const uint8_t* d_data, const uint64_t* d_out_off,
+                            const slate_block_meta* d_meta, const uint32_t* d_qblock, const uint8_t* d_keys,
+                            const uint64_t* d_key_off, uint64_t n, slate_seek* d_res) {
+  return slate_block_seek_warn_device(ctx, d_data, d_out_off, d_meta, d_qblock, d_keys, d_key_off, n, d_res, nullptr,
+                                      0);
+}
+
+int slate_block_seek_warn(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                          uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
+                          uint64_t n, slate_seek* res, slate_seek_warn* warn, uint32_t warn_cap) {
   if (!ctx || !out_off || (n_blocks && !meta) || (n && (!qblock || !key_off || !res))) return SLATE_E_INVALID_ARG;
+  if (warn_cap && !warn) return SLATE_E_INVALID_ARG;
   if (n == 0) return SLATE_OK;
   for (uint64_t i = 0; i < n; i++)
     if (qblock[i] >= n_blocks) return SLATE_E_INVALID_ARG;
@@ -179,9 +190,11 @@ int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_of
     off += (bytes + 255) & ~size_t(255);
     return o;
   };
+  const size_t wbytes = size_t(n) * warn_cap * sizeof(slate_seek_warn);
   const size_t o_data = carve(db + 16), o_off = carve((size_t(n_blocks) + 1) * 8),
                o_meta = carve(size_t(n_blocks) * sizeof(slate_block_meta) + 16), o_q = carve(n * 4),
-               o_keys = carve(kb + 16), o_koff = carve((n + 1) * 8), o_res = carve(n * sizeof(slate_seek));
+               o_keys = carve(kb + 16), o_koff = carve((n + 1) * 8), o_res = carve(n * sizeof(slate_seek)),
+               o_warn = carve(wbytes + 16);
   SLATE_HIP(ctx->e_g.ensure(off));
   uint8_t* base = ctx->e_g.as<uint8_t>();
   std::vector<uint64_t> rel(n + 1);
@@ -193,14 +206,22 @@ int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_of
   SLATE_HIP(hipMemcpyAsync(base + o_q, qblock, n * 4, hipMemcpyHostToDevice, st));
   if (kb) SLATE_HIP(hipMemcpyAsync(base + o_keys, keys + key_off[0], kb, hipMemcpyHostToDevice, st));
   SLATE_HIP(hipMemcpyAsync(base + o_koff, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  slate_seek_warn* dw = warn_cap ? reinterpret_cast<slate_seek_warn*>(base + o_warn) : nullptr;
   SLATE_HIP(launch_block_seek(st, base + o_data, reinterpret_cast<const uint64_t*>(base + o_off),
                               reinterpret_cast<const slate_block_meta*>(base + o_meta),
                               reinterpret_cast<const uint32_t*>(base + o_q), base + o_keys,
                               reinterpret_cast<const uint64_t*>(base + o_koff), n,
-                              reinterpret_cast<slate_seek*>(base + o_res)));
+                              reinterpret_cast<slate_seek*>(base + o_res), dw, warn_cap));
   SLATE_HIP(hipMemcpyAsync(res, base + o_res, n * sizeof(slate_seek), hipMemcpyDeviceToHost, st));
+  if (wbytes) SLATE_HIP(hipMemcpyAsync(warn, dw, wbytes, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
   return SLATE_OK;
+}
+
+int slate_block_seek(slate_ctx* ctx, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
+                     uint32_t n_blocks, const uint32_t* qblock, const uint8_t* keys, const uint64_t* key_off,
+                     uint64_t n, slate_seek* res) {
+  return slate_block_seek_warn(ctx, data, out_off, meta, n_blocks, qblock, keys, key_off, n, res, nullptr, 0);
 }
 
 }  // extern "C"

@@ -226,8 +226,39 @@ int lane_finish(PipeLane& L, Sink& o) {
 // remaining chunks are only planned and SLATE_E_CAPACITY is returned.
 // gsrc (sharded decode): local block j's bytes start at in + gsrc[j] (in_off then gives only
 // the local layout, i.e. the sizes); null = block j at in + in_off[j].
+// Abandons whatever a lane still has in flight (a previous call that returned early): waits for
+// its stream and forgets the chunk, copying nothing into any caller's buffers.
+void lanes_drain(slate_ctx* ctx) {
+  for (PipeLane& L : ctx->lanes) {
+    if (L.busy && L.stream) (void)hipStreamSynchronize(L.stream);
+    L.busy = false;
+    L.decoded = false;
+  }
+}
+
+// Runs lanes_drain on every early return of host_decode (an error after a chunk was queued).
+struct LaneGuard {
+  slate_ctx* ctx;
+  bool armed = true;
+  ~LaneGuard() {
+    if (armed) lanes_drain(ctx);
+  }
+};
+
+int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o,
+                     const uint64_t* gsrc);
+
 int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o,
                 const uint64_t* gsrc = nullptr) {
+  lanes_drain(ctx);  // nothing of an earlier (failed) call may reach this call's sink
+  LaneGuard guard{ctx};
+  const int st = host_decode_body(ctx, codec, in, in_off, n, o, gsrc);
+  guard.armed = st != SLATE_OK && st != SLATE_E_CAPACITY;
+  return st;
+}
+
+int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o,
+                     const uint64_t* gsrc) {
   SLATE_HIP(ctx_bind(ctx));
   const bool trace = host_trace();
   const double t_start = trace ? now_ms() : 0.0;
@@ -381,6 +412,10 @@ int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const
     out_off[0] = row_base[0] = 0;
     return SLATE_OK;
   }
+  // offsets must not decrease (a decreasing offset inside a chunk would underflow its block
+  // lengths): checked before any lane work starts, as slate_shard_pack does
+  for (uint32_t i = 0; i < n; i++)
+    if (in_off[i + 1] < in_off[i]) return SLATE_E_INVALID_ARG;
   Sink o;
   o.out = out;
   o.out_cap = out_cap;
@@ -474,8 +509,12 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
                                const uint64_t* in_off, uint32_t n, uint8_t* out, uint64_t out_cap, uint64_t* out_off,
                                slate_block_meta* meta, slate_row* rows, uint64_t rows_cap, uint64_t* row_base) {
   if (!ctxs || n_ctx == 0 || !in_off || !out_off || !row_base || (n && !in)) return SLATE_E_INVALID_ARG;
-  for (uint32_t g = 0; g < n_ctx; g++)
+  for (uint32_t g = 0; g < n_ctx; g++) {
     if (!ctxs[g]) return SLATE_E_INVALID_ARG;
+    // one host thread per context below: a context listed twice would share its lanes
+    for (uint32_t h = 0; h < g; h++)
+      if (ctxs[h] == ctxs[g]) return SLATE_E_INVALID_ARG;
+  }
   // No re-pack: each context's staging gathers its blocks straight from the caller's buffer.
   struct Shard {
     std::vector<uint64_t> in_off, gsrc, out_off, row_base;

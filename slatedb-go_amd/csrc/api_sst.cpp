@@ -763,7 +763,9 @@ struct HostBytes {
     }
     cap = len ? len : 1;
     p = static_cast<uint8_t*>(malloc(cap));
+    if (!p) cap = 0;  // callers check ok(): a host OOM becomes SLATE_E_OOM, not a fault
   }
+  bool ok() const { return p != nullptr; }
   ~HostBytes() {
     if (!mapped) {
       free(p);
@@ -996,6 +998,7 @@ static int builder_flush(slate_sst_builder* b, bool final) {
     SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
     mark("pack snappy");
     seg = std::make_shared<HostBytes>(fin[nb], ctx->seg_pool);
+    if (!seg->ok()) return SLATE_E_OOM;
     int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, fin[nb], st);
     mark("blocks D2H");
     if (s) return s;
@@ -1024,6 +1027,7 @@ static int builder_flush(slate_sst_builder* b, bool final) {
       mark("codec frames");
     }
     seg = std::make_shared<HostBytes>(out_off[nb], ctx->seg_pool);
+    if (!seg->ok()) return SLATE_E_OOM;
     int s = ctx_d2h(ctx, seg->p, src, out_off[nb], st);
     mark("blocks D2H");
     if (s) return s;
@@ -1356,9 +1360,13 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   t->info.codec = b->cfg.codec;
   t->info.first_key_len = uint32_t(b->first_key.size());
   t->first_key = b->first_key;
+  auto fin = std::make_shared<HostBytes>(buf.size());
+  if (!fin->ok()) {
+    delete t;
+    return SLATE_E_OOM;
+  }
   t->chunks.assign(b->blocks.begin(), b->blocks.end());
   b->blocks.clear();
-  auto fin = std::make_shared<HostBytes>(buf.size());
   if (!buf.empty()) memcpy(fin->p, buf.data(), buf.size());
   t->chunks.push_back(ByteView{fin, 0, buf.size()});
   *table = t;
@@ -1670,6 +1678,8 @@ int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits,
   return SLATE_OK;
 }
 
+constexpr size_t kBloomKeep = size_t(64) << 20;
+
 int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, uint16_t* num_probes, uint8_t* bits,
                        size_t bits_cap, size_t* bits_len) {
   if (!ctx || (len && !buf)) return SLATE_E_INVALID_ARG;
@@ -1681,10 +1691,22 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   size_t pn = ci;
   const bool cached = codec != SLATE_CODEC_NONE && codec == ctx->bloom_codec && len == ctx->bloom_in.size() &&
                       memcmp(buf, ctx->bloom_in.data(), len) == 0;
+  // whatever was kept belongs to at most this one retry
+  std::vector<uint8_t> kept;
+  kept.swap(ctx->bloom_dec);
+  ctx->bloom_in.clear();
+  ctx->bloom_in.shrink_to_fit();
+  ctx->bloom_codec = -1;
   if (cached) {  // the same bytes decoded (and checked) by the call that reported SLATE_E_CAPACITY
-    dec.swap(ctx->bloom_dec);
-    ctx->bloom_in.clear();
-    ctx->bloom_codec = -1;
+    dec.swap(kept);
+    p = dec.data();
+    pn = dec.size();
+  } else if (codec > SLATE_CODEC_NONE && codec <= SLATE_CODEC_ZSTD) {
+    // the GPU payload path checks the CRC first (bloom.go:75-79), then decompresses: one upload
+    int bst = 0;
+    int st = ctx_payload_decode_buffer(ctx, codec, buf, len, dec, &bst);
+    if (st) return st;
+    if (bst) return bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_FILTER_CHECKSUM : bst;
     p = dec.data();
     pn = dec.size();
   } else {
@@ -1692,21 +1714,15 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
     int st = ctx_crc32_host_buffer(ctx, buf, ci, &crc);
     if (st) return st;
     if (crc != ld_be32(buf + ci)) return SLATE_E_FILTER_CHECKSUM;
-    if (codec < SLATE_CODEC_NONE || codec > SLATE_CODEC_ZSTD) return SLATE_E_INVALID_CODEC;
-    if (codec != SLATE_CODEC_NONE) {
-      int bst = 0;
-      st = ctx_payload_decode_buffer(ctx, codec, buf, len, dec, &bst);
-      if (st) return st;
-      if (bst) return bst == SLATE_E_BLOCK_CHECKSUM ? SLATE_E_FILTER_CHECKSUM : bst;
-      p = dec.data();
-      pn = dec.size();
-    }
+    if (codec != SLATE_CODEC_NONE) return SLATE_E_INVALID_CODEC;
   }
   if (pn < 2) return SLATE_E_FILTER_PANIC;
   if (num_probes) *num_probes = ld_be16(p);
   if (bits_len) *bits_len = pn - 2;
   if (pn - 2 > bits_cap || (!bits && pn > 2)) {
-    if (codec != SLATE_CODEC_NONE) {  // keep it for the retry with a buffer of *bits_len bytes
+    // keep a decoded filter for the retry with a buffer of *bits_len bytes (bounded: a caller that
+    // only asks for the size leaves at most kBloomKeep bytes of input + output on the context)
+    if (codec != SLATE_CODEC_NONE && len + dec.size() <= kBloomKeep) {
       ctx->bloom_in.assign(buf, buf + len);
       ctx->bloom_dec.swap(dec);
       ctx->bloom_codec = codec;

@@ -132,6 +132,8 @@ hipError_t launch_rows_copy(hipStream_t st, const uint8_t* data, const uint64_t*
 hipError_t launch_gather_lengths(hipStream_t st, const uint32_t* idx, uint64_t n, const uint64_t* key_off,
                                  const uint64_t* val_off, const uint8_t* tomb, uint64_t* okey_off, uint64_t* oval_off,
                                  uint8_t* otomb, void* scratch);
+// dst[i] = src[i] + delta (rebasing concatenated offset arrays; merge.hip)
+hipError_t launch_u64_add(hipStream_t st, const uint64_t* src, uint64_t* dst, uint64_t n, uint64_t delta);
 hipError_t launch_gather_copy(hipStream_t st, const uint32_t* idx, uint64_t n, const uint8_t* keys,
                               const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off, uint8_t* okeys,
                               const uint64_t* okey_off, uint8_t* ovals, const uint64_t* oval_off);
@@ -161,7 +163,7 @@ hipError_t launch_lz4_par_bytes(hipStream_t st, const uint8_t* in, uint32_t sz, 
 // Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                              const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
-                             slate_seek* res);
+                             slate_seek* res, slate_seek_warn* warn = nullptr, uint32_t warn_cap = 0);
 hipError_t launch_index_seek(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n_blocks,
                              const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq, uint64_t* out);
 

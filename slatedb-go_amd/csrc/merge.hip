@@ -544,3 +544,21 @@ hipError_t launch_gather_copy(hipStream_t st, const uint32_t* idx, uint64_t n, c
 }
 
 }  // namespace slate
+
+namespace slate {
+
+// dst[i] = src[i] + delta: a KV view's offsets rebased when views are concatenated (slate_compact).
+__global__ void u64_add_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, uint64_t n,
+                               uint64_t delta) {
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x)
+    dst[i] = src[i] + delta;
+}
+
+hipError_t launch_u64_add(hipStream_t st, const uint64_t* src, uint64_t* dst, uint64_t n, uint64_t delta) {
+  if (n == 0) return hipSuccess;
+  const uint32_t grid = uint32_t(std::min<uint64_t>((n + 255) / 256, 4096));
+  u64_add_kernel<<<grid, 256, 0, st>>>(src, dst, n, delta);
+  return hipGetLastError();
+}
+
+}  // namespace slate

@@ -34,9 +34,22 @@ __device__ inline int peek(const uint8_t* p, uint32_t n, uint32_t fk_len, uint32
 
 __global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                                   const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
-                                  slate_seek* res) {
+                                  slate_seek* res, slate_seek_warn* wout, uint32_t wcap) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= nq) return;
+  uint32_t warn = 0;
+  // types.ErrWarn.Add, in order: the first wcap warnings are recorded, all are counted
+  auto add = [&](uint32_t kind, int err, uint32_t x, uint32_t y) {
+    if (wout && warn < wcap) {
+      slate_seek_warn w{};
+      w.kind = uint16_t(kind);
+      w.err = int16_t(err);
+      w.a = x;
+      w.b = y;
+      wout[q * wcap + warn] = w;
+    }
+    warn++;
+  };
   slate_seek r{};
   r.first_idx = -1;
   const uint32_t b = qblock[q];
@@ -58,7 +71,7 @@ __global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, 
   }
   // firstFullKey: the first row that PeekAtKey(Data[off:], nil) accepts has keyPrefixLen 0
   int32_t idx = -1;
-  uint32_t fk_off = 0, fk_len = 0, warn = 0;
+  uint32_t fk_off = 0, fk_len = 0;
   for (uint32_t i = 0; i < n; i++) {
     const uint32_t o = ld_be16(offs + 2 * i);
     if (o > dlen) {  // block.Data[offset:] panics
@@ -68,8 +81,9 @@ __global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, 
       return;
     }
     uint32_t pl, sl;
-    if (peek(d + o, dlen - o, 0, &pl, &sl) != SLATE_OK) {
-      warn++;
+    const int e = peek(d + o, dlen - o, 0, &pl, &sl);
+    if (e != SLATE_OK) {
+      add(SLATE_WARN_PEEK_FIRST_KEY, e, o, 0);  // iterator.go:121
       continue;
     }
     if (pl == 0) {
@@ -81,7 +95,8 @@ __global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, 
   }
   if (idx < 0) {  // iterator.go:130-131 -> :41-47
     r.status = SLATE_E_SEEK_NO_FULL_KEY;
-    r.n_warn = warn + 1;
+    add(SLATE_WARN_NO_FULL_KEY, SLATE_OK, 0, 0);  // iterator.go:130
+    r.n_warn = warn;
     res[q] = r;
     return;
   }
@@ -101,10 +116,11 @@ __global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, 
     const uint32_t o = ld_be16(offs + 2 * (h + uint32_t(idx)));
     bool ok = false;
     uint32_t pl, sl;
+    int e = SLATE_OK;
     if (o > uint32_t(uint16_t(dlen))) {
-      warn++;
-    } else if (peek(d + o, dlen - o, fk_len, &pl, &sl) != SLATE_OK) {
-      warn++;
+      add(SLATE_WARN_OFFSET_BOUNDS, SLATE_OK, h + uint32_t(idx), o);  // iterator.go:65
+    } else if ((e = peek(d + o, dlen - o, fk_len, &pl, &sl)) != SLATE_OK) {
+      add(SLATE_WARN_PEEK_ROW, e, h + uint32_t(idx), 0);  // iterator.go:70
     } else {
       // v0FullKey = firstKey[:prefixLen] || suffix, compared with the sought key
       const uint32_t fl = pl + sl, mm = fl < kl ? fl : kl;
@@ -151,9 +167,10 @@ __global__ void index_seek_kernel(const uint8_t* keys, const uint64_t* key_off, 
 
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                              const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
-                             slate_seek* res) {
+                             slate_seek* res, slate_seek_warn* warn, uint32_t warn_cap) {
   if (nq == 0) return hipSuccess;
-  block_seek_kernel<<<uint32_t((nq + 255) / 256), 256, 0, st>>>(data, out_off, meta, qblock, qkeys, qkey_off, nq, res);
+  block_seek_kernel<<<uint32_t((nq + 255) / 256), 256, 0, st>>>(data, out_off, meta, qblock, qkeys, qkey_off, nq, res,
+                                                                 warn, warn_cap);
   return hipGetLastError();
 }
 

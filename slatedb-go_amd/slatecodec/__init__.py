@@ -31,6 +31,7 @@ u64p = C.POINTER(C.c_uint64)
 szp = C.POINTER(C.c_size_t)
 vp = C.c_void_p
 
+SEEK_WARN_DTYPE = np.dtype([("kind", "<u2"), ("err", "<i2"), ("a", "<u4"), ("b", "<u4"), ("reserved", "<u4")])
 SEEK_DTYPE = np.dtype([("start", "<u4"), ("first_idx", "<i4"), ("n_warn", "<u4"), ("status", "<i2"),
                        ("first_len", "<u2")])
 META_DTYPE = np.dtype([("status", "<i2"), ("flags", "<u2"), ("detail", "<i4"), ("data_len", "<u4"),
@@ -80,6 +81,24 @@ _SIGS = {
     "slate_block_seek_device": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, C.c_uint64, vp]),
     "slate_block_seek": (C.c_int, [vp, vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint64, vp]),
     "slate_index_seek": (C.c_int, [vp, vp, vp, vp, C.c_uint64, vp]),
+    "slate_devbuf_alloc": (vp, [vp, C.c_uint64, C.POINTER(C.c_int)]),
+    "slate_devbuf_free": (None, [vp]),
+    "slate_devbuf_ptr": (vp, [vp]),
+    "slate_devbuf_size": (C.c_uint64, [vp]),
+    "slate_devbuf_upload": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64]),
+    "slate_devbuf_download": (C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint64]),
+    "slate_devbuf_copy": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint64]),
+    "slate_devbuf_memset": (C.c_int, [vp, vp, C.c_uint64, C.c_int, C.c_uint64]),
+    "slate_hostbuf_alloc": (vp, [vp, C.c_uint64, C.POINTER(C.c_int)]),
+    "slate_hostbuf_free": (None, [vp]),
+    "slate_hostbuf_ptr": (vp, [vp]),
+    "slate_hostbuf_size": (C.c_uint64, [vp]),
+    "slate_devbuf_upload_async": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint64]),
+    "slate_devbuf_download_async": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint64]),
+    "slate_compact": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.c_uint32, C.POINTER(SstConfig), C.c_uint64, vp,
+                                C.c_uint32, C.POINTER(C.c_uint32)]),
+    "slate_block_seek_warn_device": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, C.c_uint64, vp, vp, C.c_uint32]),
+    "slate_block_seek_warn": (C.c_int, [vp, vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint64, vp, vp, C.c_uint32]),
     "slate_shard_pack": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint64, vp]),
     "slate_block_decode_sharded": (C.c_int, [vp, C.c_uint32, C.c_int, vp, vp, C.c_uint32, vp, C.c_uint64, vp, vp,
                                              vp, C.c_uint64, vp]),
@@ -229,6 +248,20 @@ class Context:
                                       _ptr(np.ascontiguousarray(meta)), len(out_off) - 1, _ptr(qb), _ptr(kd), _ptr(ko),
                                       len(keys), _ptr(res)), "slate_block_seek")
         return res[: len(keys)]
+
+    def block_seek_warn(self, out: np.ndarray, out_off: np.ndarray, meta: np.ndarray, qblock: list[int],
+                        keys: list[bytes], warn_cap: int = 16):
+        """block_seek plus each query's warnings: (SEEK_DTYPE[n], SEEK_WARN_DTYPE[n, warn_cap])."""
+        kd, ko = _arena(keys)
+        qb = np.ascontiguousarray(qblock, np.uint32)
+        res = np.zeros(max(len(keys), 1), SEEK_DTYPE)
+        warn = np.zeros((max(len(keys), 1), max(warn_cap, 1)), SEEK_WARN_DTYPE)
+        out = np.ascontiguousarray(out, np.uint8)
+        _check(lib().slate_block_seek_warn(self._h, _ptr(out), _ptr(np.ascontiguousarray(out_off, np.uint64)),
+                                           _ptr(np.ascontiguousarray(meta)), len(out_off) - 1, _ptr(qb), _ptr(kd),
+                                           _ptr(ko), len(keys), _ptr(res), _ptr(warn), warn_cap),
+               "slate_block_seek_warn")
+        return res[: len(keys)], warn[: len(keys), :warn_cap]
 
     def block_seek_device(self, d_data: int, d_out_off: int, d_meta: int, d_qblock: int, d_keys: int, d_key_off: int,
                           n: int, d_res: int) -> None:
@@ -380,6 +413,117 @@ class Context:
                                      re_.value - rs.value, _ptr(out), out_cap, _ptr(out_off), _ptr(meta), _ptr(rows),
                                      rows.size, _ptr(row_base), C.byref(failed))
         return st, failed.value, (out, out_off, meta, rows, row_base)
+
+
+class DevBuf:
+    """slate_devbuf: HBM owned by the library (the device-resident entry points take .ptr)."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        st = C.c_int()
+        self._h = lib().slate_devbuf_alloc(ctx.handle, int(nbytes), C.byref(st))
+        if not self._h:
+            raise SlateError(st.value, "slate_devbuf_alloc")
+        self.ctx = ctx
+        self.size = int(nbytes)
+        self.ptr = int(lib().slate_devbuf_ptr(self._h))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def at(self, off: int) -> int:
+        """Device address of byte `off` (what a cgo caller computes from slate_devbuf_ptr)."""
+        assert 0 <= off <= self.size
+        return self.ptr + off
+
+    def upload(self, a, off: int = 0) -> "DevBuf":
+        a = np.ascontiguousarray(a)
+        _check(lib().slate_devbuf_upload(self.ctx.handle, self._h, off, _ptr(a), a.nbytes), "slate_devbuf_upload")
+        return self
+
+    def download(self, nbytes: int | None = None, off: int = 0, dtype=np.uint8) -> np.ndarray:
+        n = self.size - off if nbytes is None else int(nbytes)
+        out = np.zeros(max(n, 1), np.uint8)
+        _check(lib().slate_devbuf_download(self.ctx.handle, _ptr(out), self._h, off, n), "slate_devbuf_download")
+        return out[:n].view(dtype)
+
+    def u64(self, index: int) -> int:
+        return int(self.download(8, 8 * index, np.uint64)[0])
+
+    def memset(self, value: int = 0, off: int = 0, nbytes: int | None = None) -> "DevBuf":
+        n = self.size - off if nbytes is None else int(nbytes)
+        _check(lib().slate_devbuf_memset(self.ctx.handle, self._h, off, value, n), "slate_devbuf_memset")
+        return self
+
+    def free(self):
+        if getattr(self, "_h", None):
+            lib().slate_devbuf_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except (TypeError, AttributeError):
+            pass
+
+
+def devbuf_from(ctx: "Context", a) -> DevBuf:
+    """A DevBuf holding a copy of host array a."""
+    a = np.ascontiguousarray(a)
+    return DevBuf(ctx, a.nbytes).upload(a)
+
+
+class HostBuf:
+    """slate_hostbuf: page-locked host memory owned by the library (async copy endpoint)."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        st = C.c_int()
+        self._h = lib().slate_hostbuf_alloc(ctx.handle, int(nbytes), C.byref(st))
+        if not self._h:
+            raise SlateError(st.value, "slate_hostbuf_alloc")
+        self.size = int(nbytes)
+        self.view = np.ctypeslib.as_array(C.cast(lib().slate_hostbuf_ptr(self._h), u8p), shape=(max(self.size, 1),))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def free(self):
+        if getattr(self, "_h", None):
+            self.view = None
+            lib().slate_hostbuf_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except (TypeError, AttributeError):
+            pass
+
+
+def compact(ctx: "Context", sources: list[list[bytes]], max_sst_size: int, block_size: int = 4096,
+            min_filter_keys: int = 0, filter_bits_per_key: int = 10, codec: int = NONE) -> list[bytes]:
+    """slate_compact: executeCompaction's codec path in one C-ABI call -> encoded output SSTs."""
+    flat = [s for run in sources for s in run]
+    blob = np.frombuffer(b"".join(flat) or b"\0", np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(s) for s in flat])]).astype(np.uint64)
+    src = np.concatenate([[0], np.cumsum([len(r) for r in sources])]).astype(np.uint32)
+    cfg = SstConfig(block_size, min_filter_keys, filter_bits_per_key, codec)
+    cap = 16
+    while True:
+        tabs = (C.c_void_p * cap)()
+        n = C.c_uint32()
+        st = lib().slate_compact(ctx.handle, _ptr(blob), _ptr(off), len(flat), _ptr(src), len(sources), C.byref(cfg),
+                                 max_sst_size, tabs, cap, C.byref(n))
+        if st == E_CAPACITY and n.value > cap:
+            cap = n.value
+            continue
+        _check(st, "slate_compact")
+        out = []
+        for k in range(n.value):
+            t = SstTable(tabs[k])
+            out.append(t.encode())
+        return out
 
 
 def shard_blocks(n_blocks: int, n_shards: int, shard: int) -> int:

@@ -15,11 +15,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def ctx():
-    import torch
-    torch.cuda.init()
-    torch.cuda.set_device(0)
     import slatecodec as sc
     return sc.Context(0)
+
+
+@pytest.fixture(params=["c_abi", "steps"])
+def compact_fn(request):
+    """slate_compact (one C-ABI call) and the same chain step by step on slate_devbufs."""
+    from slatecodec import compaction
+    return compaction.compact if request.param == "c_abi" else compaction.compact_steps
 
 
 @pytest.mark.parametrize("seed,n_src,n_keys,space,codec,run_ssts,max_size,out_codec", [
@@ -29,11 +33,10 @@ def ctx():
     (4, 5, 800, 1200, ob.SNAPPY, 2, 9_000, ob.NONE),
     (5, 1, 2000, 2000, ob.NONE, 4, 1 << 30, ob.SNAPPY),
 ])
-def test_compaction_bit_exact(ctx, seed, n_src, n_keys, space, codec, run_ssts, max_size, out_codec):
-    from slatecodec import compaction
+def test_compaction_bit_exact(ctx, compact_fn, seed, n_src, n_keys, space, codec, run_ssts, max_size, out_codec):
     rng = random.Random(seed)
     srcs = cg.random_sources(rng, n_src, n_keys, space, codec=codec, run_ssts=run_ssts)
-    got = compaction.compact(ctx, srcs, max_size, codec=out_codec)
+    got = compact_fn(ctx, srcs, max_size, codec=out_codec)
     want = cg.oracle_compact(srcs, max_size, codec=out_codec)
     assert len(got) == len(want)
     for i, (g, w) in enumerate(zip(got, want)):
@@ -62,15 +65,14 @@ def test_compaction_many_snappy_ssts(ctx):
     assert got == cg.oracle_compact(srcs, 30_000, codec=ob.SNAPPY)
 
 
-def test_compaction_mixed_codecs(ctx):
+def test_compaction_mixed_codecs(ctx, compact_fn):
     """Each SST carries its own codec (sstable.Info.CompressionCodec): a DB whose compression
     option changed has L0 SSTs and sorted runs in different codecs."""
-    from slatecodec import compaction
     rng = random.Random(22)
     srcs = []
     for j, codec in enumerate((ob.NONE, ob.SNAPPY, ob.NONE, ob.SNAPPY)):
         srcs += cg.random_sources(rng, 1, 700, 1600, codec=codec, run_ssts=1 + j % 3)
-    got = compaction.compact(ctx, srcs, 1 << 30, codec=ob.SNAPPY)
+    got = compact_fn(ctx, srcs, 1 << 30, codec=ob.SNAPPY)
     assert got == cg.oracle_compact(srcs, 1 << 30, codec=ob.SNAPPY)
 
 
@@ -91,11 +93,11 @@ def _corrupt_first_block(sst: bytes, body: bytes) -> bytes:
     (b"\x01\x00a", 11),  # decoded length 1 (no row slot) with trailing input
     (None, 2),           # CRC mismatch
 ])
-def test_compaction_bad_block_fails(ctx, body, status):
+def test_compaction_bad_block_fails(ctx, compact_fn, body, status):
     """A block that fails block.Decode stops the compaction (sstable.Iterator returns the error,
     executeCompaction returns it: iterator.go:62-68, executor.go:107-150), also when the block
     fails before it owns a row slot."""
-    from slatecodec import compaction, SlateError
+    from slatecodec import SlateError
     rng = random.Random(23)
     srcs = cg.random_sources(rng, 2, 600, 1200, codec=ob.SNAPPY)
     if body is None:
@@ -105,5 +107,17 @@ def test_compaction_bad_block_fails(ctx, body, status):
     else:
         srcs[1][0] = _corrupt_first_block(srcs[1][0], body)
     with pytest.raises(SlateError) as e:
-        compaction.compact(ctx, srcs, 1 << 30)
+        compact_fn(ctx, srcs, 1 << 30)
     assert e.value.status == status
+
+
+def test_compaction_empty_and_capacity(ctx):
+    """No input entries: no output SST; out_cap smaller than the outputs: SLATE_E_CAPACITY with the
+    count needed (the binding then retries with enough room)."""
+    from slatecodec import compaction
+    assert compaction.compact(ctx, [[]], 1 << 30) == []
+    rng = random.Random(31)
+    srcs = cg.random_sources(rng, 2, 2000, 3000)
+    got = compaction.compact(ctx, srcs, 2_000)  # > 16 outputs: the first call reports the count
+    want = cg.oracle_compact(srcs, 2_000)
+    assert len(want) > 16 and got == want

@@ -56,14 +56,21 @@ def _layout(blocks):
 def _seek_both(ctx, blocks, queries):
     """queries: (block index, key).  GPU block_seek vs the oracle on each block's Data/Offsets."""
     out, out_off, meta = _layout(blocks)
-    got = ctx.block_seek(out, out_off, meta, [q[0] for q in queries], [q[1] for q in queries])
+    qb, qk = [q[0] for q in queries], [q[1] for q in queries]
+    got = ctx.block_seek(out, out_off, meta, qb, qk)
+    cap = 8
+    got_w, warns = ctx.block_seek_warn(out, out_off, meta, qb, qk, warn_cap=cap)
+    assert got_w.tobytes() == got.tobytes()
     for i, (b, key) in enumerate(queries):
         _, data, offs = blocks[b]
-        st, start, fi, fl, nw = ob.block_seek(data, offs, key)
+        (st, start, fi, fl, nw), ow = ob.block_seek_warnings(data, offs, key, cap)
         g = got[i]
         assert (int(g["status"]), int(g["n_warn"])) == (st, nw), (i, b, key, g, st, nw)
         if st == 0:
             assert (int(g["start"]), int(g["first_idx"]), int(g["first_len"])) == (start, fi, fl), (i, key)
+        # ErrWarn's entries in order: what a shim needs to rebuild its text
+        gw = [(int(w["kind"]), int(w["err"]), int(w["a"]), int(w["b"])) for w in warns[i][: min(nw, cap)]]
+        assert gw == ow, (i, b, key, gw, ow)
     return got
 
 
@@ -106,42 +113,40 @@ def test_random_blocks_and_keys(ctx, seed):
 
 
 def test_block_seek_device(ctx):
-    """The device-resident entry over a device-resident decode batch."""
-    import torch
+    """The device-resident entries on library-owned memory (slate_devbuf, as a cgo caller holds it):
+    plan -> decode -> seek with warnings, no torch allocation."""
     import slatecodec as sc
     rng = random.Random(7)
     kvs = bg.kv_synthetic(38 * 50)
     blocks = bg.sst_blocks(kvs, 4096, ob.SNAPPY)
     blob, off = bg.pack(blocks)
     n = len(blocks)
-    dev = torch.device("cuda", 0)
-    s = torch.cuda.current_stream(dev)
-    ctx.set_stream(s.cuda_stream)
-    d_in = torch.from_numpy(blob).to(dev)
-    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
-    d_oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_rb = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_sc = torch.empty(sc.decode_scratch_bytes(n) + 64, dtype=torch.uint8, device=dev)
-    ctx.decode_plan_device(ob.SNAPPY, d_in.data_ptr(), d_off.data_ptr(), n, d_oo.data_ptr(), d_rb.data_ptr(),
-                           d_sc.data_ptr())
-    torch.cuda.synchronize()
-    d_out = torch.empty(int(d_oo[n].item()) + 16, dtype=torch.uint8, device=dev)
-    d_meta = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-    d_rows = torch.empty(int(d_rb[n].item()) * 16 + 16, dtype=torch.uint8, device=dev)
-    ctx.decode_device(ob.SNAPPY, d_in.data_ptr(), d_off.data_ptr(), n, d_out.data_ptr(), d_oo.data_ptr(),
-                      d_meta.data_ptr(), d_rows.data_ptr(), d_rb.data_ptr())
+    ctx.set_stream(None)
+    d_in, d_off = sc.devbuf_from(ctx, blob), sc.devbuf_from(ctx, off)
+    d_oo, d_rb = sc.DevBuf(ctx, 8 * (n + 1)), sc.DevBuf(ctx, 8 * (n + 1))
+    d_sc = sc.DevBuf(ctx, sc.decode_scratch_bytes(n) + 64)
+    ctx.decode_plan_device(ob.SNAPPY, d_in.ptr, d_off.ptr, n, d_oo.ptr, d_rb.ptr, d_sc.ptr)
+    d_out = sc.DevBuf(ctx, d_oo.u64(n) + 16)
+    d_meta = sc.DevBuf(ctx, n * 16)
+    d_rows = sc.DevBuf(ctx, d_rb.u64(n) * 16 + 16)
+    ctx.decode_device(ob.SNAPPY, d_in.ptr, d_off.ptr, n, d_out.ptr, d_oo.ptr, d_meta.ptr, d_rows.ptr, d_rb.ptr)
     qb = [rng.randrange(n) for _ in range(500)]
     keys = [b"k%015d" % rng.randrange(38 * 50 + 40) for _ in qb]
     kd = np.frombuffer(b"".join(keys), np.uint8).copy()
-    ko = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.int64)
-    d_q = torch.from_numpy(np.array(qb, np.int32)).to(dev)
-    d_k = torch.from_numpy(kd).to(dev)
-    d_ko = torch.from_numpy(ko).to(dev)
-    d_res = torch.zeros(len(qb) * 16, dtype=torch.uint8, device=dev)
-    ctx.block_seek_device(d_out.data_ptr(), d_oo.data_ptr(), d_meta.data_ptr(), d_q.data_ptr(), d_k.data_ptr(),
-                          d_ko.data_ptr(), len(qb), d_res.data_ptr())
-    torch.cuda.synchronize()
-    got = np.frombuffer(d_res.cpu().numpy().tobytes(), sc.SEEK_DTYPE)
+    ko = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+    d_q, d_k, d_ko = sc.devbuf_from(ctx, np.array(qb, np.uint32)), sc.devbuf_from(ctx, kd), sc.devbuf_from(ctx, ko)
+    d_res = sc.DevBuf(ctx, len(qb) * 16)
+    cap = 4
+    d_warn = sc.DevBuf(ctx, len(qb) * cap * 16)
+    sc._check(sc.lib().slate_block_seek_warn_device(ctx.handle, d_out.ptr, d_oo.ptr, d_meta.ptr, d_q.ptr, d_k.ptr,
+                                                    d_ko.ptr, len(qb), d_res.ptr, d_warn.ptr, cap),
+              "slate_block_seek_warn_device")
+    got = d_res.download().view(sc.SEEK_DTYPE)
+    assert (d_warn.download().view(sc.SEEK_WARN_DTYPE)["kind"][: (got["n_warn"] > 0).sum()] >= 0).all()
+    # the plain device entry agrees with the warning variant
+    d_res2 = sc.DevBuf(ctx, len(qb) * 16)
+    ctx.block_seek_device(d_out.ptr, d_oo.ptr, d_meta.ptr, d_q.ptr, d_k.ptr, d_ko.ptr, len(qb), d_res2.ptr)
+    assert d_res2.download().tobytes() == d_res.download().tobytes()
     o_out, o_off, o_meta, _, _ = ob.block_decode_batch(ob.SNAPPY, blob, off)
     for i, (b, k) in enumerate(zip(qb, keys)):
         a, dl, nr = int(o_off[b]), int(o_meta["data_len"][b]), int(o_meta["n_rows"][b])

@@ -75,3 +75,37 @@ def test_index_seek_matches_bisect():
         keys = sorted({rng.randbytes(rng.randint(1, 6)) for _ in range(rng.randint(1, 40))})
         k = rng.randbytes(rng.randint(0, 6))
         assert ob.index_seek(keys, k) == max(0, bisect.bisect_right(keys, k) - 1)
+
+
+WARN_FORMATS = {1: "while peeking at key at offset {a}: {err}", 2: "unable to locate uncorrupted first key in block; "
+                "block is corrupt", 3: "block.Offset[{a}] = {b} is out of bounds", 4: "while peeking at block.Offset[{a}]: {err}"}
+
+
+def render_warnings(warns) -> str:
+    """types.ErrWarn.Error() (internal/types/errors.go:13-15) rebuilt from the warning records the
+    C-ABI returns (slate_seek_warn), as the cgo shim in INTEGRATION.md does."""
+    return "\n".join(WARN_FORMATS[k].format(a=a, b=b, err=ob.status_string(e)) for k, e, a, b in warns)
+
+
+def test_iterator_seek_warning_text(ref_vectors):
+    """The warning records reproduce the reference's ErrWarn text: the 'unable to locate' error of
+    the all-corrupt cases (block_test.go:416-466) and the first-key recovery warnings (:468-527)."""
+    for c in ref_vectors["iterator_seek_corrupt"]:
+        data, offs = _block(c["kvs"])
+        for r in c["corrupt"]:
+            data[0 if r == "data0" else offs[r]] = 0xFF
+        (st, start, fi, fl, nw), warns = ob.block_seek_warnings(bytes(data), offs, c["key"].encode())
+        assert len(warns) == nw, c["name"]
+        text = render_warnings(warns)
+        if "error" in c:
+            assert c["error"] in text and warns[-1][0] == 2, c["name"]
+        elif c["warnings"]:
+            assert nw > 0 and all(": corrupt v0 row: " in line for line in text.split("\n")), (c["name"], text)
+            if 0 in c["corrupt"] or "data0" in c["corrupt"]:
+                # firstFullKey skipped the corrupted first row: its 0xFF prefix-length byte
+                assert warns[0][0] == 1 and warns[0][2] == offs[0], c["name"]
+                assert text.startswith(f"while peeking at key at offset {offs[0]}: corrupt v0 row: "), text
+            else:  # sort.Search peeked at a corrupted row
+                assert warns[0][0] == 4, c["name"]
+        else:
+            assert nw == 0 and text == "", c["name"]

@@ -132,3 +132,50 @@ def test_sharded_decode_other_codecs(codec):
     _check_against_oracle(c, blob, off, got)
     for x in ctxs:
         x.close()
+
+
+def test_failed_batches_then_valid_batch_same_context():
+    """A batch that fails (decreasing offsets: SLATE_E_INVALID_ARG before any lane work; outputs too
+    small: SLATE_E_CAPACITY after planning every chunk) leaves nothing in flight on the context: the
+    next, smaller batch on it decodes exactly and writes nothing past its own outputs."""
+    import slatecodec as sc
+    ctx = sc.Context(0)
+    big = _mixed_batch(21, 3000)
+    blob, off = bg.pack(big, misalign=5)
+    n = len(off) - 1
+    bad = off.copy()
+    bad[n // 2] = bad[n // 2 + 1] + 7  # offset i > offset i+1
+    z = lambda k, dt: np.zeros(k, dt)  # noqa: E731
+    st = ctx.decode_batch_into(sc.SNAPPY, blob, bad, z(1 << 20, np.uint8), z(1 << 16, sc.ROW_DTYPE),
+                               z(n, sc.META_DTYPE), z(n + 1, np.uint64), z(n + 1, np.uint64))
+    assert st == sc.E_INVALID_ARG
+    st = ctx.decode_batch_into(sc.SNAPPY, blob, off, z(64, np.uint8), z(4, sc.ROW_DTYPE), z(n, sc.META_DTYPE),
+                               z(n + 1, np.uint64), z(n + 1, np.uint64))
+    assert st == sc.E_CAPACITY
+    small = big[:37]
+    sblob, soff = bg.pack(small, misalign=1)
+    m = len(soff) - 1
+    ref = ob.block_decode_batch(sc.SNAPPY, sblob, soff)
+    pad = 4096
+    out = np.full(int(ref[1][m]) + pad, 0xA5, np.uint8)
+    rows = np.zeros(int(ref[4][m]) + 64, sc.ROW_DTYPE)
+    rows["row_off"] = 0xDEADBEEF
+    meta = np.zeros(m, sc.META_DTYPE)
+    oo, rb = np.zeros(m + 1, np.uint64), np.zeros(m + 1, np.uint64)
+    assert ctx.decode_batch_into(sc.SNAPPY, sblob, soff, out, rows, meta, oo, rb) == sc.OK
+    _check_against_oracle(sc.SNAPPY, sblob, soff, (out, oo, meta, rows, rb))
+    assert (out[int(oo[m]) + 16:] == 0xA5).all(), "bytes written past the batch's outputs"
+    used = int(np.sum(np.where(meta["status"] == 0, meta["n_rows"].astype(np.int64), 0)))
+    assert (rows["row_off"][int(rb[m]):] == 0xDEADBEEF).all() and used <= int(rb[m])
+
+
+def test_sharded_rejects_duplicate_context():
+    import slatecodec as sc
+    ctx = sc.Context(0)
+    blocks = _mixed_batch(3, 100)
+    blob, off = bg.pack(blocks)
+    n = len(off) - 1
+    st = sc.decode_sharded_into([ctx, ctx], sc.SNAPPY, blob, off, np.zeros(1 << 20, np.uint8),
+                                np.zeros(1 << 15, sc.ROW_DTYPE), np.zeros(n, sc.META_DTYPE), np.zeros(n + 1, np.uint64),
+                                np.zeros(n + 1, np.uint64))
+    assert st == sc.E_INVALID_ARG

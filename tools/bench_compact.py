@@ -49,26 +49,23 @@ def main():
     ap.add_argument("--max-sst", type=int, default=256 << 20)
     ap.add_argument("--steps", type=int, default=3)
     args = ap.parse_args()
-    import torch
-    torch.cuda.set_device(0)
     import slatecodec as sc
     from slatecodec import compaction
     codec = sc.SNAPPY if args.codec == "snappy" else sc.NONE
     ctx = sc.Context(0)
-    dev = torch.device("cuda:0")
     srcs = make_sources(sc, ctx, args.k, args.kv, args.overlap, codec)
     in_bytes = sum(len(s) for run in srcs for s in run)
     compaction.compact(ctx, srcs, args.max_sst, codec=codec)  # warm-up
     dev_s, all_s, stages = [], [], {}
     for _ in range(args.steps):
-        torch.cuda.synchronize()
+        ctx.synchronize()
         t0 = time.perf_counter()
         prof = []
-        view = compaction.decode_rows_kv(ctx, srcs, dev, prof)
-        merged = compaction.merge_kv(ctx, view, dev, prof)
+        view, src_start = compaction.decode_rows_kv(ctx, srcs, prof)
+        merged = compaction.merge_kv(ctx, view, src_start, prof)
         for (_, a), (lb, b) in zip(prof, prof[1:]):
             stages[lb] = min(stages.get(lb, 1e9), round(b - a, 5))
-        torch.cuda.synchronize()
+        ctx.synchronize()
         dev_s.append(time.perf_counter() - t0)
         del view, merged
         t0 = time.perf_counter()

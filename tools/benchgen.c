@@ -428,3 +428,13 @@ int64_t bg_verify_set(uint64_t seed, int half, uint64_t block_size, uint64_t i_b
   for (int t = 0; t < nthreads; t++) { pthread_join(th[t], NULL); bad += jobs[t].bad; }
   return bad;
 }
+
+/* Blocks whose decoded bytes (out[out_off[i] ..], dec_off[i+1] - dec_off[i] bytes) differ from the
+ * blocks before encoding (dec[dec_off[i] ..]): bench.py's configs[4] check. */
+int64_t bg_compare_blocks(const uint8_t* out, const uint64_t* out_off, const uint8_t* dec, const uint64_t* dec_off,
+                          uint64_t n) {
+  int64_t bad = 0;
+  for (uint64_t i = 0; i < n; i++)
+    if (memcmp(out + out_off[i], dec + dec_off[i], dec_off[i + 1] - dec_off[i]) != 0) bad++;
+  return bad;
+}

@@ -46,6 +46,24 @@ def main():
            "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
            "hbm_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024),
            "note": "2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md)"}
+    # SQ counters per launch of the same kernel and build, and per decoded block
+    sq = {}
+    for grp in ("sq1", "sq2"):
+        path = os.path.join(out, grp, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        names = {r["Counter_Name"] for r in csv.DictReader(open(path))}
+        for c in sorted(names):
+            v = per_dispatch(path, c, kernel)
+            if v:
+                sq[c] = max(v.values())
+    if sq:
+        nb = float(res["blocks"])
+        res["sq_per_launch"] = sq
+        res["sq_per_block"] = {k: round(v / nb, 2) for k, v in sq.items()}
+        if sq.get("SQ_WAVE_CYCLES"):
+            res["sq_fractions"] = {k + "/SQ_WAVE_CYCLES": round(sq[k] / sq["SQ_WAVE_CYCLES"], 4)
+                                   for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY") if k in sq}
     dst = os.path.join(REPO, "profiles", "pmc_decode_latest.json")
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res))

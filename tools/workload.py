@@ -45,6 +45,8 @@ def lib():
         L.bg_verify_set.restype = C.c_int64
         L.bg_verify_set.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.bg_compare_blocks.restype = C.c_int64
+        L.bg_compare_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
         L.bg_build_mixed.restype = C.c_uint64
         L.bg_build_mixed.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64]
         _lib = L
@@ -137,3 +139,11 @@ def verify_set(i_begin: int, stride: int, count: int, out: np.ndarray, out_off: 
     return int(lib().bg_verify_set(seed, int(half), block_size, i_begin, stride, count, out.ctypes.data,
                                    out_off.ctypes.data, rows.ctypes.data, row_base.ctypes.data, meta.ctypes.data,
                                    threads))
+
+
+def compare_blocks(out: np.ndarray, out_off: np.ndarray, dec: np.ndarray, dec_off: np.ndarray) -> int:
+    """Blocks whose decoded bytes (at out[out_off[i]:]) differ from dec's block i."""
+    out_off = np.ascontiguousarray(out_off, np.uint64)
+    dec_off = np.ascontiguousarray(dec_off, np.uint64)
+    return int(lib().bg_compare_blocks(out.ctypes.data, out_off.ctypes.data, dec.ctypes.data, dec_off.ctypes.data,
+                                       len(dec_off) - 1))
