@@ -237,7 +237,7 @@ def main():
         # the kernel's rate against a device-to-device copy measured on this box too
         copy = measured_copy_gbps(device)
         roofline["measured_copy_GBps"] = round(copy, 1)
-        roofline["frac_of_measured_copy"] = round(achieved / copy, 4)
+        roofline["frac_of_measured_copy"] = round(roofline["achieved"] / copy, 4)
 
     if rank == 0 and world == 1 and not args.no_host_io and shard is not None:
         result["host_io"] = host_io_rate(sc, ctx, codec, blob, in_off)
