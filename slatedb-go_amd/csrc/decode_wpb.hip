@@ -56,16 +56,65 @@ constexpr uint32_t kMaxPieces = 320;
 constexpr uint32_t kWpbInCap = 4240;
 constexpr uint32_t kWpbOutCap = 4240;
 constexpr uint32_t kGuard = 16;
-constexpr uint32_t kWaveLds = kGuard + kWpbInCap + kGuard + kWpbOutCap + kMaxPieces * 8;
+constexpr uint32_t kMaxGroups = kMaxPieces;
+// per wave: guard | IN | guard | OUT | pieces (8 B) | group starts (u16, + 1 sentinel) | junk
+// (one dword per lane: where a lane's store goes when it has nothing to store)
+constexpr uint32_t kWaveLds =
+    kGuard + kWpbInCap + kGuard + kWpbOutCap + kMaxPieces * 8 + ((2 * (kMaxGroups + 1) + 15) & ~15u) + 64 * 4;
 constexpr uint32_t kBuildWaves = 2;   // waves per workgroup of the build kernel
 
 // ---- W: lane per block
-constexpr uint32_t kWalkThreads = 512;  // 8 waves: one workgroup (16 KiB tables + 8 x 16.5 KiB rings) per CU
-constexpr uint32_t kWNS = 16;                  // input ring slots (16 bytes each)
+constexpr uint32_t kWalkThreads = 256;         // 4 waves; three workgroups per CU (VGPRs: 3 waves per SIMD)
+constexpr uint32_t kWNS = 8;                   // input ring slots (16 bytes each)
 constexpr uint32_t kWIR = kWNS * 16;           // ring bytes
-constexpr uint32_t kWStride = kWIR + 8;        // lane records 264 bytes apart (bank spread)
-constexpr uint32_t kWSteps = 8;                // tags parsed per iteration
-constexpr uint32_t kWChunks = 8;               // CRC chunks absorbed per iteration (= refill rate)
+constexpr uint32_t kWStride = kWIR + 8;        // lane records 136 bytes apart (bank spread)
+constexpr uint32_t kWSteps = 4;                // tags parsed per iteration
+constexpr uint32_t kWChunks = 4;               // CRC chunks absorbed per iteration (= refill rate)
+
+// CRC32 by 6-bit digits.  A 16-byte chunk is 128 message bits; digit k (bits 6k .. 6k+5, 22
+// digits) contributes T6[k][digit], the XOR of the slicing-by-16 entries of its bits.  A 64-entry
+// table fills the 64 LDS banks exactly once, so 64 lanes reading it never conflict (distinct
+// entries sit in distinct banks, equal ones broadcast): the byte tables' random lookups cost the
+// walk ~200 bank-conflict cycles per block (SQ_LDS_BANK_CONFLICT).
+constexpr uint32_t kCrc6Digits = 22;
+struct Crc6Tables {
+  uint32_t t[kCrc6Digits][64];
+  constexpr Crc6Tables() : t{} {
+    uint32_t c8[16][256] = {};
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ kCrcPoly : c >> 1;
+      c8[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; i++)
+      for (int q = 1; q < 16; q++) c8[q][i] = (c8[q - 1][i] >> 8) ^ c8[0][c8[q - 1][i] & 0xFF];
+    for (uint32_t k = 0; k < kCrc6Digits; k++)
+      for (uint32_t v = 0; v < 64; v++) {
+        uint32_t r = 0;
+        for (uint32_t bt = 0; bt < 6; bt++) {
+          const uint32_t b = 6 * k + bt;
+          if (b < 128 && ((v >> bt) & 1)) r ^= c8[15 - b / 8][1u << (b % 8)];
+        }
+        t[k][v] = r;
+      }
+  }
+};
+static __constant__ Crc6Tables g_crc6 = Crc6Tables();
+constexpr uint32_t kTab6Bytes = kCrc6Digits * 64 * 4;
+
+// the CRC register after the 16 bytes v (little-endian dwords)
+__device__ __forceinline__ uint32_t crc6_chunk(const uint32_t* tab, uint32_t c, const v4u& v) {
+  const uint32_t x = v.x ^ c, y = v.y, z = v.z, w = v.w;
+  const uint32_t xy = __builtin_amdgcn_alignbit(y, x, 30), yz = __builtin_amdgcn_alignbit(z, y, 28);
+#define D6(k, src, off) tab[64 * (k) + (((src) >> (off)) & 63u)]
+  const uint32_t a = xor3(D6(0, x, 0), D6(1, x, 6), D6(2, x, 12)), b = xor3(D6(3, x, 18), D6(4, x, 24), D6(5, xy, 0));
+  const uint32_t e = xor3(D6(6, y, 4), D6(7, y, 10), D6(8, y, 16)), f = xor3(D6(9, y, 22), D6(10, yz, 0), D6(11, z, 2));
+  const uint32_t g = xor3(D6(12, z, 8), D6(13, z, 14), D6(14, z, 20)), h = xor3(D6(15, z, 26), D6(16, w, 0), D6(17, w, 6));
+  const uint32_t i = xor3(D6(18, w, 12), D6(19, w, 18), D6(20, w, 24));
+  const uint32_t j = tab[64 * 21 + (w >> 30)];
+#undef D6
+  return xor3(xor3(a, b, e), xor3(f, g, h), xor3(i, j, 0u));
+}
 
 struct Walk {
   uint32_t sh, clen, last_chunk, dn, s, d, err, dd, hdr;
@@ -73,7 +122,12 @@ struct Walk {
   uint32_t crc, crc_pos;
   uint32_t c_issue, c_commit, n_req;
   uint32_t ntags, pieces, nanch;
-  v4u abuf;  // two anchors waiting for one 16-byte store
+  // D's execution groups, decided here in tag order (see "Groups" above): the previous tag
+  // (literal-sourced?, its output range), the open group's first output byte and used slots
+  uint32_t p_lit, p_d, p_len, g, slots;
+  // anchors: the open one (cur), a completed even one waiting for its pair (pend), and one
+  // completed in this iteration (fin, index fin_i; fin_v set)
+  uint32_t cur_x, cur_y, pend_x, pend_y, fin_x, fin_y, fin_i, fin_v;
 };
 
 // CRC32 of the next committed input chunk (bytes outside the block zeroed) -- as decode_lpb2.hip
@@ -88,16 +142,16 @@ __device__ __forceinline__ void walk_crc(Walk& L, const uint8_t* in, const uint3
     v.z &= keep_mask(lo, hi, 2);
     v.w &= keep_mask(lo, hi, 3);
   }
-  const uint32_t c = crc16_chunk(tab, L.crc, v);
+  const uint32_t c = crc6_chunk(tab, L.crc, v);
   L.crc = go ? c : L.crc;
   L.crc_pos += go ? 1u : 0u;
 }
 
-// Transposed refill: in load j (0..7), lanes 8i..8i+7 read chunks c_issue..c_issue+7 (one
-// 128-byte run) of the block of lane 8j+i; the chunk goes into that block's ring next iteration.
+// Transposed refill: in load j (0..3), lanes 4i..4i+3 read chunks c_issue..c_issue+3 (one
+// 64-byte run) of the block of lane 16j+i; the chunk goes into that block's ring next iteration.
 __device__ __forceinline__ void walk_load(uint32_t j, uint32_t lane, uint32_t wave_lane0, uint32_t info, uint32_t rel,
                                           __amdgpu_buffer_rsrc_t rin, v4u& P, uint32_t& slot) {
-  const uint32_t o = 8 * j + (lane >> 3), c = lane & 7;
+  const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
   const uint32_t info_o = __shfl(info, int(o), 64);
   const uint32_t rel_o = __shfl(rel, int(o), 64);
   const uint32_t ci = (info_o >> 4) + c;
@@ -114,13 +168,13 @@ __global__ __launch_bounds__(kWalkThreads) void snappy_walk_kernel(const uint8_t
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   {
-    const uint32_t* src = &g_crc16.t[0][0];
-    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
+    const uint32_t* src = &g_crc6.t[0][0];
+    for (uint32_t i = threadIdx.x; i < kCrc6Digits * 64; i += blockDim.x) tab[i] = src[i];
     __syncthreads();
   }
   const uint32_t* crc_init = g_crc_lt.init;
   const uint32_t* crc_tail = g_crc_lt.tail;
-  uint8_t* rings = smem + kTab16Bytes;
+  uint8_t* rings = smem + kTab6Bytes;
   uint8_t* in = rings + threadIdx.x * kWStride;
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave_lane0 = threadIdx.x - lane;
@@ -140,7 +194,9 @@ __global__ __launch_bounds__(kWalkThreads) void snappy_walk_kernel(const uint8_t
     L.crc = 0xFFFFFFFFu;
     L.crc_pos = L.c_issue = L.c_commit = L.n_req = 0;
     L.ntags = L.pieces = L.nanch = 0;
-    L.abuf = v4u{0, 0, 0, 0};
+    L.p_lit = L.p_d = L.p_len = L.g = 0;
+    L.slots = 4;  // the first tag opens a group
+    L.cur_x = L.cur_y = L.pend_x = L.pend_y = L.fin_x = L.fin_y = L.fin_i = L.fin_v = 0;
     uint32_t rel = 0;
     bool have = b < rend;
     if (have) {
@@ -191,10 +247,10 @@ __global__ __launch_bounds__(kWalkThreads) void snappy_walk_kernel(const uint8_t
         }
       }
     }
-    v4u P[8];
-    uint32_t S[8];
+    v4u P[4];
+    uint32_t S[4];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
+    for (int j = 0; j < 4; j++) {
       P[j] = v4u{0, 0, 0, 0};
       S[j] = 0xFFFFFFFFu;
     }
@@ -203,17 +259,17 @@ __global__ __launch_bounds__(kWalkThreads) void snappy_walk_kernel(const uint8_t
     auto lane_done = [&]() { return L.dd && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk; };
     while (__ballot(have && !lane_done() && iters < budget)) {
       const bool act = have && !lane_done() && iters < budget;
-      // the chunks loaded last iteration go into their rings; ask for up to 8 more
+      // the chunks loaded last iteration go into their rings; ask for up to 4 more
 #pragma unroll
-      for (int j = 0; j < 8; j++)
+      for (int j = 0; j < 4; j++)
         if (S[j] != 0xFFFFFFFFu) wr128(rings + S[j], P[j], 0u);
       L.c_commit += L.n_req;
       const uint32_t lo_chunk = min((L.sh + (L.dd ? L.clen : L.s)) >> 4, L.crc_pos);
       const uint32_t room = lo_chunk + kWNS - L.c_issue, left = L.last_chunk + 1 - L.c_issue;
-      const uint32_t nq = act ? min(min(room, left), 8u) : 0u;
+      const uint32_t nq = act ? min(min(room, left), 4u) : 0u;
       const uint32_t info = (L.c_issue << 4) | nq;
 #pragma unroll
-      for (uint32_t j = 0; j < 8; j++) walk_load(j, lane, wave_lane0, info, rel, rin, P[j], S[j]);
+      for (uint32_t j = 0; j < 4; j++) walk_load(j, lane, wave_lane0, info, rel, rin, P[j], S[j]);
       L.c_issue += nq;
       L.n_req = nq;
       // CRC of the committed chunks
@@ -248,25 +304,59 @@ __global__ __launch_bounds__(kWalkThreads) void snappy_walk_kernel(const uint8_t
         L.err |= (can && bad) ? 1u : 0u;
         L.dd |= (fin || (can && bad)) ? 1u : 0u;
         const uint32_t len = t == 0 ? uint32_t(lit_len) : cp_len;
-        // every 8th tag: an anchor (input offset, decoded offset, first piece)
-        const bool anc = ok && (L.ntags & (kAnchorTags - 1)) == 0 && L.nanch < kMaxAnchors;
-        const uint32_t a0 = (L.s & 0xffff) | (L.d << 16);
-        const bool hi_half = (L.nanch & 1) != 0;
-        L.abuf.x = (anc && !hi_half) ? a0 : L.abuf.x;
-        L.abuf.y = (anc && !hi_half) ? L.pieces : L.abuf.y;
-        L.abuf.z = (anc && hi_half) ? a0 : L.abuf.z;
-        L.abuf.w = (anc && hi_half) ? L.pieces : L.abuf.w;
-        L.nanch += anc ? 1u : 0u;
+        // ---- D's groups (mirrored exactly by snappy_build_kernel's replay): a tag joins the open
+        // group when its source bytes are final before the group's first output byte and a slot is
+        // left; a copy whose source lies inside the previous literal-sourced tag reads that tag's
+        // input (not across anchors: D's lane starts each anchor without a previous tag)
+        const uint32_t tix = L.ntags;
+        const bool first_of_anchor = (tix & (kAnchorTags - 1)) == 0;
+        const uint32_t so = L.d - cp_off;
+        const bool ovl = t != 0 && cp_off < len;
+        const bool comp = t != 0 && !ovl && L.p_lit && !first_of_anchor && so >= L.p_d && so + len <= L.p_d + L.p_len;
+        const bool lsrc = t == 0 || comp;
+        const uint32_t np = (len + kPiece - 1) / kPiece;
+        const bool join = !ovl && L.slots < 4 && (lsrc || so + len <= L.g);
+        const uint32_t s0 = join ? L.slots : 0u;
+        const uint32_t tot = s0 + np;
+        const uint32_t nslots = ovl ? 4u : ((tot - 1) & 3) + 1;
+        const uint32_t ng = ovl ? L.g : (tot > 4 ? L.d + kPiece * (np - nslots) : (join ? L.g : L.d));
+        // every 8th tag opens an anchor (input offset, decoded offset, first piece, open slots);
+        // the tags' group-start and slow bits complete it
+        const bool opn = ok && first_of_anchor && L.nanch < kMaxAnchors;
+        const bool cls = opn && tix > 0;
+        L.fin_x = cls ? L.cur_x : L.fin_x;
+        L.fin_y = cls ? L.cur_y : L.fin_y;
+        L.fin_i = cls ? L.nanch - 1 : L.fin_i;
+        L.fin_v |= cls ? 1u : 0u;
+        L.cur_x = opn ? ((L.s & 0xffff) | (L.d << 16)) : L.cur_x;
+        L.cur_y = opn ? (L.pieces | (L.slots << 10)) : L.cur_y;
+        L.nanch += opn ? 1u : 0u;
+        const uint32_t bit = tix & (kAnchorTags - 1);
+        L.cur_y |= (ok && !join) ? (1u << (16 + bit)) : 0u;
+        L.cur_y |= (ok && ovl) ? (1u << (24 + bit)) : 0u;
+        L.slots = ok ? nslots : L.slots;
+        L.g = ok ? ng : L.g;
+        L.p_lit = ok ? uint32_t(lsrc) : L.p_lit;
+        L.p_d = ok ? L.d : L.p_d;
+        L.p_len = ok ? len : L.p_len;
         L.ntags += ok ? 1u : 0u;
-        L.pieces += ok ? (len + kPiece - 1) / kPiece : 0u;
+        L.pieces += ok ? np : 0u;
         L.s = ok ? (t == 0 ? s1 + len : s1) : L.s;
         L.d += ok ? len : 0u;
       }
-      // a completed pair of anchors: one 16-byte store (at most one pair per iteration)
-      const bool pair = act && (L.nanch & 1) == 0 && L.nanch > 0 && L.abuf.x != 0xFFFFFFFFu;
-      __builtin_amdgcn_raw_buffer_store_b128(L.abuf, rrec, pair ? lane * kWpbRecBytes + 16 + 8 * (L.nanch - 2) : kOOB,
+      // an anchor completed in this iteration (at most one: 8 tags per anchor, kWSteps per
+      // iteration): an even one waits for its partner, an odd one is stored with it (16 bytes)
+      const bool st_pair = L.fin_v && (L.fin_i & 1);
+      v4u pr;
+      pr.x = L.pend_x;
+      pr.y = L.pend_y;
+      pr.z = L.fin_x;
+      pr.w = L.fin_y;
+      __builtin_amdgcn_raw_buffer_store_b128(pr, rrec, st_pair ? lane * kWpbRecBytes + 16 + 8 * (L.fin_i - 1) : kOOB,
                                              0, 0);
-      L.abuf.x = pair ? 0xFFFFFFFFu : L.abuf.x;  // stored
+      L.pend_x = (L.fin_v && !(L.fin_i & 1)) ? L.fin_x : L.pend_x;
+      L.pend_y = (L.fin_v && !(L.fin_i & 1)) ? L.fin_y : L.pend_y;
+      L.fin_v = 0;
       iters++;
     }
     if (b < rend) {
@@ -281,10 +371,15 @@ __global__ __launch_bounds__(kWalkThreads) void snappy_walk_kernel(const uint8_t
       // what D takes: the block and its output fit its LDS staging, the tags its anchors
       okb = okb && L.dn >= 2 && L.sh + L.clen <= kWpbInCap && L.dn + 16 <= kWpbOutCap && L.ntags <= kMaxTags &&
             L.pieces <= kMaxPieces;
-      // an unpaired last anchor
-      const bool odd = (L.nanch & 1) != 0;
-      __builtin_amdgcn_raw_buffer_store_b128(L.abuf, rrec, (okb && odd) ? lane * kWpbRecBytes + 16 + 8 * (L.nanch - 1)
-                                                                         : kOOB, 0, 0);
+      // the last (open) anchor: with its waiting partner, or alone
+      const uint32_t li = L.nanch - 1;
+      v4u pr;
+      pr.x = (li & 1) ? L.pend_x : L.cur_x;
+      pr.y = (li & 1) ? L.pend_y : L.cur_y;
+      pr.z = L.cur_x;
+      pr.w = L.cur_y;
+      __builtin_amdgcn_raw_buffer_store_b128(pr, rrec, (okb && L.nanch) ? lane * kWpbRecBytes + 16 + 8 * (li & ~1u)
+                                                                       : kOOB, 0, 0);
       v4u h;
       h.x = (okb ? kWpbD : 0u) | (L.ntags << 16);
       h.y = L.dn;
@@ -306,14 +401,48 @@ __device__ __forceinline__ uint32_t bswap16_lo(uint32_t w) { return ((w & 0xff) 
 
 }  // namespace
 
-// D: one wave per block.  LDS per wave: [guard | IN | guard | OUT | pieces].
+// D: one wave per block.
+// Piece record (8 bytes): x = output offset | length << 16 | group start << 24 | slow << 25,
+// y = LDS address of the source byte (IN for literal-sourced pieces, OUT for copies).
+constexpr uint32_t kPieceGs = 1u << 24, kPieceSlow = 1u << 25;
+
+// Stores of a unit that holds bytes [lo, hi) of its dword (lo 0..3, hi 1..4), one nibble per
+// (lo, hi) at 4 * (4 lo + hi - 1): bit 0 = a b16 store (at byte 0 when lo == 0, else at 2), bit 1
+// = a b8 store, bits 2-3 its byte.  [0,4) is one b32 store.  The b16 of [1,3) also writes byte 3,
+// which belongs to a later piece: that piece's first unit is [3, 4), a b8 store, issued after
+// every b16 store of the group (or in a later group).
+constexpr uint64_t partial_stores_table() {
+  uint64_t t = 0;
+  for (uint32_t lo = 0; lo < 4; lo++)
+    for (uint32_t hi = lo + 1; hi <= 4; hi++) {
+      if (lo == 0 && hi == 4) continue;
+      const bool pair0 = lo == 0 && hi >= 2;        // bytes 0, 1
+      const bool pair2 = lo >= 1 && lo <= 2 && hi >= 3 && !(lo == 2 && hi == 3);  // bytes 2, 3
+      const uint32_t b16 = (pair0 || pair2) ? 1u : 0u;
+      // the byte a b16 does not cover
+      uint32_t a8 = 4;
+      if (lo == 0 && hi == 1) a8 = 0;
+      else if (lo == 0 && hi == 3) a8 = 2;
+      else if (lo == 1) a8 = 1;
+      else if (lo == 2 && hi == 3) a8 = 2;
+      else if (lo == 3) a8 = 3;
+      const uint32_t nib = b16 | (a8 < 4 ? 2u | (a8 << 2) : 0u);
+      t |= uint64_t(nib) << (4 * (4 * lo + hi - 1));
+    }
+  return t;
+}
+constexpr uint64_t kPartialStores = partial_stores_table();
+
 __global__ __launch_bounds__(64 * kBuildWaves) void snappy_build_kernel(DecodeArgs a, uint8_t* __restrict__ rec,
                                                                          uint32_t* block_counter) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* const lds = smem;  // addresses below are byte offsets from smem
   const uint32_t IN = wave * kWaveLds + kGuard, OUT = IN + kWpbInCap + kGuard, OPS = OUT + kWpbOutCap;
+  const uint32_t GRP = OPS + kMaxPieces * 8, JUNK = GRP + ((2 * (kMaxGroups + 1) + 15) & ~15u);
   uint2* const ops = reinterpret_cast<uint2*>(lds + OPS);
+  uint16_t* const grp = reinterpret_cast<uint16_t*>(lds + GRP);
+  const uint32_t junk = JUNK + 4 * lane;
   // blocks by a static stride: an atomic counter per block serialises on one L2 address (1 M of
   // them took longer than the decode)
   const uint32_t waves_total = gridDim.x * kBuildWaves;
@@ -333,45 +462,57 @@ __global__ __launch_bounds__(64 * kBuildWaves) void snappy_build_kernel(DecodeAr
       const uint32_t nch = (sh + clen + 15) >> 4;
       for (uint32_t c = lane; c < nch; c += 64) *reinterpret_cast<uint4*>(lds + IN + 16 * c) = g[c];
     }
-    // this lane's anchor
     uint2 anc = uint2{0, 0};
     if (lane < nanch) anc = *reinterpret_cast<const uint2*>(rec + size_t(b) * kWpbRecBytes + 16 + 8 * lane);
-    __builtin_amdgcn_s_waitcnt(0);  // (vmcnt/lgkmcnt: the staged bytes are in LDS)
+    __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    // ---- pieces: lane a re-parses tags 8a .. 8a+7 (W validated every one of them)
+    // ---- pieces: lane a re-parses tags 8a .. 8a+7 (W validated every one of them) and replays
+    // W's group decisions from the anchor's group-start / slow bits and open slots
     {
-      uint32_t s = anc.x & 0xffff, d = anc.x >> 16, p = anc.y;
-      uint32_t pl_dst = 0, pl_len = 0, pl_src = 0;  // the previous tag when it is literal-sourced
+      uint32_t s = anc.x & 0xffff, d = anc.x >> 16, p = anc.y & 0x3ff, slots = (anc.y >> 10) & 7;
+      uint32_t pl_dst = 0, pl_len = 0, pl_src = 0;
       bool plit = false;
-      const uint32_t t_end = min(ntags, kAnchorTags * (lane + 1));
-      for (uint32_t t = kAnchorTags * lane; t < t_end; t++) {
-        const uint32_t w0 = lds_at(lds, IN + sh + s), w1 = lds_at(lds, IN + sh + s + 4);
+      const uint32_t t0 = kAnchorTags * lane, t_end = min(ntags, t0 + kAnchorTags);
+      for (uint32_t t = t0; t < t_end; t++) {
+        // the tag's first bytes: three aligned dwords
+        const uint32_t a0 = IN + sh + s;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (a0 & ~3u));
+        const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, a0 & 3u), w1 = __builtin_amdgcn_alignbyte(d2, d1, a0 & 3u);
         const uint32_t c = w0 & 0xff, tt = c & 3;
         const uint32_t b14 = (w0 >> 8) | (w1 << 24);
         const uint32_t xl = c >> 2;
         const uint32_t nb = xl >= 60 ? xl - 59 : 0;
         const uint32_t ext = nb >= 4 ? b14 : (b14 & ((1u << (8 * nb)) - 1));
-        uint32_t len, src, hl;
-        bool lit;
-        if (tt == 0) {
-          hl = 1 + nb;
-          len = (nb ? ext : xl) + 1;
-          src = IN + sh + s + hl;
-          lit = true;
-        } else {
-          len = (tt == 1) ? 4 + ((c >> 2) & 7) : 1 + (c >> 2);
-          const uint32_t off = (tt & 2) ? ((tt & 1) ? b14 : (b14 & 0xffff)) : (((c & 0xe0) << 3) | (b14 & 0xff));
-          hl = (tt & 2) ? ((tt & 1) ? 5u : 3u) : 2u;
-          const uint32_t so = d - off;
-          // a copy of bytes the previous (literal-sourced) tag produced reads that tag's input
-          lit = plit && so >= pl_dst && so + len <= pl_dst + pl_len;
-          src = lit ? pl_src + (so - pl_dst) : OUT + so;
+        const uint32_t cp_len = (tt == 1) ? 4 + ((c >> 2) & 7) : 1 + (c >> 2);
+        const uint32_t off = (tt & 2) ? ((tt & 1) ? b14 : (b14 & 0xffff)) : (((c & 0xe0) << 3) | (b14 & 0xff));
+        const uint32_t hl = tt == 0 ? 1 + nb : ((tt & 2) ? ((tt & 1) ? 5u : 3u) : 2u);
+        const uint32_t len = tt == 0 ? (nb ? ext : xl) + 1 : cp_len;
+        const uint32_t so = d - off;
+        // a copy of bytes the previous (literal-sourced) tag of this anchor produced reads its input
+        const bool comp = tt != 0 && plit && so >= pl_dst && so + len <= pl_dst + pl_len;
+        const bool lsrc = tt == 0 || comp;
+        const uint32_t src = tt == 0 ? IN + sh + s + hl : (comp ? pl_src + (so - pl_dst) : OUT + so);
+        const uint32_t bit = t - t0;
+        const bool brk = (anc.y >> (16 + bit)) & 1, slow = (anc.y >> (24 + bit)) & 1;
+        const uint32_t s0g = brk ? 0u : slots;
+        const uint32_t np = (len + kPiece - 1) / kPiece;
+        // first piece (every tag has one); more only for tags longer than kPiece
+        {
+          const bool gs = slow || ((s0g & 3) == 0);
+          ops[p] = uint2{d | (min(kPiece, len) << 16) | (gs ? kPieceGs : 0u) | (slow ? kPieceSlow : 0u), src};
         }
-        for (uint32_t q = 0; q < len; q += kPiece) {
-          const uint32_t pn = min(kPiece, len - q);
-          ops[p++] = uint2{(d + q) | (pn << 16), src + q};
+        if (__builtin_expect(np > 1, 0)) {
+          for (uint32_t q = 1; q < np; q++) {
+            const bool gs = slow || (((s0g + q) & 3) == 0);
+            ops[p + q] = uint2{(d + kPiece * q) | (min(kPiece, len - kPiece * q) << 16) | (gs ? kPieceGs : 0u) |
+                                   (slow ? kPieceSlow : 0u),
+                               src + kPiece * q};
+          }
         }
-        plit = lit;
+        p += np;
+        slots = slow ? 4u : ((s0g + np - 1) & 3) + 1;
+        plit = lsrc;
         pl_dst = d;
         pl_len = len;
         pl_src = src;
@@ -381,58 +522,59 @@ __global__ __launch_bounds__(64 * kBuildWaves) void snappy_build_kernel(DecodeAr
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    // ---- execute the pieces: up to four per group, 16 lanes (4 bytes each) per piece
+    // ---- the group list: starts of groups, in piece order, + a sentinel
+    uint32_t ngroups = 0;
+    for (uint32_t i0 = 0; i0 < npieces; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool gs = i < npieces && (ops[i].x & kPieceGs);
+      const uint64_t m = __ballot(gs);
+      if (gs) grp[ngroups + __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u))] =
+          uint16_t(i);
+      ngroups += uint32_t(__builtin_popcountll(m));
+    }
+    if (lane == 0) grp[ngroups] = uint16_t(npieces);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    // ---- execute the groups: up to four pieces each, 16 lanes (4 bytes each) per piece; every
+    // store is issued by every lane (to its junk dword when it has nothing to store)
     {
-      const uint32_t j = lane >> 4, u = lane & 15;
-      uint32_t k = 0;
-      while (k < npieces) {
-        const bool have = k + j < npieces;
-        const uint2 r = ops[have ? k + j : k];
-        const uint32_t dst = r.x & 0xffff, len = r.x >> 16, src = r.y;
-        const uint32_t g = __builtin_amdgcn_readfirstlane(dst);  // the group starts at slot 0's output
-        // a piece may join the group when its source bytes were final before the group began
-        const bool valid = have && src + len <= OUT + g;
-        const uint64_t vb = __ballot(valid);
-        if (!(vb & 1)) {
-          // slot 0 copies from itself (offset < length): bytes [dst - off, dst) are final and
-          // the pattern repeats with period off; one byte per lane
-          const uint32_t dst0 = g, src0 = __builtin_amdgcn_readfirstlane(src);
-          const uint32_t off = OUT + dst0 - src0;
+      const uint32_t j = lane >> 4, u4 = 4 * (lane & 15);
+      for (uint32_t gi = 0; gi < ngroups; gi++) {
+        const uint32_t k0 = grp[gi], cnt = grp[gi + 1] - k0;  // uniform reads
+        const bool have = j < cnt;
+        const uint2 r = ops[k0 + (have ? j : 0u)];
+        const uint32_t dst = r.x & 0xffff, len = (r.x >> 16) & 0xff, src = r.y;
+        if (__builtin_amdgcn_readfirstlane(r.x) & kPieceSlow) {
+          // a copy from itself (offset < length): bytes [dst - off, dst) are final and the pattern
+          // repeats with period off; one byte per lane
+          const uint32_t dst0 = __builtin_amdgcn_readfirstlane(dst), src0 = __builtin_amdgcn_readfirstlane(src);
           const uint32_t len0 = __builtin_amdgcn_readfirstlane(len);
+          const uint32_t off = OUT + dst0 - src0;
           const float rcp = 1.0f / float(off);
-          for (uint32_t i0 = 0; i0 < len0; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const uint32_t qq = uint32_t((float(i) + 0.5f) * rcp);
-            const uint32_t m = i - qq * off;
-            if (i < len0) lds[OUT + dst0 + i] = lds[src0 + m];
-            __builtin_amdgcn_s_waitcnt(0);
-          }
-          k += 1;
+          const uint32_t i = lane;
+          const uint32_t qq = uint32_t((float(i) + 0.5f) * rcp);
+          const uint32_t m = i - qq * off;
+          const uint8_t v = lds[src0 + m];
+          lds[i < len0 ? OUT + dst0 + i : junk] = v;
           continue;
         }
-        // leading valid slots (bits 0, 16, 32, 48)
-        const uint32_t sl = uint32_t(vb & 1) | uint32_t((vb >> 15) & 2) | uint32_t((vb >> 30) & 4) |
-                            uint32_t((vb >> 45) & 8);
-        const uint32_t nv = __builtin_ctz(~sl);  // 1..4
-        const uint32_t dws = dst & ~3u, ua = dws + 4 * u;
-        const uint32_t first = max(dst, ua), end = min(dst + len, ua + 4);
-        const bool mine = j < nv && first < end;
-        const uint32_t sa = src + ua - dst;  // source of the unit's byte 0 (may precede src by < 4)
-        const uint32_t v = lds_at(lds, sa);
-        const uint32_t lo = first - ua, hi = end - ua;
-        const bool full = mine && lo == 0 && hi == 4;
-        // partial units: one b16 and one b8 cover every byte range of a dword
-        const bool b16 = mine && !full && ((lo == 0 && hi >= 2) || (lo <= 2 && hi == 4) || (lo == 1 && hi == 3));
-        const uint32_t a16 = (lo == 0) ? 0u : 2u;
-        const bool b8 = mine && !full && !(lo == 0 && hi == 2) && !(lo == 2 && hi == 4);
-        const uint32_t a8 = (lo == 0) ? 2u * (hi == 3) : lo;  // [0,1) @0, [0,3) @2, else @lo
-        if (full) *reinterpret_cast<uint32_t*>(lds + OUT + ua) = v;
+        const uint32_t ua = (dst & ~3u) + u4;
+        const uint32_t lo = u4 == 0 ? (dst & 3u) : 0u;
+        const int32_t e = int32_t(dst + len) - int32_t(ua);
+        const uint32_t hi = uint32_t(min(max(e, 1), 4));
+        // the unit's bytes [lo, hi) of its dword: full, or one b16 and one b8 (kPartialStores)
+        const uint32_t idx = (have && int32_t(lo) < e) ? 4 * lo + hi - 1 : 4u;
+        const uint32_t code = uint32_t(kPartialStores >> (4 * idx)) & 15u;
+        const uint32_t sa = src + u4 - (dst & 3u);  // source of the unit's byte 0 (may precede src by < 4)
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (sa & ~3u));
+        const uint32_t v = __builtin_amdgcn_alignbyte(w[1], w[0], sa & 3u);
+        const uint32_t a16 = lo ? 2u : 0u, a8 = code >> 2;
+        *reinterpret_cast<uint32_t*>(lds + (idx == 3 ? OUT + ua : junk)) = v;
         __builtin_amdgcn_wave_barrier();
-        if (b16) *reinterpret_cast<uint16_t*>(lds + OUT + ua + a16) = uint16_t(v >> (8 * a16));
+        *reinterpret_cast<uint16_t*>(lds + ((code & 1) ? OUT + ua + a16 : junk)) = uint16_t(v >> (8 * a16));
         __builtin_amdgcn_wave_barrier();
-        if (b8) lds[OUT + ua + a8] = uint8_t(v >> (8 * a8));
+        lds[(code & 2) ? OUT + ua + a8 : junk] = uint8_t(v >> (8 * a8));
         __builtin_amdgcn_wave_barrier();
-        k += nv;
       }
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -529,8 +671,8 @@ hipError_t launch_decode_wpb(hipStream_t st, const DecodeArgs& a_in, uint8_t* re
   DecodeArgs a = a_in;
   if (a.n == 0) return hipGetLastError();
   (void)hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), st);
-  // W: as many 4-wave workgroups as LDS allows (16 KiB tables + 264 B ring per lane)
-  const size_t w_lds = kTab16Bytes + size_t(kWalkThreads) * kWStride;
+  // W: as many 8-wave workgroups as LDS allows (5.5 KiB digit tables + 136 B ring per lane)
+  const size_t w_lds = kTab6Bytes + size_t(kWalkThreads) * kWStride;
   static const hipError_t attr_w = hipFuncSetAttribute(reinterpret_cast<const void*>(&snappy_walk_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(w_lds));
   if (attr_w != hipSuccess) return attr_w;
