@@ -219,6 +219,10 @@ void slate_ctx_destroy(slate_ctx* ctx);
  * calls; NULL restores the context's own stream. */
 int slate_ctx_set_stream(slate_ctx* ctx, void* hip_stream);
 int slate_ctx_synchronize(slate_ctx* ctx);
+/* Host threads this context copies with in the host-buffer pipelines (slate_block_decode_batch,
+ * slate_read_blocks, devbuf upload/download; default 16 or SLATE_COPY_THREADS, 1..256).  Each
+ * context has its own: slate_block_decode_sharded over G contexts uses G x threads. */
+int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads);
 
 /* ---- library-owned memory (SURVEY 8b "Ownership": device-resident mode uses opaque handles
  * owned by the C side) ----------------------------------------------------------------------

@@ -1,6 +1,7 @@
 // C-ABI: library, context and block decode (block.go:78 Decode; decode.go:107
 // ReadBlocks batches go through slate_block_decode_batch).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -103,8 +104,19 @@ slate_ctx* slate_ctx_create(int device, int* status) {
     return nullptr;
   }
   ctx->stream = ctx->own;
+  if (const char* e = getenv("SLATE_COPY_THREADS")) {
+    const unsigned long v = strtoul(e, nullptr, 0);
+    if (v >= 1 && v <= 256) ctx->copy_threads = v;
+  }
   *status = SLATE_OK;
   return ctx;
+}
+
+int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads) {
+  if (!ctx || threads == 0 || threads > 256) return SLATE_E_INVALID_ARG;
+  ctx->copy_threads = threads;
+  ctx->copy_pool.reset();  // joins the old workers; the next large copy starts the new count
+  return SLATE_OK;
 }
 
 void slate_ctx_destroy(slate_ctx* ctx) {

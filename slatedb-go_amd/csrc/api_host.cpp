@@ -18,28 +18,23 @@
 
 using namespace slate;
 
-thread_local size_t t_copy_threads = kCopyThreads;
+thread_local CopyPool* t_pool = nullptr;
 
-// memcpy split over threads for large copies between caller memory and page-locked staging
-// (one core copies ~10 GB/s, below what the PCIe link moves).  16 threads: the CPU share one
-// GPU's process gets on the MI355X boxes.
+// memcpy split over the calling context's copy threads for large copies between caller memory
+// and page-locked staging (one core copies ~10 GB/s, below what the PCIe link moves).
 void par_memcpy(void* dst, const void* src, size_t n) {
   constexpr size_t kPiece = 4u << 20;
-  if (n < 2 * kPiece) {
+  const size_t threads = t_pool ? t_pool->size() : 1;
+  if (n < 2 * kPiece || threads == 1) {
     if (n) memcpy(dst, src, n);
     return;
   }
-  const size_t t = std::max<size_t>(1, std::min<size_t>(t_copy_threads, n / kPiece));
+  const size_t t = std::max<size_t>(1, std::min<size_t>(threads, n / kPiece));
   const size_t step = (n + t - 1) / t;
-  std::vector<std::thread> th;
-  for (size_t i = 1; i < t; i++) {
+  t_pool->run(t, [&](size_t i) {
     const size_t a = i * step;
-    if (a >= n) break;
-    const size_t b = std::min(n, a + step);
-    th.emplace_back([=] { memcpy(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, b - a); });
-  }
-  memcpy(dst, src, std::min(n, step));
-  for (auto& x : th) x.join();
+    if (a < n) memcpy(static_cast<uint8_t*>(dst) + a, static_cast<const uint8_t*>(src) + a, std::min(n, a + step) - a);
+  });
 }
 
 hipError_t lane_init(PipeLane& L) {
@@ -58,6 +53,7 @@ constexpr size_t kXferDirect = 8u << 20;
 
 int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st) {
   if (n == 0) return SLATE_OK;
+  PoolScope pool(ctx);
   if (n <= kXferDirect) {
     SLATE_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
     SLATE_HIP(hipStreamSynchronize(st));
@@ -82,6 +78,7 @@ int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st
 
 int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st) {
   if (n == 0) return SLATE_OK;
+  PoolScope pool(ctx);
   if (n <= kXferDirect) {
     SLATE_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
@@ -157,22 +154,20 @@ uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len) {
   return 0;
 }
 
-// Run fn(lo, hi) over [0, n) split across up to t_copy_threads threads (pieces of >= grain).
+// Run fn(lo, hi) over [0, n) split across the calling context's copy threads (pieces of >= grain).
 template <typename F>
 void par_for(size_t n, size_t grain, F fn) {
-  const size_t t = std::max<size_t>(1, std::min<size_t>(t_copy_threads, n / std::max<size_t>(grain, 1)));
+  const size_t threads = t_pool ? t_pool->size() : 1;
+  const size_t t = std::max<size_t>(1, std::min<size_t>(threads, n / std::max<size_t>(grain, 1)));
   if (t == 1) {
     fn(size_t(0), n);
     return;
   }
   const size_t step = (n + t - 1) / t;
-  std::vector<std::thread> th;
-  for (size_t k = 1; k < t; k++) {
+  t_pool->run(t, [&](size_t k) {
     const size_t a = k * step, b = std::min(n, a + step);
-    if (a < b) th.emplace_back(fn, a, b);
-  }
-  fn(size_t(0), std::min(n, step));
-  for (auto& x : th) x.join();
+    if (a < b) fn(a, b);
+  });
 }
 
 // The lane's chunk is decoded: copy its outputs into the sink.  Its rows arrive densely (the
@@ -251,6 +246,7 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
 int host_decode(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n, Sink& o,
                 const uint64_t* gsrc = nullptr) {
   lanes_drain(ctx);  // nothing of an earlier (failed) call may reach this call's sink
+  PoolScope pool(ctx);
   LaneGuard guard{ctx};
   const int st = host_decode_body(ctx, codec, in, in_off, n, o, gsrc);
   guard.armed = st != SLATE_OK && st != SLATE_E_CAPACITY;
@@ -522,17 +518,11 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
     int st = SLATE_OK;
   };
   std::vector<Shard> sh(n_ctx);
-  const size_t share = std::max<size_t>(1, kCopyThreads / n_ctx);
+  // one host thread per context; each context's copies run on that context's own copy threads
   auto run = [&](auto&& fn) {
     std::vector<std::thread> th;
-    auto body = [&](uint32_t g) {
-      t_copy_threads = share;
-      fn(g);
-    };
-    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(body, g);
-    const size_t keep = t_copy_threads;
-    body(0);
-    t_copy_threads = keep;
+    for (uint32_t g = 1; g < n_ctx; g++) th.emplace_back(fn, g);
+    fn(0);
     for (auto& t : th) t.join();
     for (uint32_t g = 0; g < n_ctx; g++)
       if (sh[g].st) return sh[g].st;

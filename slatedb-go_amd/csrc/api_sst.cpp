@@ -1407,6 +1407,8 @@ size_t slate_sst_table_encoded_len(const slate_sst_table* t) {
 int slate_sst_table_encode(const slate_sst_table* t, uint8_t* out, size_t out_cap) {
   if (!t) return SLATE_E_INVALID_ARG;
   if (slate_sst_table_encoded_len(t) > out_cap || (!out && slate_sst_table_encoded_len(t))) return SLATE_E_CAPACITY;
+  CopyPool threads(slate_sst_table_encoded_len(t) >= (64u << 20) ? kCopyThreads : 1);  // no context here
+  PoolScope scope(&threads);
   size_t o = 0, i = 0;
   while (i < t->chunks.size()) {
     const ByteView& c = t->chunks[i];

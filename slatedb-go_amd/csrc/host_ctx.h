@@ -3,11 +3,14 @@
 // keeps no global mutable state (SURVEY 8b "Threading").
 #pragma once
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -133,6 +136,74 @@ struct SegPool {
   void close();  // unmaps the kept buffers (api_sst.cpp)
 };
 
+// A context's host copy threads: started on first use and kept, so the chunked host pipelines
+// (api_host.cpp) do not create threads per chunk.  run(tasks, fn) calls fn(k) for every k in
+// [0, tasks) on the workers and the calling thread and returns when all have run; one run at a
+// time (a context serves one caller thread at a time).
+class CopyPool {
+ public:
+  explicit CopyPool(size_t threads) : n_(threads ? threads : 1) {}
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  size_t size() const { return n_; }
+  void run(size_t tasks, const std::function<void(size_t)>& fn) {
+    if (tasks == 0) return;
+    if (tasks == 1 || n_ == 1) {
+      for (size_t k = 0; k < tasks; k++) fn(k);
+      return;
+    }
+    std::lock_guard<std::mutex> one(run_mu_);
+    std::unique_lock<std::mutex> g(mu_);
+    while (th_.size() + 1 < n_) th_.emplace_back([this] { worker(); });
+    job_ = &fn;
+    tasks_ = tasks;
+    next_ = 0;
+    pending_ = tasks;
+    gen_++;
+    cv_.notify_all();
+    drain(g);
+    done_.wait(g, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  // takes tasks until none is left; called with mu_ held, returns with it held
+  void drain(std::unique_lock<std::mutex>& g) {
+    while (job_ && next_ < tasks_) {
+      const size_t k = next_++;
+      const std::function<void(size_t)>* f = job_;
+      g.unlock();
+      (*f)(k);
+      g.lock();
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  void worker() {
+    std::unique_lock<std::mutex> g(mu_);
+    uint64_t seen = 0;
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      drain(g);
+    }
+  }
+  const size_t n_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  size_t tasks_ = 0, next_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 struct slate_ctx {
   // slate_bloom_decode: a compressed filter that did not fit the caller's buffer, kept with its
   // input so that the retry with the reported length copies it out instead of decoding again
@@ -153,6 +224,13 @@ struct slate_ctx {
   // LZ4 / Zlib / Zstd encode (encode_codecs.hip): piece tables, tag and body slots, sequences, frames
   DevBuf c_meta, c_tags, c_bodies, c_seqs, c_out, c_in;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
+  // host copy threads of this context (slate_ctx_set_copy_threads; SLATE_COPY_THREADS or 16)
+  size_t copy_threads = 16;
+  std::unique_ptr<CopyPool> copy_pool;
+  CopyPool* pool() {
+    if (!copy_pool) copy_pool.reset(new CopyPool(copy_threads));
+    return copy_pool.get();
+  }
   void release_all() {
     if (seg_pool) seg_pool->close();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
@@ -193,12 +271,19 @@ inline double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Host copies split over up to kCopyThreads threads (16: the CPU share one GPU's process gets on
-// the MI355X boxes; one core copies ~10 GB/s, below the PCIe link) -- api_host.cpp.
+// Host copies split over the context's copy threads (default 16: the CPU share one GPU's process
+// gets on the MI355X boxes; one core copies ~10 GB/s, below the PCIe link) -- api_host.cpp.
 constexpr size_t kCopyThreads = 16;
-// The calling thread's share of those threads: a sharded decode runs one host thread per
-// context and gives each kCopyThreads / contexts of them (api_host.cpp).
-extern thread_local size_t t_copy_threads;
+// The pool the calling thread's large copies use: set for the duration of a context's call by
+// PoolScope (a sharded decode runs one host thread per context, each on its own pool); without
+// one, par_memcpy copies on the calling thread alone.
+extern thread_local CopyPool* t_pool;
+struct PoolScope {
+  CopyPool* keep;
+  explicit PoolScope(slate_ctx* ctx) : keep(t_pool) { t_pool = ctx->pool(); }
+  explicit PoolScope(CopyPool* p) : keep(t_pool) { t_pool = p; }
+  ~PoolScope() { t_pool = keep; }
+};
 void par_memcpy(void* dst, const void* src, size_t n);
 // A pipeline lane's stream and events, created on first use.
 hipError_t lane_init(PipeLane& L);

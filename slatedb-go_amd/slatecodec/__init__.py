@@ -70,6 +70,7 @@ _SIGS = {
     "slate_ctx_create": (vp, [C.c_int, C.POINTER(C.c_int)]),
     "slate_ctx_destroy": (None, [vp]),
     "slate_ctx_set_stream": (C.c_int, [vp, vp]),
+    "slate_ctx_set_copy_threads": (C.c_int, [vp, C.c_uint32]),
     "slate_ctx_synchronize": (C.c_int, [vp]),
     "slate_decode_scratch_bytes": (C.c_size_t, [C.c_uint32]),
     "slate_block_decode_plan_device": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, vp, vp]),
@@ -204,6 +205,10 @@ class Context:
     def set_stream(self, stream_handle: int | None):
         _check(lib().slate_ctx_set_stream(self._h, C.c_void_p(stream_handle) if stream_handle else None),
                "slate_ctx_set_stream")
+
+    def set_copy_threads(self, threads: int):
+        """Host copy threads of this context (slate_ctx_set_copy_threads)."""
+        _check(lib().slate_ctx_set_copy_threads(self._h, int(threads)), "slate_ctx_set_copy_threads")
 
     def synchronize(self):
         _check(lib().slate_ctx_synchronize(self._h), "slate_ctx_synchronize")

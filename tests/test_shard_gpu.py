@@ -1,6 +1,6 @@
 """GPU parity of the host-buffer paths and the round-robin sharding (BASELINE configs[3],
 SURVEY 8e): slate_block_decode_batch through page-locked staging over many chunks, and
-slate_block_decode_sharded with G = 2..4 contexts on device 0 over one batch, against the
+slate_block_decode_sharded with G = 2..4 and 8 contexts on device 0 over one batch, against the
 oracle block by block, in the original order (plan layout, meta, decoded bytes, rows)."""
 import os
 import random
@@ -47,10 +47,12 @@ def _mixed_batch(seed, n_good):
     return blocks
 
 
-@pytest.mark.parametrize("g", [2, 3, 4])
+@pytest.mark.parametrize("g", [2, 3, 4, 8])
 def test_sharded_decode_matches_oracle(g):
     import slatecodec as sc
     ctxs = [sc.Context(0) for _ in range(g)]
+    for c in ctxs:  # every context has its own copy threads: 8 x 2 on the box's 16-core share
+        c.set_copy_threads(16 // g if g > 4 else 4)
     blocks = _mixed_batch(g, 3000)
     blob, off = bg.pack(blocks, misalign=5)
     got = sc.decode_sharded(ctxs, sc.SNAPPY, blob, off)
@@ -83,6 +85,11 @@ blob, off = bg.pack(blocks, misalign=3)
 ctx = sc.Context(0)
 got = ctx.decode_batch(sc.SNAPPY, blob, off)
 _check_against_oracle(sc.SNAPPY, blob, off, got)
+# 8 contexts, several chunks each, chunks in flight on all of them at once
+ctxs = [sc.Context(0) for _ in range(8)]
+for c in ctxs:
+    c.set_copy_threads(2)
+_check_against_oracle(sc.SNAPPY, blob, off, sc.decode_sharded(ctxs, sc.SNAPPY, blob, off))
 # one pass into caller-sized buffers, twice (reused staging)
 n = len(off) - 1
 out = np.zeros(int(got[1][n]) + 16, np.uint8); rows = np.zeros(int(got[4][n]) + 1, sc.ROW_DTYPE)
@@ -167,6 +174,21 @@ def test_failed_batches_then_valid_batch_same_context():
     assert (out[int(oo[m]) + 16:] == 0xA5).all(), "bytes written past the batch's outputs"
     used = int(np.sum(np.where(meta["status"] == 0, meta["n_rows"].astype(np.int64), 0)))
     assert (rows["row_off"][int(rb[m]):] == 0xDEADBEEF).all() and used <= int(rb[m])
+
+
+def test_copy_threads_setting():
+    """slate_ctx_set_copy_threads: 1..256 accepted (a batch decodes the same with 1 or 64 threads),
+    0 and > 256 rejected."""
+    import slatecodec as sc
+    ctx = sc.Context(0)
+    blocks = _mixed_batch(5, 600)
+    blob, off = bg.pack(blocks, misalign=2)
+    for t in (1, 64, 16):
+        ctx.set_copy_threads(t)
+        _check_against_oracle(sc.SNAPPY, blob, off, ctx.decode_batch(sc.SNAPPY, blob, off))
+    for bad in (0, 257):
+        with pytest.raises(sc.SlateError):
+            ctx.set_copy_threads(bad)
 
 
 def test_sharded_rejects_duplicate_context():
