@@ -369,6 +369,26 @@ static uint32_t xxh32_small(const uint8_t* p, size_t n) {
   return h;
 }
 
+// Adler-32 (RFC 1950) of n device bytes: a = 1 + sum x, b = n + sum (n - j) x, from 4 KiB slices'
+// partial sums (stream-synchronous).
+static int device_adler32(slate_ctx* ctx, const uint8_t* d, uint32_t n, uint32_t* adler) {
+  hipStream_t st = ctx->stream;
+  const uint32_t nsl = (n + 4095) / 4096;
+  SLATE_HIP(ctx->e_k.ensure(size_t(nsl) * 16 + 64));
+  if (nsl) SLATE_HIP(launch_adler_slices(st, d, n, ctx->e_k.as<uint64_t>()));
+  std::vector<uint64_t> part(2 * size_t(nsl));
+  if (nsl) SLATE_HIP(hipMemcpyAsync(part.data(), ctx->e_k.p, part.size() * 8, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  uint64_t a = 1, b = n % 65521;
+  for (uint32_t t = 0; t < nsl; t++) {
+    const uint64_t end = std::min<uint64_t>(n, 4096ull * (t + 1));
+    a = (a + part[2 * t]) % 65521;
+    b = (b + part[2 * t + 1] % 65521 + (part[2 * t] % 65521) * ((n - end) % 65521)) % 65521;
+  }
+  *adler = uint32_t((b << 16) | a);
+  return SLATE_OK;
+}
+
 // The GPU part of the split payload paths: the payload's CRC, then its blocks (blk = offset /
 // header word pairs) one wave each into 64 KiB slots, their outputs concatenated, the content size
 // and checksum (LZ4: XXH32; Zstd: XXH64's low half), and the decoded bytes back into `out`.
@@ -423,20 +443,10 @@ static int payload_split_run(slate_ctx* ctx, const uint8_t* buf, size_t len, con
     o += sizes[k];
   }
   if (has_sum && codec == SLATE_CODEC_ZLIB) {
-    // Adler-32 (RFC 1950): a = 1 + sum x, b = n + sum (n - j) x, from 4 KiB slices' partial sums
-    const uint32_t nsl = uint32_t((total + 4095) / 4096);
-    SLATE_HIP(ctx->e_k.ensure(size_t(nsl) * 16 + 64));
-    SLATE_HIP(launch_adler_slices(st, d_out, uint32_t(total), ctx->e_k.as<uint64_t>()));
-    std::vector<uint64_t> part(2 * size_t(nsl));
-    if (nsl) SLATE_HIP(hipMemcpyAsync(part.data(), ctx->e_k.p, part.size() * 8, hipMemcpyDeviceToHost, st));
-    SLATE_HIP(hipStreamSynchronize(st));
-    uint64_t a = 1, b = total % 65521;
-    for (uint32_t t = 0; t < nsl; t++) {
-      const uint64_t end = std::min<uint64_t>(total, 4096ull * (t + 1));
-      a = (a + part[2 * t]) % 65521;
-      b = (b + part[2 * t + 1] % 65521 + (part[2 * t] % 65521) * ((total - end) % 65521)) % 65521;
-    }
-    if (((b << 16) | a) != want) return SLATE_OK;  // the serial path reports the checksum
+    uint32_t got = 0;
+    s = device_adler32(ctx, d_out, uint32_t(total), &got);
+    if (s) return s;
+    if (got != want) return SLATE_OK;  // the serial path reports the checksum
   } else if (has_sum) {
     if (codec == SLATE_CODEC_LZ4) SLATE_HIP(launch_xxh32(st, d_out, uint32_t(total), d_sizes));
     else SLATE_HIP(launch_xxh64_lo(st, d_out, uint32_t(total), d_sizes));
@@ -591,6 +601,86 @@ static int lz4_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, std
                            bstatus, handled);
 }
 
+// A large CodecZstd index / filter that is one frame whose blocks depend on each other -- repeat
+// offsets, treeless literals and repeat tables across blocks, the frames klauspost/compress's
+// streaming writer (compression.go:105-118) and libzstd write -- through the block-parallel decoder
+// (zstd_par.hip): headers and entropy state first, then literals, sequences and bytes per block;
+// the content size and XXH64 last.  Same contract as lz4_payload_split.
+static int zstd_payload_par_run(slate_ctx* ctx, const uint8_t* buf, size_t len, const std::vector<uint32_t>& blk,
+                                uint32_t bmax, bool has_size, uint64_t content, bool has_sum, uint32_t want,
+                                std::vector<uint8_t>& out, int* bstatus, int* handled) {
+  *handled = 0;
+  const size_t clen = len - 4;
+  const uint32_t nblk = uint32_t(blk.size() / 2);
+  if (nblk == 0 || nblk > (1u << 16) || clen >= (1u << 28)) return SLATE_OK;
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  int s = ctx_h2d(ctx, ctx->d_in.p, buf, len, st);
+  if (s) return s;
+  uint32_t crc = 0;
+  s = ctx_crc32_device(ctx, ctx->d_in.as<uint8_t>(), clen, &crc);
+  if (s) return s;
+  if (crc != ld_be32(buf + clen)) {
+    *bstatus = SLATE_E_BLOCK_CHECKSUM;  // block.Decode / bloom.Decode / DecodeIndex check it first
+    *handled = 1;
+    return SLATE_OK;
+  }
+  const double t0 = host_trace() ? now_ms() : 0.0;
+  const uint8_t* d_in = ctx->d_in.as<uint8_t>();
+  SLATE_HIP(ctx->d_scratch.ensure(zstd_par_scratch_bytes(nblk) + 64));
+  SLATE_HIP(ctx->e_b.ensure(blk.size() * 4 + 64));
+  void* scratch = ctx->d_scratch.p;
+  SLATE_HIP(hipMemcpyAsync(ctx->e_b.p, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_zstd_par_headers(st, d_in, ctx->e_b.as<uint32_t>(), nblk, bmax, scratch, ctx->num_cus));
+  uint32_t res[4] = {1, 0, 0, 0};
+  SLATE_HIP(hipMemcpyAsync(res, zstd_par_result(scratch), sizeof(res), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  if (res[0]) {
+    if (host_trace()) fprintf(stderr, "[slate zstd-par] %u blocks: headers refused\n", nblk);
+    return SLATE_OK;  // the serial path decodes (and reports) it
+  }
+  const uint32_t nseq = res[1], nlit = res[2];
+  SLATE_HIP(ctx->d_rows.ensure(size_t(nlit) + 64));                        // literals
+  SLATE_HIP(ctx->e_c.ensure(3 * (size_t(nseq) + 64) * 4 + 256));           // ll | ml | offset
+  uint32_t* sll = ctx->e_c.as<uint32_t>();
+  uint32_t* sml = sll + nseq + 64;
+  uint32_t* sof = sml + nseq + 64;
+  SLATE_HIP(launch_zstd_par_body(st, d_in, nblk, bmax, scratch, ctx->d_rows.as<uint8_t>(), sll, sml, sof,
+                                 ctx->num_cus));
+  SLATE_HIP(hipMemcpyAsync(res, zstd_par_result(scratch), sizeof(res), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  const double t1 = host_trace() ? now_ms() : 0.0;
+  if (host_trace())
+    fprintf(stderr, "[slate zstd-par] %u blocks, %u sequences, %u literals, %u B out, fail %u: headers+body %.2f ms\n",
+            nblk, nseq, nlit, res[3], res[0], t1 - t0);
+  if (res[0]) return SLATE_OK;
+  const uint32_t total = res[3];
+  if (has_size && content != total) return SLATE_OK;  // the serial path reports the frame size
+  SLATE_HIP(ctx->d_out.ensure(size_t(total) + 64));
+  SLATE_HIP(ctx->e_a.ensure(2 * (size_t(total) + 1) * 4 + 64 * 4 + 256));  // pa | pb | changed
+  SLATE_HIP(ctx->e_d.ensure(size_t(total) + 64));                          // val
+  uint32_t* pa = ctx->e_a.as<uint32_t>();
+  uint32_t* pb = pa + total + 1;
+  uint32_t* changed = pb + total + 1;
+  uint8_t* d_out = ctx->d_out.as<uint8_t>();
+  SLATE_HIP(launch_zstd_par_bytes(st, d_in, nblk, total, scratch, ctx->d_rows.as<uint8_t>(), sll, sml, sof,
+                                  ctx->e_d.as<uint8_t>(), pa, pb, changed, d_out, ctx->num_cus));
+  if (has_sum) SLATE_HIP(launch_xxh64_lo(st, d_out, total, ctx->e_b.as<uint32_t>()));
+  uint32_t tail[2] = {1, 0};
+  SLATE_HIP(hipMemcpyAsync(tail, zstd_par_result(scratch), 4, hipMemcpyDeviceToHost, st));
+  if (has_sum) SLATE_HIP(hipMemcpyAsync(tail + 1, ctx->e_b.p, 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  if (host_trace()) fprintf(stderr, "[slate zstd-par] bytes + checksum %.2f ms, fail %u\n", now_ms() - t1, tail[0]);
+  if (tail[0] || (has_sum && tail[1] != want)) return SLATE_OK;  // the serial path reports it
+  out.resize(total);
+  s = ctx_d2h(ctx, out.data(), d_out, total, st);
+  if (s) return s;
+  *bstatus = SLATE_OK;
+  *handled = 1;
+  return SLATE_OK;
+}
+
 // A large CodecZstd index / filter decoded block by block in parallel when it is one frame whose
 // compressed blocks decode on their own (the frames this builder writes; decode.hip
 // zstd_payload_blocks_kernel checks it block by block).  Same contract as lz4_payload_split.
@@ -645,8 +735,76 @@ static int zstd_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, st
     pos += 4;
   }
   if (pos != clen) return SLATE_OK;  // one frame, nothing after it
-  return payload_split_run(ctx, buf, len, blk, bmax, SLATE_CODEC_ZSTD, fl != 0, fcs, has_sum, want, out, bstatus,
-                           handled);
+  {
+    const int s = payload_split_run(ctx, buf, len, blk, bmax, SLATE_CODEC_ZSTD, fl != 0, fcs, has_sum, want, out,
+                                    bstatus, handled);
+    if (s || *handled) return s;
+  }
+  // blocks that do not decode on their own (or larger than the split path's slots)
+  return zstd_payload_par_run(ctx, buf, len, blk, bmax, fl != 0, fcs, has_sum, want, out, bstatus, handled);
+}
+
+// A large CodecZlib index / filter whose stream has no flush points -- the shape compress/zlib's
+// writer (compression.go:96-103) and zlib produce -- through the speculative block-parallel inflate
+// (zlib_par.hip): block starts found and decoded speculatively, the true chain walked, every byte
+// resolved by pointer doubling; then the Adler-32 on the GPU.  Same contract as lz4_payload_split
+// (a FDICT header, or any failed check: the serial path decodes and reports it).
+static int zlib_payload_par_run(slate_ctx* ctx, const uint8_t* buf, size_t len, uint32_t want,
+                                std::vector<uint8_t>& out, int* bstatus, int* handled) {
+  *handled = 0;
+  const size_t clen = len - 4;
+  if (clen < 6 + 4 || clen >= (1u << 28) || (buf[1] & 0x20)) return SLATE_OK;
+  const uint32_t dend = uint32_t(clen - 4);
+  SLATE_HIP(ctx_bind(ctx));
+  hipStream_t st = ctx->stream;
+  SLATE_HIP(ctx->d_in.ensure(len + 64));
+  int s = ctx_h2d(ctx, ctx->d_in.p, buf, len, st);
+  if (s) return s;
+  uint32_t crc = 0;
+  s = ctx_crc32_device(ctx, ctx->d_in.as<uint8_t>(), clen, &crc);
+  if (s) return s;
+  if (crc != ld_be32(buf + clen)) {
+    *bstatus = SLATE_E_BLOCK_CHECKSUM;  // block.Decode / bloom.Decode / DecodeIndex check it first
+    *handled = 1;
+    return SLATE_OK;
+  }
+  const double t0 = host_trace() ? now_ms() : 0.0;
+  SLATE_HIP(ctx->d_scratch.ensure(zlib_par_scratch_bytes(uint32_t(clen)) + 64));
+  void* scratch = ctx->d_scratch.p;
+  const uint8_t* d_in = ctx->d_in.as<uint8_t>();
+  SLATE_HIP(launch_zlib_par_chain(st, d_in, uint32_t(clen), 16, dend, scratch, ctx->num_cus));
+  uint32_t res[5] = {1, 0, 0, 0, 0};
+  SLATE_HIP(hipMemcpyAsync(res, zlib_par_result(scratch), sizeof(res), hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  const double t1 = host_trace() ? now_ms() : 0.0;
+  if (host_trace())
+    fprintf(stderr, "[slate zlib-par] %zu B: %u survivors, %u candidates, %u blocks, %u B out, fail %u: chain %.2f ms\n",
+            clen, res[1], res[2], res[3], res[4], res[0], t1 - t0);
+  if (res[0]) return SLATE_OK;  // the serial path decodes (and reports) it
+  const uint32_t total = res[4];
+  SLATE_HIP(ctx->d_rows.ensure(size_t(total) + 64));                       // val
+  SLATE_HIP(ctx->e_a.ensure(2 * (size_t(total) + 1) * 4 + 64 * 4 + 256));  // pa | pb | changed
+  SLATE_HIP(ctx->d_out.ensure(size_t(total) + 64));
+  uint32_t* pa = ctx->e_a.as<uint32_t>();
+  uint32_t* pb = pa + total + 1;
+  uint32_t* changed = pb + total + 1;
+  uint8_t* d_out = ctx->d_out.as<uint8_t>();
+  SLATE_HIP(launch_zlib_par_bytes(st, d_in, uint32_t(clen), total, scratch, ctx->d_rows.as<uint8_t>(), pa, pb, changed,
+                                  d_out, ctx->num_cus));
+  SLATE_HIP(hipMemcpyAsync(res, zlib_par_result(scratch), 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
+  if (res[0]) return SLATE_OK;
+  uint32_t got = 0;
+  s = device_adler32(ctx, d_out, total, &got);
+  if (s) return s;
+  if (host_trace()) fprintf(stderr, "[slate zlib-par] bytes + adler %.2f ms\n", now_ms() - t1);
+  if (got != want) return SLATE_OK;  // the serial path reports the checksum (read at dend by the caller)
+  out.resize(total);
+  s = ctx_d2h(ctx, out.data(), d_out, total, st);
+  if (s) return s;
+  *bstatus = SLATE_OK;
+  *handled = 1;
+  return SLATE_OK;
 }
 
 // A large CodecZlib index / filter (`zlib stream || BE32 CRC`) inflated piece by piece in parallel:
@@ -673,10 +831,15 @@ static int zlib_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, st
       i += 3;
     }
   }
-  if (s0 >= dend || dend > 0xFFFFFFFFull) return SLATE_OK;
+  if (s0 >= dend || dend > 0xFFFFFFFFull) return zlib_payload_par_run(ctx, buf, len, want, out, bstatus, handled);
   seg.push_back(uint32_t(s0));
   seg.push_back(uint32_t(dend - s0));
-  return payload_split_run(ctx, buf, len, seg, 0, SLATE_CODEC_ZLIB, false, 0, true, want, out, bstatus, handled);
+  if (seg.size() > 2) {
+    const int s = payload_split_run(ctx, buf, len, seg, 0, SLATE_CODEC_ZLIB, false, 0, true, want, out, bstatus, handled);
+    if (s || *handled) return s;
+  }
+  // no piece ends (compress/zlib's and zlib's own streams), or `00 00 FF FF` inside a block's data
+  return zlib_payload_par_run(ctx, buf, len, want, out, bstatus, handled);
 }
 
 int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, size_t len, std::vector<uint8_t>& out,

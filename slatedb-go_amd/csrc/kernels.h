@@ -168,6 +168,42 @@ hipError_t launch_lz4_par_chain(hipStream_t st, const uint8_t* in, uint32_t sz, 
 hipError_t launch_lz4_par_bytes(hipStream_t st, const uint8_t* in, uint32_t sz, uint32_t cap, uint32_t dn,
                                 uint32_t prior, void* scratch, uint8_t* out);
 
+// A Zlib payload (zlib stream || BE32 CRC, clen = stream bytes) without flush points inflated in
+// parallel (zlib_par.hip): the chain pass (block-start candidates, their speculative decode, the
+// walk from bit p0 whose final block must end at byte dend), then -- the host having read
+// zlib_par_result's words: [0] != 0 = hand the payload to the exact decoder, [4] = decoded length
+// -- the bytes pass into out (val: total bytes, pa / pb: total + 1 words, changed: 64 words);
+// [0] is checked again after it.
+size_t zlib_par_scratch_bytes(uint32_t clen);
+// Bytes from per-byte pointers (zlib_par.hip): pa[x] = x for a byte whose value is val[x], else the
+// earlier byte it repeats; pointer doubling (pb, changed: 64 words of scratch) then
+// out[x] = val[root].  Skipped when flag[0] is set (a pointer out of range sets it).
+hipError_t launch_ptr_gather(hipStream_t st, uint32_t total, const uint8_t* val, uint32_t* pa, uint32_t* pb,
+                             uint32_t* changed, uint32_t* flag, uint8_t* out);
+const uint32_t* zlib_par_result(const void* scratch);
+hipError_t launch_zlib_par_chain(hipStream_t st, const uint8_t* in, uint32_t clen, uint32_t p0, uint32_t dend,
+                                 void* scratch, int num_cus);
+hipError_t launch_zlib_par_bytes(hipStream_t st, const uint8_t* in, uint32_t clen, uint32_t total, void* scratch,
+                                 uint8_t* val, uint32_t* pa, uint32_t* pb, uint32_t* changed, uint8_t* out,
+                                 int num_cus);
+
+// A Zstd payload's single frame whose blocks depend on each other (repeat offsets, treeless
+// literals, repeat tables) decoded block-parallel (zstd_par.hip), blk = nblk x (block body offset,
+// block header word) as the host parsed them, bmax = the frame's block maximum.  Three steps, the
+// host reading zstd_par_result's words between them ([0] != 0 = hand the payload to the exact
+// decoder): headers ([1] sequences, [2] literals: the sizes of lit / sll / sml / sof), body ([3] =
+// decoded length), bytes into out (val: total bytes, pa / pb: total + 1 words, changed: 64 words).
+size_t zstd_par_scratch_bytes(uint32_t nblk);
+const uint32_t* zstd_par_result(const void* scratch);
+hipError_t launch_zstd_par_headers(hipStream_t st, const uint8_t* in, const uint32_t* blk, uint32_t nblk,
+                                   uint32_t bmax, void* scratch, int num_cus);
+hipError_t launch_zstd_par_body(hipStream_t st, const uint8_t* in, uint32_t nblk, uint32_t bmax, void* scratch,
+                                uint8_t* lit, uint32_t* sll, uint32_t* sml, uint32_t* sof, int num_cus);
+hipError_t launch_zstd_par_bytes(hipStream_t st, const uint8_t* in, uint32_t nblk, uint32_t total, void* scratch,
+                                 const uint8_t* lit, const uint32_t* sll, const uint32_t* sml, const uint32_t* sof,
+                                 uint8_t* val, uint32_t* pa, uint32_t* pb, uint32_t* changed, uint8_t* out,
+                                 int num_cus);
+
 // Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                              const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
