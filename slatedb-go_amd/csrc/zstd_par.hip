@@ -306,7 +306,7 @@ __global__ __launch_bounds__(64) void zq_lit_kernel(const uint8_t* __restrict__ 
   if (Z.flag[0]) return;
   for (uint32_t k = blockIdx.x; k < nblk; k += gridDim.x) {
     const ZqBlk B = Z.blk[k];
-    if (B.kind != 2 || B.nlit == 0) continue;
+    if (B.kind != 2 || (B.nlit == 0 && B.ltype < 2)) continue;  // Huffman streams are checked even when empty
     uint8_t* dst = lit + B.lit_base;
     const uint32_t src = B.body + B.lhs;
     if (B.ltype == 0) {
