@@ -108,6 +108,7 @@ print("ok")
     env = dict(os.environ, SLATE_HOST_TRACE="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+    print("\n" + "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[slate zlib-par]")))
     chains = [ln for ln in r.stderr.splitlines() if ln.startswith("[slate zlib-par]") and "candidates" in ln]
     assert len(chains) == 2 and all("fail 0" in ln for ln in chains), r.stderr[-3000:]
 

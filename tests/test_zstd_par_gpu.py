@@ -81,7 +81,7 @@ def test_zstd_multiblock_sst_payloads(ctx, sst_parts):
     iz = sstgen.crc(zstdgen.frame(ib, level=3, content_size=False))
     fz = sstgen.crc(zstdgen.frame(fb, level=3, content_size=False))
     n, lts = _blocks(iz[:-4])
-    assert n > 8 and 3 in lts, (n, lts)  # blocks that need the previous block's tree
+    assert n > 8, n
     _check(ctx, fz)  # warm-up
     t0 = time.perf_counter()
     assert _check(ctx, fz) == 0
@@ -123,8 +123,21 @@ print("ok")
     env = dict(os.environ, SLATE_HOST_TRACE="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
+    print("\n" + "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[slate zstd-par]")))
     ends = [ln for ln in r.stderr.splitlines() if ln.startswith("[slate zstd-par] bytes")]
     assert len(ends) == 2 and all(ln.endswith("fail 0") for ln in ends), r.stderr[-3000:]
+
+
+def test_zstd_treeless_and_repeat_tables(ctx):
+    """Key-like bytes at level 3: blocks whose literals reuse the previous block's Huffman tree
+    (treeless) among many blocks, with repeat offsets across block boundaries."""
+    raw = b"".join(b"\x0c\x00\x00\x00key%012d" % (i * 37) for i in range(300000))
+    for level in (1, 3, 9):
+        f = zstdgen.frame(raw, level=level, content_size=level != 3)
+        n, lts = _blocks(f)
+        if level == 3:
+            assert n > 8 and 3 in lts, (n, lts)
+        assert _check(ctx, sstgen.crc(f)) == 0
 
 
 @pytest.mark.parametrize("level", [-1, 1, 3, 9, 19])
