@@ -1545,9 +1545,7 @@ size_t decode_scratch_bytes(uint32_t n) {
   return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16 +
          // CodecZstd fast path: count, list, records, sequences
          16 + 2 * align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
-         size_t(n) * kZsFastSeqs * sizeof(uint2) +
-         // CodecSnappy two-phase decode: counters and per-block records
-         16 + align16(size_t(n) * kWpbRecBytes);
+         size_t(n) * kZsFastSeqs * sizeof(uint2);
 }
 
 static DecodeScratch carve(void* scratch, uint32_t n) {
@@ -1573,9 +1571,6 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   p += size_t(n) * sizeof(ZsFastRec);
   s.zf.seq = reinterpret_cast<uint2*>(p);
   p += size_t(n) * kZsFastSeqs * sizeof(uint2);
-  s.wpb_ctr = reinterpret_cast<uint32_t*>(p);
-  p += 16;
-  s.wpb_rec = p;
   s.tiles = uint32_t(tiles);
   return s;
 }
@@ -1694,18 +1689,7 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   if (a.n == 0) return hipGetLastError();
   // Snappy: the lane-per-block streaming decoder (any block size); ablation bit 16 (profiling
   // variants only) selects the wave-per-block path instead
-  // Snappy: the lane-per-block streaming decoder; SLATE_SNAPPY_WPB=1 selects the two-phase
-  // decoder (decode_wpb.hip: lane-per-block walk, wave-per-block build, the streaming decoder for
-  // the rest; in development, A/B runs); ablation bit 16 (profiling variants only) the
-  // wave-per-block exact path
-  if (a.codec == SLATE_CODEC_SNAPPY && !(dbg_bits(a) & 16)) {
-    static const bool wpb = [] {
-      const char* e = getenv("SLATE_SNAPPY_WPB");
-      return e && *e == '1';
-    }();
-    if (!wpb || a.raw) return launch_decode_lpb2(st, a, num_cus);
-    return launch_decode_wpb(st, a, s.wpb_rec, s.wpb_ctr, num_cus);
-  }
+  if (a.codec == SLATE_CODEC_SNAPPY && !(dbg_bits(a) & 16)) return launch_decode_lpb2(st, a, num_cus);
   const size_t lds = a.codec == SLATE_CODEC_ZSTD
                          ? kTabBytes + (kDecodeThreads / 64) * size_t(kZsFastInCap + kZsFastOutCap + kZsScratch) + kZsShared
                          : kTabBytes + (kDecodeThreads / 64) * size_t(kFastInCap + kFastOutCap) +

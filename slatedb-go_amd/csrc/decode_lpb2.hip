@@ -676,8 +676,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     uint32_t S0 = 0xFFFFFFFFu, S1 = 0xFFFFFFFFu, S2 = 0xFFFFFFFFu, S3 = 0xFFFFFFFFu;
     const uint32_t b = round0 + lane;
     slate_block_meta m{};
-    // after the two-phase decoder (decode_wpb.hip): only the blocks its build kernel left
-    bool have = b < rend && !(a.wpb && (a.wpb[size_t(b) * kWpbRecBytes] & 1u));
+    bool have = b < rend;
     L.in_rel = L.out_rel = L.rows_rel = 0;
     L.sh = L.clen = L.dn = L.last_chunk = L.rcap = 0;
     L.crc_last = -1;

@@ -40,13 +40,7 @@ struct DecodeArgs {
   uint32_t raw = 0;       // LPB only: payload is not a block (index/filter buffer): CRC + decompress, no block checks
   uint32_t rt_zero = 0;   // always 0: a value the compiler cannot fold (see decode_lpb2.hip rd128)
   uint32_t* round_counter = nullptr;  // decode_lpb2: rounds handed out so far (launcher zeroes it)
-  const uint8_t* wpb = nullptr;       // decode_lpb2 after decode_wpb: per-block records; skip blocks D completed
 };
-
-// Two-phase Snappy decode (decode_wpb.hip): the walk kernel's per-block record (16-byte head +
-// 40 anchors of 8 bytes); bit 0 of the first byte = the build kernel decodes (decoded) the block.
-constexpr uint32_t kWpbRecBytes = 16 + 8 * 40;
-hipError_t launch_decode_wpb(hipStream_t st, const DecodeArgs& a, uint8_t* rec, uint32_t* counters, int num_cus);
 
 // Ablation bits.  The shipped library is built without SLATE_PROFILING_BUILD, so every
 // ablation branch folds away at compile time; tools/variant.sh builds profiling variants.
@@ -85,8 +79,6 @@ struct DecodeScratch {
   uint32_t* large_count;
   uint32_t* large_list;
   uint32_t* round_counter;
-  uint8_t* wpb_rec;       // decode_wpb: n records of kWpbRecBytes
-  uint32_t* wpb_ctr;      // decode_wpb: walk rounds, build blocks handed out
   uint32_t tiles;
   ZsFastArgs zf;
 };
