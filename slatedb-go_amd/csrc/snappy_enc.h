@@ -20,7 +20,6 @@
 
 namespace slate {
 
-typedef uint32_t snap_u32u __attribute__((aligned(1)));
 
 constexpr uint32_t kSnapMaxBlock = 65536;    // encode.go maxBlockSize
 constexpr uint32_t kSnapMinNonLiteral = 17;  // 1 + 1 + inputMargin
@@ -55,7 +54,13 @@ __device__ inline uint32_t snappy_table_size(uint32_t n, uint32_t* shift) {
   return ts;
 }
 
-__device__ inline uint32_t snap_ld32(const uint8_t* p) { return *reinterpret_cast<const snap_u32u*>(p); }
+// 4 unaligned bytes as two aligned dword reads (gfx950 serialises a misaligned LDS access lane by
+// lane); the buffers keep at least 4 readable bytes past their end
+__device__ inline uint32_t snap_ld32(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], uint32_t(a) & 3u);
+}
 __device__ inline uint32_t snap_hash(uint32_t u, uint32_t shift) { return (u * 0x1e35a7bdu) >> shift; }
 
 // emitLiteral (encode_other.go:12-38): header by lane 0, bytes by all lanes
