@@ -735,7 +735,7 @@ static int zstd_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, st
     pos += 4;
   }
   if (pos != clen) return SLATE_OK;  // one frame, nothing after it
-  {
+  if (bmax <= kLz4PayloadSlot) {  // this builder's frames: 64 KiB pieces (larger blocks never fit the slots)
     const int s = payload_split_run(ctx, buf, len, blk, bmax, SLATE_CODEC_ZSTD, fl != 0, fcs, has_sum, want, out,
                                     bstatus, handled);
     if (s || *handled) return s;
@@ -834,7 +834,11 @@ static int zlib_payload_split(slate_ctx* ctx, const uint8_t* buf, size_t len, st
   if (s0 >= dend || dend > 0xFFFFFFFFull) return zlib_payload_par_run(ctx, buf, len, want, out, bstatus, handled);
   seg.push_back(uint32_t(s0));
   seg.push_back(uint32_t(dend - s0));
-  if (seg.size() > 2) {
+  // this builder's pieces hold at most 64 KiB each; a longer segment means the `00 00 FF FF` were
+  // ordinary bytes of another writer's stream
+  bool pieces = seg.size() > 2;
+  for (size_t k = 1; k < seg.size() && pieces; k += 2) pieces = seg[k] <= 2 * kLz4PayloadSlot;
+  if (pieces) {
     const int s = payload_split_run(ctx, buf, len, seg, 0, SLATE_CODEC_ZLIB, false, 0, true, want, out, bstatus, handled);
     if (s || *handled) return s;
   }
