@@ -419,9 +419,8 @@ int slate_bloom_build(slate_ctx* ctx, const uint8_t* keys, const uint64_t* key_o
                       uint32_t bits_per_key, uint8_t* bits, size_t bits_cap, size_t* bits_len,
                       uint16_t* num_probes);
 /* Encode (bloom.go:52) / Decode (bloom.go:70), every codec.  Decode's bits alias nothing: copied out.
- * When bits_cap is too small, Decode returns SLATE_E_CAPACITY with *bits_len set; a compressed filter
- * of at most 64 MiB (input + decoded) is kept on the context until the next bloom_decode call, so
- * the retry with the same bytes and a large enough buffer does not decompress it again. */
+ * When bits_cap is too small, Decode returns SLATE_E_CAPACITY with *bits_len set (the retry with a
+ * buffer of that length decodes the payload again; the context keeps nothing in between). */
 int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits, size_t bits_len,
                        int codec, uint8_t* out, size_t out_cap, size_t* out_len);
 int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec,

@@ -1847,8 +1847,6 @@ int slate_bloom_encode(slate_ctx* ctx, uint16_t num_probes, const uint8_t* bits,
   return SLATE_OK;
 }
 
-constexpr size_t kBloomKeep = size_t(64) << 20;
-
 int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, uint16_t* num_probes, uint8_t* bits,
                        size_t bits_cap, size_t* bits_len) {
   if (!ctx || (len && !buf)) return SLATE_E_INVALID_ARG;
@@ -1858,19 +1856,7 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   std::vector<uint8_t> dec;
   const uint8_t* p = buf;
   size_t pn = ci;
-  const bool cached = codec != SLATE_CODEC_NONE && codec == ctx->bloom_codec && len == ctx->bloom_in.size() &&
-                      memcmp(buf, ctx->bloom_in.data(), len) == 0;
-  // whatever was kept belongs to at most this one retry
-  std::vector<uint8_t> kept;
-  kept.swap(ctx->bloom_dec);
-  ctx->bloom_in.clear();
-  ctx->bloom_in.shrink_to_fit();
-  ctx->bloom_codec = -1;
-  if (cached) {  // the same bytes decoded (and checked) by the call that reported SLATE_E_CAPACITY
-    dec.swap(kept);
-    p = dec.data();
-    pn = dec.size();
-  } else if (codec > SLATE_CODEC_NONE && codec <= SLATE_CODEC_ZSTD) {
+  if (codec > SLATE_CODEC_NONE && codec <= SLATE_CODEC_ZSTD) {
     // the GPU payload path checks the CRC first (bloom.go:75-79), then decompresses: one upload
     int bst = 0;
     int st = ctx_payload_decode_buffer(ctx, codec, buf, len, dec, &bst);
@@ -1888,16 +1874,7 @@ int slate_bloom_decode(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec
   if (pn < 2) return SLATE_E_FILTER_PANIC;
   if (num_probes) *num_probes = ld_be16(p);
   if (bits_len) *bits_len = pn - 2;
-  if (pn - 2 > bits_cap || (!bits && pn > 2)) {
-    // keep a decoded filter for the retry with a buffer of *bits_len bytes (bounded: a caller that
-    // only asks for the size leaves at most kBloomKeep bytes of input + output on the context)
-    if (codec != SLATE_CODEC_NONE && len + dec.size() <= kBloomKeep) {
-      ctx->bloom_in.assign(buf, buf + len);
-      ctx->bloom_dec.swap(dec);
-      ctx->bloom_codec = codec;
-    }
-    return SLATE_E_CAPACITY;
-  }
+  if (pn - 2 > bits_cap || (!bits && pn > 2)) return SLATE_E_CAPACITY;  // the retry decodes again
   if (pn > 2) memcpy(bits, p + 2, pn - 2);
   return SLATE_OK;
 }

@@ -205,10 +205,6 @@ class CopyPool {
 };
 
 struct slate_ctx {
-  // slate_bloom_decode: a compressed filter that did not fit the caller's buffer, kept with its
-  // input so that the retry with the reported length copies it out instead of decoding again
-  std::vector<uint8_t> bloom_in, bloom_dec;
-  int bloom_codec = -1;
   int device = 0;
   int num_cus = 256;
   hipStream_t own = nullptr;

@@ -157,9 +157,9 @@ def test_lz4_large_blocks_cross_block_matches(ctx):
 
 
 def test_bloom_decode_capacity_retry(sc, ctx):
-    """slate_bloom_decode keeps a compressed filter that did not fit the caller's buffer for the retry
-    with the reported length: the retry returns the same bytes as the oracle, and a different
-    payload of the same length (or another codec) is decoded afresh, never served from that copy."""
+    """slate_bloom_decode with a buffer too small reports the filter's length (SLATE_E_CAPACITY); the
+    retry with that length returns the oracle's bytes, and calls in between (another payload of the
+    same length, another codec) do not disturb it."""
     import ctypes as C
     rng = np.random.default_rng(5)
     raw1 = b"\x00\x06" + rng.integers(0, 4, 300_000, dtype=np.uint8).tobytes()
