@@ -13,3 +13,6 @@ grep "slate build" $OUT/enc_snappy.trace | tail -5
 python3 -c "import json;d=json.load(open('$OUT/enc_snappy.json'));print('e2e host',d['host_input']['end_to_end_s'],'device',d['device_input']['end_to_end_s'],'bit_exact',d['bit_exact'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 tools/bench_encode.py --codec snappy --steps 2 > $OUT/trace.log 2>&1 || { echo TRACE_FAILED; tail -20 $OUT/trace.log; exit 1; }
 cut -d, -f1-4 $OUT/trace/run_kernel_stats.csv | head -12 | cut -c1-160
+# opening a 10 M-KV SST's index and filter as the reference's zlib / zstd writers shape them
+timeout -k 10 300 python -u tools/payload_probe.py 10000000 zlib-ref,zstd-ref,zlib,zstd > $OUT/payload_probe.log 2>&1 || { echo PROBE_FAILED; tail -20 $OUT/payload_probe.log; exit 1; }
+cat $OUT/payload_probe.log

@@ -1,6 +1,9 @@
 """Profiling aid (tooling): opening an SST's index and filter (slate_decode_index,
 slate_bloom_decode) per codec, for a configs[2]-sized SST (10 M KV: ~11 MB index, 12.5 MB filter),
-built by the GPU builder.  Times are wall clock of the C-ABI calls (host buffer in)."""
+built by the GPU builder.  Times are wall clock of the C-ABI calls (host buffer in).
+"zlib-ref" / "zstd-ref": the CodecNone SST's raw index and filter compressed the way the reference's
+writers shape them (zlib level 6 without flush points; libzstd level 3 streaming-style frames without
+a content size), the payloads of an SST the Go DB wrote."""
 import os
 import sys
 import time
@@ -21,14 +24,24 @@ def main():
     ctx = sc.Context(0)
     keys, key_off, vals, val_off = kv_arrays(n)
     for name in codecs:
-        codec = {"none": sc.NONE, "snappy": sc.SNAPPY, "lz4": sc.LZ4, "zstd": sc.ZSTD, "zlib": sc.ZLIB}[name]
-        b = sc.SstBuilder(ctx, 4096, 0, 10, codec)
+        ref = name.endswith("-ref")
+        base = name[:-4] if ref else name
+        codec = {"none": sc.NONE, "snappy": sc.SNAPPY, "lz4": sc.LZ4, "zstd": sc.ZSTD, "zlib": sc.ZLIB}[base]
+        b = sc.SstBuilder(ctx, 4096, 0, 10, sc.NONE if ref else codec)
         assert b.add_batch(keys, key_off, vals, val_off) == 0
         sst = b.build().encode()
         st, info, _ = sc.read_info(sst)
         assert st == sc.OK, st
         ib = sst[info.index_offset:info.index_offset + info.index_len]
         fb = sst[info.filter_offset:info.filter_offset + info.filter_len]
+        if ref:
+            import zlib
+            from tests import sstgen, zstdgen
+            if base == "zlib":
+                comp = lambda raw: zlib.compress(raw, 6)  # noqa: E731
+            else:
+                comp = lambda raw: zstdgen.frame(raw, level=3, content_size=False)  # noqa: E731
+            ib, fb = sstgen.crc(comp(ib[:-4])), sstgen.crc(comp(fb[:-4]))
         res = {}
         for what, fn in (("index", lambda: ctx.decode_index(ib, codec)), ("filter", lambda: ctx.bloom_decode(fb, codec))):
             ts = []
