@@ -572,8 +572,40 @@ def host_io_rate(sc, ctx, codec, blob, in_off, max_blocks=262144):
         assert st == sc.OK and (meta["status"] == 0).all()
     res["sharded_2ctx_GiBps_decoded"] = round(dec / el / 2**30, 2)
     ctx3.close()
+    # eight contexts on this one GPU (the in-process path of an 8-GPU node), each with its share of
+    # this process's CPUs as copy threads: what the host gather / scatter sustains through one link
+    cpus = host_cpus()
+    ctxs = [sc.Context(ctx.device) for _ in range(8)]
+    for c in ctxs:
+        c.set_copy_threads(max(1, cpus // 8))
+    for _ in range(2):
+        t = time.perf_counter()
+        st = sc.decode_sharded_into(ctxs, codec, sub, sub_off, out, rows, meta, out_off, row_base)
+        el = time.perf_counter() - t
+        assert st == sc.OK and (meta["status"] == 0).all()
+    res["sharded_8ctx_GiBps_decoded"] = round(dec / el / 2**30, 2)
+    res["sharded_8ctx_copy_threads"] = max(1, cpus // 8)
+    for c in ctxs:
+        c.close()
     ctx2.close()
+    res["host_memcpy_GBps"] = host_memcpy_rate(cpus)
     return res
+
+
+def host_memcpy_rate(threads, nbytes=1 << 30, piece=64 << 20):
+    """Host memory bandwidth of plain copies over `threads` threads (numpy releases the GIL):
+    the ceiling of the host pipelines' staging copies on this box's CPU share."""
+    import concurrent.futures as cf
+    src = np.ones(nbytes, np.uint8)
+    dst = np.zeros(nbytes, np.uint8)
+    pieces = [(o, min(nbytes, o + piece)) for o in range(0, nbytes, piece)]
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        best = 0.0
+        for _ in range(3):
+            t = time.perf_counter()
+            list(ex.map(lambda ab: np.copyto(dst[ab[0]:ab[1]], src[ab[0]:ab[1]]), pieces))
+            best = max(best, nbytes / (time.perf_counter() - t) / 1e9)
+    return round(best, 1)
 
 
 CODEC_RESTATEMENT = {0: "no codec", 1: "golang/snappy", 2: "compress/zlib+flate", 3: "LZ4 frame",
