@@ -7,7 +7,7 @@ namespace slate {
 constexpr int kPackThreads = 256;        // 4 wavefronts, one block each
 constexpr uint32_t kPackCap = 8192;      // LDS bytes per wavefront for one encoded block
 constexpr uint32_t kPackBigCap = 155648; // one wavefront per workgroup
-constexpr int kSnapThreads = 128;        // Snappy pack: 2 wavefronts, ~21 KiB LDS each
+constexpr int kSnapThreads = 192;        // Snappy pack: 3 wavefronts, ~16 KiB LDS each (3 workgroups per CU)
 constexpr uint32_t kSnapRaw = 4096;      // raw block bytes handled in LDS (BlockSize 4096)
 constexpr uint64_t kSnapChunkSlot = 76544;  // >= MaxEncodedLen(64 KiB), 16-aligned
 constexpr uint64_t kSnapMaxChunk = 65536;   // golang/snappy maxBlockSize

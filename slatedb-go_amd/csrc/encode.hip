@@ -352,8 +352,10 @@ __global__ __launch_bounds__(64) void enc_pack_big_kernel(EncodeArgs a, const ui
 // pass place the blocks back to back.
 __device__ inline uint64_t snap_slot_off(uint64_t raw_off, uint64_t b) { return align16(raw_off + raw_off / 6 + 48 * b); }
 
-constexpr uint32_t kSnapOut = uint32_t(((snappy_max_encoded_len(kSnapRaw) + 4 + 15) & ~15ull) + 16);
-constexpr uint32_t kSnapWaveBytes = kSnapRaw + 16 + kSnapOut + 2 * kSnapRaw + kSnapRaw;
+// per wave: the raw block (+16 readable bytes), the 4096-slot table and its owner bytes; the encoded
+// block goes straight to its HBM slot (an LDS copy of it cost a quarter of the wave's LDS: with it,
+// six waves per CU; without, nine)
+constexpr uint32_t kSnapWaveBytes = kSnapRaw + 16 + 2 * kSnapRaw + kSnapRaw;
 
 __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
     EncodeArgs a, const uint32_t* __restrict__ adj, const uint32_t* __restrict__ flags,
@@ -365,8 +367,7 @@ __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
   load_crc_tables(tab);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* raw = smem + kTabBytes + wave * kSnapWaveBytes;
-  uint8_t* out = raw + kSnapRaw + 16;
-  uint16_t* table = reinterpret_cast<uint16_t*>(out + kSnapOut);
+  uint16_t* table = reinterpret_cast<uint16_t*>(raw + kSnapRaw + 16);
   uint8_t* owner = reinterpret_cast<uint8_t*>(table + kSnapRaw);
   const bool sorted = (*flags & 1u) == 0;
   const uint32_t waves = gridDim.x * (kSnapThreads / 64);
@@ -378,13 +379,15 @@ __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
     }
     const uint32_t s = block_start[b];
     assemble_block(a, adj, sorted, s, next[s], raw, uint32_t(raw_len), lane);
-    const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), out, table, owner, lane);
-    const uint32_t crc = wave_crc32(tab, out, 0, clen, lane);
-    if (lane == 0) st_be32(out + clen, crc);
-    __builtin_amdgcn_wave_barrier();
+    uint8_t* dst = slots + snap_slot_off(raw_off[b], b);
+    const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), dst, table, owner, lane);
     __builtin_amdgcn_s_waitcnt(0);
-    write_bytes_from_lds(slots + snap_slot_off(raw_off[b], b), out, clen + 4, lane);
-    if (lane == 0) csize[b] = clen + 4;
+    __threadfence();  // the encoded bytes (stored by every lane) are read back by every lane
+    const uint32_t crc = wave_crc32(tab, dst, 0, clen, lane);
+    if (lane == 0) {
+      st_be32(dst + clen, crc);
+      csize[b] = clen + 4;
+    }
   }
 }
 
@@ -625,7 +628,10 @@ hipError_t launch_pack_snappy(hipStream_t st, const EncodeArgs& a, const EncodeB
                               const uint64_t* raw_off, uint8_t* slots, uint64_t* csize, int num_cus) {
   if (nblocks == 0) return hipGetLastError();
   const size_t lds = kTabBytes + (kSnapThreads / 64) * size_t(kSnapWaveBytes);
-  uint32_t grid = min(blocks_for(nblocks, kSnapThreads / 64), uint32_t(num_cus) * 3);
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&enc_pack_snappy_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  uint32_t grid = min(blocks_for(nblocks, kSnapThreads / 64), uint32_t(num_cus) * uint32_t(163840 / lds));
   enc_pack_snappy_kernel<<<grid, kSnapThreads, lds, st>>>(a, w.adj, w.flags, w.block_start, w.next, raw_off, nblocks,
                                                           slots, csize, w.big_list, w.big_count);
   return hipGetLastError();
