@@ -16,3 +16,5 @@ cut -d, -f1-4 $OUT/trace/run_kernel_stats.csv | head -12 | cut -c1-160
 # opening a 10 M-KV SST's index and filter as the reference's zlib / zstd writers shape them
 timeout -k 10 300 python -u tools/payload_probe.py 10000000 zlib-ref,zstd-ref,zlib,zstd > $OUT/payload_probe.log 2>&1 || { echo PROBE_FAILED; tail -20 $OUT/payload_probe.log; exit 1; }
 cat $OUT/payload_probe.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/ptrace -o run -- python3 tools/payload_probe.py 10000000 zlib-ref,zstd-ref > $OUT/ptrace.log 2>&1 || { echo PTRACE_FAILED; tail -20 $OUT/ptrace.log; exit 1; }
+cut -d, -f1-4 $OUT/ptrace/run_kernel_stats.csv | head -24 | cut -c1-140
