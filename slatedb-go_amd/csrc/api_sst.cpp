@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <future>
 #include <sys/mman.h>
 #include <memory>
@@ -87,19 +88,21 @@ int ctx_snappy_encode_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std
 }
 
 // The same encoding assembled on the device: varint header and the chunks' encodings back to back
-// at ctx->e_k (device-to-device copies on the context's stream), then its CRC32 on the device, so
-// the encoded payload crosses the link once (into `out` after `out`'s current bytes), with its
-// BE32 CRC appended (bloom.Encode / encodeIndex framing).
-int ctx_snappy_encode_crc_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std::vector<uint8_t>& out) {
+// in `asmb` (device-to-device copies on stream st), then its CRC32 on the device, so the encoded
+// payload crosses the link once (into `out` after `out`'s current bytes), with its BE32 CRC
+// appended (bloom.Encode / encodeIndex framing).  slots / asmb / crcb: the buffers it may use;
+// lanes: large copies through the context's page-locked lanes (only from the context's own thread).
+static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, DevBuf& asmb, DevBuf& crcb,
+                                const uint8_t* d_src, size_t n, std::vector<uint8_t>& out, bool lanes) {
   SLATE_HIP(ctx_bind(ctx));
   const uint64_t nch = (uint64_t(n) + kSnapMaxChunk - 1) / kSnapMaxChunk;
-  SLATE_HIP(ctx->e_h.ensure(nch * kSnapChunkSlot + nch * 4 + 64));
-  uint8_t* slots = ctx->e_h.as<uint8_t>();
+  SLATE_HIP(slotb.ensure(nch * kSnapChunkSlot + nch * 4 + 64));
+  uint8_t* slots = slotb.as<uint8_t>();
   uint32_t* lens = reinterpret_cast<uint32_t*>(slots + nch * kSnapChunkSlot);
-  SLATE_HIP(launch_snappy_chunks(ctx->stream, d_src, n, slots, lens, ctx->num_cus));
+  SLATE_HIP(launch_snappy_chunks(st, d_src, n, slots, lens, ctx->num_cus));
   std::vector<uint32_t> hl(nch);
-  if (nch) SLATE_HIP(hipMemcpyAsync(hl.data(), lens, nch * 4, hipMemcpyDeviceToHost, ctx->stream));
-  SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  if (nch) SLATE_HIP(hipMemcpyAsync(hl.data(), lens, nch * 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
   uint8_t hdr[10];
   size_t hn = 0;
   for (uint64_t v = n; ; v >>= 7) {
@@ -108,26 +111,39 @@ int ctx_snappy_encode_crc_device(slate_ctx* ctx, const uint8_t* d_src, size_t n,
   }
   size_t total = hn;
   for (uint64_t c = 0; c < nch; c++) total += hl[c];
-  SLATE_HIP(ctx->e_k.ensure(total + 64));
-  uint8_t* d = ctx->e_k.as<uint8_t>();
-  SLATE_HIP(hipMemcpyAsync(d, hdr, hn, hipMemcpyHostToDevice, ctx->stream));
+  SLATE_HIP(asmb.ensure(total + 64));
+  uint8_t* d = asmb.as<uint8_t>();
+  SLATE_HIP(hipMemcpyAsync(d, hdr, hn, hipMemcpyHostToDevice, st));
   size_t o = hn;
   for (uint64_t c = 0; c < nch; c++) {
-    if (hl[c]) SLATE_HIP(hipMemcpyAsync(d + o, slots + c * kSnapChunkSlot, hl[c], hipMemcpyDeviceToDevice, ctx->stream));
+    if (hl[c]) SLATE_HIP(hipMemcpyAsync(d + o, slots + c * kSnapChunkSlot, hl[c], hipMemcpyDeviceToDevice, st));
     o += hl[c];
   }
+  SLATE_HIP(crcb.ensure(crc_scratch_bytes(total) + 16));
+  uint32_t* scratch = crcb.as<uint32_t>();
+  uint32_t* cout = scratch + (crc_scratch_bytes(total) / 4);
+  SLATE_HIP(launch_crc32(st, d, total, scratch, cout));
   uint32_t crc = 0;
-  const int st = ctx_crc32_device(ctx, d, total, &crc);  // stream-synchronous
-  if (st) return st;
+  SLATE_HIP(hipMemcpyAsync(&crc, cout, 4, hipMemcpyDeviceToHost, st));
+  SLATE_HIP(hipStreamSynchronize(st));
   const size_t base = out.size();
   out.resize(base + total + 4);
-  const int s2 = ctx_d2h(ctx, out.data() + base, d, total, ctx->stream);
-  if (s2) return s2;
+  if (lanes) {
+    const int s2 = ctx_d2h(ctx, out.data() + base, d, total, st);
+    if (s2) return s2;
+  } else if (total) {
+    SLATE_HIP(hipMemcpyAsync(out.data() + base, d, total, hipMemcpyDeviceToHost, st));
+    SLATE_HIP(hipStreamSynchronize(st));
+  }
   out[base + total] = uint8_t(crc >> 24);
   out[base + total + 1] = uint8_t(crc >> 16);
   out[base + total + 2] = uint8_t(crc >> 8);
   out[base + total + 3] = uint8_t(crc);
   return SLATE_OK;
+}
+
+int ctx_snappy_encode_crc_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std::vector<uint8_t>& out) {
+  return snappy_encode_crc_on(ctx, ctx->stream, ctx->e_h, ctx->e_k, ctx->e_j, d_src, n, out, true);
 }
 
 int ctx_snappy_encode_host(slate_ctx* ctx, const uint8_t* data, size_t n, std::vector<uint8_t>& out) {
@@ -1050,7 +1066,7 @@ static int pending_push_host(slate_sst_builder* b) {
   return st;
 }
 
-static int builder_flush(slate_sst_builder* b, bool final) {
+static int builder_flush(slate_sst_builder* b, bool final, const std::function<void(uint64_t)>* after_hashes = nullptr) {
   slate_ctx* ctx = b->ctx;
   hipStream_t st = ctx->stream;
   int pst = pending_push_host(b);
@@ -1115,6 +1131,8 @@ static int builder_flush(slate_sst_builder* b, bool final) {
   uint64_t nb_total = 0;
   SLATE_HIP(hipMemcpyAsync(&nb_total, w.counts + chunks, 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
+  // every key's hash is in d_hashes now (the final flush consumes all pending keys)
+  if (final && after_hashes) (*after_hashes)(b->n_hashes + n64);
   SLATE_HIP(launch_encode_blocks(st, a, w));
   // the last block is still open unless this is the final flush (Build)
   const uint64_t nb = final ? nb_total : nb_total - 1;
@@ -1404,13 +1422,96 @@ int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_
   return SLATE_OK;
 }
 
+}  // extern "C"
+
+// The SST filter of every key added (builder.go:225-235: bloom.go:112-133 Build, :52-67 Encode)
+// for CodecNone / CodecSnappy, computed on the context's second stream by a host thread of its own
+// while the final flush encodes the blocks on the main stream (the flush touches none of these
+// buffers, and nothing here goes through the context's page-locked lanes).
+struct FilterOut {
+  int st = SLATE_OK;
+  uint16_t np = 0;
+  std::vector<uint8_t> section;  // compress(BE16 numProbes || bits) || BE32 CRC
+  std::vector<uint8_t> bits;
+};
+
+static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
+  FilterOut f;
+  slate_ctx* ctx = b->ctx;
+  auto fail = [&](int st) {
+    f.st = st;
+    return f;
+  };
+  if (ctx_bind(ctx) != hipSuccess) return fail(SLATE_E_NO_DEVICE);
+  if (!ctx->aux) {
+    const hipError_t e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+    if (e != hipSuccess) return fail(hip_status(e));
+  }
+  hipStream_t st = ctx->aux;
+  uint64_t nb = 0;
+  if (b->num_keys > 0) {
+    f.np = bloom_num_probes(b->cfg.filter_bits_per_key);
+    nb = bloom_filter_bytes(b->num_keys, b->cfg.filter_bits_per_key);
+    if (nb * 8 == 0 || nb * 8 > 0xFFFFFFFFull) return fail(SLATE_E_INVALID_ARG);  // Go: divide by zero / uint32 bits
+  }
+  auto hip = [&](hipError_t e) { return e == hipSuccess ? SLATE_OK : hip_status(e); };
+  int s = hip(ctx->x_words.ensure(((nb + 3) & ~uint64_t(3)) + 16));
+  if (!s) s = hip(ctx->x_enc.ensure(nb + 2 + 16));
+  if (s) return fail(s);
+  uint32_t* words = ctx->x_words.as<uint32_t>();
+  uint8_t* enc = ctx->x_enc.as<uint8_t>();
+  const uint8_t hdr[2] = {uint8_t(f.np >> 8), uint8_t(f.np)};
+  if (nb) {
+    s = hip(hipMemsetAsync(words, 0, (nb + 3) & ~uint64_t(3), st));
+    if (!s) s = hip(launch_bloom_build(st, b->d_hashes.as<uint64_t>(), n_hashes, f.np, uint32_t(nb * 8), words));
+  }
+  if (!s) s = hip(hipMemcpyAsync(enc, hdr, 2, hipMemcpyHostToDevice, st));
+  if (!s && nb) s = hip(hipMemcpyAsync(enc + 2, words, nb, hipMemcpyDeviceToDevice, st));
+  f.bits.resize(nb);
+  if (!s && nb) s = hip(hipMemcpyAsync(f.bits.data(), words, nb, hipMemcpyDeviceToHost, st));
+  if (!s) s = hip(hipStreamSynchronize(st));
+  if (s) return fail(s);
+  if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
+    s = snappy_encode_crc_on(ctx, st, ctx->x_slots, ctx->x_asm, ctx->x_crc, enc, nb + 2, f.section, false);
+    if (s) return fail(s);
+    return f;
+  }
+  // CodecNone: BE16 numProbes || bits || BE32 CRC (the CRC on the device)
+  s = hip(ctx->x_crc.ensure(crc_scratch_bytes(nb + 2) + 16));
+  if (s) return fail(s);
+  uint32_t* scratch = ctx->x_crc.as<uint32_t>();
+  uint32_t* cout = scratch + crc_scratch_bytes(nb + 2) / 4;
+  uint32_t crc = 0;
+  s = hip(launch_crc32(st, enc, nb + 2, scratch, cout));
+  if (!s) s = hip(hipMemcpyAsync(&crc, cout, 4, hipMemcpyDeviceToHost, st));
+  if (!s) s = hip(hipStreamSynchronize(st));
+  if (s) return fail(s);
+  f.section.reserve(nb + 6);
+  f.section.push_back(hdr[0]);
+  f.section.push_back(hdr[1]);
+  f.section.insert(f.section.end(), f.bits.begin(), f.bits.end());
+  put_be32(f.section, crc);
+  return f;
+}
+
+extern "C" {
+
 int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   if (!b || !table || b->built) return SLATE_E_INVALID_ARG;
   if (b->sticky) return b->sticky;
   slate_ctx* ctx = b->ctx;
   const double t0 = host_trace() ? now_ms() : 0.0;
-  int st = builder_flush(b, true);
-  if (st) return st;
+  // None / Snappy: the filter is built beside the final flush (its GPU work overlaps the blocks'
+  // encode and their transfer); other codecs' filter encoders share the flush's buffers
+  const bool side_filter = (b->cfg.codec == SLATE_CODEC_NONE || b->cfg.codec == SLATE_CODEC_SNAPPY) &&
+                           b->num_keys >= b->cfg.min_filter_keys;
+  std::future<FilterOut> fjob;
+  const std::function<void(uint64_t)> start_filter = [&](uint64_t nh) {
+    fjob = std::async(std::launch::async, build_filter_aux, b, nh);
+  };
+  int st = builder_flush(b, true, side_filter ? &start_filter : nullptr);
+  if (side_filter && !fjob.valid() && !st) start_filter(b->n_hashes);  // nothing was pending
+  if (st) return st;  // (a started filter job is joined by its future)
   const double t1 = host_trace() ? now_ms() : 0.0;
   b->built = true;
   slate_sst_table* t = new slate_sst_table();
@@ -1422,7 +1523,19 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   const uint64_t filter_off = b->current_len + buf.size();
   uint64_t filter_len = 0;
   // ---- bloom filter (builder.go:225-235, bloom.go:112-133 Build, :52-67 Encode)
-  if (b->num_keys >= b->cfg.min_filter_keys) {
+  if (side_filter) {
+    FilterOut f = fjob.get();
+    if (f.st) {
+      fb_job.wait();
+      delete t;
+      return f.st;
+    }
+    buf.insert(buf.end(), f.section.begin(), f.section.end());
+    t->bloom_bits.swap(f.bits);
+    t->has_bloom = true;
+    t->num_probes = f.np;
+    filter_len = f.section.size();
+  } else if (b->num_keys >= b->cfg.min_filter_keys) {
     uint16_t np = 0;
     uint64_t nb = 0;
     if (b->num_keys > 0) {
