@@ -986,6 +986,14 @@ struct slate_sst_builder {
   std::vector<uint64_t> hko{0}, hvo{0};
   uint64_t pending_lower = 2;  // lower bound of the pending KVs' encoded size
   bool dirty = false;
+  // Go's block.Builder for the single-add path (builder.go:160-176, block.go:162-182), replayed on
+  // the host so that NextBlock hands out a block after the very Add that finished it: the open
+  // block's first key and curBlockSize, and whether a block was finished since the last GPU pass.
+  // A batch add leaves the open block unknown here (track = false: the lower bound decides).
+  bool track = true;
+  std::vector<uint8_t> open_first;
+  uint64_t open_size = 0;
+  bool boundary = false;
   std::deque<ByteView> blocks;  // finished, not yet popped
   std::vector<uint64_t> meta_off;
   std::vector<uint8_t> meta_keys;
@@ -1309,6 +1317,27 @@ int slate_sst_builder_add(slate_sst_builder* b, const uint8_t* key, size_t key_l
   b->ht.push_back(tomb ? 1 : 0);
   b->pending_lower += 2 + 13 + (tomb ? 0 : 4 + value_len);
   b->dirty = true;
+  if (b->track) {
+    // v0Size (row.go:95-107) + the offset, the key prefix against the block's first key
+    // (computePrefixLen, row.go:292-318: a uint16)
+    auto entry = [&](uint64_t prefix) { return 2 + 2 + 2 + (key_len - prefix) + 8 + 1 + (tomb ? 0 : 4 + value_len); };
+    if (b->open_first.empty()) {
+      b->open_first.assign(key, key + key_len);
+      b->open_size = 2 + entry(0);
+    } else {
+      const size_t m = std::min(key_len, b->open_first.size());
+      size_t lcp = 0;
+      while (lcp < m && b->open_first[lcp] == key[lcp]) lcp++;
+      const uint64_t sz = b->open_size + entry(uint16_t(lcp));
+      if (sz > b->cfg.block_size) {  // block.Builder.Add refuses it: the block is finished
+        b->boundary = true;
+        b->open_first.assign(key, key + key_len);
+        b->open_size = 2 + entry(0);
+      } else {
+        b->open_size = sz;
+      }
+    }
+  }
   if (!b->has_first_key) {  // builder.go:178-180
     b->first_key.assign(key, key + key_len);
     b->has_first_key = true;
@@ -1336,6 +1365,7 @@ int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const
     m++;
   }
   if (m) {
+    b->track = false;
     int st = pending_push_host(b);  // keep the order of earlier single adds
     if (st) return b->sticky = st;
     if (is_tomb) {
@@ -1374,6 +1404,7 @@ int slate_sst_builder_add_batch_device(slate_sst_builder* b, const uint8_t* d_ke
   slate_ctx* ctx = b->ctx;
   hipStream_t st = ctx->stream;
   SLATE_HIP(ctx_bind(ctx));
+  b->track = false;
   int s = pending_push_host(b);
   if (s) return b->sticky = s;
   // the first empty key ends the batch (block.go:163); the range and the first key
@@ -1406,11 +1437,14 @@ int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_
   if (!b || !present) return SLATE_E_INVALID_ARG;
   *present = 0;
   if (b->sticky) return b->sticky;
-  // A finished block exists only once the pending KVs overflow one block; the
-  // lower bound avoids a GPU pass while they certainly fit.
-  if (b->blocks.empty() && b->dirty && b->pending_lower > b->cfg.block_size) {
+  // A finished block exists only once the pending KVs overflow one block: single adds know exactly
+  // when Go finished one (the replayed block.Builder); after batch adds, the lower bound avoids a
+  // GPU pass while they certainly fit.
+  const bool due = b->track ? b->boundary : b->pending_lower > b->cfg.block_size;
+  if (b->blocks.empty() && b->dirty && due) {
     int st = builder_flush(b, false);
     if (st) return b->sticky = st;
+    b->boundary = false;
   }
   if (b->blocks.empty()) return SLATE_OK;
   const ByteView& blk = b->blocks.front();

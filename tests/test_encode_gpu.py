@@ -65,6 +65,27 @@ def test_random_sst_bytes(sc, ctx, seed):
     assert t.bloom() == o.bloom()
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_next_block_after_each_add(sc, ctx, seed):
+    """sstable.Builder.NextBlock timing (builder.go:160-190): after every AddValue, the blocks the
+    library hands out are exactly the ones the reference's builder has finished by then (the block
+    is finished by the Add whose row no longer fits), byte for byte."""
+    rng = random.Random(100 + seed)
+    kvs = bg.random_kvs(rng, rng.randint(200, 900), alphabet=rng.choice([3, 256]), tomb_p=0.1)
+    bs = rng.choice([64, 200, 1024, 4096])
+    g = sc.SstBuilder(ctx, bs, 0, 10, ob.NONE)
+    o = ob.SstBuilder(bs, 0, 10, ob.NONE)
+    for i, (k, v) in enumerate(kvs):
+        assert g.add_value(k, v) == 0 and o.add_value(k, v) == 0
+        gb, ob_ = [], []
+        while (b := g.next_block()) is not None:
+            gb.append(b)
+        while (b := o.next_block()) is not None:
+            ob_.append(b)
+        assert gb == ob_, (i, len(gb), len(ob_))
+    assert g.build().encode() == (o.build(), o.encode_table())[1]
+
+
 def test_unsorted_and_duplicate_keys(sc, ctx):
     rng = random.Random(9)
     kvs = [(bytes(rng.randrange(3) for _ in range(rng.randint(1, 6))), b"v" * rng.randint(0, 40)) for _ in range(800)]
