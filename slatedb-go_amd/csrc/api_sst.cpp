@@ -1537,7 +1537,11 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   const double t0 = host_trace() ? now_ms() : 0.0;
   // None / Snappy: the filter is built beside the final flush (its GPU work overlaps the blocks'
   // encode and their transfer); other codecs' filter encoders share the flush's buffers
-  const bool side_filter = (b->cfg.codec == SLATE_CODEC_NONE || b->cfg.codec == SLATE_CODEC_SNAPPY) &&
+  static const bool side_ok = [] {  // SLATE_SIDE_FILTER=0: the filter after the flush (A/B runs)
+    const char* e = getenv("SLATE_SIDE_FILTER");
+    return !(e && *e == '0');
+  }();
+  const bool side_filter = side_ok && (b->cfg.codec == SLATE_CODEC_NONE || b->cfg.codec == SLATE_CODEC_SNAPPY) &&
                            b->num_keys >= b->cfg.min_filter_keys;
   std::future<FilterOut> fjob;
   const std::function<void(uint64_t)> start_filter = [&](uint64_t nh) {

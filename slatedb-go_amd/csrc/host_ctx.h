@@ -243,10 +243,13 @@ struct slate_ctx {
   }
 };
 
-#define SLATE_HIP(expr)                                   \
-  do {                                                    \
-    hipError_t _e = (expr);                               \
-    if (_e != hipSuccess) return hip_status(_e);          \
+#define SLATE_HIP(expr)                                                                               \
+  do {                                                                                                \
+    hipError_t _e = (expr);                                                                           \
+    if (_e != hipSuccess) {                                                                           \
+      if (host_trace()) fprintf(stderr, "[slate hip] %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+      return hip_status(_e);                                                                          \
+    }                                                                                                 \
   } while (0)
 
 inline int hip_status(hipError_t e) {
