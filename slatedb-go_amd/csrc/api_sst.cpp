@@ -1169,9 +1169,11 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     // raw sizes -> per-block slots; golang/snappy + CRC per block; scan of the
     // compressed sizes; compaction into back-to-back blocks
     const uint64_t raw_total = out_off[nb];
-    SLATE_HIP(ctx->s_slots.ensure(snappy_slots_bytes(raw_total, nb)));
+    // 16 guard bytes in front: the wave CRC of a slot reads the aligned dword around its first
+    // byte, i.e. up to 3 bytes before block 0's slot (outside a fresh allocation: a fault)
+    SLATE_HIP(ctx->s_slots.ensure(snappy_slots_bytes(raw_total, nb) + 16));
     SLATE_HIP(ctx->s_aux.ensure((nb + 1) * 8 + 64));
-    uint8_t* slots = ctx->s_slots.as<uint8_t>();
+    uint8_t* slots = ctx->s_slots.as<uint8_t>() + 16;
     uint64_t* csize = ctx->s_aux.as<uint64_t>();
     SLATE_HIP(hipMemsetAsync(csize + nb, 0, 8, st));
     SLATE_HIP(launch_pack_snappy(st, a, w, uint32_t(nb), w.block_size, slots, csize, ctx->num_cus));
