@@ -113,14 +113,16 @@ __device__ int zq_table(uint32_t mode, const uint8_t* in, int32_t off, uint32_t 
   }
   if (mode == 2) {
     int hs = 0, a = 0, last = 0;
-    if (lane == 0) {
+    if (lane == 0) {  // built in LDS (the build's scattered read-modify-writes), then copied out
       hs = zs_ncount(in, off, n, sc->norm, maxs, maxal, &a, &last);
-      if (hs >= 0 && zs_fse_build(fse + size_t(own) * kZqSlot, sc->norm, last, a, sc->next)) hs = -1;
+      if (hs >= 0 && zs_fse_build(sc->ll, sc->norm, last, a, sc->next)) hs = -1;
     }
     hs = zrfl(hs);
     a = zrfl(a);
     zs_sync();
     if (hs < 0) return -1;
+    for (uint32_t i = uint32_t(lane); i < (1u << a); i += 64) fse[size_t(own) * kZqSlot + i] = sc->ll[i];
+    zs_sync();
     *slot = own;
     *al = uint32_t(a);
     return hs;
@@ -133,14 +135,20 @@ __global__ __launch_bounds__(64) void zq_scan_kernel(const uint8_t* __restrict__
   __shared__ __attribute__((aligned(16))) ZsScratch sc;
   const int lane = threadIdx.x;
   const uint32_t pre = 3 * nblk;  // predefined tables: slots pre + 0..2
-  if (lane == 0) {
+  if (lane == 0) {  // in LDS, then copied out
     for (int i = 0; i < 36; i++) sc.norm[i] = kZsLLDef[i];
-    zs_fse_build(Z.fse + size_t(pre) * kZqSlot, sc.norm, 35, 6, sc.next);
+    zs_fse_build(sc.ll, sc.norm, 35, 6, sc.next);
     for (int i = 0; i < 29; i++) sc.norm[i] = kZsOFDef[i];
-    zs_fse_build(Z.fse + size_t(pre + 1) * kZqSlot, sc.norm, 28, 5, sc.next);
+    zs_fse_build(sc.of, sc.norm, 28, 5, sc.next);
     for (int i = 0; i < 53; i++) sc.norm[i] = kZsMLDef[i];
-    zs_fse_build(Z.fse + size_t(pre + 2) * kZqSlot, sc.norm, 52, 6, sc.next);
+    zs_fse_build(sc.ml, sc.norm, 52, 6, sc.next);
   }
+  zs_sync();
+  for (uint32_t i = uint32_t(lane); i < 64; i += 64) {
+    Z.fse[size_t(pre) * kZqSlot + i] = sc.ll[i];
+    Z.fse[size_t(pre + 2) * kZqSlot + i] = sc.ml[i];
+  }
+  for (uint32_t i = uint32_t(lane); i < 32; i += 64) Z.fse[size_t(pre + 1) * kZqSlot + i] = sc.of[i];
   zs_sync();
   uint32_t huf = kZqNone, cur[3] = {kZqNone, kZqNone, kZqNone}, cal[3] = {0, 0, 0};
   uint32_t nseq_all = 0, nlit_all = 0;
