@@ -381,6 +381,8 @@ class Context:
                 if byte < 0x80:
                     break
             cap = max(cap, min(x, 1 << 32) + 64)
+        elif codec != NONE:  # no size header: room for 4x, so a typical filter decodes in one call
+            cap = 4 * len(buf) + 65536
         out = np.zeros(cap, np.uint8)
         npr = C.c_uint16()
         bl = C.c_size_t()
@@ -593,7 +595,10 @@ class Index:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            lib().slate_index_free(self._h)
+            try:
+                lib().slate_index_free(self._h)
+            except TypeError:  # interpreter shutdown: the module's globals are already gone
+                pass
             self._h = None
 
     def block_offsets(self) -> np.ndarray:

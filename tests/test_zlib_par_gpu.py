@@ -110,7 +110,8 @@ print("ok")
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
     print("\n" + "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[slate zlib-par]")))
     chains = [ln for ln in r.stderr.splitlines() if ln.startswith("[slate zlib-par]") and "candidates" in ln]
-    assert len(chains) == 2 and all("fail 0" in ln for ln in chains), r.stderr[-3000:]
+    # the index and the filter (and the filter again if the binding's first capacity was short)
+    assert len(chains) >= 2 and all("fail 0" in ln for ln in chains), r.stderr[-3000:]
 
 
 @pytest.mark.parametrize("level,strategy", [(1, zlib.Z_DEFAULT_STRATEGY), (9, zlib.Z_DEFAULT_STRATEGY),
