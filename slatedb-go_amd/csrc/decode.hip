@@ -1734,6 +1734,12 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
     if (e != hipSuccess) return e;
     decode_list_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);
     decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  } else if (a.codec == SLATE_CODEC_NONE && !a.raw && !(dbg_bits(a) & 16)) {
+    // CodecNone blocks: the streaming wave-per-block decoder (decode_none.hip); blocks beyond its
+    // size window take the exact wave path through large_list
+    hipError_t e = launch_decode_none(st, a, num_cus);
+    if (e != hipSuccess) return e;
+    decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else {
     decode_fast_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a);
     decode_large_kernel<0><<<uint32_t(num_cus), 64, lds_large, st>>>(a);

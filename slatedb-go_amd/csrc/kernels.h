@@ -88,6 +88,9 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
+// CodecNone blocks (not raw payloads): one wave per block, streaming (decode_none.hip); blocks with
+// more than 5104 or fewer than 4 data bytes are appended to a.large_list for decode_large_kernel<0>.
+hipError_t launch_decode_none(hipStream_t st, const DecodeArgs& a, int num_cus);
 // CodecLz4 blocks: the lane-per-block decoder for one-block frames (XXH32 content checksum in its
 // loop); every other shape and any failed check is appended to z.list for the exact path.
 hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);

@@ -4,6 +4,7 @@ Bit-exact on every field: plan layout (out_off / row_base), per-block meta
 (status, detail, aux, data_len, n_rows, flags), decoded bytes, row descriptors.
 """
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -137,3 +138,39 @@ def test_single_block_api(ctx, ref_vectors):
         assert st == 0 and d == data and o == offs
         st, m, d, o = ctx.block_decode(enc[:-1] + bytes([enc[-1] ^ 1]), codec)
         assert st == 2
+
+
+@pytest.mark.parametrize("misalign", [0, 1, 7, 12, 13, 15])
+def test_none_size_window(ctx, misalign):
+    """CodecNone blocks around the streaming kernel's window (decode_none.hip: 4..5104 data bytes in
+    five register rows of 64 chunks; outside it the exact wave path): valid one- and many-row blocks
+    of exact data lengths, random bytes under a valid CRC (the block checks' error paths) and a
+    flipped CRC, at every chunk phase."""
+    rng = random.Random(77 + misalign)
+    blocks = []
+    for t in [4, 5, 6, 15, 16, 17, 31, 33, 63, 64, 65, 1023, 1024, 1025, 2047, 4095, 4096, 4097, 5087, 5088, 5089,
+              5103, 5104, 5105, 5120, 5200, 6000]:
+        if t >= 26:  # one KV: 4 + key + 8 + 1 + 4 + value bytes, then one offset and the count
+            bb = ob.BlockBuilder(1 << 16)
+            bb.add_value(b"k" * 5, bytes(rng.randrange(256) for _ in range(t - 26)))
+            data, offs, _ = bb.build()
+            assert len(data) + 2 * len(offs) + 2 == t
+            blocks.append(ob.block_encode(data, offs, ob.NONE)[1])
+        body = bytes(rng.randrange(256) for _ in range(t))
+        blocks.append(bg.recrc(body))
+        blocks.append(body + bytes([rng.randrange(256) for _ in range(4)]))
+        if t >= 8:  # random rows under a plausible offset array: the bounds / FirstKey / row error paths
+            cnt = rng.randint(1, min(80, (t - 4) // 2))
+            osi = t - 2 - 2 * cnt
+            offs = [rng.randrange(osi + 2) if rng.random() < 0.1 else rng.randrange(max(osi - 12, 1))
+                    for _ in range(cnt)]
+            data = bytearray(body[:osi])
+            if rng.random() < 0.7 and offs[0] + 2 <= osi:  # a FirstKey that fits: rows decode (or fail) one by one
+                data[offs[0]:offs[0] + 2] = struct.pack(">H", rng.randrange(max(1, min(9, osi - offs[0] - 1))))
+            body2 = bytes(data) + b"".join(struct.pack(">H", o) for o in offs) + struct.pack(">H", cnt)
+            blocks.append(bg.recrc(body2))
+    kvs = bg.random_kvs(rng, 400, alphabet=16)
+    for bs in (300, 4096, 5000, 5100):
+        blocks += bg.sst_blocks(kvs, bs, ob.NONE)
+    meta = _compare(ctx, ob.NONE, blocks, misalign=misalign)
+    assert (meta["status"] == 0).sum() > 20 and len(set(meta["status"].tolist())) > 3
