@@ -64,7 +64,8 @@ def parse():
                    help="skip the extra legs (codec_none, configs4_zstd, configs2_encode; N=1 only)")
     p.add_argument("--extra-steps", type=int, default=10, help="timed steps of each extra leg")
     p.add_argument("--allow-variant", action="store_true", help="profiling only: accept SLATE_LIB_VARIANT")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_decode_latest.json"))
+    p.add_argument("--pmc-json", default="", help="PMC traffic file (default: profiles/pmc_decode_latest.json, "
+                   "CodecNone: profiles/pmc_decode_none_latest.json)")
     return p.parse_args()
 
 
@@ -195,12 +196,15 @@ def main():
 
     # roofline of the dominant kernel: algorithmic bytes per launch / its event time
     roofline = decode_roofline(enc_bytes, n, dec_bytes, n_rows, kern_ms)
-    traffic, traffic_src = pmc_traffic(args.pmc_json, n, args.codec)
+    pmc_json = args.pmc_json or os.path.join(REPO, "profiles", "pmc_decode_none_latest.json" if args.codec == "none"
+                                             else "pmc_decode_latest.json")
+    traffic, traffic_src = pmc_traffic(pmc_json, n, args.codec)
     roofline["traffic"] = traffic
     roofline["traffic_source"] = traffic_src
     roofline["kernel"] = {"snappy": "decode_lpb2_kernel", "lz4": "decode_lpb2_kernel<true> (+ decode_list_kernel<0>)",
                           "zstd": "zstd decode: zs_fast_parse/crc/build/sum + decode_list_kernel<2> "
-                                  "(HIP events around the whole decode)"}.get(args.codec, "decode_fast_kernel<0>")
+                                  "(HIP events around the whole decode)",
+                          "none": "decode_none_kernel"}.get(args.codec, "decode_fast_kernel<0>")
 
     if args.codec == "zstd":
         workload = (f"configs[4] mixed: {n} x 4 KiB Zstd blocks per GPU, 1 KiB values, skewed key prefixes, "
@@ -377,7 +381,9 @@ def codec_none_leg(sc, ctx, stream, wl, args, threads):
     blob, in_off = wl.block_set(sc.NONE, 0, 1, n, seed=SEED, half=True, threads=threads)
     leg = DecodeLeg(sc, ctx, sc.NONE, blob, in_off)
     meta, res = _decode_leg_result(sc, leg, torch, stream, args.extra_steps, 2, int(in_off[-1]))
-    res["roofline"]["kernel"] = "decode_fast_kernel<0> (+ plan)"
+    res["roofline"]["kernel"] = "decode_none_kernel (+ decode_large_kernel<0> over an empty list)"
+    res["roofline"]["traffic"], res["roofline"]["traffic_source"] = pmc_traffic(
+        os.path.join(REPO, "profiles", "pmc_decode_none_latest.json"), n, "none")
     res["verified"] = leg.verify_against_generator(wl, (0, 1, n), "all", meta, threads, True)
     res["workload"] = f"{n} x 4 KiB CodecNone blocks (configs[1] keys and V-half values), device-resident decode"
     leg.free()

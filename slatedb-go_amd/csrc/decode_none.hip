@@ -36,6 +36,16 @@ constexpr uint32_t kNoneMaxData = (kNoneSlots - 1) * 16;  // 5104 data bytes at 
 constexpr uint32_t kNoneStage = 5120;  // per-wave LDS staging: input chunks 0 .. nout
 constexpr uint32_t kAdvN = 6;  // zero-byte advance tables for 32, 64, ..., 1024 bytes
 constexpr uint32_t kNoneLds = kTab16Bytes + kAdvN * 4096 + (kNoneThreads / 64) * kNoneStage;
+// cache policy of the output / row stores (0 default, 2 nt, 16 sc1): nt, and nt block loads, measured
+// 2.04 vs 2.12 ms per 1 M blocks (profiles/round3/none/ab_policy.txt)
+#ifndef SLATE_NONE_CPOL
+#define SLATE_NONE_CPOL 2
+#endif
+constexpr int kNoneCpol = SLATE_NONE_CPOL;
+#ifndef SLATE_NONE_LDPOL  // cache policy of the block loads (0 default, 2 nt)
+#define SLATE_NONE_LDPOL 2
+#endif
+constexpr int kNoneLdpol = SLATE_NONE_LDPOL;
 static_assert(2 * kNoneLds <= 163840, "two workgroups per CU");
 
 // x^(8N) mod P for N = 32 << s: multiplying a raw CRC register by it advances the register over
@@ -48,14 +58,60 @@ struct AdvConsts {
 };
 static __constant__ AdvConsts g_adv = AdvConsts();
 
-// register advanced over N zero bytes by four lookups: t = 4 x 256 entries, t[j][i] = (i << 8j) * x^(8N)
-__device__ __forceinline__ uint32_t adv_tab(const uint32_t* t, uint32_t c) {
-  return xor3(t[c & 0xff], t[256 + ((c >> 8) & 0xff)], t[512 + ((c >> 16) & 0xff)]) ^ t[768 + (c >> 24)];
+// Table lookups.  A lookup's LDS address is (byte k of x) * 4 plus a table offset: one SDWA shift
+// (src1_sel picks the byte) instead of an extract and a shift, and the table offset rides in the
+// ds_read's immediate (the tables start at LDS address 0).
+template <int K>
+__device__ __forceinline__ uint32_t idx4(uint32_t x) {
+  uint32_t r;
+  if constexpr (K == 0)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
+  else if constexpr (K == 1)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
+  else if constexpr (K == 2)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(x));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
+  return r;
+}
+template <uint32_t kOff>
+__device__ __forceinline__ uint32_t lut(const uint8_t* lds, uint32_t i4) {
+  return *reinterpret_cast<const uint32_t*>(lds + kOff + i4);
+}
+// the four lookups of one dword against tables kT, kT - 1, kT - 2, kT - 3 (1 KiB each) at byte offset kBase
+template <uint32_t kBase, int kT>
+__device__ __forceinline__ void lut4(const uint8_t* lds, uint32_t x, uint32_t& a, uint32_t& b, uint32_t& c,
+                                     uint32_t& d) {
+  a = lut<kBase + 1024 * kT>(lds, idx4<0>(x));
+  b = lut<kBase + 1024 * (kT - 1)>(lds, idx4<1>(x));
+  c = lut<kBase + 1024 * (kT - 2)>(lds, idx4<2>(x));
+  d = lut<kBase + 1024 * (kT - 3)>(lds, idx4<3>(x));
+}
+// the raw CRC register of a 16-byte chunk from a zero register (slicing-by-16, crc16_step)
+__device__ __forceinline__ uint32_t crc_chunk0(const uint8_t* lds, const v4u& v) {
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, c2, c3, d0, d1, d2, d3;
+  lut4<0, 15>(lds, v.x, a0, a1, a2, a3);
+  lut4<0, 11>(lds, v.y, b0, b1, b2, b3);
+  lut4<0, 7>(lds, v.z, c0, c1, c2, c3);
+  lut4<0, 3>(lds, v.w, d0, d1, d2, d3);
+  return xor3(xor3(a0, a1, a2), xor3(a3, b0, b1), xor3(xor3(b2, b3, c0), xor3(c1, c2, c3), xor3(d0, d1, xor3(d2, d3, 0u))));
+}
+// register advanced over N zero bytes by four lookups: table s (N = 32 << s), t[j][i] = (i << 8j) * x^(8N)
+template <int kS>
+__device__ __forceinline__ uint32_t adv_tab(const uint8_t* lds, uint32_t c) {
+  constexpr uint32_t o = kTab16Bytes + 4096 * kS;
+  return xor3(lut<o>(lds, idx4<0>(c)), lut<o + 1024>(lds, idx4<1>(c)), lut<o + 2048>(lds, idx4<2>(c))) ^
+         lut<o + 3072>(lds, idx4<3>(c));
 }
 // over 16 zero bytes: rows 12..15 of the slicing-by-16 tables (a chunk of zeros after c)
-__device__ __forceinline__ uint32_t adv16(const uint32_t* tab, uint32_t c) {
-  return xor3(tab[15 * 256 + (c & 0xff)], tab[14 * 256 + ((c >> 8) & 0xff)], tab[13 * 256 + ((c >> 16) & 0xff)]) ^
-         tab[12 * 256 + (c >> 24)];
+__device__ __forceinline__ uint32_t adv16(const uint8_t* lds, uint32_t c) {
+  uint32_t a, b, d, e;
+  lut4<0, 15>(lds, c, a, b, d, e);
+  return xor3(a, b, d) ^ e;
+}
+template <int kShift>
+__device__ __forceinline__ uint32_t row_shl(uint32_t v) {  // lane i <- lane i + kShift of its row of 16
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x100 + kShift, 0xf, 0xf, true));
 }
 // over t < 16 zero bytes: byte i < t of c is looked up after i steps and then carried over
 // t - 1 - i more zero bytes (slicing row t - 1 - i); the bytes from t on only shift down
@@ -165,7 +221,7 @@ __device__ __forceinline__ void issue_loads(const Geo& g, uint32_t lane, Loads& 
 #pragma unroll
   for (uint32_t q = 0; q < 5; q++) {
     const int32_t c = int32_t(64 * q + lane) - int32_t(g.pad);
-    L.p[q] = __builtin_amdgcn_raw_buffer_load_b128(R, c >= 0 ? uint32_t(16 * c) : kOOB, 0, 0);
+    L.p[q] = __builtin_amdgcn_raw_buffer_load_b128(R, c >= 0 ? uint32_t(16 * c) : kOOB, 0, kNoneLdpol);
   }
   L.x = __builtin_amdgcn_raw_buffer_load_b128(R, 16 * g.nout, 0, 0);
   const uint32_t pc = g.sh + g.clen;  // the stored CRC's first byte
@@ -191,6 +247,159 @@ __device__ __forceinline__ v4u out_chunk(const uint8_t* stage, uint32_t sh, int3
   return r;
 }
 
+// One block: stage its chunks (LDS), put the loads of the block two steps ahead into the same
+// registers, then decode it.  b / g / L advance to that block.
+__device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* tab, uint8_t* stage, uint32_t lane,
+                                           uint32_t step, uint32_t& b, Geo& g, Loads& L) {
+  const uint8_t* lds = reinterpret_cast<const uint8_t*>(tab);
+  slate_block_meta m{};
+  const Geo gc = g;
+  const uint32_t sh = gc.sh, clen = gc.clen, nout = gc.nout, pad = gc.pad;
+  if (gc.kind == 0) {
+#pragma unroll
+    for (uint32_t q = 0; q < 5; q++) {
+      const int32_t c = int32_t(64 * q + lane) - int32_t(pad);
+      if (c >= 0) wr128(stage + 16 * c, L.p[q], a.rt_zero);
+    }
+    if (lane == 0) wr128(stage + 16 * nout, L.x, a.rt_zero);
+  }
+  const uint32_t pc = sh + clen;
+  const uint32_t stored = __builtin_bswap32(alignb(L.s1, L.s0, pc & 3u));
+  const uint32_t bc = b;
+  b += step;
+  g = geo_of(a, b);
+  issue_loads(g, lane, L);
+  if (gc.kind == 1) {
+    m.status = SLATE_E_BLOCK_TOO_SMALL;
+    if (lane == 0) a.meta[bc] = m;
+  } else if (gc.kind == 2) {
+    if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = bc;
+  } else {
+    // ---- output chunks (slot v = 64q + lane holds output chunk j = v - pad) and their CRC:
+    // zero below chunk 0, the initial 0xFFFFFFFF folded into data bytes 0..3, the bytes after
+    // the data zeroed in the last chunk (t = 16 nout - clen of them)
+    v4u O[5];
+    uint32_t acc = 0;
+    const uint32_t r = clen - 16 * (nout - 1);  // data bytes in the last chunk (1..16)
+    const uint32_t t = 16 - r;
+#pragma unroll
+    for (uint32_t q = 0; q < 5; q++) {
+      const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
+      O[q] = out_chunk(stage, sh, j);
+      v4u c = O[q];
+      const bool first = j == 0, last = j == int32_t(nout) - 1, none = j < 0;
+      c.x ^= first ? 0xFFFFFFFFu : 0u;
+      if (q == 4) {  // the last chunk is slot 319: lane 63 of row 4
+        c.x &= (last && r < 4) ? (1u << (8 * r)) - 1u : 0xFFFFFFFFu;
+        c.y &= (last && r < 8) ? (r <= 4 ? 0u : (1u << (8 * (r - 4))) - 1u) : 0xFFFFFFFFu;
+        c.z &= (last && r < 12) ? (r <= 8 ? 0u : (1u << (8 * (r - 8))) - 1u) : 0xFFFFFFFFu;
+        c.w &= (last && r < 16) ? (r <= 12 ? 0u : (1u << (8 * (r - 12))) - 1u) : 0xFFFFFFFFu;
+      }
+      if (!(dbg_bits(a) & 1)) {  // (profiling variants only: bit 1 skips the CRC, 4 the rows, 8 the output stores)
+        const uint32_t k = crc_chunk0(lds, c);
+        // Horner over the rows: row q's chunks lie 1024 (4 - q) bytes before row 4's
+        acc = (q == 0 ? 0u : adv_tab<5>(lds, acc)) ^ (none ? 0u : k);
+      }
+    }
+    bool crc_ok = true;
+    if (!(dbg_bits(a) & 1)) {
+      // lane tree: lane l's chunks end 16 (63 - l) bytes before lane 63's; inside rows of 16 lanes
+      // by DPP row shifts, then the four row heads (lanes 0, 16, 32, 48) combined
+      acc = adv16(lds, acc) ^ row_shl<1>(acc);
+      acc = adv_tab<0>(lds, acc) ^ row_shl<2>(acc);
+      acc = adv_tab<1>(lds, acc) ^ row_shl<4>(acc);
+      acc = adv_tab<2>(lds, acc) ^ row_shl<8>(acc);
+      const uint32_t h1 = __builtin_amdgcn_readlane(acc, 16), h2 = __builtin_amdgcn_readlane(acc, 32),
+                     h3 = __builtin_amdgcn_readlane(acc, 48);
+      acc = adv_tab<3>(lds, acc) ^ h1;  // lane 0: rows 0-1
+      acc = adv_tab<3>(lds, acc) ^ h2;  // rows 0-2
+      acc = adv_tab<3>(lds, acc) ^ h3;  // rows 0-3
+      const uint32_t total = __builtin_amdgcn_readfirstlane(acc);
+      crc_ok = total == adv_small(tab, ~stored, t);
+    }
+    if (!crc_ok) {
+      m.status = SLATE_E_BLOCK_CHECKSUM;
+      if (lane == 0) a.meta[bc] = m;
+    } else {
+      // ---- the decoded block (16-byte slots; bytes after the data are padding)
+      const __amdgpu_buffer_rsrc_t RO = make_rsrc(a.out + a.out_off[bc], 16 * uint64_t(nout));
+#pragma unroll
+      for (uint32_t q = 0; q < 5; q++) {
+        const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
+        __builtin_amdgcn_raw_buffer_store_b128(O[q], RO, (j >= 0 && !(dbg_bits(a) & 8)) ? uint32_t(16 * j) : kOOB, 0,
+                                               kNoneCpol);
+      }
+      // ---- block.go:101-134 and the rows (rows.h block_finish arithmetic)
+      const uint32_t n = clen;
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(st_be16(stage, sh + n - 2));
+      const int32_t osi = int32_t(n) - 2 - 2 * int32_t(cnt);
+      if (osi <= 0) {
+        m.status = SLATE_E_BLOCK_INDEX_OFFSET;
+        m.detail = osi;
+      } else {
+        const uint32_t osu = uint32_t(osi);  // < 65536 on this path: uint16(offsetStartIndex) == osi
+        uint32_t bad = 0xFFFFFFFFu, bad_off = 0;
+        for (uint32_t i0 = 0; i0 < cnt && bad == 0xFFFFFFFFu; i0 += 64) {
+          const uint32_t i = i0 + lane;
+          const uint32_t off = i < cnt ? st_be16(stage, sh + osu + 2 * i) : 0u;
+          const uint64_t m64 = __ballot(i < cnt && off > osu);
+          if (m64) {
+            const uint32_t l0 = uint32_t(__builtin_ctzll(m64));
+            bad = i0 + l0;
+            bad_off = __builtin_amdgcn_readlane(off, l0);
+          }
+        }
+        if (bad != 0xFFFFFFFFu) {
+          m.status = SLATE_E_BLOCK_OFFSET_BOUNDS;
+          m.aux = uint16_t(bad);
+          m.detail = int32_t(bad_off);
+        } else {
+          m.data_len = osu;
+          m.n_rows = uint16_t(cnt);
+          if (cnt == 0) {
+            m.status = SLATE_E_BLOCK_NO_OFFSETS;
+          } else {
+            // FirstKey (block.go:130-131): uint16 arithmetic, Go panics out of range
+            const uint32_t off0 = __builtin_amdgcn_readfirstlane(st_be16(stage, sh + osu));
+            if (osu - off0 < 2) {
+              m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
+            } else {
+              const uint16_t kl = uint16_t(__builtin_amdgcn_readfirstlane(st_be16(stage, sh + off0)));
+              const uint16_t lo = uint16_t(off0 + 2), hi = uint16_t(off0 + 2 + kl);
+              if (lo > hi || hi > n) {
+                m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
+              } else {
+                m.aux = kl;
+                const uint64_t rb = a.row_base[bc];
+                const uint32_t rcap = uint32_t(min(uint64_t(0xFFFFFFFFu), a.row_base[bc + 1] - rb));
+                uint32_t nr = cnt;
+                if (nr > rcap) {
+                  nr = rcap;
+                  m.flags |= SLATE_BLKF_ROWS_TRUNCATED;
+                }
+                // the first key's length: row 0 decoded against an empty first key
+                uint32_t sl0;
+                (void)row_stage(stage, sh, osu, off0, -1, &sl0);
+                const int fk = sl0 == 0xFFFFFFFFu ? -1 : int(__builtin_amdgcn_readfirstlane(sl0));
+                const __amdgpu_buffer_rsrc_t RR = make_rsrc(a.rows + rb, 16 * uint64_t(nr));
+                if (dbg_bits(a) & 4) nr = 0;
+                for (uint32_t i0 = 0; i0 < nr; i0 += 64) {
+                  const uint32_t i = i0 + lane;
+                  const uint32_t off = st_be16(stage, sh + osu + 2 * min(i, cnt - 1));
+                  uint32_t sl;
+                  const v4u row = row_stage(stage, sh, osu, off, i == 0 ? -1 : fk, &sl);
+                  __builtin_amdgcn_raw_buffer_store_b128(row, RR, i < nr ? 16 * i : kOOB, 0, kNoneCpol);
+                }
+              }
+            }
+          }
+        }
+      }
+      if (lane == 0) a.meta[bc] = m;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kNoneThreads) void decode_none_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);  // slicing-by-16 (16 KiB)
@@ -206,147 +415,17 @@ __global__ __launch_bounds__(kNoneThreads) void decode_none_kernel(DecodeArgs a)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* stage = smem + kTab16Bytes + kAdvN * 4096 + wave * kNoneStage;
   const uint32_t waves_total = gridDim.x * (kNoneThreads / 64);
-  uint32_t b = blockIdx.x * (kNoneThreads / 64) + wave;
-
-  Geo g = geo_of(a, b);
-  Loads L;
-  issue_loads(g, lane, L);
-  while (g.kind != 3) {
-    const uint32_t bn = b + waves_total;
-    const Geo gn = geo_of(a, bn);
-    slate_block_meta m{};
-    const Geo gc = g;
-    const uint32_t sh = gc.sh, clen = gc.clen, nout = gc.nout, pad = gc.pad;
-    // ---- stage this block's chunks (input chunk c at 16c), then start the next block's loads
-    if (gc.kind == 0) {
-#pragma unroll
-      for (uint32_t q = 0; q < 5; q++) {
-        const int32_t c = int32_t(64 * q + lane) - int32_t(pad);
-        if (c >= 0) wr128(stage + 16 * c, L.p[q], a.rt_zero);
-      }
-      if (lane == 0) wr128(stage + 16 * nout, L.x, a.rt_zero);
-    }
-    const uint32_t pc = sh + clen;
-    const uint32_t stored = __builtin_bswap32(alignb(L.s1, L.s0, pc & 3u));
-    issue_loads(gn, lane, L);
-
-    if (gc.kind == 1) {
-      m.status = SLATE_E_BLOCK_TOO_SMALL;
-      if (lane == 0) a.meta[b] = m;
-    } else if (gc.kind == 2) {
-      if (lane == 0) a.large_list[atomicAdd(a.large_count, 1u)] = b;
-    } else {
-      // ---- output chunks (slot v = 64q + lane holds output chunk j = v - pad) and their CRC:
-      // zero below chunk 0, the initial 0xFFFFFFFF folded into data bytes 0..3, the bytes after
-      // the data zeroed in the last chunk (t = 16 nout - clen of them)
-      v4u O[5];
-      uint32_t acc = 0;
-      const uint32_t r = clen - 16 * (nout - 1);  // data bytes in the last chunk (1..16)
-      const uint32_t t = 16 - r;
-#pragma unroll
-      for (uint32_t q = 0; q < 5; q++) {
-        const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
-        O[q] = out_chunk(stage, sh, j);
-        v4u c = O[q];
-        const bool first = j == 0, last = j == int32_t(nout) - 1, none = j < 0;
-        c.x ^= first ? 0xFFFFFFFFu : 0u;
-        if (q == 4) {  // the last chunk is slot 319: lane 63 of row 4
-          c.x &= (last && r < 4) ? (1u << (8 * r)) - 1u : 0xFFFFFFFFu;
-          c.y &= (last && r < 8) ? (r <= 4 ? 0u : (1u << (8 * (r - 4))) - 1u) : 0xFFFFFFFFu;
-          c.z &= (last && r < 12) ? (r <= 8 ? 0u : (1u << (8 * (r - 8))) - 1u) : 0xFFFFFFFFu;
-          c.w &= (last && r < 16) ? (r <= 12 ? 0u : (1u << (8 * (r - 12))) - 1u) : 0xFFFFFFFFu;
-        }
-        const uint32_t k = crc16_step(tab, 0u, c.x, c.y, c.z, c.w);
-        // Horner over the rows: row q's chunks lie 1024 (4 - q) bytes before row 4's
-        acc = (q == 0 ? 0u : adv_tab(adv + 5 * 1024, acc)) ^ (none ? 0u : k);
-      }
-      // lane tree: lane l's chunks end 16 (63 - l) bytes before lane 63's
-      acc = adv16(tab, acc) ^ __shfl_down(acc, 1, 64);
-#pragma unroll
-      for (uint32_t s = 1; s < 6; s++) acc = adv_tab(adv + (s - 1) * 1024, acc) ^ __shfl_down(acc, 1u << s, 64);
-      const uint32_t total = __builtin_amdgcn_readfirstlane(acc);
-      const bool crc_ok = total == adv_small(tab, ~stored, t);
-      if (!crc_ok) {
-        m.status = SLATE_E_BLOCK_CHECKSUM;
-        if (lane == 0) a.meta[b] = m;
-      } else {
-        // ---- the decoded block (16-byte slots; bytes after the data are padding)
-        const __amdgpu_buffer_rsrc_t RO = make_rsrc(a.out + a.out_off[b], 16 * uint64_t(nout));
-#pragma unroll
-        for (uint32_t q = 0; q < 5; q++) {
-          const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
-          __builtin_amdgcn_raw_buffer_store_b128(O[q], RO, j >= 0 ? uint32_t(16 * j) : kOOB, 0, 0);
-        }
-        // ---- block.go:101-134 and the rows (rows.h block_finish arithmetic)
-        const uint32_t n = clen;
-        const uint32_t cnt = __builtin_amdgcn_readfirstlane(st_be16(stage, sh + n - 2));
-        const int32_t osi = int32_t(n) - 2 - 2 * int32_t(cnt);
-        if (osi <= 0) {
-          m.status = SLATE_E_BLOCK_INDEX_OFFSET;
-          m.detail = osi;
-        } else {
-          const uint32_t osu = uint32_t(osi);  // < 65536 on this path: uint16(offsetStartIndex) == osi
-          uint32_t bad = 0xFFFFFFFFu, bad_off = 0;
-          for (uint32_t i0 = 0; i0 < cnt && bad == 0xFFFFFFFFu; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const uint32_t off = i < cnt ? st_be16(stage, sh + osu + 2 * i) : 0u;
-            const uint64_t m64 = __ballot(i < cnt && off > osu);
-            if (m64) {
-              const uint32_t l0 = uint32_t(__builtin_ctzll(m64));
-              bad = i0 + l0;
-              bad_off = __builtin_amdgcn_readlane(off, l0);
-            }
-          }
-          if (bad != 0xFFFFFFFFu) {
-            m.status = SLATE_E_BLOCK_OFFSET_BOUNDS;
-            m.aux = uint16_t(bad);
-            m.detail = int32_t(bad_off);
-          } else {
-            m.data_len = osu;
-            m.n_rows = uint16_t(cnt);
-            if (cnt == 0) {
-              m.status = SLATE_E_BLOCK_NO_OFFSETS;
-            } else {
-              // FirstKey (block.go:130-131): uint16 arithmetic, Go panics out of range
-              const uint32_t off0 = __builtin_amdgcn_readfirstlane(st_be16(stage, sh + osu));
-              if (osu - off0 < 2) {
-                m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
-              } else {
-                const uint16_t kl = uint16_t(__builtin_amdgcn_readfirstlane(st_be16(stage, sh + off0)));
-                const uint16_t lo = uint16_t(off0 + 2), hi = uint16_t(off0 + 2 + kl);
-                if (lo > hi || hi > n) {
-                  m.status = SLATE_E_BLOCK_FIRSTKEY_PANIC;
-                } else {
-                  m.aux = kl;
-                  const uint64_t rb = a.row_base[b];
-                  const uint32_t rcap = uint32_t(min(uint64_t(0xFFFFFFFFu), a.row_base[b + 1] - rb));
-                  uint32_t nr = cnt;
-                  if (nr > rcap) {
-                    nr = rcap;
-                    m.flags |= SLATE_BLKF_ROWS_TRUNCATED;
-                  }
-                  // the first key's length: row 0 decoded against an empty first key
-                  uint32_t sl0;
-                  (void)row_stage(stage, sh, osu, off0, -1, &sl0);
-                  const int fk = sl0 == 0xFFFFFFFFu ? -1 : int(__builtin_amdgcn_readfirstlane(sl0));
-                  const __amdgpu_buffer_rsrc_t RR = make_rsrc(a.rows + rb, 16 * uint64_t(nr));
-                  for (uint32_t i0 = 0; i0 < nr; i0 += 64) {
-                    const uint32_t i = i0 + lane;
-                    const uint32_t off = st_be16(stage, sh + osu + 2 * min(i, cnt - 1));
-                    uint32_t sl;
-                    const v4u row = row_stage(stage, sh, osu, off, i == 0 ? -1 : fk, &sl);
-                    __builtin_amdgcn_raw_buffer_store_b128(row, RR, i < nr ? 16 * i : kOOB, 0, 0);
-                  }
-                }
-              }
-            }
-          }
-        }
-        if (lane == 0) a.meta[b] = m;
-      }
-    }
-    b = bn;
-    g = gn;
+  // two register sets: blocks b, b + W, b + 2W, ... alternate between them, so while one block
+  // is decoded the next one's loads are in flight and the one after it is being issued
+  uint32_t bA = blockIdx.x * (kNoneThreads / 64) + wave, bB = bA + waves_total;
+  Geo gA = geo_of(a, bA), gB = geo_of(a, bB);
+  Loads LA, LB;
+  issue_loads(gA, lane, LA);
+  issue_loads(gB, lane, LB);
+  while (gA.kind != 3) {
+    none_block(a, tab, stage, lane, 2 * waves_total, bA, gA, LA);
+    if (gB.kind == 3) break;
+    none_block(a, tab, stage, lane, 2 * waves_total, bB, gB, LB);
   }
 }
 

@@ -24,7 +24,8 @@ def per_dispatch(path, counter, kernel):
 
 def main():
     out = sys.argv[1]
-    kernel = "decode_lpb2_kernel"
+    codec = sys.argv[2] if len(sys.argv) > 2 else "snappy"
+    kernel = {"snappy": "decode_lpb2_kernel", "none": "decode_none_kernel"}[codec]
     f = per_dispatch(os.path.join(out, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", kernel)
     w = per_dispatch(os.path.join(out, "write", "run_counter_collection.csv"), "WRITE_SIZE", kernel)
     fetch_kib = max(f.values())  # the launches are identical; the max skips any partial one
@@ -64,7 +65,7 @@ def main():
         if sq.get("SQ_WAVE_CYCLES"):
             res["sq_fractions"] = {k + "/SQ_WAVE_CYCLES": round(sq[k] / sq["SQ_WAVE_CYCLES"], 4)
                                    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY") if k in sq}
-    dst = os.path.join(REPO, "profiles", "pmc_decode_latest.json")
+    dst = os.path.join(REPO, "profiles", "pmc_decode_latest.json" if codec == "snappy" else f"pmc_decode_{codec}_latest.json")
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res))
 
