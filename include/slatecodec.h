@@ -223,6 +223,12 @@ int slate_ctx_synchronize(slate_ctx* ctx);
  * slate_read_blocks, devbuf upload/download; default 16 or SLATE_COPY_THREADS, 1..256).  Each
  * context has its own: slate_block_decode_sharded over G contexts uses G x threads. */
 int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads);
+/* Measurement aid (no Go counterpart): with timing on, the SST builder's GPU passes (segmentation,
+ * pack, Snappy, bloom, CRC kernels) are bracketed by HIP events and their device time summed;
+ * slate_ctx_gpu_time returns the sum in milliseconds (and zeroes it when reset != 0).  Kernel
+ * groups on the filter's side stream overlap the flush, so the sum can exceed the wall time. */
+int slate_ctx_set_timing(slate_ctx* ctx, int on);
+int slate_ctx_gpu_time(slate_ctx* ctx, double* ms, int reset);
 
 /* ---- library-owned memory (SURVEY 8b "Ownership": device-resident mode uses opaque handles
  * owned by the C side) ----------------------------------------------------------------------

@@ -119,6 +119,18 @@ int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads) {
   return SLATE_OK;
 }
 
+int slate_ctx_set_timing(slate_ctx* ctx, int on) {
+  if (!ctx) return SLATE_E_INVALID_ARG;
+  ctx->timing = on != 0;
+  return SLATE_OK;
+}
+
+int slate_ctx_gpu_time(slate_ctx* ctx, double* ms, int reset) {
+  if (!ctx || !ms) return SLATE_E_INVALID_ARG;
+  *ms = double(reset ? ctx->gpu_ns.exchange(0) : ctx->gpu_ns.load()) * 1e-6;
+  return SLATE_OK;
+}
+
 void slate_ctx_destroy(slate_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);

@@ -42,7 +42,10 @@ int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* 
   SLATE_HIP(ctx->e_j.ensure(crc_scratch_bytes(n) + 16));
   uint32_t* scratch = ctx->e_j.as<uint32_t>();
   uint32_t* out = scratch + (crc_scratch_bytes(n) / 4);
-  SLATE_HIP(launch_crc32(ctx->stream, d_data, n, scratch, out));
+  {
+    GpuSpan gs(ctx, ctx->stream);
+    SLATE_HIP(launch_crc32(ctx->stream, d_data, n, scratch, out));
+  }
   SLATE_HIP(hipMemcpyAsync(crc, out, 4, hipMemcpyDeviceToHost, ctx->stream));
   SLATE_HIP(hipStreamSynchronize(ctx->stream));
   return SLATE_OK;
@@ -99,7 +102,10 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
   SLATE_HIP(slotb.ensure(nch * kSnapChunkSlot + nch * 4 + 64));
   uint8_t* slots = slotb.as<uint8_t>();
   uint32_t* lens = reinterpret_cast<uint32_t*>(slots + nch * kSnapChunkSlot);
-  SLATE_HIP(launch_snappy_chunks(st, d_src, n, slots, lens, ctx->num_cus));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_snappy_chunks(st, d_src, n, slots, lens, ctx->num_cus));
+  }
   std::vector<uint32_t> hl(nch);
   if (nch) SLATE_HIP(hipMemcpyAsync(hl.data(), lens, nch * 4, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
@@ -122,7 +128,10 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
   SLATE_HIP(crcb.ensure(crc_scratch_bytes(total) + 16));
   uint32_t* scratch = crcb.as<uint32_t>();
   uint32_t* cout = scratch + (crc_scratch_bytes(total) / 4);
-  SLATE_HIP(launch_crc32(st, d, total, scratch, cout));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_crc32(st, d, total, scratch, cout));
+  }
   uint32_t crc = 0;
   SLATE_HIP(hipMemcpyAsync(&crc, cout, 4, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
@@ -1133,15 +1142,19 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     fprintf(stderr, "[slate build]   %s %.2f ms\n", what, t - tp);
     tp = t;
   };
+  GpuSpan g_seg(ctx, st);
   SLATE_HIP(launch_encode(st, a, w, ctx->num_cus));
   SLATE_HIP(hipMemsetAsync(w.counts + chunks, 0, 8, st));
   SLATE_HIP(launch_scan_u64(st, w.counts, uint32_t(chunks + 1), scan_scratch));
+  g_seg.stop();
   uint64_t nb_total = 0;
   SLATE_HIP(hipMemcpyAsync(&nb_total, w.counts + chunks, 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));
   // every key's hash is in d_hashes now (the final flush consumes all pending keys)
   if (final && after_hashes) (*after_hashes)(b->n_hashes + n64);
+  GpuSpan g_blocks(ctx, st);
   SLATE_HIP(launch_encode_blocks(st, a, w));
+  g_blocks.stop();
   // the last block is still open unless this is the final flush (Build)
   const uint64_t nb = final ? nb_total : nb_total - 1;
   std::vector<uint32_t> starts(nb_total);
@@ -1149,7 +1162,9 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
   // the finished blocks' first keys (the index's BlockMeta keys), gathered on the device
   uint64_t* fko = reinterpret_cast<uint64_t*>(base + o_fko);
   SLATE_HIP(ctx->e_h.ensure(b->kbytes + 16));
+  GpuSpan g_pick(ctx, st);
   SLATE_HIP(launch_kv_pick_keys(st, w.block_start, nb, d_keys, d_key_off, fko, base + o_pick, ctx->e_h.as<uint8_t>()));
+  g_pick.stop();
   std::vector<uint64_t> fk_off(nb + 1);
   SLATE_HIP(hipMemcpyAsync(fk_off.data(), fko, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipMemsetAsync(w.block_size + nb, 0, 8, st));
@@ -1175,22 +1190,29 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     SLATE_HIP(ctx->s_aux.ensure((nb + 1) * 8 + 64));
     uint8_t* slots = ctx->s_slots.as<uint8_t>() + 16;
     uint64_t* csize = ctx->s_aux.as<uint64_t>();
+    GpuSpan g_pack(ctx, st);
     SLATE_HIP(hipMemsetAsync(csize + nb, 0, 8, st));
     SLATE_HIP(launch_pack_snappy(st, a, w, uint32_t(nb), w.block_size, slots, csize, ctx->num_cus));
+    g_pack.stop();
     uint32_t big = 0;
     SLATE_HIP(hipMemcpyAsync(&big, w.big_count, 4, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
+    GpuSpan g_big(ctx, st);
     if (big) {
       SLATE_HIP(ctx->s_raw.ensure(raw_total + 64));
       SLATE_HIP(launch_pack_snappy_big(st, a, w, w.block_size, ctx->s_raw.as<uint8_t>(), slots, csize, big,
                                        ctx->num_cus));
     }
     SLATE_HIP(launch_scan_u64(st, csize, uint32_t(nb + 1), scan_scratch));
+    g_big.stop();
     std::vector<uint64_t> fin(nb + 1);
     SLATE_HIP(hipMemcpyAsync(fin.data(), csize, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
     SLATE_HIP(ctx->e_e.ensure(fin[nb] + 16));
-    SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
+    {
+      GpuSpan gs(ctx, st);
+      SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
+    }
     mark("pack snappy");
     seg = std::make_shared<HostBytes>(fin[nb], ctx->seg_pool);
     if (!seg->ok()) return SLATE_E_OOM;
@@ -1201,7 +1223,10 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
   } else if (nb) {
     const uint64_t total = out_off[nb];
     SLATE_HIP(ctx->e_e.ensure(total + 16));
-    SLATE_HIP(launch_pack(st, a, w, uint32_t(nb), w.block_size, ctx->e_e.as<uint8_t>(), ctx->num_cus));
+    {
+      GpuSpan gs(ctx, st);
+      SLATE_HIP(launch_pack(st, a, w, uint32_t(nb), w.block_size, ctx->e_e.as<uint8_t>(), ctx->num_cus));
+    }
     uint32_t status = 0;
     SLATE_HIP(hipMemcpyAsync(&status, w.status, 4, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
@@ -1499,7 +1524,10 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
   const uint8_t hdr[2] = {uint8_t(f.np >> 8), uint8_t(f.np)};
   if (nb) {
     s = hip(hipMemsetAsync(words, 0, (nb + 3) & ~uint64_t(3), st));
-    if (!s) s = hip(launch_bloom_build(st, b->d_hashes.as<uint64_t>(), n_hashes, f.np, uint32_t(nb * 8), words));
+    if (!s) {
+      GpuSpan gs(ctx, st);
+      s = hip(launch_bloom_build(st, b->d_hashes.as<uint64_t>(), n_hashes, f.np, uint32_t(nb * 8), words));
+    }
   }
   if (!s) s = hip(hipMemcpyAsync(enc, hdr, 2, hipMemcpyHostToDevice, st));
   if (!s && nb) s = hip(hipMemcpyAsync(enc + 2, words, nb, hipMemcpyDeviceToDevice, st));
@@ -1518,7 +1546,10 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
   uint32_t* scratch = ctx->x_crc.as<uint32_t>();
   uint32_t* cout = scratch + crc_scratch_bytes(nb + 2) / 4;
   uint32_t crc = 0;
-  s = hip(launch_crc32(st, enc, nb + 2, scratch, cout));
+  {
+    GpuSpan gs(ctx, st);
+    s = hip(launch_crc32(st, enc, nb + 2, scratch, cout));
+  }
   if (!s) s = hip(hipMemcpyAsync(&crc, cout, 4, hipMemcpyDeviceToHost, st));
   if (!s) s = hip(hipStreamSynchronize(st));
   if (s) return fail(s);
@@ -1593,7 +1624,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
     uint32_t* words = ctx->e_f.as<uint32_t>();
     if (nb) {
       SLATE_HIP(hipMemsetAsync(words, 0, (nb + 3) & ~uint64_t(3), ctx->stream));
-      SLATE_HIP(launch_bloom_build(ctx->stream, b->d_hashes.as<uint64_t>(), b->n_hashes, np, uint32_t(nb * 8), words));
+      {
+        GpuSpan gs(ctx, ctx->stream);
+        SLATE_HIP(launch_bloom_build(ctx->stream, b->d_hashes.as<uint64_t>(), b->n_hashes, np, uint32_t(nb * 8), words));
+      }
     }
     // encoded filter = compress(BE16 numProbes || bits) || BE32 CRC (bloom.go:52-67)
     uint8_t hdr[2] = {uint8_t(np >> 8), uint8_t(np)};

@@ -2,6 +2,7 @@
 // buffers.  Each slate_ctx is used by one caller thread at a time; the library
 // keeps no global mutable state (SURVEY 8b "Threading").
 #pragma once
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -223,6 +224,10 @@ struct slate_ctx {
   hipStream_t aux = nullptr;
   DevBuf x_words, x_enc, x_slots, x_asm, x_crc;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
+  // device time of the builder's GPU passes (slate_ctx_set_timing): nanoseconds, summed over the
+  // kernel groups of every stream the context uses (GpuSpan)
+  bool timing = false;
+  std::atomic<uint64_t> gpu_ns{0};
   // host copy threads of this context (slate_ctx_set_copy_threads; SLATE_COPY_THREADS or 16)
   size_t copy_threads = 16;
   std::unique_ptr<CopyPool> copy_pool;
@@ -241,6 +246,45 @@ struct slate_ctx {
     for (PipeLane& l : lanes) l.release();
     h_small.release();
   }
+};
+
+// A group of kernel launches on one stream, timed by two HIP events when the context's timing is
+// on (slate_ctx_set_timing; a no-op otherwise): begin at construction, stop() after the group's
+// last launch (before any copy the caller queues next), read at destruction -- callers synchronise
+// the stream before they return anyway.
+struct GpuSpan {
+  slate_ctx* ctx;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  bool stopped = false;
+  GpuSpan(slate_ctx* c, hipStream_t s) : ctx(c), st(s) {
+    if (!c->timing) return;
+    if (hipEventCreate(&a) != hipSuccess) {
+      a = nullptr;
+      return;
+    }
+    if (hipEventCreate(&b) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      a = b = nullptr;
+      return;
+    }
+    (void)hipEventRecord(a, st);
+  }
+  void stop() {
+    if (a && !stopped) (void)hipEventRecord(b, st);
+    stopped = true;
+  }
+  ~GpuSpan() {
+    if (!a) return;
+    stop();
+    float ms = 0.f;
+    if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess && ms > 0.f)
+      ctx->gpu_ns.fetch_add(uint64_t(double(ms) * 1e6));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+  }
+  GpuSpan(const GpuSpan&) = delete;
+  GpuSpan& operator=(const GpuSpan&) = delete;
 };
 
 #define SLATE_HIP(expr)                                                                               \

@@ -71,6 +71,8 @@ _SIGS = {
     "slate_ctx_destroy": (None, [vp]),
     "slate_ctx_set_stream": (C.c_int, [vp, vp]),
     "slate_ctx_set_copy_threads": (C.c_int, [vp, C.c_uint32]),
+    "slate_ctx_set_timing": (C.c_int, [vp, C.c_int]),
+    "slate_ctx_gpu_time": (C.c_int, [vp, C.POINTER(C.c_double), C.c_int]),
     "slate_ctx_synchronize": (C.c_int, [vp]),
     "slate_decode_scratch_bytes": (C.c_size_t, [C.c_uint32]),
     "slate_block_decode_plan_device": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, vp, vp]),
@@ -210,6 +212,15 @@ class Context:
         """Host copy threads of this context (slate_ctx_set_copy_threads)."""
         _check(lib().slate_ctx_set_copy_threads(self._h, int(threads)), "slate_ctx_set_copy_threads")
 
+
+    def set_timing(self, on: bool) -> None:
+        """Sum the SST builder's GPU pass times on this context (slate_ctx_set_timing)."""
+        _check(lib().slate_ctx_set_timing(self._h, 1 if on else 0), "slate_ctx_set_timing")
+
+    def gpu_time_ms(self, reset: bool = False) -> float:
+        v = C.c_double()
+        _check(lib().slate_ctx_gpu_time(self._h, C.byref(v), 1 if reset else 0), "slate_ctx_gpu_time")
+        return v.value
     def synchronize(self):
         _check(lib().slate_ctx_synchronize(self._h), "slate_ctx_synchronize")
 

@@ -263,3 +263,22 @@ def test_snappy_block_encode_and_bloom(sc, ctx, ref_vectors):
     bad = bytearray(ctx.bloom_encode(6, b"abc" * 100, sc.SNAPPY)[1])
     bad[3] ^= 0x40
     assert ctx.bloom_decode(bytes(bad), sc.SNAPPY)[0] == 31
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+def test_builder_gpu_time(sc, codec):
+    """slate_ctx_set_timing / slate_ctx_gpu_time (the bench's configs[2] kernel time): nothing is
+    summed while timing is off, a build sums its GPU passes when it is on, and the bytes do not
+    change either way."""
+    c = sc.Context(0)
+    kvs = bg.kv_synthetic(38 * 300, half=True)
+    t0, o, _ = _build_both(sc, c, kvs, codec=codec)
+    assert c.gpu_time_ms() == 0.0
+    c.set_timing(True)
+    t1, _, _ = _build_both(sc, c, kvs, codec=codec)
+    ms = c.gpu_time_ms(reset=True)
+    assert 0.0 < ms < 10_000.0
+    assert c.gpu_time_ms() == 0.0
+    c.set_timing(False)
+    assert t0.encode() == t1.encode() == o.encode_table()
+    c.close()
