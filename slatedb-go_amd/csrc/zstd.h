@@ -257,7 +257,8 @@ __device__ int zs_weights_fse(const uint8_t* base, int32_t off, uint32_t hb, ZsS
 }
 
 // Huffman_Tree_Description at base[off, off+n): bytes used or -1; fills sc->huf, *tl
-__device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScratch* sc, int lane, uint32_t* tl_out) {
+__device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScratch* sc, int lane, uint32_t* tl_out,
+                           uint32_t dbg = 0) {  // dbg: profiling ablations (1<<25 no table fill, 1<<23 no weight decode)
   if (n < 1) return -1;
   const uint32_t hb = zrfl(uint32_t(base[off]));
   int nw, used;
@@ -273,7 +274,11 @@ __device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScrat
   } else {
     if (1 + hb > n) return -1;
     int k = 0;
-    if (zs_weights_fse(base, off + 1, hb, sc, lane, &k) < 0) return -1;
+    if (dbg & (1u << 23)) {
+      k = 255;  // profiling: weights left as they are
+    } else if (zs_weights_fse(base, off + 1, hb, sc, lane, &k) < 0) {
+      return -1;
+    }
     nw = k;
     used = int(1 + hb);
   }
@@ -323,7 +328,7 @@ __device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScrat
       pos = (my == k) ? before + (rank << (k - 1)) : pos;
       cur += (uint32_t(lane) == k) ? (uint32_t(__builtin_popcountll(m)) << (k - 1)) : 0u;
     }
-    if (my) {
+    if (my && !(dbg & (1u << 25))) {
       const uint16_t e = uint16_t(((tl + 1 - my) << 8) | uint32_t(s));
       for (uint32_t i = 0; i < (1u << (my - 1)); i++) sc->huf[pos + i] = e;
     }

@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
     const uint32_t nlit = cur.nlit, lbase = cur.cap - nlit;
     uint32_t tl = 0;
     // 1<<30: profiling, no tree (a flat 8-bit table is assumed)
-    const int t = (dbg_bits(a) & (1u << 30)) ? (tl = 8, 1) : zs_huf_read(win, int32_t(shift + cur.lit), cur.cs, sc, int(lane), &tl);
+    const int t = (dbg_bits(a) & (1u << 30)) ? (tl = 8, 1) : zs_huf_read(win, int32_t(shift + cur.lit), cur.cs, sc, int(lane), &tl, dbg_bits(a));
     bool fail = t < 0;
     if (!fail) {
       const uint32_t q = shift + cur.lit + uint32_t(t), qn = cur.cs - uint32_t(t);
