@@ -7,7 +7,18 @@ namespace slate {
 constexpr int kPackThreads = 256;        // 4 wavefronts, one block each
 constexpr uint32_t kPackCap = 8192;      // LDS bytes per wavefront for one encoded block
 constexpr uint32_t kPackBigCap = 155648; // one wavefront per workgroup
-constexpr int kSnapThreads = 192;        // Snappy pack: 3 wavefronts, ~16 KiB LDS each (3 workgroups per CU)
+#ifndef SLATE_SNAP_THREADS
+#define SLATE_SNAP_THREADS 768
+#endif
+#ifndef SLATE_SNAP_OWNER
+#define SLATE_SNAP_OWNER 512
+#endif
+// Snappy pack: one 12-wave workgroup per CU.  Per wave the raw block, its 4096-slot table and a
+// 512-byte owner array for the duplicate-slot check (4 KiB before: nine waves per CU; 512 B
+// aliases slots, which only makes the exact check run more often): 72 vs 79 ms of GPU time per
+// 10 M-KV build, bit-exact (profiles/round3/enc_ab/occupancy.txt)
+constexpr int kSnapThreads = SLATE_SNAP_THREADS;
+constexpr uint32_t kSnapOwner = SLATE_SNAP_OWNER;
 constexpr uint32_t kSnapRaw = 4096;      // raw block bytes handled in LDS (BlockSize 4096)
 constexpr uint64_t kSnapChunkSlot = 76544;  // >= MaxEncodedLen(64 KiB), 16-aligned
 constexpr uint64_t kSnapMaxChunk = 65536;   // golang/snappy maxBlockSize

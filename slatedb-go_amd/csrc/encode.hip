@@ -355,7 +355,7 @@ __device__ inline uint64_t snap_slot_off(uint64_t raw_off, uint64_t b) { return 
 // per wave: the raw block (+16 readable bytes), the 4096-slot table and its owner bytes; the encoded
 // block goes straight to its HBM slot (an LDS copy of it cost a quarter of the wave's LDS: with it,
 // six waves per CU; without, nine)
-constexpr uint32_t kSnapWaveBytes = kSnapRaw + 16 + 2 * kSnapRaw + kSnapRaw;
+constexpr uint32_t kSnapWaveBytes = kSnapRaw + 16 + 2 * kSnapRaw + kSnapOwner;
 
 __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
     EncodeArgs a, const uint32_t* __restrict__ adj, const uint32_t* __restrict__ flags,
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
     const uint32_t s = block_start[b];
     assemble_block(a, adj, sorted, s, next[s], raw, uint32_t(raw_len), lane);
     uint8_t* dst = slots + snap_slot_off(raw_off[b], b);
-    const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), dst, table, owner, lane);
+    const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), dst, table, owner, lane, kSnapOwner - 1);
     __builtin_amdgcn_s_waitcnt(0);
     __threadfence();  // the encoded bytes (stored by every lane) are read back by every lane
     const uint32_t crc = wave_crc32(tab, dst, 0, clen, lane);

@@ -166,8 +166,10 @@ __device__ inline void snap_slot_neighbours(uint32_t h, bool valid, int lane, in
 
 // encodeBlock (encode_other.go:165-238) for kSnapMinNonLiteral <= n <= 65536.
 // table: kSnapMaxTable u16 slots (LDS); owner: kSnapMaxTable bytes (LDS).
+// owner_mask: the owner array has owner_mask + 1 bytes (a power of two); slots that share an owner
+// byte only make the duplicate check fire for nothing (the sort then finds the true neighbours)
 __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table,
-                                             uint8_t* owner, int lane) {
+                                             uint8_t* owner, int lane, uint32_t owner_mask = kSnapMaxTable - 1) {
   uint32_t shift;
   const uint32_t ts = snappy_table_size(n, &shift);
   for (uint32_t i = lane; i < ts; i += kWave) table[i] = 0;
@@ -189,10 +191,10 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
       if (valid) {
         cur = snap_ld32(src + st);
         h = snap_hash(cur, shift);
-        owner[h] = uint8_t(lane);
+        owner[h & owner_mask] = uint8_t(lane);
       }
       snap_sync();
-      const bool dup = valid && owner[h] != uint8_t(lane);
+      const bool dup = valid && owner[h & owner_mask] != uint8_t(lane);
       const uint64_t dupmask = __ballot(dup);
       const uint64_t validmask = __ballot(valid);
       int32_t c = valid ? int32_t(table[h]) : 0;
@@ -262,7 +264,7 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
 
 // snappy.Encode (encode.go:17-42): uvarint length, then 64 KiB blocks.
 __device__ __forceinline__ uint32_t snappy_encode_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table, uint8_t* owner,
-                                       int lane) {
+                                       int lane, uint32_t owner_mask = kSnapMaxTable - 1) {
   uint32_t d = 0;
   {
     uint64_t v = n;
@@ -277,7 +279,7 @@ __device__ __forceinline__ uint32_t snappy_encode_wave(const uint8_t* src, uint3
   for (uint32_t p = 0; p < n;) {
     const uint32_t pn = min(n - p, kSnapMaxBlock);
     if (pn < kSnapMinNonLiteral) d = snap_emit_literal(dst, d, src + p, pn, lane);
-    else d += snappy_encode_block_wave(src + p, pn, dst + d, table, owner, lane);
+    else d += snappy_encode_block_wave(src + p, pn, dst + d, table, owner, lane, owner_mask);
     p += pn;
   }
   snap_sync();
