@@ -26,6 +26,12 @@ constexpr uint32_t kSnapMinNonLiteral = 17;  // 1 + 1 + inputMargin
 constexpr uint32_t kSnapInputMargin = 15;
 constexpr uint32_t kSnapMaxTable = 1u << 14;
 constexpr uint32_t kProbeSlots = 320;        // cum[] reaches past 65536 at t = 266
+#ifndef SLATE_SNAP_CUMREG  // the probe schedule in registers (1) or read per batch from constant memory (0)
+#define SLATE_SNAP_CUMREG 1
+#endif
+#ifndef SLATE_SNAP_ALWAYS_SORT  // A/B: sort every probe batch instead of the owner-array duplicate check
+#define SLATE_SNAP_ALWAYS_SORT 0
+#endif
 
 struct SnapProbe {
   uint32_t cum[kProbeSlots + 1];
@@ -56,10 +62,13 @@ __device__ inline uint32_t snappy_table_size(uint32_t n, uint32_t* shift) {
 
 // 4 unaligned bytes as two aligned dword reads (gfx950 serialises a misaligned LDS access lane by
 // lane); the buffers keep at least 4 readable bytes past their end
+// The aligned address is formed from p by pointer arithmetic, not an integer round trip, so the
+// compiler still knows an LDS pointer is one: a generic (flat) load also counts in vmcnt, and its
+// wait then drains every outstanding global store of the encoded output first.
 __device__ inline uint32_t snap_ld32(const uint8_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], uint32_t(a) & 3u);
+  const uint32_t m = uint32_t(reinterpret_cast<uintptr_t>(p)) & 3u;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p - m);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], m);
 }
 __device__ inline uint32_t snap_hash(uint32_t u, uint32_t shift) { return (u * 0x1e35a7bdu) >> shift; }
 
@@ -142,20 +151,56 @@ __device__ inline void snap_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// v from lane (lane ^ J), in VALU cross-lane operations (DPP, gfx950 permlane swaps) rather than
+// LDS-crossbar shuffles: the sort below is one serial chain of 21 of these per probe batch.
+template <uint32_t J>
+__device__ __forceinline__ uint32_t snap_xor(uint32_t v, int lane) {
+  if constexpr (J == 1) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const int m = __builtin_amdgcn_update_dpp(0, int(v), 0x141, 0xf, 0xf, false);  // row_half_mirror: lane ^ 7
+    return uint32_t(__builtin_amdgcn_update_dpp(0, m, 0x1B, 0xf, 0xf, false));      // quad_perm [3,2,1,0]: ^ 3
+  } else if constexpr (J == 8) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x128, 0xf, 0xf, false));  // row_ror:8
+  } else if constexpr (J == 16) {
+    // odd rows of the first operand swap with even rows of the second: {r0 r0 r2 r2}, {r1 r1 r3 r3}
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else {
+    // upper half of the first operand swaps with the lower half of the second: {lo lo}, {hi hi}
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? r[0] : r[1];
+  }
+}
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ uint32_t snap_bitonic_step(uint32_t v, int lane) {
+  const uint32_t o = snap_xor<J>(v, lane);
+  const bool up = (uint32_t(lane) & K) == 0 || K == 64;
+  const bool lower = (uint32_t(lane) & J) == 0;
+  return (lower == up) ? min(v, o) : max(v, o);
+}
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ uint32_t snap_bitonic_merge(uint32_t v, int lane) {
+  v = snap_bitonic_step<K, J>(v, lane);
+  if constexpr (J > 1) v = snap_bitonic_merge<K, J / 2>(v, lane);
+  return v;
+}
+
 // For each valid lane: the latest earlier (*prev) and the earliest later (*next) valid lane of the
 // wave with the same hash slot h (< 2^14), or 64.  Bitonic sort of (h, lane) keys across the wave;
 // invalid lanes get unique keys above every slot.  Results go back to their lanes by ds_permute.
 __device__ inline void snap_slot_neighbours(uint32_t h, bool valid, int lane, int32_t* prev, int32_t* next) {
   uint32_t v = ((valid ? h : (1u << 14) + uint32_t(lane)) << 6) | uint32_t(lane);
-  for (uint32_t k = 2; k <= 64; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint32_t o = uint32_t(__shfl_xor(int(v), int(j), 64));
-      const bool up = (uint32_t(lane) & k) == 0 || k == 64;
-      const bool lower = (uint32_t(lane) & j) == 0;
-      v = (lower == up) ? min(v, o) : max(v, o);
-    }
-  }
-  const uint32_t pv = uint32_t(__shfl_up(int(v), 1, 64)), nv = uint32_t(__shfl_down(int(v), 1, 64));
+  v = snap_bitonic_merge<2, 1>(v, lane);
+  v = snap_bitonic_merge<4, 2>(v, lane);
+  v = snap_bitonic_merge<8, 4>(v, lane);
+  v = snap_bitonic_merge<16, 8>(v, lane);
+  v = snap_bitonic_merge<32, 16>(v, lane);
+  v = snap_bitonic_merge<64, 32>(v, lane);
+  const uint32_t pv = uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x138, 0xf, 0xf, false));  // wave_shr:1
+  const uint32_t nv = uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x130, 0xf, 0xf, false));  // wave_shl:1
   const bool vv = (v >> 6) < (1u << 14);
   const uint32_t p_lane = (lane > 0 && vv && (pv >> 6) == (v >> 6)) ? (pv & 63) : 64u;
   const uint32_t n_lane = (lane < 63 && vv && (nv >> 6) == (v >> 6)) ? (nv & 63) : 64u;
@@ -177,6 +222,15 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
   const int32_t s_limit = int32_t(n) - int32_t(kSnapInputMargin);
   uint32_t d = 0, next_emit = 0;
   int32_t s = 1;
+#if SLATE_SNAP_CUMREG
+  // the probe schedule held in registers: cum[64 k + lane] and cum[64 k + lane + 1], k = 0..4
+  uint32_t cu[5], cn[5];
+#pragma unroll
+  for (uint32_t k = 0; k < 5; k++) {
+    cu[k] = g_snap_probe.cum[64 * k + uint32_t(lane)];
+    cn[k] = g_snap_probe.cum[64 * k + uint32_t(lane) + 1];
+  }
+#endif
   for (;;) {
     // ---------------- probe loop, 64 probes per batch
     int32_t cand = 0;
@@ -184,17 +238,25 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
     for (uint32_t t0 = 0;; t0 += kWave) {
       const uint32_t t = t0 + lane;
       const bool in_sched = t + 1 <= kProbeSlots;
+#if SLATE_SNAP_CUMREG
+      const uint32_t kb = t0 >> 6;  // wave-uniform
+      const uint32_t ct = kb == 0 ? cu[0] : kb == 1 ? cu[1] : kb == 2 ? cu[2] : kb == 3 ? cu[3] : cu[4];
+      const uint32_t ctn = kb == 0 ? cn[0] : kb == 1 ? cn[1] : kb == 2 ? cn[2] : kb == 3 ? cn[3] : cn[4];
+      const int32_t st = in_sched ? s + int32_t(ct) : 0x7FFFFFFF;
+      const int32_t snext = in_sched ? s + int32_t(ctn) : 0x7FFFFFFF;
+#else
       const int32_t st = in_sched ? s + int32_t(g_snap_probe.cum[t]) : 0x7FFFFFFF;
       const int32_t snext = in_sched ? s + int32_t(g_snap_probe.cum[t + 1]) : 0x7FFFFFFF;
+#endif
       const bool valid = in_sched && snext <= s_limit;
       uint32_t cur = 0, h = 0;
       if (valid) {
         cur = snap_ld32(src + st);
         h = snap_hash(cur, shift);
-        owner[h & owner_mask] = uint8_t(lane);
+        if (!SLATE_SNAP_ALWAYS_SORT) owner[h & owner_mask] = uint8_t(lane);
       }
       snap_sync();
-      const bool dup = valid && owner[h & owner_mask] != uint8_t(lane);
+      const bool dup = valid && (SLATE_SNAP_ALWAYS_SORT || owner[h & owner_mask] != uint8_t(lane));
       const uint64_t dupmask = __ballot(dup);
       const uint64_t validmask = __ballot(valid);
       int32_t c = valid ? int32_t(table[h]) : 0;
@@ -204,9 +266,11 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
       // with a 64-wide bitonic network, so the neighbours in sorted order are exactly those
       // lanes (21 exchange steps, instead of two 63-step shuffle scans).
       int32_t prev = 64, next = 64;
-      if (dupmask) snap_slot_neighbours(h, valid, lane, &prev, &next);
-      const int32_t sp = __shfl(st, prev < 64 ? prev : lane, 64);  // every lane takes part
-      if (valid && prev < 64) c = sp;
+      if (dupmask) {  // (wave-uniform: every lane takes part in the cross-lane operations)
+        snap_slot_neighbours(h, valid, lane, &prev, &next);
+        const int32_t sp = __shfl(st, prev < 64 ? prev : lane, 64);
+        if (valid && prev < 64) c = sp;
+      }
       const bool match = valid && cur == snap_ld32(src + c);
       const uint64_t mm = __ballot(match);
       const uint32_t istar = mm ? uint32_t(__builtin_ctzll(mm)) : 64u;
@@ -215,8 +279,8 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
       if (ran && last) table[h] = uint16_t(st);
       snap_sync();
       if (mm) {
-        s = __shfl(st, int(istar), 64);
-        cand = __shfl(c, int(istar), 64);
+        s = __builtin_amdgcn_readlane(st, int(istar));  // istar is wave-uniform
+        cand = __builtin_amdgcn_readlane(c, int(istar));
         found = true;
         break;
       }
