@@ -1083,7 +1083,8 @@ static int pending_push_host(slate_sst_builder* b) {
   return st;
 }
 
-static int builder_flush(slate_sst_builder* b, bool final, const std::function<void(uint64_t)>* after_hashes = nullptr) {
+static int builder_flush(slate_sst_builder* b, bool final, const std::function<void(uint64_t)>* after_hashes = nullptr,
+                         const std::function<void()>* after_meta = nullptr) {
   slate_ctx* ctx = b->ctx;
   hipStream_t st = ctx->stream;
   int pst = pending_push_host(b);
@@ -1179,6 +1180,17 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     int s = ctx_d2h(ctx, b->meta_keys.data() + mk, ctx->e_h.p, fk_off[nb], st);
     if (s) return s;
   }
+  // the index entries of the finished blocks (builder.go:169-176) are known once their final sizes
+  // are: queued before the blocks' D2H, so the Build's index flatbuffer can start beside it
+  auto queue_meta = [&](const std::vector<uint64_t>& oo) {
+    uint64_t cl = b->current_len;
+    for (uint64_t k = 0; k < nb; k++) {
+      b->meta_off.push_back(cl);
+      b->meta_key_off.push_back(b->meta_key_off.back() + (fk_off[k + 1] - fk_off[k]));
+      if (!(final && k + 1 == nb)) cl += oo[k + 1] - oo[k];
+    }
+    if (final && after_meta) (*after_meta)();
+  };
   std::shared_ptr<HostBytes> seg;
   if (nb && b->cfg.codec == SLATE_CODEC_SNAPPY) {
     // raw sizes -> per-block slots; golang/snappy + CRC per block; scan of the
@@ -1214,12 +1226,13 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
       SLATE_HIP(launch_compact(st, slots, w.block_size, csize, uint32_t(nb), ctx->e_e.as<uint8_t>(), ctx->num_cus));
     }
     mark("pack snappy");
-    seg = std::make_shared<HostBytes>(fin[nb], ctx->seg_pool);
+    out_off.swap(fin);
+    seg = std::make_shared<HostBytes>(out_off[nb], ctx->seg_pool);
     if (!seg->ok()) return SLATE_E_OOM;
-    int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, fin[nb], st);
+    queue_meta(out_off);
+    int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, out_off[nb], st);
     mark("blocks D2H");
     if (s) return s;
-    out_off.swap(fin);
   } else if (nb) {
     const uint64_t total = out_off[nb];
     SLATE_HIP(ctx->e_e.ensure(total + 16));
@@ -1248,14 +1261,14 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     }
     seg = std::make_shared<HostBytes>(out_off[nb], ctx->seg_pool);
     if (!seg->ok()) return SLATE_E_OOM;
+    queue_meta(out_off);
     int s = ctx_d2h(ctx, seg->p, src, out_off[nb], st);
     mark("blocks D2H");
     if (s) return s;
   }
-  // ---- queue the finished blocks (builder.go:169-176, finishBlock :192-213)
+  // ---- queue the finished blocks (builder.go:169-176, finishBlock :192-213; their index
+  // entries went in before the D2H)
   for (uint64_t k = 0; k < nb; k++) {
-    b->meta_off.push_back(b->current_len);
-    b->meta_key_off.push_back(b->meta_key_off.back() + (fk_off[k + 1] - fk_off[k]));
     ByteView v{seg, out_off[k], out_off[k + 1] - out_off[k]};
     if (final && k + 1 == nb) {
       b->last_block = v;  // Build: the last block opens the final chunk
@@ -1580,17 +1593,20 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   const std::function<void(uint64_t)> start_filter = [&](uint64_t nh) {
     fjob = std::async(std::launch::async, build_filter_aux, b, nh);
   };
-  int st = builder_flush(b, true, side_filter ? &start_filter : nullptr);
+  // the index flatbuffer (host work) is built beside the last blocks' D2H and the filter's encode:
+  // the final flush starts it once every index entry is queued (b->meta_* are not touched after)
+  std::future<std::vector<uint8_t>> fb_job;
+  const std::function<void()> start_index = [&] {
+    fb_job = std::async(std::launch::async, [b] { return fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off); });
+  };
+  int st = builder_flush(b, true, side_filter ? &start_filter : nullptr, &start_index);
   if (side_filter && !fjob.valid() && !st) start_filter(b->n_hashes);  // nothing was pending
-  if (st) return st;  // (a started filter job is joined by its future)
+  if (st) return st;  // (started filter / index jobs are joined by their futures)
+  if (!fb_job.valid()) start_index();  // no block was finished by the final flush
   const double t1 = host_trace() ? now_ms() : 0.0;
   b->built = true;
   slate_sst_table* t = new slate_sst_table();
   std::vector<uint8_t> buf(b->last_block.data(), b->last_block.data() + b->last_block.len);
-  // the index flatbuffer (host work) is built while the filter is encoded on the GPU
-  std::future<std::vector<uint8_t>> fb_job = std::async(std::launch::async, [b] {
-    return fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
-  });
   const uint64_t filter_off = b->current_len + buf.size();
   uint64_t filter_len = 0;
   // ---- bloom filter (builder.go:225-235, bloom.go:112-133 Build, :52-67 Encode)
@@ -1670,8 +1686,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   const double t2 = host_trace() ? now_ms() : 0.0;
   // ---- index (builder.go:238-244, flatbuf.go:126-139)
   std::vector<uint8_t> index;
+  double t_fb = 0.0;
   {
     std::vector<uint8_t> fb = fb_job.get();
+    t_fb = host_trace() ? now_ms() : 0.0;
     if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
       // encoded and CRC'd on the device: the payload comes back once, with its CRC
       SLATE_HIP(ctx_bind(ctx));
@@ -1725,8 +1743,8 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   t->chunks.push_back(ByteView{fin, 0, buf.size()});
   *table = t;
   if (host_trace())
-    fprintf(stderr, "[slate build] flush %.2f ms, filter %.2f ms, index + info %.2f ms\n", t1 - t0, t2 - t1,
-            now_ms() - t2);
+    fprintf(stderr, "[slate build] flush %.2f ms, filter %.2f ms, index + info %.2f ms (index flatbuffer wait %.2f ms)\n",
+            t1 - t0, t2 - t1, now_ms() - t2, t_fb - t2);
   return SLATE_OK;
 }
 
