@@ -99,9 +99,10 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
                                 const uint8_t* d_src, size_t n, std::vector<uint8_t>& out, bool lanes) {
   SLATE_HIP(ctx_bind(ctx));
   const uint64_t nch = (uint64_t(n) + kSnapMaxChunk - 1) / kSnapMaxChunk;
-  SLATE_HIP(slotb.ensure(nch * kSnapChunkSlot + nch * 4 + 64));
+  SLATE_HIP(slotb.ensure(nch * kSnapChunkSlot + nch * 12 + 64));
   uint8_t* slots = slotb.as<uint8_t>();
   uint32_t* lens = reinterpret_cast<uint32_t*>(slots + nch * kSnapChunkSlot);
+  uint64_t* d_off = reinterpret_cast<uint64_t*>(slots + nch * kSnapChunkSlot + ((nch * 4 + 7) & ~uint64_t(7)));
   {
     GpuSpan gs(ctx, st);
     SLATE_HIP(launch_snappy_chunks(st, d_src, n, slots, lens, ctx->num_cus));
@@ -120,11 +121,15 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
   SLATE_HIP(asmb.ensure(total + 64));
   uint8_t* d = asmb.as<uint8_t>();
   SLATE_HIP(hipMemcpyAsync(d, hdr, hn, hipMemcpyHostToDevice, st));
+  // the chunks back to back after the length header: one gather launch (offsets from the host)
+  std::vector<uint64_t> ho(nch);
   size_t o = hn;
   for (uint64_t c = 0; c < nch; c++) {
-    if (hl[c]) SLATE_HIP(hipMemcpyAsync(d + o, slots + c * kSnapChunkSlot, hl[c], hipMemcpyDeviceToDevice, st));
+    ho[c] = o;
     o += hl[c];
   }
+  if (nch) SLATE_HIP(hipMemcpyAsync(d_off, ho.data(), nch * 8, hipMemcpyHostToDevice, st));
+  SLATE_HIP(launch_snappy_gather(st, slots, lens, d_off, nch, d));
   SLATE_HIP(crcb.ensure(crc_scratch_bytes(total) + 16));
   uint32_t* scratch = crcb.as<uint32_t>();
   uint32_t* cout = scratch + (crc_scratch_bytes(total) / 4);

@@ -71,6 +71,9 @@ hipError_t launch_pack_snappy_big(hipStream_t st, const EncodeArgs& a, const Enc
                                   uint8_t* rawbuf, uint8_t* slots, uint64_t* csize, uint32_t big_count, int num_cus);
 hipError_t launch_compact(hipStream_t st, const uint8_t* slots, const uint64_t* raw_off, const uint64_t* final_off,
                           uint32_t nblocks, uint8_t* out, int num_cus);
+// chunk c's encoding (slots + c * kSnapChunkSlot, len[c] bytes) to dst + off[c], one launch
+hipError_t launch_snappy_gather(hipStream_t st, const uint8_t* slots, const uint32_t* len, const uint64_t* off,
+                                uint64_t nch, uint8_t* dst);
 hipError_t launch_snappy_chunks(hipStream_t st, const uint8_t* src, uint64_t n, uint8_t* dst, uint32_t* len,
                                 int num_cus);
 size_t crc_scratch_bytes(uint64_t n);

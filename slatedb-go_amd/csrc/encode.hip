@@ -666,6 +666,22 @@ hipError_t launch_snappy_chunks(hipStream_t st, const uint8_t* src, uint64_t n, 
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void snappy_gather_kernel(const uint8_t* __restrict__ slots,
+                                                            const uint32_t* __restrict__ len,
+                                                            const uint64_t* __restrict__ off, uint8_t* __restrict__ dst) {
+  const uint64_t c = blockIdx.x;
+  const uint32_t n = len[c];
+  const uint8_t* s = slots + c * kSnapChunkSlot;
+  uint8_t* o = dst + off[c];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) o[i] = s[i];
+}
+
+hipError_t launch_snappy_gather(hipStream_t st, const uint8_t* slots, const uint32_t* len, const uint64_t* off,
+                                uint64_t nch, uint8_t* dst) {
+  if (nch) snappy_gather_kernel<<<uint32_t(nch), 256, 0, st>>>(slots, len, off, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_bloom_build(hipStream_t st, const uint64_t* hashes, uint64_t n, uint32_t num_probes,
                               uint32_t filter_bits, uint32_t* words) {
   if (n == 0) return hipGetLastError();
