@@ -117,6 +117,8 @@ enum slate_status {
   SLATE_E_CAPACITY = 103,           /* caller-provided output buffer too small */
   SLATE_E_OOM = 104,
   SLATE_E_MERGE_UNSORTED = 105,     /* an iterator handed to the merge is not sorted (merge.go's precondition) */
+  SLATE_E_LIMIT = 106,              /* an internal limit of this library (e.g. >= 2^32 rows in one call) */
+  SLATE_E_WARNINGS = 107,           /* slate_compact_ex: done, with types.ErrWarn warnings (see there) */
 };
 
 /* ---- layouts ----------------------------------------------------------------- */
@@ -382,6 +384,10 @@ int slate_sst_table_encode(const slate_sst_table* t, uint8_t* out, size_t out_ca
 int slate_sst_table_bloom(const slate_sst_table* t, int* present, uint16_t* num_probes,
                           uint8_t* bits, size_t bits_cap, size_t* bits_len);
 
+/* crc32.ChecksumIEEE of n device bytes at any alignment (the checksum every block, filter, index
+ * and info payload carries: block.go:73, bloom.go:61, flatbuf.go:53-60), computed on the GPU. */
+int slate_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* crc);
+
 /* ---- SST reader (decode.go / flatbuf.go) ------------------------------------------
  * The caller performs the object-store reads (ReadOnlyBlob.ReadRange) and hands
  * the byte ranges in; nothing is retained. */
@@ -461,8 +467,9 @@ int slate_merge_sorted_device(slate_ctx* ctx, uint32_t k, const uint8_t* d_keys,
  * count d_row_base[n_blocks]), the rows in block order (*d_n_kv of them), each with its full key
  * (block.Iterator, block/iterator.go:84-107: row 0's key is its suffix and is the block's
  * firstKey; row i's key = firstKey[:prefixLen] || suffix, row.go:72-79), value bytes (empty for
- * tombstones) and tombstone flag.  *d_flags bit 1 = a block or row failed to decode (its rows
- * contribute no KV).  d_key_off/d_val_off hold n_rows+1 entries (entries past *d_n_kv repeat the
+ * tombstones) and tombstone flag.  *d_flags bit 1 = a block or row failed to decode: a failed block
+ * contributes no KV, a failed row neither it nor the rows after it in its block (block.Iterator
+ * stops there, block/iterator.go:92-96).  d_key_off/d_val_off hold n_rows+1 entries (entries past *d_n_kv repeat the
  * total).  d_scratch holds slate_kv_scratch_bytes(n_rows) and must be kept, unchanged, from the
  * lengths call to the copy call (it carries the row-slot map).
  * gather: the KV of every merge result index (slate_merge_sorted_device's d_out_idx), in order,
@@ -493,16 +500,54 @@ int slate_kv_gather_copy_device(slate_ctx* ctx, const uint32_t* d_idx, uint64_t 
  * merged entries written through one SST builder per output (EncodedSSTableWriter.Add,
  * table_store.go:221-266: AddValue, an empty value is a tombstone), a new output starting after
  * the entry that takes the running key + value size past max_sst_size (executor.go:119-139).
- * Inputs: n_sst encoded SSTs, sst i = ssts[sst_off[i] .. sst_off[i+1]); n_src sources in
- * precedence order (executor.go:55-90: L0 SSTs, then sorted runs), source j = SSTs
- * [src_sst[j], src_sst[j+1]) read in order (src_sst: n_src + 1 entries, 0 .. n_sst).
- * Outputs: *n_out tables in out_tables (the caller frees them with slate_sst_table_free); with
- * out_cap too small, SLATE_E_CAPACITY and *n_out = the number needed.  The first failing input
- * block's status is returned as executeCompaction returns its iterator's error; a row that fails
- * to decode returns SLATE_E_INVALID_ARG.  Every intermediate stays in library-owned HBM. */
+ * Inputs: n_sst encoded SSTs in HOST memory (the object-store GET buffers), sst i =
+ * ssts[sst_off[i] .. sst_off[i+1]); n_src sources in precedence order (executor.go:55-90: L0 SSTs,
+ * then sorted runs), source j = SSTs [src_sst[j], src_sst[j+1]) read in order (src_sst: n_src + 1
+ * entries, 0 .. n_sst).  The library uploads the data blocks itself; every intermediate stays in
+ * library-owned HBM.
+ * Outputs: *n_out tables in out_tables (the caller frees them with slate_sst_table_free).
+ * out_cap too small (including out_cap = 0 to ask): SLATE_E_CAPACITY with *n_out = the number
+ * needed (> out_cap); the merged entries are recomputed by the retry.
+ *
+ * Corrupt inputs end iterators the way Go's do, and the compaction goes on:
+ *  - a data block that fails block.Decode ends its SST's iterator: the SST contributes the rows of
+ *    the blocks before it (sstable.Iterator.Next, iterator.go:59-68 + nextBlockIter :92-118);
+ *  - a row that fails v0RowCodec.Decode ends its block's iterator: the block contributes the rows
+ *    before it, and the SST goes on with its next block (block/iterator.go:84-99);
+ * the outputs are built from what is left, and the warnings Go collects in types.ErrWarn are
+ * reported as records (below).  executeCompaction then returns warn.If() beside the sorted run
+ * (executor.go:150) and startCompaction turns that into a failed Result (:166-173).
+ * Internal limits (more than 2^32 - 1 rows or slots in one call, a block with more rows than its
+ * planned slots) return SLATE_E_LIMIT with *n_out = 0.  A row that is not sorted within its source
+ * returns SLATE_E_MERGE_UNSORTED. */
+typedef struct slate_compact_warning {
+  uint32_t src;       /* source index (0 .. n_src-1) */
+  uint32_t sst;       /* input SST index (0 .. n_sst-1) */
+  uint32_t block;     /* data block index within that SST */
+  int32_t row;        /* block.Offsets index of the failing row; -1: the block failed block.Decode */
+  int32_t status;     /* the block's SLATE_E_* (block.Decode) or the row's SLATE_E_ROW_* */
+  uint32_t block_len; /* encoded bytes of the block: "data[0:block_len]" in the message */
+} slate_compact_warning;
+/* One record per warning, in the order types.ErrWarn receives them (iter.MergeSort merges a
+ * source's warnings up to its first row when it is created, and the rest when the source ends;
+ * sources end in the order their last keys leave the merge heap).  The texts, with the SST id the
+ * caller knows (slate_status_string gives err):
+ *   row = -1: "while fetching blocks for SST '%s': while reading block range [%d:%d]: while decoding
+ *              block '%d' data[0:%d]: %s"   (sst id, block, block + 1, block, block_len, err)
+ *   row >= 0: "while decoding block.Offset[%d]: %s"   (row, err)
+ * ErrWarn.Merge drops a text equal to one already kept (types/errors.go:41-52); the records are
+ * not de-duplicated, so a shim drops repeats as it formats them. */
 int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst, const uint32_t* src_sst,
                   uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size, slate_sst_table** out_tables,
                   uint32_t out_cap, uint32_t* n_out);
+/* slate_compact with the warning records: up to warn_cap records in warns, *n_warn = the number Go
+ * collects (may exceed warn_cap).  Returns SLATE_E_WARNINGS, with the outputs built, when there is at
+ * least one warning.  slate_compact returns the first record's status instead and frees the outputs
+ * (*n_out = 0), as startCompaction drops the sorted run of a compaction that returned an error. */
+int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst,
+                     const uint32_t* src_sst, uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size,
+                     slate_sst_table** out_tables, uint32_t out_cap, uint32_t* n_out, slate_compact_warning* warns,
+                     uint32_t warn_cap, uint32_t* n_warn);
 
 #ifdef __cplusplus
 }

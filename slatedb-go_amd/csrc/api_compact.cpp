@@ -60,10 +60,20 @@ std::shared_ptr<Dev> dev(size_t bytes, hipError_t* e) {
   auto var = dev((bytes), &var##_e);          \
   if (var##_e != hipSuccess) return hip_status(var##_e)
 
+// A warning with the surviving rows its SST had produced before it (decides when MergeSort merges it).
+struct Warn {
+  slate_compact_warning w;
+  uint64_t rows_before;  // rows of the warning's SST returned before it
+};
+
 // One device batch over the data blocks of SSTs that share a codec -> a KV view and the rows of
-// each SST (in order).  blocks: the SSTs' data-block byte ranges, gathered on the host.
+// each SST (in order), with Go's iterator semantics on corrupt input: a block that fails
+// block.Decode ends its SST (sstable.Iterator.Next, iterator.go:59-68), a row that fails ends its
+// block (block/iterator.go:92-96); each adds a warning.  blocks: the SSTs' data-block byte ranges,
+// gathered on the host; sst0 / sst_src: the first SST's index and every SST's source.
 int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, const std::vector<uint64_t>& in_off,
-                 const std::vector<uint32_t>& sst_blocks, View* v, std::vector<uint64_t>* rows_per_sst) {
+                 const std::vector<uint32_t>& sst_blocks, uint32_t sst0, const std::vector<uint32_t>& sst_src, View* v,
+                 std::vector<uint64_t>* rows_per_sst, std::vector<Warn>* warns) {
   const uint32_t n = uint32_t(in_off.size() - 1);
   hipStream_t st = ctx->stream;
   DEV(d_in, blob.size() + 16);
@@ -80,20 +90,38 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   if ((s = d2h_small(ctx, &tot[0], d_out_off->as<uint64_t>() + n, 8))) return s;
   if ((s = d2h_small(ctx, &tot[1], d_row_base->as<uint64_t>() + n, 8))) return s;
   const uint64_t slots = tot[1];
-  if (slots >= 0xFFFFFFFFull) return SLATE_E_CAPACITY;
+  if (slots >= 0xFFFFFFFFull) return SLATE_E_LIMIT;
   DEV(d_out, tot[0] + 16);
   DEV(d_meta, size_t(n) * sizeof(slate_block_meta));
   DEV(d_rows, (slots + 1) * sizeof(slate_row));
   DecodeArgs a{codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(),
                d_meta->as<slate_block_meta>(), d_rows->as<slate_row>(), d_row_base->as<uint64_t>(), nullptr, nullptr, 0};
   SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus));
-  // every block's status: executeCompaction returns the iterator's first error (iterator.go:62-68)
+  // every block's status: the first failing block of an SST ends that SST's iterator with a
+  // warning (iterator.go:62-68 wrapping decode.go:143-144); it and the SST's later blocks keep no
+  // rows (their metas are patched to 0 rows for the rows phase)
   std::vector<slate_block_meta> meta(n);
   if ((s = ctx_d2h(ctx, meta.data(), d_meta->b.p, size_t(n) * sizeof(slate_block_meta), st))) return s;
-  for (uint32_t i = 0; i < n; i++) {
-    if (meta[i].status != SLATE_OK) return meta[i].status;
-    if (meta[i].flags & SLATE_BLKF_ROWS_TRUNCATED) return SLATE_E_CAPACITY;
+  std::vector<int32_t> block_warn(n, 0);  // per block: status of its block.Decode failure (0 = none)
+  bool patched = false;
+  for (size_t j = 0; j + 1 < sst_blocks.size(); j++) {
+    bool cut = false;
+    for (uint32_t i = sst_blocks[j]; i < sst_blocks[j + 1]; i++) {
+      if (!cut && meta[i].status == SLATE_OK && (meta[i].flags & SLATE_BLKF_ROWS_TRUNCATED)) return SLATE_E_LIMIT;
+      if (!cut && meta[i].status != SLATE_OK) {
+        cut = true;
+        block_warn[i] = meta[i].status;
+      }
+      if (cut) {
+        meta[i].status = SLATE_OK;
+        meta[i].flags = 0;
+        meta[i].n_rows = 0;
+        patched = true;
+      }
+    }
   }
+  if (patched) SLATE_HIP(hipMemcpyAsync(d_meta->b.p, meta.data(), size_t(n) * sizeof(slate_block_meta),
+                                        hipMemcpyHostToDevice, st));
   // rows -> KV view
   DEV(key_off, (slots + 1) * 8);
   DEV(val_off, (slots + 1) * 8);
@@ -109,7 +137,28 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   uint32_t flags = 0;
   uint64_t n_kv = 0;
   if ((s = d2h_small(ctx, &flags, d_flags->b.p, 4))) return s;
-  if (flags & 2) return SLATE_E_INVALID_ARG;  // a row failed to decode (block.Iterator stops there)
+  // rows each block returns: all of them, or those before its first failing row (the rows phase
+  // dropped the rest, block/iterator.go:92-96); the failing rows' statuses are read only here
+  std::vector<uint32_t> kept(n);
+  std::vector<int32_t> row_warn(n, -1), row_status(n, 0);
+  for (uint32_t i = 0; i < n; i++) kept[i] = meta[i].n_rows;
+  if (flags & 2) {
+    std::vector<int16_t> rst(slots + 1);
+    SLATE_HIP(hipMemcpy2DAsync(rst.data(), 2, reinterpret_cast<const uint8_t*>(d_rows->b.p) + offsetof(slate_row, status),
+                               sizeof(slate_row), 2, slots, hipMemcpyDeviceToHost, st));
+    std::vector<uint64_t> rb(size_t(n) + 1);
+    if ((s = ctx_d2h(ctx, rb.data(), d_row_base->b.p, (size_t(n) + 1) * 8, st))) return s;
+    for (uint32_t i = 0; i < n; i++) {
+      for (uint32_t r = 0; r < meta[i].n_rows && rb[i] + r < rb[i + 1]; r++) {
+        if (rst[rb[i] + r] != SLATE_OK) {
+          kept[i] = r;
+          row_warn[i] = int32_t(r);
+          row_status[i] = rst[rb[i] + r];
+          break;
+        }
+      }
+    }
+  }
   if ((s = d2h_small(ctx, &n_kv, d_nkv->b.p, 8))) return s;
   uint64_t kb = 0, vb = 0;
   if ((s = d2h_small(ctx, &kb, key_off->as<uint64_t>() + slots, 8))) return s;
@@ -120,12 +169,18 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
                              d_rows->as<slate_row>(), slots, d_nkv->as<uint64_t>(), d_kvs->b.p, key_off->as<uint64_t>(),
                              keys->as<uint8_t>(), val_off->as<uint64_t>(), vals->as<uint8_t>()));
   SLATE_HIP(hipStreamSynchronize(st));
-  // rows of each SST from its blocks' row counts
+  // rows of each SST from its blocks' row counts; the warnings in the order its iterator adds them
   uint64_t acc = 0;
   size_t k = 0;
   for (size_t j = 0; j + 1 < sst_blocks.size(); j++) {
     uint64_t r = 0;
-    for (; k < sst_blocks[j + 1]; k++) r += meta[k].n_rows;
+    const uint32_t sst = sst0 + uint32_t(j);
+    for (; k < sst_blocks[j + 1]; k++) {
+      const uint32_t blk = uint32_t(k - sst_blocks[j]), len = uint32_t(in_off[k + 1] - in_off[k]);
+      if (block_warn[k]) warns->push_back({{sst_src[sst], sst, blk, -1, block_warn[k], len}, r});
+      r += kept[k];
+      if (row_warn[k] >= 0) warns->push_back({{sst_src[sst], sst, blk, row_warn[k], row_status[k], len}, r});
+    }
     rows_per_sst->push_back(r);
     acc += r;
   }
@@ -189,11 +244,14 @@ int concat_views(slate_ctx* ctx, const std::vector<View>& vs, View* out) {
 
 extern "C" {
 
-int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst, const uint32_t* src_sst,
-                  uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size, slate_sst_table** out_tables,
-                  uint32_t out_cap, uint32_t* n_out) {
-  if (!ctx || !sst_off || !src_sst || !out_cfg || !n_out || n_src == 0 || (n_sst && !ssts)) return SLATE_E_INVALID_ARG;
+int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst,
+                     const uint32_t* src_sst, uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size,
+                     slate_sst_table** out_tables, uint32_t out_cap, uint32_t* n_out, slate_compact_warning* warns,
+                     uint32_t warn_cap, uint32_t* n_warn) {
+  if (!ctx || !sst_off || !src_sst || !out_cfg || !n_out || n_src == 0 || (n_sst && !ssts) || (warn_cap && !warns))
+    return SLATE_E_INVALID_ARG;
   *n_out = 0;
+  if (n_warn) *n_warn = 0;
   if (src_sst[0] != 0 || src_sst[n_src] != n_sst) return SLATE_E_INVALID_ARG;
   for (uint32_t j = 0; j < n_src; j++)
     if (src_sst[j + 1] < src_sst[j]) return SLATE_E_INVALID_ARG;
@@ -224,9 +282,13 @@ int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, 
       if (offs[i][b + 1] < offs[i][b] || offs[i][b + 1] > len) return SLATE_E_BLOB_RANGE;
     codec[i] = info.codec;
   }
+  std::vector<uint32_t> sst_src(n_sst);
+  for (uint32_t j = 0; j < n_src; j++)
+    for (uint32_t i = src_sst[j]; i < src_sst[j + 1]; i++) sst_src[i] = j;
   // ---- decode: one device batch per run of SSTs sharing a codec, views in source order
   std::vector<View> views;
   std::vector<uint64_t> rows_per_sst;
+  std::vector<Warn> wl;
   for (uint32_t i = 0; i < n_sst;) {
     uint32_t e = i;
     while (e < n_sst && codec[e] == codec[i]) e++;
@@ -245,7 +307,7 @@ int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, 
     }
     if (in_off.size() > 1) {
       View v;
-      int s = decode_group(ctx, codec[i], blob, in_off, sst_blocks, &v, &rows_per_sst);
+      int s = decode_group(ctx, codec[i], blob, in_off, sst_blocks, i, sst_src, &v, &rows_per_sst, &wl);
       if (s) return s;
       views.push_back(v);
     } else {
@@ -253,19 +315,55 @@ int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, 
     }
     i = e;
   }
-  if (views.empty()) return SLATE_OK;  // no entries: no output SST (executor.go opens a writer on the first entry)
-  View all;
-  int s = concat_views(ctx, views, &all);
-  if (s) return s;
-  views.clear();
   // ---- iter.MergeSort: source j = the rows of its SSTs, in precedence order
-  std::vector<uint64_t> src_start(size_t(n_src) + 1, 0);
+  std::vector<uint64_t> src_start(size_t(n_src) + 1, 0), sst_rows_before(n_sst, 0);
   for (uint32_t j = 0; j < n_src; j++) {
     uint64_t r = 0;
-    for (uint32_t i = src_sst[j]; i < src_sst[j + 1]; i++) r += rows_per_sst[i];
+    for (uint32_t i = src_sst[j]; i < src_sst[j + 1]; i++) {
+      sst_rows_before[i] = r;
+      r += rows_per_sst[i];
+    }
     src_start[j + 1] = src_start[j] + r;
   }
-  if (all.n >= 0xFFFFFFFFull) return SLATE_E_CAPACITY;
+  View all;
+  int s = SLATE_OK;
+  if (!views.empty() && (s = concat_views(ctx, views, &all))) return s;
+  views.clear();
+  // the warnings in the order types.ErrWarn gets them: NewMergeSort merges each source's warnings
+  // up to its first row (merge.go:33-44), then a source's remaining ones when it ends (:55-63), and
+  // sources end in the order their last entries (key, source) leave the heap
+  {
+    std::vector<std::pair<uint32_t, uint64_t>> order;  // (source, rank of its end) for sources with rows
+    std::vector<std::pair<std::vector<uint8_t>, uint32_t>> last;
+    for (uint32_t j = 0; j < n_src && !wl.empty(); j++) {
+      if (src_start[j + 1] == src_start[j]) continue;
+      uint64_t ko[2];
+      if ((s = d2h_small(ctx, ko, all.key_off->as<uint64_t>() + src_start[j + 1] - 1, 16))) return s;
+      std::vector<uint8_t> key(ko[1] - ko[0]);
+      if (!key.empty() && (s = d2h_small(ctx, key.data(), all.keys->as<uint8_t>() + ko[0], key.size()))) return s;
+      last.push_back({std::move(key), j});
+    }
+    std::sort(last.begin(), last.end());
+    std::vector<uint32_t> end_rank(n_src, 0);
+    for (size_t r = 0; r < last.size(); r++) end_rank[last[r].second] = uint32_t(r);
+    std::vector<const Warn*> init, later;
+    for (const Warn& w : wl) {
+      const bool first = src_start[w.w.src + 1] == src_start[w.w.src] || sst_rows_before[w.w.sst] + w.rows_before == 0;
+      (first ? init : later).push_back(&w);
+    }
+    std::stable_sort(later.begin(), later.end(),
+                     [&](const Warn* a, const Warn* b) { return end_rank[a->w.src] < end_rank[b->w.src]; });
+    uint32_t k = 0;
+    for (const auto* part : {&init, &later})
+      for (const Warn* w : *part) {
+        if (k < warn_cap) warns[k] = w->w;
+        k++;
+      }
+    if (n_warn) *n_warn = k;
+  }
+  const int done = wl.empty() ? SLATE_OK : SLATE_E_WARNINGS;
+  if (all.n == 0) return done;  // no entries: no output SST (executor.go opens a writer on the first entry)
+  if (all.n >= 0xFFFFFFFFull) return SLATE_E_LIMIT;
   hipStream_t st = ctx->stream;
   DEV(d_idx, all.n * 4 + 16);
   DEV(d_misc, 64);
@@ -314,7 +412,7 @@ int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, 
   }
   if (ends.size() > out_cap || (!ends.empty() && !out_tables)) {
     *n_out = uint32_t(ends.size());
-    return SLATE_E_CAPACITY;
+    return SLATE_E_CAPACITY;  // *n_out > out_cap: the number needed
   }
   uint64_t start = 0;
   uint32_t made = 0;
@@ -338,7 +436,21 @@ int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, 
     start = end;
   }
   *n_out = made;
-  return SLATE_OK;
+  return done;
+}
+
+int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst, const uint32_t* src_sst,
+                  uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size, slate_sst_table** out_tables,
+                  uint32_t out_cap, uint32_t* n_out) {
+  slate_compact_warning w{};
+  uint32_t nw = 0;
+  const int s = slate_compact_ex(ctx, ssts, sst_off, n_sst, src_sst, n_src, out_cfg, max_sst_size, out_tables, out_cap,
+                                 n_out, &w, 1, &nw);
+  if (s != SLATE_E_WARNINGS) return s;
+  // a compaction that returned an error has no sorted run (startCompaction, executor.go:166-173)
+  for (uint32_t k = 0; k < *n_out; k++) slate_sst_table_free(out_tables[k]);
+  *n_out = 0;
+  return w.status;
 }
 
 }  // extern "C"

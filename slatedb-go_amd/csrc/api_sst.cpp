@@ -44,7 +44,7 @@ int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* 
   uint32_t* out = scratch + (crc_scratch_bytes(n) / 4);
   {
     GpuSpan gs(ctx, ctx->stream);
-    SLATE_HIP(launch_crc32(ctx->stream, d_data, n, scratch, out));
+    SLATE_HIP(launch_crc32(ctx->stream, d_data, n, scratch, out, ctx->num_cus));
   }
   SLATE_HIP(hipMemcpyAsync(crc, out, 4, hipMemcpyDeviceToHost, ctx->stream));
   SLATE_HIP(hipStreamSynchronize(ctx->stream));
@@ -135,7 +135,7 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
   uint32_t* cout = scratch + (crc_scratch_bytes(total) / 4);
   {
     GpuSpan gs(ctx, st);
-    SLATE_HIP(launch_crc32(st, d, total, scratch, cout));
+    SLATE_HIP(launch_crc32(st, d, total, scratch, cout, ctx->num_cus));
   }
   uint32_t crc = 0;
   SLATE_HIP(hipMemcpyAsync(&crc, cout, 4, hipMemcpyDeviceToHost, st));
@@ -1566,7 +1566,7 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
   uint32_t crc = 0;
   {
     GpuSpan gs(ctx, st);
-    s = hip(launch_crc32(st, enc, nb + 2, scratch, cout));
+    s = hip(launch_crc32(st, enc, nb + 2, scratch, cout, ctx->num_cus));
   }
   if (!s) s = hip(hipMemcpyAsync(&crc, cout, 4, hipMemcpyDeviceToHost, st));
   if (!s) s = hip(hipStreamSynchronize(st));
@@ -1606,7 +1606,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   };
   int st = builder_flush(b, true, side_filter ? &start_filter : nullptr, &start_index);
   if (side_filter && !fjob.valid() && !st) start_filter(b->n_hashes);  // nothing was pending
-  if (st) return st;  // (started filter / index jobs are joined by their futures)
+  // a failed final flush may have queued index entries of blocks it never delivered: the builder
+  // keeps the error instead of letting a retry push them twice (started filter / index jobs are
+  // joined by their futures)
+  if (st) return b->sticky = st;
   if (!fb_job.valid()) start_index();  // no block was finished by the final flush
   const double t1 = host_trace() ? now_ms() : 0.0;
   b->built = true;
@@ -1620,7 +1623,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
     if (f.st) {
       fb_job.wait();
       delete t;
-      return f.st;
+      return b->sticky = f.st;
     }
     buf.insert(buf.end(), f.section.begin(), f.section.end());
     t->bloom_bits.swap(f.bits);
@@ -1872,6 +1875,11 @@ struct slate_index {
 };
 
 extern "C" {
+
+int slate_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* crc) {
+  if (!ctx || !crc || (n && !d_data)) return SLATE_E_INVALID_ARG;
+  return ctx_crc32_device(ctx, d_data, n, crc);
+}
 
 // DecodeIndex (flatbuf.go:83-100) + Index.BlockMeta() (flatbuf.go:22-31).
 int slate_decode_index(slate_ctx* ctx, const uint8_t* buf, size_t len, int codec, slate_index** index) {

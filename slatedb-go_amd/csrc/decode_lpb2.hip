@@ -50,6 +50,12 @@ namespace {
 // ring positions still valid behind d: a step's store reaches 20 bytes past d's dword
 // (five dwords), i.e. 109 bytes behind d modulo the ring
 constexpr uint32_t kReach = kOR - 20;
+// section markers in the assembly (tools/loop_mix.py --marks): reading aid only, they fence the scheduler
+#ifdef SLATE_ASM_MARKS
+#define LPB_MARK(x) asm volatile("; @@" #x ::: "memory")
+#else
+#define LPB_MARK(x) ((void)0)
+#endif
 // CodecLz4 frame constants (LZ4 frame format; decode.hip has the exact path's copies)
 constexpr uint32_t kLz4Magic = 0x184D2204u;
 constexpr uint32_t kXP1 = 2654435761u, kXP2 = 2246822519u, kXP3 = 3266489917u, kXP4 = 668265263u,
@@ -81,6 +87,17 @@ constexpr uint32_t kVerifyBatch = SLATE_VERIFY_BATCH;
 #define SLATE_ROW_CPOL 16
 #endif
 constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
+// Row-descriptor stores wait until after the iteration's hole-source load (1), or go out right
+// after the walker (0).  vmcnt retires in issue order, so the next iteration's wait for the hole
+// source (issued after the steps) also waited for every row store of the steps before it.
+#ifndef SLATE_ROWS_DEFER
+#define SLATE_ROWS_DEFER 0
+#endif
+// the step before which the previous iteration's hole source is merged (0..3): later gives the
+// load longer to arrive; a lane's next hole waits for it
+#ifndef SLATE_ABSORB_AT
+#define SLATE_ABSORB_AT 0
+#endif
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
 #endif
@@ -140,15 +157,19 @@ struct Lane {
   uint32_t sh, clen, dn, last_chunk, rcap;
   int32_t crc_last;
   uint32_t crc, crc_pos;
-  // decode
-  uint32_t s, d, rem, src, eff, lit, far, dd, err;
+  // decode: s = the next tag (payload-relative); src = the current item's source: an input-ring
+  // position (sh included) for a literal, an output position for a copy
+  uint32_t s, d, rem, src, eff;
+  bool lit, far, dd, err;
   uint32_t T;  // the output ring's dword at d & ~3 (what the next store merges below d)
   uint32_t z;  // a run-time zero (see rd128)
-  uint32_t c_issue, c_commit, n_req, fpend, fready, fl;
-  uint32_t qoff;  // far-copy / hole source requested this iteration (loaded once, before the flush)
-  // pending hole: a copy with offset > kReach and length <= 16 reserves output [hd, hd+hl)
-  // and decoding goes on; its source arrives at the start of the next iteration
-  uint32_t hpend, hd, hl;
+  uint32_t c_issue, c_commit, n_req, fl;
+  uint32_t qoff;  // hole source requested this iteration (loaded once, before the flush)
+  // pending hole: up to 16 bytes of a copy with offset > kReach reserve output [hd, hd+hl) and
+  // decoding goes on; the source is loaded at the end of the iteration and merged at the start
+  // of the next one (hp is set exactly from a hole's step to the next iteration's start)
+  bool hp;
+  uint32_t hd, hl;
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
   uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
@@ -166,6 +187,12 @@ struct Rsrc {
   __amdgpu_buffer_rsrc_t in, out, rows;
 };
 
+// the rows the walker finished in an iteration's steps 1 and 3 (stored after the hole-source load)
+struct RowOut {
+  v4u row1, row3;
+  uint32_t off1, off3;
+};
+
 // CRC32 of the next committed input chunk (bytes outside the block zeroed).
 __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint32_t* tab, bool go) {
   const uint32_t k = L.crc_pos;
@@ -178,8 +205,8 @@ __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint
     v.z &= keep_mask(lo, hi, 2);
     v.w &= keep_mask(lo, hi, 3);
   }
-  uint32_t c = L.crc;
-  c = crc16_chunk(tab, c, v);
+  v.x ^= L.crc;
+  const uint32_t c = crc_chunk0(reinterpret_cast<const uint8_t*>(tab), v);
   L.crc = go ? c : L.crc;
   L.crc_pos += go ? 1u : 0u;
 }
@@ -211,7 +238,7 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   const uint32_t fp = L.R + 4 + L.rsl + 8;
   const bool p0 = L.rphase == 0, p1 = L.rphase == 1;
   const uint32_t rpos = p0 ? L.R : (p1 ? fp : L.R + L.ro);
-  const bool in_hole = L.hpend && rpos < L.hd + L.hl && rpos + 8 > L.hd;
+  const bool in_hole = L.hp && rpos < L.hd + L.hl && rpos + 8 > L.hd;
   const bool wa = act & (L.rphase < 3) & (L.d >= L.rneed) & !in_hole;
   const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
   const W6 q = ring_rd24(ring, rpos);
@@ -225,7 +252,7 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   const uint32_t vl0 = __builtin_bswap32(vb == 0 ? fw1 : alignb(fw1, fw, vb));
   const bool tomb0 = (fl0 & 1) != 0;
   const uint32_t rlen0 = 4 + sl0 + 9 + (tomb0 ? 0u : 4u);
-  const bool hole0 = L.hpend && rpos < L.hd + L.hl && rpos + rlen0 > L.hd;
+  const bool hole0 = L.hp && rpos < L.hd + L.hl && rpos + rlen0 > L.hd;
   const bool one = p0 & (sl0 <= 7) & !(fl0 & 6) & (L.d >= L.R + rlen0) & !hole0;
   // phase 1: flags, and the value length right after them when there are no timestamps
   const uint32_t fl1 = q.w[0] & 0xff;
@@ -282,6 +309,79 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   return emit;
 }
 
+// The walker's common case alone (phase 0: a row whose header, flags and value length lie in its
+// first 24 bytes, one action), for lanes in phase 0; walk() runs the general walk_step only when
+// some lane is in phase 1 or 2 (a suffix over 7 bytes, timestamps).  Same transitions as
+// walk_step's phase 0.
+__device__ __forceinline__ bool walk_fast(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
+  const uint32_t rpos = L.R;
+  const bool in_hole = L.hp & (rpos < L.hd + L.hl) & (rpos + 8 > L.hd);
+  const bool wa = act & (L.rphase == 0) & (L.d >= L.rneed) & !in_hole;
+  const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
+  const W6 q = ring_rd24(ring, rpos);
+  const uint32_t pl0 = be16_of(q.w[0]), sl0 = be16_of(q.w[0] >> 16);
+  const uint32_t f0 = 12 + sl0;
+  const bool hi0 = (f0 & 16) != 0;
+  const uint32_t fw = hi0 ? q.w[4] : q.w[3], fw1 = hi0 ? q.w[5] : q.w[4];
+  const uint32_t fl0 = (fw >> (8 * (f0 & 3))) & 0xff;
+  const uint32_t vb = (f0 + 1) & 3;
+  const uint32_t fa = alignb(fw1, fw, vb);
+  const uint32_t vl0 = __builtin_bswap32(vb == 0 ? fw1 : fa);
+  const bool tomb0 = (fl0 & 1) != 0;
+  const uint32_t rlen0 = 4 + sl0 + 9 + (tomb0 ? 0u : 4u);
+  const bool hole0 = L.hp & (rpos < L.hd + L.hl) & (rpos + rlen0 > L.hd);
+  const bool one = (sl0 <= 7) & !(fl0 & 6) & (L.d >= rpos + rlen0) & !hole0;
+  const bool done = wa & !lost & one;
+  const uint32_t vl = tomb0 ? 0u : vl0;
+  const bool pfail = pl0 > uint32_t(max(L.fk, 0));
+  row = pack_row(rpos, pl0, sl0, pfail ? 0u : vl, pfail ? 0u : fl0 & 7, pfail ? 0u : rlen0 - 4 - sl0,
+                 pfail ? uint32_t(SLATE_E_ROW_PREFIX) : uint32_t(SLATE_OK));
+  ridx = L.nwalk;
+  L.fk = (done & (L.nwalk == 0) & !pfail) ? int32_t(sl0) : L.fk;
+  const bool emit = done & (L.nwalk < L.rcap);
+  const uint32_t next = rpos + rlen0 + vl;  // < 2^32: vl0 is checked against dn below first
+  const bool vbig = vl > L.dn;
+  const bool to1 = wa & !lost & !one;
+  L.rpl = to1 ? pl0 : L.rpl;
+  L.pl0 = (wa & !lost & (rpos == 0)) ? pl0 : L.pl0;
+  L.rsl = to1 ? sl0 : L.rsl;
+  L.nwalk += done ? 1u : 0u;
+  const bool stop = (wa & lost) | (done & (vbig | (next > L.dn)));
+  const bool adv = done & !vbig & (next <= L.dn);
+  L.R = adv ? next : L.R;
+  uint32_t rph = L.rphase, rn = L.rneed;
+  const uint32_t rn1 = rpos + 4 + sl0 + 13, rna = min(next + 24, L.dn);
+  rph = to1 ? 1u : rph;
+  rn = to1 ? rn1 : rn;
+  rph = adv ? 0u : rph;
+  rn = adv ? rna : rn;
+  rph = stop ? 3u : rph;
+  rn = stop ? 0xFFFFFFFFu : rn;
+  L.rphase = rph;
+  L.rneed = rn;
+  return emit;
+}
+
+// One walker call: the fast phase-0 action, and the general one for lanes in phase 1 or 2.
+__device__ __forceinline__ bool walk(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
+  const bool slow = act & ((L.rphase == 1) | (L.rphase == 2));
+  const bool slow_go = slow & (L.d >= L.rneed);
+  bool emit = walk_fast(L, ring, act, row, ridx);
+#ifdef SLATE_COUNT_FAST_ONLY  // static instruction counts of the common path (tools/loop_mix.py)
+  if (false) {
+#else
+  if (__builtin_amdgcn_ballot_w64(slow_go)) {
+#endif
+    v4u row2;
+    uint32_t ridx2;
+    const bool e2 = walk_step(L, ring, slow, row2, ridx2);
+    row = slow ? row2 : row;
+    ridx = slow ? ridx2 : ridx;
+    emit = slow ? e2 : emit;
+  }
+  return emit;
+}
+
 // Start of an iteration: (1) the chunks loaded one iteration ago go into their blocks'
 // input rings (the loading lane writes them: transposed layout); (2) every block asks for
 // up to four more chunks (ring room and payload end permitting); (3) four transposed
@@ -309,14 +409,11 @@ __device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, ui
   return act ? min(min(room, left), 4u) : 0u;
 }
 
-// Start of an iteration, after the refill: the far-copy source loaded in the previous
-// iteration (at most one per lane) either fills the pending hole -- a read-modify-write of
-// the five ring dwords around [hd, hd+hl): the bytes after the hole were decoded meanwhile --
-// or feeds a long far copy through FD.
-__device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q, v4u& FD, uint8_t* ring) {
-  const bool fc = L.fpend != 0;
-  const bool fill = fc && L.hpend;
-  if (__builtin_amdgcn_ballot_w64(fill)) {
+// Start of an iteration, after the refill: the hole source loaded at the end of the previous
+// iteration (Q) fills the pending hole -- a read-modify-write of the five ring dwords around
+// [hd, hd+hl): the bytes after the hole were decoded meanwhile.
+__device__ __forceinline__ void absorb_hole(Lane& L, const v4u& Q, uint8_t* ring) {
+  if (__builtin_amdgcn_ballot_w64(L.hp)) {
     const uint32_t hd = L.hd, b = hd & 3, a4 = hd & ~3u, a = hd & ~7u;
     const v2u A = rd64(ring, a), B = rd64(ring, a + 8), C = rd64(ring, a + 16);
     const bool q = (hd & 4) != 0;
@@ -327,22 +424,26 @@ __device__ __forceinline__ void absorb_far(Lane& L, const v4u& Q, v4u& FD, uint8
     o.y3 = q ? C.x : B.y;
     o.y4 = q ? C.y : C.x;
     const Win5 y = shift_in(Q, o.y0, b);
-    const int32_t lo = int32_t(b), hi = int32_t(b + L.hl);
+    // window bytes [b, e) are the hole's: dword j keeps bytes below e - 4j (a 64-bit shift
+    // gives 0 for a count of 32), dword 0 also only from b on
+    const int32_t e8 = int32_t(8 * (b + L.hl));
+    auto upto = [&](int32_t j) -> uint32_t {
+      const uint32_t sh = uint32_t(min(max(32 * (j + 1) - e8, 0), 32));
+      return uint32_t(0xFFFFFFFFull >> sh);
+    };
+    const uint32_t m0 = upto(0) & (0xFFFFFFFFu << (8 * b)), m1 = upto(1), m2 = upto(2), m3 = upto(3), m4 = upto(4);
     Win5 n;
-    n.y0 = (y.y0 & keep_mask(lo, hi, 0)) | (o.y0 & ~keep_mask(lo, hi, 0));
-    n.y1 = (y.y1 & keep_mask(lo, hi, 1)) | (o.y1 & ~keep_mask(lo, hi, 1));
-    n.y2 = (y.y2 & keep_mask(lo, hi, 2)) | (o.y2 & ~keep_mask(lo, hi, 2));
-    n.y3 = (y.y3 & keep_mask(lo, hi, 3)) | (o.y3 & ~keep_mask(lo, hi, 3));
-    n.y4 = (y.y4 & keep_mask(lo, hi, 4)) | (o.y4 & ~keep_mask(lo, hi, 4));
-    if (fill) store_win(ring, a4, n);
+    n.y0 = (y.y0 & m0) | (o.y0 & ~m0);
+    n.y1 = (y.y1 & m1) | (o.y1 & ~m1);
+    n.y2 = (y.y2 & m2) | (o.y2 & ~m2);
+    n.y3 = (y.y3 & m3) | (o.y3 & ~m3);
+    n.y4 = (y.y4 & m4) | (o.y4 & ~m4);
+    if (L.hp) store_win(ring, a4, n);
     // the register copy of d's dword follows a store into that dword
     const uint32_t jd = (((L.d & ~3u) - a4) & (kOR - 1)) >> 2;
-    L.T = (fill && jd <= 4) ? pick5(n, jd) : L.T;
+    L.T = (L.hp && jd <= 4) ? pick5(n, jd) : L.T;
   }
-  FD = (fc && !fill) ? Q : FD;
-  L.fready = (fc && !fill) ? 1u : L.fready;
-  L.hpend = fill ? 0u : L.hpend;
-  L.fpend = 0;
+  L.hp = false;
 }
 
 // Appends item to list (wave-aggregated: one atomic per wave); every lane of the wave calls it.
@@ -373,12 +474,10 @@ __device__ __forceinline__ void xxh_absorb(Lane& L, const uint8_t* ring, bool go
 // (decode.hip wave_lz4_decode) for one independent block; a run of extension bytes
 // longer than the 8-byte window, or any failed check, hands the block to the exact path
 // (L.hb), which then decodes and reports it.  A token without literals is parsed with its match.
-__device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, int32_t avail, bool& hole_new,
-                                          uint32_t& hole_src) {
+__device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, int32_t avail, uint32_t lim_d) {
   const bool need = act && !L.dd && L.rem == 0;
   const bool fin = need && L.lph == 2;
-  const bool room_out = L.d - 16 * L.fl <= kUnflushed;
-  const bool can = need & (L.lph < 2) & (avail >= int32_t(min(L.s + 8, L.clen))) & room_out;
+  const bool can = need & (L.lph < 2) & (avail >= int32_t(min(L.s + 8, L.clen))) & (L.d <= lim_d);
   const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
   const uint64_t w64 = (uint64_t(w.y) << 32) | w.x;
   const uint32_t tok = w.x & 0xff;
@@ -411,13 +510,12 @@ __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, 
   const bool bad = ext_bad || (mph ? bad_m : bad_tok);
   const bool ok = can && !bad;
   L.hb |= (can && bad) ? 1u : 0u;
-  L.dd |= (fin || (can && bad)) ? 1u : 0u;
-  L.lit = ok ? uint32_t(!mph) : L.lit;
+  L.dd = L.dd || fin || (can && bad);
+  L.lit = ok ? !mph : L.lit;
   L.rem = ok ? (mph ? ml : len) : L.rem;
-  L.src = ok ? (mph ? L.d - off : s1) : L.src;
+  L.src = ok ? (mph ? L.d - off : L.sh + s1) : L.src;
   L.eff = ok ? (mph ? off : 16u) : L.eff;
-  const bool far = mph && off > kReach;
-  L.far = ok ? uint32_t(far) : L.far;
+  L.far = ok ? (mph && off > kReach) : L.far;
   L.s = ok ? (mph ? s1 : lit_end) : L.s;
   L.mtok = (ok && !mph) ? (tok & 15) : L.mtok;
   L.lph = ok ? (mph ? 0u : (last ? 2u : 1u)) : L.lph;
@@ -425,100 +523,106 @@ __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, 
   const bool fix = ok && !mph && last;
   L.dn = fix ? L.d + len : L.dn;
   L.rneed = fix ? min(L.rneed, L.d + len) : L.rneed;
-  hole_new = ok && far && ml <= 16 && !L.hpend && !L.fpend;
-  hole_src = L.d - off;
-  L.hd = hole_new ? L.d : L.hd;
-  L.hl = hole_new ? ml : L.hl;
-  L.hpend = hole_new ? 1u : L.hpend;
-  L.d += hole_new ? ml : 0u;
-  L.rem = hole_new ? 0u : L.rem;
-  L.far = hole_new ? 0u : L.far;
 }
 
-// One step: CRC (two of four steps), parse, copy, the far-copy / hole load, and the row
-// walker (the other two steps).
+// golang/snappy's tag parse (decode_other.go:19-110) at payload position L.s, in 32-bit
+// arithmetic: a literal length that does not fit saturates, and any length beyond the output or
+// the payload fails the same checks.
+__device__ __forceinline__ void snappy_parse(Lane& L, bool act, const uint8_t* in, int32_t avail, uint32_t lim_d) {
+  // written with & | and selects between computed values: short-circuit operators and
+  // conditional expressions became divergent branches
+  const uint32_t sn = L.clen;
+  const bool need = act & !L.dd & (L.rem == 0);
+  const bool fin = need & (L.s >= sn);
+  // throttle (a hole delays the flush): after any step d - 16*fl <= 96, so the ring keeps every
+  // unflushed byte and every far source (offset > kReach) is already flushed
+  const uint32_t s5 = min(L.s + 5, sn);
+  const bool can = need & (L.s < sn) & (avail >= int32_t(s5)) & (L.d <= lim_d);
+  const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
+  const uint32_t c = w.x & 0xff, t = c & 3, xl = c >> 2;
+  const uint32_t b14 = alignb(w.y, w.x, 1);  // bytes s+1 .. s+4
+  const uint32_t xl59 = xl - 59;
+  const uint32_t nb = xl >= 60 ? xl59 : 0u;  // literal length bytes (1..4)
+  const uint32_t ext = b14 & (0xFFFFFFFFu >> ((32 - 8 * nb) & 31));
+  const uint32_t lm1 = nb ? ext : xl;
+  const uint32_t lm1p = lm1 + 1;
+  const uint32_t lit_len = lm1p == 0 ? lm1 : lm1p;  // saturating: fails the bounds below
+  const bool tl = t == 0, t1 = t == 1;
+  const uint32_t l1 = 4 + (xl & 7), l23 = xl + 1;
+  const uint32_t cp_len = t1 ? l1 : l23;
+  const uint32_t off1 = ((c >> 5) << 8) | (b14 & 0xff), o16 = b14 & 0xffff;
+  const uint32_t off23 = (t & 1) ? b14 : o16;
+  const uint32_t cp_off = t1 ? off1 : off23;
+  const uint32_t hl_cp = (0x5320u >> (4 * t)) & 15, hl_lit = 1 + nb;  // header bytes: 2, 3, 5 for copies
+  const uint32_t hl = tl ? hl_lit : hl_cp;
+  const uint32_t len = tl ? lit_len : cp_len;
+  const uint32_t s1 = L.s + hl;
+  const uint32_t room = L.dn - L.d, left = sn - s1;
+  const bool bad_lit = len > left, bad_cp = (cp_off == 0) | (cp_off > L.d);
+  const bool bad_t = tl ? bad_lit : bad_cp;
+  const bool bad = (s1 > sn) | (len > room) | bad_t;
+  const bool ok = can & !bad, fail = can & bad;
+  L.err = L.err | fail;
+  L.dd = L.dd | fin | fail;
+  const uint32_t src_lit = L.sh + s1, src_cp = L.d - cp_off, s_lit = s1 + len;
+  const uint32_t src_new = tl ? src_lit : src_cp, eff_new = tl ? 16u : cp_off, s_new = tl ? s_lit : s1;
+  const bool far_new = !tl & (cp_off > kReach);
+  L.lit = ok ? tl : L.lit;
+  L.far = ok ? far_new : L.far;
+  L.rem = vsel(ok, len, L.rem);
+  L.src = vsel(ok, src_new, L.src);
+  L.eff = vsel(ok, eff_new, L.eff);
+  L.s = vsel(ok, s_new, L.s);
+}
+
+// One step: CRC (two of four steps), parse, a hole or a 16-byte move, and the row walker
+// (the other two steps).
 // kSlot: 0 and 2 absorb a CRC chunk; 1 and (when needed) 3 run the walker
 template <int kSlot, bool kLz4>
-__device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint8_t* ring,
-                                          uint8_t* in, const uint32_t* tab, const Rsrc& R, uint32_t dbg) {
+__device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint8_t* in, const uint32_t* tab,
+                                          const Rsrc& R, uint32_t lim_d, uint32_t cend, uint32_t dbg, RowOut& ro) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
   dbg = SLATE_FORCE_DBG;
 #endif
   // ---- CRC32 of one committed chunk (the two steps without the walker)
+  LPB_MARK(crc);
   if (kSlot == 0 || kSlot == 2) {
     const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
     if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
     else crc_chunk(L, in, tab, go);
   }
-  const int32_t avail = int32_t(16 * L.c_commit) - int32_t(L.sh);  // committed payload bytes [0, avail)
-  bool hole_new = false;
-  uint32_t hole_src = 0;
-  if constexpr (kLz4) {
-    lz4_parse(L, act, in, avail, hole_new, hole_src);
-  } else {
-  const uint32_t sn = L.clen;
-  // ---- parse the next tag (golang/snappy decode_other.go:19-110)
+  const int32_t avail = int32_t(cend) - int32_t(L.sh);  // committed payload bytes [0, avail)
+  LPB_MARK(parse);
+  if constexpr (kLz4) lz4_parse(L, act, in, avail, lim_d);
+  else snappy_parse(L, act, in, avail, lim_d);
+  LPB_MARK(hole);
+  // ---- a far copy (offset > kReach: its source left the ring and is flushed) goes on as holes
+  // of up to 16 bytes, one pending per lane: reserve the bytes, load the source, go on decoding
   {
-    const bool need = act && !L.dd && L.rem == 0;
-    const bool fin = need && L.s >= sn;
-    // throttle (a hole delays the flush): after any step d - 16*fl <= 96, so the ring keeps
-    // every unflushed byte and every far source (offset > kReach) is already flushed
-    const bool room_out = L.d - 16 * L.fl <= kUnflushed;
-    const bool can = need & (L.s < sn) & (avail >= int32_t(min(L.s + 5, sn))) & room_out;
-    const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
-    const uint32_t c = w.x & 0xff, t = c & 3;
-    const uint32_t b14 = (w.x >> 8) | (w.y << 24);  // bytes s+1 .. s+4
-    const uint32_t xl = c >> 2;
-    const uint32_t nb = xl >= 60 ? xl - 59 : 0;
-    const uint32_t ext = nb >= 4 ? b14 : (b14 & ((1u << (8 * nb)) - 1));
-    const uint64_t lit_len = uint64_t(nb ? ext : xl) + 1;
-    // selects on the tag's bits (equality chains on t became branch trees)
-    const uint32_t cp_len = (t == 1) ? 4 + ((c >> 2) & 7) : 1 + (c >> 2);
-    const uint32_t off1 = ((c & 0xe0) << 3) | (b14 & 0xff), off2 = b14 & 0xffff;
-    const uint32_t cp_off = (t & 2) ? ((t & 1) ? b14 : off2) : off1;
-    const uint32_t hl_cp = (t & 2) ? ((t & 1) ? 5u : 3u) : 2u;
-    const uint32_t hl = (t == 0) ? 1 + nb : hl_cp;
-    const uint32_t s1 = L.s + hl;
-    const bool bad_lit = lit_len > uint64_t(L.dn - L.d) || lit_len > uint64_t(sn - min(s1, sn));
-    const bool bad_cp = cp_off == 0 || L.d < cp_off || cp_len > L.dn - L.d;
-    const bool bad = s1 > sn || (t == 0 ? bad_lit : bad_cp);
-    const bool ok = can && !bad;
-    L.err |= (can && bad) ? 1u : 0u;
-    L.dd |= (fin || (can && bad)) ? 1u : 0u;
-    L.lit = ok ? uint32_t(t == 0) : L.lit;
-    L.rem = ok ? (t == 0 ? uint32_t(lit_len) : cp_len) : L.rem;
-    L.src = ok ? (t == 0 ? s1 : L.d - cp_off) : L.src;
-    L.eff = ok ? (t == 0 ? 16u : cp_off) : L.eff;
-    const bool far = t != 0 && cp_off > kReach && !(dbg & 256);
-    L.far = ok ? uint32_t(far) : L.far;
-    L.s = ok ? (t == 0 ? s1 + uint32_t(lit_len) : s1) : L.s;
-    // a short far copy becomes a hole: reserve its bytes, load its source, go on decoding
-    hole_new = ok && far && cp_len <= 16 && !L.hpend && !L.fpend && !(dbg & 8192);
-    hole_src = L.d - cp_off;
-    L.hd = hole_new ? L.d : L.hd;
-    L.hl = hole_new ? cp_len : L.hl;
-    L.hpend = hole_new ? 1u : L.hpend;
-    L.d += hole_new ? cp_len : 0u;
-    L.rem = hole_new ? 0u : L.rem;
-    L.far = hole_new ? 0u : L.far;
+    const bool mk = act & !L.dd & L.far & (L.rem != 0) & !L.hp & (L.d <= lim_d);
+    const uint32_t n = min(L.rem, 16u);
+    L.hd = mk ? L.d : L.hd;
+    L.hl = mk ? n : L.hl;
+    L.qoff = mk ? L.out_rel + L.src : L.qoff;
+    L.hp = L.hp || mk;
+    L.d += mk ? n : 0u;
+    L.rem -= mk ? n : 0u;
+    L.src += mk ? n : 0u;
   }
-  }
-  // ---- move up to 16 bytes of the current tag into the output ring
+  // ---- move up to 16 bytes of a literal or a near copy into the output ring
+  LPB_MARK(move);
   {
-    const bool cp = act && !L.dd && L.rem != 0;
-    uint32_t k = min(L.rem, 16u);
-    {
-      const uint32_t k_lit = min(k, uint32_t(max(avail - int32_t(L.src), 0)));
-      const uint32_t k_far = L.fready ? k : 0u, k_near = min(k, L.eff);
-      const uint32_t k_cp = L.far ? k_far : k_near;
-      k = L.lit ? k_lit : k_cp;
-    }
+    const bool cp = act & !L.dd & (L.rem != 0) & !L.far & (L.d <= lim_d);
+    const uint32_t k16 = min(L.rem, 16u);
+    const uint32_t in_left = cend - L.src;
+    const uint32_t k_lit = min(k16, cend > L.src ? in_left : 0u), k_near = min(k16, L.eff);
+    uint32_t k = L.lit ? k_lit : k_near;
     // a ring copy stops short of the pending hole's bytes
-    const bool near = !L.lit && !L.far;
-    if (near && L.hpend && L.src < L.hd + L.hl && L.src + k > L.hd) k = L.src < L.hd ? L.hd - L.src : 0u;
-    k = (cp && L.d - 16 * L.fl <= kUnflushed) ? k : 0u;
-    const v4u vl = ring_rd16(L.lit ? in : ring, L.lit ? L.sh + L.src : L.src, L.lit ? kIR - 8 : kOR - 8);
-    const v4u v = L.far ? FD : vl;
+    const uint32_t to_hole = L.hd - L.src, k_hole = L.src < L.hd ? to_hole : 0u;
+    const bool cut = !L.lit & L.hp & (L.src < L.hd + L.hl) & (L.src + k > L.hd);
+    k = cut ? k_hole : k;
+    k = cp ? k : 0u;
+    const v4u v = ring_rd16(L.lit ? in : ring, L.src);
     // bytes from d on are not yet output: storing them when k == 0 is harmless; the first
     // dword keeps the bytes below d (L.T)
     const uint32_t b = L.d & 3;
@@ -528,28 +632,31 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
     L.d += k;
     L.rem -= k;
     // periodic output: once a whole period was copied, the pattern can be read twice as far back
-    const bool step_cp = k != 0 && k == L.eff && near;
-    const uint32_t eff2 = (step_cp && L.eff < 16) ? 2 * L.eff : L.eff;
-    L.src = (L.lit || L.far) ? L.src + k : L.d - eff2;
+    const bool step_cp = (k != 0) & (k == L.eff) & !L.lit & (L.eff < 16);
+    const uint32_t eff2 = step_cp ? 2 * L.eff : L.eff;
+    const uint32_t src_l = L.src + k, src_c = L.d - eff2;
+    L.src = L.lit ? src_l : src_c;
     L.eff = eff2;
-    L.fready = (L.far && k) ? 0u : L.fready;
   }
-  // ---- the far-copy / hole source request of this step (loaded at the end of the iteration)
-  {
-    const bool wantf = act && !L.dd && L.rem && L.far && !L.fready && !L.fpend;
-    L.qoff = hole_new ? L.out_rel + hole_src : (wantf ? L.out_rel + L.src : L.qoff);
-    L.fpend = (wantf || hole_new) ? 1u : L.fpend;
-    // the walker: every iteration once, and a second time only when some lane's walker has
-    // fallen more than 64 bytes behind (rows shorter than the iteration's output)
-    if (kSlot == 1 ||
-        (kSlot == 3 && __builtin_amdgcn_ballot_w64(act & (L.rphase < 3) & (L.d >= L.rneed) & (L.d - L.R > kWalkLag)))) {
-      v4u row;
-      uint32_t ridx;
-      const bool have_row = walk_step(L, ring, act && !(dbg & 128), row, ridx);
-      // stored right away: the loads waited on later were issued before it (refill) or are
-      // waited on an iteration later (far source), so its acknowledgement is off the path
-      __builtin_amdgcn_raw_buffer_store_b128(row, R.rows, (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB,
-                                             0, kRowCpol);
+  LPB_MARK(walk);
+  // ---- the walker: every iteration once, and a second time only when some lane's walker has
+  // fallen more than 64 bytes behind (rows shorter than the iteration's output)
+  if (kSlot == 1 ||
+      (kSlot == 3 && __builtin_amdgcn_ballot_w64(act & (L.rphase < 3) & (L.d >= L.rneed) & (L.d - L.R > kWalkLag)))) {
+    v4u row;
+    uint32_t ridx;
+    const bool have_row = walk(L, ring, act && !(dbg & 128), row, ridx);
+    const uint32_t off = (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB;
+    if (SLATE_ROWS_DEFER) {
+      if (kSlot == 1) {
+        ro.row1 = row;
+        ro.off1 = off;
+      } else {
+        ro.row3 = row;
+        ro.off3 = off;
+      }
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(row, R.rows, off, 0, kRowCpol);
     }
   }
 }
@@ -562,7 +669,7 @@ __device__ __forceinline__ void lane_step(Lane& L, const v4u& FD, bool act, uint
 // instead of 64 scattered 16-byte pieces (tools/scatter_probe.hip: ~3.5x cheaper).
 __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
                                                 uint32_t dbg) {
-  const uint32_t done = act ? min(L.d >> 4, L.hpend ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
+  const uint32_t done = act ? min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
   const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
   const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
   const uint32_t wave_lane0 = threadIdx.x - lane;
@@ -671,7 +778,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
     Lane L;
     const v4u zero = {0, 0, 0, 0};
-    v4u Q = zero, FD = zero;
+    v4u Q = zero;
     v4u P0 = zero, P1 = zero, P2 = zero, P3 = zero;
     uint32_t S0 = 0xFFFFFFFFu, S1 = 0xFFFFFFFFu, S2 = 0xFFFFFFFFu, S3 = 0xFFFFFFFFu;
     const uint32_t b = round0 + lane;
@@ -682,13 +789,15 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     L.crc_last = -1;
     L.crc = 0xFFFFFFFFu;
     L.crc_pos = 0;
-    L.s = L.d = L.rem = L.src = L.lit = L.far = L.err = L.T = 0;
+    L.s = L.d = L.rem = L.src = L.T = 0;
+    L.lit = L.far = L.err = false;
     L.z = a.rt_zero;
     L.eff = 16;
-    L.dd = 1;
-    L.c_issue = L.c_commit = L.n_req = L.fpend = L.fready = L.fl = 0;
+    L.dd = true;
+    L.c_issue = L.c_commit = L.n_req = L.fl = 0;
     L.qoff = kOOB;
-    L.hpend = L.hd = L.hl = 0;
+    L.hp = false;
+    L.hd = L.hl = 0;
     L.R = 0;
     L.rphase = 0;
     L.rneed = 4;
@@ -740,7 +849,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
                     q2 = ring_rd8(in, L.sh + 16, kIR - 8);
           const uint32_t dw[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
           const uint32_t cap = uint32_t(min<uint64_t>(a.out_off[b + 1] - a.out_off[b], 0xFFFFFFF0ull));
-          if (lz4_frame_head(L, dw, cap, want_size)) L.dd = 0;
+          if (lz4_frame_head(L, dw, cap, want_size)) L.dd = false;
           else L.hb = 1;
         }
       } else if (have) {
@@ -766,11 +875,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
           }
         }
         if (!ok || x > kSnappyMaxExpansion * uint64_t(L.clen)) {
-          L.err = 1;
+          L.err = true;
         } else {
           L.dn = uint32_t(x);
           L.s = hdr;
-          L.dd = 0;
+          L.dd = false;
         }
       }
     }
@@ -784,10 +893,11 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     // `budget` iterations; the budget only guarantees that the loop ends (an exhausted
     // lane reports SLATE_E_HIP, never a wrong result).
     const uint32_t budget = have ? (L.clen + L.dn) / 2 + 1024 : 0u;
-    while (__ballot(have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
+    while (__ballot(have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                     iters < budget)) {
-      const bool act = have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
+      const bool act = have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                        iters < budget;
+      LPB_MARK(refill);
       {
         commit_one(ins, S0, P0, L.z);
         commit_one(ins, S1, P1, L.z);
@@ -795,8 +905,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         commit_one(ins, S3, P3, L.z);
         L.c_commit += L.n_req;
         // the ring keeps every chunk from the oldest byte still to be read or CRC'd
-        const uint32_t lo_pos = L.dd ? L.clen : ((L.rem && L.lit) ? L.src : L.s);
-        const uint32_t lo_chunk = min((L.sh + lo_pos) >> 4, L.crc_pos);
+        const uint32_t lo_pos = L.dd ? L.sh + L.clen : ((L.rem && L.lit) ? L.src : L.sh + L.s);
+        const uint32_t lo_chunk = min(lo_pos >> 4, L.crc_pos);
         const uint32_t n = refill_count(act, lo_chunk, L.c_issue, L.last_chunk);
         const uint32_t info = (L.c_issue << 3) | n;
         const uint32_t wave_lane0 = threadIdx.x - lane;
@@ -808,16 +918,30 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         L.c_issue += n;
         L.n_req = n;
       }
-      absorb_far(L, Q, FD, ring);
-      lane_step<0, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      lane_step<1, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      lane_step<2, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      lane_step<3, kLz4>(L, FD, act, ring, in, tab, R, dbg_bits(a));
-      // the far-copy / hole source requested in this iteration (at most one per lane; sc1:
-      // L1 bypass), before the flush stores so that vmcnt waits stay static; it is merged
-      // at the start of the next iteration
+      // per iteration: the throttle's limit on d, and the end of the committed input (ring positions)
+      const uint32_t lim_d = 16 * L.fl + kUnflushed, cend = 16 * L.c_commit;
+      RowOut ro;
+      ro.off1 = ro.off3 = kOOB;
+      ro.row1 = ro.row3 = zero;
+      LPB_MARK(absorb);
+      if (SLATE_ABSORB_AT == 0) absorb_hole(L, Q, ring);
+      lane_step<0, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_ABSORB_AT == 1) absorb_hole(L, Q, ring);
+      lane_step<1, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_ABSORB_AT == 2) absorb_hole(L, Q, ring);
+      lane_step<2, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_ABSORB_AT == 3) absorb_hole(L, Q, ring);
+      lane_step<3, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      // the hole source requested in this iteration (at most one per lane; sc1: L1 bypass),
+      // before the flush stores so that vmcnt waits stay static; it is merged at the start of
+      // the next iteration
+      LPB_MARK(flush);
       Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg_bits(a) & 32768) ? kOOB : L.qoff, 0, 16);
       L.qoff = kOOB;
+      if (SLATE_ROWS_DEFER) {
+        __builtin_amdgcn_raw_buffer_store_b128(ro.row1, R.rows, ro.off1, 0, kRowCpol);
+        __builtin_amdgcn_raw_buffer_store_b128(ro.row3, R.rows, ro.off3, 0, kRowCpol);
+      }
       flush_iteration(L, act, outs, lane, R, dbg_bits(a));
       if constexpr (kLz4) {
         // the content checksum's stripes: the chunks just completed (at most four), still in the ring
@@ -831,7 +955,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
     // ---------------- finalise the round's blocks (SIMD across lanes)
     // iters counts the wave's iterations: a lane that finished early is not exhausted
-    if (have && !(L.dd && !L.hpend && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk)) {
+    if (have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk)) {
       m.status = SLATE_E_HIP;  // step budget exhausted (see above): a kernel defect, reported loudly
       a.meta[b] = m;
       have = false;

@@ -77,7 +77,7 @@ hipError_t launch_snappy_gather(hipStream_t st, const uint8_t* slots, const uint
 hipError_t launch_snappy_chunks(hipStream_t st, const uint8_t* src, uint64_t n, uint8_t* dst, uint32_t* len,
                                 int num_cus);
 size_t crc_scratch_bytes(uint64_t n);
-hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out);
+hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out, int num_cus);
 // In-place exclusive scan of one u64 array of n+1 entries (the last becomes the total).
 hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t n_plus_1, void* scratch);
 size_t scan_scratch_bytes(uint32_t n_plus_1);

@@ -25,6 +25,7 @@
 #include "common.h"
 #include "encode.h"
 #include "wave_crc.h"
+#include "lpb_common.h"
 #include "snappy_enc.h"
 
 namespace slate {
@@ -512,70 +513,130 @@ __global__ void bloom_check_kernel(const uint8_t* __restrict__ keys, const uint6
 }
 
 // --------------------------------------------------------- large-buffer CRC
-// Chunks of 4096 bytes, front-aligned; chunk partials R(0, chunk) (chunk 0 with
-// the 0xFFFFFFFF init folded in), combined by one wavefront.
-constexpr int kCrcThreads = 256;
+// crc32.ChecksumIEEE of a device buffer (the SST builder's filter and index payloads, up to tens of
+// MB).  The buffer is cut into 16-byte chunks aligned to memory (chunk j = aligned bytes
+// [16j, 16j + 16) from the 16-byte line of its first byte); the chunks wholly before the end form
+// the "body", the bytes of the last partial chunk the "tail".  Each wave turns a stripe of 256
+// body chunks into its raw CRC (slicing-by-16 per lane, lanes and rows joined by the zero-advance
+// tables, as decode_none's block CRC), grid-stride, tables loaded once per workgroup; one wave
+// then joins the stripes (GF(2) products) and the tail.  The 0xFFFFFFFF initial register is
+// folded into message bytes 0..3 and the bytes before the message are zeroed.
+constexpr uint32_t kCrcThreads = 256;
+constexpr uint32_t kCrcStripeChunks = 256;
+constexpr uint32_t kCrcLds = kTab16Bytes + kAdvN * 4096;
 
-__global__ __launch_bounds__(kCrcThreads) void crc_chunks_kernel(const uint8_t* __restrict__ data, uint64_t n,
-                                                                 uint32_t* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
-  load_crc_tables(tab);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t* buf = smem + kTabBytes + wave * (kCrcStripe + 32);
-  uint64_t nchunks = (n + kCrcStripe - 1) / kCrcStripe;
-  uint64_t k = uint64_t(blockIdx.x) * (kCrcThreads / 64) + wave;
-  if (k >= nchunks) return;
-  uint64_t s0 = k * kCrcStripe;
-  uint32_t len = uint32_t(min<uint64_t>(kCrcStripe, n - s0));
-  const uint8_t* g = data + s0;
-  uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(g) & 15);
-  const uint4* src = reinterpret_cast<const uint4*>(g - shift);
-  uint32_t chunks = (shift + len + 15) / 16;
-  for (uint32_t c = lane; c < chunks; c += kWave) reinterpret_cast<uint4*>(buf)[c] = src[c];
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  uint32_t r;
-  if (k == 0 && len < 4) {
-    uint32_t c = 0xFFFFFFFFu;
-    for (uint32_t i = 0; i < len; i++) c = tab[(c ^ buf[shift + i]) & 0xff] ^ (c >> 8);
-    r = c;  // register after the tiny message (n < 4 => single chunk)
-  } else {
-    r = wave_crc_raw(tab, buf, int32_t(shift), len, lane, k == 0);
-  }
-  if (lane == 0) partial[k] = r;
+struct CrcGeo {
+  const uint8_t* base;  // 16-byte line of the first byte
+  uint32_t sh;          // message byte 0 = base[sh]
+  uint64_t body;        // whole chunks
+};
+__device__ __forceinline__ CrcGeo crc_geo(const uint8_t* data, uint64_t n) {
+  CrcGeo g;
+  g.sh = uint32_t(reinterpret_cast<uintptr_t>(data) & 15);
+  g.base = data - g.sh;
+  g.body = (g.sh + n) / 16;
+  // the initial register is folded into message bytes 0..3: the body must hold them (else the
+  // whole message is the tail)
+  if (16 * g.body < g.sh + 4) g.body = 0;
+  return g;
 }
 
-// One wavefront: total = sum_k partial_k * x^(8 * bytes after chunk k), inverted.
-__global__ void crc_combine_kernel(const uint32_t* __restrict__ partial, uint64_t n, uint32_t* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  uint64_t nchunks = (n + kCrcStripe - 1) / kCrcStripe;
-  if (nchunks == 0) {
-    if (lane == 0) *out = 0;  // ChecksumIEEE of nothing
-    return;
+__global__ __launch_bounds__(kCrcThreads) void crc_stripes_kernel(const uint8_t* __restrict__ data, uint64_t n,
+                                                                  uint32_t* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  {
+    const uint32_t* src = &g_crc16.t[0][0];
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
+    load_adv_tables(tab + 4096);
+    __syncthreads();
   }
-  // Horner over full chunks 0..K-2 per lane (stride 64), then the tail shift.
-  const uint32_t x_stripe = g_crc_shift.stripe;  // x^(8*4096)
-  uint64_t full = nchunks - 1;
-  // lane l handles chunks l, l+64, ...: acc_l = sum partial_k x^(8*4096*(#own later chunks)*64)
-  uint32_t x64 = x_stripe;
-  for (int q = 0; q < 6; q++) x64 = gf2_mulmod(x64, x64);  // x^(8*4096*64)
-  uint32_t acc = 0;
-  uint64_t mine = 0;
-  for (uint64_t k = lane; k < full; k += 64) {
-    acc = gf2_mulmod(acc, x64) ^ partial[k];
-    mine++;
+  const uint8_t* lds = smem;
+  const uint32_t lane = threadIdx.x & 63;
+  const CrcGeo g = crc_geo(data, n);
+  const uint64_t stripes = (g.body + kCrcStripeChunks - 1) / kCrcStripeChunks;
+  const uint64_t waves = uint64_t(gridDim.x) * (kCrcThreads / 64);
+  for (uint64_t k = blockIdx.x * (kCrcThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < stripes;
+       k += waves) {
+    // the last stripe may be short: its chunks sit at the end of the 256 slots (zeros in front of
+    // a zero register change nothing)
+    const uint64_t c0 = k * kCrcStripeChunks;
+    const uint32_t nck = uint32_t(min<uint64_t>(kCrcStripeChunks, g.body - c0));
+    const uint32_t pad = kCrcStripeChunks - nck;
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(g.base + 16 * c0, 16 * uint64_t(nck));
+    v4u v[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
+      v[q] = __builtin_amdgcn_raw_buffer_load_b128(R, j >= 0 ? uint32_t(16 * j) : kOOB, 0, 2);
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
+      v4u c = v[q];
+      if (k == 0 && __builtin_amdgcn_ballot_w64(j >= 0 && j < 2)) {
+        // message bytes 0..3 take the initial register, the bytes before the message are zero:
+        // chunk-relative message start at -sh + 16 j
+        const int32_t m0 = 16 * j - int32_t(g.sh);  // message position of the chunk's byte 0
+        const bool in = j >= 0 && j < 2;
+        c.x = (in ? keep_mask(-m0, 16, 0) : ~0u) & c.x ^ (in ? keep_mask(-m0, 4 - m0, 0) : 0u);
+        c.y = (in ? keep_mask(-m0, 16, 1) : ~0u) & c.y ^ (in ? keep_mask(-m0, 4 - m0, 1) : 0u);
+        c.z = (in ? keep_mask(-m0, 16, 2) : ~0u) & c.z ^ (in ? keep_mask(-m0, 4 - m0, 2) : 0u);
+        c.w = (in ? keep_mask(-m0, 16, 3) : ~0u) & c.w ^ (in ? keep_mask(-m0, 4 - m0, 3) : 0u);
+      }
+      const uint32_t r = crc_chunk0(lds, c);
+      acc = (q == 0 ? 0u : adv_tab<5>(lds, acc)) ^ (j >= 0 ? r : 0u);
+    }
+    // lane l's chunks are followed by 63 - l chunks of their row: rows of 16 lanes by DPP, then
+    // the four row heads
+    acc = adv16(lds, acc) ^ row_shl<1>(acc);
+    acc = adv_tab<0>(lds, acc) ^ row_shl<2>(acc);
+    acc = adv_tab<1>(lds, acc) ^ row_shl<4>(acc);
+    acc = adv_tab<2>(lds, acc) ^ row_shl<8>(acc);
+    const uint32_t h1 = __builtin_amdgcn_readlane(acc, 16), h2 = __builtin_amdgcn_readlane(acc, 32),
+                   h3 = __builtin_amdgcn_readlane(acc, 48);
+    acc = adv_tab<3>(lds, acc) ^ h1;
+    acc = adv_tab<3>(lds, acc) ^ h2;
+    acc = adv_tab<3>(lds, acc) ^ h3;
+    if (lane == 0) partial[k] = acc;
   }
-  // chunk k = l + 64*j is followed by (full-1-k) full chunks; lanes differ by how
-  // many of their own chunks follow and by their position modulo 64.
-  uint64_t last_k = mine ? uint64_t(lane) + 64 * (mine - 1) : 0;
-  uint32_t v = 0;
-  if (mine) v = gf2_mulmod(acc, x8n(uint64_t(kCrcStripe) * (full - 1 - last_k)));
-  for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
+}
+
+// One wave: body = sum_k partial_k * x^(8 * bytes after stripe k), then the tail bytes (and the
+// whole message when it has no whole chunk), inverted.
+__global__ void crc_join_kernel(const uint8_t* __restrict__ data, uint64_t n, const uint32_t* __restrict__ partial,
+                                uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const CrcGeo g = crc_geo(data, n);
+  const uint64_t stripes = (g.body + kCrcStripeChunks - 1) / kCrcStripeChunks;
+  uint32_t body = 0;
+  if (stripes) {
+    // stripes 0 .. S-2 are whole; stripe S-1 has nl chunks: Horner per lane over k = l, l+64, ...
+    const uint64_t full = stripes - 1;
+    const uint32_t nl = uint32_t(g.body - full * kCrcStripeChunks);
+    const uint32_t x64 = x8n(uint64_t(16) * kCrcStripeChunks * 64);
+    uint32_t acc = 0;
+    uint64_t last = 0;
+    bool any = false;
+    for (uint64_t k = lane; k < full; k += 64) {
+      acc = gf2_mulmod(acc, x64) ^ partial[k];
+      last = k;
+      any = true;
+    }
+    // lane's last stripe is followed by (full - 1 - last) whole stripes and the short one
+    uint32_t v = any ? gf2_mulmod(acc, x8n(uint64_t(16) * kCrcStripeChunks * (full - 1 - last) + 16 * uint64_t(nl)))
+                     : 0u;
+    for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
+    body = v ^ partial[full];
+  }
   if (lane == 0) {
-    uint64_t tail = n - full * kCrcStripe;
-    uint32_t total = gf2_mulmod(v, x8n(tail)) ^ partial[full];
-    *out = ~total;
+    // tail: message bytes from 16 * body - sh on (all of them when there is no whole chunk, the
+    // initial register then folded here)
+    const uint64_t t0 = g.body ? 16 * g.body - g.sh : 0;
+    uint32_t c = g.body ? body : 0xFFFFFFFFu;
+    for (uint64_t i = t0; i < n; i++) c = g_crc16.t[0][(c ^ data[i]) & 0xff] ^ (c >> 8);
+    *out = ~c;
   }
 }
 
@@ -696,15 +757,22 @@ hipError_t launch_bloom_check(hipStream_t st, const uint8_t* keys, const uint64_
   return hipGetLastError();
 }
 
-size_t crc_scratch_bytes(uint64_t n) { return ((n + kCrcStripe - 1) / kCrcStripe + 1) * 4 + 16; }
+size_t crc_scratch_bytes(uint64_t n) { return ((n + 16) / (16 * kCrcStripeChunks) + 2) * 4 + 16; }
 
-hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out) {
-  uint64_t nchunks = (n + kCrcStripe - 1) / kCrcStripe;
-  if (nchunks) {
-    const size_t lds = kTabBytes + (kCrcThreads / 64) * size_t(kCrcStripe + 32);
-    crc_chunks_kernel<<<uint32_t((nchunks + 3) / 4), kCrcThreads, lds, st>>>(data, n, scratch);
+hipError_t launch_crc32(hipStream_t st, const uint8_t* data, uint64_t n, uint32_t* scratch, uint32_t* out,
+                        int num_cus) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&crc_stripes_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(kCrcLds));
+  if (attr != hipSuccess) return attr;
+  const uint64_t sh = reinterpret_cast<uintptr_t>(data) & 15;
+  const uint64_t body = (sh + n) / 16 * 16 >= sh + 4 ? (sh + n) / 16 : 0;
+  const uint64_t stripes = (body + kCrcStripeChunks - 1) / kCrcStripeChunks;
+  if (stripes) {
+    const uint64_t wgs = (stripes + kCrcThreads / 64 - 1) / (kCrcThreads / 64);
+    const uint32_t grid = uint32_t(std::min<uint64_t>(wgs, uint64_t(std::max(num_cus, 1)) * 2));
+    crc_stripes_kernel<<<grid, kCrcThreads, kCrcLds, st>>>(data, n, scratch);
   }
-  crc_combine_kernel<<<1, 64, 0, st>>>(scratch, n, out);
+  crc_join_kernel<<<1, 64, 0, st>>>(data, n, scratch, out);
   return hipGetLastError();
 }
 

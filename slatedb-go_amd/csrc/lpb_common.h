@@ -35,6 +35,105 @@ __device__ __forceinline__ uint32_t crc16_chunk(const uint32_t* tab, uint32_t c,
   return crc16_step(tab, c, v.x, v.y, v.z, v.w);
 }
 
+// CRC table lookups (decode_none.hip, decode_lpb2.hip).  A lookup's LDS address is (byte k of x) * 4 plus a table offset: one SDWA shift
+// (src1_sel picks the byte) instead of an extract and a shift, and the table offset rides in the
+// ds_read's immediate (the tables start at LDS address 0).
+template <int K>
+__device__ __forceinline__ uint32_t idx4(uint32_t x) {
+  uint32_t r;
+  if constexpr (K == 0)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
+  else if constexpr (K == 1)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
+  else if constexpr (K == 2)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(x));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(x));
+  return r;
+}
+// The lookup's LDS address is formed from the integer: through the extern __shared__ array's
+// symbol the compiler added its address (0) to every index with a v_add_u32 of its own.  The
+// kernels that use these tables declare no static LDS, so the dynamic array starts at address 0.
+typedef const __attribute__((address_space(3))) uint32_t lds_u32_t;
+template <uint32_t kOff>
+__device__ __forceinline__ uint32_t lut(const uint8_t* lds, uint32_t i4) {
+  (void)lds;
+  return *(lds_u32_t*)(kOff + i4);
+}
+// the four lookups of one dword against tables kT, kT - 1, kT - 2, kT - 3 (1 KiB each) at byte offset kBase
+template <uint32_t kBase, int kT>
+__device__ __forceinline__ void lut4(const uint8_t* lds, uint32_t x, uint32_t& a, uint32_t& b, uint32_t& c,
+                                     uint32_t& d) {
+  a = lut<kBase + 1024 * kT>(lds, idx4<0>(x));
+  b = lut<kBase + 1024 * (kT - 1)>(lds, idx4<1>(x));
+  c = lut<kBase + 1024 * (kT - 2)>(lds, idx4<2>(x));
+  d = lut<kBase + 1024 * (kT - 3)>(lds, idx4<3>(x));
+}
+// the raw CRC register of a 16-byte chunk from a zero register (slicing-by-16, crc16_step)
+__device__ __forceinline__ uint32_t crc_chunk0(const uint8_t* lds, const v4u& v) {
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, c2, c3, d0, d1, d2, d3;
+  lut4<0, 15>(lds, v.x, a0, a1, a2, a3);
+  lut4<0, 11>(lds, v.y, b0, b1, b2, b3);
+  lut4<0, 7>(lds, v.z, c0, c1, c2, c3);
+  lut4<0, 3>(lds, v.w, d0, d1, d2, d3);
+  return xor3(xor3(a0, a1, a2), xor3(a3, b0, b1), xor3(xor3(b2, b3, c0), xor3(c1, c2, c3), xor3(d0, d1, xor3(d2, d3, 0u))));
+}
+// CRC register advance over zero bytes (decode_none.hip, encode.hip): tables in LDS after the
+// slicing-by-16 tables, kAdvN x 4 KiB; table s advances by 32 << s bytes.
+constexpr uint32_t kAdvN = 6;  // zero-byte advance tables for 32, 64, ..., 1024 bytes
+// x^(8N) mod P for N = 32 << s: multiplying a raw CRC register by it advances the register over
+// N zero bytes (zlib's crc32_combine arithmetic)
+struct AdvConsts {
+  uint32_t k[kAdvN];
+  constexpr AdvConsts() : k{} {
+    for (uint32_t s = 0; s < kAdvN; s++) k[s] = x8n(uint64_t(32) << s);
+  }
+};
+static __constant__ AdvConsts g_adv = AdvConsts();
+
+// register advanced over N zero bytes by four lookups: table s (N = 32 << s), t[j][i] = (i << 8j) * x^(8N)
+template <int kS>
+__device__ __forceinline__ uint32_t adv_tab(const uint8_t* lds, uint32_t c) {
+  constexpr uint32_t o = kTab16Bytes + 4096 * kS;
+  return xor3(lut<o>(lds, idx4<0>(c)), lut<o + 1024>(lds, idx4<1>(c)), lut<o + 2048>(lds, idx4<2>(c))) ^
+         lut<o + 3072>(lds, idx4<3>(c));
+}
+// over 16 zero bytes: rows 12..15 of the slicing-by-16 tables (a chunk of zeros after c)
+__device__ __forceinline__ uint32_t adv16(const uint8_t* lds, uint32_t c) {
+  uint32_t a, b, d, e;
+  lut4<0, 15>(lds, c, a, b, d, e);
+  return xor3(a, b, d) ^ e;
+}
+template <int kShift>
+__device__ __forceinline__ uint32_t row_shl(uint32_t v) {  // lane i <- lane i + kShift of its row of 16
+  return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x100 + kShift, 0xf, 0xf, true));
+}
+// over t < 16 zero bytes: byte i < t of c is looked up after i steps and then carried over
+// t - 1 - i more zero bytes (slicing row t - 1 - i); the bytes from t on only shift down
+__device__ __forceinline__ uint32_t adv_small(const uint32_t* tab, uint32_t c, uint32_t t) {
+  uint32_t r = t >= 4 ? 0u : c >> (8 * t);
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) {
+    const uint32_t v = tab[((t - 1 - i) & 15) * 256 + ((c >> (8 * i)) & 0xff)];
+    r ^= i < t ? v : 0u;
+  }
+  return r;
+}
+
+// LDS table of the advance tables: entry i of table s = ((i & 255) << 8 * ((i >> 8) & 3)) * x^(8 * (32 << s))
+__device__ __forceinline__ void load_adv_tables(uint32_t* adv) {
+  for (uint32_t i = threadIdx.x; i < kAdvN * 1024; i += blockDim.x)
+    adv[i] = gf2_mulmod((i & 255u) << (8 * ((i >> 8) & 3u)), g_adv.k[i >> 10]);
+}
+
+// c ? a : b as one v_cndmask_b32 on the lane mask of c: the compiler turned groups of selects
+// on one condition into divergent branches (exec-mask save/restore around both arms)
+__device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(__builtin_amdgcn_ballot_w64(c)));
+  return r;
+}
+
 // Rings and natural alignment.  gfx950 executes ds_read/ds_write of 8 or 16 bytes at any
 // byte address, but an access that is not naturally aligned is serialised lane by lane:
 // ~64 CU-cycles per wave-instruction against 2-9 aligned, for b32, b64 and b128 alike

@@ -393,6 +393,22 @@ __global__ __launch_bounds__(256) void rows_valid_kernel(const uint64_t* row_bas
   valid[r] = v ? 1u : 0u;
 }
 
+// Go's block.Iterator stops at the first row that fails to decode (block/iterator.go:92-96): the
+// rows after it are not returned either.  Does work only when rows_valid_kernel found a failure.
+__global__ __launch_bounds__(256) void rows_cut_kernel(const uint64_t* row_base, uint32_t n_blocks,
+                                                       const slate_block_meta* meta, const slate_row* rows,
+                                                       uint32_t* valid, const uint32_t* flags) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= n_blocks || !(*flags & 2u)) return;
+  const uint64_t r0 = row_base[b], cap = row_base[b + 1] - r0;
+  const uint64_t n = min<uint64_t>(meta[b].n_rows, cap);  // a failed block has no valid rows already
+  bool cut = false;
+  for (uint64_t j = 0; j < n; j++) {
+    cut = cut || rows[r0 + j].status != SLATE_OK;
+    if (cut) valid[r0 + j] = 0;
+  }
+}
+
 // compacted row i -> its slot; lengths of row i (slots past the row count give zero lengths)
 __global__ __launch_bounds__(256) void rows_slot_kernel(const uint32_t* valid, const uint64_t* pos, uint64_t n_slots,
                                                         uint32_t* slot) {
@@ -491,8 +507,11 @@ hipError_t launch_rows_lengths(hipStream_t st, const uint64_t* row_base, uint32_
   hipError_t e = hipMemsetAsync(flags, 0, 4, st);
   if (e != hipSuccess) return e;
   const dim3 g(uint32_t((n_slots + 255) / 256));
-  if (n_slots)
+  if (n_slots) {
     hipLaunchKernelGGL(rows_valid_kernel, g, dim3(256), 0, st, row_base, n_blocks, meta, rows, n_slots, valid, flags);
+    hipLaunchKernelGGL(rows_cut_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, row_base, n_blocks, meta, rows,
+                       valid, flags);
+  }
   e = scan_u32_to_u64(st, valid, n_slots, pos, tiles);
   if (e != hipSuccess) return e;
   e = hipMemcpyAsync(n_kv, pos + n_slots, 8, hipMemcpyDeviceToDevice, st);

@@ -24,6 +24,8 @@ E_NO_DEVICE = 100
 E_CAPACITY = 103
 E_INVALID_ARG = 102
 E_MERGE_UNSORTED = 105
+E_LIMIT = 106
+E_WARNINGS = 107
 
 u8p = C.POINTER(C.c_uint8)
 u16p = C.POINTER(C.c_uint16)
@@ -100,6 +102,9 @@ _SIGS = {
     "slate_devbuf_download_async": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint64]),
     "slate_compact": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.c_uint32, C.POINTER(SstConfig), C.c_uint64, vp,
                                 C.c_uint32, C.POINTER(C.c_uint32)]),
+    "slate_crc32_device": (C.c_int, [vp, vp, C.c_size_t, C.POINTER(C.c_uint32)]),
+    "slate_compact_ex": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.c_uint32, C.POINTER(SstConfig), C.c_uint64, vp,
+                                   C.c_uint32, C.POINTER(C.c_uint32), vp, C.c_uint32, C.POINTER(C.c_uint32)]),
     "slate_block_seek_warn_device": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, C.c_uint64, vp, vp, C.c_uint32]),
     "slate_block_seek_warn": (C.c_int, [vp, vp, vp, vp, C.c_uint32, vp, vp, vp, C.c_uint64, vp, vp, C.c_uint32]),
     "slate_shard_pack": (C.c_int, [vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint64, vp]),
@@ -517,6 +522,39 @@ class HostBuf:
             self.free()
         except (TypeError, AttributeError):
             pass
+
+
+# slate_compact_warning (include/slatecodec.h): one types.ErrWarn entry of a compaction
+COMPACT_WARN_DTYPE = np.dtype([("src", "<u4"), ("sst", "<u4"), ("block", "<u4"), ("row", "<i4"), ("status", "<i4"),
+                               ("block_len", "<u4")])
+
+
+def compact_ex(ctx: "Context", sources: list[list[bytes]], max_sst_size: int, block_size: int = 4096,
+               min_filter_keys: int = 0, filter_bits_per_key: int = 10, codec: int = NONE):
+    """slate_compact_ex -> (encoded output SSTs, warning records in ErrWarn order): corrupt input
+    blocks / rows end their SST / block iterators as Go's do and the compaction goes on."""
+    flat = [s for run in sources for s in run]
+    blob = np.frombuffer(b"".join(flat) or b"\0", np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(s) for s in flat])]).astype(np.uint64)
+    src = np.concatenate([[0], np.cumsum([len(r) for r in sources])]).astype(np.uint32)
+    cfg = SstConfig(block_size, min_filter_keys, filter_bits_per_key, codec)
+    cap, wcap = 16, 16
+    while True:
+        tabs = (C.c_void_p * cap)()
+        warns = np.zeros(wcap, COMPACT_WARN_DTYPE)
+        n, nw = C.c_uint32(), C.c_uint32()
+        st = lib().slate_compact_ex(ctx.handle, _ptr(blob), _ptr(off), len(flat), _ptr(src), len(sources),
+                                    C.byref(cfg), max_sst_size, tabs, cap, C.byref(n), _ptr(warns), wcap, C.byref(nw))
+        if st == E_CAPACITY and n.value > cap:
+            cap = n.value
+            continue
+        if st not in (0, E_WARNINGS):
+            _check(st, "slate_compact_ex")
+        out = [SstTable(tabs[k]).encode() for k in range(n.value)]
+        if nw.value > wcap:  # more warnings than records: run again with room for all of them
+            wcap = nw.value
+            continue
+        return out, warns[:nw.value]
 
 
 def compact(ctx: "Context", sources: list[list[bytes]], max_sst_size: int, block_size: int = 4096,

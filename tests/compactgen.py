@@ -44,11 +44,70 @@ def sst_rows(sst: bytes) -> list[tuple[bytes, bytes | None]]:
     return out
 
 
-def oracle_compact(sources: list[list[bytes]], max_sst_size: int, codec: int = ob.NONE,
-                   block_size: int = 4096) -> list[bytes]:
-    iters = [[kv for sst in run for kv in sst_rows(sst)] for run in sources]
+def sst_rows_go(sst: bytes):
+    """sstable.Iterator over one SST with Go's behaviour on corrupt input (oracle): a block that fails
+    block.Decode ends the SST (iterator.go:59-68), a row that fails v0RowCodec.Decode ends its block
+    (block/iterator.go:92-96).  -> (rows, warnings): warning = (block, row or -1, status, block_len,
+    rows returned before it)."""
+    st, info = ob.sst_read_info(sst)
+    assert st == 0, st
+    codec = info["codec"]
+    st, metas = ob.decode_index(sst[info["index_offset"]:info["index_offset"] + info["index_len"]], codec)
+    assert st == 0, st
+    offs = [o for o, _ in metas] + [info["filter_offset"]]
+    out, warns = [], []
+    for bi, (a, b) in enumerate(zip(offs, offs[1:])):
+        m, data, rows = ob.block_decode(sst[a:b], codec)
+        if m["status"] != 0:
+            warns.append((bi, -1, int(m["status"]), b - a, len(out)))
+            break
+        fk = b""
+        for i, r in enumerate(rows):
+            if int(r["status"]) != 0:
+                warns.append((bi, i, int(r["status"]), b - a, len(out)))
+                break
+            o, sl = int(r["row_off"]), int(r["key_suffix_len"])
+            sfx = data[o + 4:o + 4 + sl]
+            key = sfx if i == 0 else fk[:int(r["key_prefix_len"])] + sfx
+            if i == 0:
+                fk = key
+            if r["flags"] & 1:
+                out.append((key, None))
+            else:
+                vs = o + 4 + sl + int(r["meta_len"])
+                out.append((key, data[vs:vs + int(r["value_len"])]))
+    return out, warns
+
+
+def oracle_compact_go(sources: list[list[bytes]], max_sst_size: int, codec: int = ob.NONE, block_size: int = 4096):
+    """executeCompaction with corrupt inputs (oracle): the rows Go's iterators still return, merged and
+    written as oracle_compact does, and the warnings in the order types.ErrWarn receives them --
+    NewMergeSort merges each source's warnings up to its first row, a source's remaining ones when
+    it ends, sources ending in (last key, source) order (merge.go:33-63).
+    -> (outputs, [(src, sst, block, row, status, block_len)])."""
+    iters, early, late, last = [], [], {}, []
+    k = 0
+    for j, run in enumerate(sources):
+        rows = []
+        for sst in run:
+            r, w = sst_rows_go(sst)
+            for (blk, row, status, blen, before) in w:
+                rec = (j, k, blk, row, status, blen)
+                (early if len(rows) + before == 0 else late.setdefault(j, [])).append(rec)
+            rows += r
+            k += 1
+        iters.append(rows)
+        if rows:
+            last.append((rows[-1][0], j))
+    warns = list(early)
+    for _, j in sorted(last):
+        warns += late.get(j, [])
     flat = [kv for it in iters for kv in it]
-    merged = [flat[i] for i in ob.merge_sort([[k for k, _ in it] for it in iters])]
+    merged = [flat[i] for i in ob.merge_sort([[key for key, _ in it] for it in iters])]
+    return _write_outputs(merged, max_sst_size, codec, block_size), warns
+
+
+def _write_outputs(merged, max_sst_size, codec, block_size):
     out, size = [], 0
     w = ob.SstBuilder(block_size, 0, 10, codec)
     for k, v in merged:
@@ -63,6 +122,14 @@ def oracle_compact(sources: list[list[bytes]], max_sst_size: int, codec: int = o
         assert w.build() == 0
         out.append(w.encode_table())
     return out
+
+
+def oracle_compact(sources: list[list[bytes]], max_sst_size: int, codec: int = ob.NONE,
+                   block_size: int = 4096) -> list[bytes]:
+    iters = [[kv for sst in run for kv in sst_rows(sst)] for run in sources]
+    flat = [kv for it in iters for kv in it]
+    merged = [flat[i] for i in ob.merge_sort([[k for k, _ in it] for it in iters])]
+    return _write_outputs(merged, max_sst_size, codec, block_size)
 
 
 def random_sources(rng: random.Random, n_sources: int, n_keys: int, space: int, codec: int = ob.NONE,

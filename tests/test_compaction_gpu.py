@@ -121,3 +121,52 @@ def test_compaction_empty_and_capacity(ctx):
     got = compaction.compact(ctx, srcs, 2_000)  # > 16 outputs: the first call reports the count
     want = cg.oracle_compact(srcs, 2_000)
     assert len(want) > 16 and got == want
+
+
+def _corrupt_row(sst: bytes, block: int, row: int, field: int = 0) -> bytes:
+    """CodecNone SST: row `row` of data block `block` gets a key prefix longer than the block's first
+    key (field 0, row.go:203-206) or a key suffix longer than the block (field 2, :208-211): a corrupt
+    v0 row; the block's CRC32 re-sealed."""
+    import struct
+    import zlib
+    st, info = ob.sst_read_info(sst)
+    assert info["codec"] == ob.NONE
+    st, metas = ob.decode_index(sst[info["index_offset"]:info["index_offset"] + info["index_len"]], info["codec"])
+    offs = [o for o, _ in metas] + [info["filter_offset"]]
+    a, b = offs[block], offs[block + 1]
+    m, data, rows = ob.block_decode(sst[a:b], ob.NONE)
+    body = bytearray(sst[a:b - 4])
+    o = int(rows[row]["row_off"])
+    body[o + field:o + field + 2] = b"\xff\xff"
+    return sst[:a] + bytes(body) + struct.pack(">I", zlib.crc32(bytes(body))) + sst[b:]
+
+
+@pytest.mark.parametrize("case", ["block", "row", "both", "first_row", "run"])
+def test_compaction_corrupt_inputs_warn(ctx, case):
+    """Corrupt inputs end iterators as Go's do and the compaction goes on (sstable.Iterator,
+    block.Iterator, iter.MergeSort, executeCompaction returning warn.If()): the output SSTs are
+    built from the rows Go still returns, and slate_compact_ex reports one warning record per
+    ErrWarn entry, in Go's order -- against the oracle restated with the same iterator rules."""
+    import slatecodec as sc
+    rng = random.Random(41)
+    srcs = cg.random_sources(rng, 3, 900, 2000, run_ssts=2 if case == "run" else 1)
+    if case in ("block", "both"):
+        srcs[1][0] = _corrupt_first_block(srcs[1][0], b"\x00")  # CodecNone: 1 byte "block": too small
+    if case in ("row", "both"):
+        srcs[2][0] = _corrupt_row(srcs[2][0], 1, 5)
+    if case == "first_row":  # before source 0's first row (merged when the merge starts), then source 1's
+        srcs[0][0] = _corrupt_row(srcs[0][0], 0, 0, field=2)
+        srcs[1][0] = _corrupt_row(srcs[1][0], 2, 7)
+    if case == "run":  # the second SST of source 0's run: its first block, then a row of source 2
+        srcs[0][1] = _corrupt_first_block(srcs[0][1], b"\x00")
+        srcs[2][1] = _corrupt_row(srcs[2][1], 2, 3)
+    got, warns = sc.compact_ex(ctx, srcs, 30_000)
+    want, want_w = cg.oracle_compact_go(srcs, 30_000)
+    assert len(want_w) >= 1
+    assert [tuple(int(x) for x in w) for w in warns] == [tuple(w) for w in want_w]
+    assert len(got) == len(want) and all(g == w for g, w in zip(got, want))
+    # slate_compact: the first warning's status, no outputs (startCompaction drops the sorted run)
+    from slatecodec import SlateError
+    with pytest.raises(SlateError) as e:
+        sc.compact(ctx, srcs, 30_000)
+    assert e.value.status == want_w[0][4]

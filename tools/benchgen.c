@@ -2,6 +2,7 @@
  * blocks with the C++ snappy library or liblz4's frame API in /opt/conda (dlopen)
  * and append the block CRC32 trailer (block.go:54-75 layout), in parallel.  Used
  * only to synthesise encoded blocks for bench.py's and tools/ablate.py's workloads. */
+#define _GNU_SOURCE 1 /* RTLD_DEEPBIND */
 #include <dlfcn.h>
 #include <pthread.h>
 #include <stddef.h>
@@ -26,7 +27,7 @@ static lz4f_err_fn g_lz4f_err;
 
 /* pierrec/lz4 v4 writer defaults: 4 MiB max blocks, independent blocks, content checksum */
 int bg_init_lz4(const char* liblz4) {
-  void* h = dlopen(liblz4, RTLD_NOW);
+  void* h = dlopen(liblz4, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
   if (!h) return -1;
   g_lz4f = (lz4f_fn)dlsym(h, "LZ4F_compressFrame");
   g_lz4f_err = (lz4f_err_fn)dlsym(h, "LZ4F_isError");
@@ -44,7 +45,7 @@ static zsetp_fn g_zsetp;
 static zc2_fn g_zc2;
 static zerr_fn g_zerr;
 int bg_init_zstd(const char* libzstd) {
-  void* h = dlopen(libzstd, RTLD_NOW);
+  void* h = dlopen(libzstd, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
   if (!h) return -1;
   g_zcreate = (zcreate_fn)dlsym(h, "ZSTD_createCCtx");
   g_zfree = (zfree_fn)dlsym(h, "ZSTD_freeCCtx");
@@ -67,7 +68,7 @@ int bg_init(const char* libsnappy) {
     for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
     g_tab[i] = c;
   }
-  void* h = dlopen(libsnappy, RTLD_NOW);
+  void* h = dlopen(libsnappy, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
   if (!h) return -1;
   g_compress = (compress_fn)dlsym(h, "snappy_compress");
   return g_compress ? 0 : -2;

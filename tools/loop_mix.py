@@ -1,6 +1,6 @@
 """Static instruction mix of the lane-per-block decode loop (tooling): compiles
-decode_lpb2.hip with SLATE_FORCE_DBG=<mask> (ablation bits folded at compile time)
-and reports VALU/SALU/DS/VMEM counts of the main step loop (4 steps)."""
+decode_lpb2.hip with SLATE_FORCE_DBG=<mask> (ablation bits folded at compile time) and the
+walker's general phases compiled out (SLATE_COUNT_FAST_ONLY: the bench's rows never take them), and reports VALU/SALU/DS/VMEM counts of the main step loop (4 steps)."""
 import collections
 import os
 import re
@@ -14,7 +14,7 @@ SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 
 def mix(dbg):
     with tempfile.TemporaryDirectory() as d:
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-S", "--cuda-device-only",
-               f"-DSLATE_FORCE_DBG={dbg}", SRC, "-o", os.path.join(d, "k.s")]
+               f"-DSLATE_FORCE_DBG={dbg}", "-DSLATE_COUNT_FAST_ONLY", SRC, "-o", os.path.join(d, "k.s")]
         subprocess.run(cmd, check=True, capture_output=True)
         text = open(os.path.join(d, "k.s")).read()
     start = text.index("_ZN5slate18decode_lpb2_kernelILb0E")
