@@ -240,8 +240,9 @@ def main():
     if rank == 0 and world == 1:
         # the kernel's rate against a device-to-device copy measured on this box too
         copy = measured_copy_gbps(device)
-        roofline["measured_copy_GBps"] = round(copy, 1)
-        roofline["frac_of_measured_copy"] = round(roofline["achieved"] / copy, 4)
+        roofline["measured_copy_GBps"] = copy["value"]
+        roofline["measured_copy"] = copy
+        roofline["frac_of_measured_copy"] = round(roofline["achieved"] / copy["value"], 4)
 
     if rank == 0 and world == 1 and not args.no_host_io and shard is not None:
         result["host_io"] = host_io_rate(sc, ctx, codec, blob, in_off)
@@ -251,6 +252,12 @@ def main():
         result["codec_none"] = codec_none_leg(sc, ctx, stream, wl, args, threads)
         result["configs4_zstd"] = zstd_leg(sc, ctx, stream, wl, args, threads)
         result["configs2_encode"] = encode_leg(sc, ctx, args)
+        # the unchanged per-block reader path (one GPU round trip per 4 KiB block) and BASELINE
+        # configs[0] (one 64-block CodecNone SST encoded + decoded), next to the oracle on one thread
+        from oracle import binding as ob
+        from tools import percall_bench as pb
+        result["per_call"] = pb.per_call(ctx, sc, ob, wl, 300)
+        result["configs0"] = pb.configs0(ctx, sc, ob)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(codec, blob, in_off, args.cpu_seconds)
@@ -413,6 +420,10 @@ def zstd_leg(sc, ctx, stream, wl, args, threads):
     used = np.concatenate([np.arange(int(o_rb[i]), int(o_rb[i]) + int(o_meta["n_rows"][i])) for i in range(m)])
     assert rows[used].tobytes() == o_rows[used].tobytes(), "configs4 rows differ from the oracle"
     res["oracle_checked_blocks"] = m
+    res["roofline"]["traffic"], res["roofline"]["traffic_source"] = pmc_traffic(
+        os.path.join(REPO, "profiles", "pmc_decode_zstd_latest.json"), n, "zstd")
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(sc.ZSTD, blob, in_off, args.cpu_seconds / 2)
     res["gen_seconds"] = round(gen_s, 1)
     res["workload"] = f"configs[4] mixed: {n} x 4 KiB Zstd blocks, 1 KiB values, skewed key prefixes"
     leg.free()
@@ -466,6 +477,8 @@ def encode_leg(sc, ctx, args):
         assert o.build() == 0
         ref = o.encode_table()
         oracle_s = time.perf_counter() - t0
+        oracle_mt = oracle_threads_encode(ob, keys, key_off, vals, val_off,
+                                          ob.NONE if codec == sc.NONE else ob.SNAPPY, host_cpus())
         exact = ref == enc.tobytes() and ref == host.tobytes()
         assert exact, f"configs[2] {name}: SST bytes differ from the oracle"
         s_dev = float(np.median(times))
@@ -481,30 +494,77 @@ def encode_leg(sc, ctx, args):
                                           "streams, slate_ctx_gpu_time; the filter's side stream overlaps the flush)",
                                   "wall_frac": round(alg / s_dev / 1e9 / HBM_PEAK_GBPS, 5)},
                      "cpu_baseline": {"value": round(n / oracle_s, 1), "unit": "KV/s", "cores": 1, "kind": "port",
-                                      "sample": "the same 10 M KV through oracle/slate_oracle.c's sstable.Builder"}}
+                                      "sample": "the same 10 M KV through oracle/slate_oracle.c's sstable.Builder",
+                                      "n_threads": oracle_mt}}
     for x in (d_keys, d_vals, d_ko, d_vo):
         x.free()
     res["workload"] = "configs[2]: 10 M x 100 B KV (keys k%015d, V-half values) -> SST blocks + bloom, BlockSize 4096"
     return res
 
 
-def measured_copy_gbps(device, nbytes: int = 2 << 30, reps: int = 10) -> float:
-    """Read + write bytes per second of a large device-to-device copy (torch copy_, the same
-    stream as the decode), outside the timed region."""
+def oracle_threads_encode(ob, keys, key_off, vals, val_off, codec, threads):
+    """The oracle's sstable.Builder on every CPU this process may use: the 10 M KV cut into one
+    contiguous slice per thread, each slice its own SST (the reference builds one SST per flush /
+    compaction output serially: independent builders are how N cores serve N SSTs)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(key_off) - 1
+    bounds = [n * t // threads for t in range(threads + 1)]
+
+    def one(t):
+        a, b = bounds[t], bounds[t + 1]
+        ko = (key_off[a:b + 1] - key_off[a]).astype(np.uint64)
+        vo = (val_off[a:b + 1] - val_off[a]).astype(np.uint64)
+        o = ob.SstBuilder(4096, 0, 10, codec)
+        assert o.add_batch(keys[int(key_off[a]):int(key_off[b])], ko, vals[int(val_off[a]):int(val_off[b])], vo) == 0
+        assert o.build() == 0
+        return len(o.encode_table())
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, range(threads)))
+    s = time.perf_counter() - t0
+    return {"value": round(n / s, 1), "unit": "KV/s", "cores": threads,
+            "sample": f"the same 10 M KV as {threads} SSTs of contiguous slices, one oracle builder per thread"}
+
+
+def measured_copy_gbps(device, nbytes: int = 2 << 30, reps: int = 10) -> dict:
+    """Read + write bytes per second of a large device-to-device copy, outside the timed region:
+    a hand-written streaming copy kernel (tools/copy_kernel.hip: 16 B per lane, nontemporal, four
+    loads in flight per lane; the best of 4 / 8 / 16 workgroups per CU) and torch's copy_."""
+    import ctypes
     import torch
     a = torch.empty(nbytes, dtype=torch.uint8, device=device)
     b = torch.empty_like(a)
     a.fill_(1)
-    b.copy_(a)
+    stream = torch.cuda.current_stream(device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record()
-    for _ in range(reps):
-        b.copy_(a)
-    ev[1].record()
-    ev[1].synchronize()
-    ms = ev[0].elapsed_time(ev[1]) / reps
+
+    def timed(fn):
+        fn()
+        ev[0].record(stream)
+        for _ in range(reps):
+            fn()
+        ev[1].record(stream)
+        ev[1].synchronize()
+        return 2 * nbytes / (ev[0].elapsed_time(ev[1]) / reps * 1e-3) / 1e9
+
+    res = {"torch_copy_GBps": round(timed(lambda: b.copy_(a)), 1)}
+    so = os.path.join(REPO, "tools", "build", "libcopykernel.so")
+    if os.path.exists(so):
+        lib = ctypes.CDLL(so)
+        lib.slate_probe_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                ctypes.c_int, ctypes.c_int]
+        cus = torch.cuda.get_device_properties(device).multi_processor_count
+        best = 0.0
+        for g in (4, 8, 16):
+            rate = timed(lambda: lib.slate_probe_stream_copy(a.data_ptr(), b.data_ptr(), nbytes, stream.cuda_stream,
+                                                             cus, g))
+            best = max(best, rate)
+        assert torch.equal(a[:4096], b[:4096]) and torch.equal(a[-4096:], b[-4096:]), "copy kernel"
+        res["stream_copy_GBps"] = round(best, 1)
     del a, b
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    res["value"] = res.get("stream_copy_GBps", res["torch_copy_GBps"])
+    return res
 
 
 def pmc_traffic(path: str, n: int, codec: str):
@@ -600,6 +660,24 @@ def host_io_rate(sc, ctx, codec, blob, in_off, max_blocks=262144):
         assert st == sc.OK and (meta["status"] == 0).all()
     res["sharded_8ctx_GiBps_decoded"] = round(dec / el / 2**30, 2)
     res["sharded_8ctx_copy_threads"] = max(1, cpus // 8)
+    # the same calls with page-locked outputs (slate_hostbuf): the GPU writes decoded bytes and rows
+    # straight into the caller's buffers, so no staging copy and no host memcpy of the output
+    hb_o, hb_r = sc.HostBuf(ctx2, out.nbytes), sc.HostBuf(ctx2, rows.nbytes)
+    out_h, rows_h = hb_o.view[: out.nbytes], hb_r.view[: rows.nbytes].view(sc.ROW_DTYPE)
+    for name, cs in (("pinned_out_1ctx_GiBps_decoded", None), ("pinned_out_sharded_8ctx_GiBps_decoded", ctxs)):
+        for _ in range(2):
+            t = time.perf_counter()
+            if cs is None:
+                st = ctx2.decode_batch_into(codec, sub, sub_off, out_h, rows_h, meta, out_off, row_base)
+            else:
+                st = sc.decode_sharded_into(cs, codec, sub, sub_off, out_h, rows_h, meta, out_off, row_base)
+            el = time.perf_counter() - t
+            assert st == sc.OK and (meta["status"] == 0).all()
+        res[name] = round(dec / el / 2**30, 2)
+    assert out_h[: int(out_off[n])].tobytes() == out[: int(out_off[n])].tobytes(), "pinned output bytes"
+    out_h = rows_h = None
+    hb_o.free()
+    hb_r.free()
     for c in ctxs:
         c.close()
     ctx2.close()

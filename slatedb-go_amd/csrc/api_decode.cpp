@@ -106,7 +106,10 @@ slate_ctx* slate_ctx_create(int device, int* status) {
   ctx->stream = ctx->own;
   if (const char* e = getenv("SLATE_COPY_THREADS")) {
     const unsigned long v = strtoul(e, nullptr, 0);
-    if (v >= 1 && v <= 256) ctx->copy_threads = v;
+    if (v >= 1 && v <= 256) {
+      ctx->copy_threads = v;
+      ctx->copy_threads_set = true;
+    }
   }
   *status = SLATE_OK;
   return ctx;
@@ -115,6 +118,7 @@ slate_ctx* slate_ctx_create(int device, int* status) {
 int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads) {
   if (!ctx || threads == 0 || threads > 256) return SLATE_E_INVALID_ARG;
   ctx->copy_threads = threads;
+  ctx->copy_threads_set = true;
   ctx->copy_pool.reset();  // joins the old workers; the next large copy starts the new count
   return SLATE_OK;
 }

@@ -19,12 +19,20 @@
 using namespace slate;
 
 thread_local CopyPool* t_pool = nullptr;
+// at most this many copy tasks per copy on this thread (0: the pool's size): a sharded call's
+// contexts share the host's cores unless their counts were set explicitly
+thread_local size_t t_pool_cap = 0;
+
+static size_t pool_threads() {
+  const size_t n = t_pool ? t_pool->size() : 1;
+  return t_pool_cap ? std::min(n, t_pool_cap) : n;
+}
 
 // memcpy split over the calling context's copy threads for large copies between caller memory
 // and page-locked staging (one core copies ~10 GB/s, below what the PCIe link moves).
 void par_memcpy(void* dst, const void* src, size_t n) {
   constexpr size_t kPiece = 4u << 20;
-  const size_t threads = t_pool ? t_pool->size() : 1;
+  const size_t threads = pool_threads();
   if (n < 2 * kPiece || threads == 1) {
     if (n) memcpy(dst, src, n);
     return;
@@ -126,7 +134,45 @@ struct Sink {
   uint32_t G = 0, g = 0;
   const uint64_t* g_out_off = nullptr;
   const uint64_t* g_row_base = nullptr;
+  // device addresses of out / rows when both are page-locked (slate_hostbuf, hipHostMalloc or
+  // hipHostRegister'ed) and 16-byte aligned: decoded chunks are then written there by the GPU
+  // (blocks_to_host_kernel) instead of going through staging and a host copy
+  uint8_t* out_dev = nullptr;
+  slate_row* rows_dev = nullptr;
 };
+
+// The device address of page-locked host memory, null for pageable memory.
+void* mapped_ptr(void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost) return nullptr;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
+// Sets the sink's direct path when the caller's out and rows arrays are page-locked and aligned
+// (SLATE_HOST_DIRECT=0 turns it off: A/B runs).
+void sink_map(Sink& o) {
+  static const bool off = [] {
+    const char* e = getenv("SLATE_HOST_DIRECT");
+    return e && *e == '0';
+  }();
+  if (off || !o.out || !o.rows || (reinterpret_cast<uintptr_t>(o.out) & 15)) return;
+  void* od = mapped_ptr(o.out);
+  void* rd = od ? mapped_ptr(o.rows) : nullptr;
+  if (od && rd) {
+    o.out_dev = static_cast<uint8_t*>(od);
+    o.rows_dev = static_cast<slate_row*>(rd);
+  }
+}
 
 
 // plan_sizes_kernel's decoded length for CodecNone / CodecSnappy on the host (decode.hip
@@ -157,7 +203,7 @@ uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len) {
 // Run fn(lo, hi) over [0, n) split across the calling context's copy threads (pieces of >= grain).
 template <typename F>
 void par_for(size_t n, size_t grain, F fn) {
-  const size_t threads = t_pool ? t_pool->size() : 1;
+  const size_t threads = pool_threads();
   const size_t t = std::max<size_t>(1, std::min<size_t>(threads, n / std::max<size_t>(grain, 1)));
   if (t == 1) {
     fn(size_t(0), n);
@@ -179,6 +225,15 @@ int lane_finish(PipeLane& L, Sink& o) {
   SLATE_HIP(hipEventSynchronize(L.done));
   if (host_trace()) fprintf(stderr, "[slate host]   wait decode+D2H %.2f ms\n", now_ms() - t0);
   if (!L.decoded) return SLATE_OK;
+  if (L.direct) {  // bytes and rows are in place: the metas only
+    const slate_block_meta* hm = L.h_meta.as<slate_block_meta>();
+    if (o.G) {
+      for (uint32_t k = 0; k < L.n; k++) o.meta[uint64_t(o.g) + uint64_t(L.b0 + k) * o.G] = hm[k];
+    } else {
+      memcpy(o.meta + L.b0, hm, size_t(L.n) * sizeof(slate_block_meta));
+    }
+    return SLATE_OK;
+  }
   const uint8_t* hout = L.h_out.as<uint8_t>();
   const slate_row* hrows = L.h_rows.as<slate_row>();
   const slate_block_meta* hmeta = L.h_meta.as<slate_block_meta>();
@@ -363,6 +418,38 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
                    L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
                    L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
       SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
+      L.direct = o.out_dev != nullptr;
+      if (L.direct) {
+        // page-locked caller buffers: the GPU writes the chunk's bytes and rows in place
+        const uint64_t* gout = nullptr;
+        const uint64_t* grow = nullptr;
+        if (o.G) {  // sharded: each block's place in the whole batch's layout
+          SLATE_HIP(L.h_gmap.ensure(2 * size_t(m) * 8));
+          SLATE_HIP(L.d_gmap.ensure(2 * size_t(m) * 8));
+          uint64_t* hg = L.h_gmap.as<uint64_t>();
+          for (uint32_t k = 0; k < m; k++) {
+            const uint64_t i = uint64_t(o.g) + uint64_t(b + k) * o.G;
+            hg[k] = o.g_out_off[i];
+            hg[m + k] = o.g_row_base[i];
+          }
+          SLATE_HIP(hipMemcpyAsync(L.d_gmap.p, hg, 2 * size_t(m) * 8, hipMemcpyHostToDevice, s));
+          gout = L.d_gmap.as<uint64_t>();
+          grow = gout + m;
+        }
+        SLATE_HIP(launch_blocks_to_host(s, L.d_out.as<uint8_t>(), L.d_out_off.as<uint64_t>(),
+                                        L.d_row_base.as<uint64_t>(), L.d_meta.as<slate_block_meta>(),
+                                        L.d_rows.as<slate_row>(), m, o.out_dev, o.rows_dev, gout, grow, L.out_base,
+                                        L.row_base));
+        SLATE_HIP(hipMemcpyAsync(L.h_meta.p, L.d_meta.p, size_t(m) * sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
+        L.decoded = true;
+        SLATE_HIP(hipEventRecord(L.done, s));
+        if (&prev != &L) {
+          st = lane_finish(prev, o);
+          if (st) return st;
+        }
+        b = e;
+        continue;
+      }
       // the rows, densely, written by the GPU straight into the page-locked staging
       SLATE_HIP(L.d_dense.ensure((size_t(m) + 1) * 8 + rows_pack_scratch_bytes(m)));
       void* hrows_dev = nullptr;
@@ -420,6 +507,7 @@ int slate_block_decode_batch(slate_ctx* ctx, int codec, const uint8_t* in, const
   o.rows = rows;
   o.rows_cap = rows_cap;
   o.row_base = row_base;
+  sink_map(o);
   return host_decode(ctx, codec, in, in_off, n, o);
 }
 
@@ -587,7 +675,16 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
     o.g = g;
     o.g_out_off = out_off;
     o.g_row_base = row_base;
+    // the device addresses are per device: each context maps the buffers for its own GPU
+    if (ctx_bind(ctxs[g]) != hipSuccess) {
+      S.st = SLATE_E_HIP;
+      return;
+    }
+    sink_map(o);
+    // G contexts on this host: kCopyThreads / G copy tasks each, unless the count was set
+    t_pool_cap = ctxs[g]->copy_threads_set ? 0 : std::max<size_t>(1, kCopyThreads / n_ctx);
     S.st = host_decode(ctxs[g], codec, in, S.in_off.data(), S.m, o, S.gsrc.data());
+    t_pool_cap = 0;
   });
 }
 

@@ -1645,6 +1645,45 @@ __global__ __launch_bounds__(256) void rows_pack_kernel(const uint64_t* __restri
 
 size_t rows_pack_scratch_bytes(uint32_t n) { return scan_scratch_bytes(n + 1) + 64; }
 
+// One wave per block: the block's decoded bytes and rows written straight into the caller's
+// page-locked buffers through their device addresses (host decode with pinned outputs: no
+// staging, no host copy).  Block i lands at g_out[i] / g_row[i] when given (sharded batch), else
+// at out_base + out_off[i] / row_base0 + row_base[i].  Bytes go as 16-byte stores (16-aligned
+// destinations: every plan offset is), the rows of a decoded block as 16-byte stores.
+__global__ __launch_bounds__(256) void blocks_to_host_kernel(const uint8_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ out_off,
+                                                             const uint64_t* __restrict__ row_base,
+                                                             const slate_block_meta* __restrict__ meta,
+                                                             const slate_row* __restrict__ rows, uint32_t n,
+                                                             uint8_t* dst_out, slate_row* dst_rows,
+                                                             const uint64_t* __restrict__ g_out,
+                                                             const uint64_t* __restrict__ g_row, uint64_t out_base,
+                                                             uint64_t row_base0) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) {
+    const uint64_t o0 = out_off[i], ob = out_off[i + 1] - o0;
+    const uint64_t od = g_out ? g_out[i] : out_base + o0;
+    for (uint64_t k = lane; k < ob / 16; k += 64)
+      reinterpret_cast<uint4*>(dst_out + od)[k] = reinterpret_cast<const uint4*>(out + o0)[k];
+    const slate_block_meta m = meta[i];
+    const uint64_t r0 = row_base[i], cap = row_base[i + 1] - r0;
+    const uint64_t c = m.status == SLATE_OK ? min(uint64_t(m.n_rows), cap) : 0;
+    const uint64_t rd = g_row ? g_row[i] : row_base0 + r0;
+    for (uint64_t r = lane; r < c; r += 64)
+      reinterpret_cast<uint4*>(dst_rows)[rd + r] = reinterpret_cast<const uint4*>(rows)[r0 + r];
+  }
+}
+
+hipError_t launch_blocks_to_host(hipStream_t st, const uint8_t* out, const uint64_t* out_off, const uint64_t* row_base,
+                                 const slate_block_meta* meta, const slate_row* rows, uint32_t n, uint8_t* dst_out,
+                                 slate_row* dst_rows, const uint64_t* g_out, const uint64_t* g_row, uint64_t out_base,
+                                 uint64_t row_base0) {
+  if (n == 0) return hipSuccess;
+  blocks_to_host_kernel<<<min((n + 3) / 4, 8192u), 256, 0, st>>>(out, out_off, row_base, meta, rows, n, dst_out,
+                                                                 dst_rows, g_out, g_row, out_base, row_base0);
+  return hipGetLastError();
+}
+
 hipError_t launch_rows_pack(hipStream_t st, const slate_block_meta* meta, const uint64_t* row_base, uint32_t n,
                             const slate_row* rows, uint64_t* dense_off, void* scratch, slate_row* dense) {
   if (n == 0) return hipSuccess;

@@ -73,8 +73,14 @@ constexpr uint32_t kIR = kNS * 16;
 // 2 mod 32 dwords spreads them over the banks (a 128-byte stride put all 32 lanes of a
 // half-wave on one bank).  Records are therefore 8-byte aligned: 16-byte chunks move as
 // two b64 halves.
-constexpr uint32_t kOutStride = kOR + 8;
-constexpr uint32_t kInStride = kIR + 8;
+#ifndef SLATE_LPB_OPAD
+#define SLATE_LPB_OPAD 8
+#endif
+#ifndef SLATE_LPB_IPAD
+#define SLATE_LPB_IPAD 8
+#endif
+constexpr uint32_t kOutStride = kOR + SLATE_LPB_OPAD;
+constexpr uint32_t kInStride = kIR + SLATE_LPB_IPAD;
 #ifndef SLATE_VERIFY_BATCH
 #define SLATE_VERIFY_BATCH 4
 #endif
@@ -94,9 +100,14 @@ constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
 #define SLATE_ROWS_DEFER 0
 #endif
 // the step before which the previous iteration's hole source is merged (0..3): later gives the
-// load longer to arrive; a lane's next hole waits for it
+// load longer to arrive; a lane's next hole waits for it.  Measured (configs[1], 1M blocks,
+// round 4): 0 -> 4.535 ms, 1 -> 4.469 ms, 2 -> 4.524 ms
 #ifndef SLATE_ABSORB_AT
-#define SLATE_ABSORB_AT 0
+#define SLATE_ABSORB_AT 1
+#endif
+// the step before which the next chunks' loads are issued (0..2)
+#ifndef SLATE_REFILL_AT
+#define SLATE_REFILL_AT 0
 #endif
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
@@ -599,7 +610,9 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
   // ---- a far copy (offset > kReach: its source left the ring and is flushed) goes on as holes
   // of up to 16 bytes, one pending per lane: reserve the bytes, load the source, go on decoding
   {
-    const bool mk = act & !L.dd & L.far & (L.rem != 0) & !L.hp & (L.d <= lim_d);
+    // (a step before the merge of the previous iteration's hole source makes no hole: the merge
+    // would take its pending flag for the old one)
+    const bool mk = (kSlot >= SLATE_ABSORB_AT) & act & !L.dd & L.far & (L.rem != 0) & !L.hp & (L.d <= lim_d);
     const uint32_t n = min(L.rem, 16u);
     L.hd = mk ? L.d : L.hd;
     L.hl = mk ? n : L.hl;
@@ -752,6 +765,9 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
   const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
   const uint32_t wave_g = blockIdx.x * (kLpb2Threads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
+#ifdef SLATE_LPB_PRIO  // experiment: static issue priority for the second half of the workgroup's waves
+  if ((threadIdx.x >> 6) >= kLpb2Threads / 128) __builtin_amdgcn_s_setprio(1);
+#endif
 
   // Rounds are handed out by an atomic counter (one dequeue per round, lane 0): waves that
   // finish early take more, so the launch ends when the work does, not when the unluckiest
@@ -898,12 +914,14 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       const bool act = have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                        iters < budget;
       LPB_MARK(refill);
-      {
-        commit_one(ins, S0, P0, L.z);
-        commit_one(ins, S1, P1, L.z);
-        commit_one(ins, S2, P2, L.z);
-        commit_one(ins, S3, P3, L.z);
-        L.c_commit += L.n_req;
+      commit_one(ins, S0, P0, L.z);
+      commit_one(ins, S1, P1, L.z);
+      commit_one(ins, S2, P2, L.z);
+      commit_one(ins, S3, P3, L.z);
+      L.c_commit += L.n_req;
+      // the next chunks' loads (committed at the next iteration's start): at the iteration's start,
+      // or after step SLATE_REFILL_AT - 1 (their registers then live for fewer steps)
+      auto issue_refill = [&]() {
         // the ring keeps every chunk from the oldest byte still to be read or CRC'd
         const uint32_t lo_pos = L.dd ? L.sh + L.clen : ((L.rem && L.lit) ? L.src : L.sh + L.s);
         const uint32_t lo_chunk = min(lo_pos >> 4, L.crc_pos);
@@ -917,7 +935,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         load_one(3, lane, wave_lane0, info, rel, R, P3, S3);
         L.c_issue += n;
         L.n_req = n;
-      }
+      };
+      if (SLATE_REFILL_AT == 0) issue_refill();
       // per iteration: the throttle's limit on d, and the end of the committed input (ring positions)
       const uint32_t lim_d = 16 * L.fl + kUnflushed, cend = 16 * L.c_commit;
       RowOut ro;
@@ -927,8 +946,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       if (SLATE_ABSORB_AT == 0) absorb_hole(L, Q, ring);
       lane_step<0, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
       if (SLATE_ABSORB_AT == 1) absorb_hole(L, Q, ring);
+      if (SLATE_REFILL_AT == 1) issue_refill();
       lane_step<1, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
       if (SLATE_ABSORB_AT == 2) absorb_hole(L, Q, ring);
+      if (SLATE_REFILL_AT == 2) issue_refill();
       lane_step<2, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
       if (SLATE_ABSORB_AT == 3) absorb_hole(L, Q, ring);
       lane_step<3, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
@@ -1345,7 +1366,12 @@ hipError_t launch_lz4_plan(hipStream_t st, const uint8_t* in, const uint64_t* in
 
 hipError_t launch_lz4_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
   if (a.n == 0) return hipGetLastError();
+#ifdef SLATE_LPB_NO_LZ4  // experiment builds of the Snappy kernel alone (LZ4 frames take the exact path)
+  (void)st, (void)z, (void)num_cus;
+  return hipErrorNotSupported;
+#else
   return launch_lpb<true>(st, a, z, num_cus);
+#endif
 }
 
 }  // namespace slate

@@ -87,16 +87,18 @@ struct PinBuf {
 struct PipeLane {
   hipStream_t stream = nullptr;
   hipEvent_t planned = nullptr, done = nullptr;
-  DevBuf d_in, d_in_off, d_out_off, d_row_base, d_scratch, d_out, d_meta, d_rows, d_dense;
-  PinBuf h_in, h_in_off, h_plan, h_out, h_meta, h_rows;  // h_rows: the chunk's rows, dense (rows_pack)
+  DevBuf d_in, d_in_off, d_out_off, d_row_base, d_scratch, d_out, d_meta, d_rows, d_dense, d_gmap;
+  PinBuf h_in, h_in_off, h_plan, h_out, h_meta, h_rows, h_gmap;  // h_rows: the chunk's rows, dense (rows_pack)
+  bool direct = false;  // the chunk's bytes and rows went straight to the caller's page-locked buffers
   // the chunk in flight: blocks [b0, b0+n), its place in the caller's outputs
   uint32_t b0 = 0, n = 0;
   uint64_t out_base = 0, row_base = 0, out_total = 0, rows_total = 0;
   bool busy = false, decoded = false;
   void release() {
-    for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows, &d_dense})
+    for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows, &d_dense,
+                      &d_gmap})
       b->release();
-    for (PinBuf* b : {&h_in, &h_in_off, &h_plan, &h_out, &h_meta, &h_rows}) b->release();
+    for (PinBuf* b : {&h_in, &h_in_off, &h_plan, &h_out, &h_meta, &h_rows, &h_gmap}) b->release();
     if (planned) (void)hipEventDestroy(planned);
     if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
@@ -161,7 +163,7 @@ class CopyPool {
     }
     std::lock_guard<std::mutex> one(run_mu_);
     std::unique_lock<std::mutex> g(mu_);
-    while (th_.size() + 1 < n_) th_.emplace_back([this] { worker(); });
+    while (th_.size() + 1 < std::min(n_, tasks)) th_.emplace_back([this] { worker(); });
     job_ = &fn;
     tasks_ = tasks;
     next_ = 0;
@@ -230,6 +232,7 @@ struct slate_ctx {
   std::atomic<uint64_t> gpu_ns{0};
   // host copy threads of this context (slate_ctx_set_copy_threads; SLATE_COPY_THREADS or 16)
   size_t copy_threads = 16;
+  bool copy_threads_set = false;  // set explicitly (API or SLATE_COPY_THREADS): sharded calls keep it
   std::unique_ptr<CopyPool> copy_pool;
   CopyPool* pool() {
     if (!copy_pool) copy_pool.reset(new CopyPool(copy_threads));

@@ -109,6 +109,11 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
 // counts.  For host transfers: the plan's row capacity is an upper bound several times the rows
 // a block holds.  scratch: rows_pack_scratch_bytes(n).
 size_t rows_pack_scratch_bytes(uint32_t n);
+// decoded bytes and rows of n blocks into mapped page-locked caller memory (decode.hip)
+hipError_t launch_blocks_to_host(hipStream_t st, const uint8_t* out, const uint64_t* out_off, const uint64_t* row_base,
+                                 const slate_block_meta* meta, const slate_row* rows, uint32_t n, uint8_t* dst_out,
+                                 slate_row* dst_rows, const uint64_t* g_out, const uint64_t* g_row, uint64_t out_base,
+                                 uint64_t row_base0);
 hipError_t launch_rows_pack(hipStream_t st, const slate_block_meta* meta, const uint64_t* row_base, uint32_t n,
                             const slate_row* rows, uint64_t* dense_off, void* scratch, slate_row* dense);
 // Index / filter payloads (`payload || BE32 CRC`) of any size for LZ4 / Zlib / Zstd (raw mode;

@@ -129,6 +129,9 @@ __device__ __forceinline__ void load_adv_tables(uint32_t* adv) {
 // c ? a : b as one v_cndmask_b32 on the lane mask of c: the compiler turned groups of selects
 // on one condition into divergent branches (exec-mask save/restore around both arms)
 __device__ __forceinline__ uint32_t vsel(bool c, uint32_t a, uint32_t b) {
+#ifdef SLATE_NO_ASM_SEL
+  return c ? a : b;
+#endif
   uint32_t r;
   asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(__builtin_amdgcn_ballot_w64(c)));
   return r;

@@ -19,3 +19,18 @@ if [ -n "$R4ABLATE" ]; then
   SLATE_LIB_VARIANT=libslatecodec_prof.so timeout -k 10 400 python -u tools/ablate.py 1000000 $R4ABLATE > $OUT/ablate.json 2> $OUT/ablate.err || { echo ABLATE_FAILED; tail -30 $OUT/ablate.err; exit 1; }
   python3 -c "import json;d=json.load(open('$OUT/ablate.json'));print({k:v['ms_median'] for k,v in d['modes'].items()})"
 fi
+if [ -n "$R4ZSTD" ]; then
+  ZA="--codec zstd --no-extras --no-host-io --no-cpu-baseline --steps 10 --verify none --cache /tmp/zc"
+  timeout -k 10 300 python -u bench.py $ZA > $OUT/zstd_par.json 2> $OUT/zstd_par.err || { echo ZSTD_FAILED; tail -20 $OUT/zstd_par.err; exit 1; }
+  SLATE_ZF_SERIAL=1 timeout -k 10 300 python -u bench.py $ZA > $OUT/zstd_ser.json 2> $OUT/zstd_ser.err || { echo ZSTD_SER_FAILED; tail -20 $OUT/zstd_ser.err; exit 1; }
+  timeout -k 10 300 python -u bench.py $ZA > $OUT/zstd_par2.json 2> $OUT/zstd_par2.err || { echo ZSTD_FAILED; tail -20 $OUT/zstd_par2.err; exit 1; }
+  for f in zstd_par zstd_ser zstd_par2; do python3 -c "import json;d=json.load(open('$OUT/$f.json'));print('$f',d['roofline']['kernel_ms'],d['roofline']['frac'])"; done
+fi
+if [ -n "$R4RATIO" ]; then
+  timeout -k 10 300 python -u tools/ratio_probe.py > $OUT/ratio.json 2> $OUT/ratio.err || { echo RATIO_FAILED; tail -20 $OUT/ratio.err; exit 1; }
+  cat $OUT/ratio.json
+fi
+if [ -n "$R4PERCALL" ]; then
+  timeout -k 10 300 python -u tools/percall_bench.py > $OUT/percall.json 2> $OUT/percall.err || { echo PERCALL_FAILED; tail -20 $OUT/percall.err; exit 1; }
+  cat $OUT/percall.json
+fi

@@ -2,8 +2,9 @@
 # HBM traffic of the decode kernels on the bench workload (run on the GPU box):
 # separate rocprofv3 --pmc passes for FETCH_SIZE, WRITE_SIZE and two SQ groups over a short bench.py
 # run, then tools/traffic.py folds them into profiles/pmc_decode_latest.json, which
-# bench.py reports as roofline.traffic.  usage: tools/traffic.sh OUTDIR [snappy|none]
-# (none: the CodecNone leg's decode_none_kernel -> profiles/pmc_decode_none_latest.json)
+# bench.py reports as roofline.traffic.  usage: tools/traffic.sh OUTDIR [snappy|none|zstd]
+# (none: the CodecNone leg's decode_none_kernel -> profiles/pmc_decode_none_latest.json; zstd: the configs[4]
+# decode's kernels summed -> profiles/pmc_decode_zstd_latest.json)
 set -e
 OUT=${1:-gpurun_out/traffic}
 CODEC=${2:-snappy}
