@@ -231,6 +231,12 @@ int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads);
  * groups on the filter's side stream overlap the flush, so the sum can exceed the wall time. */
 int slate_ctx_set_timing(slate_ctx* ctx, int on);
 int slate_ctx_gpu_time(slate_ctx* ctx, double* ms, int reset);
+/* The same spans' union (*busy_ms: device time with overlapping spans of the side streams counted
+ * once) and sum (*sum_ms, may be null) since timing was switched on or last reset.  Every device
+ * pass of slate_sst_builder_add_batch_device and slate_sst_builder_build is inside a span
+ * (device copies, rebases, scans and memsets included); host-to-device uploads of host batches
+ * and the blocks' device-to-host copies are not. */
+int slate_ctx_gpu_busy(slate_ctx* ctx, double* busy_ms, double* sum_ms, int reset);
 
 /* ---- library-owned memory (SURVEY 8b "Ownership": device-resident mode uses opaque handles
  * owned by the C side) ----------------------------------------------------------------------

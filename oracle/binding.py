@@ -410,6 +410,8 @@ def block_decode_batch(codec: int, blob: np.ndarray, in_off: np.ndarray, nthread
     out_off = np.zeros(n + 1, np.uint64)
     row_base = np.zeros(n + 1, np.uint64)
     blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    if blob.size == 0:  # an empty blob has no data pointer; the offsets say every block is empty
+        blob = np.zeros(1, np.uint8)
     in_off = np.ascontiguousarray(in_off, dtype=np.uint64)
     # first call with zero capacity just computes the plan
     L = lib()

@@ -1052,6 +1052,7 @@ int or_block_decode_batch(int codec, const uint8_t* in, const uint64_t* in_off, 
   }
   out_off[n] = o; row_base[n] = r;
   if (o > out_cap || r > rows_cap) return OR_E_CAPACITY;
+  if (!meta) return OR_OK; /* plan only (no outputs given: a batch of empty plans fits zero capacity) */
   if (nthreads < 1) nthreads = 1;
   if ((uint32_t)nthreads > n) nthreads = n ? (int)n : 1;
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);

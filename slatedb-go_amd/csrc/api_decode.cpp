@@ -9,6 +9,10 @@
 
 using namespace slate;
 
+namespace {
+constexpr size_t kSeekStageMax = size_t(1) << 20;  // slate_block_seek calls up to this many device bytes: one upload
+}  // namespace
+
 extern "C" {
 
 int slate_abi_version(void) { return SLATECODEC_ABI_VERSION; }
@@ -126,6 +130,25 @@ int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads) {
 int slate_ctx_set_timing(slate_ctx* ctx, int on) {
   if (!ctx) return SLATE_E_INVALID_ARG;
   ctx->timing = on != 0;
+  if (ctx->timing) {
+    SLATE_HIP(ctx_bind(ctx));
+    if (!ctx->t_ref) SLATE_HIP(hipEventCreate(&ctx->t_ref));
+    SLATE_HIP(hipEventRecord(ctx->t_ref, ctx->stream));
+    std::lock_guard<std::mutex> lk(ctx->span_mu);
+    ctx->spans.clear();
+  }
+  return SLATE_OK;
+}
+
+int slate_ctx_gpu_busy(slate_ctx* ctx, double* busy_ms, double* sum_ms, int reset) {
+  if (!ctx || !busy_ms) return SLATE_E_INVALID_ARG;
+  *busy_ms = ctx->span_union_ms();
+  const uint64_t ns = reset ? ctx->gpu_ns.exchange(0) : ctx->gpu_ns.load();
+  if (sum_ms) *sum_ms = double(ns) * 1e-6;
+  if (reset) {
+    std::lock_guard<std::mutex> lk(ctx->span_mu);
+    ctx->spans.clear();
+  }
   return SLATE_OK;
 }
 
@@ -225,6 +248,34 @@ int slate_block_seek_warn(slate_ctx* ctx, const uint8_t* data, const uint64_t* o
                o_warn = carve(wbytes + 16);
   SLATE_HIP(ctx->e_g.ensure(off));
   uint8_t* base = ctx->e_g.as<uint8_t>();
+  // Small calls (a point read: one block, one key): every input packed into page-locked staging
+  // in the device layout and uploaded by one copy; the kernel writes the results into that
+  // staging through its device address; one wait.  Pageable copies cost ~10 us each.
+  if (off <= kSeekStageMax) {
+    SLATE_HIP(ctx->h_seek.ensure(off));
+    uint8_t* h = ctx->h_seek.as<uint8_t>();
+    if (db) memcpy(h + o_data, data, db);
+    memcpy(h + o_off, out_off, (size_t(n_blocks) + 1) * 8);
+    if (n_blocks) memcpy(h + o_meta, meta, size_t(n_blocks) * sizeof(slate_block_meta));
+    memcpy(h + o_q, qblock, n * 4);
+    if (kb) memcpy(h + o_keys, keys + key_off[0], kb);
+    uint64_t* hk = reinterpret_cast<uint64_t*>(h + o_koff);
+    for (uint64_t i = 0; i <= n; i++) hk[i] = key_off[i] - key_off[0];
+    uint8_t* hdev = static_cast<uint8_t*>(mapped_ptr(h));
+    if (hdev) {
+      SLATE_HIP(hipMemcpyAsync(base, h, o_res, hipMemcpyHostToDevice, st));
+      SLATE_HIP(launch_block_seek(st, base + o_data, reinterpret_cast<const uint64_t*>(base + o_off),
+                                  reinterpret_cast<const slate_block_meta*>(base + o_meta),
+                                  reinterpret_cast<const uint32_t*>(base + o_q), base + o_keys,
+                                  reinterpret_cast<const uint64_t*>(base + o_koff), n,
+                                  reinterpret_cast<slate_seek*>(hdev + o_res),
+                                  warn_cap ? reinterpret_cast<slate_seek_warn*>(hdev + o_warn) : nullptr, warn_cap));
+      SLATE_HIP(hipStreamSynchronize(st));
+      memcpy(res, h + o_res, n * sizeof(slate_seek));
+      if (wbytes) memcpy(warn, h + o_warn, wbytes);
+      return SLATE_OK;
+    }
+  }
   std::vector<uint64_t> rel(n + 1);
   for (uint64_t i = 0; i <= n; i++) rel[i] = key_off[i] - key_off[0];
   if (db) SLATE_HIP(hipMemcpyAsync(base + o_data, data, db, hipMemcpyHostToDevice, st));

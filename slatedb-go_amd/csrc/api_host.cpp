@@ -141,23 +141,6 @@ struct Sink {
   slate_row* rows_dev = nullptr;
 };
 
-// The device address of page-locked host memory, null for pageable memory.
-void* mapped_ptr(void* p) {
-  if (!p) return nullptr;
-  hipPointerAttribute_t at{};
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (at.type != hipMemoryTypeHost) return nullptr;
-  void* d = nullptr;
-  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  return d;
-}
-
 // Sets the sink's direct path when the caller's out and rows arrays are page-locked and aligned
 // (SLATE_HOST_DIRECT=0 turns it off: A/B runs).
 void sink_map(Sink& o) {
@@ -198,6 +181,31 @@ uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len) {
     sh += 7;
   }
   return 0;
+}
+
+// SLATE_ONE_LAUNCH=0: slate_block_decode takes the generic plan + decode path for every codec
+// (A/B and tests of both paths)
+bool one_off() {
+  static const bool off = [] {
+    const char* e = getenv("SLATE_ONE_LAUNCH");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
+// slate_block_decode's outputs from the decoded block (m: its meta, dec: its decoded bytes)
+int block_decode_finish(const slate_block_meta& m, const uint8_t* dec, uint8_t* out, size_t out_cap, size_t* out_len,
+                        slate_block_meta* meta, uint16_t* offsets, size_t offsets_cap) {
+  *meta = m;
+  if (m.status != SLATE_OK) return m.status;
+  // decoded length = data_len + 2 * n_rows + 2 for a successfully decoded block
+  const size_t dl = size_t(m.data_len) + 2 * size_t(m.n_rows) + 2;
+  if (out_len) *out_len = dl;
+  if (dl > out_cap || (offsets && m.n_rows > offsets_cap)) return SLATE_E_CAPACITY;
+  if (out && dl) memcpy(out, dec, dl);
+  if (offsets)
+    for (uint32_t i = 0; i < m.n_rows; i++) offsets[i] = ld_be16(dec + m.data_len + 2 * i);
+  return SLATE_OK;
 }
 
 // Run fn(lo, hi) over [0, n) split across the calling context's copy threads (pieces of >= grain).
@@ -527,6 +535,27 @@ int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_l
   hv[0] = 0;
   hv[1] = in_len;
   if (in_len) memcpy(hin, in, in_len);
+  // CodecNone / CodecSnappy within the large-block LDS budget: the plan here, one launch that
+  // reads the staging and writes meta and decoded bytes through their device addresses, one wait
+  uint64_t dl1 = host_plannable(codec) ? host_decoded_len(codec, in, in_len) : 0;
+  if (host_plannable(codec) && in_len + 15 <= kLargeInCap && align16(dl1) <= kLargeOutCap && !one_off()) {
+    const uint64_t osz = align16(dl1), rsz = row_capacity(dl1);
+    SLATE_HIP(L.d_in.ensure(in_len + 32));
+    SLATE_HIP(L.d_out.ensure(osz + 16));
+    SLATE_HIP(L.d_rows.ensure((rsz + 1) * sizeof(slate_row)));
+    SLATE_HIP(L.h_out.ensure(osz + 16));
+    uint8_t* hin_dev = static_cast<uint8_t*>(mapped_ptr(hin));
+    uint8_t* hout_dev = static_cast<uint8_t*>(mapped_ptr(L.h_out.p));
+    slate_block_meta* hmeta = reinterpret_cast<slate_block_meta*>(hv + 6);
+    slate_block_meta* hmeta_dev = static_cast<slate_block_meta*>(mapped_ptr(hmeta));
+    if (hin_dev && hout_dev && hmeta_dev) {
+      DecodeArgs a{codec, L.d_in.as<uint8_t>(), nullptr, 1, L.d_out.as<uint8_t>(), nullptr, hmeta_dev,
+                   L.d_rows.as<slate_row>(), nullptr, nullptr, nullptr, 0};
+      SLATE_HIP(launch_decode_one(s, a, hin_dev, in_len, osz, rsz, hout_dev));
+      SLATE_HIP(hipStreamSynchronize(s));
+      return block_decode_finish(*hmeta, L.h_out.as<uint8_t>(), out, out_cap, out_len, meta, offsets, offsets_cap);
+    }
+  }
   SLATE_HIP(L.d_in.ensure(in_len + 32));
   SLATE_HIP(L.d_in_off.ensure(64));
   SLATE_HIP(L.d_out_off.ensure(64));
@@ -551,17 +580,8 @@ int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_l
   SLATE_HIP(hipMemcpyAsync(hv + 6, L.d_meta.p, sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
   if (cap) SLATE_HIP(hipMemcpyAsync(L.h_out.p, L.d_out.p, cap, hipMemcpyDeviceToHost, s));
   SLATE_HIP(hipStreamSynchronize(s));
-  memcpy(meta, hv + 6, sizeof(slate_block_meta));
-  if (meta->status != SLATE_OK) return meta->status;
-  // decoded length = data_len + 2 * n_rows + 2 for a successfully decoded block
-  const size_t dl = size_t(meta->data_len) + 2 * size_t(meta->n_rows) + 2;
-  if (out_len) *out_len = dl;
-  if (dl > out_cap || (offsets && meta->n_rows > offsets_cap)) return SLATE_E_CAPACITY;
-  const uint8_t* dec = L.h_out.as<uint8_t>();
-  if (out && dl) memcpy(out, dec, dl);
-  if (offsets)
-    for (uint32_t i = 0; i < meta->n_rows; i++) offsets[i] = ld_be16(dec + meta->data_len + 2 * i);
-  return SLATE_OK;
+  return block_decode_finish(*reinterpret_cast<const slate_block_meta*>(hv + 6), L.h_out.as<uint8_t>(), out, out_cap,
+                             out_len, meta, offsets, offsets_cap);
 }
 
 uint32_t slate_shard_blocks(uint32_t n_blocks, uint32_t n_shards, uint32_t shard) {

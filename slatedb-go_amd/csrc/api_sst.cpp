@@ -129,12 +129,12 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
     o += hl[c];
   }
   if (nch) SLATE_HIP(hipMemcpyAsync(d_off, ho.data(), nch * 8, hipMemcpyHostToDevice, st));
-  SLATE_HIP(launch_snappy_gather(st, slots, lens, d_off, nch, d));
   SLATE_HIP(crcb.ensure(crc_scratch_bytes(total) + 16));
   uint32_t* scratch = crcb.as<uint32_t>();
   uint32_t* cout = scratch + (crc_scratch_bytes(total) / 4);
   {
     GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_snappy_gather(st, slots, lens, d_off, nch, d));
     SLATE_HIP(launch_crc32(st, d, total, scratch, cout, ctx->num_cus));
   }
   uint32_t crc = 0;
@@ -1044,7 +1044,9 @@ static int pending_append(slate_sst_builder* b, const uint8_t* keys, const uint6
   uint64_t* dko = b->d_koff.as<uint64_t>() + b->n_pend;  // entry n_pend (== kbytes) is rewritten
   uint64_t* dvo = b->d_voff.as<uint64_t>() + b->n_pend;
   uint8_t* dt = b->d_tomb.as<uint8_t>() + b->n_pend;
+  std::unique_ptr<GpuSpan> g_add;  // the device passes (a host batch's uploads are not in it)
   if (dev) {
+    g_add.reset(new GpuSpan(ctx, st));
     if (kb) SLATE_HIP(hipMemcpyAsync(dk, keys + k0, kb, hipMemcpyDeviceToDevice, st));
     if (vb) SLATE_HIP(hipMemcpyAsync(dv, vals + v0, vb, hipMemcpyDeviceToDevice, st));
     SLATE_HIP(launch_kv_rebase(st, key_off, n, dko, b->kbytes));
@@ -1060,6 +1062,7 @@ static int pending_append(slate_sst_builder* b, const uint8_t* keys, const uint6
     if (!s) s = ctx_h2d(ctx, t0 + n + 1, val_off, (n + 1) * 8, st);
     if (!s && tomb) s = ctx_h2d(ctx, dt, tomb, n, st);
     if (s) return s;
+    g_add.reset(new GpuSpan(ctx, st));
     SLATE_HIP(launch_kv_rebase(st, t0, n, dko, b->kbytes));
     SLATE_HIP(launch_kv_rebase(st, t0 + n + 1, n, dvo, b->vbytes));
   }
@@ -1173,8 +1176,11 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
   g_pick.stop();
   std::vector<uint64_t> fk_off(nb + 1);
   SLATE_HIP(hipMemcpyAsync(fk_off.data(), fko, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
-  SLATE_HIP(hipMemsetAsync(w.block_size + nb, 0, 8, st));
-  SLATE_HIP(launch_scan_u64(st, w.block_size, uint32_t(nb + 1), scan_scratch));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(hipMemsetAsync(w.block_size + nb, 0, 8, st));
+    SLATE_HIP(launch_scan_u64(st, w.block_size, uint32_t(nb + 1), scan_scratch));
+  }
   std::vector<uint64_t> out_off(nb + 1);
   SLATE_HIP(hipMemcpyAsync(out_off.data(), w.block_size, (nb + 1) * 8, hipMemcpyDeviceToHost, st));
   SLATE_HIP(hipStreamSynchronize(st));

@@ -1674,6 +1674,56 @@ __global__ __launch_bounds__(256) void blocks_to_host_kernel(const uint8_t* __re
   }
 }
 
+// One block at the lowest latency (slate_block_decode, CodecNone / CodecSnappy): one launch, one
+// wave.  The plan (decoded length -> output and row capacity) is the host's (the same
+// decoded_len rules), so the offsets arrive as kernel arguments and sit in LDS; the encoded block
+// is read once from the caller's page-locked staging through its device address into HBM
+// (a.in), decoded by the large-kernel wave with its LDS budget (the host checks the block fits),
+// and the decoded bytes go to page-locked host memory (host_out) the same way.  a.meta may be
+// host memory too.  Replaces the generic path's plan kernel, scans, transfers and two waits.
+__global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint8_t* __restrict__ host_in,
+                                                        uint64_t in_len, uint64_t out_sz, uint64_t row_sz,
+                                                        uint8_t* __restrict__ host_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint64_t offs[6];
+  const int lane = threadIdx.x;
+  if (lane < 6) offs[lane] = lane == 1 ? in_len : lane == 3 ? out_sz : lane == 5 ? row_sz : 0;
+  uint8_t* din = const_cast<uint8_t*>(a.in);
+  for (uint64_t k = lane; k < (in_len + 15) / 16; k += 64)
+    reinterpret_cast<uint4*>(din)[k] = reinterpret_cast<const uint4*>(host_in)[k];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  load_crc_tables(tab);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the staged block, before the wave reads it
+  __syncthreads();
+  a.in_off = offs;
+  a.out_off = offs + 2;
+  a.row_base = offs + 4;
+  WaveBufs w{tab, smem + kTabBytes, smem + kTabBytes + kLargeInCap, kLargeInCap, kLargeOutCap};
+  decode_block_wave<0>(a, 0, w, lane, false);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the decoded bytes, before the copy out
+  __syncthreads();
+  for (uint64_t k = lane; k < out_sz / 16; k += 64)
+    reinterpret_cast<uint4*>(host_out)[k] = reinterpret_cast<const uint4*>(a.out)[k];
+}
+
+hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& args_in, const uint8_t* host_in, uint64_t in_len,
+                             uint64_t out_sz, uint64_t row_sz, uint8_t* host_out) {
+  DecodeArgs a = args_in;
+  a.n = 1;
+  a.debug = 0;
+  a.raw = 0;
+  a.rt_zero = 0;
+  if ((a.codec != SLATE_CODEC_NONE && a.codec != SLATE_CODEC_SNAPPY) || in_len + 15 > kLargeInCap ||
+      out_sz > kLargeOutCap)
+    return hipErrorInvalidValue;
+  constexpr size_t lds = kTabBytes + kLargeInCap + kLargeOutCap;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_one_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+  if (attr != hipSuccess) return attr;
+  decode_one_kernel<<<1, 64, lds, st>>>(a, host_in, in_len, out_sz, row_sz, host_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_blocks_to_host(hipStream_t st, const uint8_t* out, const uint64_t* out_off, const uint64_t* row_base,
                                  const slate_block_meta* meta, const slate_row* rows, uint32_t n, uint8_t* dst_out,
                                  slate_row* dst_rows, const uint64_t* g_out, const uint64_t* g_row, uint64_t out_base,

@@ -2,6 +2,7 @@
 // buffers.  Each slate_ctx is used by one caller thread at a time; the library
 // keeps no global mutable state (SURVEY 8b "Threading").
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -59,6 +60,23 @@ struct DevBuf {
 };
 
 // Page-locked host staging (hipHostMalloc): DMA-able, so copies overlap kernels.
+// The device address of page-locked host memory, null for pageable memory.
+inline void* mapped_ptr(void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (at.type != hipMemoryTypeHost) return nullptr;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -214,6 +232,7 @@ struct slate_ctx {
   hipStream_t stream = nullptr;
   PipeLane lanes[kPipeLanes];
   PinBuf h_small;  // single-block staging (slate_block_decode)
+  PinBuf h_seek;   // slate_block_seek(_warn) inputs (one upload) and results (written by the kernel)
   // decode batch buffers
   DevBuf d_in, d_in_off, d_out, d_out_off, d_meta, d_rows, d_row_base, d_scratch;
   // encode / misc buffers
@@ -230,6 +249,38 @@ struct slate_ctx {
   // kernel groups of every stream the context uses (GpuSpan)
   bool timing = false;
   std::atomic<uint64_t> gpu_ns{0};
+  // the same spans as [start, end) in ms after t_ref (recorded on the context's stream when timing
+  // is switched on), for their union: device time with the overlap of the side streams counted once
+  hipEvent_t t_ref = nullptr;
+  std::mutex span_mu;
+  std::vector<std::pair<double, double>> spans;
+  void add_span(hipEvent_t a, hipEvent_t b, double ms) {
+    gpu_ns.fetch_add(uint64_t(ms * 1e6));
+    float s0 = 0.f;
+    if (!t_ref || hipEventElapsedTime(&s0, t_ref, a) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(span_mu);
+    spans.emplace_back(double(s0), double(s0) + ms);
+    (void)b;
+  }
+  double span_union_ms() {
+    std::lock_guard<std::mutex> lk(span_mu);
+    std::vector<std::pair<double, double>> v = spans;
+    std::sort(v.begin(), v.end());
+    double tot = 0, lo = 0, hi = 0;
+    bool open = false;
+    for (const auto& iv : v) {
+      if (open && iv.first <= hi) {
+        hi = std::max(hi, iv.second);
+        continue;
+      }
+      if (open) tot += hi - lo;
+      lo = iv.first;
+      hi = iv.second;
+      open = true;
+    }
+    if (open) tot += hi - lo;
+    return tot;
+  }
   // host copy threads of this context (slate_ctx_set_copy_threads; SLATE_COPY_THREADS or 16)
   size_t copy_threads = 16;
   bool copy_threads_set = false;  // set explicitly (API or SLATE_COPY_THREADS): sharded calls keep it
@@ -246,8 +297,11 @@ struct slate_ctx {
       b->release();
     if (aux) (void)hipStreamDestroy(aux);
     aux = nullptr;
+    if (t_ref) (void)hipEventDestroy(t_ref);
+    t_ref = nullptr;
     for (PipeLane& l : lanes) l.release();
     h_small.release();
+    h_seek.release();
   }
 };
 
@@ -282,7 +336,7 @@ struct GpuSpan {
     stop();
     float ms = 0.f;
     if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess && ms > 0.f)
-      ctx->gpu_ns.fetch_add(uint64_t(double(ms) * 1e6));
+      ctx->add_span(a, b, double(ms));
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
   }

@@ -114,6 +114,11 @@ hipError_t launch_blocks_to_host(hipStream_t st, const uint8_t* out, const uint6
                                  const slate_block_meta* meta, const slate_row* rows, uint32_t n, uint8_t* dst_out,
                                  slate_row* dst_rows, const uint64_t* g_out, const uint64_t* g_row, uint64_t out_base,
                                  uint64_t row_base0);
+// One CodecNone / CodecSnappy block, one launch (slate_block_decode): host_in / host_out are device
+// addresses of page-locked host memory; out_sz = align16(decoded length), row_sz = its row capacity
+// (the plan the host computed with decoded_len's rules); a.in / a.out / a.rows: device scratch.
+hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& a, const uint8_t* host_in, uint64_t in_len,
+                             uint64_t out_sz, uint64_t row_sz, uint8_t* host_out);
 hipError_t launch_rows_pack(hipStream_t st, const slate_block_meta* meta, const uint64_t* row_base, uint32_t n,
                             const slate_row* rows, uint64_t* dense_off, void* scratch, slate_row* dense);
 // Index / filter payloads (`payload || BE32 CRC`) of any size for LZ4 / Zlib / Zstd (raw mode;

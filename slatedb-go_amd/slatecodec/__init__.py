@@ -75,6 +75,7 @@ _SIGS = {
     "slate_ctx_set_copy_threads": (C.c_int, [vp, C.c_uint32]),
     "slate_ctx_set_timing": (C.c_int, [vp, C.c_int]),
     "slate_ctx_gpu_time": (C.c_int, [vp, C.POINTER(C.c_double), C.c_int]),
+    "slate_ctx_gpu_busy": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int]),
     "slate_ctx_synchronize": (C.c_int, [vp]),
     "slate_decode_scratch_bytes": (C.c_size_t, [C.c_uint32]),
     "slate_block_decode_plan_device": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, vp, vp]),
@@ -226,6 +227,12 @@ class Context:
         v = C.c_double()
         _check(lib().slate_ctx_gpu_time(self._h, C.byref(v), 1 if reset else 0), "slate_ctx_gpu_time")
         return v.value
+
+    def gpu_busy_ms(self, reset: bool = False) -> tuple:
+        """(union, sum) of the timed spans in ms (slate_ctx_gpu_busy)."""
+        u, t = C.c_double(), C.c_double()
+        _check(lib().slate_ctx_gpu_busy(self._h, C.byref(u), C.byref(t), 1 if reset else 0), "slate_ctx_gpu_busy")
+        return u.value, t.value
     def synchronize(self):
         _check(lib().slate_ctx_synchronize(self._h), "slate_ctx_synchronize")
 

@@ -140,6 +140,36 @@ def test_single_block_api(ctx, ref_vectors):
         assert st == 2
 
 
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+def test_single_block_api_matrix(ctx, codec):
+    """slate_block_decode: the one-launch path (CodecNone / CodecSnappy blocks within the large-block
+    LDS budget, plan on the host) and the generic plan + decode path beyond it, meta bit-exact
+    against the oracle's batch decode of the same block, decoded bytes and offsets on success.
+    Valid blocks of several block sizes, mutated blocks (stale and fixed CRC), the edge lengths,
+    and a block whose decoded length is past the budget (90112 B)."""
+    rng = random.Random(31 + codec)
+    blocks = []
+    for bs in (64, 512, 4096, 32768):
+        kvs = bg.random_kvs(rng, 300, alphabet=rng.choice([4, 256]))
+        blocks += bg.sst_blocks(kvs, bs, codec)[:6]
+    blocks += [bg.mutate(rng, b, fix) for b in blocks[:16] for fix in (False, True)]
+    blocks += [b"", b"\x00", b"\x00" * 5, bg.recrc(b"\x00\x00"), bg.recrc(b"\x00\x00\x00\x00\x00\x01"),
+               bg.recrc(b"\x00"), bg.recrc(b"\x02\x04ab"), bg.recrc(b"\xff" * 11), bg.recrc(b"\x80"),
+               bg.recrc(b"\x05\x00a\x01\x01")]
+    big = [(b"big%05d" % i, bytes(rng.randrange(3) for _ in range(30000))) for i in range(4)]
+    blocks += bg.sst_blocks(big, 1 << 17, codec)[:1]
+    assert max(len(b) for b in blocks[-1:]) > 90112 or codec == ob.SNAPPY
+    for i, blk in enumerate(blocks):
+        st, m, data, offs = ctx.block_decode(blk, codec)
+        blob, off = bg.pack([blk])
+        o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(codec, blob, off)
+        assert m.tobytes() == o_meta[0].tobytes(), (i, m, o_meta[0], blk[:16].hex())
+        assert st == int(o_meta[0]["status"])
+        if st == 0:
+            assert data == o_out[: int(m["data_len"])].tobytes(), i
+            assert offs == [int(r["row_off"]) for r in o_rows[: int(m["n_rows"])]], i
+
+
 @pytest.mark.parametrize("misalign", [0, 1, 7, 12, 13, 15])
 def test_none_size_window(ctx, misalign):
     """CodecNone blocks around the streaming kernel's window (decode_none.hip: 4..5104 data bytes in

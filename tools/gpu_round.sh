@@ -24,6 +24,9 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   bash tools/traffic.sh "$OUT/traffic_none" none > "$OUT/traffic_none.log" 2>&1 || { echo TRAFFIC_NONE_FAILED; tail -20 "$OUT/traffic_none.log"; exit 1; }
   tail -1 "$OUT/traffic_none.log" | cut -c1-400
   cp profiles/pmc_decode_none_latest.json "$OUT/"
+  bash tools/traffic.sh "$OUT/traffic_zstd" zstd > "$OUT/traffic_zstd.log" 2>&1 || { echo TRAFFIC_ZSTD_FAILED; tail -20 "$OUT/traffic_zstd.log"; exit 1; }
+  tail -1 "$OUT/traffic_zstd.log" | cut -c1-400
+  cp profiles/pmc_decode_zstd_latest.json "$OUT/"
   timeout -k 10 500 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo BENCH_FAILED; tail -30 "$OUT/bench.err"; exit 1; }
   cat "$OUT/bench.json"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- python3 bench.py --no-extras \
