@@ -907,7 +907,7 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
   uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
   if (len > 0xFFFFFF00ull || shift + len > w.in_cap || (a.codec != SLATE_CODEC_NONE && dl > w.out_cap)) {
     if (defer_large) return false;
-    m.status = SLATE_E_CAPACITY;  // beyond the large kernel's LDS budget
+    m.status = SLATE_E_CAPACITY;  // beyond the large kernel's LDS budget (its caller then takes the HBM mode)
     write_meta(&a.meta[b], m, lane);
     return true;
   }
@@ -1122,7 +1122,12 @@ __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   if (CK == 1) zlib_lds(w, smem + kTabBytes + in_cap, 1, 0, lane);
   if (CK == 2) zstd_lds(w, smem + kTabBytes + in_cap, 0, lane);
   uint32_t count = *a.large_count;
-  for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) decode_block_wave<CK>(a, a.large_list[k], w, lane, false);
+  for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) {
+    // beyond this kernel's LDS budget (encoded > 64 KiB or decoded > 88 KiB: a block holding one
+    // large value): the same wave decoder with input and output in HBM
+    const uint32_t b = a.large_list[k];
+    if (!decode_block_wave<CK>(a, b, w, lane, true)) decode_block_wave<CK, true>(a, b, w, lane, false);
+  }
 }
 
 // Index / filter payloads of any size (LZ4 / Zlib / Zstd; raw mode): one wave per payload,

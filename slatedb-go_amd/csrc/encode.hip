@@ -453,7 +453,17 @@ __global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __rest
     const uint32_t pn = uint32_t(min<uint64_t>(n - c * kSnapMaxBlock, kSnapMaxBlock));
     uint8_t* o = dst + c * kSnapChunkSlot;
     snap_sync();  // the previous chunk's reads of the stage are done
-    for (uint32_t i = uint32_t(lane); i < pn; i += kWave) stage[i] = p[i];
+    // 16-byte loads for the whole chunks (the source is 16-aligned: chunk starts are 64 KiB apart
+    // from an aligned buffer), bytes for the tail; all loads of a lane issue before its LDS stores
+    const uint32_t nq = pn / 16;
+    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+#pragma unroll 4
+      for (uint32_t q = uint32_t(lane); q < nq; q += kWave)
+        reinterpret_cast<uint4*>(stage)[q] = reinterpret_cast<const uint4*>(p)[q];
+      for (uint32_t i = 16 * nq + uint32_t(lane); i < pn; i += kWave) stage[i] = p[i];
+    } else {
+      for (uint32_t i = uint32_t(lane); i < pn; i += kWave) stage[i] = p[i];
+    }
     if (lane < 16) stage[pn + lane] = 0;  // bytes past the chunk (never part of a match)
     snap_sync();
     uint32_t d;

@@ -35,6 +35,30 @@ def crc(body: bytes) -> bytes:
     return body + struct.pack(">I", zlib.crc32(body))
 
 
+def go_zlib(raw: bytes, level: int = 6) -> bytes:
+    """A zlib stream in the shape Go's compress/zlib writer closes with: the data's (non-final)
+    deflate blocks, then an empty FINAL stored block (compress/flate deflate.go close ->
+    huffmanBitWriter.writeStoredHeader(0, true): bytes ..01 00 00 FF FF), then the Adler-32.
+    Built from zlib's sync flush, whose empty non-final stored block is made final by setting its
+    BFINAL bit (the one bit flip after which a raw inflater ends there with the same bytes).  Go's
+    own block splitting is not reproduced (parity for it is unpinned)."""
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    body = c.compress(raw) + c.flush(zlib.Z_SYNC_FLUSH)
+    assert body.endswith(b"\x00\x00\xff\xff")
+    for pos in (len(body) - 5, len(body) - 6):
+        for bit in range(8):
+            t = bytearray(body)
+            t[pos] ^= 1 << bit
+            d = zlib.decompressobj(-15)
+            try:
+                out = d.decompress(bytes(t))
+            except zlib.error:
+                continue
+            if d.eof and out == raw and not d.unused_data:
+                return b"\x78\x9c" + bytes(t) + struct.pack(">I", zlib.adler32(raw))
+    raise AssertionError("no BFINAL bit found")
+
+
 def recode(sst_none: bytes, codec: int, rng: random.Random) -> bytes:
     """The CodecNone SST `sst_none` re-encoded with `codec` (same keys, blocks and filter bits)."""
     st, info = ob.sst_read_info(sst_none)

@@ -157,6 +157,7 @@ def test_single_block_api_matrix(ctx, codec):
                bg.recrc(b"\x00"), bg.recrc(b"\x02\x04ab"), bg.recrc(b"\xff" * 11), bg.recrc(b"\x80"),
                bg.recrc(b"\x05\x00a\x01\x01")]
     big = [(b"big%05d" % i, bytes(rng.randrange(3) for _ in range(30000))) for i in range(4)]
+    blocks += bg.sst_blocks([(b"one", bytes(rng.randrange(3) for _ in range(70000)))], 4096, codec)
     blocks += bg.sst_blocks(big, 1 << 17, codec)[:1]
     assert max(len(b) for b in blocks[-1:]) > 90112 or codec == ob.SNAPPY
     for i, blk in enumerate(blocks):
@@ -168,6 +169,32 @@ def test_single_block_api_matrix(ctx, codec):
         if st == 0:
             assert data == o_out[: int(m["data_len"])].tobytes(), i
             assert offs == [int(r["row_off"]) for r in o_rows[: int(m["n_rows"])]], i
+
+
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY, ob.LZ4, ob.ZLIB, ob.ZSTD])
+def test_blocks_beyond_lds_budget(ctx, codec):
+    """Blocks holding one large value (encoded > 64 KiB or decoded > 88 KiB: beyond the large-block
+    kernel's LDS budget) decode with input and output in HBM, like the oracle -- block.Decode has no
+    size limit (block.go:78-101) and a Builder puts a value larger than BlockSize in a block of its
+    own.  Batch and single-block calls, with smaller blocks around them, under flipped CRCs too."""
+    from tests import sstgen
+    rng = random.Random(11 + codec)
+    nrng = np.random.default_rng(11 + codec)
+    blocks = []
+    for vl in (70000, 100000, 200000):
+        kv = [(b"one%06d" % vl, nrng.integers(0, 4, vl, dtype=np.uint8).tobytes())]
+        raw = bg.sst_blocks(kv, 4096, ob.NONE)[0][:-4]
+        blocks.append(sstgen.crc(sstgen.compress(codec, raw, rng)))
+    small = [sstgen.crc(sstgen.compress(codec, b[:-4], rng))
+             for b in bg.sst_blocks(bg.random_kvs(rng, 200), 4096, ob.NONE)[:4]]
+    flipped = [b[:-1] + bytes([b[-1] ^ 1]) for b in blocks[:2]]
+    meta = _compare(ctx, codec, small[:2] + blocks + small[2:] + flipped)
+    assert (meta["status"][:7] == 0).all() and (meta["status"][7:] == 2).all(), meta["status"]
+    for blk in blocks:
+        st, m, data, offs = ctx.block_decode(blk, codec)
+        om, odata, orows = ob.block_decode(blk, codec)
+        assert st == 0 == int(om["status"]) and data == odata[:int(om["data_len"])]
+        assert offs == [int(r["row_off"]) for r in orows]
 
 
 @pytest.mark.parametrize("misalign", [0, 1, 7, 12, 13, 15])

@@ -414,3 +414,18 @@ def test_snappy_cross_libsnappy(oracle):
         if lib_bytes != oracle.snappy_encode(src) and name not in LIBSNAPPY_ALLOWED_DIFF:
             diff.append(name)
     assert not diff, f"restated golang/snappy encoder differs from libsnappy on {diff}"
+
+
+def test_go_shaped_zlib_stream(oracle):
+    """tests/sstgen.go_zlib (the stream shape Go's compress/zlib closes with, used by the GPU
+    zlib-par tests): zlib reads it back, its last deflate block is an empty final stored block, and
+    the oracle's bloom reader (compression.go:134-140 under bloom.go:70-91) decodes it."""
+    from tests import sstgen
+    rng = np.random.default_rng(3)
+    raw = rng.integers(0, 3, 200_000, dtype=np.uint8).tobytes()
+    z = sstgen.go_zlib(raw, 6)
+    assert zlib.decompress(z) == raw and z[-8:-4] == b"\x00\x00\xff\xff"
+    d = zlib.decompressobj(-15)
+    assert d.decompress(z[2:-4]) == raw and d.eof and not d.unused_data  # ends at the stored block
+    st, *_ = oracle.bloom_decode(sstgen.crc(z), oracle.ZLIB, cap=1 << 22)
+    assert st == 0

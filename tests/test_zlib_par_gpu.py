@@ -86,8 +86,24 @@ def test_zlib_par_taken(sst_parts, tmp_path):
     """The parallel path is the one that decodes these streams (SLATE_HOST_TRACE reports its chain:
     no hand-off to the exact decoder), in a child process (the trace switch is read once)."""
     ib, fb = sst_parts
+    _par_chains(tmp_path, _zlib(ib, 6), _zlib(fb, 9))
+
+
+def test_go_shaped_streams(ctx, sst_parts, tmp_path):
+    """Streams closed the way Go's compress/zlib closes them (data blocks, then an empty final
+    stored block: sstgen.go_zlib): decoded like the oracle, and by the parallel path (no hand-off)."""
+    ib, fb = sst_parts
+    iz, fz = sstgen.crc(sstgen.go_zlib(ib, 6)), sstgen.crc(sstgen.go_zlib(fb, 9))
+    assert iz[-12:-8] == fz[-12:-8] == b"\x00\x00\xff\xff"  # LEN / NLEN of the empty stored block
+    assert _check_filter(ctx, fz) == 0
+    st, index = ctx.decode_index(iz, ob.ZLIB)
+    ost, ometas = ob.decode_index(iz, ob.ZLIB, cap=1 << 26)
+    assert st == ost == 0 and index.block_metas() == ometas
+    _par_chains(tmp_path, iz, fz)
+
+
+def _par_chains(tmp_path, iz: bytes, fz: bytes):
     p = tmp_path / "payloads.bin"
-    iz, fz = _zlib(ib, 6), _zlib(fb, 9)
     p.write_bytes(len(iz).to_bytes(8, "little") + iz + fz)
     code = r"""
 import sys
