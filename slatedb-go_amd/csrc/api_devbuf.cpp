@@ -15,7 +15,8 @@
 
 struct slate_devbuf {
   int device = 0;
-  void* p = nullptr;
+  void* p = nullptr;     // base + kDevGuard (readable bytes in front, as DevBuf)
+  void* base = nullptr;
   uint64_t size = 0;
 };
 
@@ -47,12 +48,13 @@ slate_devbuf* slate_devbuf_alloc(slate_ctx* ctx, uint64_t bytes, int* status) {
   b->device = ctx->device;
   b->size = bytes;
   // a zero-byte buffer still has a valid, distinct address (16 bytes: the decode kernels' alignment)
-  const hipError_t e = hipMalloc(&b->p, std::max<uint64_t>(bytes, 16));
+  const hipError_t e = hipMalloc(&b->base, std::max<uint64_t>(bytes, 16) + kDevGuard);
   if (e != hipSuccess) {
     delete b;
     *status = hip_status(e);
     return nullptr;
   }
+  b->p = static_cast<uint8_t*>(b->base) + kDevGuard;
   *status = SLATE_OK;
   return b;
 }
@@ -61,7 +63,7 @@ void slate_devbuf_free(slate_devbuf* b) {
   if (!b) return;
   (void)hipSetDevice(b->device);
   // hipFree synchronises the device: no kernel still reads or writes the buffer afterwards
-  if (b->p) (void)hipFree(b->p);
+  if (b->base) (void)hipFree(b->base);
   delete b;
 }
 

@@ -18,17 +18,24 @@
 
 #include "kernels.h"
 
+// Device allocations keep kDevGuard readable bytes in front of p: the wave decoders' HBM mode
+// (blocks beyond the LDS budget, index / filter payloads) reads the aligned dword or chunk around a
+// block's first byte, which for a block at offset 0 lies before the buffer.
+constexpr size_t kDevGuard = 256;
 struct DevBuf {
   void* p = nullptr;
+  void* base = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     size_t c = n < 4096 ? 4096 : n + n / 4;
-    hipError_t e = hipMalloc(&p, c);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipMalloc(&base, c + kDevGuard);
+    if (e != hipSuccess) {
+      base = nullptr;
+      return e;
+    }
+    p = static_cast<uint8_t*>(base) + kDevGuard;
     cap = c;
     return hipSuccess;
   }
@@ -37,24 +44,28 @@ struct DevBuf {
     if (n <= cap) return hipSuccess;
     void* q = nullptr;
     size_t c = n + n / 2;
-    hipError_t e = hipMalloc(&q, c);
+    hipError_t e = hipMalloc(&q, c + kDevGuard);
     if (e != hipSuccess) return e;
+    void* qp = static_cast<uint8_t*>(q) + kDevGuard;
     if (p && keep) {
-      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, st);
-      if (e != hipSuccess) return e;
-      e = hipStreamSynchronize(st);
-      if (e != hipSuccess) return e;
+      e = hipMemcpyAsync(qp, p, keep, hipMemcpyDeviceToDevice, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e != hipSuccess) {
+        (void)hipFree(q);
+        return e;
+      }
     }
-    if (p) (void)hipFree(p);
-    p = q;
+    if (base) (void)hipFree(base);
+    base = q;
+    p = qp;
     cap = c;
     return hipSuccess;
   }
   template <typename T>
   T* as() const { return static_cast<T*>(p); }
   void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
+    if (base) (void)hipFree(base);
+    p = base = nullptr;
     cap = 0;
   }
 };

@@ -107,8 +107,10 @@ __device__ inline uint32_t wave_crc_raw(const uint32_t* tab, const uint8_t* lds,
         int64_t p = p0 + 4 * q;
         uint32_t w = 0;
         if (p > -4) {
-          w = lds_u32(lds, int32_t(int64_t(msg) + p));
-          if (p < 0) w &= 0xFFFFFFFFu << (8 * uint32_t(-p));
+          // p < 0: the message's first bytes shifted up (the same word as the aligned read around
+          // msg + p with its leading bytes cleared, without touching bytes before msg: in HBM mode
+          // those can lie before the buffer)
+          w = p < 0 ? lds_u32(lds, msg) << (8 * uint32_t(-p)) : lds_u32(lds, int32_t(int64_t(msg) + p));
           if (fold_init && p < 4) {
             uint32_t m = 0;
             for (int b = 0; b < 4; b++) {
