@@ -1694,8 +1694,18 @@ __global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint
   const int lane = threadIdx.x;
   if (lane < 6) offs[lane] = lane == 1 ? in_len : lane == 3 ? out_sz : lane == 5 ? row_sz : 0;
   uint8_t* din = const_cast<uint8_t*>(a.in);
-  for (uint64_t k = lane; k < (in_len + 15) / 16; k += 64)
-    reinterpret_cast<uint4*>(din)[k] = reinterpret_cast<const uint4*>(host_in)[k];
+  // four 16-byte chunks per lane in flight per round trip over the link (loads first, clamped
+  // indices: no predicated register arrays)
+  const uint32_t nch = uint32_t((in_len + 15) / 16);
+  for (uint32_t k0 = 0; k0 < nch; k0 += 256) {
+    uint4 v[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++)
+      v[u] = reinterpret_cast<const uint4*>(host_in)[min(k0 + 64 * u + uint32_t(lane), nch - 1)];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++)
+      if (k0 + 64 * u + uint32_t(lane) < nch) reinterpret_cast<uint4*>(din)[k0 + 64 * u + lane] = v[u];
+  }
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   load_crc_tables(tab);
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // the staged block, before the wave reads it

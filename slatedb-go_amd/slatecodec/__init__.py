@@ -308,8 +308,8 @@ class Context:
         """block.Decode(&b, input, codec) -> (status, meta, Data, Offsets)."""
         a = np.frombuffer(bytes(encoded) or b"\0", dtype=np.uint8)
         cap = max(len(encoded) * 24, 64)
-        out = np.zeros(cap, np.uint8)
-        offs = np.zeros(cap // 2 + 1, np.uint16)
+        out = np.empty(cap, np.uint8)
+        offs = np.empty(cap // 2 + 1, np.uint16)
         meta = np.zeros(1, META_DTYPE)
         ol = C.c_size_t()
         st = lib().slate_block_decode(self._h, codec, _ptr(a), len(encoded), _ptr(out), cap, C.byref(ol),

@@ -1,0 +1,101 @@
+/* Per-call latency of the single-block entry points from C, the way a cgo shim calls them
+ * (tooling for bench.py's per_call leg; tools/percall_bench.py writes the input file):
+ *   slate_block_decode  (block.Decode, internal/sstable/block/block.go:78) against the oracle's
+ *                       or_block_decode (CPU baseline, one thread), same blocks, same order;
+ *   slate_block_seek    (block.NewIteratorAtKey) over one decoded block against or_block_seek.
+ * Input file: u32 n, n x (u32 len, bytes) Snappy blocks, then u32 klen, key bytes (a key of block 0).
+ * usage: percall FILE CALLS   -> one JSON object on stdout */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "slatecodec.h"
+#include "slate_oracle.h"
+
+static double now_us(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static uint32_t rd32(FILE* f) {
+  uint32_t v = 0;
+  if (fread(&v, 4, 1, f) != 1) exit(2);
+  return v;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) return 2;
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) return 2;
+  const int calls = atoi(argv[2]);
+  const uint32_t n = rd32(f);
+  uint8_t** blk = malloc(n * sizeof(uint8_t*));
+  uint32_t* len = malloc(n * 4);
+  for (uint32_t i = 0; i < n; i++) {
+    len[i] = rd32(f);
+    blk[i] = malloc(len[i] + 16);
+    if (fread(blk[i], 1, len[i], f) != len[i]) return 2;
+  }
+  const uint32_t klen = rd32(f);
+  uint8_t* key = malloc(klen + 1);
+  if (fread(key, 1, klen, f) != klen) return 2;
+  fclose(f);
+
+  int st = 0;
+  slate_ctx* ctx = slate_ctx_create(0, &st);
+  if (!ctx) return 3;
+  const size_t cap = 1 << 20;
+  uint8_t* out = malloc(cap);
+  uint16_t* offs = malloc(cap);
+  or_row* rows = malloc(sizeof(or_row) * 70000);
+  slate_block_meta m;
+  or_block_meta om;
+  size_t ol = 0;
+
+  /* block.Decode, one block per call */
+  for (int w = 0; w < 20; w++) slate_block_decode(ctx, 1, blk[w % n], len[w % n], out, cap, &ol, &m, offs, cap / 2);
+  double t0 = now_us();
+  for (int c = 0; c < calls; c++) {
+    st = slate_block_decode(ctx, 1, blk[c % n], len[c % n], out, cap, &ol, &m, offs, cap / 2);
+    if (st) return 4;
+  }
+  const double gpu_dec = (now_us() - t0) / calls;
+  t0 = now_us();
+  for (int c = 0; c < calls; c++) {
+    st = or_block_decode(blk[c % n], len[c % n], 1, out, cap, &ol, &om, rows, 70000);
+    if (st) return 5;
+  }
+  const double cpu_dec = (now_us() - t0) / calls;
+
+  /* block.NewIteratorAtKey over block 0 */
+  st = slate_block_decode(ctx, 1, blk[0], len[0], out, cap, &ol, &m, offs, cap / 2);
+  if (st) return 6;
+  uint64_t out_off[2] = {0, (ol + 15) & ~(uint64_t)15};
+  uint32_t qb = 0;
+  uint64_t key_off[2] = {0, klen};
+  slate_seek res;
+  for (int w = 0; w < 20; w++) slate_block_seek(ctx, out, out_off, &m, 1, &qb, key, key_off, 1, &res);
+  t0 = now_us();
+  for (int c = 0; c < calls; c++) {
+    st = slate_block_seek(ctx, out, out_off, &m, 1, &qb, key, key_off, 1, &res);
+    if (st || res.status) return 7;
+  }
+  const double gpu_seek = (now_us() - t0) / calls;
+  uint32_t s0, fl, nw;
+  int32_t fi;
+  t0 = now_us();
+  for (int c = 0; c < calls; c++) {
+    st = or_block_seek(out, m.data_len, offs, m.n_rows, key, klen, &s0, &fi, &fl, &nw);
+    if (st) return 8;
+  }
+  const double cpu_seek = (now_us() - t0) / calls;
+  if (s0 != res.start || fi != res.first_idx) return 9;
+  printf("{\"calls\": %d, \"slate_block_decode_us\": %.2f, \"oracle_block_decode_us_1thread\": %.2f, "
+         "\"slate_block_seek_us\": %.2f, \"oracle_block_seek_us_1thread\": %.2f}\n",
+         calls, gpu_dec, cpu_dec, gpu_seek, cpu_seek);
+  slate_ctx_destroy(ctx);
+  return 0;
+}

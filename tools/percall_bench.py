@@ -55,7 +55,7 @@ def per_call(ctx, sc, ob, wl, calls=400):
     pl = (data0[o] << 8) | data0[o + 1]
     fk_sl = (data0[offs0[0] + 2] << 8) | data0[offs0[0] + 3]
     fk = data0[offs0[0] + 4:offs0[0] + 4 + fk_sl]
-    key = fk[:pl] + data0[o + 4:o + 4 + sl]
+    key = bytes(fk[:pl]) + bytes(data0[o + 4:o + 4 + sl])
     one_off = np.array([0, out_off[1]], np.uint64)
     one_out = out[: int(out_off[1])]
 
@@ -76,7 +76,34 @@ def per_call(ctx, sc, ob, wl, calls=400):
         ctx.decode_batch(sc.SNAPPY, sub, sub_off)
 
     res["slate_block_decode_batch64_us_per_block"] = round(_us(gpu_batch64, max(calls // 8, 10)) / 64, 2)
+    res["python_binding_overhead_note"] = ("the *_us figures above are per Python call (ctypes, numpy "
+                                           "allocations) for both sides; c_abi has the same calls from C")
+    res["c_abi"] = c_harness(blocks, key, calls)
     return res
+
+
+def c_harness(blocks, key, calls):
+    """The same blocks and key through tools/build/percall (C, as a cgo shim calls the library),
+    slate_block_decode / slate_block_seek against the oracle's or_block_decode / or_block_seek."""
+    import struct
+    import subprocess
+    import tempfile
+    exe = os.path.join(REPO, "tools", "build", "percall")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/build/percall not built (make -C tools)"}
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(struct.pack("<I", len(blocks)))
+        for b in blocks:
+            f.write(struct.pack("<I", len(b)) + b)
+        f.write(struct.pack("<I", len(key)) + bytes(key))
+        path = f.name
+    try:
+        r = subprocess.run([exe, path, str(max(calls, 200) * 5)], capture_output=True, text=True, timeout=120)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"failed": r.returncode, "stderr": r.stderr[-400:]}
+    return json.loads(r.stdout)
 
 
 def configs0(ctx, sc, ob, calls=20):
