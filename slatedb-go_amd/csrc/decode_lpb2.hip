@@ -109,6 +109,11 @@ constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
 #ifndef SLATE_REFILL_AT
 #define SLATE_REFILL_AT 0
 #endif
+// flush stores: at the iteration's end (0), or deferred into the next iteration, two after step 0
+// and two after step 1 (1), or one after each step (2)
+#ifndef SLATE_FLUSH_DEFER
+#define SLATE_FLUSH_DEFER 0
+#endif
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
 #endif
@@ -699,6 +704,34 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
   L.fl += min(done, 4u);
 }
 
+// SLATE_FLUSH_DEFER (experiment): the same four transposed stores, their data read from the ring at
+// the end of the iteration into registers, issued between the next iteration's steps instead of
+// back to back (the wave keeps computing while the address unit takes them)
+struct Flush {
+  v4u v[4];
+  uint32_t off[4];
+};
+__device__ __forceinline__ void flush_prepare(Lane& L, bool act, uint8_t* outs, uint32_t lane, Flush& F,
+                                              uint32_t dbg) {
+  const uint32_t done = act ? min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
+  const uint32_t base = L.out_rel + 16 * L.fl;
+  const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+    const uint32_t info_o = __shfl(info, int(o), 64);
+    const uint32_t base_o = __shfl(base, int(o), 64);
+    const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
+    F.v[j] = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)), L.z);
+    F.off[j] = (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB;
+  }
+  L.fl += min(done, 4u);
+}
+__device__ __forceinline__ void flush_issue(const Flush& F, uint32_t j, const Rsrc& R) {
+  __builtin_amdgcn_raw_buffer_store_b128(F.v[j], R.out, F.off[j], 0, kOutCpol);
+}
+
 }  // namespace
 
 // The LZ4 frame descriptor check (HC = second byte of XXH32(FLG .. DictID), seed 0) for the two
@@ -909,6 +942,12 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     // `budget` iterations; the budget only guarantees that the loop ends (an exhausted
     // lane reports SLATE_E_HIP, never a wrong result).
     const uint32_t budget = have ? (L.clen + L.dn) / 2 + 1024 : 0u;
+    Flush F;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      F.v[j] = zero;
+      F.off[j] = kOOB;
+    }
     while (__ballot(have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                     iters < budget)) {
       const bool act = have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
@@ -945,14 +984,26 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       LPB_MARK(absorb);
       if (SLATE_ABSORB_AT == 0) absorb_hole(L, Q, ring);
       lane_step<0, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_FLUSH_DEFER == 1) {
+        flush_issue(F, 0, R);
+        flush_issue(F, 1, R);
+      }
+      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 0, R);
       if (SLATE_ABSORB_AT == 1) absorb_hole(L, Q, ring);
       if (SLATE_REFILL_AT == 1) issue_refill();
       lane_step<1, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_FLUSH_DEFER == 1) {
+        flush_issue(F, 2, R);
+        flush_issue(F, 3, R);
+      }
+      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 1, R);
       if (SLATE_ABSORB_AT == 2) absorb_hole(L, Q, ring);
       if (SLATE_REFILL_AT == 2) issue_refill();
       lane_step<2, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 2, R);
       if (SLATE_ABSORB_AT == 3) absorb_hole(L, Q, ring);
       lane_step<3, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
+      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 3, R);
       // the hole source requested in this iteration (at most one per lane; sc1: L1 bypass),
       // before the flush stores so that vmcnt waits stay static; it is merged at the start of
       // the next iteration
@@ -963,7 +1014,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         __builtin_amdgcn_raw_buffer_store_b128(ro.row1, R.rows, ro.off1, 0, kRowCpol);
         __builtin_amdgcn_raw_buffer_store_b128(ro.row3, R.rows, ro.off3, 0, kRowCpol);
       }
-      flush_iteration(L, act, outs, lane, R, dbg_bits(a));
+      if (SLATE_FLUSH_DEFER) flush_prepare(L, act, outs, lane, F, dbg_bits(a));
+      else flush_iteration(L, act, outs, lane, R, dbg_bits(a));
       if constexpr (kLz4) {
         // the content checksum's stripes: the chunks just completed (at most four), still in the ring
 #pragma unroll
@@ -971,6 +1023,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       }
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
+    }
+    if (SLATE_FLUSH_DEFER) {  // the last iteration's chunks, before anything reads the output back
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) flush_issue(F, j, R);
     }
     const uint32_t round_cycles = (dbg_bits(a) & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
 
