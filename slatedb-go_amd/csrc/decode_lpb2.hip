@@ -114,6 +114,13 @@ constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
 #ifndef SLATE_FLUSH_DEFER
 #define SLATE_FLUSH_DEFER 0
 #endif
+// row descriptors staged in LDS per lane (4 slots + a pad slot) and written as transposed runs of
+// 3-4 rows (48-64 bytes) when a lane holds three, instead of one scattered 16-byte store per row
+// (needs 80 more LDS bytes per lane: with SLATE_LPB_THREADS=384, 6 waves per CU)
+#ifndef SLATE_ROW_STAGE
+#define SLATE_ROW_STAGE 0
+#endif
+constexpr uint32_t kRowStageSlots = 4, kRowStride = 16 * (kRowStageSlots + 1);
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
 #endif
@@ -189,6 +196,7 @@ struct Lane {
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
   uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
+  uint32_t rs_n, rs_idx0;  // SLATE_ROW_STAGE: rows staged in LDS, the row index of the first
   int32_t fk;    // first key length for the prefix check (row.go:203-206), -1 before row 0 decodes
   uint32_t pl0;  // row 0's prefix-length field: block.go's FirstKey length when offsets[0] == 0
   // CodecLz4 (kLz4 instantiation only): the frame's one data block is payload bytes [s0, sn);
@@ -207,6 +215,7 @@ struct Rsrc {
 struct RowOut {
   v4u row1, row3;
   uint32_t off1, off3;
+  uint8_t* rst;  // SLATE_ROW_STAGE: this lane's row stage in LDS
 };
 
 // CRC32 of the next committed input chunk (bytes outside the block zeroed).
@@ -665,7 +674,13 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
     uint32_t ridx;
     const bool have_row = walk(L, ring, act && !(dbg & 128), row, ridx);
     const uint32_t off = (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB;
-    if (SLATE_ROWS_DEFER) {
+    if (SLATE_ROW_STAGE) {
+      // staged in LDS (slot rs_n; lanes without a row write the pad slot), stored as transposed
+      // runs at the iteration's end (row_flush)
+      const bool st = have_row && !(dbg & 16384);
+      wr128(ro.rst + 16 * (st ? L.rs_n : kRowStageSlots), row, L.z);
+      L.rs_n += st ? 1u : 0u;
+    } else if (SLATE_ROWS_DEFER) {
       if (kSlot == 1) {
         ro.row1 = row;
         ro.off1 = off;
@@ -732,6 +747,27 @@ __device__ __forceinline__ void flush_issue(const Flush& F, uint32_t j, const Rs
   __builtin_amdgcn_raw_buffer_store_b128(F.v[j], R.out, F.off[j], 0, kOutCpol);
 }
 
+// SLATE_ROW_STAGE: the staged rows of every lane holding at least `min_rows` (1 at the round's
+// end, 3 in the loop: a lane adds at most two per iteration), as four transposed stores: in store j
+// lanes 4i..4i+3 write rows 0..3 of the stage of lane 16j+i, runs of 16-64 contiguous bytes.
+__device__ __forceinline__ void row_flush(Lane& L, const uint8_t* rstages, uint32_t lane, const Rsrc& R,
+                                          uint32_t min_rows) {
+  const bool go = L.rs_n >= min_rows;
+  const uint32_t cnt = go ? L.rs_n : 0u;
+  const uint32_t base = L.rows_rel + 16 * L.rs_idx0;
+  const uint32_t wave_lane0 = threadIdx.x - lane;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+    const uint32_t cnt_o = __shfl(cnt, int(o), 64);
+    const uint32_t base_o = __shfl(base, int(o), 64);
+    const v4u v = rd128(rstages + (wave_lane0 + o) * kRowStride + 16 * c, L.z);
+    __builtin_amdgcn_raw_buffer_store_b128(v, R.rows, c < cnt_o ? base_o + 16 * c : kOOB, 0, kRowCpol);
+  }
+  L.rs_idx0 += cnt;
+  L.rs_n -= cnt;
+}
+
 }  // namespace
 
 // The LZ4 frame descriptor check (HC = second byte of XXH32(FLG .. DictID), seed 0) for the two
@@ -794,6 +830,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
+  uint8_t* rstages = ins + kLpb2Threads * kInStride;  // SLATE_ROW_STAGE (empty otherwise)
+  uint8_t* rst = rstages + threadIdx.x * kRowStride;
   // wave-uniform by construction: the buffer resources derived from it must live in SGPRs
   const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
   const uint32_t wave_g = blockIdx.x * (kLpb2Threads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -851,6 +889,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     L.rphase = 0;
     L.rneed = 4;
     L.rsl = L.rpl = L.rflags = L.ro = L.nwalk = 0;
+    L.rs_n = L.rs_idx0 = 0;
     L.fk = -1;
     L.pl0 = 0xFFFFFFFFu;
     L.sn = L.lph = L.mtok = L.hb = 0;
@@ -979,6 +1018,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       // per iteration: the throttle's limit on d, and the end of the committed input (ring positions)
       const uint32_t lim_d = 16 * L.fl + kUnflushed, cend = 16 * L.c_commit;
       RowOut ro;
+      ro.rst = rst;
       ro.off1 = ro.off3 = kOOB;
       ro.row1 = ro.row3 = zero;
       LPB_MARK(absorb);
@@ -1016,6 +1056,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       }
       if (SLATE_FLUSH_DEFER) flush_prepare(L, act, outs, lane, F, dbg_bits(a));
       else flush_iteration(L, act, outs, lane, R, dbg_bits(a));
+      if (SLATE_ROW_STAGE) row_flush(L, rstages, lane, R, 3);
       if constexpr (kLz4) {
         // the content checksum's stripes: the chunks just completed (at most four), still in the ring
 #pragma unroll
@@ -1024,6 +1065,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
     }
+    if (SLATE_ROW_STAGE) row_flush(L, rstages, lane, R, 1);  // the rows still staged
     if (SLATE_FLUSH_DEFER) {  // the last iteration's chunks, before anything reads the output back
 #pragma unroll
       for (uint32_t j = 0; j < 4; j++) flush_issue(F, j, R);
@@ -1239,7 +1281,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
 
 size_t lpb2_lds_bytes() {
-  return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
+  return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride + (SLATE_ROW_STAGE ? kRowStride : 0));
 }
 
 // CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order
