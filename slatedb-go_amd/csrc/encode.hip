@@ -223,31 +223,8 @@ __device__ inline void write_bytes_from_lds(uint8_t* gdst, const uint8_t* lds, u
 
 // rows ‖ BE16 offsets ‖ BE16 count of the block holding KVs [s, e) into buf
 // (block.go:162-182 Add, :54-64 Encode before compression); raw_len bytes.
-// The block's keys and values staged in LDS (k == nullptr: read them from HBM): key bytes of KV i
-// at k + (key_off[i] - kb), value bytes at v + (val_off[i] - vb); k and v 16-aligned.
-struct KvStage {
-  const uint8_t* k = nullptr;
-  uint64_t kb = 0;
-  const uint8_t* v = nullptr;
-  uint64_t vb = 0;
-};
-
-// n bytes from the LDS stage (at offset o of the 16-aligned stage base) to dst (any alignment):
-// four at a time from two aligned dword reads
-__device__ inline void copy_from_stage(uint8_t* dst, const uint8_t* base, uint32_t o, uint32_t n) {
-  uint32_t b = 0;
-  for (; b + 4 <= n; b += 4) {
-    const uint32_t w = lds_u32(base, int32_t(o + b));
-    dst[b] = uint8_t(w);
-    dst[b + 1] = uint8_t(w >> 8);
-    dst[b + 2] = uint8_t(w >> 16);
-    dst[b + 3] = uint8_t(w >> 24);
-  }
-  for (; b < n; b++) dst[b] = base[o + b];
-}
-
 __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
-                               uint8_t* buf, uint32_t raw_len, int lane, const KvStage& kst = KvStage{}) {
+                               uint8_t* buf, uint32_t raw_len, int lane) {
   const uint32_t nrows = e - s;
   const uint32_t data_len = raw_len - 2 * nrows - 2;
   // rows, 64 at a time: prefix (running min of adjacent LCPs), row offset (scan)
@@ -280,9 +257,7 @@ __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool so
       uint8_t* row = buf + off;
       st_be16(row, uint16_t(p16));
       st_be16(row + 2, uint16_t(sl));
-      if (kst.k) copy_from_stage(row + 4, kst.k, uint32_t(a.key_off[i] - kst.kb) + p16, sl);
-      else
-        for (uint32_t b = 0; b < sl; b++) row[4 + b] = key[p16 + b];
+      for (uint32_t b = 0; b < sl; b++) row[4 + b] = key[p16 + b];
       uint8_t* q = row + 4 + sl;
       for (int b = 0; b < 8; b++) q[b] = 0;  // seq 0 (builder.go:162 Row{Value: ...})
       bool tomb = a.tomb[i] != 0;
@@ -291,9 +266,7 @@ __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool so
         uint32_t vl = uint32_t(value_len(a, i));
         st_be32(q + 9, vl);
         const uint8_t* v = a.vals + a.val_off[i];
-        if (kst.v) copy_from_stage(q + 13, kst.v, uint32_t(a.val_off[i] - kst.vb), vl);
-        else
-          for (uint32_t b = 0; b < vl; b++) q[13 + b] = v[b];
+        for (uint32_t b = 0; b < vl; b++) q[13 + b] = v[b];
       }
       st_be16(buf + data_len + 2 * r, uint16_t(off));  // uint16(len(b.data)) (block.go:176)
     }
@@ -405,62 +378,13 @@ __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
       if (lane == 0) big_list[atomicAdd(big_count, 1u)] = b;
       continue;
     }
-    const uint32_t s = block_start[b], e = next[s];
-    // the block's keys and values: staged in the (not yet used) table area with 16-byte loads all in
-    // flight at once, so the rows are assembled from LDS rather than by dependent byte loads from HBM
-    KvStage kst;
-    {
-      const uint64_t k0 = a.key_off[s] & ~uint64_t(15), k1 = align16(a.key_off[e]);
-      const uint64_t v0 = a.val_off[s] & ~uint64_t(15), v1 = align16(a.val_off[e]);
-      const uint32_t nk = uint32_t((k1 - k0) / 16), nv = uint32_t((v1 - v0) / 16);
-      if (16 * uint64_t(nk + nv) <= 2 * kSnapRaw) {
-        uint4* st = reinterpret_cast<uint4*>(table);
-        const uint4* gk = reinterpret_cast<const uint4*>(a.keys + k0);
-        const uint4* gv = reinterpret_cast<const uint4*>(a.vals + v0);
-        for (uint32_t q0 = 0; q0 < nk + nv; q0 += 4 * kWave) {
-          uint4 w[4];
-#pragma unroll
-          for (uint32_t u = 0; u < 4; u++) {
-            const uint32_t q = min(q0 + u * kWave + uint32_t(lane), nk + nv - 1);
-            w[u] = q < nk ? gk[q] : gv[q - nk];
-          }
-#pragma unroll
-          for (uint32_t u = 0; u < 4; u++) {
-            const uint32_t q = q0 + u * kWave + uint32_t(lane);
-            if (q < nk + nv) st[q] = w[u];
-          }
-        }
-        kst.k = reinterpret_cast<const uint8_t*>(table);
-        kst.kb = k0;
-        kst.v = kst.k + 16 * nk;
-        kst.vb = v0;
-        snap_sync();
-      }
-    }
-    assemble_block(a, adj, sorted, s, e, raw, uint32_t(raw_len), lane, kst);
+    const uint32_t s = block_start[b];
+    assemble_block(a, adj, sorted, s, next[s], raw, uint32_t(raw_len), lane);
     uint8_t* dst = slots + snap_slot_off(raw_off[b], b);
     const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), dst, table, owner, lane, kSnapOwner - 1);
     __builtin_amdgcn_s_waitcnt(0);
     __threadfence();  // the encoded bytes (stored by every lane) are read back by every lane
-    // the encoded block back into the (now free) table area with 16-byte loads, its CRC from LDS
-    uint32_t crc;
-    if (clen + 16 <= 2 * kSnapRaw) {
-      uint4* cst = reinterpret_cast<uint4*>(table);
-      const uint4* g = reinterpret_cast<const uint4*>(dst);
-      const uint32_t nq = (clen + 15) / 16;
-      for (uint32_t q0 = 0; q0 < nq; q0 += 4 * kWave) {
-        uint4 w[4];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) w[u] = g[min(q0 + u * kWave + uint32_t(lane), nq - 1)];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++)
-          if (q0 + u * kWave + uint32_t(lane) < nq) cst[q0 + u * kWave + lane] = w[u];
-      }
-      snap_sync();
-      crc = wave_crc32(tab, reinterpret_cast<const uint8_t*>(table), 0, clen, lane);
-    } else {
-      crc = wave_crc32(tab, dst, 0, clen, lane);
-    }
+    const uint32_t crc = wave_crc32(tab, dst, 0, clen, lane);
     if (lane == 0) {
       st_be32(dst + clen, crc);
       csize[b] = clen + 4;
