@@ -371,8 +371,11 @@ __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
   uint16_t* table = reinterpret_cast<uint16_t*>(raw + kSnapRaw + 16);
   uint8_t* owner = reinterpret_cast<uint8_t*>(table + kSnapRaw);
   const bool sorted = (*flags & 1u) == 0;
-  const uint32_t waves = gridDim.x * (kSnapThreads / 64);
-  for (uint32_t b = blockIdx.x * (kSnapThreads / 64) + wave; b < nblocks; b += waves) {
+  // blocks handed out one at a time by a counter (flags word 4, zeroed with the flags): a wave that
+  // drew cheap blocks takes more, so the launch ends when the work does
+  uint32_t* work = const_cast<uint32_t*>(flags) + 4;
+  auto draw = [&]() { return __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(work, 1u) : 0u); };
+  for (uint32_t b = draw(); b < nblocks; b = draw()) {
     const uint64_t raw_len = raw_off[b + 1] - raw_off[b] - 4;
     if (raw_len > kSnapRaw) {
       if (lane == 0) big_list[atomicAdd(big_count, 1u)] = b;
@@ -660,7 +663,7 @@ hipError_t launch_kv_hashes(hipStream_t st, const EncodeArgs& a, uint64_t* hashe
 
 hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w, int num_cus) {
   const uint32_t n = a.n;
-  (void)hipMemsetAsync(w.flags, 0, 16, st);  // flags, maxlen, big_count, status
+  (void)hipMemsetAsync(w.flags, 0, 20, st);  // flags, maxlen, big_count, status, pack work counter
   if (n == 0) return hipGetLastError();
   enc_kv_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.hashes, w.adj, w.flags);
   enc_next_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.adj, w.flags, w.next, w.bytes, w.maxlen);
