@@ -441,6 +441,10 @@ __global__ void enc_compact_kernel(const uint8_t* __restrict__ slots, const uint
 
 // snappy.Encode of one large buffer (bloom filter, index): one wave per 64 KiB
 // chunk, chunk c's encoding at dst + c * kSnapChunkSlot, its length in len[c].
+#ifndef SLATE_SNAP_CHUNK_SERIAL
+#define SLATE_SNAP_CHUNK_SERIAL 4
+#endif
+constexpr uint32_t kSnapChunkSerialProbes = SLATE_SNAP_CHUNK_SERIAL;  // serial probes before a batch (snappy_enc.h)
 __global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __restrict__ src, uint64_t n,
                                                            uint8_t* __restrict__ dst, uint32_t* __restrict__ len) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __rest
     snap_sync();
     uint32_t d;
     if (pn < kSnapMinNonLiteral) d = snap_emit_literal(o, 0, stage, pn, lane);
-    else d = snappy_encode_block_wave(stage, pn, o, table, owner, lane);
+    else d = snappy_encode_block_wave<kSnapChunkSerialProbes>(stage, pn, o, table, owner, lane);
     if (lane == 0) len[c] = d;
   }
 }

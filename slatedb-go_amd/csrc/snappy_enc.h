@@ -46,6 +46,7 @@ struct SnapProbe {
   }
 };
 static __constant__ SnapProbe g_snap_probe = SnapProbe();
+constexpr SnapProbe kSnapProbeConst{};  // the same schedule as compile-time constants (serial probes)
 
 __host__ __device__ constexpr uint64_t snappy_max_encoded_len(uint64_t n) { return 32 + n + n / 6; }
 
@@ -213,6 +214,11 @@ __device__ inline void snap_slot_neighbours(uint32_t h, bool valid, int lane, in
 // table: kSnapMaxTable u16 slots (LDS); owner: kSnapMaxTable bytes (LDS).
 // owner_mask: the owner array has owner_mask + 1 bytes (a power of two); slots that share an owner
 // byte only make the duplicate check fire for nothing (the sort then finds the true neighbours)
+// K > 0: each search for the next match first probes K positions one at a time (wave-uniform, one
+// lane writing the table; golang's order exactly), then goes on with 64-probe batches from probe K.
+// Short literal runs (a bloom filter's bits: ~3 bytes between matches) then cost a few dependent LDS
+// reads instead of a whole batch with its duplicate-slot sort.
+template <uint32_t K = 0>
 __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table,
                                              uint8_t* owner, int lane, uint32_t owner_mask = kSnapMaxTable - 1) {
   uint32_t shift;
@@ -227,16 +233,34 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
   uint32_t cu[5], cn[5];
 #pragma unroll
   for (uint32_t k = 0; k < 5; k++) {
-    cu[k] = g_snap_probe.cum[64 * k + uint32_t(lane)];
-    cn[k] = g_snap_probe.cum[64 * k + uint32_t(lane) + 1];
+    cu[k] = g_snap_probe.cum[min(64 * k + uint32_t(lane) + K, kProbeSlots)];
+    cn[k] = g_snap_probe.cum[min(64 * k + uint32_t(lane) + K + 1, kProbeSlots)];
   }
 #endif
   for (;;) {
     // ---------------- probe loop, 64 probes per batch
     int32_t cand = 0;
-    bool found = false;
-    for (uint32_t t0 = 0;; t0 += kWave) {
-      const uint32_t t = t0 + lane;
+    bool found = false, remainder = false;
+#pragma unroll
+    for (uint32_t t = 0; t < K; t++) {
+      const int32_t st = s + int32_t(kSnapProbeConst.cum[t]);
+      if (s + int32_t(kSnapProbeConst.cum[t + 1]) > s_limit) {  // nextS > sLimit: emitRemainder
+        remainder = true;
+        break;
+      }
+      const uint32_t cur = snap_ld32(src + st);
+      const uint32_t h = snap_hash(cur, shift);
+      const int32_t c = int32_t(table[h]);
+      if (lane == 0) table[h] = uint16_t(st);  // (LDS accesses of a wave stay in order)
+      if (cur == snap_ld32(src + c)) {
+        s = st;
+        cand = c;
+        found = true;
+        break;
+      }
+    }
+    for (uint32_t t0 = 0; !found && !remainder; t0 += kWave) {
+      const uint32_t t = K + t0 + lane;
       const bool in_sched = t + 1 <= kProbeSlots;
 #if SLATE_SNAP_CUMREG
       const uint32_t kb = t0 >> 6;  // wave-uniform
