@@ -31,6 +31,15 @@
 namespace slate {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+// golang/snappy searches: serial probes before each 64-probe batch (snappy_enc.h) for the filter /
+// index chunks and for the data blocks
+#ifndef SLATE_SNAP_CHUNK_SERIAL
+#define SLATE_SNAP_CHUNK_SERIAL 8
+#endif
+#ifndef SLATE_SNAP_PACK_SERIAL
+#define SLATE_SNAP_PACK_SERIAL 0
+#endif
+constexpr uint32_t kSnapChunkSerialProbes = SLATE_SNAP_CHUNK_SERIAL;  // serial probes before a batch (snappy_enc.h)
 
 // ------------------------------------------------------------------ KV pass
 __global__ void enc_kv_kernel(EncodeArgs a, uint64_t* __restrict__ hashes, uint32_t* __restrict__ adj,
@@ -384,7 +393,8 @@ __global__ __launch_bounds__(kSnapThreads) void enc_pack_snappy_kernel(
     const uint32_t s = block_start[b];
     assemble_block(a, adj, sorted, s, next[s], raw, uint32_t(raw_len), lane);
     uint8_t* dst = slots + snap_slot_off(raw_off[b], b);
-    const uint32_t clen = snappy_encode_wave(raw, uint32_t(raw_len), dst, table, owner, lane, kSnapOwner - 1);
+    const uint32_t clen =
+        snappy_encode_wave<SLATE_SNAP_PACK_SERIAL>(raw, uint32_t(raw_len), dst, table, owner, lane, kSnapOwner - 1);
     __builtin_amdgcn_s_waitcnt(0);
     __threadfence();  // the encoded bytes (stored by every lane) are read back by every lane
     const uint32_t crc = wave_crc32(tab, dst, 0, clen, lane);
@@ -441,10 +451,6 @@ __global__ void enc_compact_kernel(const uint8_t* __restrict__ slots, const uint
 
 // snappy.Encode of one large buffer (bloom filter, index): one wave per 64 KiB
 // chunk, chunk c's encoding at dst + c * kSnapChunkSlot, its length in len[c].
-#ifndef SLATE_SNAP_CHUNK_SERIAL
-#define SLATE_SNAP_CHUNK_SERIAL 4
-#endif
-constexpr uint32_t kSnapChunkSerialProbes = SLATE_SNAP_CHUNK_SERIAL;  // serial probes before a batch (snappy_enc.h)
 __global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __restrict__ src, uint64_t n,
                                                            uint8_t* __restrict__ dst, uint32_t* __restrict__ len) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -351,6 +351,7 @@ __device__ __forceinline__ uint32_t snappy_encode_block_wave(const uint8_t* src,
 }
 
 // snappy.Encode (encode.go:17-42): uvarint length, then 64 KiB blocks.
+template <uint32_t K = 0>
 __device__ __forceinline__ uint32_t snappy_encode_wave(const uint8_t* src, uint32_t n, uint8_t* dst, uint16_t* table, uint8_t* owner,
                                        int lane, uint32_t owner_mask = kSnapMaxTable - 1) {
   uint32_t d = 0;
@@ -367,7 +368,7 @@ __device__ __forceinline__ uint32_t snappy_encode_wave(const uint8_t* src, uint3
   for (uint32_t p = 0; p < n;) {
     const uint32_t pn = min(n - p, kSnapMaxBlock);
     if (pn < kSnapMinNonLiteral) d = snap_emit_literal(dst, d, src + p, pn, lane);
-    else d += snappy_encode_block_wave(src + p, pn, dst + d, table, owner, lane, owner_mask);
+    else d += snappy_encode_block_wave<K>(src + p, pn, dst + d, table, owner, lane, owner_mask);
     p += pn;
   }
   snap_sync();
