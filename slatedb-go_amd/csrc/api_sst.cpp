@@ -96,7 +96,8 @@ int ctx_snappy_encode_device(slate_ctx* ctx, const uint8_t* d_src, size_t n, std
 // appended (bloom.Encode / encodeIndex framing).  slots / asmb / crcb: the buffers it may use;
 // lanes: large copies through the context's page-locked lanes (only from the context's own thread).
 static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, DevBuf& asmb, DevBuf& crcb,
-                                const uint8_t* d_src, size_t n, std::vector<uint8_t>& out, bool lanes) {
+                                const uint8_t* d_src, size_t n, std::vector<uint8_t>& out, bool lanes,
+                                const std::function<void()>* launched = nullptr) {
   SLATE_HIP(ctx_bind(ctx));
   const uint64_t nch = (uint64_t(n) + kSnapMaxChunk - 1) / kSnapMaxChunk;
   SLATE_HIP(slotb.ensure(nch * kSnapChunkSlot + nch * 12 + 64));
@@ -106,6 +107,8 @@ static int snappy_encode_crc_on(slate_ctx* ctx, hipStream_t st, DevBuf& slotb, D
   {
     GpuSpan gs(ctx, st);
     SLATE_HIP(launch_snappy_chunks(st, d_src, n, slots, lens, ctx->num_cus));
+    gs.stop();
+    if (launched) (*launched)();  // (before the span's destructor waits for the kernel, timing on)
   }
   std::vector<uint32_t> hl(nch);
   if (nch) SLATE_HIP(hipMemcpyAsync(hl.data(), lens, nch * 4, hipMemcpyDeviceToHost, st));
@@ -991,6 +994,9 @@ struct slate_sst_table {
 struct slate_sst_builder {
   slate_ctx* ctx;
   slate_sst_config cfg;
+  // Snappy filter beside the final flush: 1 while its chunk encode is not yet queued (the flush then
+  // holds its pack launch, so the filter's serial chains get CUs before the pack fills them), 2 after
+  std::atomic<int> filter_gate{0};
   // pending KVs (not yet in a finished block), on the device: key / value bytes, n+1 offsets
   // into them, tombstone flags
   DevBuf d_keys, d_vals, d_koff, d_voff, d_tomb, d_tmp;
@@ -1213,6 +1219,10 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     SLATE_HIP(ctx->s_aux.ensure((nb + 1) * 8 + 64));
     uint8_t* slots = ctx->s_slots.as<uint8_t>() + 16;
     uint64_t* csize = ctx->s_aux.as<uint64_t>();
+    // the filter's chunk encode queued first (it holds one CU per 64 KiB piece for its serial
+    // chains; launched after the pack it would wait for the whole pack): at most 20 ms
+    for (int spin = 0; final && b->filter_gate.load() == 1 && spin < 1000; spin++)
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
     GpuSpan g_pack(ctx, st);
     SLATE_HIP(hipMemsetAsync(csize + nb, 0, 8, st));
     SLATE_HIP(launch_pack_snappy(st, a, w, uint32_t(nb), w.block_size, slots, csize, ctx->num_cus));
@@ -1520,7 +1530,20 @@ struct FilterOut {
   std::vector<uint8_t> bits;
 };
 
+// SLATE_FILTER_FIRST=0: the flush does not hold its pack for the filter's chunk launch (A/B runs)
+static bool filter_first() {
+  static const bool on = [] {
+    const char* e = getenv("SLATE_FILTER_FIRST");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
+  struct GateOpen {
+    slate_sst_builder* b;
+    ~GateOpen() { b->filter_gate.store(2); }
+  } gate_open{b};
   FilterOut f;
   slate_ctx* ctx = b->ctx;
   auto fail = [&](int st) {
@@ -1553,17 +1576,27 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
       s = hip(launch_bloom_build(st, b->d_hashes.as<uint64_t>(), n_hashes, f.np, uint32_t(nb * 8), words));
     }
   }
-  if (!s) s = hip(hipMemcpyAsync(enc, hdr, 2, hipMemcpyHostToDevice, st));
+  // the BE16 header by two device memsets (a pageable host-to-device copy would hold this thread until
+  // the stream drains, delaying the launches queued behind it)
+  if (!s) s = hip(hipMemsetAsync(enc, hdr[0], 1, st));
+  if (!s) s = hip(hipMemsetAsync(enc + 1, hdr[1], 1, st));
   if (!s && nb) s = hip(hipMemcpyAsync(enc + 2, words, nb, hipMemcpyDeviceToDevice, st));
   f.bits.resize(nb);
-  if (!s && nb) s = hip(hipMemcpyAsync(f.bits.data(), words, nb, hipMemcpyDeviceToHost, st));
-  if (!s) s = hip(hipStreamSynchronize(st));
-  if (s) return fail(s);
   if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
-    s = snappy_encode_crc_on(ctx, st, ctx->x_slots, ctx->x_asm, ctx->x_crc, enc, nb + 2, f.section, false);
+    // the Snappy chunks are queued right behind the bloom build, ahead of the bits' copy to the host:
+    // launched before the flush's pack kernel takes every CU's LDS, the filter's serial chains run
+    // beside the pack instead of after it
+    if (s) return fail(s);
+    const std::function<void()> launched = [b] { b->filter_gate.store(2); };
+    s = snappy_encode_crc_on(ctx, st, ctx->x_slots, ctx->x_asm, ctx->x_crc, enc, nb + 2, f.section, false, &launched);
+    if (!s && nb) s = hip(hipMemcpyAsync(f.bits.data(), words, nb, hipMemcpyDeviceToHost, st));
+    if (!s) s = hip(hipStreamSynchronize(st));
     if (s) return fail(s);
     return f;
   }
+  if (!s && nb) s = hip(hipMemcpyAsync(f.bits.data(), words, nb, hipMemcpyDeviceToHost, st));
+  if (!s) s = hip(hipStreamSynchronize(st));
+  if (s) return fail(s);
   // CodecNone: BE16 numProbes || bits || BE32 CRC (the CRC on the device)
   s = hip(ctx->x_crc.ensure(crc_scratch_bytes(nb + 2) + 16));
   if (s) return fail(s);
@@ -1602,6 +1635,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
                            b->num_keys >= b->cfg.min_filter_keys;
   std::future<FilterOut> fjob;
   const std::function<void(uint64_t)> start_filter = [&](uint64_t nh) {
+    if (b->cfg.codec == SLATE_CODEC_SNAPPY && filter_first()) b->filter_gate.store(1);
     fjob = std::async(std::launch::async, build_filter_aux, b, nh);
   };
   // the index flatbuffer (host work) is built beside the last blocks' D2H and the filter's encode:
