@@ -72,7 +72,8 @@ def mixed_blocks(n_blocks: int, seed: int = 20250307, block_size: int = 4096):
     """BASELINE configs[4] decoded blocks (1 KiB V-half values, Zipf-prefixed 8-256 B keys)."""
     out = np.empty(n_blocks * (block_size + 256), np.uint8)
     off = np.zeros(n_blocks + 1, np.uint64)
-    nb = lib().bg_build_mixed(seed, n_blocks * 8 + 64, block_size, out.ctypes.data, off.ctypes.data, n_blocks)
+    kvs = n_blocks * max(8, block_size // 512) + 64  # (1 KiB values: enough KVs for every block)
+    nb = lib().bg_build_mixed(seed, kvs, block_size, out.ctypes.data, off.ctypes.data, n_blocks)
     assert nb == n_blocks, (nb, n_blocks)
     return out[: int(off[nb])], off
 
