@@ -31,6 +31,10 @@
 namespace slate {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+#ifndef SLATE_PACK_STAGE  // CodecNone pack: stage the block's keys and values in LDS first (1) or not (0)
+#define SLATE_PACK_STAGE 1
+#endif
+constexpr bool kPackStage = SLATE_PACK_STAGE != 0;
 // golang/snappy searches: serial probes before each 64-probe batch (snappy_enc.h) for the filter /
 // index chunks and for the data blocks
 #ifndef SLATE_SNAP_CHUNK_SERIAL
@@ -232,8 +236,65 @@ __device__ inline void write_bytes_from_lds(uint8_t* gdst, const uint8_t* lds, u
 
 // rows ‖ BE16 offsets ‖ BE16 count of the block holding KVs [s, e) into buf
 // (block.go:162-182 Add, :54-64 Encode before compression); raw_len bytes.
+// The block's keys and values staged in LDS (k == nullptr: read them from HBM): key bytes of KV i
+// at k + (key_off[i] - kb), value bytes at v + (val_off[i] - vb); k and v 16-aligned.
+struct KvStage {
+  const uint8_t* k = nullptr;
+  uint64_t kb = 0;
+  const uint8_t* v = nullptr;
+  uint64_t vb = 0;
+};
+
+// n bytes from the LDS stage (offset o of its 16-aligned base) to dst (any alignment), four at a
+// time from two aligned dword reads
+__device__ inline void copy_from_stage(uint8_t* dst, const uint8_t* base, uint32_t o, uint32_t n) {
+  uint32_t b = 0;
+  for (; b + 4 <= n; b += 4) {
+    const uint32_t w = lds_u32(base, int32_t(o + b));
+    dst[b] = uint8_t(w);
+    dst[b + 1] = uint8_t(w >> 8);
+    dst[b + 2] = uint8_t(w >> 16);
+    dst[b + 3] = uint8_t(w >> 24);
+  }
+  for (; b < n; b++) dst[b] = base[o + b];
+}
+
+// Keys and values of KVs [s, e) into LDS at st (16-aligned, cap bytes) with 16-byte loads all in
+// flight at once, so the rows are assembled from LDS instead of by dependent byte loads from HBM;
+// an empty stage (read from HBM) when they do not fit.
+__device__ inline KvStage stage_kvs(const EncodeArgs& a, uint32_t s, uint32_t e, uint8_t* st, uint32_t cap, int lane) {
+  KvStage kst;
+  const uint64_t k0 = a.key_off[s] & ~uint64_t(15), k1 = align16(a.key_off[e]);
+  const uint64_t v0 = a.val_off[s] & ~uint64_t(15), v1 = align16(a.val_off[e]);
+  const uint32_t nk = uint32_t((k1 - k0) / 16), nv = uint32_t((v1 - v0) / 16);
+  if (16 * uint64_t(nk + nv) + 16 > cap) return kst;
+  uint4* d = reinterpret_cast<uint4*>(st);
+  const uint4* gk = reinterpret_cast<const uint4*>(a.keys + k0);
+  const uint4* gv = reinterpret_cast<const uint4*>(a.vals + v0);
+  for (uint32_t q0 = 0; q0 < nk + nv; q0 += 4 * kWave) {
+    uint4 w[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t q = min(q0 + u * kWave + uint32_t(lane), nk + nv - 1);
+      w[u] = q < nk ? gk[q] : gv[q - nk];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t q = q0 + u * kWave + uint32_t(lane);
+      if (q < nk + nv) d[q] = w[u];
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  kst.k = st;
+  kst.kb = k0;
+  kst.v = st + 16 * nk;
+  kst.vb = v0;
+  return kst;
+}
+
 __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
-                               uint8_t* buf, uint32_t raw_len, int lane) {
+                               uint8_t* buf, uint32_t raw_len, int lane, const KvStage& kst = KvStage{}) {
   const uint32_t nrows = e - s;
   const uint32_t data_len = raw_len - 2 * nrows - 2;
   // rows, 64 at a time: prefix (running min of adjacent LCPs), row offset (scan)
@@ -266,7 +327,9 @@ __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool so
       uint8_t* row = buf + off;
       st_be16(row, uint16_t(p16));
       st_be16(row + 2, uint16_t(sl));
-      for (uint32_t b = 0; b < sl; b++) row[4 + b] = key[p16 + b];
+      if (kst.k) copy_from_stage(row + 4, kst.k, uint32_t(a.key_off[i] - kst.kb) + p16, sl);
+      else
+        for (uint32_t b = 0; b < sl; b++) row[4 + b] = key[p16 + b];
       uint8_t* q = row + 4 + sl;
       for (int b = 0; b < 8; b++) q[b] = 0;  // seq 0 (builder.go:162 Row{Value: ...})
       bool tomb = a.tomb[i] != 0;
@@ -275,7 +338,9 @@ __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool so
         uint32_t vl = uint32_t(value_len(a, i));
         st_be32(q + 9, vl);
         const uint8_t* v = a.vals + a.val_off[i];
-        for (uint32_t b = 0; b < vl; b++) q[13 + b] = v[b];
+        if (kst.v) copy_from_stage(q + 13, kst.v, uint32_t(a.val_off[i] - kst.vb), vl);
+        else
+          for (uint32_t b = 0; b < vl; b++) q[13 + b] = v[b];
       }
       st_be16(buf + data_len + 2 * r, uint16_t(off));  // uint16(len(b.data)) (block.go:176)
     }
@@ -289,9 +354,10 @@ __device__ void assemble_block(const EncodeArgs& a, const uint32_t* adj, bool so
 
 template <bool kLds>
 __device__ void pack_block(const EncodeArgs& a, const uint32_t* adj, bool sorted, uint32_t s, uint32_t e,
-                           uint8_t* buf, const uint32_t* tab, uint8_t* gdst, uint64_t enc_len, int lane) {
+                           uint8_t* buf, const uint32_t* tab, uint8_t* gdst, uint64_t enc_len, int lane,
+                           const KvStage& kst = KvStage{}) {
   const uint32_t raw_len = uint32_t(enc_len - 4);
-  assemble_block(a, adj, sorted, s, e, buf, raw_len, lane);
+  assemble_block(a, adj, sorted, s, e, buf, raw_len, lane, kst);
   uint32_t crc = wave_crc32(tab, buf, 0, raw_len, lane);
   if (lane == 0) st_be32(buf + raw_len, crc);
   __builtin_amdgcn_wave_barrier();
@@ -321,7 +387,11 @@ __global__ __launch_bounds__(kPackThreads) void enc_pack_kernel(EncodeArgs a, co
       continue;
     }
     uint32_t s = block_start[b];
-    pack_block<true>(a, adj, sorted, s, next[s], buf, tab, out + out_off[b], enc_len, lane);
+    // the KVs staged in the rest of the wave's buffer, past the block (+ CRC and slack)
+    const uint32_t used = uint32_t(align16(enc_len + 16));
+    const KvStage kst = kPackStage && used < kPackCap ? stage_kvs(a, s, next[s], buf + used, kPackCap - used, lane)
+                                                      : KvStage{};
+    pack_block<true>(a, adj, sorted, s, next[s], buf, tab, out + out_off[b], enc_len, lane, kst);
   }
 }
 

@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../slatedb-go_amd"
 make -s
 mkdir -p build/ab_$TAG
 HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -Wno-unused-parameter"
-/opt/rocm/bin/hipcc $HIPFLAGS -mllvm -amdgpu-sched-strategy=max-ilp -Icsrc $FLAGS -c "$SRC" -o build/ab_$TAG/decode_lpb2.hip.o
+/opt/rocm/bin/hipcc $HIPFLAGS ${SCHED--mllvm -amdgpu-sched-strategy=max-ilp} -Icsrc $FLAGS -c "$SRC" -o build/ab_$TAG/decode_lpb2.hip.o
 objs=$(ls build/*.o | grep -v decode_lpb2.hip.o)
 /opt/rocm/bin/hipcc $HIPFLAGS -shared -o lib/libslatecodec_$TAG.so $objs build/ab_$TAG/decode_lpb2.hip.o
 echo lib/libslatecodec_$TAG.so
