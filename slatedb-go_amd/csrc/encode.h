@@ -49,7 +49,7 @@ struct EncodeBufs {
   uint64_t* block_size;  // [n + 1] -> exclusive scan = out_off
   uint32_t* big_list;    // [n]
   uint32_t* flags;       // 4 words: flags, maxlen, big_count, status
-  uint32_t* maxlen;
+  uint32_t* maxlen;      // (not written: enc_next_kernel reduces the longest block per workgroup)
   uint32_t* big_count;
   uint32_t* status;
 };

@@ -46,10 +46,14 @@ constexpr bool kPackStage = SLATE_PACK_STAGE != 0;
 constexpr uint32_t kSnapChunkSerialProbes = SLATE_SNAP_CHUNK_SERIAL;  // serial probes before a batch (snappy_enc.h)
 
 // ------------------------------------------------------------------ KV pass
+__device__ inline uint64_t row_slot(const EncodeArgs& a, uint32_t i, uint32_t p16);
+
+// slot0[i] (optional) = row_slot(i, 0) saturated to u32: enc_next_kernel's row sizes, prefix-free
 __global__ void enc_kv_kernel(EncodeArgs a, uint64_t* __restrict__ hashes, uint32_t* __restrict__ adj,
-                              uint32_t* __restrict__ flags) {
+                              uint32_t* __restrict__ flags, uint32_t* __restrict__ slot0 = nullptr) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
+  if (slot0) slot0[i] = uint32_t(min(row_slot(a, i, 0), uint64_t(0xFFFFFFFFu)));
   const uint8_t* k = a.keys + a.key_off[i];
   uint64_t kl = a.key_off[i + 1] - a.key_off[i];
   uint64_t h = 0xcbf29ce484222325ull;  // FNV-1 64 (hash/fnv New64)
@@ -94,23 +98,66 @@ __device__ inline uint32_t lcp_direct(const EncodeArgs& a, uint32_t x, uint32_t 
 
 // block.Builder.Add fill rule (block.go:171): cur + 2 + v0Size(row) > blockSize
 // rejects unless the block is empty.  prefix = uint16(computePrefixLen(first, key)).
-__global__ void enc_next_kernel(EncodeArgs a, const uint32_t* __restrict__ adj, const uint32_t* __restrict__ flags,
-                                uint32_t* __restrict__ next, uint64_t* __restrict__ bytes,
-                                uint32_t* __restrict__ maxlen) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= a.n) return;
+// Sorted keys (the builder's case): the workgroup's KVs and the kNextWin - 256 after them have their
+// LCP with the previous key and their prefix-free slot size (slot0) staged in LDS, so a KV's walk
+// over the rows of its block reads LDS; a walk that leaves the window continues from HBM.
+// row_slot(k, p16) = slot0[k] - p16 (p16 <= LCP <= key length).  A saturated slot0 (a row of
+// >= 4 GiB) still ends the block when block_size < 2^32 - 2^16, the condition for this path.
+constexpr uint32_t kNextThreads = 256, kNextWin = 1024;
+__global__ __launch_bounds__(kNextThreads) void enc_next_kernel(EncodeArgs a, const uint32_t* __restrict__ adj,
+                                                                const uint32_t* __restrict__ flags,
+                                                                const uint32_t* __restrict__ slot0,
+                                                                uint32_t* __restrict__ next,
+                                                                uint64_t* __restrict__ bytes,
+                                                                uint32_t* __restrict__ wg_max) {
+  __shared__ uint32_t s_adj[kNextWin], s_slot[kNextWin];
+  const uint32_t j0 = blockIdx.x * kNextThreads;
   const bool sorted = (*flags & 1u) == 0;
-  uint64_t cur = 2 + row_slot(a, j, 0);
-  uint32_t p = 0xFFFFFFFFu, k = j + 1;
-  for (; k < a.n; k++) {
-    p = sorted ? min(p, adj[k]) : lcp_direct(a, j, k);
-    uint64_t rs = row_slot(a, k, p & 0xFFFFu);
-    if (cur + rs > a.block_size) break;
-    cur += rs;
+  const bool win = sorted && a.block_size < 0xFFFF0000ull;  // (workgroup-uniform)
+  const uint32_t wend = win ? min(j0 + kNextWin, a.n) : j0;
+  for (uint32_t x = threadIdx.x; j0 + x < wend; x += kNextThreads) {
+    s_adj[x] = adj[j0 + x];
+    s_slot[x] = slot0[j0 + x];
   }
-  next[j] = k;
-  bytes[j] = cur;
-  atomicMax(maxlen, k - j);
+  __syncthreads();
+  const uint32_t j = j0 + threadIdx.x;
+  uint32_t len = 0;
+  if (j < a.n) {
+    uint64_t cur = 2 + row_slot(a, j, 0);
+    uint32_t p = 0xFFFFFFFFu, k = j + 1;
+    bool full = false;
+    for (; k < wend; k++) {
+      p = min(p, s_adj[k - j0]);
+      const uint64_t rs = uint64_t(s_slot[k - j0]) - (p & 0xFFFFu);
+      if (cur + rs > a.block_size) {
+        full = true;
+        break;
+      }
+      cur += rs;
+    }
+    for (; !full && k < a.n; k++) {
+      p = sorted ? min(p, adj[k]) : lcp_direct(a, j, k);
+      uint64_t rs = row_slot(a, k, p & 0xFFFFu);
+      if (cur + rs > a.block_size) break;
+      cur += rs;
+    }
+    next[j] = k;
+    bytes[j] = cur;
+    len = k - j;
+  }
+  // the longest block in KVs, one word per workgroup (wg_max[blockIdx.x]; enc_chain_kernel reduces
+  // them): an atomicMax per wave on one address serialised at ~11 ns each, 1.8 ms per 10 M KVs
+  __shared__ uint32_t s_wmax[kNextThreads / 64];
+#pragma unroll
+  for (int o = 32; o; o >>= 1) len = max(len, uint32_t(__shfl_xor(int(len), o, 64)));
+  if ((threadIdx.x & 63) == 0) s_wmax[threadIdx.x >> 6] = len;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kNextThreads / 64; w++) m = max(m, s_wmax[w]);
+    wg_max[blockIdx.x] = m;
+  }
 }
 
 // ------------------------------------------------------------ block chains
@@ -139,12 +186,27 @@ __global__ __launch_bounds__(kChunkThreads) void enc_exit_kernel(uint32_t n, con
 // prefetched into LDS; the true entry is always inside its chunk's window
 // (W = longest block in KVs).
 __global__ __launch_bounds__(kChunkThreads) void enc_chain_kernel(uint32_t n, const uint32_t* __restrict__ exit_pos,
-                                                                  const uint32_t* __restrict__ maxlen,
-                                                                  uint32_t* __restrict__ entry) {
+                                                                  const uint32_t* __restrict__ wg_max,
+                                                                  uint32_t n_wg, uint32_t* __restrict__ entry) {
   __shared__ uint32_t win[8192];
   __shared__ uint32_t e_sh;
   uint32_t nchunks = (n + kChunk - 1) / kChunk;
-  uint32_t W = min(*maxlen, kChunk);
+  {  // W = the longest block in KVs: the max over enc_next_kernel's per-workgroup words
+    uint32_t m = 0;
+    for (uint32_t x = threadIdx.x; x < n_wg; x += kChunkThreads) m = max(m, wg_max[x]);
+    win[threadIdx.x] = m;
+    __syncthreads();
+    for (uint32_t s = kChunkThreads / 2; s; s >>= 1) {
+      if (threadIdx.x < s) win[threadIdx.x] = max(win[threadIdx.x], win[threadIdx.x + s]);
+      __syncthreads();
+    }
+    m = win[0];
+    __syncthreads();
+    if (threadIdx.x == 0) e_sh = m;
+  }
+  __syncthreads();
+  uint32_t W = min(e_sh, kChunk);
+  __syncthreads();
   if (W == 0) W = 1;
   uint32_t G = max(1u, 8192u / W);
   if (threadIdx.x == 0) e_sh = 0;
@@ -745,11 +807,14 @@ hipError_t launch_encode(hipStream_t st, const EncodeArgs& a, const EncodeBufs& 
   const uint32_t n = a.n;
   (void)hipMemsetAsync(w.flags, 0, 20, st);  // flags, maxlen, big_count, status, pack work counter
   if (n == 0) return hipGetLastError();
-  enc_kv_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.hashes, w.adj, w.flags);
-  enc_next_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.adj, w.flags, w.next, w.bytes, w.maxlen);
+  // slot0 lives in exit_pos until enc_exit_kernel overwrites it
+  enc_kv_kernel<<<blocks_for(n, 256), 256, 0, st>>>(a, w.hashes, w.adj, w.flags, w.exit_pos);
+  // the per-workgroup longest blocks live in starts_tmp until enc_mark_kernel writes it
+  const uint32_t n_wg = blocks_for(n, kNextThreads);
+  enc_next_kernel<<<n_wg, kNextThreads, 0, st>>>(a, w.adj, w.flags, w.exit_pos, w.next, w.bytes, w.starts_tmp);
   uint32_t nchunks = blocks_for(n, kChunk);
   enc_exit_kernel<<<nchunks, kChunkThreads, 0, st>>>(n, w.next, w.exit_pos);
-  enc_chain_kernel<<<1, kChunkThreads, 0, st>>>(n, w.exit_pos, w.maxlen, w.entry);
+  enc_chain_kernel<<<1, kChunkThreads, 0, st>>>(n, w.exit_pos, w.starts_tmp, n_wg, w.entry);
   enc_mark_kernel<<<nchunks, kChunkThreads, 0, st>>>(n, w.next, w.entry, w.starts_tmp, w.counts);
   return hipGetLastError();
 }
@@ -895,15 +960,39 @@ __global__ void kv_pick_len_kernel(const uint32_t* __restrict__ idx, uint64_t m,
   if (i == m) len[m] = 0;
 }
 
-// one wave per picked key
-__global__ void kv_pick_copy_kernel(const uint32_t* __restrict__ idx, uint64_t m, const uint8_t* __restrict__ keys,
-                                    const uint64_t* __restrict__ key_off, const uint64_t* __restrict__ out_off,
-                                    uint8_t* __restrict__ out) {
-  const uint64_t w = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+// one lane per picked key (a block's first key: a few dozen bytes), 16 loads in flight per lane; a
+// key longer than kPickLane bytes is copied by the whole wave afterwards, one such key at a time
+constexpr uint32_t kPickLane = 256;
+__global__ __launch_bounds__(256) void kv_pick_copy_kernel(const uint32_t* __restrict__ idx, uint64_t m,
+                                                           const uint8_t* __restrict__ keys,
+                                                           const uint64_t* __restrict__ key_off,
+                                                           const uint64_t* __restrict__ out_off,
+                                                           uint8_t* __restrict__ out) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63;
-  if (w >= m) return;
-  const uint64_t s = key_off[idx[w]], l = key_off[idx[w] + 1] - s, o = out_off[w];
-  for (uint64_t k = lane; k < l; k += 64) out[o + k] = keys[s + k];
+  uint64_t s = 0, l = 0, o = 0;
+  if (i < m) {
+    s = key_off[idx[i]];
+    l = key_off[idx[i] + 1] - s;
+    o = out_off[i];
+  }
+  if (l <= kPickLane) {
+    for (uint64_t k = 0; k < l; k += 16) {
+      uint8_t v[16];
+#pragma unroll
+      for (uint32_t t = 0; t < 16; t++) v[t] = k + t < l ? keys[s + k + t] : 0;
+#pragma unroll
+      for (uint32_t t = 0; t < 16; t++)
+        if (k + t < l) out[o + k + t] = v[t];
+    }
+  }
+  uint64_t longs = __ballot(l > kPickLane);
+  while (longs) {
+    const int src = __builtin_ctzll(longs);
+    longs &= longs - 1;
+    const uint64_t ws = __shfl(s, src, 64), wl = __shfl(l, src, 64), wo = __shfl(o, src, 64);
+    for (uint64_t k = lane; k < wl; k += 64) out[wo + k] = keys[ws + k];
+  }
 }
 
 hipError_t launch_kv_rebase(hipStream_t st, const uint64_t* src, uint64_t n, uint64_t* dst, uint64_t base) {
@@ -932,7 +1021,7 @@ hipError_t launch_kv_pick_keys(hipStream_t st, const uint32_t* idx, uint64_t m, 
   kv_pick_len_kernel<<<uint32_t((m + 256) / 256), 256, 0, st>>>(idx, m, key_off, out_off);
   hipError_t e = launch_scan_u64(st, out_off, uint32_t(m + 1), scratch);
   if (e != hipSuccess) return e;
-  if (m) kv_pick_copy_kernel<<<uint32_t((m * 64 + 255) / 256), 256, 0, st>>>(idx, m, keys, key_off, out_off, out);
+  if (m) kv_pick_copy_kernel<<<uint32_t((m + 255) / 256), 256, 0, st>>>(idx, m, keys, key_off, out_off, out);
   return hipGetLastError();
 }
 

@@ -65,6 +65,29 @@ def test_random_sst_bytes(sc, ctx, seed):
     assert t.bloom() == o.bloom()
 
 
+@pytest.mark.parametrize("case", ["many_rows", "long_first_keys"])
+def test_segmentation_windows_and_first_keys(sc, ctx, case):
+    """enc_next_kernel's LDS window (1024 KVs from a workgroup's first) and kv_pick_copy_kernel's
+    lane / wave split (first keys longer than 256 bytes): blocks of ~4000 tiny rows walk past the
+    window into HBM; long first keys are copied by the wave, short ones by their lane."""
+    rng = random.Random(7)
+    if case == "many_rows":
+        kvs = [(b"%08d" % i, b"" if i % 5 else b"v") for i in range(60000)]
+        bs = 65536
+    else:
+        kvs = []
+        for i in range(3000):
+            k = b"%06d" % i
+            if rng.random() < 0.3:
+                k += bytes(rng.randrange(256) for _ in range(rng.choice([250, 257, 300, 1000, 5000])))
+            kvs.append((k, bytes(rng.randrange(256) for _ in range(rng.randrange(1, 600)))))
+        bs = 4096
+    for batch in (True, False):
+        t, o, _ = _build_both(sc, ctx, kvs, bs, batch=batch)
+        assert t.encode() == o.encode_table()
+        assert t.info() == o.info()
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_next_block_after_each_add(sc, ctx, seed):
     """sstable.Builder.NextBlock timing (builder.go:160-190): after every AddValue, the blocks the
