@@ -1565,6 +1565,8 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
   auto hip = [&](hipError_t e) { return e == hipSuccess ? SLATE_OK : hip_status(e); };
   int s = hip(ctx->x_words.ensure(((nb + 3) & ~uint64_t(3)) + 16));
   if (!s) s = hip(ctx->x_enc.ensure(nb + 2 + 16));
+  const size_t bkt = nb ? bloom_bucket_scratch_bytes(n_hashes, f.np, uint32_t(nb * 8)) : 0;
+  if (!s && bkt) s = hip(ctx->x_bkt.ensure(bkt));
   if (s) return fail(s);
   uint32_t* words = ctx->x_words.as<uint32_t>();
   uint8_t* enc = ctx->x_enc.as<uint8_t>();
@@ -1573,7 +1575,8 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
     s = hip(hipMemsetAsync(words, 0, (nb + 3) & ~uint64_t(3), st));
     if (!s) {
       GpuSpan gs(ctx, st);
-      s = hip(launch_bloom_build(st, b->d_hashes.as<uint64_t>(), n_hashes, f.np, uint32_t(nb * 8), words));
+      s = hip(launch_bloom_build_bucketed(st, b->d_hashes.as<uint64_t>(), n_hashes, f.np, uint32_t(nb * 8), words,
+                                          bkt ? ctx->x_bkt.p : nullptr));
     }
   }
   // the BE16 header by two device memsets (a pageable host-to-device copy would hold this thread until

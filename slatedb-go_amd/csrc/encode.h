@@ -61,6 +61,12 @@ hipError_t launch_pack(hipStream_t st, const EncodeArgs& a, const EncodeBufs& w,
                        const uint64_t* out_off, uint8_t* out, int num_cus);
 hipError_t launch_bloom_build(hipStream_t st, const uint64_t* hashes, uint64_t n, uint32_t num_probes,
                               uint32_t filter_bits, uint32_t* words);
+// The same bits (words zeroed beforehand) without global atomics: probes bucketed per 64 KiB slice of
+// the filter, each slice OR-ed in LDS.  Scratch bytes from bloom_bucket_scratch_bytes; 0 there means
+// the shape is outside the bucketed path's bounds, and the call runs launch_bloom_build.
+size_t bloom_bucket_scratch_bytes(uint64_t n, uint32_t num_probes, uint32_t filter_bits);
+hipError_t launch_bloom_build_bucketed(hipStream_t st, const uint64_t* hashes, uint64_t n, uint32_t num_probes,
+                                       uint32_t filter_bits, uint32_t* words, void* scratch);
 hipError_t launch_bloom_check(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, uint64_t n,
                               const uint8_t* bits, uint64_t bits_len, uint32_t num_probes, uint8_t* out);
 // Snappy (golang/snappy byte-exact) block and buffer encode

@@ -639,6 +639,89 @@ __global__ void bloom_build_kernel(const uint64_t* __restrict__ hashes, uint64_t
   }
 }
 
+// Bucketed build: the same probes, no global atomics.  ~70 M scattered device-scope atomicOr for a
+// 10 M-key filter ran at ~30 G/s (2.35 ms); here a workgroup of keys counts its probes per 64 KiB
+// slice of the filter (LDS histogram), a scan gives every (slice, workgroup) its range of a probe
+// array, the workgroup scatters its probes there, and one workgroup per slice ORs the slice's probes
+// into LDS and writes the slice out.  OR is order-free: the bits are the atomic kernel's.
+constexpr uint32_t kBktThreads = 256, kBktKeysPerThread = 8, kBktKeys = kBktThreads * kBktKeysPerThread;
+constexpr uint32_t kBktSliceLog = 19;  // 2^19 bits = 64 KiB of LDS per slice
+constexpr uint32_t kBktMaxSlices = 8192, kBktOrThreads = 1024;
+constexpr uint64_t kBktMaxCells = 1ull << 24;  // (slices x key workgroups) counters
+
+struct BloomProbes {
+  uint64_t h, delta, m;
+  uint32_t k;
+  __device__ BloomProbes(uint64_t h64, uint32_t filter_bits) : m(filter_bits), k(0) {
+    h = (h64 & 0xFFFFFFFFull) % m;
+    delta = (h64 >> 32) % m;
+  }
+  __device__ uint32_t next() {  // bloom.go:147-160, as bloom_build_kernel
+    delta = (delta + k++) % m;
+    const uint32_t p = uint32_t(h);
+    h = (h + delta) % m;
+    return p;
+  }
+};
+
+__global__ __launch_bounds__(kBktThreads) void bloom_count_kernel(const uint64_t* __restrict__ hashes, uint64_t n,
+                                                                  uint32_t num_probes, uint32_t filter_bits,
+                                                                  uint32_t n_slices, uint64_t* __restrict__ cells) {
+  __shared__ uint32_t hist[kBktMaxSlices];
+  for (uint32_t s = threadIdx.x; s < n_slices; s += kBktThreads) hist[s] = 0;
+  __syncthreads();
+  const uint64_t k0 = uint64_t(blockIdx.x) * kBktKeys;
+  for (uint32_t r = 0; r < kBktKeysPerThread; r++) {
+    const uint64_t i = k0 + r * kBktThreads + threadIdx.x;
+    if (i >= n) break;
+    BloomProbes pr(hashes[i], filter_bits);
+    for (uint32_t q = 0; q < num_probes; q++) atomicAdd(&hist[pr.next() >> kBktSliceLog], 1u);
+  }
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < n_slices; s += kBktThreads) cells[uint64_t(s) * gridDim.x + blockIdx.x] = hist[s];
+}
+
+__global__ __launch_bounds__(kBktThreads) void bloom_scatter_kernel(const uint64_t* __restrict__ hashes, uint64_t n,
+                                                                    uint32_t num_probes, uint32_t filter_bits,
+                                                                    uint32_t n_slices,
+                                                                    const uint64_t* __restrict__ cells,
+                                                                    uint32_t* __restrict__ probes) {
+  __shared__ uint32_t cur[kBktMaxSlices];
+  for (uint32_t s = threadIdx.x; s < n_slices; s += kBktThreads)
+    cur[s] = uint32_t(cells[uint64_t(s) * gridDim.x + blockIdx.x]);
+  __syncthreads();
+  const uint64_t k0 = uint64_t(blockIdx.x) * kBktKeys;
+  for (uint32_t r = 0; r < kBktKeysPerThread; r++) {
+    const uint64_t i = k0 + r * kBktThreads + threadIdx.x;
+    if (i >= n) break;
+    BloomProbes pr(hashes[i], filter_bits);
+    for (uint32_t q = 0; q < num_probes; q++) {
+      const uint32_t p = pr.next();
+      probes[atomicAdd(&cur[p >> kBktSliceLog], 1u)] = p;
+    }
+  }
+}
+
+// one workgroup per slice: its probes (cells[s * n_wg] .. cells[(s + 1) * n_wg]) OR-ed into LDS
+__global__ __launch_bounds__(kBktOrThreads) void bloom_or_kernel(const uint64_t* __restrict__ cells, uint32_t n_wg,
+                                                                 const uint32_t* __restrict__ probes,
+                                                                 uint32_t filter_bits, uint32_t* __restrict__ words) {
+  __shared__ uint32_t slice[1u << (kBktSliceLog - 5)];
+  const uint32_t s = blockIdx.x;
+  for (uint32_t w = threadIdx.x; w < (1u << (kBktSliceLog - 5)); w += kBktOrThreads) slice[w] = 0;
+  __syncthreads();
+  const uint64_t lo = cells[uint64_t(s) * n_wg], hi = cells[uint64_t(s + 1) * n_wg];
+  for (uint64_t j = lo + threadIdx.x; j < hi; j += kBktOrThreads) {
+    const uint32_t p = probes[j] & ((1u << kBktSliceLog) - 1);
+    atomicOr(&slice[p >> 5], 1u << (p & 31));
+  }
+  __syncthreads();
+  const uint64_t w0 = uint64_t(s) << (kBktSliceLog - 5);
+  const uint64_t total = (uint64_t(filter_bits) + 31) / 32;
+  const uint32_t nw = uint32_t(min(uint64_t(1u << (kBktSliceLog - 5)), total - w0));
+  for (uint32_t w = threadIdx.x; w < nw; w += kBktOrThreads) words[w0 + w] = slice[w];
+}
+
 __global__ void bloom_check_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, uint64_t n,
                                    const uint8_t* __restrict__ bits, uint64_t bits_len, uint32_t num_probes,
                                    uint8_t* __restrict__ out) {
@@ -905,6 +988,49 @@ hipError_t launch_bloom_build(hipStream_t st, const uint64_t* hashes, uint64_t n
                               uint32_t filter_bits, uint32_t* words) {
   if (n == 0) return hipGetLastError();
   bloom_build_kernel<<<uint32_t((n + 255) / 256), 256, 0, st>>>(hashes, n, num_probes, filter_bits, words);
+  return hipGetLastError();
+}
+
+namespace {
+struct BktShape {
+  uint32_t n_slices = 0, n_wg = 0;
+  uint64_t cells = 0;
+  size_t o_scan = 0, o_probes = 0, bytes = 0;
+};
+BktShape bkt_shape(uint64_t n, uint32_t num_probes, uint32_t filter_bits) {
+  BktShape b;
+  if (n < 65536 || num_probes == 0 || filter_bits == 0) return b;  // small filters: the atomic kernel
+  const uint64_t slices = (uint64_t(filter_bits) + (1ull << kBktSliceLog) - 1) >> kBktSliceLog;
+  const uint64_t wg = (n + kBktKeys - 1) / kBktKeys;
+  const uint64_t cells = slices * wg;
+  if (slices > kBktMaxSlices || cells > kBktMaxCells || n * num_probes >= (1ull << 32)) return b;
+  b.n_slices = uint32_t(slices);
+  b.n_wg = uint32_t(wg);
+  b.cells = cells;
+  b.o_scan = ((cells + 1) * 8 + 255) & ~size_t(255);
+  b.o_probes = b.o_scan + ((scan_scratch_bytes(uint32_t(cells + 1)) + 255) & ~size_t(255));
+  b.bytes = b.o_probes + n * num_probes * 4 + 64;
+  return b;
+}
+}  // namespace
+
+size_t bloom_bucket_scratch_bytes(uint64_t n, uint32_t num_probes, uint32_t filter_bits) {
+  return bkt_shape(n, num_probes, filter_bits).bytes;
+}
+
+hipError_t launch_bloom_build_bucketed(hipStream_t st, const uint64_t* hashes, uint64_t n, uint32_t num_probes,
+                                       uint32_t filter_bits, uint32_t* words, void* scratch) {
+  const BktShape b = bkt_shape(n, num_probes, filter_bits);
+  if (!b.bytes || !scratch) return launch_bloom_build(st, hashes, n, num_probes, filter_bits, words);
+  uint8_t* base = static_cast<uint8_t*>(scratch);
+  uint64_t* cells = reinterpret_cast<uint64_t*>(base);
+  uint32_t* probes = reinterpret_cast<uint32_t*>(base + b.o_probes);
+  bloom_count_kernel<<<b.n_wg, kBktThreads, 0, st>>>(hashes, n, num_probes, filter_bits, b.n_slices, cells);
+  hipError_t e = hipMemsetAsync(cells + b.cells, 0, 8, st);
+  if (e == hipSuccess) e = launch_scan_u64(st, cells, uint32_t(b.cells + 1), base + b.o_scan);
+  if (e != hipSuccess) return e;
+  bloom_scatter_kernel<<<b.n_wg, kBktThreads, 0, st>>>(hashes, n, num_probes, filter_bits, b.n_slices, cells, probes);
+  bloom_or_kernel<<<b.n_slices, kBktOrThreads, 0, st>>>(cells, b.n_wg, probes, filter_bits, words);
   return hipGetLastError();
 }
 

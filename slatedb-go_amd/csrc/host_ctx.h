@@ -254,7 +254,7 @@ struct slate_ctx {
   DevBuf c_meta, c_tags, c_bodies, c_seqs, c_out, c_in;
   // SST filter built beside the final flush (api_sst.cpp build_filter_aux): its own stream and buffers
   hipStream_t aux = nullptr;
-  DevBuf x_words, x_enc, x_slots, x_asm, x_crc;
+  DevBuf x_words, x_enc, x_slots, x_asm, x_crc, x_bkt;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
   // device time of the builder's GPU passes (slate_ctx_set_timing): nanoseconds, summed over the
   // kernel groups of every stream the context uses (GpuSpan)
@@ -304,7 +304,7 @@ struct slate_ctx {
     if (seg_pool) seg_pool->close();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
                       &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &e_k, &s_slots, &s_raw, &s_aux, &c_meta,
-                      &c_tags, &c_bodies, &c_seqs, &c_out, &c_in, &x_words, &x_enc, &x_slots, &x_asm, &x_crc})
+                      &c_tags, &c_bodies, &c_seqs, &c_out, &c_in, &x_words, &x_enc, &x_slots, &x_asm, &x_crc, &x_bkt})
       b->release();
     if (aux) (void)hipStreamDestroy(aux);
     aux = nullptr;

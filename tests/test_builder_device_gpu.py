@@ -118,3 +118,21 @@ def test_large_device_batch(sc, ctx):
     assert o.add_batch(keys, ko.view(np.uint64), vals, vo.view(np.uint64)) == 0
     assert o.build() == 0
     assert g.build().encode() == o.encode_table()
+
+
+@pytest.mark.parametrize("bpk", [1, 7, 23])
+def test_bucketed_bloom_filter_shapes(sc, ctx, bpk):
+    """Filters of >= 64 k keys take the bucketed build (probes per 64 KiB slice OR-ed in LDS):
+    1, 5 and 16 probes, 1-33 slices with a partial last one, bits equal to the oracle's."""
+    n = 90_001
+    kvs = [(k, v or None) for k, v in bg.kv_synthetic(n)]
+    keys, ko, vals, vo, _ = _arrays(kvs)
+    dk, dko, dv, dvo = _dev(keys), _dev(ko), _dev(vals), _dev(vo)
+    g = sc.SstBuilder(ctx, 4096, 0, bpk, sc.NONE)
+    assert g.add_batch_device(dk.data_ptr(), dko.data_ptr(), dv.data_ptr(), dvo.data_ptr(), n) == 0
+    o = ob.SstBuilder(4096, 0, bpk, ob.NONE)
+    assert o.add_batch(keys, ko.view(np.uint64), vals, vo.view(np.uint64)) == 0
+    assert o.build() == 0
+    t = g.build()
+    assert t.bloom() == o.bloom()
+    assert t.encode() == o.encode_table()
