@@ -645,8 +645,14 @@ __global__ void bloom_build_kernel(const uint64_t* __restrict__ hashes, uint64_t
 // array, the workgroup scatters its probes there, and one workgroup per slice ORs the slice's probes
 // into LDS and writes the slice out.  OR is order-free: the bits are the atomic kernel's.
 constexpr uint32_t kBktThreads = 256, kBktKeysPerThread = 8, kBktKeys = kBktThreads * kBktKeysPerThread;
-constexpr uint32_t kBktSliceLog = 19;  // 2^19 bits = 64 KiB of LDS per slice
-constexpr uint32_t kBktMaxSlices = 8192, kBktOrThreads = 1024;
+#ifndef SLATE_BKT_SLICE_LOG
+#define SLATE_BKT_SLICE_LOG 19
+#endif
+#ifndef SLATE_BKT_OR_THREADS
+#define SLATE_BKT_OR_THREADS 1024
+#endif
+constexpr uint32_t kBktSliceLog = SLATE_BKT_SLICE_LOG;  // 2^19 bits = 64 KiB of LDS per slice
+constexpr uint32_t kBktMaxSlices = 8192, kBktOrThreads = SLATE_BKT_OR_THREADS;
 constexpr uint64_t kBktMaxCells = 1ull << 24;  // (slices x key workgroups) counters
 
 struct BloomProbes {
@@ -711,9 +717,22 @@ __global__ __launch_bounds__(kBktOrThreads) void bloom_or_kernel(const uint64_t*
   for (uint32_t w = threadIdx.x; w < (1u << (kBktSliceLog - 5)); w += kBktOrThreads) slice[w] = 0;
   __syncthreads();
   const uint64_t lo = cells[uint64_t(s) * n_wg], hi = cells[uint64_t(s + 1) * n_wg];
-  for (uint64_t j = lo + threadIdx.x; j < hi; j += kBktOrThreads) {
-    const uint32_t p = probes[j] & ((1u << kBktSliceLog) - 1);
-    atomicOr(&slice[p >> 5], 1u << (p & 31));
+  // eight loads in flight per thread before their ORs (one at a time: ~360 dependent round trips)
+  constexpr uint32_t kU = 8;
+  for (uint64_t j0 = lo + threadIdx.x; j0 < hi; j0 += kU * kBktOrThreads) {
+    uint32_t p[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint64_t j = j0 + u * kBktOrThreads;
+      p[u] = j < hi ? probes[j] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      if (j0 + u * kBktOrThreads < hi) {
+        const uint32_t q = p[u] & ((1u << kBktSliceLog) - 1);
+        atomicOr(&slice[q >> 5], 1u << (q & 31));
+      }
+    }
   }
   __syncthreads();
   const uint64_t w0 = uint64_t(s) << (kBktSliceLog - 5);
