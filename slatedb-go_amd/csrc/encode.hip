@@ -48,6 +48,44 @@ constexpr uint32_t kSnapChunkSerialProbes = SLATE_SNAP_CHUNK_SERIAL;  // serial 
 // ------------------------------------------------------------------ KV pass
 __device__ inline uint64_t row_slot(const EncodeArgs& a, uint32_t i, uint32_t p16);
 
+// A key of at most kKvShort bytes as 8 little-endian dwords (bytes past its length zero), read as the
+// aligned dwords that hold it -- all loads in flight at once, then realigned by alignbyte -- instead
+// of one dependent byte load per step (the byte loops kept the KV pass latency-bound).  A dword
+// holding one of the key's bytes lies inside the key buffer's pages, so no load can fault.
+constexpr uint32_t kKvShort = 32;
+__device__ inline void key_words(const uint8_t* k, uint32_t kl, uint32_t (&r)[8]) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(k);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(addr & ~uintptr_t(3));
+  const uint32_t sh = uint32_t(addr & 3);
+  const uint32_t nw = (sh + kl + 3) >> 2;  // aligned dwords holding the key (<= 9)
+  uint32_t w[9];
+#pragma unroll
+  for (uint32_t t = 0; t < 9; t++) w[t] = t < nw ? base[t] : 0u;
+#pragma unroll
+  for (uint32_t t = 0; t < 8; t++) {
+    const int rem = int(kl) - int(4 * t);
+    const uint32_t mask = rem >= 4 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+    r[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh) & mask;
+  }
+}
+
+__device__ inline uint64_t fnv_words(const uint32_t (&r)[8], uint32_t kl) {
+  uint64_t h = 0xcbf29ce484222325ull;  // FNV-1 64 (hash/fnv New64)
+#pragma unroll
+  for (uint32_t b = 0; b < 16; b++) {
+    const uint64_t hn = (h * 0x100000001b3ull) ^ ((r[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+    h = b < kl ? hn : h;
+  }
+  if (kl > 16) {
+#pragma unroll
+    for (uint32_t b = 16; b < 32; b++) {
+      const uint64_t hn = (h * 0x100000001b3ull) ^ ((r[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+      h = b < kl ? hn : h;
+    }
+  }
+  return h;
+}
+
 // slot0[i] (optional) = row_slot(i, 0) saturated to u32: enc_next_kernel's row sizes, prefix-free
 __global__ void enc_kv_kernel(EncodeArgs a, uint64_t* __restrict__ hashes, uint32_t* __restrict__ adj,
                               uint32_t* __restrict__ flags, uint32_t* __restrict__ slot0 = nullptr) {
@@ -56,6 +94,33 @@ __global__ void enc_kv_kernel(EncodeArgs a, uint64_t* __restrict__ hashes, uint3
   if (slot0) slot0[i] = uint32_t(min(row_slot(a, i, 0), uint64_t(0xFFFFFFFFu)));
   const uint8_t* k = a.keys + a.key_off[i];
   uint64_t kl = a.key_off[i + 1] - a.key_off[i];
+  const uint64_t pl = i > 0 ? a.key_off[i] - a.key_off[i - 1] : 0;
+  if (kl <= kKvShort && pl <= kKvShort) {
+    uint32_t r[8], q[8];
+    key_words(k, uint32_t(kl), r);
+    hashes[i] = fnv_words(r, uint32_t(kl));
+    uint32_t l = 0;
+    if (i > 0) {
+      key_words(a.keys + a.key_off[i - 1], uint32_t(pl), q);
+      const uint32_t m = uint32_t(min(pl, kl));
+      uint32_t d = 32, qd = 0, rd = 0;  // first differing byte (bytes past both lengths are zero)
+#pragma unroll
+      for (uint32_t t = 0; t < 8; t++) {
+        const uint32_t x = r[t] ^ q[t];
+        const bool first = d == 32 && x != 0;
+        d = first ? 4 * t + (__builtin_ctz(x) >> 3) : d;
+        qd = first ? q[t] : qd;
+        rd = first ? r[t] : rd;
+      }
+      const uint32_t o = min(d, m);
+      l = o;
+      const uint32_t s8 = 8 * (d & 3);
+      const bool desc = (o < m) ? (((qd >> s8) & 0xFFu) > ((rd >> s8) & 0xFFu)) : (pl > kl);
+      if (desc) atomicOr(flags, 1u);  // not sorted: the min-LCP shortcut does not hold
+    }
+    adj[i] = l;
+    return;
+  }
   uint64_t h = 0xcbf29ce484222325ull;  // FNV-1 64 (hash/fnv New64)
   for (uint64_t b = 0; b < kl; b++) {
     h *= 0x100000001b3ull;
@@ -65,7 +130,6 @@ __global__ void enc_kv_kernel(EncodeArgs a, uint64_t* __restrict__ hashes, uint3
   uint32_t l = 0;
   if (i > 0) {
     const uint8_t* p = a.keys + a.key_off[i - 1];
-    uint64_t pl = a.key_off[i] - a.key_off[i - 1];
     uint64_t m = pl < kl ? pl : kl, o = 0;
     while (o < m && p[o] == k[o]) o++;
     l = o > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(o);

@@ -88,6 +88,29 @@ def test_segmentation_windows_and_first_keys(sc, ctx, case):
         assert t.info() == o.info()
 
 
+def test_kv_pass_key_lengths_and_prefixes(sc, ctx):
+    """enc_kv_kernel's dword path (keys of <= 32 bytes: FNV-1 64, LCP with the previous key and the
+    sortedness check from realigned aligned dwords) and its byte path (longer keys), with key lengths
+    0-40 at every alignment and LCPs ending at every byte position."""
+    rng = random.Random(11)
+    keys = set()
+    while len(keys) < 4000:
+        base = bytes(rng.choice(b"ab\x00\xff") for _ in range(rng.randrange(1, 41)))
+        keys.add(base)
+        cut = rng.randrange(0, len(base) + 1)
+        keys.add(base[:cut] + bytes([rng.randrange(256)]) + base[cut:][: rng.randrange(0, 8)])
+    kvs = [(k, bytes(rng.randrange(256) for _ in range(rng.randrange(0, 40)))) for k in sorted(keys) if k]
+    for batch in (True, False):
+        t, o, _ = _build_both(sc, ctx, kvs, 1024, batch=batch)
+        assert t.encode() == o.encode_table()
+        assert t.bloom() == o.bloom()
+    # a descending pair inside the short path: the sortedness flag sends the segmentation to its
+    # direct-LCP walk; bytes still equal the oracle's
+    bad = kvs[:50] + [(kvs[60][0], b"x"), (kvs[55][0], b"y")] + kvs[70:120]
+    t, o, _ = _build_both(sc, ctx, bad, 256, batch=True)
+    assert t.encode() == o.encode_table()
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_next_block_after_each_add(sc, ctx, seed):
     """sstable.Builder.NextBlock timing (builder.go:160-190): after every AddValue, the blocks the
