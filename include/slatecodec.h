@@ -541,8 +541,9 @@ typedef struct slate_compact_warning {
  *   row = -1: "while fetching blocks for SST '%s': while reading block range [%d:%d]: while decoding
  *              block '%d' data[0:%d]: %s"   (sst id, block, block + 1, block, block_len, err)
  *   row >= 0: "while decoding block.Offset[%d]: %s"   (row, err)
- * ErrWarn.Merge drops a text equal to one already kept (types/errors.go:41-52); the records are
- * not de-duplicated, so a shim drops repeats as it formats them. */
+ * ErrWarn.Merge drops a text equal to one already kept (types/errors.go:41-52), and so does the
+ * library: a row record whose (row, status) pair an earlier record has is not returned (the row
+ * text depends on nothing else; a block record names its SST, so it never repeats). */
 int slate_compact(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst, const uint32_t* src_sst,
                   uint32_t n_src, const slate_sst_config* out_cfg, uint64_t max_sst_size, slate_sst_table** out_tables,
                   uint32_t out_cap, uint32_t* n_out);

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstring>
 #include <memory>
+#include <set>
 #include <vector>
 
 #include "../../include/slatecodec.h"
@@ -96,6 +97,7 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   DEV(d_rows, (slots + 1) * sizeof(slate_row));
   DecodeArgs a{codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(),
                d_meta->as<slate_block_meta>(), d_rows->as<slate_row>(), d_row_base->as<uint64_t>(), nullptr, nullptr, 0};
+  if (st == ctx->stream) a.side = &ctx->side;
   SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus));
   // every block's status: the first failing block of an SST ends that SST's iterator with a
   // warning (iterator.go:62-68 wrapping decode.go:143-144); it and the SST's later blocks keep no
@@ -353,9 +355,14 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
     }
     std::stable_sort(later.begin(), later.end(),
                      [&](const Warn* a, const Warn* b) { return end_rank[a->w.src] < end_rank[b->w.src]; });
+    // ErrWarn.Merge drops a text it already holds (types/errors.go:41-52).  A row warning's text
+    // depends only on its row index and status ("while decoding block.Offset[%d]: %s" with a fixed
+    // row.go message), a block warning's names its SST, so repeats are (row, status) pairs
     uint32_t k = 0;
+    std::set<std::pair<int32_t, int32_t>> row_texts;
     for (const auto* part : {&init, &later})
       for (const Warn* w : *part) {
+        if (w->w.row >= 0 && !row_texts.insert({w->w.row, w->w.status}).second) continue;
         if (k < warn_cap) warns[k] = w->w;
         k++;
       }

@@ -199,6 +199,7 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
   // the scratch is owned by the context for the device-resident call
   SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes(n)));
   DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
+  a.side = &ctx->side;
   SLATE_HIP(launch_decode(ctx->stream, a, ctx->d_scratch.p, ctx->num_cus));
   return SLATE_OK;
 }

@@ -148,9 +148,13 @@ void sink_map(Sink& o) {
     const char* e = getenv("SLATE_HOST_DIRECT");
     return e && *e == '0';
   }();
-  if (off || !o.out || !o.rows || (reinterpret_cast<uintptr_t>(o.out) & 15)) return;
-  void* od = mapped_ptr(o.out);
-  void* rd = od ? mapped_ptr(o.rows) : nullptr;
+  // both arrays 16-byte aligned (blocks_to_host_kernel stores 16 bytes at a time into each) and
+  // page-locked over their whole capacity, or the staging path
+  if (off || !o.out || !o.rows || (reinterpret_cast<uintptr_t>(o.out) & 15) ||
+      (reinterpret_cast<uintptr_t>(o.rows) & 15))
+    return;
+  void* od = mapped_range(o.out, o.out_cap);
+  void* rd = od ? mapped_range(o.rows, o.rows_cap * sizeof(slate_row)) : nullptr;
   if (od && rd) {
     o.out_dev = static_cast<uint8_t*>(od);
     o.rows_dev = static_cast<slate_row*>(rd);
@@ -425,6 +429,7 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
       DecodeArgs a{codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), m, L.d_out.as<uint8_t>(),
                    L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
                    L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
+      a.side = &L.side;
       SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
       L.direct = o.out_dev != nullptr;
       if (L.direct) {
@@ -576,6 +581,7 @@ int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_l
   DecodeArgs a{codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), 1, L.d_out.as<uint8_t>(),
                L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
                L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
+  a.side = &L.side;
   SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
   SLATE_HIP(hipMemcpyAsync(hv + 6, L.d_meta.p, sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
   if (cap) SLATE_HIP(hipMemcpyAsync(L.h_out.p, L.d_out.p, cap, hipMemcpyDeviceToHost, s));
@@ -687,8 +693,10 @@ int slate_block_decode_sharded(slate_ctx* const* ctxs, uint32_t n_ctx, int codec
     if (S.m == 0) return;
     Sink o;
     o.out = out;
+    o.out_cap = out_cap;
     o.meta = meta;
     o.rows = rows;
+    o.rows_cap = rows_cap;
     o.out_off = S.out_off.data();
     o.row_base = S.row_base.data();
     o.G = n_ctx;

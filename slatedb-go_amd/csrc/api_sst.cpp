@@ -997,6 +997,7 @@ struct slate_sst_builder {
   // Snappy filter beside the final flush: 1 while its chunk encode is not yet queued (the flush then
   // holds its pack launch, so the filter's serial chains get CUs before the pack fills them), 2 after
   std::atomic<int> filter_gate{0};
+  uint32_t gate_timeouts = 0;  // final flushes whose pack stopped waiting for the filter (host trace)
   // pending KVs (not yet in a finished block), on the device: key / value bytes, n+1 offsets
   // into them, tombstone flags
   DevBuf d_keys, d_vals, d_koff, d_voff, d_tomb, d_tmp;
@@ -1223,6 +1224,7 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     // chains; launched after the pack it would wait for the whole pack): at most 20 ms
     for (int spin = 0; final && b->filter_gate.load() == 1 && spin < 1000; spin++)
       std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (final && b->filter_gate.load() == 1) b->gate_timeouts++;
     GpuSpan g_pack(ctx, st);
     SLATE_HIP(hipMemsetAsync(csize + nb, 0, 8, st));
     SLATE_HIP(launch_pack_snappy(st, a, w, uint32_t(nb), w.block_size, slots, csize, ctx->num_cus));
@@ -1539,6 +1541,23 @@ static bool filter_first() {
   return on;
 }
 
+// The filter's device buffers sized before the flush holds its pack for the filter (the gate): an
+// ensure() that has to grow a buffer frees the old one, and hipFree waits for the device, so growing
+// them on the filter's thread while the flush waits would stretch the wait.  Failures are left to
+// build_filter_aux, which makes the same calls and reports them.
+static void filter_prealloc(slate_sst_builder* b, uint64_t n_hashes) {
+  slate_ctx* ctx = b->ctx;
+  if (b->num_keys == 0) return;
+  const uint32_t np = bloom_num_probes(b->cfg.filter_bits_per_key);
+  const uint64_t nb = bloom_filter_bytes(b->num_keys, b->cfg.filter_bits_per_key);
+  if (nb * 8 == 0 || nb * 8 > 0xFFFFFFFFull) return;
+  (void)ctx->x_words.ensure(((nb + 3) & ~uint64_t(3)) + 16);
+  (void)ctx->x_enc.ensure(nb + 2 + 16);
+  (void)ctx->x_bkt.ensure(bloom_bucket_scratch_bytes(n_hashes, np, uint32_t(nb * 8)));
+  const uint64_t nch = (nb + 2 + kSnapMaxChunk - 1) / kSnapMaxChunk;
+  (void)ctx->x_slots.ensure(nch * kSnapChunkSlot + nch * 12 + 64);
+}
+
 static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
   struct GateOpen {
     slate_sst_builder* b;
@@ -1638,7 +1657,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
                            b->num_keys >= b->cfg.min_filter_keys;
   std::future<FilterOut> fjob;
   const std::function<void(uint64_t)> start_filter = [&](uint64_t nh) {
-    if (b->cfg.codec == SLATE_CODEC_SNAPPY && filter_first()) b->filter_gate.store(1);
+    if (b->cfg.codec == SLATE_CODEC_SNAPPY && filter_first()) {
+      filter_prealloc(b, nh);
+      b->filter_gate.store(1);
+    }
     fjob = std::async(std::launch::async, build_filter_aux, b, nh);
   };
   // the index flatbuffer (host work) is built beside the last blocks' D2H and the filter's encode:
@@ -1794,8 +1816,10 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   t->chunks.push_back(ByteView{fin, 0, buf.size()});
   *table = t;
   if (host_trace())
-    fprintf(stderr, "[slate build] flush %.2f ms, filter %.2f ms, index + info %.2f ms (index flatbuffer wait %.2f ms)\n",
-            t1 - t0, t2 - t1, now_ms() - t2, t_fb - t2);
+    fprintf(stderr,
+            "[slate build] flush %.2f ms, filter %.2f ms, index + info %.2f ms (index flatbuffer wait %.2f ms), "
+            "filter gate timeouts %u\n",
+            t1 - t0, t2 - t1, now_ms() - t2, t_fb - t2, b->gate_timeouts);
   return SLATE_OK;
 }
 

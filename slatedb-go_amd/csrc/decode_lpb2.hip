@@ -38,6 +38,9 @@
 // the key prefix inline; at block end a wave-cooperative pass compares the walked row
 // starts with the block's offset array, and mismatches re-derive rows from HBM with the
 // exact row.go decoder.
+#ifndef SLATE_LPB_OR
+#define SLATE_LPB_OR 256
+#endif
 #include "common.h"
 #include "kernels.h"
 #include "wave_crc.h"
@@ -49,7 +52,14 @@ namespace {
 
 // ring positions still valid behind d: a step's store reaches 20 bytes past d's dword
 // (five dwords), i.e. 109 bytes behind d modulo the ring
-constexpr uint32_t kReach = kOR - 20;
+// bytes a step moves at most (16 or 32); its store writes kStep/4 + 1 dwords from d's dword
+#ifndef SLATE_LPB_STEP
+#define SLATE_LPB_STEP 16
+#endif
+constexpr uint32_t kStep = SLATE_LPB_STEP;
+static_assert(kStep == 16 || kStep == 32, "step");
+constexpr uint32_t kStoreReach = kStep + 4;
+constexpr uint32_t kReach = kOR - kStoreReach;
 // section markers in the assembly (tools/loop_mix.py --marks): reading aid only, they fence the scheduler
 #ifdef SLATE_ASM_MARKS
 #define LPB_MARK(x) asm volatile("; @@" #x ::: "memory")
@@ -61,7 +71,18 @@ constexpr uint32_t kLz4Magic = 0x184D2204u;
 constexpr uint32_t kXP1 = 2654435761u, kXP2 = 2246822519u, kXP3 = 3266489917u, kXP4 = 668265263u,
                    kXP5 = 374761393u;
 __device__ __forceinline__ uint32_t xrotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
-constexpr uint32_t kUnflushed = 80;    // d - 16*fl before a step may advance d (see the throttle)
+// d - 16*fl before a step may advance d (see the throttle): a hole's source ends flushed
+// (U <= kReach - 15) and the unflushed bytes plus a step's store stay in the ring (U + kStep +
+// kStoreReach <= kOR)
+constexpr uint32_t kUnflushed = kOR - 16 - 2 * kStep;
+static_assert(kUnflushed + 15 <= kReach && kUnflushed + kStep + kStoreReach <= kOR, "throttle");
+// output chunks per block per flush store: lanes kRun*i .. kRun*i + kRun-1 write one run of kRun chunks
+// (64-byte runs from the 128-byte ring, 128-byte runs from a 256-byte one); an iteration's
+// kFlushStores stores cover 64 / kFlushParts blocks, so with 128-byte runs and 16-byte steps each half
+// of the wave flushes every other iteration
+constexpr uint32_t kRun = kOR / 32, kFlushStores = kStep / 4;
+constexpr uint32_t kFlushBlocks = kFlushStores * (64 / kRun), kFlushParts = 64 / kFlushBlocks;
+static_assert(kFlushParts >= 1 && kFlushBlocks * kFlushParts == 64, "flush");
 #ifndef SLATE_LPB_NS
 #define SLATE_LPB_NS 8
 #endif
@@ -219,6 +240,21 @@ struct RowOut {
 };
 
 // CRC32 of the next committed input chunk (bytes outside the block zeroed).
+// slicing-by-8 (SLATE_LPB_CRC8: 8 KiB of tables instead of 16, two dependent lookup rounds per chunk)
+#ifndef SLATE_LPB_CRC8
+#define SLATE_LPB_CRC8 1
+#endif
+constexpr uint32_t kLpbTabBytes = SLATE_LPB_CRC8 ? kTab16Bytes / 2 : kTab16Bytes;
+__device__ __forceinline__ uint32_t crc_chunk8(const uint8_t* lds, const v4u& v) {
+  uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+  lut4<0, 7>(lds, v.x, a0, a1, a2, a3);
+  lut4<0, 3>(lds, v.y, b0, b1, b2, b3);
+  const uint32_t c = xor3(xor3(a0, a1, a2), xor3(a3, b0, b1), b2) ^ b3;
+  lut4<0, 7>(lds, v.z ^ c, a0, a1, a2, a3);
+  lut4<0, 3>(lds, v.w, b0, b1, b2, b3);
+  return xor3(xor3(a0, a1, a2), xor3(a3, b0, b1), b2) ^ b3;
+}
+
 __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint32_t* tab, bool go) {
   const uint32_t k = L.crc_pos;
   v4u v = rd128(in + (k & (kNS - 1)) * 16, L.z);
@@ -231,7 +267,8 @@ __device__ __forceinline__ void crc_chunk(Lane& L, const uint8_t* in, const uint
     v.w &= keep_mask(lo, hi, 3);
   }
   v.x ^= L.crc;
-  const uint32_t c = crc_chunk0(reinterpret_cast<const uint8_t*>(tab), v);
+  const uint32_t c = SLATE_LPB_CRC8 ? crc_chunk8(reinterpret_cast<const uint8_t*>(tab), v)
+                                    : crc_chunk0(reinterpret_cast<const uint8_t*>(tab), v);
   L.crc = go ? c : L.crc;
   L.crc_pos += go ? 1u : 0u;
 }
@@ -539,7 +576,7 @@ __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, 
   L.lit = ok ? !mph : L.lit;
   L.rem = ok ? (mph ? ml : len) : L.rem;
   L.src = ok ? (mph ? L.d - off : L.sh + s1) : L.src;
-  L.eff = ok ? (mph ? off : 16u) : L.eff;
+  L.eff = ok ? (mph ? off : kStep) : L.eff;
   L.far = ok ? (mph && off > kReach) : L.far;
   L.s = ok ? (mph ? s1 : lit_end) : L.s;
   L.mtok = (ok && !mph) ? (tok & 15) : L.mtok;
@@ -590,7 +627,7 @@ __device__ __forceinline__ void snappy_parse(Lane& L, bool act, const uint8_t* i
   L.err = L.err | fail;
   L.dd = L.dd | fin | fail;
   const uint32_t src_lit = L.sh + s1, src_cp = L.d - cp_off, s_lit = s1 + len;
-  const uint32_t src_new = tl ? src_lit : src_cp, eff_new = tl ? 16u : cp_off, s_new = tl ? s_lit : s1;
+  const uint32_t src_new = tl ? src_lit : src_cp, eff_new = tl ? kStep : cp_off, s_new = tl ? s_lit : s1;
   const bool far_new = !tl & (cp_off > kReach);
   L.lit = ok ? tl : L.lit;
   L.far = ok ? far_new : L.far;
@@ -611,7 +648,7 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
 #endif
   // ---- CRC32 of one committed chunk (the two steps without the walker)
   LPB_MARK(crc);
-  if (kSlot == 0 || kSlot == 2) {
+  if (kSlot == 0 || kSlot == 2 || (kStep == 32 && kSlot == 1)) {
     const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
     if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
     else crc_chunk(L, in, tab, go);
@@ -640,7 +677,7 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
   LPB_MARK(move);
   {
     const bool cp = act & !L.dd & (L.rem != 0) & !L.far & (L.d <= lim_d);
-    const uint32_t k16 = min(L.rem, 16u);
+    const uint32_t k16 = min(L.rem, kStep);
     const uint32_t in_left = cend - L.src;
     const uint32_t k_lit = min(k16, cend > L.src ? in_left : 0u), k_near = min(k16, L.eff);
     uint32_t k = L.lit ? k_lit : k_near;
@@ -649,17 +686,25 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
     const bool cut = !L.lit & L.hp & (L.src < L.hd + L.hl) & (L.src + k > L.hd);
     k = cut ? k_hole : k;
     k = cp ? k : 0u;
-    const v4u v = ring_rd16(L.lit ? in : ring, L.src);
     // bytes from d on are not yet output: storing them when k == 0 is harmless; the first
     // dword keeps the bytes below d (L.T)
     const uint32_t b = L.d & 3;
-    const Win5 y = shift_in(v, L.T, b);
-    store_win(ring, L.d & ~3u, y);
-    L.T = pick5(y, (b + k) >> 2);
+    const uint32_t m8 = (kOR == kIR || !L.lit) ? kOR - 8 : kIR - 8;
+    if constexpr (kStep == 16) {
+      const v4u v = ring_rd16(L.lit ? in : ring, L.src, m8);
+      const Win5 y = shift_in(v, L.T, b);
+      store_win(ring, L.d & ~3u, y);
+      L.T = pick5(y, (b + k) >> 2);
+    } else {
+      const V8 v = ring_rd32(L.lit ? in : ring, L.src, m8);
+      const Win9 y = shift_in9(v, L.T, b);
+      store_win9(ring, L.d & ~3u, y);
+      L.T = pick9(y, (b + k) >> 2);
+    }
     L.d += k;
     L.rem -= k;
     // periodic output: once a whole period was copied, the pattern can be read twice as far back
-    const bool step_cp = (k != 0) & (k == L.eff) & !L.lit & (L.eff < 16);
+    const bool step_cp = (k != 0) & (k == L.eff) & !L.lit & (L.eff < kStep);
     const uint32_t eff2 = step_cp ? 2 * L.eff : L.eff;
     const uint32_t src_l = L.src + k, src_c = L.d - eff2;
     L.src = L.lit ? src_l : src_c;
@@ -701,22 +746,23 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
 // block of lane 16j+i, so every store instruction writes 16 runs of 64 contiguous bytes
 // instead of 64 scattered 16-byte pieces (tools/scatter_probe.hip: ~3.5x cheaper).
 __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
-                                                uint32_t dbg) {
-  const uint32_t done = act ? min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
+                                                uint32_t dbg, uint32_t part) {
+  const bool mine = kFlushParts == 1 || (lane / kFlushBlocks) == part;
+  const uint32_t done = (act && mine) ? min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
   const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
   const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
   const uint32_t wave_lane0 = threadIdx.x - lane;
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+  for (uint32_t j = 0; j < kFlushStores; j++) {
+    const uint32_t o = part * kFlushBlocks + (64 / kRun) * j + lane / kRun, c = lane % kRun;
     const uint32_t info_o = __shfl(info, int(o), 64);
     const uint32_t base_o = __shfl(base, int(o), 64);
     const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
-    const v4u v = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)), L.z);
+    const v4u v = rd128(ring_o + ((((info_o & 127) + c) * 16) & (kOR - 1)), L.z);
     __builtin_amdgcn_raw_buffer_store_b128(v, R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, 0,
                                            kOutCpol);
   }
-  L.fl += min(done, 4u);
+  L.fl += min(done, kRun);
 }
 
 // SLATE_FLUSH_DEFER (experiment): the same four transposed stores, their data read from the ring at
@@ -821,12 +867,12 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   {
     const uint32_t* src = &g_crc16.t[0][0];
-    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < kLpbTabBytes / 4; i += blockDim.x) tab[i] = src[i];
     __syncthreads();
   }
   const uint32_t* crc_init = g_crc_lt.init;  // used once per round: constant memory
   const uint32_t* crc_tail = g_crc_lt.tail;
-  uint8_t* outs = smem + kTab16Bytes;
+  uint8_t* outs = smem + kLpbTabBytes;
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
@@ -1055,12 +1101,12 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         __builtin_amdgcn_raw_buffer_store_b128(ro.row3, R.rows, ro.off3, 0, kRowCpol);
       }
       if (SLATE_FLUSH_DEFER) flush_prepare(L, act, outs, lane, F, dbg_bits(a));
-      else flush_iteration(L, act, outs, lane, R, dbg_bits(a));
+      else flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts);
       if (SLATE_ROW_STAGE) row_flush(L, rstages, lane, R, 3);
       if constexpr (kLz4) {
         // the content checksum's stripes: the chunks just completed (at most four), still in the ring
 #pragma unroll
-        for (int j = 0; j < 4; j++) xxh_absorb(L, ring, L.xp < L.fl);
+        for (uint32_t j = 0; j < kStep / 4; j++) xxh_absorb(L, ring, L.xp < min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu));
       }
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
@@ -1281,7 +1327,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
 
 size_t lpb2_lds_bytes() {
-  return kTab16Bytes + size_t(kLpb2Threads) * (kOutStride + kInStride + (SLATE_ROW_STAGE ? kRowStride : 0));
+  return kLpbTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride + (SLATE_ROW_STAGE ? kRowStride : 0));
 }
 
 // CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order

@@ -88,6 +88,15 @@ inline void* mapped_ptr(void* p) {
   return d;
 }
 
+// The device address of host range [p, p + len) when the whole range is page-locked in one mapping
+// (its last byte maps to d + len - 1); nullptr otherwise, e.g. when a caller registered only a prefix.
+inline void* mapped_range(void* p, uint64_t len) {
+  void* d = mapped_ptr(p);
+  if (!d || len == 0) return d;
+  void* e = mapped_ptr(static_cast<uint8_t*>(p) + (len - 1));
+  return e == static_cast<uint8_t*>(d) + (len - 1) ? d : nullptr;
+}
+
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -123,7 +132,9 @@ struct PipeLane {
   uint32_t b0 = 0, n = 0;
   uint64_t out_base = 0, row_base = 0, out_total = 0, rows_total = 0;
   bool busy = false, decoded = false;
+  slate::SideStream side;  // the lane's second stream (DecodeArgs::side)
   void release() {
+    side.release();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows, &d_dense,
                       &d_gmap})
       b->release();
@@ -254,6 +265,7 @@ struct slate_ctx {
   DevBuf c_meta, c_tags, c_bodies, c_seqs, c_out, c_in;
   // SST filter built beside the final flush (api_sst.cpp build_filter_aux): its own stream and buffers
   hipStream_t aux = nullptr;
+  slate::SideStream side;  // the context stream's second stream (DecodeArgs::side)
   DevBuf x_words, x_enc, x_slots, x_asm, x_crc, x_bkt;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
   // device time of the builder's GPU passes (slate_ctx_set_timing): nanoseconds, summed over the
@@ -308,6 +320,7 @@ struct slate_ctx {
       b->release();
     if (aux) (void)hipStreamDestroy(aux);
     aux = nullptr;
+    side.release();
     if (t_ref) (void)hipEventDestroy(t_ref);
     t_ref = nullptr;
     for (PipeLane& l : lanes) l.release();

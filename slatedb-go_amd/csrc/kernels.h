@@ -20,9 +20,35 @@ constexpr uint32_t kLargeOutCap = 90112;
 // iterations, and 3 waves per SIMD gained only 15 % per iteration.)  SLATE_LPB_THREADS /
 // SLATE_LPB_NS override them for experiments (tools/variant.sh).
 #ifndef SLATE_LPB_THREADS
-#define SLATE_LPB_THREADS 512
+#define SLATE_LPB_THREADS 384
 #endif
 constexpr int kLpb2Threads = SLATE_LPB_THREADS;
+
+// A second stream with its fork / join events, owned by the caller's context (slate_ctx, or a
+// pipeline lane of it) and destroyed with it: the CodecZstd fast path runs its Huffman-literal phase
+// on it beside the build phase.  Created on first use; a failed creation leaves the launch serial.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  bool tried = false;
+  hipStream_t get() {
+    if (!tried) {
+      tried = true;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&join, hipEventDisableTiming) != hipSuccess)
+        release();
+    }
+    return s;
+  }
+  void release() {
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+    if (s) (void)hipStreamDestroy(s);
+    s = nullptr;
+    fork = join = nullptr;
+  }
+};
 
 struct DecodeArgs {
   int codec;
@@ -40,6 +66,7 @@ struct DecodeArgs {
   uint32_t raw = 0;       // LPB only: payload is not a block (index/filter buffer): CRC + decompress, no block checks
   uint32_t rt_zero = 0;   // always 0: a value the compiler cannot fold (see decode_lpb2.hip rd128)
   uint32_t* round_counter = nullptr;  // decode_lpb2: rounds handed out so far (launcher zeroes it)
+  SideStream* side = nullptr;         // host only: the caller's side stream (nullptr: one stream)
 };
 
 // Ablation bits.  The shipped library is built without SLATE_PROFILING_BUILD, so every

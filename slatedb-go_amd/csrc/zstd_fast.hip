@@ -931,30 +931,8 @@ size_t zstd_fast_parse_lds() { return ((sizeof(ZfShared) + 15) & ~size_t(15)) + 
 
 // Phase B' runs beside phase B: they take disjoint blocks (B skips Huffman-literal blocks, B' takes
 // only those), B' keeps a few lanes of few waves busy for about a millisecond per 1 M configs[4]
-// blocks, and B fills the chip.  A side stream per host thread and device (a slate_ctx is used by
-// one thread at a time), forked after phase A2 and joined before phase C.
-namespace {
-struct ZfFork {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  bool tried = false;
-};
-ZfFork* zf_fork() {
-  static thread_local ZfFork forks[16];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  ZfFork& f = forks[dev];
-  if (!f.tried) {
-    f.tried = true;
-    if (hipStreamCreateWithFlags(&f.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&f.join, hipEventDisableTiming) != hipSuccess)
-      f.s = nullptr;
-  }
-  return f.s ? &f : nullptr;
-}
-}  // namespace
-
+// blocks, and B fills the chip.  On the caller's side stream (DecodeArgs::side, owned by its
+// context), forked after phase A2 and joined before phase C.
 hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
   if (a.n == 0) return hipGetLastError();
   const size_t lds_a = zstd_fast_parse_lds();
@@ -973,9 +951,10 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_h));
   if (attr_h != hipSuccess) return attr_h;
   static const bool serial = getenv("SLATE_ZF_SERIAL") != nullptr;  // one stream (A/B runs)
-  ZfFork* f = serial ? nullptr : zf_fork();
+  SideStream* f = (serial || !a.side) ? nullptr : a.side;
   hipStream_t sh = st;
-  if (f && hipEventRecord(f->fork, st) == hipSuccess && hipStreamWaitEvent(f->s, f->fork, 0) == hipSuccess) sh = f->s;
+  if (f && f->get() && hipEventRecord(f->fork, st) == hipSuccess && hipStreamWaitEvent(f->s, f->fork, 0) == hipSuccess)
+    sh = f->s;
   zs_fast_huf_kernel<<<uint32_t(num_cus) * 2u, kZfHufThreads, lds_h, sh>>>(a, z);
   zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
   if (sh != st) {

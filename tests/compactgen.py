@@ -102,6 +102,15 @@ def oracle_compact_go(sources: list[list[bytes]], max_sst_size: int, codec: int 
     warns = list(early)
     for _, j in sorted(last):
         warns += late.get(j, [])
+    # ErrWarn.Merge keeps a text once (types/errors.go:41-52): a row warning's text is its row index
+    # and its status, a block warning's names its SST
+    seen, kept = set(), []
+    for w in warns:
+        key = ("row", w[3], w[4]) if w[3] >= 0 else ("blk", w[1], w[2])
+        if key not in seen:
+            seen.add(key)
+            kept.append(w)
+    warns = kept
     flat = [kv for it in iters for kv in it]
     merged = [flat[i] for i in ob.merge_sort([[key for key, _ in it] for it in iters])]
     return _write_outputs(merged, max_sst_size, codec, block_size), warns

@@ -141,7 +141,7 @@ def _corrupt_row(sst: bytes, block: int, row: int, field: int = 0) -> bytes:
     return sst[:a] + bytes(body) + struct.pack(">I", zlib.crc32(bytes(body))) + sst[b:]
 
 
-@pytest.mark.parametrize("case", ["block", "row", "both", "first_row", "run"])
+@pytest.mark.parametrize("case", ["block", "row", "both", "first_row", "run", "dup"])
 def test_compaction_corrupt_inputs_warn(ctx, case):
     """Corrupt inputs end iterators as Go's do and the compaction goes on (sstable.Iterator,
     block.Iterator, iter.MergeSort, executeCompaction returning warn.If()): the output SSTs are
@@ -157,12 +157,17 @@ def test_compaction_corrupt_inputs_warn(ctx, case):
     if case == "first_row":  # before source 0's first row (merged when the merge starts), then source 1's
         srcs[0][0] = _corrupt_row(srcs[0][0], 0, 0, field=2)
         srcs[1][0] = _corrupt_row(srcs[1][0], 2, 7)
+    if case == "dup":  # the same row index and status in two sources: Go's ErrWarn keeps one text
+        srcs[1][0] = _corrupt_row(srcs[1][0], 1, 5)
+        srcs[2][0] = _corrupt_row(srcs[2][0], 2, 5)
     if case == "run":  # the second SST of source 0's run: its first block, then a row of source 2
         srcs[0][1] = _corrupt_first_block(srcs[0][1], b"\x00")
         srcs[2][1] = _corrupt_row(srcs[2][1], 2, 3)
     got, warns = sc.compact_ex(ctx, srcs, 30_000)
     want, want_w = cg.oracle_compact_go(srcs, 30_000)
     assert len(want_w) >= 1
+    if case == "dup":
+        assert len(want_w) == 1
     assert [tuple(int(x) for x in w) for w in warns] == [tuple(w) for w in want_w]
     assert len(got) == len(want) and all(g == w for g, w in zip(got, want))
     # slate_compact: the first warning's status, no outputs (startCompaction drops the sorted run)

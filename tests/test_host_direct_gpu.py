@@ -86,3 +86,48 @@ def test_pinned_outputs_match_pageable(ctxs, monkeypatch, codec, sharded):
         r, k = int(rb_h[i]), int(meta_h["n_rows"][i])
         assert rows_h[r:r + k].tobytes() == rows_p[r:r + k].tobytes() == o_rows[int(o_rb[i]):int(o_rb[i]) + k].tobytes()
     del hb_o, hb_r
+
+
+def test_partly_registered_outputs_use_staging(ctxs):
+    """Outputs whose first pages only are page-locked (hipHostRegister over a prefix): the library
+    must not write them through device addresses (the rest is not mapped) and decodes through
+    staging instead -- same bytes as the oracle, no fault (api_host.cpp sink_map / mapped_range)."""
+    import ctypes
+    import slatecodec as sc
+    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")  # the runtime the library links
+    codec = ob.SNAPPY
+    blob, off = _workload(codec, corrupt=False)
+    n = len(off) - 1
+    out_off, row_base = _plan(ctxs[0], sc, codec, blob, off)
+    page = 4096
+
+    def aligned(nbytes):
+        raw = np.zeros(nbytes + 2 * page, np.uint8)
+        a = (-raw.ctypes.data) % page
+        return raw, raw[a:a + nbytes]
+
+    out_raw, out_h = aligned(int(out_off[n]) + 16 + page)
+    rows_raw, rows_b = aligned(16 * (int(row_base[n]) + 1) + page)
+    rows_h = rows_b[:16 * (int(row_base[n]) + 1)].view(sc.ROW_DTYPE)
+    regs = []
+    for arr in (out_h, rows_b):
+        ptr, size = ctypes.c_void_p(arr.ctypes.data), ctypes.c_size_t(page)  # the first page only
+        assert hip.hipHostRegister(ptr, size, ctypes.c_uint(0)) == 0
+        regs.append(ptr)
+    try:
+        meta_h = np.zeros(n, sc.META_DTYPE)
+        oo_h, rb_h = np.zeros(n + 1, np.uint64), np.zeros(n + 1, np.uint64)
+        st = ctxs[0].decode_batch_into(codec, blob, off, out_h, rows_h, meta_h, oo_h, rb_h)
+        assert st == sc.OK
+        o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(codec, blob, off)
+        assert o_meta.tobytes() == meta_h.tobytes()
+        for i in range(n):
+            dl = int(meta_h["data_len"][i]) + 2 * int(meta_h["n_rows"][i]) + 2
+            a = int(oo_h[i])
+            assert out_h[a:a + dl].tobytes() == o_out[int(o_off[i]):int(o_off[i]) + dl].tobytes()
+            r, k = int(rb_h[i]), int(meta_h["n_rows"][i])
+            assert rows_h[r:r + k].tobytes() == o_rows[int(o_rb[i]):int(o_rb[i]) + k].tobytes()
+    finally:
+        for ptr in regs:
+            hip.hipHostUnregister(ptr)
+    del out_raw, rows_raw
