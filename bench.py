@@ -251,6 +251,10 @@ def main():
         del leg  # the extra legs get the HBM back
         result["codec_none"] = codec_none_leg(sc, ctx, stream, wl, args, threads)
         result["configs4_zstd"] = zstd_leg(sc, ctx, stream, wl, args, threads)
+        # configs[1]'s block shape (100-byte KVs, 4 KiB blocks) written by the Zstd and Zlib writers
+        # the reference's other codecs stand for (compression.go:110-121, 88-97)
+        result["kv100_zstd"] = kv100_leg(sc, ctx, stream, wl, args, threads, sc.ZSTD)
+        result["kv100_zlib"] = kv100_leg(sc, ctx, stream, wl, args, threads, sc.ZLIB)
         result["configs2_encode"] = encode_leg(sc, ctx, args)
         # the unchanged per-block reader path (one GPU round trip per 4 KiB block) and BASELINE
         # configs[0] (one 64-block CodecNone SST encoded + decoded), next to the oracle on one thread
@@ -426,6 +430,48 @@ def zstd_leg(sc, ctx, stream, wl, args, threads):
         res["cpu_baseline"] = cpu_baseline(sc.ZSTD, blob, in_off, args.cpu_seconds / 2)
     res["gen_seconds"] = round(gen_s, 1)
     res["workload"] = f"configs[4] mixed: {n} x 4 KiB Zstd blocks, 1 KiB values, skewed key prefixes"
+    leg.free()
+    return res
+
+
+def kv100_leg(sc, ctx, stream, wl, args, threads, codec):
+    """configs[1]'s blocks (1 M x 4 KiB, 100-byte V-half KVs) in CodecZstd (libzstd level 3 + checksum
+    + content size: ~112 sequences and FSE_Compressed tables per block) or CodecZlib (zlib level 6
+    closed as Go's compress/zlib closes a stream: tools/benchgen.c go_zlib6), device-resident decode.
+    Every block's bytes are checked against the blocks before encoding, the first 4096 blocks'
+    metas and rows against the oracle; `handbacks` = blocks a fast path left to the exact decoder in
+    one step (slate_ctx_handbacks)."""
+    import torch
+    from oracle import binding as ob
+    n = args.blocks
+    t0 = time.time()
+    dec, dec_off = wl.decoded_blocks(n, seed=SEED, half=True)
+    blob, in_off = wl.encode_blocks(codec, dec, dec_off, threads=threads)
+    gen_s = time.time() - t0
+    leg = DecodeLeg(sc, ctx, codec, blob, in_off)
+    ctx.handbacks(reset=True)
+    leg.step()
+    handbacks = ctx.handbacks(reset=True)
+    meta, res = _decode_leg_result(sc, leg, torch, stream, max(2, args.extra_steps // (1 if codec == sc.ZSTD else 5)), 1,
+                                   int(in_off[-1]))
+    name = {sc.ZSTD: "zstd", sc.ZLIB: "zlib"}[codec]
+    res["roofline"]["kernel"] = ("zs_fast_parse + zs_fse_parse/crc/build/sum + decode_list_kernel<2> (+ plan)"
+                                 if codec == sc.ZSTD else "decode_fast_kernel<1> (+ plan_zlib_kernel)")
+    res["handbacks"] = int(handbacks)
+    res["verified"] = leg.verify_against_decoded((dec, dec_off), meta)
+    m = min(4096, n)
+    sub_off = np.ascontiguousarray(in_off[:m + 1], np.uint64)
+    obc = {sc.ZSTD: ob.ZSTD, sc.ZLIB: ob.ZLIB}[codec]
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(obc, blob[:int(sub_off[m])], sub_off, nthreads=threads)
+    assert o_meta.tobytes() == meta[:m].tobytes(), f"kv100 {name} metas differ from the oracle"
+    rows = leg.d_rows.download(16 * int(o_rb[m])).view(sc.ROW_DTYPE)
+    used = np.concatenate([np.arange(int(o_rb[i]), int(o_rb[i]) + int(o_meta["n_rows"][i])) for i in range(m)])
+    assert rows[used].tobytes() == o_rows[used].tobytes(), f"kv100 {name} rows differ from the oracle"
+    res["oracle_checked_blocks"] = m
+    res["gen_seconds"] = round(gen_s, 1)
+    res["workload"] = (f"{n} x 4 KiB {name} blocks of configs[1]'s 100-byte V-half KVs, "
+                       + ("libzstd level 3 + checksum + content size" if codec == sc.ZSTD else
+                          "zlib level 6 + Go's empty final stored block"))
     leg.free()
     return res
 

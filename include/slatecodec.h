@@ -119,6 +119,8 @@ enum slate_status {
   SLATE_E_MERGE_UNSORTED = 105,     /* an iterator handed to the merge is not sorted (merge.go's precondition) */
   SLATE_E_LIMIT = 106,              /* an internal limit of this library (e.g. >= 2^32 rows in one call) */
   SLATE_E_WARNINGS = 107,           /* slate_compact_ex: done, with types.ErrWarn warnings (see there) */
+  SLATE_E_READER_NEED_DATA = 108,   /* slate_block_reader_next: fetch the range slate_block_reader_want gives */
+  SLATE_E_READER_END = 109,         /* slate_block_reader_next: no block left (or the iteration ended on an error) */
 };
 
 /* ---- layouts ----------------------------------------------------------------- */
@@ -230,6 +232,11 @@ int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads);
  * slate_ctx_gpu_time returns the sum in milliseconds (and zeroes it when reset != 0).  Kernel
  * groups on the filter's side stream overlap the flush, so the sum can exceed the wall time. */
 int slate_ctx_set_timing(slate_ctx* ctx, int on);
+/* Observability (no Go counterpart): the number of blocks this context's decodes handed from a fast
+ * path (CodecZstd, CodecLz4) to the exact wave-per-block decoder since the context was made or the
+ * count last reset (reset != 0 zeroes it).  Waits for the context's stream.  The results are the
+ * same either way; a hand-back only costs time. */
+int slate_ctx_handbacks(slate_ctx* ctx, uint64_t* n, int reset);
 int slate_ctx_gpu_time(slate_ctx* ctx, double* ms, int reset);
 /* The same spans' union (*busy_ms: device time with overlapping spans of the side streams counted
  * once) and sum (*sum_ms, may be null) since timing was switched on or last reset.  Every device
@@ -430,6 +437,33 @@ int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_in
                       uint8_t* out, uint64_t out_cap, uint64_t* out_off, slate_block_meta* meta,
                       slate_row* rows, uint64_t rows_cap, uint64_t* row_base,
                       uint64_t* failed_block);
+
+/* Read-ahead block reader: sstable.Iterator's nextBlockIter (internal/sstable/iterator.go:92-118)
+ * asks ReadBlocksUsingIndex for one block per call; this reader keeps that contract -- the blocks
+ * in order from first_block, one at a time, an iteration that ends at the first failing block
+ * with that block's status -- but fetches and decodes read_ahead blocks per GPU call (one object-
+ * store range read and one batch).  The caller's loop:
+ *   st = slate_block_reader_next(r, &view):
+ *     SLATE_OK                 view is the next block (pointers valid until the next feed);
+ *     SLATE_E_READER_NEED_DATA slate_block_reader_want(r, &rs, &re) gives the SST byte range to
+ *                              read [rs, re); hand it to slate_block_reader_feed, then call next;
+ *     SLATE_E_READER_END       no block left;
+ *     any other status         view.block failed block.Decode with it: the SST iterator adds its
+ *                              warning and ends (iterator.go:59-68); later calls return END.
+ * feed returns the decode call's status (a range / length error of the data handed in). */
+typedef struct slate_block_reader slate_block_reader;
+typedef struct slate_block_view {
+  uint64_t block;          /* index of the block in the SST */
+  slate_block_meta meta;   /* block.Decode's result (status, data_len, n_rows, FirstKey length) */
+  const uint8_t* data;     /* Block.Data: meta.data_len bytes, then the BE16 offsets (n_rows) */
+  const slate_row* rows;   /* the row descriptors (n_rows, or the capacity when truncated) */
+} slate_block_view;
+int slate_block_reader_create(slate_ctx* ctx, const slate_sst_info* info, const slate_index* index,
+                              uint64_t first_block, uint32_t read_ahead, slate_block_reader** reader);
+void slate_block_reader_free(slate_block_reader* reader);
+int slate_block_reader_next(slate_block_reader* reader, slate_block_view* view);
+int slate_block_reader_want(const slate_block_reader* reader, uint64_t* range_start, uint64_t* range_end);
+int slate_block_reader_feed(slate_block_reader* reader, const uint8_t* data, size_t data_len);
 
 /* ---- bloom filter (bloom.go) -------------------------------------------------------- */
 /* Build (bloom.go:112) over n keys (key i = keys[key_off[i]..key_off[i+1])) on the GPU. */

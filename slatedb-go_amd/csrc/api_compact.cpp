@@ -98,6 +98,7 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   DecodeArgs a{codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(),
                d_meta->as<slate_block_meta>(), d_rows->as<slate_row>(), d_row_base->as<uint64_t>(), nullptr, nullptr, 0};
   if (st == ctx->stream) a.side = &ctx->side;
+  a.handbacks = ctx_handbacks(ctx);
   SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus));
   // every block's status: the first failing block of an SST ends that SST's iterator with a
   // warning (iterator.go:62-68 wrapping decode.go:143-144); it and the SST's later blocks keep no

@@ -152,11 +152,36 @@ int slate_ctx_gpu_busy(slate_ctx* ctx, double* busy_ms, double* sum_ms, int rese
   return SLATE_OK;
 }
 
+int slate_ctx_handbacks(slate_ctx* ctx, uint64_t* n, int reset) {
+  if (!ctx || !n) return SLATE_E_INVALID_ARG;
+  *n = 0;
+  SLATE_HIP(ctx_bind(ctx));
+  SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  if (!ctx->d_handbacks.p) return SLATE_OK;
+  SLATE_HIP(hipMemcpy(n, ctx->d_handbacks.p, 8, hipMemcpyDeviceToHost));
+  if (reset) SLATE_HIP(hipMemset(ctx->d_handbacks.p, 0, 8));
+  return SLATE_OK;
+}
+
 int slate_ctx_gpu_time(slate_ctx* ctx, double* ms, int reset) {
   if (!ctx || !ms) return SLATE_E_INVALID_ARG;
   *ms = double(reset ? ctx->gpu_ns.exchange(0) : ctx->gpu_ns.load()) * 1e-6;
   return SLATE_OK;
 }
+
+}  // extern "C"
+
+uint64_t* ctx_handbacks(slate_ctx* ctx) {
+  if (!ctx->d_handbacks.p) {
+    if (ctx->d_handbacks.ensure(16) != hipSuccess || hipMemset(ctx->d_handbacks.p, 0, 16) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+  }
+  return ctx->d_handbacks.as<uint64_t>();
+}
+
+extern "C" {
 
 void slate_ctx_destroy(slate_ctx* ctx) {
   if (!ctx) return;
@@ -200,6 +225,7 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
   SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes(n)));
   DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
   a.side = &ctx->side;
+  a.handbacks = ctx_handbacks(ctx);
   SLATE_HIP(launch_decode(ctx->stream, a, ctx->d_scratch.p, ctx->num_cus));
   return SLATE_OK;
 }
@@ -263,6 +289,16 @@ int slate_block_seek_warn(slate_ctx* ctx, const uint8_t* data, const uint64_t* o
     uint64_t* hk = reinterpret_cast<uint64_t*>(h + o_koff);
     for (uint64_t i = 0; i <= n; i++) hk[i] = key_off[i] - key_off[0];
     uint8_t* hdev = static_cast<uint8_t*>(mapped_ptr(h));
+    if (hdev && n <= 256) {  // one launch: the kernel pulls the staging over the link itself
+      SLATE_HIP(launch_block_seek_staged(st, hdev, o_res, base, o_data, o_off, o_meta, o_q, o_keys, o_koff, n,
+                                         reinterpret_cast<slate_seek*>(hdev + o_res),
+                                         warn_cap ? reinterpret_cast<slate_seek_warn*>(hdev + o_warn) : nullptr,
+                                         warn_cap));
+      SLATE_HIP(hipStreamSynchronize(st));
+      memcpy(res, h + o_res, n * sizeof(slate_seek));
+      if (wbytes) memcpy(warn, h + o_warn, wbytes);
+      return SLATE_OK;
+    }
     if (hdev) {
       SLATE_HIP(hipMemcpyAsync(base, h, o_res, hipMemcpyHostToDevice, st));
       SLATE_HIP(launch_block_seek(st, base + o_data, reinterpret_cast<const uint64_t*>(base + o_off),

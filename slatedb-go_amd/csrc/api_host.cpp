@@ -430,6 +430,7 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
                    L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
                    L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
       a.side = &L.side;
+      a.handbacks = ctx_handbacks(ctx);
       SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
       L.direct = o.out_dev != nullptr;
       if (L.direct) {
@@ -582,6 +583,7 @@ int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_l
                L.d_out_off.as<uint64_t>(), L.d_meta.as<slate_block_meta>(), L.d_rows.as<slate_row>(),
                L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
   a.side = &L.side;
+  a.handbacks = ctx_handbacks(ctx);
   SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
   SLATE_HIP(hipMemcpyAsync(hv + 6, L.d_meta.p, sizeof(slate_block_meta), hipMemcpyDeviceToHost, s));
   if (cap) SLATE_HIP(hipMemcpyAsync(L.h_out.p, L.d_out.p, cap, hipMemcpyDeviceToHost, s));

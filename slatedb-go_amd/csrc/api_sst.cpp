@@ -2072,6 +2072,101 @@ int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_in
   return SLATE_OK;
 }
 
+// ---------------------------------------------------------------------- read-ahead block reader
+}  // extern "C"
+
+// sstable.Iterator.nextBlockIter (iterator.go:92-118) with read-ahead: batches of read_ahead blocks
+// decoded by slate_read_blocks into reader-owned host buffers, served one block at a time.
+struct slate_block_reader {
+  slate_ctx* ctx;
+  slate_sst_info info;
+  const slate_index* index;
+  uint64_t next = 0, nblocks = 0;
+  uint32_t ahead = 64;
+  uint64_t b0 = 0, b1 = 0;         // the decoded batch: blocks [b0, b1)
+  uint64_t fail = UINT64_MAX;      // its first failing block (served as an error, then the end)
+  uint64_t w0 = 0, w1 = 0;         // the batch the next feed decodes
+  bool ended = false;
+  std::vector<uint8_t> out;
+  std::vector<uint64_t> out_off, row_base;
+  std::vector<slate_block_meta> meta;
+  std::vector<slate_row> rows;
+};
+
+extern "C" {
+
+int slate_block_reader_create(slate_ctx* ctx, const slate_sst_info* info, const slate_index* index,
+                              uint64_t first_block, uint32_t read_ahead, slate_block_reader** reader) {
+  if (!ctx || !info || !index || !reader || read_ahead == 0) return SLATE_E_INVALID_ARG;
+  slate_block_reader* r = new (std::nothrow) slate_block_reader();
+  if (!r) return SLATE_E_OOM;
+  r->ctx = ctx;
+  r->info = *info;
+  r->index = index;
+  r->next = first_block;
+  r->nblocks = index->offsets.size();
+  r->ahead = read_ahead;
+  *reader = r;
+  return SLATE_OK;
+}
+
+void slate_block_reader_free(slate_block_reader* reader) { delete reader; }
+
+int slate_block_reader_next(slate_block_reader* r, slate_block_view* view) {
+  if (!r || !view) return SLATE_E_INVALID_ARG;
+  if (r->ended || r->next >= r->nblocks) {
+    r->ended = true;
+    return SLATE_E_READER_END;
+  }
+  if (r->next < r->b0 || r->next >= r->b1) {  // not decoded yet: the next batch
+    r->w0 = r->next;
+    r->w1 = std::min<uint64_t>(r->next + r->ahead, r->nblocks);
+    return SLATE_E_READER_NEED_DATA;
+  }
+  const uint64_t i = r->next - r->b0;
+  view->block = r->next;
+  view->meta = r->meta[i];
+  view->data = r->out.data() + r->out_off[i];
+  view->rows = r->rows.data() + r->row_base[i];
+  if (r->next == r->fail) {  // the SST iterator's warning, and its end (iterator.go:59-68)
+    r->ended = true;
+    return view->meta.status ? view->meta.status : SLATE_E_HIP;
+  }
+  r->next++;
+  return SLATE_OK;
+}
+
+int slate_block_reader_want(const slate_block_reader* r, uint64_t* range_start, uint64_t* range_end) {
+  if (!r || !range_start || !range_end || r->w1 <= r->w0) return SLATE_E_INVALID_ARG;
+  return slate_read_blocks_range(&r->info, r->index, r->w0, r->w1, range_start, range_end);
+}
+
+int slate_block_reader_feed(slate_block_reader* r, const uint8_t* data, size_t data_len) {
+  if (!r || (data_len && !data) || r->w1 <= r->w0) return SLATE_E_INVALID_ARG;
+  const uint64_t n = r->w1 - r->w0;
+  r->out_off.resize(n + 1);
+  r->row_base.resize(n + 1);
+  r->meta.resize(n);
+  if (r->out.empty()) r->out.resize(16);
+  if (r->rows.empty()) r->rows.resize(1);
+  uint64_t failed = UINT64_MAX;
+  int st = SLATE_OK;
+  for (int pass = 0; pass < 2; pass++) {
+    st = slate_read_blocks(r->ctx, &r->info, r->index, r->w0, r->w1, data, data_len, r->out.data(), r->out.size(),
+                           r->out_off.data(), r->meta.data(), r->rows.data(), r->rows.size(), r->row_base.data(),
+                           &failed);
+    if (st != SLATE_E_CAPACITY) break;
+    r->out.resize(r->out_off[n] + 16);  // the sizes the plan reported
+    r->rows.resize(r->row_base[n] + 1);
+  }
+  if (st) return st;
+  r->b0 = r->w0;
+  r->b1 = r->w1;
+  r->fail = failed;
+  r->w0 = r->w1 = 0;
+  return SLATE_OK;
+}
+
 // ---------------------------------------------------------------------- bloom
 int slate_bloom_build(slate_ctx* ctx, const uint8_t* keys, const uint64_t* key_off, uint64_t n, uint32_t bits_per_key,
                       uint8_t* bits, size_t bits_cap, size_t* bits_len, uint16_t* num_probes) {

@@ -1090,6 +1090,7 @@ __global__ __launch_bounds__(kDecodeThreads) void decode_list_kernel(DecodeArgs 
                                                                      const uint32_t* count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t items = *count;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.handbacks && items) atomicAdd(a.handbacks, uint64_t(items));
   if (blockIdx.x * (kDecodeThreads / 64) >= items) return;  // (workgroup-uniform) no block: skip the tables
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   load_crc_tables(tab);
@@ -1549,8 +1550,8 @@ size_t decode_scratch_bytes(uint32_t n) {
   size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
   return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16 +
          // CodecZstd fast path: count, list, records, sequences
-         16 + 2 * align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
-         size_t(n) * kZsFastSeqs * sizeof(uint2);
+         16 + 3 * align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
+         size_t(n) * kZfSeqSlot * sizeof(uint32_t);
 }
 
 static DecodeScratch carve(void* scratch, uint32_t n) {
@@ -1572,10 +1573,12 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   p += align16(size_t(n) * sizeof(uint32_t));
   s.zf.hlist = reinterpret_cast<uint32_t*>(p);
   p += align16(size_t(n) * sizeof(uint32_t));
+  s.zf.flist = reinterpret_cast<uint32_t*>(p);
+  p += align16(size_t(n) * sizeof(uint32_t));
   s.zf.rec = reinterpret_cast<ZsFastRec*>(p);
   p += size_t(n) * sizeof(ZsFastRec);
-  s.zf.seq = reinterpret_cast<uint2*>(p);
-  p += size_t(n) * kZsFastSeqs * sizeof(uint2);
+  s.zf.seq = reinterpret_cast<uint32_t*>(p);
+  p += size_t(n) * kZfSeqSlot * sizeof(uint32_t);
   s.tiles = uint32_t(tiles);
   return s;
 }
@@ -1721,6 +1724,245 @@ __global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint
     reinterpret_cast<uint4*>(host_out)[k] = reinterpret_cast<const uint4*>(a.out)[k];
 }
 
+// One CodecSnappy block for a single-block call (slate_block_decode: sstable.Iterator's one block per
+// nextBlockIter, a point read), by a whole 1024-thread workgroup instead of one wave walking the
+// ~170-tag chain serially (~70 us).  golang/snappy decode (decode_other.go:19-110) in parallel
+// passes over the block staged in LDS:
+//   1. every payload position p: the tag that would start there -- the next tag's position
+//      (END at the payload end, ERR for a tag running past it) and its decoded length;
+//   2. pointer doubling to 4-tag hops, one thread walks the hops from the header (~43 steps), and
+//      the hops are expanded in parallel: the chain's tags with their output offsets;
+//   3. every output byte finds its tag (binary search): a literal byte takes its value, a copied
+//      byte points at the byte it repeats; pointer jumping until every byte holds a value;
+// with the CRC32 on wave 0 beside pass 1.  Any check the serial decoder would fail (a tag past the
+// payload, offset 0 or beyond the output, a length beyond the header's) sends the block to that
+// decoder (wave 0), which then reports it; block.Decode's checks and rows are wave 0's block_finish.
+constexpr uint32_t kOneParIn = 6144, kOneParOut = 12288, kOneParThreads = 1024;
+constexpr uint32_t kOneParTags = kOneParIn / 2;
+constexpr uint16_t kPEnd = 0xFFFE, kPErr = 0xFFFF;
+constexpr size_t kOneParLds = kTabBytes + (kOneParIn + 32) + (kOneParOut + 16) + 6 * 2 * (kOneParIn + 16) +
+                              4 * kOneParTags + 4 * (kOneParTags / 4 + 16) + 64;
+
+__device__ __forceinline__ void snappy_tag_at(const uint8_t* in, uint32_t p, uint32_t clen, uint32_t* np, uint32_t* dl,
+                                              uint32_t* hl, uint32_t* off, bool* lit) {
+  const uint32_t c = in[p], t = c & 3;
+  uint32_t len, h, o = 0;
+  if (t == 0) {
+    const uint32_t x = c >> 2;
+    if (x < 60) {
+      len = x + 1;
+      h = 1;
+    } else {
+      const uint32_t nb = x - 59;
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < nb; k++) v |= uint32_t(p + 1 + k < clen ? in[p + 1 + k] : 0u) << (8 * k);
+      len = v + 1;  // (v + 1 == 0: wraps, fails below)
+      h = 1 + nb;
+    }
+  } else if (t == 1) {
+    len = 4 + ((c >> 2) & 7);
+    o = ((c >> 5) << 8) | (p + 1 < clen ? in[p + 1] : 0u);
+    h = 2;
+  } else {
+    len = 1 + (c >> 2);
+    h = t == 2 ? 3 : 5;
+    for (uint32_t k = 0; k < h - 1; k++) o |= uint32_t(p + 1 + k < clen ? in[p + 1 + k] : 0u) << (8 * k);
+  }
+  const uint64_t e = uint64_t(p) + h + (t == 0 ? uint64_t(len) : 0);
+  *np = (len == 0 || e > clen) ? kPErr : uint32_t(e);
+  *dl = len;
+  *hl = h;
+  *off = o;
+  *lit = t == 0;
+}
+
+__global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeArgs a, const uint8_t* __restrict__ host_in,
+                                                                        uint64_t in_len, uint64_t out_sz, uint64_t row_sz,
+                                                                        uint8_t* __restrict__ host_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint64_t offs[6];
+  __shared__ uint32_t sh_crc, sh_bad, sh_ntags, sh_nhops, sh_more;
+  const uint32_t tid = threadIdx.x;
+  const int lane = int(tid & 63), wave = int(tid >> 6);
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
+  uint8_t* in = smem + kTabBytes;
+  uint8_t* out = in + kOneParIn + 32;
+  uint16_t* nxt = reinterpret_cast<uint16_t*>(out + kOneParOut + 16);
+  uint16_t* dln = nxt + (kOneParIn + 16);
+  uint16_t* j2 = dln + (kOneParIn + 16);
+  uint16_t* s2 = j2 + (kOneParIn + 16);
+  uint16_t* j4 = s2 + (kOneParIn + 16);
+  uint16_t* s4 = j4 + (kOneParIn + 16);
+  uint16_t* P = j2;  // the output bytes' pointers reuse j2 / s2 (2 * kOneParOut <= 4 * (kOneParIn + 16))
+  uint32_t* T = reinterpret_cast<uint32_t*>(s4 + (kOneParIn + 16));  // tags: position | output offset << 16
+  uint32_t* H = T + kOneParTags;                                     // 4-tag hops: position | offset << 16
+  if (tid < 6) offs[tid] = tid == 1 ? in_len : tid == 3 ? out_sz : tid == 5 ? row_sz : 0;
+  if (tid == 0) {
+    sh_bad = 0;
+    sh_ntags = 0;
+    sh_nhops = 0;
+  }
+  // ---- stage the block and the CRC tables
+  const uint32_t nch = uint32_t((in_len + 15) / 16);
+  for (uint32_t c = tid; c < nch; c += kOneParThreads)
+    reinterpret_cast<uint4*>(in)[c] = reinterpret_cast<const uint4*>(host_in)[c];
+  for (uint32_t i = tid; i < 1024; i += kOneParThreads) tab[i] = g_crc_tables.t[0][i];
+  __syncthreads();
+  const uint32_t clen = uint32_t(in_len - 4);
+  uint64_t dl64 = 0;
+  uint32_t hdr = 0;
+  const bool hdr_ok = decoded_len(SLATE_CODEC_SNAPPY, in, in_len, &dl64, &hdr);
+  const uint32_t dn = uint32_t(dl64);
+  // ---- pass 1: the tag at every position (wave 0: the CRC32 first)
+  if (wave == 0) {
+    const uint32_t crc = wave_crc32(tab, in, 0, clen, lane);
+    if (lane == 0) sh_crc = crc;
+  }
+  for (uint32_t p = hdr + tid; p < clen; p += kOneParThreads) {
+    uint32_t np, dl, hl, off;
+    bool lit;
+    snappy_tag_at(in, p, clen, &np, &dl, &hl, &off, &lit);
+    nxt[p] = uint16_t(np == clen ? kPEnd : np);
+    dln[p] = uint16_t(min(dl, 0xFFFFu));
+  }
+  __syncthreads();
+  const uint32_t stored = ld_be32(in + clen);
+  auto fin = [&](slate_block_meta m, bool decoded) {
+    // wave 0: block.Decode's checks and rows over the decoded block (or the status), then the copy-out
+    if (wave == 0) {
+      a.in_off = offs;
+      a.out_off = offs + 2;
+      a.row_base = offs + 4;
+      if (decoded) block_finish(a, 0, out, dn, lane, m);
+      else write_meta(&a.meta[0], m, lane);
+    }
+    __syncthreads();
+    if (decoded)
+      for (uint32_t k = tid; k < (dn + 15) / 16; k += kOneParThreads)
+        reinterpret_cast<uint4*>(host_out)[k] = reinterpret_cast<const uint4*>(out)[k];
+  };
+  if (sh_crc != stored) {
+    slate_block_meta m{};
+    m.status = SLATE_E_BLOCK_CHECKSUM;
+    fin(m, false);
+    return;
+  }
+  bool bad = !hdr_ok || hdr > clen;
+  if (!bad) {
+    // ---- pass 2: 2- and 4-tag hops (END stays END, ERR propagates)
+    auto hop = [&](const uint16_t* J, const uint16_t* S, uint16_t* J2, uint16_t* S2) {
+      for (uint32_t p = hdr + tid; p < clen; p += kOneParThreads) {
+        const uint32_t q = J[p];
+        if (q >= kPEnd) {
+          J2[p] = uint16_t(q);
+          S2[p] = S[p];
+        } else {
+          J2[p] = J[q];
+          S2[p] = uint16_t(min(uint32_t(S[p]) + S[q], 0xFFFFu));
+        }
+      }
+    };
+    hop(nxt, dln, j2, s2);
+    __syncthreads();
+    hop(j2, s2, j4, s4);
+    __syncthreads();
+    // one thread walks the chain in 4-tag hops from the header
+    if (tid == 0) {
+      uint32_t p = hdr, o = 0, k = 0, b = 0;
+      while (p < clen) {
+        if (k >= kOneParTags / 4 + 16 || o > dn) {
+          b = 1;
+          break;
+        }
+        H[k++] = p | (o << 16);
+        o += s4[p];
+        const uint32_t q = j4[p];
+        p = q == kPEnd ? clen : q;
+        if (q == kPErr) {
+          b = 1;
+          break;
+        }
+      }
+      if (o != dn) b = 1;  // the tags' bytes are exactly the header's length
+      sh_nhops = k;
+      sh_bad = b;
+    }
+    __syncthreads();
+    bad = sh_bad != 0;
+  }
+  if (!bad) {
+    const uint32_t nh = sh_nhops;
+    // hops expanded: the chain's tags with their output offsets, checked as decode_other.go does
+    uint32_t b = 0;
+    for (uint32_t t = tid; t < nh; t += kOneParThreads) {
+      uint32_t p = H[t] & 0xFFFF, o = H[t] >> 16, i = 0;
+      for (; i < 4 && p < clen; i++) {
+        T[4 * t + i] = p | (o << 16);
+        uint32_t np, dl, hl, off;
+        bool lit;
+        snappy_tag_at(in, p, clen, &np, &dl, &hl, &off, &lit);
+        if (!lit && (off == 0 || off > o)) b = 1;
+        o += dl;
+        const uint32_t q = nxt[p];
+        p = q == kPEnd ? clen : q;
+      }
+      if (t == nh - 1) sh_ntags = 4 * t + i;
+    }
+    if (b) sh_bad = 1;
+    __syncthreads();
+    bad = sh_bad != 0;
+  }
+  if (!bad) {
+    // ---- pass 3: every output byte from its tag; copies as pointers, then pointer jumping
+    const uint32_t nt = sh_ntags;
+    for (uint32_t x = tid; x < dn; x += kOneParThreads) {
+      uint32_t lo = 0, hi = nt;  // the last tag with offset <= x
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((T[mid] >> 16) <= x) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t p = T[lo] & 0xFFFF, o = T[lo] >> 16;
+      uint32_t np, dl, hl, off;
+      bool lit;
+      snappy_tag_at(in, p, clen, &np, &dl, &hl, &off, &lit);
+      P[x] = lit ? uint16_t(0x8000u | in[p + hl + (x - o)]) : uint16_t(x - off);
+    }
+    __syncthreads();
+    for (uint32_t round = 0; round < 16; round++) {
+      if (tid == 0) sh_more = 0;
+      __syncthreads();
+      uint32_t more = 0;
+      for (uint32_t x = tid; x < dn; x += kOneParThreads) {
+        const uint32_t v = P[x];
+        if (!(v & 0x8000u)) {
+          const uint32_t w = P[v];
+          P[x] = uint16_t(w);
+          more |= (w & 0x8000u) ? 0u : 1u;
+        }
+      }
+      if (more) sh_more = 1;
+      __syncthreads();
+      if (!sh_more) break;
+    }
+    if (!sh_more) {  // (every byte resolved: 16 rounds cover any chain in kOneParOut bytes)
+      for (uint32_t x = tid; x < dn; x += kOneParThreads) out[x] = uint8_t(P[x]);
+      __syncthreads();
+      fin(slate_block_meta{}, true);
+      return;
+    }
+  }
+  // ---- anything the passes refused: the serial decoder reports it (or decodes it)
+  slate_block_meta m{};
+  int st = SLATE_E_SNAPPY_CORRUPT;
+  if (wave == 0 && hdr_ok) st = wave_snappy_decode(in, clen, hdr, out, dn, lane);
+  if (wave == 0 && lane == 0) sh_bad = uint32_t(st);
+  __syncthreads();
+  st = int(sh_bad);
+  m.status = int16_t(st);
+  fin(m, st == SLATE_OK);
+}
+
 hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& args_in, const uint8_t* host_in, uint64_t in_len,
                              uint64_t out_sz, uint64_t row_sz, uint8_t* host_out) {
   DecodeArgs a = args_in;
@@ -1731,6 +1973,15 @@ hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& args_in, const ui
   if ((a.codec != SLATE_CODEC_NONE && a.codec != SLATE_CODEC_SNAPPY) || in_len + 15 > kLargeInCap ||
       out_sz > kLargeOutCap)
     return hipErrorInvalidValue;
+  static const bool par_off = getenv("SLATE_ONE_SERIAL") != nullptr;  // A/B runs: the one-wave decoder
+  if (a.codec == SLATE_CODEC_SNAPPY && !par_off && in_len >= 6 && in_len + 16 <= kOneParIn && out_sz <= kOneParOut &&
+      (reinterpret_cast<uintptr_t>(host_in) & 15) == 0) {
+    static const hipError_t attr_p = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_one_par_kernel),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(kOneParLds));
+    if (attr_p != hipSuccess) return attr_p;
+    decode_one_par_kernel<<<1, kOneParThreads, kOneParLds, st>>>(a, host_in, in_len, out_sz, row_sz, host_out);
+    return hipGetLastError();
+  }
   constexpr size_t lds = kTabBytes + kLargeInCap + kLargeOutCap;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_one_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
@@ -1806,7 +2057,7 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
     decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else if (a.codec == SLATE_CODEC_ZSTD) {
     // the fast path (zstd_fast.hip), then the exact path over the blocks it handed back
-    (void)hipMemsetAsync(s.zf.count, 0, 2 * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(s.zf.count, 0, 3 * sizeof(uint32_t), st);
     hipError_t e = launch_zstd_fast(st, a, s.zf, num_cus);
     if (e != hipSuccess) return e;
     decode_list_kernel<2><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);
@@ -1833,7 +2084,7 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
 #endif
   } else if (a.codec == SLATE_CODEC_LZ4 && !a.raw && !(dbg_bits(a) & 16)) {
     // one-block frames lane per block (decode_lpb2.hip), then the exact path over the hand-backs
-    (void)hipMemsetAsync(s.zf.count, 0, 2 * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(s.zf.count, 0, 3 * sizeof(uint32_t), st);
     hipError_t e = launch_lz4_fast(st, a, s.zf, num_cus);
     if (e != hipSuccess) return e;
     decode_list_kernel<0><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);

@@ -114,34 +114,8 @@ constexpr uint32_t kVerifyBatch = SLATE_VERIFY_BATCH;
 #define SLATE_ROW_CPOL 16
 #endif
 constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
-// Row-descriptor stores wait until after the iteration's hole-source load (1), or go out right
-// after the walker (0).  vmcnt retires in issue order, so the next iteration's wait for the hole
-// source (issued after the steps) also waited for every row store of the steps before it.
-#ifndef SLATE_ROWS_DEFER
-#define SLATE_ROWS_DEFER 0
-#endif
-// the step before which the previous iteration's hole source is merged (0..3): later gives the
-// load longer to arrive; a lane's next hole waits for it.  Measured (configs[1], 1M blocks,
-// round 4): 0 -> 4.535 ms, 1 -> 4.469 ms, 2 -> 4.524 ms
-#ifndef SLATE_ABSORB_AT
-#define SLATE_ABSORB_AT 1
-#endif
-// the step before which the next chunks' loads are issued (0..2)
-#ifndef SLATE_REFILL_AT
-#define SLATE_REFILL_AT 0
-#endif
-// flush stores: at the iteration's end (0), or deferred into the next iteration, two after step 0
-// and two after step 1 (1), or one after each step (2)
-#ifndef SLATE_FLUSH_DEFER
-#define SLATE_FLUSH_DEFER 0
-#endif
-// row descriptors staged in LDS per lane (4 slots + a pad slot) and written as transposed runs of
-// 3-4 rows (48-64 bytes) when a lane holds three, instead of one scattered 16-byte store per row
-// (needs 80 more LDS bytes per lane: with SLATE_LPB_THREADS=384, 6 waves per CU)
-#ifndef SLATE_ROW_STAGE
-#define SLATE_ROW_STAGE 0
-#endif
-constexpr uint32_t kRowStageSlots = 4, kRowStride = 16 * (kRowStageSlots + 1);
+// the previous iteration's hole source is merged before step 1 (measured, configs[1], 1 M blocks,
+// round 4: before step 0 4.535 ms, step 1 4.469, step 2 4.524): a step more for the load to arrive
 #ifndef SLATE_WALK_LAG
 #define SLATE_WALK_LAG 64
 #endif
@@ -217,7 +191,6 @@ struct Lane {
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
   uint32_t R, rphase, rneed, rsl, rpl, rflags, ro, nwalk;
-  uint32_t rs_n, rs_idx0;  // SLATE_ROW_STAGE: rows staged in LDS, the row index of the first
   int32_t fk;    // first key length for the prefix check (row.go:203-206), -1 before row 0 decodes
   uint32_t pl0;  // row 0's prefix-length field: block.go's FirstKey length when offsets[0] == 0
   // CodecLz4 (kLz4 instantiation only): the frame's one data block is payload bytes [s0, sn);
@@ -230,13 +203,6 @@ struct Lane {
 
 struct Rsrc {
   __amdgpu_buffer_rsrc_t in, out, rows;
-};
-
-// the rows the walker finished in an iteration's steps 1 and 3 (stored after the hole-source load)
-struct RowOut {
-  v4u row1, row3;
-  uint32_t off1, off3;
-  uint8_t* rst;  // SLATE_ROW_STAGE: this lane's row stage in LDS
 };
 
 // CRC32 of the next committed input chunk (bytes outside the block zeroed).
@@ -642,7 +608,7 @@ __device__ __forceinline__ void snappy_parse(Lane& L, bool act, const uint8_t* i
 // kSlot: 0 and 2 absorb a CRC chunk; 1 and (when needed) 3 run the walker
 template <int kSlot, bool kLz4>
 __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint8_t* in, const uint32_t* tab,
-                                          const Rsrc& R, uint32_t lim_d, uint32_t cend, uint32_t dbg, RowOut& ro) {
+                                          const Rsrc& R, uint32_t lim_d, uint32_t cend, uint32_t dbg) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
   dbg = SLATE_FORCE_DBG;
 #endif
@@ -663,7 +629,7 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
   {
     // (a step before the merge of the previous iteration's hole source makes no hole: the merge
     // would take its pending flag for the old one)
-    const bool mk = (kSlot >= SLATE_ABSORB_AT) & act & !L.dd & L.far & (L.rem != 0) & !L.hp & (L.d <= lim_d);
+    const bool mk = (kSlot >= 1) & act & !L.dd & L.far & (L.rem != 0) & !L.hp & (L.d <= lim_d);
     const uint32_t n = min(L.rem, 16u);
     L.hd = mk ? L.d : L.hd;
     L.hl = mk ? n : L.hl;
@@ -719,23 +685,7 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
     uint32_t ridx;
     const bool have_row = walk(L, ring, act && !(dbg & 128), row, ridx);
     const uint32_t off = (have_row && !(dbg & 16384)) ? L.rows_rel + 16 * ridx : kOOB;
-    if (SLATE_ROW_STAGE) {
-      // staged in LDS (slot rs_n; lanes without a row write the pad slot), stored as transposed
-      // runs at the iteration's end (row_flush)
-      const bool st = have_row && !(dbg & 16384);
-      wr128(ro.rst + 16 * (st ? L.rs_n : kRowStageSlots), row, L.z);
-      L.rs_n += st ? 1u : 0u;
-    } else if (SLATE_ROWS_DEFER) {
-      if (kSlot == 1) {
-        ro.row1 = row;
-        ro.off1 = off;
-      } else {
-        ro.row3 = row;
-        ro.off3 = off;
-      }
-    } else {
-      __builtin_amdgcn_raw_buffer_store_b128(row, R.rows, off, 0, kRowCpol);
-    }
+    __builtin_amdgcn_raw_buffer_store_b128(row, R.rows, off, 0, kRowCpol);
   }
 }
 
@@ -763,55 +713,6 @@ __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs
                                            kOutCpol);
   }
   L.fl += min(done, kRun);
-}
-
-// SLATE_FLUSH_DEFER (experiment): the same four transposed stores, their data read from the ring at
-// the end of the iteration into registers, issued between the next iteration's steps instead of
-// back to back (the wave keeps computing while the address unit takes them)
-struct Flush {
-  v4u v[4];
-  uint32_t off[4];
-};
-__device__ __forceinline__ void flush_prepare(Lane& L, bool act, uint8_t* outs, uint32_t lane, Flush& F,
-                                              uint32_t dbg) {
-  const uint32_t done = act ? min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
-  const uint32_t base = L.out_rel + 16 * L.fl;
-  const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;
-  const uint32_t wave_lane0 = threadIdx.x - lane;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
-    const uint32_t info_o = __shfl(info, int(o), 64);
-    const uint32_t base_o = __shfl(base, int(o), 64);
-    const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
-    F.v[j] = rd128(ring_o + ((((info_o & 7) + c) * 16) & (kOR - 1)), L.z);
-    F.off[j] = (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB;
-  }
-  L.fl += min(done, 4u);
-}
-__device__ __forceinline__ void flush_issue(const Flush& F, uint32_t j, const Rsrc& R) {
-  __builtin_amdgcn_raw_buffer_store_b128(F.v[j], R.out, F.off[j], 0, kOutCpol);
-}
-
-// SLATE_ROW_STAGE: the staged rows of every lane holding at least `min_rows` (1 at the round's
-// end, 3 in the loop: a lane adds at most two per iteration), as four transposed stores: in store j
-// lanes 4i..4i+3 write rows 0..3 of the stage of lane 16j+i, runs of 16-64 contiguous bytes.
-__device__ __forceinline__ void row_flush(Lane& L, const uint8_t* rstages, uint32_t lane, const Rsrc& R,
-                                          uint32_t min_rows) {
-  const bool go = L.rs_n >= min_rows;
-  const uint32_t cnt = go ? L.rs_n : 0u;
-  const uint32_t base = L.rows_rel + 16 * L.rs_idx0;
-  const uint32_t wave_lane0 = threadIdx.x - lane;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
-    const uint32_t cnt_o = __shfl(cnt, int(o), 64);
-    const uint32_t base_o = __shfl(base, int(o), 64);
-    const v4u v = rd128(rstages + (wave_lane0 + o) * kRowStride + 16 * c, L.z);
-    __builtin_amdgcn_raw_buffer_store_b128(v, R.rows, c < cnt_o ? base_o + 16 * c : kOOB, 0, kRowCpol);
-  }
-  L.rs_idx0 += cnt;
-  L.rs_n -= cnt;
 }
 
 }  // namespace
@@ -876,15 +777,10 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
-  uint8_t* rstages = ins + kLpb2Threads * kInStride;  // SLATE_ROW_STAGE (empty otherwise)
-  uint8_t* rst = rstages + threadIdx.x * kRowStride;
   // wave-uniform by construction: the buffer resources derived from it must live in SGPRs
   const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
   const uint32_t wave_g = blockIdx.x * (kLpb2Threads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
-#ifdef SLATE_LPB_PRIO  // experiment: static issue priority for the second half of the workgroup's waves
-  if ((threadIdx.x >> 6) >= kLpb2Threads / 128) __builtin_amdgcn_s_setprio(1);
-#endif
 
   // Rounds are handed out by an atomic counter (one dequeue per round, lane 0): waves that
   // finish early take more, so the launch ends when the work does, not when the unluckiest
@@ -935,7 +831,6 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     L.rphase = 0;
     L.rneed = 4;
     L.rsl = L.rpl = L.rflags = L.ro = L.nwalk = 0;
-    L.rs_n = L.rs_idx0 = 0;
     L.fk = -1;
     L.pl0 = 0xFFFFFFFFu;
     L.sn = L.lph = L.mtok = L.hb = 0;
@@ -1027,12 +922,6 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     // `budget` iterations; the budget only guarantees that the loop ends (an exhausted
     // lane reports SLATE_E_HIP, never a wrong result).
     const uint32_t budget = have ? (L.clen + L.dn) / 2 + 1024 : 0u;
-    Flush F;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
-      F.v[j] = zero;
-      F.off[j] = kOOB;
-    }
     while (__ballot(have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
                     iters < budget)) {
       const bool act = have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
@@ -1043,9 +932,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       commit_one(ins, S2, P2, L.z);
       commit_one(ins, S3, P3, L.z);
       L.c_commit += L.n_req;
-      // the next chunks' loads (committed at the next iteration's start): at the iteration's start,
-      // or after step SLATE_REFILL_AT - 1 (their registers then live for fewer steps)
-      auto issue_refill = [&]() {
+      // the next chunks' loads (committed at the next iteration's start)
+      {
         // the ring keeps every chunk from the oldest byte still to be read or CRC'd
         const uint32_t lo_pos = L.dd ? L.sh + L.clen : ((L.rem && L.lit) ? L.src : L.sh + L.s);
         const uint32_t lo_chunk = min(lo_pos >> 4, L.crc_pos);
@@ -1059,62 +947,29 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         load_one(3, lane, wave_lane0, info, rel, R, P3, S3);
         L.c_issue += n;
         L.n_req = n;
-      };
-      if (SLATE_REFILL_AT == 0) issue_refill();
+      }
       // per iteration: the throttle's limit on d, and the end of the committed input (ring positions)
       const uint32_t lim_d = 16 * L.fl + kUnflushed, cend = 16 * L.c_commit;
-      RowOut ro;
-      ro.rst = rst;
-      ro.off1 = ro.off3 = kOOB;
-      ro.row1 = ro.row3 = zero;
       LPB_MARK(absorb);
-      if (SLATE_ABSORB_AT == 0) absorb_hole(L, Q, ring);
-      lane_step<0, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
-      if (SLATE_FLUSH_DEFER == 1) {
-        flush_issue(F, 0, R);
-        flush_issue(F, 1, R);
-      }
-      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 0, R);
-      if (SLATE_ABSORB_AT == 1) absorb_hole(L, Q, ring);
-      if (SLATE_REFILL_AT == 1) issue_refill();
-      lane_step<1, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
-      if (SLATE_FLUSH_DEFER == 1) {
-        flush_issue(F, 2, R);
-        flush_issue(F, 3, R);
-      }
-      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 1, R);
-      if (SLATE_ABSORB_AT == 2) absorb_hole(L, Q, ring);
-      if (SLATE_REFILL_AT == 2) issue_refill();
-      lane_step<2, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
-      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 2, R);
-      if (SLATE_ABSORB_AT == 3) absorb_hole(L, Q, ring);
-      lane_step<3, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a), ro);
-      if (SLATE_FLUSH_DEFER == 2) flush_issue(F, 3, R);
+      lane_step<0, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      absorb_hole(L, Q, ring);
+      lane_step<1, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      lane_step<2, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      lane_step<3, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
       // the hole source requested in this iteration (at most one per lane; sc1: L1 bypass),
       // before the flush stores so that vmcnt waits stay static; it is merged at the start of
       // the next iteration
       LPB_MARK(flush);
       Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg_bits(a) & 32768) ? kOOB : L.qoff, 0, 16);
       L.qoff = kOOB;
-      if (SLATE_ROWS_DEFER) {
-        __builtin_amdgcn_raw_buffer_store_b128(ro.row1, R.rows, ro.off1, 0, kRowCpol);
-        __builtin_amdgcn_raw_buffer_store_b128(ro.row3, R.rows, ro.off3, 0, kRowCpol);
-      }
-      if (SLATE_FLUSH_DEFER) flush_prepare(L, act, outs, lane, F, dbg_bits(a));
-      else flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts);
-      if (SLATE_ROW_STAGE) row_flush(L, rstages, lane, R, 3);
+      flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts);
       if constexpr (kLz4) {
-        // the content checksum's stripes: the chunks just completed (at most four), still in the ring
+        // the content checksum's stripes: the chunks completed so far (up to kStep / 4), still in the ring
 #pragma unroll
         for (uint32_t j = 0; j < kStep / 4; j++) xxh_absorb(L, ring, L.xp < min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu));
       }
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
-    }
-    if (SLATE_ROW_STAGE) row_flush(L, rstages, lane, R, 1);  // the rows still staged
-    if (SLATE_FLUSH_DEFER) {  // the last iteration's chunks, before anything reads the output back
-#pragma unroll
-      for (uint32_t j = 0; j < 4; j++) flush_issue(F, j, R);
     }
     const uint32_t round_cycles = (dbg_bits(a) & 512) ? uint32_t(__builtin_amdgcn_s_memtime() - t_round) : 0u;
 
@@ -1327,7 +1182,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
 
 size_t lpb2_lds_bytes() {
-  return kLpbTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride + (SLATE_ROW_STAGE ? kRowStride : 0));
+  return kLpbTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
 // CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order

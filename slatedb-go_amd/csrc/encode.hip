@@ -685,21 +685,37 @@ __global__ __launch_bounds__(64) void snappy_chunks_kernel(const uint8_t* __rest
 // ------------------------------------------------------------------- bloom
 __device__ inline uint32_t mod_u32(uint32_t x, uint32_t m) { return x % m; }
 
+// bloom.go:147-160 probesForKey in 32-bit arithmetic: every value is below filterBits (< 2^32), so
+// the first two reductions are 32-bit and the later ones a conditional subtraction (h + delta <
+// 2 filterBits; delta + i below filterBits + i, with the modulo kept for i >= filterBits) -- the
+// same values as Go's uint64 % (the probes computed two 64-bit modulos each)
+struct BloomProbes {
+  uint32_t h, delta, m, k;
+  __device__ BloomProbes(uint64_t h64, uint32_t filter_bits) : m(filter_bits), k(0) {
+    h = uint32_t(h64) % m;
+    delta = uint32_t(h64 >> 32) % m;
+  }
+  __device__ uint32_t next() {
+    const uint64_t d = uint64_t(delta) + k;
+    delta = d < m ? uint32_t(d) : (d - m < m ? uint32_t(d - m) : uint32_t(d % m));
+    k++;
+    const uint32_t p = h;
+    const uint64_t hh = uint64_t(h) + delta;
+    h = hh < m ? uint32_t(hh) : uint32_t(hh - m);
+    return p;
+  }
+};
+
 // bloom.go:147-160 probes for one key hash, setBit (bloom.go:169-172) as an
 // atomicOr on the little-endian 32-bit word holding byte p/8.
 __global__ void bloom_build_kernel(const uint64_t* __restrict__ hashes, uint64_t n, uint32_t num_probes,
                                    uint32_t filter_bits, uint32_t* __restrict__ words) {
   uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t h64 = hashes[i];
-  uint64_t m = filter_bits;
-  uint64_t h = (h64 & 0xFFFFFFFFull) % m;
-  uint64_t delta = (h64 >> 32) % m;
+  BloomProbes pr(hashes[i], filter_bits);
   for (uint32_t k = 0; k < num_probes; k++) {
-    delta = (delta + k) % m;
-    uint32_t p = uint32_t(h);
+    const uint32_t p = pr.next();
     atomicOr(&words[p >> 5], 1u << (p & 31));
-    h = (h + delta) % m;
   }
 }
 
@@ -719,20 +735,6 @@ constexpr uint32_t kBktSliceLog = SLATE_BKT_SLICE_LOG;  // 2^19 bits = 64 KiB of
 constexpr uint32_t kBktMaxSlices = 8192, kBktOrThreads = SLATE_BKT_OR_THREADS;
 constexpr uint64_t kBktMaxCells = 1ull << 24;  // (slices x key workgroups) counters
 
-struct BloomProbes {
-  uint64_t h, delta, m;
-  uint32_t k;
-  __device__ BloomProbes(uint64_t h64, uint32_t filter_bits) : m(filter_bits), k(0) {
-    h = (h64 & 0xFFFFFFFFull) % m;
-    delta = (h64 >> 32) % m;
-  }
-  __device__ uint32_t next() {  // bloom.go:147-160, as bloom_build_kernel
-    delta = (delta + k++) % m;
-    const uint32_t p = uint32_t(h);
-    h = (h + delta) % m;
-    return p;
-  }
-};
 
 __global__ __launch_bounds__(kBktThreads) void bloom_count_kernel(const uint64_t* __restrict__ hashes, uint64_t n,
                                                                   uint32_t num_probes, uint32_t filter_bits,
@@ -822,13 +824,10 @@ __global__ void bloom_check_kernel(const uint8_t* __restrict__ keys, const uint6
   m &= 0xFFFFFFFFull;  // uint32(len(f.Data)*8) (bloom.go:24)
   uint8_t res = 1;
   if (m == 0) { out[i] = 0; return; }
-  uint64_t h = (h64 & 0xFFFFFFFFull) % m;
-  uint64_t delta = (h64 >> 32) % m;
+  BloomProbes pr(h64, uint32_t(m));
   for (uint32_t q = 0; q < num_probes; q++) {
-    delta = (delta + q) % m;
-    uint32_t p = uint32_t(h);
+    const uint32_t p = pr.next();
     if (!(bits[p >> 3] & (1u << (p & 7)))) { res = 0; break; }
-    h = (h + delta) % m;
   }
   out[i] = res;
 }

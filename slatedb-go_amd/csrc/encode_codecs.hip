@@ -208,7 +208,12 @@ __device__ uint32_t lz4_body(const uint8_t* tags, uint32_t tn, const uint8_t* ra
   return w.d;
 }
 
-// ------------------------------------------------------------------ deflate (fixed Huffman)
+// a match of the parse: Zstd (literal run before, length, offset) / deflate (position, length, offset)
+struct Seq {
+  uint32_t ll, ml, off;
+};
+
+// ------------------------------------------------------------------ deflate
 __device__ __constant__ uint16_t kDLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                                   31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
 __device__ __constant__ uint8_t kDLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
@@ -267,38 +272,386 @@ __device__ void deflate_matches(const uint8_t* tags, uint32_t tn, uint32_t lane,
   }
 }
 
-// one piece as deflate blocks: fixed Huffman, or stored when that is not larger; a non-final
-// piece ends with an empty stored block (byte alignment for the next piece)
-__device__ uint32_t deflate_body(const uint8_t* tags, uint32_t tn, const uint8_t* raw, uint32_t n, bool final,
-                                 uint8_t* dst, uint32_t cap, uint32_t lane, bool* over) {
-  // size of the fixed-Huffman form, in bits
-  uint64_t bits = 3 + 7;
+// ---- dynamic Huffman (RFC 1951 3.2.7).  Per-wave scratch of the entropy stage (LDS).
+constexpr uint32_t kDSyms = 286 + 30;  // literal / length codes, then distance codes
+struct DFse {
+  uint32_t freq[kDSyms];
+  uint32_t A[kDSyms];          // the in-place Huffman array (sorted weights -> lengths)
+  uint16_t order[kDSyms];      // symbols by ascending frequency
+  uint16_t code[kDSyms];       // bit-reversed canonical codes
+  uint8_t len[kDSyms];
+  uint16_t rle[kDSyms];        // the code-length sequence, RLE-coded: symbol | extra << 5
+  uint32_t cfreq[19];
+  uint8_t clen[19];
+  uint16_t ccode[19];
+  uint32_t blc[17];
+  uint32_t nextc[17];
+};
+constexpr uint32_t kDFseBytes = (sizeof(DFse) + 15) & ~15u;
+constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// Code lengths of a minimum-redundancy code over freq[0..n) limited to maxbits (Moffat-Katajainen
+// in-place algorithm on the weights sorted by a wave-parallel rank, then zlib's overflow fix: leaves
+// deeper than maxbits lifted, the Kraft sum restored by splitting shallower leaves, the lengths
+// handed out shortest-first by frequency).  A single used symbol gets length 1.  len[] is written.
+__device__ void huff_lengths(DFse* F, const uint32_t* freq, uint8_t* len, uint16_t* order, uint32_t n, uint32_t maxbits,
+                             uint32_t lane) {
+  // rank sort of the used symbols by (frequency, symbol)
+  uint32_t used = 0;
+  for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+    const uint32_t s = s0 + lane;
+    const bool u = s < n && freq[s] != 0;
+    used += uint32_t(__builtin_popcountll(__ballot(u)));
+  }
+  for (uint32_t s = lane; s < n; s += 64) {
+    len[s] = 0;
+    const uint32_t f = freq[s];
+    if (!f) continue;
+    uint32_t r = 0;
+    for (uint32_t t = 0; t < n; t++) {
+      const uint32_t g = freq[t];
+      r += (g != 0 && (g < f || (g == f && t < s))) ? 1u : 0u;
+    }
+    order[r] = uint16_t(s);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane == 0 && used) {
+    uint32_t* A = F->A;
+    if (used == 1) {
+      len[order[0]] = 1;
+    } else {
+      const int m = int(used);
+      for (int i = 0; i < m; i++) A[i] = freq[order[i]];
+      // phase 1: internal node weights, parents
+      A[0] += A[1];
+      int root = 0, leaf = 2;
+      for (int next = 1; next < m - 1; next++) {
+        if (leaf >= m || A[root] < A[leaf]) {
+          A[next] = A[root];
+          A[root++] = uint32_t(next);
+        } else {
+          A[next] = A[leaf++];
+        }
+        if (leaf >= m || (root < next && A[root] < A[leaf])) {
+          A[next] += A[root];
+          A[root++] = uint32_t(next);
+        } else {
+          A[next] += A[leaf++];
+        }
+      }
+      // phase 2: internal node depths
+      A[m - 2] = 0;
+      for (int next = m - 3; next >= 0; next--) A[next] = A[A[next]] + 1;
+      // phase 3: leaf depths (ascending weight -> descending depth)
+      int avail = 1, usedn = 0, depth = 0, r = m - 2, next = m - 1;
+      while (avail > 0) {
+        while (r >= 0 && int(A[r]) == depth) {
+          usedn++;
+          r--;
+        }
+        while (avail > usedn) {
+          A[next--] = uint32_t(depth);
+          avail--;
+        }
+        avail = 2 * usedn;
+        depth++;
+        usedn = 0;
+      }
+      // A[i] = the length of order[i] (A ascending in weight: A[0] the rarest, longest)
+      uint32_t* bl = F->blc;
+      for (uint32_t k = 0; k <= 16; k++) bl[k] = 0;
+      uint32_t maxl = 0;
+      for (int i = 0; i < m; i++) {
+        const uint32_t l = A[i] > maxbits ? maxbits : A[i];
+        maxl = A[i] > maxl ? A[i] : maxl;
+        bl[l]++;
+      }
+      if (maxl > maxbits) {
+        uint64_t kraft = 0;
+        for (uint32_t l = 1; l <= maxbits; l++) kraft += uint64_t(bl[l]) << (maxbits - l);
+        while (kraft > (uint64_t(1) << maxbits)) {
+          uint32_t l = maxbits - 1;
+          while (bl[l] == 0) l--;
+          bl[l]--;
+          bl[l + 1] += 2;
+          bl[maxbits]--;
+          kraft--;
+        }
+        // shortest lengths to the most frequent symbols
+        int i = m - 1;
+        for (uint32_t l = 1; l <= maxbits; l++)
+          for (uint32_t k = 0; k < bl[l]; k++) A[i--] = l;
+      }
+      for (int i = 0; i < m; i++) len[order[i]] = uint8_t(A[i]);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// canonical codes (RFC 1951 3.2.2), bit-reversed for the LSB-first writer; one lane
+__device__ void huff_codes(const uint8_t* len, uint16_t* code, uint32_t n, uint32_t* blc, uint32_t* next) {
+  for (uint32_t k = 0; k <= 16; k++) blc[k] = 0;
+  for (uint32_t s = 0; s < n; s++) blc[len[s]]++;
+  blc[0] = 0;
+  uint32_t c = 0;
+  for (uint32_t b = 1; b <= 16; b++) {
+    c = (c + blc[b - 1]) << 1;
+    next[b] = c;
+  }
+  for (uint32_t s = 0; s < n; s++) {
+    const uint32_t l = len[s];
+    code[s] = l ? uint16_t(rev(next[l]++, l)) : 0;
+  }
+}
+
+// A source of deflate matches (lengths 3..258, distances <= 32768) in order: the golang/snappy
+// parse's copies (tags), or a list the chain parse built (Seq: ll = position, ml = length).
+struct DSrc {
+  const uint8_t* tags;
+  uint32_t tn;
+  const Seq* list;  // nullptr: the tags
+  uint32_t nlist;
+  template <typename F>
+  __device__ void each(uint32_t lane, F&& emit) const {
+    if (!list) {
+      deflate_matches(tags, tn, lane, emit);
+      return;
+    }
+    for (uint32_t i = 0; i < nlist; i++) {
+      const Seq q = list[i];
+      emit(uint32_t(__builtin_amdgcn_readfirstlane(q.ll)), uint32_t(__builtin_amdgcn_readfirstlane(q.ml)),
+           uint32_t(__builtin_amdgcn_readfirstlane(q.off)));
+    }
+  }
+};
+
+// Greedy LZ77 parse with hash chains (3-byte minimum, zlib's match rules: lengths 3..258,
+// distances <= 32768, up to kChain candidates per position) of a piece of at most kSmallPiece bytes
+// staged in LDS (`raw`); matches into `out` (at most cap).  Candidates are compared 64 bytes at a
+// time across the lanes.  The count, or ~0u when cap is exceeded.
+constexpr uint32_t kChain = 32, kNice = 128, kHashBits = 12;
+__device__ uint32_t chain_parse(const uint8_t* raw, uint32_t n, uint16_t* head, uint16_t* prev, Seq* out, uint32_t cap,
+                                uint32_t lane) {
+  for (uint32_t h = lane; h < (1u << kHashBits); h += 64) head[h] = 0xFFFF;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  auto hash = [&](uint32_t p) {
+    const uint32_t v = uint32_t(raw[p]) | (uint32_t(raw[p + 1]) << 8) | (uint32_t(raw[p + 2]) << 16);
+    return (v * 2654435761u) >> (32 - kHashBits);
+  };
+  auto insert = [&](uint32_t p) {
+    const uint32_t h = hash(p);
+    const uint32_t c = head[h];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      prev[p] = uint16_t(c);
+      head[h] = uint16_t(p);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  uint32_t nm = 0, p = 0;
+  while (p + 3 <= n) {
+    const uint32_t lim = min(258u, n - p);
+    uint32_t best = 0, boff = 0, c = head[hash(p)];
+    for (uint32_t k = 0; k < kChain && c != 0xFFFF && best < kNice; k++) {
+      uint32_t l = 0;
+      for (;;) {  // common prefix of raw[c..] and raw[p..], 64 bytes per round
+        const uint32_t i = l + lane;
+        const bool same = i < lim && raw[c + i] == raw[p + i];
+        const uint64_t miss = ~__ballot(same);
+        if (miss) {
+          l += uint32_t(__builtin_ctzll(miss));
+          break;
+        }
+        l += 64;
+      }
+      if (l > best) {
+        best = l;
+        boff = p - c;
+      }
+      c = prev[c];
+    }
+    if (best >= 3) {
+      if (nm >= cap) return ~0u;
+      if (lane == 0) out[nm] = Seq{p, best, boff};
+      nm++;
+      for (uint32_t q = p; q < p + best && q + 3 <= n; q++) insert(q);
+      p += best;
+    } else {
+      insert(p);
+      p++;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return nm;
+}
+
+// One piece as deflate blocks: dynamic Huffman, fixed Huffman or stored, whichever is smallest; a
+// non-final piece ends with an empty stored block (byte alignment for the next piece).
+__device__ uint32_t deflate_body(const DSrc& src, const uint8_t* raw, uint32_t n, bool final, uint8_t* dst, uint32_t cap,
+                                 DFse* F, uint32_t lane, bool* over) {
+  auto sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // symbol frequencies (and the fixed form's size, in bits)
+  for (uint32_t s = lane; s < kDSyms; s += 64) F->freq[s] = 0;
+  sync();
+  uint64_t fbits = 3 + 7, xbits = 0;  // fixed-form bits; extra bits (both Huffman forms)
   {
-    Win r{raw, n};
     uint32_t lit = 0;
     auto lits = [&](uint32_t a, uint32_t e) {
-      for (uint32_t p = a; p < e; p++) bits += fixed_bits(r.at(p, lane));
+      uint32_t fb = 0;
+      for (uint32_t q = a + lane; q < e; q += 64) {
+        const uint32_t c = raw[q];
+        atomicAdd(&F->freq[c], 1u);
+        fb += fixed_bits(c);
+      }
+      for (int o = 32; o >= 1; o >>= 1) fb += uint32_t(__shfl_xor(int(fb), o, 64));
+      fbits += uint32_t(__builtin_amdgcn_readfirstlane(fb));
     };
-    deflate_matches(tags, tn, lane, [&](uint32_t pos, uint32_t len, uint32_t off) {
+    src.each(lane, [&](uint32_t pos, uint32_t len, uint32_t off) {
       lits(lit, pos);
       const uint32_t lc = dcode_len(len), dc = dcode_dist(off);
-      bits += fixed_bits(257 + lc) + kDLenExtra[lc] + 5 + kDDistExtra[dc];
+      if (lane == 0) {
+        F->freq[257 + lc]++;
+        F->freq[286 + dc]++;
+      }
+      fbits += fixed_bits(257 + lc) + 5;
+      xbits += kDLenExtra[lc] + kDDistExtra[dc];
       lit = pos + len;
     });
     lits(lit, n);
   }
+  sync();
+  if (lane == 0) {
+    F->freq[256] = 1;
+    bool anyd = false;
+    for (uint32_t d = 0; d < 30; d++) anyd |= F->freq[286 + d] != 0;
+    if (!anyd) F->freq[286] = 1;  // one distance code of length 1: no match uses it
+  }
+  sync();
+  fbits += 7 + xbits;
+  huff_lengths(F, F->freq, F->len, F->order, 286, 15, lane);
+  huff_lengths(F, F->freq + 286, F->len + 286, F->order, 30, 15, lane);
+  // the header: HLIT / HDIST, the code lengths RLE-coded (16: repeat the previous 3..6 times, 17 / 18:
+  // 3..10 / 11..138 zeros), the code-length code
+  uint32_t hlit = 257, hdist = 1, nrle = 0, hclen = 4;
+  uint64_t dbits = 0;
+  if (lane == 0) {
+    for (uint32_t s = 257; s < 286; s++)
+      if (F->len[s]) hlit = s + 1;
+    for (uint32_t d = 1; d < 30; d++)
+      if (F->len[286 + d]) hdist = d + 1;
+    auto L = [&](uint32_t i) -> uint32_t { return i < hlit ? F->len[i] : F->len[286 + i - hlit]; };
+    const uint32_t tot = hlit + hdist;
+    for (uint32_t k = 0; k < 19; k++) F->cfreq[k] = 0;
+    uint32_t i = 0;
+    while (i < tot) {
+      const uint32_t v = L(i);
+      uint32_t r = 1;
+      while (i + r < tot && L(i + r) == v) r++;
+      uint32_t k = r;
+      if (v == 0 && r >= 3) {
+        while (k >= 3) {
+          const uint32_t m = k < 138 ? k : 138;
+          const uint32_t sym = m >= 11 ? 18u : 17u;
+          F->rle[nrle++] = uint16_t(sym | ((m - (m >= 11 ? 11u : 3u)) << 5));
+          F->cfreq[sym]++;
+          k -= m;
+        }
+      } else if (v != 0 && r >= 4) {
+        F->rle[nrle++] = uint16_t(v);
+        F->cfreq[v]++;
+        k = r - 1;
+        while (k >= 3) {
+          const uint32_t m = k < 6 ? k : 6;
+          F->rle[nrle++] = uint16_t(16 | ((m - 3) << 5));
+          F->cfreq[16]++;
+          k -= m;
+        }
+      }
+      for (; k > 0; k--) {
+        F->rle[nrle++] = uint16_t(v);
+        F->cfreq[v]++;
+      }
+      i += r;
+    }
+  }
+  hlit = uint32_t(__builtin_amdgcn_readfirstlane(hlit));
+  hdist = uint32_t(__builtin_amdgcn_readfirstlane(hdist));
+  nrle = uint32_t(__builtin_amdgcn_readfirstlane(nrle));
+  sync();
+  huff_lengths(F, F->cfreq, F->clen, F->order, 19, 7, lane);
+  if (lane == 0) {
+    for (uint32_t k = 0; k < 19; k++)
+      if (F->clen[kClOrder[k]]) hclen = k + 1 > hclen ? k + 1 : hclen;
+    huff_codes(F->len, F->code, 286, F->blc, F->nextc);
+    huff_codes(F->len + 286, F->code + 286, 30, F->blc, F->nextc);
+    huff_codes(F->clen, F->ccode, 19, F->blc, F->nextc);
+    dbits = 3 + 5 + 5 + 4 + 3 * hclen;
+    for (uint32_t j = 0; j < nrle; j++) {
+      const uint32_t sym = F->rle[j] & 31;
+      dbits += F->clen[sym] + (sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0);
+    }
+    for (uint32_t s = 0; s < kDSyms; s++) dbits += uint64_t(F->freq[s]) * F->len[s];
+    dbits += xbits;
+  }
+  hclen = uint32_t(__builtin_amdgcn_readfirstlane(hclen));
+  dbits = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(dbits >> 32))) << 32) |
+          __builtin_amdgcn_readfirstlane(uint32_t(dbits));
+  sync();
   const uint64_t stored = 8ull * (n + 5 * ((n + 65534) / 65535 + (n == 0))) + 8;
   BW w{dst, 0, cap, false};
   Bits b;
-  if (bits <= stored) {
+  if (dbits <= fbits && dbits <= stored) {
     b.add(w, lane, final ? 1 : 0, 1);
-    b.add(w, lane, 1, 2);  // BTYPE 01
-    Win r{raw, n};
+    b.add(w, lane, 2, 2);  // BTYPE 10
+    b.add(w, lane, hlit - 257, 5);
+    b.add(w, lane, hdist - 1, 5);
+    b.add(w, lane, hclen - 4, 4);
+    for (uint32_t k = 0; k < hclen; k++) b.add(w, lane, F->clen[kClOrder[k]], 3);
+    for (uint32_t j = 0; j < nrle; j++) {
+      const uint32_t e = F->rle[j], sym = e & 31;
+      b.add(w, lane, F->ccode[sym], F->clen[sym]);
+      if (sym >= 16) b.add(w, lane, e >> 5, sym == 16 ? 2 : sym == 17 ? 3 : 7);
+    }
     uint32_t lit = 0;
     auto lits = [&](uint32_t a, uint32_t e) {
-      for (uint32_t p = a; p < e; p++) fixed_sym(b, w, lane, r.at(p, lane));
+      for (uint32_t q = a; q < e; q++) {
+        const uint32_t c = raw[q];
+        b.add(w, lane, F->code[c], F->len[c]);
+      }
     };
-    deflate_matches(tags, tn, lane, [&](uint32_t pos, uint32_t len, uint32_t off) {
+    src.each(lane, [&](uint32_t pos, uint32_t len, uint32_t off) {
+      lits(lit, pos);
+      const uint32_t lc = dcode_len(len), dc = dcode_dist(off);
+      b.add(w, lane, F->code[257 + lc], F->len[257 + lc]);
+      b.add(w, lane, len - kDLenBase[lc], kDLenExtra[lc]);
+      b.add(w, lane, F->code[286 + dc], F->len[286 + dc]);
+      b.add(w, lane, off - kDDistBase[dc], kDDistExtra[dc]);
+      lit = pos + len;
+    });
+    lits(lit, n);
+    b.add(w, lane, F->code[256], F->len[256]);
+  } else if (fbits <= stored) {
+    b.add(w, lane, final ? 1 : 0, 1);
+    b.add(w, lane, 1, 2);  // BTYPE 01
+    uint32_t lit = 0;
+    auto lits = [&](uint32_t a, uint32_t e) {
+      for (uint32_t q = a; q < e; q++) fixed_sym(b, w, lane, raw[q]);
+    };
+    src.each(lane, [&](uint32_t pos, uint32_t len, uint32_t off) {
       lits(lit, pos);
       const uint32_t lc = dcode_len(len), dc = dcode_dist(off);
       fixed_sym(b, w, lane, 257 + lc);
@@ -410,20 +763,30 @@ __device__ __constant__ FseCT<36, 6> kCtLL(kLLDef);
 __device__ __constant__ FseCT<53, 6> kCtML(kMLDef);
 __device__ __constant__ FseCT<29, 5> kCtOF(kOFDef);
 
+// An FSE compression table in memory (the predefined ones above, or one built for a block).
+struct FseRT {
+  const uint16_t* state;
+  const uint32_t* dnb;
+  const int32_t* dfs;
+  uint32_t L;
+};
 template <int N, int LOG>
-struct FseState {
+__device__ inline FseRT fse_rt(const FseCT<N, LOG>& t) {
+  return FseRT{t.state, t.delta_nb, reinterpret_cast<const int32_t*>(t.delta_find), uint32_t(LOG)};
+}
+struct FseStateR {
   uint32_t v;
-  __device__ void init(const FseCT<N, LOG>& t, uint32_t s) {
-    const uint32_t nb_out = (t.delta_nb[s] + (1u << 15)) >> 16;
-    const uint32_t v0 = (nb_out << 16) - t.delta_nb[s];
-    v = t.state[(v0 >> nb_out) + t.delta_find[s]];
+  __device__ void init(const FseRT& t, uint32_t s) {
+    const uint32_t nb_out = (t.dnb[s] + (1u << 15)) >> 16;
+    const uint32_t v0 = (nb_out << 16) - t.dnb[s];
+    v = t.state[(v0 >> nb_out) + t.dfs[s]];
   }
-  __device__ void enc(Bits& b, BW& w, uint32_t lane, const FseCT<N, LOG>& t, uint32_t s) {
-    const uint32_t nb_out = (v + t.delta_nb[s]) >> 16;
+  __device__ void enc(Bits& b, BW& w, uint32_t lane, const FseRT& t, uint32_t s) {
+    const uint32_t nb_out = (v + t.dnb[s]) >> 16;
     b.add(w, lane, v, nb_out);
-    v = t.state[(v >> nb_out) + t.delta_find[s]];
+    v = t.state[(v >> nb_out) + t.dfs[s]];
   }
-  __device__ void flush(Bits& b, BW& w, uint32_t lane) { b.add(w, lane, v, LOG); }
+  __device__ void flush(Bits& b, BW& w, uint32_t lane, const FseRT& t) { b.add(w, lane, v, t.L); }
 };
 
 __device__ inline uint32_t ll_code(uint32_t v) {
@@ -439,13 +802,144 @@ __device__ inline uint32_t ml_code(uint32_t m) {  // m = match length
   return c;
 }
 
-struct Seq {
-  uint32_t ll, ml, off;
+// The sequences' entropy stage (per wave, LDS): symbol counts, a normalized distribution, and the
+// three compression tables built for the block.  Symbols of the three types side by side: LL codes
+// at 0..35, OF at 36..67, ML at 68..120.
+constexpr uint32_t kSymLL = 0, kSymOF = 36, kSymML = 68, kNSym = 121;
+struct ZFse {
+  uint32_t cnt[kNSym];
+  uint32_t dnb[kNSym];
+  int32_t dfs[kNSym];
+  int16_t norm[kNSym + 1];
+  uint32_t cumul[56];
+  uint16_t state[512 + 256 + 512];  // LL (log <= 9), OF (<= 8), ML (<= 9)
+  uint8_t sym[512];
 };
+constexpr uint32_t kZFseBytes = (sizeof(ZFse) + 15) & ~15u;
+constexpr uint32_t kStOff[3] = {0, 512, 768};
 
-// a compressed block body: raw literals section, then the sequences (predefined tables)
+// log2(x) * 256 for x >= 1, linear between powers of two (the mode choice's cost estimate)
+__device__ inline uint32_t lg256(uint32_t x) {
+  const uint32_t h = 31 - __builtin_clz(x);
+  return 256 * h + (((x << 8) >> h) - 256);
+}
+
+// zstd's FSE_optimalTableLog for nseq sequences whose largest code is maxsym
+__device__ inline uint32_t fse_table_log(uint32_t nseq, uint32_t maxsym, uint32_t maxlog) {
+  const int hb_src = nseq > 1 ? 31 - __builtin_clz(nseq - 1) : 0;
+  const uint32_t maxbits = hb_src >= 2 ? uint32_t(hb_src - 2) : 0u;
+  const uint32_t minbits = min(uint32_t(31 - __builtin_clz(nseq)) + 1, (maxsym ? uint32_t(31 - __builtin_clz(maxsym)) : 0u) + 2);
+  uint32_t L = maxlog;
+  if (maxbits < L) L = maxbits;
+  if (minbits > L) L = minbits;
+  return max(5u, min(L, maxlog));
+}
+
+// counts -> a distribution over 2^L (every used symbol at least -1, the remainder on the most frequent);
+// false if the remainder does not fit
+__device__ bool fse_normalize(const uint32_t* cnt, uint32_t n, uint32_t tot, uint32_t L, int16_t* norm) {
+  const uint32_t size = 1u << L;
+  int32_t rest = int32_t(size);
+  uint32_t big = 0;
+  for (uint32_t s = 0; s < n; s++) {
+    big = cnt[s] > cnt[big] ? s : big;
+    int32_t v = 0;
+    if (cnt[s]) {
+      v = int32_t((uint64_t(cnt[s]) * size) / tot);
+      v = v ? v : -1;
+      rest -= v < 0 ? 1 : v;
+    }
+    norm[s] = int16_t(v);
+  }
+  const int32_t nb = int32_t(norm[big]) + rest;
+  if (nb <= 0) return false;
+  norm[big] = int16_t(nb);
+  return true;
+}
+
+// FSE_writeNCount of norm[0..n) at accuracy L (dry: count the bits only); the bit count
+__device__ uint32_t fse_ncount(Bits* b, BW* w, uint32_t lane, const int16_t* norm, uint32_t n, uint32_t L) {
+  uint32_t bits = 4;
+  if (b) b->add(*w, lane, L - 5, 4);
+  int32_t rem = (1 << L) + 1, thr = 1 << L;
+  uint32_t nbits = L + 1, s = 0;
+  bool prev0 = false;
+  while (s < n && rem > 1) {
+    if (prev0) {
+      uint32_t start = s;
+      while (s < n && norm[s] == 0) s++;
+      while (s >= start + 3) {
+        start += 3;
+        if (b) b->add(*w, lane, 3, 2);
+        bits += 2;
+      }
+      if (b) b->add(*w, lane, s - start, 2);
+      bits += 2;
+    }
+    int32_t c = norm[s++];
+    const int32_t mx = 2 * thr - 1 - rem;
+    rem -= c < 0 ? -c : c;
+    c++;
+    if (c >= thr) c += mx;
+    const uint32_t k = nbits - (c < mx ? 1u : 0u);
+    if (b) b->add(*w, lane, uint32_t(c), k);
+    bits += k;
+    prev0 = c == 1;
+    while (rem < thr) {
+      nbits--;
+      thr >>= 1;
+    }
+  }
+  return bits;
+}
+
+// FSE_buildCTable (the FseCT constructor at run time, on one lane): state[2^L], dnb / dfs per symbol
+__device__ void fse_build_ct(const int16_t* norm, uint32_t n, uint32_t L, uint16_t* state, uint32_t* dnb, int32_t* dfs,
+                             uint32_t* cumul, uint8_t* sym) {
+  const uint32_t size = 1u << L, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+  uint32_t high = size - 1;
+  cumul[0] = 0;
+  for (uint32_t u = 1; u <= n; u++) {
+    if (norm[u - 1] == -1) {
+      cumul[u] = cumul[u - 1] + 1;
+      sym[high--] = uint8_t(u - 1);
+    } else {
+      cumul[u] = cumul[u - 1] + uint32_t(norm[u - 1]);
+    }
+  }
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s < n; s++)
+    for (int k = 0; k < norm[s]; k++) {
+      sym[pos] = uint8_t(s);
+      pos = (pos + step) & mask;
+      while (pos > high) pos = (pos + step) & mask;
+    }
+  for (uint32_t u = 0; u < size; u++) state[cumul[sym[u]]++] = uint16_t(size + u);
+  uint32_t total = 0;
+  for (uint32_t s = 0; s < n; s++) {
+    const int c = norm[s];
+    if (c == 0) {
+      dnb[s] = ((L + 1) << 16) - size;
+      dfs[s] = 0;
+    } else if (c == -1 || c == 1) {
+      dnb[s] = (L << 16) - size;
+      dfs[s] = int32_t(total) - 1;
+      total++;
+    } else {
+      const uint32_t hb = 31 - __builtin_clz(uint32_t(c - 1));
+      const uint32_t max_bits = L - hb;
+      dnb[s] = (max_bits << 16) - (uint32_t(c) << max_bits);
+      dfs[s] = int32_t(total) - c;
+      total += uint32_t(c);
+    }
+  }
+}
+
+// a compressed block body: raw literals section, then the sequences with repeat offsets (RFC 8878
+// 3.1.2.5) and, per symbol type, the predefined, RLE or a block-built FSE table -- whichever the
+// cost estimate prefers (Python model over configs[1] blocks: 1.097 -> 1.009 x libzstd level 3)
 __device__ uint32_t zstd_body(const uint8_t* tags, uint32_t tn, const uint8_t* raw, uint32_t n, uint8_t* dst, uint32_t cap,
-                              Seq* seqs, uint32_t seq_cap, uint32_t lane, bool* over) {
+                              Seq* seqs, uint32_t seq_cap, ZFse* F, uint32_t lane, bool* over) {
   // pass 1: the sequences (literal run before each match) and the literal count
   uint32_t ns = 0, lit = 0, nlit = 0;
   bool too_many = false;
@@ -469,9 +963,17 @@ __device__ uint32_t zstd_body(const uint8_t* tags, uint32_t tn, const uint8_t* r
     return 0;
   }
   nlit += n - lit;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  auto sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  sync();
+  auto rd = [&](uint32_t i) {
+    const Seq q = seqs[i];
+    return Seq{uint32_t(__builtin_amdgcn_readfirstlane(q.ll)), uint32_t(__builtin_amdgcn_readfirstlane(q.ml)),
+               uint32_t(__builtin_amdgcn_readfirstlane(q.off))};
+  };
   BW w{dst, 0, cap, false};
   // Literals_Section_Header, Raw_Literals_Block (RFC 8878 3.1.1.3.1.1)
   if (nlit < 32) {
@@ -508,40 +1010,146 @@ __device__ uint32_t zstd_body(const uint8_t* tags, uint32_t tn, const uint8_t* r
     w.put(lane, (ns - 0x7F00) >> 8);
   }
   if (ns) {
-    w.put(lane, 0);  // Literals_Lengths_Mode, Offsets_Mode, Match_Lengths_Mode: predefined
-    Bits b;
-    FseState<36, 6> sll;
-    FseState<53, 6> sml;
-    FseState<29, 5> sof;
-    auto rd = [&](uint32_t i) {
+    // offsets as Offset_Values with the repeat offsets (the decoder's rules, zs_block): a repeat
+    // when the offset equals one, else offset + 3; seqs[i].off becomes the value
+    {
+      uint32_t r0 = 1, r1 = 4, r2 = 8;
+      for (uint32_t i = 0; i < ns; i++) {
+        const Seq q = rd(i);
+        const uint32_t o = q.off;
+        uint32_t ov;
+        if (q.ll != 0) ov = o == r0 ? 1u : (o == r1 ? 2u : (o == r2 ? 3u : o + 3));
+        else ov = o == r1 ? 1u : (o == r2 ? 2u : (o + 1 == r0 ? 3u : o + 3));
+        if (ov > 3) {
+          r2 = r1;
+          r1 = r0;
+          r0 = o;
+        } else {
+          const uint32_t idx = ov - 1 + (q.ll == 0 ? 1u : 0u);
+          if (idx >= 2) r2 = r1;
+          if (idx >= 1) {
+            r1 = r0;
+            r0 = o;
+          }
+        }
+        if (lane == 0) seqs[i].off = ov;
+      }
+    }
+    for (uint32_t s = lane; s < kNSym; s += 64) F->cnt[s] = 0;
+    sync();
+    for (uint32_t i = lane; i < ns; i += 64) {
       const Seq q = seqs[i];
-      return Seq{uint32_t(__builtin_amdgcn_readfirstlane(q.ll)), uint32_t(__builtin_amdgcn_readfirstlane(q.ml)),
-                 uint32_t(__builtin_amdgcn_readfirstlane(q.off))};
-    };
+      atomicAdd(&F->cnt[kSymLL + ll_code(q.ll)], 1u);
+      atomicAdd(&F->cnt[kSymOF + (31 - __builtin_clz(q.off))], 1u);
+      atomicAdd(&F->cnt[kSymML + ml_code(q.ml)], 1u);
+    }
+    sync();
+    // per type (LL, OF, ML, in the modes byte's order): predefined, RLE or an FSE_Compressed table
+    constexpr uint32_t kBase[3] = {kSymLL, kSymOF, kSymML}, kN[3] = {36, 32, 53}, kMaxLog[3] = {9, 8, 9},
+                       kDefLog[3] = {6, 5, 6};
+    uint32_t mode[3], L[3], nsym[3], rle[3];
+    if (lane == 0) {
+      for (int k = 0; k < 3; k++) {
+        const uint32_t* c = F->cnt + kBase[k];
+        const int16_t* def = k == 0 ? kLLDef : (k == 1 ? kOFDef : kMLDef);
+        const uint32_t defs = k == 0 ? 36u : (k == 1 ? 29u : 53u);
+        uint32_t used = 0, maxs = 0;
+        for (uint32_t s = 0; s < kN[k]; s++)
+          if (c[s]) {
+            used++;
+            maxs = s;
+          }
+        rle[k] = maxs;
+        nsym[k] = maxs + 1;
+        L[k] = kDefLog[k];
+        mode[k] = 0;
+        if (used == 1) {
+          mode[k] = 1;
+          continue;
+        }
+        // the predefined table's cost (x256 bits; a symbol it cannot code rules it out)
+        uint64_t cp = 0;
+        bool def_ok = maxs < defs;
+        for (uint32_t s = 0; s < nsym[k] && def_ok; s++)
+          if (c[s]) {
+            const int d = def[s];
+            if (d == 0) def_ok = false;
+            cp += uint64_t(c[s]) * (256 * kDefLog[k] - lg256(uint32_t(d < 0 ? 1 : d)));
+          }
+        // a table built for this block
+        const uint32_t Lb = fse_table_log(ns, maxs, kMaxLog[k]);
+        int16_t* nrm = F->norm;
+        if (fse_normalize(c, nsym[k], ns, Lb, nrm)) {
+          uint64_t cc = 256ull * fse_ncount(nullptr, nullptr, lane, nrm, nsym[k], Lb);
+          for (uint32_t s = 0; s < nsym[k]; s++)
+            if (c[s]) cc += uint64_t(c[s]) * (256 * Lb - lg256(uint32_t(nrm[s] < 0 ? 1 : nrm[s])));
+          if (!def_ok || cc < cp) {
+            mode[k] = 2;
+            L[k] = Lb;
+            fse_build_ct(nrm, nsym[k], Lb, F->state + kStOff[k], F->dnb + kBase[k], F->dfs + kBase[k], F->cumul, F->sym);
+          }
+        }
+        // (a distribution that does not normalize keeps the predefined table: every code used here
+        // is below 29, which the predefined offsets cover)
+      }
+    }
+    for (int k = 0; k < 3; k++) {
+      mode[k] = uint32_t(__builtin_amdgcn_readfirstlane(mode[k]));
+      L[k] = uint32_t(__builtin_amdgcn_readfirstlane(L[k]));
+      nsym[k] = uint32_t(__builtin_amdgcn_readfirstlane(nsym[k]));
+      rle[k] = uint32_t(__builtin_amdgcn_readfirstlane(rle[k]));
+    }
+    sync();
+    w.put(lane, (mode[0] << 6) | (mode[1] << 4) | (mode[2] << 2));
+    // the table descriptions: an FSE_Compressed table's counts (renormalized, as built), an RLE symbol
+    for (int k = 0; k < 3; k++) {
+      if (mode[k] == 1) {
+        w.put(lane, rle[k]);
+      } else if (mode[k] == 2) {
+        const uint32_t* c = F->cnt + kBase[k];
+        int16_t* nrm = F->norm;
+        if (lane == 0) (void)fse_normalize(c, nsym[k], ns, L[k], nrm);
+        sync();
+        Bits hb;
+        fse_ncount(&hb, &w, lane, nrm, nsym[k], L[k]);
+        hb.pad(w, lane);
+        sync();
+      }
+    }
+    FseRT t[3];
+    for (int k = 0; k < 3; k++) {
+      if (mode[k] == 2) t[k] = FseRT{F->state + kStOff[k], F->dnb + kBase[k], F->dfs + kBase[k], L[k]};
+      else if (k == 0) t[k] = fse_rt(kCtLL);
+      else if (k == 1) t[k] = fse_rt(kCtOF);
+      else t[k] = fse_rt(kCtML);
+    }
+    const bool act_ll = mode[0] != 1, act_of = mode[1] != 1, act_ml = mode[2] != 1;
+    Bits b;
+    FseStateR sll{0}, sml{0}, sof{0};
     // zstd's ZSTD_encodeSequences order: the last sequence first, states last (read first)
     {
       const Seq q = rd(ns - 1);
-      const uint32_t lc = ll_code(q.ll), mc = ml_code(q.ml), ob = q.off + 3, oc = 31 - __builtin_clz(ob);
-      sml.init(kCtML, mc);
-      sof.init(kCtOF, oc);
-      sll.init(kCtLL, lc);
+      const uint32_t lc = ll_code(q.ll), mc = ml_code(q.ml), ob = q.off, oc = 31 - __builtin_clz(ob);
+      if (act_ml) sml.init(t[2], mc);
+      if (act_of) sof.init(t[1], oc);
+      if (act_ll) sll.init(t[0], lc);
       b.add(w, lane, q.ll - kLLBase[lc], kLLBits[lc]);
       b.add(w, lane, q.ml - kMLBase[mc], kMLBits[mc]);
       b.add(w, lane, ob, oc);
     }
     for (uint32_t i = ns - 1; i-- > 0;) {
       const Seq q = rd(i);
-      const uint32_t lc = ll_code(q.ll), mc = ml_code(q.ml), ob = q.off + 3, oc = 31 - __builtin_clz(ob);
-      sof.enc(b, w, lane, kCtOF, oc);
-      sml.enc(b, w, lane, kCtML, mc);
-      sll.enc(b, w, lane, kCtLL, lc);
+      const uint32_t lc = ll_code(q.ll), mc = ml_code(q.ml), ob = q.off, oc = 31 - __builtin_clz(ob);
+      if (act_of) sof.enc(b, w, lane, t[1], oc);
+      if (act_ml) sml.enc(b, w, lane, t[2], mc);
+      if (act_ll) sll.enc(b, w, lane, t[0], lc);
       b.add(w, lane, q.ll - kLLBase[lc], kLLBits[lc]);
       b.add(w, lane, q.ml - kMLBase[mc], kMLBits[mc]);
       b.add(w, lane, ob, oc);
     }
-    sml.flush(b, w, lane);
-    sof.flush(b, w, lane);
-    sll.flush(b, w, lane);
+    if (act_ml) sml.flush(b, w, lane, t[2]);
+    if (act_of) sof.flush(b, w, lane, t[1]);
+    if (act_ll) sll.flush(b, w, lane, t[0]);
     b.add(w, lane, 1, 1);  // end mark
     b.pad(w, lane);
   }
@@ -699,6 +1307,14 @@ __global__ __launch_bounds__(kBig ? 64 : 256) void pc_snappy_kernel(const uint8_
   }
 }
 
+// per-wave LDS of pass 2 after the sequence lists: the entropy stage (Zstd, Zlib), and for Zlib's
+// small pieces the staged piece and the chain parse's hash head and links
+template <int kCodec, bool kBig>
+constexpr uint32_t kTcWaveBytes =
+    kCodec == SLATE_CODEC_ZSTD ? kZFseBytes
+    : kCodec == SLATE_CODEC_ZLIB ? (kDFseBytes + (kBig ? 0u : kSmallPiece + 16 + 4u * (1u << kHashBits)))
+                                 : 0u;
+
 // pass 2: the tags of each piece transcoded into the codec's body (global slot); body_len
 // gets the length, or kBodyRaw when the piece goes out in its raw / stored form
 template <int kCodec, bool kBig>
@@ -712,7 +1328,11 @@ __global__ __launch_bounds__(kBig ? 64 : 256) void pc_transcode_kernel(const uin
                                                                         Seq* __restrict__ big_seqs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves_wg = blockDim.x >> 6;
-  Seq* lds_seqs = reinterpret_cast<Seq*>(smem) + wave * kSmallSeqs;
+  Seq* lds_seqs = reinterpret_cast<Seq*>(smem) + (kBig ? 0 : wave * kSmallSeqs);
+  // the entropy stage's scratch per wave after the sequence lists (small pieces) or alone (big);
+  // CodecZlib small pieces also stage the piece and the chain parse's hash head / links there
+  uint8_t* wscr = smem + (kBig ? 0 : waves_wg * kSmallSeqs * sizeof(Seq)) + wave * kTcWaveBytes<kCodec, kBig>;
+  ZFse* fse = reinterpret_cast<ZFse*>(wscr);
   for (uint32_t k = blockIdx.x * waves_wg + wave; k < count; k += gridDim.x * waves_wg) {
     const uint32_t id = list[k];
     const CodecPiece pc = pieces[id];
@@ -727,10 +1347,29 @@ __global__ __launch_bounds__(kBig ? 64 : 256) void pc_transcode_kernel(const uin
       d = lz4_body(t, tn, p, pc.len, o, cap, lane, &over);
       if (d >= pc.len) over = true;  // an uncompressed block is smaller
     } else if (kCodec == SLATE_CODEC_ZLIB) {
-      d = deflate_body(t, tn, p, pc.len, (pc.flags & 2) != 0, o, cap, lane, &over);
+      DFse* F = reinterpret_cast<DFse*>(wscr);
+      DSrc src{t, tn, nullptr, 0};
+      const uint8_t* rp = p;
+      if (!kBig && pc.len <= kSmallPiece) {
+        // a block-sized piece: the hash-chain parse over the piece staged in LDS
+        uint8_t* lraw = wscr + kDFseBytes;
+        uint16_t* head = reinterpret_cast<uint16_t*>(lraw + kSmallPiece + 16);
+        uint16_t* prev = head + (1u << kHashBits);
+        for (uint32_t i = lane; i < pc.len; i += 64) lraw[i] = p[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t nm = chain_parse(lraw, pc.len, head, prev, lds_seqs, kSmallSeqs, lane);
+        if (nm != ~0u) {
+          src.list = lds_seqs;
+          src.nlist = nm;
+        }
+        rp = lraw;
+      }
+      d = deflate_body(src, rp, pc.len, (pc.flags & 2) != 0, o, cap, F, lane, &over);
     } else {
       Seq* seqs = kBig ? big_seqs + pc.seqs : lds_seqs;
-      d = zstd_body(t, tn, p, pc.len, o, cap, seqs, kBig ? pc.len / 3 + 2 : kSmallSeqs, lane, &over);
+      d = zstd_body(t, tn, p, pc.len, o, cap, seqs, kBig ? pc.len / 3 + 2 : kSmallSeqs, fse, lane, &over);
       if (d >= pc.len) over = true;  // a raw block is smaller
     }
     if (lane == 0) body_len[id] = over ? kBodyRaw : d;
@@ -846,20 +1485,38 @@ hipError_t launch_codec_encode(hipStream_t st, int codec, const uint8_t* raw, co
         raw, pieces, small_list, n_small, tags, tag_len);
   if (n_big) pc_snappy_kernel<true><<<min(n_big, uint32_t(num_cus)), 64, lds_big, st>>>(raw, pieces, big_list, n_big, tags, tag_len);
   Seq* bs = static_cast<Seq*>(big_seqs);
-  const size_t lds_seq = 4 * kSmallSeqs * sizeof(Seq);
+  // (+ the per-wave scratch of the entropy stage, kTcWaveBytes)
+  const size_t lds_seq = 4 * kSmallSeqs * sizeof(Seq) + 4 * (codec == SLATE_CODEC_ZSTD   ? kTcWaveBytes<SLATE_CODEC_ZSTD, false>
+                                                          : codec == SLATE_CODEC_ZLIB ? kTcWaveBytes<SLATE_CODEC_ZLIB, false>
+                                                                                      : 0u);
+  const size_t lds_big_tc = codec == SLATE_CODEC_ZSTD   ? kTcWaveBytes<SLATE_CODEC_ZSTD, true>
+                            : codec == SLATE_CODEC_ZLIB ? kTcWaveBytes<SLATE_CODEC_ZLIB, true>
+                                                        : 0u;
 #define SLATE_PC_TRANSCODE(C)                                                                                       \
   do {                                                                                                            \
     if (n_small)                                                                                                  \
       pc_transcode_kernel<C, false><<<min((n_small + 3) / 4, uint32_t(num_cus) * 8), 256, lds_seq, st>>>(          \
           raw, pieces, small_list, n_small, tags, tag_len, bodies, body_len, bs);                                   \
     if (n_big)                                                                                                    \
-      pc_transcode_kernel<C, true><<<min(n_big, uint32_t(num_cus) * 4), 64, 0, st>>>(raw, pieces, big_list, n_big, \
+      pc_transcode_kernel<C, true><<<min(n_big, uint32_t(num_cus) * 4), 64, lds_big_tc, st>>>(raw, pieces, big_list, n_big, \
                                                                                       tags, tag_len, bodies,       \
                                                                                       body_len, bs);              \
   } while (0)
   if (codec == SLATE_CODEC_LZ4) SLATE_PC_TRANSCODE(SLATE_CODEC_LZ4);
-  else if (codec == SLATE_CODEC_ZLIB) SLATE_PC_TRANSCODE(SLATE_CODEC_ZLIB);
-  else if (codec == SLATE_CODEC_ZSTD) SLATE_PC_TRANSCODE(SLATE_CODEC_ZSTD);
+  else if (codec == SLATE_CODEC_ZLIB) {
+    static const hipError_t a4 = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&pc_transcode_kernel<SLATE_CODEC_ZLIB, false>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_seq));
+    if (a4 != hipSuccess) return a4;
+    SLATE_PC_TRANSCODE(SLATE_CODEC_ZLIB);
+  }
+  else if (codec == SLATE_CODEC_ZSTD) {
+    static const hipError_t a3 = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&pc_transcode_kernel<SLATE_CODEC_ZSTD, false>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_seq));
+    if (a3 != hipSuccess) return a3;
+    SLATE_PC_TRANSCODE(SLATE_CODEC_ZSTD);
+  }
   else return hipErrorInvalidValue;
 #undef SLATE_PC_TRANSCODE
   return hipGetLastError();

@@ -88,6 +88,11 @@ inline void* mapped_ptr(void* p) {
   return d;
 }
 
+// The context's hand-back counter (DecodeArgs::handbacks), zeroed when first made; nullptr if it
+// cannot be allocated (decoding goes on uncounted).
+struct slate_ctx;
+uint64_t* ctx_handbacks(slate_ctx* ctx);
+
 // The device address of host range [p, p + len) when the whole range is page-locked in one mapping
 // (its last byte maps to d + len - 1); nullptr otherwise, e.g. when a caller registered only a prefix.
 inline void* mapped_range(void* p, uint64_t len) {
@@ -266,6 +271,7 @@ struct slate_ctx {
   // SST filter built beside the final flush (api_sst.cpp build_filter_aux): its own stream and buffers
   hipStream_t aux = nullptr;
   slate::SideStream side;  // the context stream's second stream (DecodeArgs::side)
+  DevBuf d_handbacks;      // DecodeArgs::handbacks of every decode through this context (u64)
   DevBuf x_words, x_enc, x_slots, x_asm, x_crc, x_bkt;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
   // device time of the builder's GPU passes (slate_ctx_set_timing): nanoseconds, summed over the
@@ -316,7 +322,8 @@ struct slate_ctx {
     if (seg_pool) seg_pool->close();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
                       &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &e_k, &s_slots, &s_raw, &s_aux, &c_meta,
-                      &c_tags, &c_bodies, &c_seqs, &c_out, &c_in, &x_words, &x_enc, &x_slots, &x_asm, &x_crc, &x_bkt})
+                      &c_tags, &c_bodies, &c_seqs, &c_out, &c_in, &x_words, &x_enc, &x_slots, &x_asm, &x_crc, &x_bkt,
+                      &d_handbacks})
       b->release();
     if (aux) (void)hipStreamDestroy(aux);
     aux = nullptr;

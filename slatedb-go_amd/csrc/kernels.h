@@ -67,6 +67,7 @@ struct DecodeArgs {
   uint32_t rt_zero = 0;   // always 0: a value the compiler cannot fold (see decode_lpb2.hip rd128)
   uint32_t* round_counter = nullptr;  // decode_lpb2: rounds handed out so far (launcher zeroes it)
   SideStream* side = nullptr;         // host only: the caller's side stream (nullptr: one stream)
+  uint64_t* handbacks = nullptr;      // device counter: blocks a fast path handed to the exact path
 };
 
 // Ablation bits.  The shipped library is built without SLATE_PROFILING_BUILD, so every
@@ -81,8 +82,12 @@ __host__ __device__ inline uint32_t dbg_bits(const DecodeArgs& a) {
 }
 
 // CodecZstd fast path (zstd_fast.hip): per block, what the lane-per-block parse found
-constexpr uint32_t kZsFastSeqs = 16;  // sequences per block on the fast path (more: exact path)
-constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4, kZfHuf = 8, kZfHuf4 = 16;  // kZfHuf: Huffman literals
+constexpr uint32_t kZsFastSeqs = 16;  // sequences per block on the predefined-table parse (8-byte records)
+// the FSE parse (FSE_Compressed tables, or more sequences): 4-byte records (kZfSeq4), up to 128
+constexpr uint32_t kZsFseSeqs = 128;
+constexpr uint32_t kZfSeqSlot = 128;  // dwords of z.seq per block (16 x 8 or 128 x 4 bytes)
+constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4, kZfHuf = 8, kZfHuf4 = 16,
+                   kZfSeq4 = 32;  // kZfHuf: Huffman literals; kZfSeq4: 4-byte sequence records
 struct ZsFastRec {
   uint32_t lit;       // frame offset of the raw literals, or the RLE literal byte
   uint32_t nlit;      // literal bytes
@@ -94,10 +99,12 @@ struct ZsFastRec {
 };
 struct ZsFastArgs {
   ZsFastRec* rec;   // n
-  uint2* seq;       // n * kZsFastSeqs: (ll | ml << 16, offset)
+  uint32_t* seq;    // n * kZfSeqSlot dwords: uint2 (ll | ml << 16, offset) records, or (kZfSeq4) u32
+                    // records ll | (ml - 3) << 10 | (offset - 1) << 20
   uint32_t* list;   // blocks for the exact path
-  uint32_t* count;  // (count[1]: hlist entries)
+  uint32_t* count;  // count[0]: list, count[1]: hlist, count[2]: flist entries
   uint32_t* hlist;  // kZfHuf blocks (phase B': Huffman literals)
+  uint32_t* flist;  // blocks for the FSE parse (phase A')
 };
 
 struct DecodeScratch {
@@ -237,6 +244,9 @@ hipError_t launch_zstd_par_bytes(hipStream_t st, const uint8_t* in, uint32_t nbl
                                  int num_cus);
 
 // Seeks (seek.hip): block.NewIteratorAtKey per query over decoded blocks; the SST index seek.
+hipError_t launch_block_seek_staged(hipStream_t st, const void* hsrc_dev, size_t bytes, void* base, size_t o_data,
+                                    size_t o_off, size_t o_meta, size_t o_q, size_t o_keys, size_t o_koff, uint64_t nq,
+                                    slate_seek* res, slate_seek_warn* warn, uint32_t warn_cap);
 hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                              const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
                              slate_seek* res, slate_seek_warn* warn = nullptr, uint32_t warn_cap = 0);

@@ -32,11 +32,50 @@ __device__ inline int peek(const uint8_t* p, uint32_t n, uint32_t fk_len, uint32
 
 }  // namespace
 
+__device__ __forceinline__ void seek_one(uint64_t q, const uint8_t* data, const uint64_t* out_off,
+                                         const slate_block_meta* meta, const uint32_t* qblock, const uint8_t* qkeys,
+                                         const uint64_t* qkey_off, slate_seek* res, slate_seek_warn* wout,
+                                         uint32_t wcap);
+
 __global__ void block_seek_kernel(const uint8_t* data, const uint64_t* out_off, const slate_block_meta* meta,
                                   const uint32_t* qblock, const uint8_t* qkeys, const uint64_t* qkey_off, uint64_t nq,
                                   slate_seek* res, slate_seek_warn* wout, uint32_t wcap) {
   const uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (q >= nq) return;
+  seek_one(q, data, out_off, meta, qblock, qkeys, qkey_off, res, wout, wcap);
+}
+
+// The point-read form (one workgroup, nq <= 256): the inputs, packed by the host into page-locked
+// staging in the device layout, are copied into device memory by the kernel itself -- one burst
+// over the link in place of a separate copy call -- then searched as above; the results go straight
+// back into the staging through its device address.
+__global__ __launch_bounds__(256) void block_seek_staged_kernel(const uint4* __restrict__ hsrc, uint64_t chunks,
+                                                                uint4* __restrict__ base, size_t o_data, size_t o_off,
+                                                                size_t o_meta, size_t o_q, size_t o_keys,
+                                                                size_t o_koff, uint64_t nq, slate_seek* res,
+                                                                slate_seek_warn* wout, uint32_t wcap) {
+  for (uint64_t c = threadIdx.x; c < chunks; c += 4 * blockDim.x) {  // four 16-byte chunks in flight
+    uint4 v[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) v[u] = hsrc[min(c + u * blockDim.x, chunks - 1)];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++)
+      if (c + u * blockDim.x < chunks) base[c + u * blockDim.x] = v[u];
+  }
+  __threadfence_block();
+  __syncthreads();
+  const uint64_t q = threadIdx.x;
+  if (q >= nq) return;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(base);
+  seek_one(q, b + o_data, reinterpret_cast<const uint64_t*>(b + o_off), reinterpret_cast<const slate_block_meta*>(b + o_meta),
+           reinterpret_cast<const uint32_t*>(b + o_q), b + o_keys, reinterpret_cast<const uint64_t*>(b + o_koff), res,
+           wout, wcap);
+}
+
+__device__ __forceinline__ void seek_one(uint64_t q, const uint8_t* data, const uint64_t* out_off,
+                                         const slate_block_meta* meta, const uint32_t* qblock, const uint8_t* qkeys,
+                                         const uint64_t* qkey_off, slate_seek* res, slate_seek_warn* wout,
+                                         uint32_t wcap) {
   uint32_t warn = 0;
   // types.ErrWarn.Add, in order: the first wcap warnings are recorded, all are counted
   auto add = [&](uint32_t kind, int err, uint32_t x, uint32_t y) {
@@ -171,6 +210,18 @@ hipError_t launch_block_seek(hipStream_t st, const uint8_t* data, const uint64_t
   if (nq == 0) return hipSuccess;
   block_seek_kernel<<<uint32_t((nq + 255) / 256), 256, 0, st>>>(data, out_off, meta, qblock, qkeys, qkey_off, nq, res,
                                                                  warn, warn_cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_block_seek_staged(hipStream_t st, const void* hsrc_dev, size_t bytes, void* base, size_t o_data,
+                                    size_t o_off, size_t o_meta, size_t o_q, size_t o_keys, size_t o_koff, uint64_t nq,
+                                    slate_seek* res, slate_seek_warn* warn, uint32_t warn_cap) {
+  if (nq == 0) return hipSuccess;
+  if (nq > 256 || (reinterpret_cast<uintptr_t>(hsrc_dev) & 15) || (reinterpret_cast<uintptr_t>(base) & 15))
+    return hipErrorInvalidValue;
+  block_seek_staged_kernel<<<1, 256, 0, st>>>(static_cast<const uint4*>(hsrc_dev), (bytes + 15) / 16,
+                                               static_cast<uint4*>(base), o_data, o_off, o_meta, o_q, o_keys, o_koff, nq,
+                                               res, warn, warn_cap);
   return hipGetLastError();
 }
 

@@ -50,6 +50,9 @@ constexpr uint32_t kZfParseThreads = 256;
 // phase B: one wave per block, eight 4-wave workgroups per CU (64 VGPRs), the decoded block in LDS
 // with the frame staged around its tail (the bytes after the literals and the 16-byte phase: +256)
 constexpr uint32_t kZfBuildThreads = 256;
+#ifndef SLATE_ZF_BUILD_WG
+#define SLATE_ZF_BUILD_WG 7  // workgroups per CU (the VGPR budget: 7 -> 72 per lane)
+#endif
 constexpr uint32_t kZfIn = kZsFastInCap, kZfOut = kZsFastOutCap;
 constexpr uint32_t kZfJunk = kZfOut + 256;      // 64 junk dwords (lanes' discarded writes)
 constexpr uint32_t kZfOutLds = kZfJunk + 256;
@@ -314,6 +317,7 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
     }
     const uint8_t* tb = tb0 + shift - 16 * c_lo;  // tb[i] = frame byte i for i in [s, wend)
     uint32_t nseq = 0, produced = 0;
+    bool defer = false;  // to phase A' (zs_fse_parse_kernel)
     if (ok) {
       const uint32_t sn = nb - pos;
       const uint32_t c0 = tb[s];
@@ -330,7 +334,15 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
         nseq = uint32_t(tb[s + 1]) + (uint32_t(tb[s + 2]) << 8) + 0x7F00;
         sp = 3;
       }
-      ok = ok && nseq <= kZsFastSeqs;
+      // FSE_Compressed tables, or more than kZsFastSeqs sequences (and no repeat tables, which a
+      // one-block frame cannot use): phase A' decodes them
+      {
+        const uint32_t m0 = (ok && nseq != 0 && sp < sn) ? uint32_t(tb[s + sp]) : 0u;
+        const uint32_t a_ll = m0 >> 6, a_of = (m0 >> 4) & 3, a_ml = (m0 >> 2) & 3;
+        defer = ok && nseq != 0 && sp < sn && !(m0 & 3) && a_ll != 3 && a_of != 3 && a_ml != 3 &&
+                (nseq > kZsFastSeqs || a_ll == 2 || a_of == 2 || a_ml == 2) && nseq <= kZsFseSeqs;
+      }
+      ok = ok && !defer && nseq <= kZsFastSeqs;
       uint32_t lp = 0, o = 0;
       const uint32_t lbase = cap - nlit;
       if (ok && nseq == 0) {
@@ -367,7 +379,7 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
           sml = zf_rd(bits, m_ml ? 0 : 6);
         }
         uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
-        uint2* seqs = z.seq + size_t(b) * kZsFastSeqs;
+        uint2* seqs = reinterpret_cast<uint2*>(z.seq + size_t(b) * kZfSeqSlot);
         for (uint32_t i = 0; ok && i < nseq; i++) {
           const ZsFse ell = m_ll ? ZsFse{uint8_t(r_ll), 0, 0} : sh->fse.ll[sll];
           const ZsFse eof = m_of ? ZsFse{uint8_t(r_of), 0, 0} : sh->fse.of[sof];
@@ -442,8 +454,362 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
                             : 0u;
     }
     if (b < a.n) z.rec[b] = rec;
-    list_append(b < a.n && !ok, b, z.list, z.count);
+    list_append(b < a.n && !ok && !defer, b, z.list, z.count);
     list_append(b < a.n && ok && huf, b, z.hlist, z.count + 1);
+    list_append(b < a.n && defer, b, z.flist, z.count + 2);
+  }
+}
+
+// ------------------------------------------------------------------------------- phase A'
+// Blocks whose sequence tables are FSE_Compressed -- libzstd's choice for a block of many short
+// sequences: a 4 KiB block of 100-byte KVs (configs[1]'s shape) has ~112 sequences and LL / OF / ML
+// tables of accuracy 6 / 5 / 7 -- or that have 17..128 sequences, from phase A's list: lane per
+// block as phase A, each lane building its block's three decoding tables (RFC 8878 4.1.1, zs_ncount
+// / zs_fse_build: FSE_Compressed, predefined or RLE) in its own LDS with 16-bit entries (accuracy
+// logs <= 7, 224 entries in all), then the sequences as phase A, written as 4-byte records, four per
+// store.  Anything else -- a larger table, a length or offset the record cannot hold, any failed
+// check -- goes to the exact path, which decodes and reports it.
+namespace {
+constexpr uint32_t kZfFseThreads = 64;
+constexpr uint32_t kZfFseTailChunks = 12;
+constexpr uint32_t kZfFseTail = 16 * kZfFseTailChunks + 16;
+constexpr uint32_t kZfFseTab = 224;  // u16 entries, the LL, OF and ML tables back to back
+constexpr uint32_t kZfFseScr = 112;  // int8 norm[53] + u8 next[53]
+constexpr uint32_t kZfFseLane = kZfHead + kZfFseTail + 2 * kZfFseTab + kZfFseScr;
+static_assert(kZfFseLane % 16 == 0, "lane records stay 16-byte aligned");
+
+// FSE_readNCount (oracle zs_ncount, zstd.h zs_ncount) into int8 counts: bytes used or -1 (also for
+// a count above 127, which this parse leaves to the exact path)
+__device__ int zf_ncount8(const uint8_t* base, int32_t off, uint32_t n, int8_t* norm, int maxs, int maxal) {
+  if (n == 0) return -1;
+  const int al = (base[off] & 15) + 5;
+  if (al > maxal) return -1;
+  uint64_t bp = 4;
+  int remaining = (1 << al) + 1, threshold = 1 << al, nb = al + 1, s = 0;
+  bool prev0 = false;
+  for (int i = 0; i <= maxs; i++) norm[i] = 0;
+  while (remaining > 1 && s <= maxs) {
+    if (prev0) {
+      int n0 = s;
+      for (;;) {
+        const uint32_t r = zs_fbits(base, off, n, bp, 2);
+        bp += 2;
+        n0 += int(r);
+        if (r != 3) break;
+      }
+      if (n0 > maxs) return -1;
+      s = n0;
+      prev0 = false;
+    }
+    const uint32_t v = zs_fbits(base, off, n, bp, uint32_t(nb));
+    const int max = (2 * threshold - 1) - remaining;
+    int count;
+    if (int(v & uint32_t(threshold - 1)) < max) {
+      count = int(v & uint32_t(threshold - 1));
+      bp += uint32_t(nb - 1);
+    } else {
+      count = int(v & uint32_t(2 * threshold - 1));
+      if (count >= threshold) count -= max;
+      bp += uint32_t(nb);
+    }
+    count--;
+    if (count > 127) return -1;
+    remaining -= count < 0 ? -count : count;
+    norm[s++] = int8_t(count);
+    prev0 = count == 0;
+    while (remaining < threshold && nb > 1) {
+      nb--;
+      threshold >>= 1;
+    }
+  }
+  if (remaining != 1 || (bp + 7) / 8 > n) return -1;
+  return int((bp + 7) / 8) | (al << 16) | ((s - 1) << 24);  // used (< 2^16), the log, the last symbol
+}
+
+// FSE decoding table (oracle zs_fse_build) with 16-bit entries sym | nb << 6 | base << 9 (al <= 7)
+__device__ bool zf_fse_build16(uint16_t* t, const int8_t* norm, int last, int al, uint8_t* next) {
+  const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+  uint32_t hi = size - 1;
+  for (int s = 0; s <= last; s++) {
+    const int c = norm[s];
+    if (c == -1) {
+      t[hi--] = uint16_t(s);
+      next[s] = 1;
+    } else {
+      next[s] = uint8_t(c > 0 ? c : 0);
+    }
+  }
+  uint32_t pos = 0;
+  for (int s = 0; s <= last; s++)
+    for (int i = 0; i < norm[s]; i++) {
+      t[pos] = uint16_t(s);
+      do pos = (pos + step) & mask;
+      while (pos > hi);
+    }
+  if (pos != 0) return false;
+  for (uint32_t u = 0; u < size; u++) {
+    const uint32_t sym = t[u] & 63u;
+    const uint32_t x = next[sym]++;
+    const uint32_t nbits = uint32_t(al) - (31 - __builtin_clz(x));
+    t[u] = uint16_t(sym | (nbits << 6) | (((x << nbits) - size) << 9));
+  }
+  return true;
+}
+
+// One table (zs_table): mode 0 = the predefined distribution, 1 = RLE, 2 = FSE_Compressed at
+// base[off, off + n).  Builds it at t (at most `room` entries); returns bytes used | accuracy log
+// << 16, or -1.
+__device__ int zf_table16(uint32_t mode, const uint8_t* base, int32_t off, uint32_t n, const int16_t* def, int defs,
+                          int defal, int maxs, uint16_t* t, uint32_t room, int8_t* norm, uint8_t* next) {
+  if (mode == 1) {
+    if (n < 1 || int(base[off]) > maxs) return -1;
+    t[0] = uint16_t(base[off]);  // nb 0, base 0
+    return 1;
+  }
+  int a = defal, last = defs - 1, used = 0;
+  if (mode == 0) {
+    for (int i = 0; i < defs; i++) norm[i] = int8_t(def[i]);
+  } else {
+    const int r = zf_ncount8(base, off, n, norm, maxs, 7);
+    if (r < 0) return -1;
+    used = r & 0xFFFF;
+    a = (r >> 16) & 0xFF;
+    last = r >> 24;
+  }
+  if ((1u << a) > room || !zf_fse_build16(t, norm, last, a, next)) return -1;
+  return used | (a << 16);
+}
+}  // namespace
+
+// (LDS allows three waves per CU: the registers need not be rationed)
+__global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void zs_fse_parse_kernel(
+    DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint32_t ll_base[36], ml_base[53];
+  __shared__ uint8_t ll_bits[36], ml_bits[53];
+  for (uint32_t i = threadIdx.x; i < 36; i += blockDim.x) {
+    ll_base[i] = kZsLLBase[i];
+    ll_bits[i] = kZsLLBits[i];
+  }
+  for (uint32_t i = threadIdx.x; i < 53; i += blockDim.x) {
+    ml_base[i] = kZsMLBase[i];
+    ml_bits[i] = kZsMLBits[i];
+  }
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  uint8_t* hb0 = smem + threadIdx.x * kZfFseLane;
+  uint8_t* tb0 = hb0 + kZfHead;
+  uint16_t* tab = reinterpret_cast<uint16_t*>(tb0 + kZfFseTail);
+  int8_t* norm = reinterpret_cast<int8_t*>(tab + kZfFseTab);
+  uint8_t* next = reinterpret_cast<uint8_t*>(norm + 56);
+  const uint32_t items = z.count[2];
+  const uint32_t waves = gridDim.x * (kZfFseThreads / 64);
+  for (uint32_t r0 = (blockIdx.x * (kZfFseThreads / 64) + (threadIdx.x >> 6)) * 64; r0 < items; r0 += waves * 64) {
+    const bool have = r0 + lane < items;
+    const uint32_t b = have ? z.flist[r0 + lane] : 0u;
+    bool ok = false;
+    uint32_t shift = 0, clen = 0, cap = 0;
+    const uint8_t* gin = nullptr;
+    if (have) {
+      const uint64_t s0 = a.in_off[b], len = a.in_off[b + 1] - s0;
+      gin = a.in + s0;
+      shift = uint32_t(reinterpret_cast<uintptr_t>(gin) & 15);
+      const uint64_t cap64 = a.out_off[b + 1] - a.out_off[b];
+      if (len >= 6 && shift + len <= kZfIn && cap64 <= kZfOut) {  // (phase A checked these)
+        clen = uint32_t(len - 4);
+        cap = uint32_t(cap64);
+        ok = true;
+      }
+    }
+    // the block's aligned chunks 0 .. lastc (no read beyond the block: the input may end there)
+    const v4u* gal = reinterpret_cast<const v4u*>(gin - shift);
+    const uint32_t lastc = ok ? (shift + clen + 3) >> 4 : 0u;
+    const v4u zero4 = {0, 0, 0, 0};
+    if (ok) {
+      lds_put16(hb0, gal[0]);
+      lds_put16(hb0 + 16, lastc >= 1 ? gal[1] : zero4);
+      lds_put16(hb0 + 32, lastc >= 2 ? gal[2] : zero4);
+    }
+    const uint8_t* hb = hb0 + shift;
+    ZfHead h{};
+    ok = ok && zf_head(hb, clen, h) && h.bt == 2;
+    // the literals section header: raw or RLE (phase A sent Huffman-literal blocks here only when
+    // their sequences need this parse; they take the exact path)
+    uint32_t nlit = 0, pos = 0, lit = 0, rle = 0;
+    const uint32_t nb = h.bs, body = h.body;
+    if (ok) {
+      const uint32_t b0 = hb[body], type = b0 & 3, sf = (b0 >> 2) & 3;
+      uint32_t hs = 1;
+      if (sf == 1) {
+        hs = 2;
+        nlit = (b0 >> 4) + (uint32_t(hb[body + 1]) << 4);
+      } else if (sf == 3) {
+        hs = 3;
+        nlit = (b0 >> 4) + (uint32_t(hb[body + 1]) << 4) + (uint32_t(hb[body + 2]) << 12);
+      } else {
+        nlit = b0 >> 3;
+      }
+      ok = type <= 1 && nb >= hs && nlit <= h.bmax && (type == 0 ? nb - hs >= nlit : nb - hs >= 1) && nlit <= cap;
+      rle = type == 1;
+      lit = rle ? uint32_t(hb[body + hs]) : body + hs;
+      pos = hs + (type == 0 ? nlit : 1);
+      ok = ok && pos < nb;
+    }
+    // the sequences section: kZfFseTailChunks chunks from the one holding its first byte
+    const uint32_t s = body + pos;
+    const uint32_t c_lo = (shift + s) >> 4;
+    const uint32_t wend = 16 * (c_lo + kZfFseTailChunks) - shift;
+    ok = ok && body + nb + (h.checksum ? 4u : 0u) <= wend;
+    if (ok) {
+#pragma unroll
+      for (uint32_t k = 0; k < kZfFseTailChunks; k++) lds_put16(tb0 + 16 * k, c_lo + k <= lastc ? gal[c_lo + k] : zero4);
+    }
+    const uint8_t* tb = tb0 + shift - 16 * c_lo;  // tb[i] = frame byte i for i in [s, wend)
+    const int32_t tofs = int32_t(shift) - int32_t(16 * c_lo);  // frame byte i = tb0[i + tofs]
+    uint32_t nseq = 0, produced = 0;
+    v4u qv = {0, 0, 0, 0};  // the current group of four records
+    uint32_t* seqs = z.seq + size_t(b) * kZfSeqSlot;
+    if (ok) {
+      const uint32_t sn = nb - pos;
+      const uint32_t c0 = tb[s];
+      uint32_t sp;
+      if (c0 < 128) {
+        nseq = c0;
+        sp = 1;
+      } else if (c0 < 255) {
+        ok = sn >= 2;
+        nseq = ((c0 - 128) << 8) + tb[s + 1];
+        sp = 2;
+      } else {
+        ok = sn >= 3;
+        nseq = uint32_t(tb[s + 1]) + (uint32_t(tb[s + 2]) << 8) + 0x7F00;
+        sp = 3;
+      }
+      ok = ok && nseq != 0 && nseq <= kZsFseSeqs && sp < sn;
+      const uint32_t modes = ok ? uint32_t(tb[s + sp++]) : 0u;
+      ok = ok && !(modes & 3);
+      const uint32_t m_ll = modes >> 6, m_of = (modes >> 4) & 3, m_ml = (modes >> 2) & 3;
+      ok = ok && m_ll <= 2 && m_of <= 2 && m_ml <= 2;
+      // the three tables, LL / OF / ML as they follow each other, back to back in the lane's LDS
+      uint32_t al_ll = 0, al_of = 0, al_ml = 0, t_of = 0, t_ml = 0;
+      if (ok) {
+        const int u = zf_table16(m_ll, tb0, int32_t(s + sp) + tofs, sn - sp, kZsLLDef, 36, 6, 35, tab, kZfFseTab, norm,
+                                 next);
+        ok = u >= 0;
+        sp += ok ? uint32_t(u & 0xFFFF) : 0u;
+        al_ll = ok ? uint32_t(u >> 16) : 0u;
+      }
+      if (ok) {
+        t_of = 1u << al_ll;
+        const int u = zf_table16(m_of, tb0, int32_t(s + sp) + tofs, sn - sp, kZsOFDef, 29, 5, 31, tab + t_of,
+                                 kZfFseTab - t_of, norm, next);
+        ok = u >= 0;
+        sp += ok ? uint32_t(u & 0xFFFF) : 0u;
+        al_of = ok ? uint32_t(u >> 16) : 0u;
+      }
+      if (ok) {
+        t_ml = t_of + (1u << al_of);
+        const int u = zf_table16(m_ml, tb0, int32_t(s + sp) + tofs, sn - sp, kZsMLDef, 53, 6, 52, tab + t_ml,
+                                 kZfFseTab - t_ml, norm, next);
+        ok = u >= 0;
+        sp += ok ? uint32_t(u & 0xFFFF) : 0u;
+        al_ml = ok ? uint32_t(u >> 16) : 0u;
+      }
+      // zs_bstart
+      const uint32_t bn = ok ? sn - sp : 0u;
+      const uint32_t last = bn ? uint32_t(tb[s + sn - 1]) : 0u;
+      ok = ok && last != 0;
+      ZfBits bits{tb0, 8 * int64_t(int32_t(s + sp) + tofs), ok ? 8 * int64_t(bn - 1) + (31 - __builtin_clz(last)) : 0};
+      uint32_t sll = 0, sof = 0, sml = 0;
+      if (ok) {
+        sll = zf_rd(bits, al_ll);
+        sof = zf_rd(bits, al_of);
+        sml = zf_rd(bits, al_ml);
+      }
+      uint32_t rep0 = 1, rep1 = 4, rep2 = 8, lp = 0, o = 0;
+      const uint32_t lbase = cap - nlit;
+      for (uint32_t i = 0; ok && i < nseq; i++) {
+        const uint32_t ell = tab[sll], eof = tab[t_of + sof], eml = tab[t_ml + sml];
+        const uint32_t llc = ell & 63u, ofc = eof & 63u, mlc = eml & 63u;
+        if (ofc > 31) {
+          ok = false;
+          break;
+        }
+        uint64_t ofv = (1ull << ofc);
+        if (ofc > 24) {
+          const uint32_t hi = zf_rd(bits, ofc - 24);
+          ofv += (uint64_t(hi) << 24) + zf_rd(bits, 24);
+        } else {
+          ofv += zf_rd(bits, ofc);
+        }
+        const uint32_t ml = ml_base[mlc] + zf_rd(bits, ml_bits[mlc]);
+        const uint32_t ll = ll_base[llc] + zf_rd(bits, ll_bits[llc]);
+        uint64_t offv;
+        if (ofv > 3) {
+          offv = ofv - 3;
+          rep2 = rep1;
+          rep1 = rep0;
+          rep0 = uint32_t(offv);
+        } else {
+          const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1u : 0u);
+          offv = idx == 3 ? uint64_t(rep0) - 1 : (idx == 0 ? rep0 : idx == 1 ? rep1 : rep2);
+          if (offv == 0) offv = 1;
+          if (idx >= 2) rep2 = rep1;
+          if (idx >= 1) {
+            rep1 = rep0;
+            rep0 = uint32_t(offv);
+          }
+        }
+        if (i + 1 < nseq) {
+          sll = (ell >> 9) + zf_rd(bits, (ell >> 6) & 7u);
+          sml = (eml >> 9) + zf_rd(bits, (eml >> 6) & 7u);
+          sof = (eof >> 9) + zf_rd(bits, (eof >> 6) & 7u);
+        }
+        if (bits.bp < 0 || ll > nlit - lp || uint64_t(o) + ll + ml > h.bmax || uint64_t(o) + ll + ml > cap ||
+            uint64_t(o) + ll + ml > uint64_t(lbase) + lp + ll) {
+          ok = false;
+          break;
+        }
+        lp += ll;
+        o += ll;
+        // fstart = 0: one frame; the record holds ll < 1024, ml - 3 < 1024, offset - 1 < 4096
+        if (offv > o || ll > 1023 || ml - 3 > 1023 || offv > 4096) {
+          ok = false;
+          break;
+        }
+        const uint32_t r = ll | ((ml - 3) << 10) | (uint32_t(offv - 1) << 20);
+        qv.x = (i & 3) == 0 ? r : qv.x;
+        qv.y = (i & 3) == 1 ? r : qv.y;
+        qv.z = (i & 3) == 2 ? r : qv.z;
+        qv.w = (i & 3) == 3 ? r : qv.w;
+        if ((i & 3) == 3) reinterpret_cast<v4u*>(seqs)[i >> 2] = qv;
+        o += ml;
+      }
+      ok = ok && bits.bp == 0;
+      const uint32_t rest = nlit - lp;
+      ok = ok && uint64_t(o) + rest <= h.bmax && uint64_t(o) + rest <= cap;
+      produced = o + rest;
+      ok = ok && (!h.has_fcs || uint64_t(produced) == h.fcs);
+    }
+    if (ok && (nseq & 3)) reinterpret_cast<v4u*>(seqs)[nseq >> 2] = qv;
+    // the record (ZsFastRec: lit, nlit, produced, info | want, cs, pad), as two 16-byte stores
+    v4u w0 = {0, 0, 0, 0}, w1 = {0, 0, 0, 0};
+    if (ok) {
+      const uint32_t qq = body + nb;
+      w0.x = lit;
+      w0.y = nlit;
+      w0.z = produced;
+      w0.w = nseq | ((kZfFast | kZfSeq4 | (rle ? kZfRle : 0u) | (h.checksum ? kZfSum : 0u)) << 16);
+      w1.x = h.checksum ? uint32_t(tb[qq]) | (uint32_t(tb[qq + 1]) << 8) | (uint32_t(tb[qq + 2]) << 16) |
+                              (uint32_t(tb[qq + 3]) << 24)
+                        : 0u;
+    }
+    static_assert(sizeof(ZsFastRec) == 32, "record layout");
+    if (have) {
+      reinterpret_cast<v4u*>(z.rec + b)[0] = w0;
+      reinterpret_cast<v4u*>(z.rec + b)[1] = w1;
+    }
+    list_append(have && !ok, b, z.list, z.count);
   }
 }
 
@@ -454,7 +820,7 @@ namespace {
 struct ZfRaw {
   ZsFastRec rec;
   uint64_t i0, i1, o0, o1;
-  uint2 seq;  // lane i: sequence i (lanes < kZsFastSeqs)
+  uint2 seq;  // lane i: dwords 2i, 2i + 1 of the block's sequence slot
   uint32_t b;
 };
 __device__ __forceinline__ ZfRaw zf_load(const DecodeArgs& a, const ZsFastArgs& z, uint32_t b, uint32_t lane) {
@@ -466,15 +832,18 @@ __device__ __forceinline__ ZfRaw zf_load(const DecodeArgs& a, const ZsFastArgs& 
     r.i1 = a.in_off[b + 1];
     r.o0 = a.out_off[b];
     r.o1 = a.out_off[b + 1];
-    r.seq = lane < kZsFastSeqs ? z.seq[size_t(b) * kZsFastSeqs + lane] : make_uint2(0, 0);
+    r.seq = reinterpret_cast<const uint2*>(z.seq + size_t(b) * kZfSeqSlot)[lane];
   }
   return r;
 }
+// A block's sequences, two slots per lane: 8-byte records put sequence i on lane i (slot A),
+// 4-byte records (kZfSeq4) sequences 2i and 2i + 1 on lane i (slots A and B); a slot past the
+// block's sequences holds zeros.
 struct ZfBlock {
-  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs;
+  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs, s4;
   const uint8_t* gin;
   uint8_t* gout;
-  uint2 seq;  // lane i < nseq: sequence i, else 0
+  uint32_t llA, mlA, offA, llB, mlB, offB;
 };
 __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r, uint32_t lane) {
   ZfBlock k{};
@@ -494,7 +863,23 @@ __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r
   k.rle = fl & kZfRle;
   k.huf = (fl & kZfHuf) ? ((fl & kZfHuf4) ? 4u : 1u) : 0u;
   k.cs = __builtin_amdgcn_readfirstlane(r.rec.cs);
-  k.seq = (k.fast && lane < k.nseq) ? r.seq : make_uint2(0, 0);
+  k.s4 = (fl & kZfSeq4) ? 1u : 0u;
+  if (!k.fast) return k;
+  if (k.s4) {
+    const bool va = 2 * lane < k.nseq, vb = 2 * lane + 1 < k.nseq;
+    const uint32_t x = va ? r.seq.x : 0u, y = vb ? r.seq.y : 0u;
+    k.llA = x & 1023u;
+    k.mlA = va ? ((x >> 10) & 1023u) + 3 : 0u;
+    k.offA = va ? (x >> 20) + 1 : 0u;
+    k.llB = y & 1023u;
+    k.mlB = vb ? ((y >> 10) & 1023u) + 3 : 0u;
+    k.offB = vb ? (y >> 20) + 1 : 0u;
+  } else {
+    const bool va = lane < k.nseq;
+    k.llA = va ? r.seq.x & 0xFFFFu : 0u;
+    k.mlA = va ? r.seq.x >> 16 : 0u;
+    k.offA = va ? r.seq.y : 0u;
+  }
   return k;
 }
 }  // namespace
@@ -503,14 +888,14 @@ __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r
 // (or the RLE byte), write it back, then block.Decode's checks and rows (phases B and B').
 __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur, uint8_t* wout, uint32_t lb,
                                          uint32_t lane, uint32_t dbg) {
-  const uint2 seq = cur.seq;
   const uint32_t lit = cur.lit;
   slate_block_meta m{};
-  // sequence lane i: (ll, ml, offset); exclusive scans give each one's literal source and
-  // output position
+  // exclusive scans over the lanes (two sequences per lane) give each sequence's literal source
+  // and output position
   const uint32_t nseq = cur.nseq, nlit = cur.nlit;
-  const uint32_t ll = seq.x & 0xFFFFu, ml = seq.x >> 16, off = seq.y;
-  uint32_t x_ll = ll, x_out = ll + ml;
+  const uint32_t llA = cur.llA, mlA = cur.mlA, llB = cur.llB, mlB = cur.mlB;
+  const uint32_t t_ll = llA + llB, t_out = llA + mlA + llB + mlB;
+  uint32_t x_ll = t_ll, x_out = t_out;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y1 = __shfl_up(x_ll, d, 64), y2 = __shfl_up(x_out, d, 64);
@@ -519,50 +904,83 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
       x_out += y2;
     }
   }
-  const uint32_t lsrc = x_ll - ll, dpos = x_out - ll - ml;  // exclusive
+  const uint32_t lsrcA = x_ll - t_ll, dposA = x_out - t_out;  // exclusive
+  const uint32_t lsrcB = lsrcA + llA, dposB = dposA + llA + mlA;
   const uint32_t tot_ll = __shfl(x_ll, 63, 64), tot_out = __shfl(x_out, 63, 64);
   const uint32_t rle4 = (lit & 0xFF) * 0x01010101u;
-  // Literal runs of every sequence and the trailing run, in order, four dwords per lane.  A run
-  // moves down (destination <= source: the cursor rule), so a lane reads its source bytes
-  // before any lane writes over them.  Only the dwords that hold run bytes are written (the
-  // others go to the lane's junk dword); the (up to three) bytes the first or last of them
-  // spills over lie in the neighbouring match (>= 3 bytes), written afterwards, or past the
-  // block, and never reach the literals still to be moved (the cursor rule again, ml >= 3).
   uint8_t* junk = wout + kZfJunk + 4 * lane;
-  for (uint32_t i = 0; i <= nseq && !(dbg & (1u << 22)); i++) {
-    const uint32_t L = i < nseq ? __builtin_amdgcn_readlane(ll, i) : nlit - tot_ll;
-    if (L == 0) continue;
-    const uint32_t src = i < nseq ? __builtin_amdgcn_readlane(lsrc, i) : tot_ll;
-    const uint32_t dst = i < nseq ? __builtin_amdgcn_readlane(dpos, i) : tot_out;
-    const int32_t delta = int32_t(lb + src) - int32_t(dst);  // output byte p = wout[p + delta]
-    const uint32_t end = dst + L;
-    for (uint32_t w = (dst & ~3u) + 16 * lane; w < end; w += 16 * kWave) {
-      uint32_t o[4];
-      if (cur.rle) {
-        o[0] = o[1] = o[2] = o[3] = rle4;
-      } else {
-        const int32_t sa = int32_t(w) + delta;
-        const uint32_t* sp = reinterpret_cast<const uint32_t*>(wout + (sa & ~3));
-        const uint32_t sh = uint32_t(sa) & 3;
-        const uint32_t d0 = sp[0], d1 = sp[1], d2 = sp[2], d3 = sp[3], d4 = sp[4];
-        o[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
-        o[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
-        o[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
-        o[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (uint32_t k = 0; k < 4; k++)
-        *reinterpret_cast<uint32_t*>(w + 4 * k < end ? wout + w + 4 * k : junk) = o[k];
+  // One 16-byte piece of a literal run: output dwords w .. w + 12 of the run [dst, end), moved down
+  // by delta (output byte p = wout[p + delta]).  Only the dwords that hold run bytes are written
+  // (the others go to the lane's junk dword); the (up to three) bytes the first or last of them
+  // spills over lie in the neighbouring match (>= 3 bytes), written afterwards, or past the block,
+  // and never reach literals still to be moved (the cursor rule: o + ml <= cap - nlit + lp, ml >= 3).
+  // A run moves down, and a later run's source lies above every earlier run's destination, so
+  // pieces read in one instruction and written in the next may come from any runs.
+  auto piece = [&](bool go, uint32_t w, uint32_t end, int32_t delta) {
+    uint32_t o[4];
+    if (cur.rle) {
+      o[0] = o[1] = o[2] = o[3] = rle4;
+    } else {
+      const int32_t sa = int32_t(w) + delta;
+      const uint32_t* sp = reinterpret_cast<const uint32_t*>(wout + (go ? (sa & ~3) : 0));
+      const uint32_t sh = uint32_t(sa) & 3;
+      const uint32_t d0 = sp[0], d1 = sp[1], d2 = sp[2], d3 = sp[3], d4 = sp[4];
+      o[0] = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      o[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      o[2] = __builtin_amdgcn_alignbyte(d3, d2, sh);
+      o[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
     }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++)
+      *reinterpret_cast<uint32_t*>((go && w + 4 * k < end) ? wout + w + 4 * k : junk) = o[k];
+  };
+  if (!(dbg & (1u << 22))) {
+    // the sequences' runs: piece j of all of them (lane-major, A before B) on lane j mod 64; a
+    // piece finds its lane by a binary search over the lanes' exclusive piece counts
+    const uint32_t pcA = llA ? (dposA + llA - (dposA & ~3u) + 15) / 16 : 0u;
+    const uint32_t pcB = llB ? (dposB + llB - (dposB & ~3u) + 15) / 16 : 0u;
+    const uint32_t t_pc = pcA + pcB;
+    uint32_t x_pc = t_pc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x_pc, d, 64);
+      if (int(lane) >= d) x_pc += y;
+    }
+    const uint32_t e_pc = x_pc - t_pc, n_pc = __shfl(x_pc, 63, 64);
+    for (uint32_t j0 = 0; j0 < n_pc; j0 += kWave) {
+      const uint32_t j = j0 + lane;
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t st = 32; st >= 1; st >>= 1) k = uint32_t(__shfl(e_pc, int(k + st), 64)) <= j ? k + st : k;
+      // (every lane takes part in every shuffle: a ds_bpermute reads nothing from a lane the exec
+      // mask leaves out, so no shuffle sits in a divergent select)
+      const uint32_t q = j - uint32_t(__shfl(e_pc, int(k), 64));
+      const uint32_t qa = __shfl(pcA, int(k), 64);
+      const uint32_t dA = __shfl(dposA, int(k), 64), dB = __shfl(dposB, int(k), 64);
+      const uint32_t sA = __shfl(lsrcA, int(k), 64), sB = __shfl(lsrcB, int(k), 64);
+      const uint32_t lA = __shfl(llA, int(k), 64), lB = __shfl(llB, int(k), 64);
+      const bool inA = q < qa;
+      const uint32_t dst = inA ? dA : dB, src = inA ? sA : sB, L = inA ? lA : lB;
+      const uint32_t p = inA ? q : q - qa;
+      piece(j < n_pc, (dst & ~3u) + 16 * p, dst + L, int32_t(lb + src) - int32_t(dst));
+      zs_sync();
+    }
+    // the trailing run (after the last match)
+    const uint32_t L = nlit - tot_ll, dst = tot_out, end = dst + L;
+    const int32_t delta = int32_t(lb + tot_ll) - int32_t(dst);
+    for (uint32_t w = (dst & ~3u) + 16 * lane; __ballot(L != 0 && w < end); w += 16 * kWave) piece(w < end, w, end, delta);
   }
   zs_sync();
   // Matches in order: each reads only bytes before its own position.  Non-overlapping ones
   // (offset >= length) a dword per lane, the edge dwords merged with the bytes around the
   // match; overlapping ones a byte per lane.
+  const uint32_t offA = cur.offA, offB = cur.offB, s4 = cur.s4;
   for (uint32_t i = 0; i < nseq && !(dbg & (1u << 21)); i++) {
-    const uint32_t M = __builtin_amdgcn_readlane(ml, i), O = __builtin_amdgcn_readlane(off, i);
-    const uint32_t mp = __builtin_amdgcn_readlane(dpos, i) + __builtin_amdgcn_readlane(ll, i);
+    const uint32_t li = i >> s4;
+    const bool hB = s4 && (i & 1);  // (wave-uniform)
+    const uint32_t M = __builtin_amdgcn_readlane(hB ? mlB : mlA, li), O = __builtin_amdgcn_readlane(hB ? offB : offA, li);
+    const uint32_t mp = __builtin_amdgcn_readlane(hB ? dposB + llB : dposA + llA, li);
     if (O >= M) {
       const uint32_t me = mp + M;
       const uint32_t lo_keep = (1u << (8 * (mp & 3))) - 1u, hi_keep = (me & 3) ? ~((1u << (8 * (me & 3))) - 1u) : 0u;
@@ -592,7 +1010,7 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
 // so that its raw literals start at lb >= cap - nlit: phase A checked zs_block's rule that the
 // write cursor never passes the unread literals (o + ml <= cap - nlit + lp before each literal
 // run), so the runs can be moved down in place, in order.
-__global__ __launch_bounds__(kZfBuildThreads, 8) void zs_fast_build_kernel(DecodeArgs a, ZsFastArgs z) {
+__global__ __launch_bounds__(kZfBuildThreads, SLATE_ZF_BUILD_WG) void zs_fast_build_kernel(DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = threadIdx.x >> 6;
@@ -938,6 +1356,8 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const size_t lds_a = zstd_fast_parse_lds();
   const uint32_t grid_a = min((a.n + kZfParseThreads - 1) / kZfParseThreads, uint32_t(num_cus) * 2u);
   zs_fast_parse_kernel<<<grid_a, kZfParseThreads, lds_a, st>>>(a, z);
+  // phase A': the blocks phase A listed for the FSE parse (three one-wave workgroups per CU)
+  zs_fse_parse_kernel<<<uint32_t(num_cus) * 3u, kZfFseThreads, size_t(kZfFseThreads) * kZfFseLane, st>>>(a, z);
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
@@ -945,7 +1365,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
   if (attr != hipSuccess) return attr;
-  const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * 8u);
+  const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG);
   const size_t lds_h = size_t(kZfHufThreads / 64) * kZfHufWave;
   static const hipError_t attr_h = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_huf_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_h));

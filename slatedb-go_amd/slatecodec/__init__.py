@@ -26,6 +26,7 @@ E_INVALID_ARG = 102
 E_MERGE_UNSORTED = 105
 E_LIMIT = 106
 E_WARNINGS = 107
+E_READER_NEED_DATA, E_READER_END = 108, 109
 
 u8p = C.POINTER(C.c_uint8)
 u16p = C.POINTER(C.c_uint16)
@@ -52,6 +53,10 @@ class SstInfo(C.Structure):
                 ("filter_len", C.c_uint64), ("codec", C.c_int32), ("first_key_len", C.c_uint32)]
 
 
+class BlockView(C.Structure):
+    _fields_ = [("block", C.c_uint64), ("meta", C.c_uint8 * 16), ("data", C.c_void_p), ("rows", C.c_void_p)]
+
+
 class SlateError(RuntimeError):
     def __init__(self, status: int, where: str = ""):
         self.status = status
@@ -75,6 +80,7 @@ _SIGS = {
     "slate_ctx_set_copy_threads": (C.c_int, [vp, C.c_uint32]),
     "slate_ctx_set_timing": (C.c_int, [vp, C.c_int]),
     "slate_ctx_gpu_time": (C.c_int, [vp, C.POINTER(C.c_double), C.c_int]),
+    "slate_ctx_handbacks": (C.c_int, [vp, C.POINTER(C.c_uint64), C.c_int]),
     "slate_ctx_gpu_busy": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int]),
     "slate_ctx_synchronize": (C.c_int, [vp]),
     "slate_decode_scratch_bytes": (C.c_size_t, [C.c_uint32]),
@@ -137,6 +143,11 @@ _SIGS = {
     "slate_read_blocks_range": (C.c_int, [C.POINTER(SstInfo), vp, C.c_uint64, C.c_uint64, u64p, u64p]),
     "slate_read_blocks": (C.c_int, [vp, C.POINTER(SstInfo), vp, C.c_uint64, C.c_uint64, vp, C.c_size_t, vp,
                                     C.c_uint64, vp, vp, vp, C.c_uint64, vp, u64p]),
+    "slate_block_reader_create": (C.c_int, [vp, C.POINTER(SstInfo), vp, C.c_uint64, C.c_uint32, C.POINTER(vp)]),
+    "slate_block_reader_free": (None, [vp]),
+    "slate_block_reader_next": (C.c_int, [vp, C.POINTER(BlockView)]),
+    "slate_block_reader_want": (C.c_int, [vp, u64p, u64p]),
+    "slate_block_reader_feed": (C.c_int, [vp, vp, C.c_size_t]),
     "slate_bloom_build": (C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, vp, C.c_size_t, szp, u16p]),
     "slate_bloom_encode": (C.c_int, [vp, C.c_uint16, vp, C.c_size_t, C.c_int, vp, C.c_size_t, szp]),
     "slate_bloom_decode": (C.c_int, [vp, vp, C.c_size_t, C.c_int, u16p, vp, C.c_size_t, szp]),
@@ -222,6 +233,12 @@ class Context:
     def set_timing(self, on: bool) -> None:
         """Sum the SST builder's GPU pass times on this context (slate_ctx_set_timing)."""
         _check(lib().slate_ctx_set_timing(self._h, 1 if on else 0), "slate_ctx_set_timing")
+
+    def handbacks(self, reset: bool = False) -> int:
+        """slate_ctx_handbacks: blocks the fast paths handed to the exact decoder since the last reset."""
+        v = C.c_uint64()
+        _check(lib().slate_ctx_handbacks(self._h, C.byref(v), 1 if reset else 0), "slate_ctx_handbacks")
+        return v.value
 
     def gpu_time_ms(self, reset: bool = False) -> float:
         v = C.c_double()
@@ -423,6 +440,11 @@ class Context:
         if st != OK:
             return st, None
         return st, Index(h)
+
+    def iter_blocks(self, info: "SstInfo", index: "Index", sst: bytes, first: int = 0, read_ahead: int = 64):
+        """sstable.Iterator's block walk through slate_block_reader (read-ahead batches): a list of
+        (block, status, meta, data bytes incl. offsets, rows) in order; a failing block comes last."""
+        return reader_walk(self, info, index, sst, first, read_ahead)[0]
 
     def read_blocks(self, info: "SstInfo", index: "Index", start: int, end: int, sst: bytes):
         """ReadBlocks over the object bytes: returns (status, failed_block, decode outputs)."""
@@ -785,6 +807,41 @@ def _arena(items: list[bytes]):
         off[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
     data = np.frombuffer(b"".join(items) or b"\0", dtype=np.uint8).copy()
     return data, off
+
+
+def reader_walk(ctx: "Context", info: "SstInfo", index: "Index", sst: bytes, first: int = 0, read_ahead: int = 64):
+    """Drives slate_block_reader as a Go shim would: -> ([(block, status, meta, data, rows)], [(rs, re)
+    ranges fetched])."""
+    h = C.c_void_p()
+    _check(lib().slate_block_reader_create(ctx._h, C.byref(info), index.handle, first, read_ahead, C.byref(h)),
+           "slate_block_reader_create")
+    out, fetches = [], []
+    buf = None
+    try:
+        v = BlockView()
+        while True:
+            st = lib().slate_block_reader_next(h, C.byref(v))
+            if st == E_READER_END:
+                break
+            if st == E_READER_NEED_DATA:
+                rs, re_ = C.c_uint64(), C.c_uint64()
+                _check(lib().slate_block_reader_want(h, C.byref(rs), C.byref(re_)), "slate_block_reader_want")
+                fetches.append((rs.value, re_.value))
+                buf = np.frombuffer(bytes(sst[rs.value:re_.value]) or b"\0", dtype=np.uint8)
+                _check(lib().slate_block_reader_feed(h, _ptr(buf), re_.value - rs.value), "slate_block_reader_feed")
+                continue
+            meta = np.frombuffer(bytes(v.meta), META_DTYPE)[0]
+            n = int(meta["n_rows"])
+            dl = int(meta["data_len"]) + 2 * n
+            data = C.string_at(v.data, dl) if st == OK else b""
+            rows = np.frombuffer(C.string_at(v.rows, 16 * n), ROW_DTYPE).copy() if st == OK and n else \
+                np.zeros(0, ROW_DTYPE)
+            out.append((int(v.block), st, meta, data, rows))
+            if st != OK:
+                break
+    finally:
+        lib().slate_block_reader_free(h)
+    return out, fetches
 
 
 def read_info(sst: bytes) -> tuple[int, "SstInfo", bytes]:

@@ -231,3 +231,31 @@ def test_none_size_window(ctx, misalign):
         blocks += bg.sst_blocks(kvs, bs, ob.NONE)
     meta = _compare(ctx, ob.NONE, blocks, misalign=misalign)
     assert (meta["status"] == 0).sum() > 20 and len(set(meta["status"].tolist())) > 3
+
+
+def test_single_block_parallel_snappy(ctx):
+    """slate_block_decode of CodecSnappy blocks within the workgroup-parallel decoder's window
+    (decode.hip decode_one_par_kernel: tag chain by pointer doubling, bytes by pointer jumping):
+    V-half and random blocks, and the same blocks with one byte flipped and the CRC re-sealed (a
+    tag, a length, an offset, the varint header), so that every refusal of the parallel passes and
+    every serial fallback is exercised -- meta, bytes and offsets against the oracle."""
+    rng = random.Random(77)
+    blocks = bg.sst_blocks(bg.kv_synthetic(38 * 40), 4096, ob.SNAPPY)[:40]
+    blocks += bg.sst_blocks(bg.random_kvs(rng, 2000, alphabet=4), 4096, ob.SNAPPY)[:20]
+    blocks += bg.sst_blocks(bg.kv_synthetic(38 * 20, half=False), 4096, ob.SNAPPY)[:10]
+    muts = []
+    for b in blocks:
+        for _ in range(3):
+            body = bytearray(b[:-4])
+            pos = rng.choice([0, 1, rng.randrange(len(body)), rng.randrange(min(len(body), 40))])
+            body[pos] ^= 1 << rng.randrange(8)
+            muts.append(bg.recrc(bytes(body)))
+    for i, blk in enumerate(blocks + muts):
+        st, m, data, offs = ctx.block_decode(blk, ob.SNAPPY)
+        blob, off = bg.pack([blk])
+        o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(ob.SNAPPY, blob, off)
+        assert m.tobytes() == o_meta[0].tobytes(), (i, m, o_meta[0])
+        assert st == int(o_meta[0]["status"])
+        if st == 0:
+            assert data == o_out[: int(m["data_len"])].tobytes(), i
+            assert offs == [int(r["row_off"]) for r in o_rows[: int(m["n_rows"])]], i

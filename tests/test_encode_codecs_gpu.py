@@ -187,3 +187,34 @@ def test_vhalf_blocks_compress(sc, ctx, codec):
     assert st == 0 and len(metas) > 1000
     fb = sizes[codec][info["filter_offset"]:info["filter_offset"] + info["filter_len"]]
     assert ob.bloom_decode(fb, codec, cap=1 << 23)[0] == 0
+
+
+@pytest.mark.parametrize("codec", [ob.ZLIB, ob.ZSTD])
+def test_vhalf_block_ratio(sc, ctx, codec):
+    """configs[1]-shaped blocks (100-byte V-half KVs, 4 KiB): block.Encode's Zlib bodies (a hash-chain
+    parse with dynamic Huffman codes) and Zstd bodies (repeat offsets, FSE_Compressed tables) come
+    within 2 % of the library each Go writer stands for (zlib level 6 + Go's 5-byte final block;
+    libzstd level 3), and every one decodes to its block (oracle and the library)."""
+    kvs = bg.kv_synthetic(38 * 120)
+    ours = lib = 0
+    bb = None
+    blocks = []
+    for k, v in kvs:
+        if bb is None:
+            bb = ob.BlockBuilder(4096)
+        if not bb.add_value(k, v):
+            blocks.append(bb.build()[:2])
+            bb = ob.BlockBuilder(4096)
+            assert bb.add_value(k, v)
+    for data, offs in blocks:
+        st, enc = ctx.block_encode(data, offs, codec)
+        assert st == 0
+        m, dec, _ = ob.block_decode(enc, codec)
+        assert int(m["status"]) == 0 and dec[:int(m["data_len"])] == data
+        frame = enc[:-4]
+        raw = bytes(dec[:len(dec)])
+        raw = raw[:int(m["data_len"]) + 2 * len(offs) + 2]
+        assert _lib_decode(codec, frame, len(raw)) == raw
+        ours += len(frame)
+        lib += len(zlib.compress(raw, 6)) + 5 if codec == ob.ZLIB else len(zstdgen.frame(raw, 3, True, True))
+    assert ours <= 1.02 * lib, (ours, lib, ours / lib)

@@ -167,3 +167,59 @@ def test_fast_path_crc_every_length(ctx, misalign):
     st = [int(x) for x in meta["status"]]
     assert [i for i, x in enumerate(st) if x == 2] == [i for i in range(96) if i % 6 in (1, 2, 3, 4)], st
     assert st.count(0) >= 10, st
+
+
+def _kv100_blocks(n_kv, seed=20250307):
+    """configs[1]'s block shape: 16-byte keys, 84-byte V-half values, 4 KiB blocks, CodecNone bodies."""
+    kvs = bg.kv_synthetic(n_kv, seed=seed, half=True)
+    return [b[:-4] for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+
+
+@pytest.mark.parametrize("level", [1, 3, 6, 9, 19])
+def test_kv100_fse_table_blocks(ctx, level):
+    """4 KiB blocks of 100-byte KVs through libzstd: ~112 sequences and FSE_Compressed LL / OF / ML
+    tables per block (zstd_fast.hip phase A', the lane-per-block FSE parse), at every input alignment,
+    with and without checksum and content size; bit-exact against the oracle, and (level 3, the
+    reference writer's default class) no block handed to the exact path."""
+    bodies = _kv100_blocks(38 * 96)
+    for misalign in range(16):
+        chk, fcs = misalign % 3 != 1, misalign % 4 != 2
+        blocks = [_crc(_z(d, level, chk, fcs)) for d in bodies[misalign * 6:misalign * 6 + 12]]
+        ctx.handbacks(reset=True)
+        meta = _compare(ctx, blocks, misalign=misalign)
+        assert (meta["status"] == 0).all()
+        if level == 3:
+            assert ctx.handbacks() == 0, misalign
+
+
+def test_kv100_fse_damaged(ctx):
+    """The same frames with one byte of the sequences section (table descriptions or bitstream) or
+    of the literals flipped under a re-sealed CRC, or a stale CRC: every status and byte is the
+    exact path's (the FSE parse hands back whatever fails a check)."""
+    rng = random.Random(5)
+    bodies = _kv100_blocks(38 * 40)
+    blocks = []
+    for d in bodies:
+        f = bytearray(_z(d, 3, True, True))
+        kind = rng.randrange(4)
+        if kind == 0:  # the sequences section (the frame's last ~150 bytes before the checksum)
+            f[len(f) - 4 - rng.randrange(1, 150)] ^= 1 << rng.randrange(8)
+        elif kind == 1:  # a literal byte (XXH64 mismatch -> exact path)
+            f[rng.randrange(20, 200)] ^= 0x40
+        elif kind == 2:  # the checksum itself
+            f[-1] ^= 1
+        blk = _crc(bytes(f))
+        if kind == 3:  # stale CRC
+            blk = blk[:-1] + bytes([blk[-1] ^ 0xFF])
+        blocks.append(blk)
+    _compare(ctx, blocks, misalign=3)
+
+
+def test_kv100_fse_large_batch(ctx):
+    """A few thousand configs[1]-shaped Zstd blocks in one batch: phase A' over many rounds."""
+    bodies = _kv100_blocks(38 * 3000, seed=7)
+    blocks = [_crc(_z(d, 3, True, True)) for d in bodies]
+    ctx.handbacks(reset=True)
+    meta = _compare(ctx, blocks, misalign=9)
+    assert (meta["status"] == 0).all()
+    assert ctx.handbacks() == 0

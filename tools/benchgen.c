@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <zlib.h>
 
 typedef int (*compress_fn)(const char*, size_t, char*, size_t*);
 static compress_fn g_compress;
@@ -56,7 +57,7 @@ int bg_init_zstd(const char* libzstd) {
 }
 static uint32_t g_tab[256];
 
-static uint32_t crc32(const uint8_t* p, size_t n) {
+static uint32_t bg_crc32(const uint8_t* p, size_t n) {
   uint32_t c = 0xFFFFFFFFu;
   for (size_t i = 0; i < n; i++) c = g_tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
   return ~c;
@@ -72,6 +73,52 @@ int bg_init(const char* libsnappy) {
   if (!h) return -1;
   g_compress = (compress_fn)dlsym(h, "snappy_compress");
   return g_compress ? 0 : -2;
+}
+
+/* CodecZlib (codec 2): zlib level 6, in the shape Go's compress/zlib writer closes a stream with --
+ * the data's non-final deflate blocks, an empty FINAL stored block, the Adler-32 (tests/sstgen.py
+ * go_zlib): zlib's sync flush ends with an empty non-final stored block, whose BFINAL bit is set
+ * (the bit found by trial: the one flip after which inflate ends there with the same bytes). */
+static long go_zlib6(const uint8_t* s, size_t n, uint8_t* d, size_t cap) {
+  if (cap < 16) return -1;
+  z_stream z;
+  memset(&z, 0, sizeof z);
+  if (deflateInit2(&z, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return -1;
+  z.next_in = (Bytef*)s;
+  z.avail_in = (uInt)n;
+  z.next_out = d + 2;
+  z.avail_out = (uInt)(cap - 6);
+  int r = deflate(&z, Z_SYNC_FLUSH);
+  size_t bl = (cap - 6) - z.avail_out;
+  deflateEnd(&z);
+  if (r != Z_OK || z.avail_in != 0 || bl < 5) return -1;
+  uint8_t* body = d + 2;
+  static __thread uint8_t chk[1 << 17];
+  int found = 0;
+  for (size_t pos = bl - 5; !found && pos + 6 >= bl && pos < bl; pos--) {
+    for (int bit = 0; bit < 8 && !found; bit++) {
+      body[pos] ^= (uint8_t)(1u << bit);
+      z_stream t;
+      memset(&t, 0, sizeof t);
+      if (inflateInit2(&t, -15) == Z_OK) {
+        t.next_in = body;
+        t.avail_in = (uInt)bl;
+        t.next_out = chk;
+        t.avail_out = sizeof chk;
+        const int e = inflate(&t, Z_FINISH);
+        found = e == Z_STREAM_END && t.avail_in == 0 && t.total_out == n && memcmp(chk, s, n) == 0;
+        inflateEnd(&t);
+      }
+      if (!found) body[pos] ^= (uint8_t)(1u << bit);
+    }
+    if (pos == 0) break;
+  }
+  if (!found) return -1;
+  d[0] = 0x78;
+  d[1] = 0x9c;
+  const uint32_t a = (uint32_t)adler32(adler32(0L, Z_NULL, 0), s, (uInt)n);
+  d[2 + bl] = (uint8_t)(a >> 24); d[3 + bl] = (uint8_t)(a >> 16); d[4 + bl] = (uint8_t)(a >> 8); d[5 + bl] = (uint8_t)a;
+  return (long)(bl + 6);
 }
 
 typedef struct {
@@ -103,13 +150,18 @@ static void* work(void* arg) {
       if (g_lz4f_err(r)) { j->rc = -4; return NULL; }
       cl = r;
     }
+    else if (j->codec == 2) {
+      const long r = go_zlib6(s, n, d, j->stride - 4);
+      if (r < 0) { j->rc = -6; return NULL; }
+      cl = (size_t)r;
+    }
     else if (j->codec == 4) {
       size_t r = g_zc2(zc, d, j->stride - 4, s, n);
       if (g_zerr(r)) { j->rc = -5; g_zfree(zc); return NULL; }
       cl = r;
     }
     else if (g_compress((const char*)s, n, (char*)d, &cl) != 0) { j->rc = -3; return NULL; }
-    uint32_t c = crc32(d, cl);
+    uint32_t c = bg_crc32(d, cl);
     d[cl] = (uint8_t)(c >> 24); d[cl + 1] = (uint8_t)(c >> 16); d[cl + 2] = (uint8_t)(c >> 8); d[cl + 3] = (uint8_t)c;
     j->dst_len[i] = cl + 4;
   }
@@ -351,7 +403,7 @@ static void* set_build_work(void* arg) {
       if (g_zerr(r)) { j->rc = -5; break; }
       cl = r;
     } else if (g_compress((const char*)blk, n, (char*)d, &cl) != 0) { j->rc = -3; break; }
-    uint32_t c = crc32(d, cl);
+    uint32_t c = bg_crc32(d, cl);
     d[cl] = (uint8_t)(c >> 24); d[cl + 1] = (uint8_t)(c >> 16); d[cl + 2] = (uint8_t)(c >> 8); d[cl + 3] = (uint8_t)c;
     j->enc_len[k] = cl + 4;
   }

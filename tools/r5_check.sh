@@ -1,0 +1,26 @@
+#!/bin/bash
+# round-5 development run (one GPU call): new-feature tests, the extra bench legs alone, then a
+# same-box A/B of decode library builds.  env: TESTS, LEGS ("kv100_zstd:262144 kv100_zlib:65536"),
+# VLIB + VTESTS (tests on a variant library), LIBS, ROUNDS, TAG
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/${TAG:-r5}
+mkdir -p $OUT
+export TMPDIR=/tmp
+if [ -n "$TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo TESTS_FAILED; tail -60 $OUT/tests.log; exit 1; }
+  tail -2 $OUT/tests.log
+fi
+for L in $LEGS; do
+  name=${L%%:*}; blocks=${L#*:}
+  timeout -k 10 300 python -u tools/leg_probe.py $name --blocks $blocks --extra-steps 5 > $OUT/$name.json 2> $OUT/$name.err || { echo LEG_FAILED $name; tail -30 $OUT/$name.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$OUT/$name.json'));[print(k,{x:v[x] for x in ('value','ms_per_step','handbacks') if x in v}, v['roofline']['kernel_ms'], v['roofline']['frac']) for k,v in d.items()]"
+done
+if [ -n "$VTESTS" ]; then
+  SLATE_LIB_VARIANT=${VLIB:-libslatecodec.so} timeout -k 10 600 python -u -m pytest $VTESTS -x -q --timeout 120 --timeout-method thread > $OUT/vtests.log 2>&1 || { echo VTESTS_FAILED; tail -40 $OUT/vtests.log; exit 1; }
+  tail -1 $OUT/vtests.log
+fi
+if [ -n "$LIBS" ]; then
+  timeout -k 10 900 python -u tools/lib_ab.py ${BLOCKS:-1000000} ${ROUNDS:-3} $LIBS > $OUT/ab.log 2>&1 || { echo AB_FAILED; tail -30 $OUT/ab.log; exit 1; }
+  tail -1 $OUT/ab.log
+fi
