@@ -580,8 +580,9 @@ def oracle_threads_encode(ob, keys, key_off, vals, val_off, codec, threads):
 
 def measured_copy_gbps(device, nbytes: int = 2 << 30, reps: int = 10) -> dict:
     """Read + write bytes per second of a large device-to-device copy, outside the timed region:
-    a hand-written streaming copy kernel (tools/copy_kernel.hip: 16 B per lane, nontemporal, four
-    loads in flight per lane; the best of 4 / 8 / 16 workgroups per CU) and torch's copy_."""
+    the best of the hand-written streaming copy shapes in tools/copy_kernel.hip (16 B per lane;
+    grid-stride with 4 or 8 loads in flight, plain or nontemporal, at 4 / 8 / 16 workgroups per CU,
+    and one-pass grids covering the buffer), and torch's copy_."""
     import ctypes
     import torch
     a = torch.empty(nbytes, dtype=torch.uint8, device=device)
@@ -603,16 +604,28 @@ def measured_copy_gbps(device, nbytes: int = 2 << 30, reps: int = 10) -> dict:
     so = os.path.join(REPO, "tools", "build", "libcopykernel.so")
     if os.path.exists(so):
         lib = ctypes.CDLL(so)
-        lib.slate_probe_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                                                ctypes.c_int, ctypes.c_int]
+        fn = getattr(lib, "slate_probe_stream_copy_v", None)
         cus = torch.cuda.get_device_properties(device).multi_processor_count
-        best = 0.0
-        for g in (4, 8, 16):
-            rate = timed(lambda: lib.slate_probe_stream_copy(a.data_ptr(), b.data_ptr(), nbytes, stream.cuda_stream,
-                                                             cus, g))
-            best = max(best, rate)
-        assert torch.equal(a[:4096], b[:4096]) and torch.equal(a[-4096:], b[-4096:]), "copy kernel"
-        res["stream_copy_GBps"] = round(best, 1)
+        shapes = {}
+        if fn is None:  # an older build: the round-4 kernel only
+            lib.slate_probe_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            for g in (4, 8, 16):
+                shapes[f"v0_g{g}"] = timed(lambda: lib.slate_probe_stream_copy(a.data_ptr(), b.data_ptr(), nbytes,
+                                                                               stream.cuda_stream, cus, g))
+        else:
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int,
+                           ctypes.c_int, ctypes.c_int]
+            for v in range(8):
+                for g in ((4, 8, 16) if v < 5 else (8,)):
+                    b.zero_()
+                    shapes[f"v{v}_g{g}" if v < 5 else f"v{v}"] = timed(
+                        lambda: fn(a.data_ptr(), b.data_ptr(), nbytes, stream.cuda_stream, cus, g, v))
+                    assert torch.equal(a[:4096], b[:4096]) and torch.equal(a[-4096:], b[-4096:]), f"copy kernel v{v}"
+        best = max(shapes, key=shapes.get)
+        res["stream_copy_GBps"] = round(shapes[best], 1)
+        res["stream_copy_shape"] = best
+        res["stream_copy_shapes"] = {k: round(v, 1) for k, v in shapes.items()}
     del a, b
     res["value"] = res.get("stream_copy_GBps", res["torch_copy_GBps"])
     return res

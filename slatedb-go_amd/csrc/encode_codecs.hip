@@ -938,8 +938,12 @@ __device__ void fse_build_ct(const int16_t* norm, uint32_t n, uint32_t L, uint16
 // a compressed block body: raw literals section, then the sequences with repeat offsets (RFC 8878
 // 3.1.2.5) and, per symbol type, the predefined, RLE or a block-built FSE table -- whichever the
 // cost estimate prefers (Python model over configs[1] blocks: 1.097 -> 1.009 x libzstd level 3)
+// first: the frame's first block.  A later block starts from the repeat offsets the previous
+// block left (RFC 8878 3.1.2.5: they carry across a frame's blocks), which this piece, parsed on
+// its own, does not know: its first three sequences use explicit offsets, after which the
+// encoder's repeat offsets equal the decoder's whatever came before.
 __device__ uint32_t zstd_body(const uint8_t* tags, uint32_t tn, const uint8_t* raw, uint32_t n, uint8_t* dst, uint32_t cap,
-                              Seq* seqs, uint32_t seq_cap, ZFse* F, uint32_t lane, bool* over) {
+                              Seq* seqs, uint32_t seq_cap, ZFse* F, bool first, uint32_t lane, bool* over) {
   // pass 1: the sequences (literal run before each match) and the literal count
   uint32_t ns = 0, lit = 0, nlit = 0;
   bool too_many = false;
@@ -1018,7 +1022,8 @@ __device__ uint32_t zstd_body(const uint8_t* tags, uint32_t tn, const uint8_t* r
         const Seq q = rd(i);
         const uint32_t o = q.off;
         uint32_t ov;
-        if (q.ll != 0) ov = o == r0 ? 1u : (o == r1 ? 2u : (o == r2 ? 3u : o + 3));
+        if (!first && i < 3) ov = o + 3;
+        else if (q.ll != 0) ov = o == r0 ? 1u : (o == r1 ? 2u : (o == r2 ? 3u : o + 3));
         else ov = o == r1 ? 1u : (o == r2 ? 2u : (o + 1 == r0 ? 3u : o + 3));
         if (ov > 3) {
           r2 = r1;
@@ -1369,7 +1374,8 @@ __global__ __launch_bounds__(kBig ? 64 : 256) void pc_transcode_kernel(const uin
       d = deflate_body(src, rp, pc.len, (pc.flags & 2) != 0, o, cap, F, lane, &over);
     } else {
       Seq* seqs = kBig ? big_seqs + pc.seqs : lds_seqs;
-      d = zstd_body(t, tn, p, pc.len, o, cap, seqs, kBig ? pc.len / 3 + 2 : kSmallSeqs, fse, lane, &over);
+      d = zstd_body(t, tn, p, pc.len, o, cap, seqs, kBig ? pc.len / 3 + 2 : kSmallSeqs, fse, (pc.flags & 1) != 0, lane,
+                    &over);
       if (d >= pc.len) over = true;  // a raw block is smaller
     }
     if (lane == 0) body_len[id] = over ? kBodyRaw : d;

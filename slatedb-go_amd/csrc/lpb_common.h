@@ -303,6 +303,14 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
   return (uint64_t(hi) << 32) | lo;
 }
+// A wave-uniform load of memory the running kernel never writes (plan arrays: in_off, out_off,
+// row_base), as a scalar load.  The constant address space says so to the compiler; a plain load
+// of a uniform address otherwise becomes a vector load + readfirstlane, and its s_waitcnt vmcnt(0)
+// also drains every block load the wave has in flight.  p must be wave-uniform.
+template <typename T>
+__device__ __forceinline__ T sload(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)(p);
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
   const uint64_t b = uniform64(reinterpret_cast<uint64_t>(base));
   const uint32_t n = __builtin_amdgcn_readfirstlane(bytes < kOOB ? uint32_t(bytes) : kOOB);

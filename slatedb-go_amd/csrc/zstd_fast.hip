@@ -307,7 +307,10 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
     const uint32_t s = body + pos;  // frame offset of the sequences section
     const uint32_t c_lo = (shift + s) >> 4;
     const uint32_t wend = 16 * (c_lo + kZfTailChunks) - shift;  // frame offset past the window
-    ok = ok && body + nb + (h.checksum ? 4u : 0u) <= wend;
+    // the whole section (and the checksum) in the window: needed by this parse, not by the
+    // deferral to phase A' (which reads its own, larger window) -- a 4 KiB block of 100-byte KVs
+    // can have a 164-byte section + checksum
+    const bool inwin = body + nb + (h.checksum ? 4u : 0u) <= wend;
     {
       v4u t[kZfTailChunks];
 #pragma unroll
@@ -342,7 +345,7 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
         defer = ok && nseq != 0 && sp < sn && !(m0 & 3) && a_ll != 3 && a_of != 3 && a_ml != 3 &&
                 (nseq > kZsFastSeqs || a_ll == 2 || a_of == 2 || a_ml == 2) && nseq <= kZsFseSeqs;
       }
-      ok = ok && !defer && nseq <= kZsFastSeqs;
+      ok = ok && !defer && nseq <= kZsFastSeqs && inwin;
       uint32_t lp = 0, o = 0;
       const uint32_t lbase = cap - nlit;
       if (ok && nseq == 0) {

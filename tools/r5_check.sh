@@ -1,14 +1,19 @@
 #!/bin/bash
 # round-5 development run (one GPU call): new-feature tests, the extra bench legs alone, then a
 # same-box A/B of decode library builds.  env: TESTS, LEGS ("kv100_zstd:262144 kv100_zlib:65536"),
-# VLIB + VTESTS (tests on a variant library), LIBS, ROUNDS, TAG
+# VLIB + VTESTS (tests on a variant library), LIBS, ROUNDS, TAG, PRE (a probe script run first),
+# DESELECT (pytest --deselect options), NLIBS (libraries for a CodecNone A/B)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/${TAG:-r5}
 mkdir -p $OUT
 export TMPDIR=/tmp
+if [ -n "$PRE" ]; then
+  timeout -k 10 300 python -u $PRE > $OUT/pre.log 2>&1 || { echo PRE_FAILED; tail -30 $OUT/pre.log; exit 1; }
+  cat $OUT/pre.log
+fi
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo TESTS_FAILED; tail -60 $OUT/tests.log; exit 1; }
+  timeout -k 10 600 python -u -m pytest $TESTS $DESELECT -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { echo TESTS_FAILED; tail -60 $OUT/tests.log; exit 1; }
   tail -2 $OUT/tests.log
 fi
 for L in $LEGS; do
@@ -23,4 +28,8 @@ fi
 if [ -n "$LIBS" ]; then
   timeout -k 10 900 python -u tools/lib_ab.py ${BLOCKS:-1000000} ${ROUNDS:-3} $LIBS > $OUT/ab.log 2>&1 || { echo AB_FAILED; tail -30 $OUT/ab.log; exit 1; }
   tail -1 $OUT/ab.log
+fi
+if [ -n "$NLIBS" ]; then  # a second A/B on the CodecNone workload
+  SLATE_AB_CODEC=none timeout -k 10 900 python -u tools/lib_ab.py ${BLOCKS:-1000000} ${ROUNDS:-3} $NLIBS > $OUT/ab_none.log 2>&1 || { echo AB_NONE_FAILED; tail -30 $OUT/ab_none.log; exit 1; }
+  tail -1 $OUT/ab_none.log
 fi
