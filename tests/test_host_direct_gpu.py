@@ -94,7 +94,10 @@ def test_partly_registered_outputs_use_staging(ctxs):
     staging instead -- same bytes as the oracle, no fault (api_host.cpp sink_map / mapped_range)."""
     import ctypes
     import slatecodec as sc
-    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")  # the runtime the library links
+    sc.lib()
+    # the HIP runtime already in the process, by its soname (a second copy by path would bind to
+    # whatever HSA runtime torch loaded and may not resolve)
+    hip = ctypes.CDLL("libamdhip64.so.7")
     codec = ob.SNAPPY
     blob, off = _workload(codec, corrupt=False)
     n = len(off) - 1

@@ -2,7 +2,8 @@
 # round-5 development run (one GPU call): new-feature tests, the extra bench legs alone, then a
 # same-box A/B of decode library builds.  env: TESTS, LEGS ("kv100_zstd:262144 kv100_zlib:65536"),
 # VLIB + VTESTS (tests on a variant library), LIBS, ROUNDS, TAG, PRE (a probe script run first),
-# DESELECT (pytest --deselect options), NLIBS (libraries for a CodecNone A/B)
+# DESELECT (pytest --deselect options), NLIBS (libraries for a CodecNone A/B), PERCALL=1,
+# ENCTRACE=1, VLIB2 + VTESTS2
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/${TAG:-r5}
@@ -25,6 +26,10 @@ if [ -n "$VTESTS" ]; then
   SLATE_LIB_VARIANT=${VLIB:-libslatecodec.so} timeout -k 10 600 python -u -m pytest $VTESTS -x -q --timeout 120 --timeout-method thread > $OUT/vtests.log 2>&1 || { echo VTESTS_FAILED; tail -40 $OUT/vtests.log; exit 1; }
   tail -1 $OUT/vtests.log
 fi
+if [ -n "$VTESTS2" ]; then
+  SLATE_LIB_VARIANT=$VLIB2 timeout -k 10 600 python -u -m pytest $VTESTS2 -x -q --timeout 120 --timeout-method thread > $OUT/vtests2.log 2>&1 || { echo VTESTS2_FAILED; tail -40 $OUT/vtests2.log; exit 1; }
+  tail -1 $OUT/vtests2.log
+fi
 if [ -n "$LIBS" ]; then
   timeout -k 10 900 python -u tools/lib_ab.py ${BLOCKS:-1000000} ${ROUNDS:-3} $LIBS > $OUT/ab.log 2>&1 || { echo AB_FAILED; tail -30 $OUT/ab.log; exit 1; }
   tail -1 $OUT/ab.log
@@ -33,3 +38,14 @@ if [ -n "$NLIBS" ]; then  # a second A/B on the CodecNone workload
   SLATE_AB_CODEC=none timeout -k 10 900 python -u tools/lib_ab.py ${BLOCKS:-1000000} ${ROUNDS:-3} $NLIBS > $OUT/ab_none.log 2>&1 || { echo AB_NONE_FAILED; tail -30 $OUT/ab_none.log; exit 1; }
   tail -1 $OUT/ab_none.log
 fi
+if [ -n "$PERCALL" ]; then  # per-call latency (C harness + Python)
+  timeout -k 10 300 python -u tools/percall_bench.py > $OUT/percall.json 2> $OUT/percall.err || { echo PERCALL_FAILED; tail -20 $OUT/percall.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$OUT/percall.json'));print({k:v for k,v in d.items() if 'us' in k}, d.get('c_abi'))"
+fi
+if [ -n "$ENCTRACE" ]; then  # configs[2] host-input split, with the builder's host trace
+  for c in none snappy; do
+    SLATE_HOST_TRACE=1 timeout -k 10 300 python -u tools/bench_encode.py --codec $c --steps 3 > $OUT/enc_$c.json 2> $OUT/enc_$c.trace || { echo ENC_FAILED; tail -20 $OUT/enc_$c.trace; exit 1; }
+    python3 -c "import json;d=json.load(open('$OUT/enc_$c.json'));print('$c', d['host_input'], d['device_input'])"
+  done
+fi
+
