@@ -54,7 +54,9 @@ int ctx_crc32_device(slate_ctx* ctx, const uint8_t* d_data, size_t n, uint32_t* 
 int ctx_crc32_host_buffer(slate_ctx* ctx, const uint8_t* data, size_t n, uint32_t* crc) {
   SLATE_HIP(ctx_bind(ctx));
   SLATE_HIP(ctx->e_i.ensure(n + 16));
-  if (n) SLATE_HIP(hipMemcpyAsync(ctx->e_i.p, data, n, hipMemcpyHostToDevice, ctx->stream));
+  // through the context's page-locked staging (a pageable copy of a 10 MB index ran at a few GB/s)
+  const int s = ctx_h2d(ctx, ctx->e_i.p, data, n, ctx->stream);
+  if (s) return s;
   return ctx_crc32_device(ctx, ctx->e_i.as<uint8_t>(), n, crc);
 }
 
@@ -1771,7 +1773,8 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
       if (!st) st = ctx_snappy_encode_crc_device(ctx, ctx->e_i.as<uint8_t>(), fb.size(), index);
       if (st) { delete t; return st; }
     } else {
-      st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
+      if (b->cfg.codec == SLATE_CODEC_NONE) index.swap(fb);  // (the payload as built: no copy)
+      else st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
       if (st) { delete t; return st; }
       uint32_t icrc = 0;
       st = ctx_crc32_host_buffer(ctx, index.data(), index.size(), &icrc);
@@ -1780,8 +1783,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
     }
   }
   const uint64_t index_off = b->current_len + buf.size();
-  buf.insert(buf.end(), index.begin(), index.end());
-  const uint64_t meta_off = b->current_len + buf.size();
+  const uint64_t meta_off = index_off + index.size();
   // ---- info (builder.go:246-258, flatbuf.go:62-81)
   InfoFields inf;
   inf.index_offset = index_off;
@@ -1796,8 +1798,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   st = ctx_crc32_host_buffer(ctx, info.data(), info.size(), &fcrc);
   if (st) { delete t; return st; }
   put_be32(info, fcrc);
-  buf.insert(buf.end(), info.begin(), info.end());
-  put_be32(buf, uint32_t(meta_off));  // builder.go:260 uint32(metaOffset)
+  put_be32(info, uint32_t(meta_off));  // builder.go:260 uint32(metaOffset)
   t->info.index_offset = index_off;
   t->info.index_len = index.size();
   t->info.filter_offset = filter_off;
@@ -1805,15 +1806,20 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   t->info.codec = b->cfg.codec;
   t->info.first_key_len = uint32_t(b->first_key.size());
   t->first_key = b->first_key;
-  auto fin = std::make_shared<HostBytes>(buf.size());
+  // the final chunk: last block and filter (buf), index, info and the meta offset, each copied once
+  PoolScope pool(ctx);
+  const size_t fin_len = buf.size() + index.size() + info.size();
+  auto fin = std::make_shared<HostBytes>(fin_len);
   if (!fin->ok()) {
     delete t;
     return SLATE_E_OOM;
   }
   t->chunks.assign(b->blocks.begin(), b->blocks.end());
   b->blocks.clear();
-  if (!buf.empty()) memcpy(fin->p, buf.data(), buf.size());
-  t->chunks.push_back(ByteView{fin, 0, buf.size()});
+  if (!buf.empty()) par_memcpy(fin->p, buf.data(), buf.size());
+  if (!index.empty()) par_memcpy(fin->p + buf.size(), index.data(), index.size());
+  memcpy(fin->p + buf.size() + index.size(), info.data(), info.size());
+  t->chunks.push_back(ByteView{fin, 0, fin_len});
   *table = t;
   if (host_trace())
     fprintf(stderr,

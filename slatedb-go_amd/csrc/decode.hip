@@ -207,7 +207,8 @@ __global__ void plan_list_kernel(int codec, const uint8_t* __restrict__ in, cons
 // oracle or_block_decode_batch), one wave per block reading the stream from HBM.
 __global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off, uint32_t n,
-                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz);
+                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz,
+                                                        const uint32_t* list, const uint32_t* count);
 
 // ------------------------------------------------ exclusive scan (2 arrays)
 constexpr int kScanThreads = 256;
@@ -812,9 +813,12 @@ __device__ int wave_inflate(const uint8_t* in, uint32_t n, uint8_t* out, uint32_
   return SLATE_OK;
 }
 
+// list: the blocks to plan (list[0 .. *count): the ones the lane-per-block plan left), or nullptr
+// for all n
 __global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restrict__ in,
                                                         const uint64_t* __restrict__ in_off, uint32_t n,
-                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz) {
+                                                        uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz,
+                                                        const uint32_t* list, const uint32_t* count) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[kZFixed + 4 * kZScratch];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   ZHuff* fix = reinterpret_cast<ZHuff*>(smem);
@@ -822,7 +826,9 @@ __global__ __launch_bounds__(256) void plan_zlib_kernel(const uint8_t* __restric
   if (wave == 0) zfixed_build(fix, fix + 1, zs->lens, lane);
   __syncthreads();
   const uint32_t waves = gridDim.x * 4;
-  for (uint32_t b = blockIdx.x * 4 + wave; b < n; b += waves) {
+  const uint32_t items = list ? *count : n;
+  for (uint32_t k = blockIdx.x * 4 + wave; k < items; k += waves) {
+    const uint32_t b = list ? list[k] : k;
     const uint64_t s0 = in_off[b], len = in_off[b + 1] - s0;
     uint32_t dl = 0;
     if (len >= 6 && len - 4 < 0xFFFFFFFFull) wave_inflate(in + s0, uint32_t(len - 4), nullptr, 0xFFFFFFFFu, zs, fix, fix + 1, lane, &dl);
@@ -1598,8 +1604,15 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
   } else {
     plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
   }
-  if (codec == SLATE_CODEC_ZLIB && n > 0)
-    plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base);
+  if (codec == SLATE_CODEC_ZLIB && n >= 64) {
+    // block-sized streams lane per block (zlib_fast.hip); the rest: the wave plan
+    (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
+    hipError_t e = launch_zlib_plan_fast(st, in, in_off, n, out_off, row_base, s.zf.list, s.zf.count, 0);
+    if (e != hipSuccess) return e;
+    plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, s.zf.list, s.zf.count);
+  } else if (codec == SLATE_CODEC_ZLIB && n > 0) {
+    plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, nullptr, nullptr);
+  }
   if (codec == SLATE_CODEC_ZSTD && n > 0) {
     // single-frame blocks with a content size: lane per block; the rest: the wave plan
     (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
@@ -2052,7 +2065,15 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   uint32_t wgs_needed = (a.n + kDecodeThreads / 64 - 1) / (kDecodeThreads / 64);
   uint32_t grid = min(wgs_needed, uint32_t(num_cus) * kDecodeWgPerCu);
   const size_t lds_large = kTabBytes + size_t(kLargeInCap) + kLargeOutCap;
-  if (a.codec == SLATE_CODEC_ZLIB) {
+  if (a.codec == SLATE_CODEC_ZLIB && !a.raw && !(dbg_bits(a) & 16)) {
+    // the fast path (zlib_fast.hip phase Z + zstd_fast.hip phases A2 and B), then the exact path
+    // over the blocks it handed back
+    (void)hipMemsetAsync(s.zf.count, 0, 3 * sizeof(uint32_t), st);
+    hipError_t e = launch_zlib_fast(st, a, s.zf, num_cus);
+    if (e != hipSuccess) return e;
+    decode_list_kernel<1><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);
+    decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
+  } else if (a.codec == SLATE_CODEC_ZLIB) {
     decode_fast_kernel<1><<<grid, kDecodeThreads, lds, st>>>(a);
     decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else if (a.codec == SLATE_CODEC_ZSTD) {

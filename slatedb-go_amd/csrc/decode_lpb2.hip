@@ -52,12 +52,9 @@ namespace {
 
 // ring positions still valid behind d: a step's store reaches 20 bytes past d's dword
 // (five dwords), i.e. 109 bytes behind d modulo the ring
-// bytes a step moves at most (16 or 32); its store writes kStep/4 + 1 dwords from d's dword
-#ifndef SLATE_LPB_STEP
-#define SLATE_LPB_STEP 16
-#endif
-constexpr uint32_t kStep = SLATE_LPB_STEP;
-static_assert(kStep == 16 || kStep == 32, "step");
+// bytes a step moves at most; its store writes kStep/4 + 1 dwords from d's dword (a 32-byte step
+// was measured slower in round 5: 4.189 vs 4.151 ms per 1 M blocks, same box, and removed)
+constexpr uint32_t kStep = 16;
 constexpr uint32_t kStoreReach = kStep + 4;
 constexpr uint32_t kReach = kOR - kStoreReach;
 // section markers in the assembly (tools/loop_mix.py --marks): reading aid only, they fence the scheduler
@@ -614,7 +611,7 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
 #endif
   // ---- CRC32 of one committed chunk (the two steps without the walker)
   LPB_MARK(crc);
-  if (kSlot == 0 || kSlot == 2 || (kStep == 32 && kSlot == 1)) {
+  if (kSlot == 0 || kSlot == 2) {
     const bool go = L.crc_pos < L.c_commit && int32_t(L.crc_pos) <= L.crc_last;
     if (dbg & 64) L.crc_pos += go ? 1u : 0u;  // ablation: skip the lookups, keep the ring moving
     else crc_chunk(L, in, tab, go);
@@ -656,16 +653,11 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
     // dword keeps the bytes below d (L.T)
     const uint32_t b = L.d & 3;
     const uint32_t m8 = (kOR == kIR || !L.lit) ? kOR - 8 : kIR - 8;
-    if constexpr (kStep == 16) {
+    {
       const v4u v = ring_rd16(L.lit ? in : ring, L.src, m8);
       const Win5 y = shift_in(v, L.T, b);
       store_win(ring, L.d & ~3u, y);
       L.T = pick5(y, (b + k) >> 2);
-    } else {
-      const V8 v = ring_rd32(L.lit ? in : ring, L.src, m8);
-      const Win9 y = shift_in9(v, L.T, b);
-      store_win9(ring, L.d & ~3u, y);
-      L.T = pick9(y, (b + k) >> 2);
     }
     L.d += k;
     L.rem -= k;

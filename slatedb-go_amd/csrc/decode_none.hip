@@ -30,23 +30,12 @@ namespace slate {
 
 namespace {
 
-// SLATE_NONE_REP: the chunk CRCs from slicing-by-2 tables replicated 32 times, copy c in LDS bank
-// c, lane l reading copy l mod 32 (no bank conflicts on the random indices; the slicing-by-16 tables
-// conflict ~3-way per lookup), one 12-wave workgroup per CU for the 64 KiB of tables.
-#ifndef SLATE_NONE_REP
-#define SLATE_NONE_REP 0
-#endif
-constexpr int kNoneThreads = SLATE_NONE_REP ? 768 : 512;  // 12 waves, one workgroup per CU / 8 waves, two
-constexpr uint32_t kNoneWgPerCu = SLATE_NONE_REP ? 1 : 2;
+constexpr int kNoneThreads = 512;  // 8 waves; two workgroups per CU (LDS: 80 KiB each)
+constexpr uint32_t kNoneWgPerCu = 2;
 constexpr uint32_t kNoneSlots = 320;  // 5 register rows x 64 lanes of 16-byte chunks
 constexpr uint32_t kNoneMaxData = (kNoneSlots - 2) * 16;  // 5088 data bytes at most on this path
 constexpr uint32_t kNoneStage = 5120;  // per-wave LDS staging: input chunks 0 .. nout
-// SLATE_NONE_REP layout: advance tables for N = 16 (4 KiB) and N = 32 .. 1024 (kAdvN x 4 KiB), then
-// the replicated slicing tables T0, T1 (32 KiB each: entry i of copy c at 128 i + 4 c), all inside
-// the ds_read immediate-offset range
-constexpr uint32_t kRepAdv16 = 0, kRepAdv = 4096, kRepT0 = kRepAdv + kAdvN * 4096, kRepT1 = kRepT0 + 32768;
-constexpr uint32_t kNoneTabBytes = SLATE_NONE_REP ? kRepT1 + 32768 : kTab16Bytes + kAdvN * 4096;
-static_assert(!SLATE_NONE_REP || kRepT1 < 65536, "table bases in the ds_read immediate offset");
+constexpr uint32_t kNoneTabBytes = kTab16Bytes + kAdvN * 4096;
 constexpr uint32_t kNoneLds = kNoneTabBytes + (kNoneThreads / 64) * kNoneStage;
 // cache policy of the output / row stores (0 default, 2 nt, 16 sc1): nt, and nt block loads, measured
 // 2.04 vs 2.12 ms per 1 M blocks (profiles/round3/none/ab_policy.txt)
@@ -147,39 +136,10 @@ __device__ __forceinline__ Geo geo_of(const DecodeArgs& a, uint32_t b) {
 // The block's loads: register row q of lane l = input chunk 64q + l - pin, so that the chunk
 // holding the stored CRC's last byte (after the tail of the last output chunk) lands on slot 319;
 // nothing before chunk 0 (zeros).  They are staged slot by slot, so the stage holds input chunk c
-// at 16 (c + pin): every lane stores, no divergent branch (whose merge made the compiler's waitcnt
-// placement drain the next blocks' loads).
+// at 16 (c + pin): every lane stores, no divergent branch.
 struct Loads {
   v4u p[5];
 };
-#ifndef SLATE_NONE_ASMLD
-#define SLATE_NONE_ASMLD 1
-#endif
-#if SLATE_NONE_ASMLD
-// The loads are issued by inline asm, which the compiler's s_waitcnt placement does not see, and
-// waited for by an explicit vmcnt: its placement otherwise over-waits at the staging of one
-// register set and drains the other set's loads, so a wave had one block in flight, not two.
-// Each set's loads are issued at the end of its block (after that block's stores), so at a
-// set's staging the other set's five loads are always the newest vector-memory operations:
-// vmcnt(5) completes this set's loads and leaves the other's in flight.  The values pass through
-// the wait's asm as read-write operands, so nothing reads them before it.
-__device__ __forceinline__ void issue_loads(const Geo& g, uint32_t lane, Loads& L) {
-  const bool go = g.kind == 0;
-  const uint64_t base = uniform64(reinterpret_cast<uint64_t>(g.base));
-  const uint32_t n = __builtin_amdgcn_readfirstlane(go ? uint32_t(align16(uint64_t(g.sh) + g.clen + 4)) : 0u);
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
-  const i32x4 R = {int(uint32_t(base)), int(uint32_t(base >> 32) & 0xFFFFu), int(n), 0x00020000};
-#pragma unroll
-  for (uint32_t q = 0; q < 5; q++) {
-    const int32_t c = int32_t(64 * q + lane) - int32_t(g.pin);
-    const uint32_t off = c >= 0 ? uint32_t(16 * c) : kOOB;
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(L.p[q]) : "v"(off), "s"(R) : "memory");
-  }
-}
-__device__ __forceinline__ void wait_loads(Loads& L) {
-  asm volatile("s_waitcnt vmcnt(5)" : "+v"(L.p[0]), "+v"(L.p[1]), "+v"(L.p[2]), "+v"(L.p[3]), "+v"(L.p[4]));
-}
-#else
 __device__ __forceinline__ void issue_loads(const Geo& g, uint32_t lane, Loads& L) {
   const bool go = g.kind == 0;
   const __amdgpu_buffer_rsrc_t R = make_rsrc(g.base, go ? align16(uint64_t(g.sh) + g.clen + 4) : 0);
@@ -189,8 +149,6 @@ __device__ __forceinline__ void issue_loads(const Geo& g, uint32_t lane, Loads& 
     L.p[q] = __builtin_amdgcn_raw_buffer_load_b128(R, c >= 0 ? uint32_t(16 * c) : kOOB, 0, kNoneLdpol);
   }
 }
-__device__ __forceinline__ void wait_loads(Loads&) {}
-#endif
 
 // the 16 data bytes of output chunk j: stage bytes [sh + 16j, sh + 16j + 16), from three aligned
 // 8-byte reads (gfx950 serialises misaligned LDS accesses)
@@ -210,54 +168,6 @@ __device__ __forceinline__ v4u out_chunk(const uint8_t* stage, uint32_t sh, int3
   return r;
 }
 
-// advance tables: N = 32 << kS zero bytes, and N = 16 (the slicing-by-16 rows, or SLATE_NONE_REP's
-// table at kRepAdv16)
-template <uint32_t kOff>
-__device__ __forceinline__ uint32_t adv_at(const uint8_t* lds, uint32_t c) {
-  return xor3(lut<kOff>(lds, idx4<0>(c)), lut<kOff + 1024>(lds, idx4<1>(c)), lut<kOff + 2048>(lds, idx4<2>(c))) ^
-         lut<kOff + 3072>(lds, idx4<3>(c));
-}
-template <int kS>
-__device__ __forceinline__ uint32_t advN(const uint8_t* lds, uint32_t c) {
-  if constexpr (SLATE_NONE_REP) return adv_at<kRepAdv + 4096 * kS>(lds, c);
-  else return adv_tab<kS>(lds, c);
-}
-__device__ __forceinline__ uint32_t adv16n(const uint8_t* lds, uint32_t c) {
-  if constexpr (SLATE_NONE_REP) return adv_at<kRepAdv16>(lds, c);
-  else return adv16(lds, c);
-}
-// (byte K of x) << 7: the row of a replicated table entry (one SDWA shift)
-template <int K>
-__device__ __forceinline__ uint32_t idx7(uint32_t x) {
-  uint32_t r;
-  if constexpr (K == 0)
-    asm("v_lshlrev_b32_sdwa %0, 7, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(x));
-  else
-    asm("v_lshlrev_b32_sdwa %0, 7, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(x));
-  return r;
-}
-// two bytes (the low half of h) into the raw CRC register c, slicing-by-2 on the lane's table copies
-// (c4 = 4 x copy)
-__device__ __forceinline__ uint32_t rep2(uint32_t c, uint32_t h, uint32_t c4) {
-  const uint32_t x = c ^ h;
-  return xor3(c >> 16, *(lds_u32_t*)(kRepT1 + idx7<0>(x) + c4), *(lds_u32_t*)(kRepT0 + idx7<1>(x) + c4));
-}
-__device__ __forceinline__ uint32_t crc_chunk_rep(const v4u& v, uint32_t c4) {
-  uint32_t c = rep2(0u, v.x, c4);
-  c = rep2(c, v.x >> 16, c4);
-  c = rep2(c, v.y, c4);
-  c = rep2(c, v.y >> 16, c4);
-  c = rep2(c, v.z, c4);
-  c = rep2(c, v.z >> 16, c4);
-  c = rep2(c, v.w, c4);
-  return rep2(c, v.w >> 16, c4);
-}
-// the register advanced over t < 16 zero bytes, bytewise from a uniform value (broadcast reads)
-__device__ __forceinline__ uint32_t adv_small_rep(uint32_t c, uint32_t t) {
-  for (uint32_t i = 0; i < t; i++) c = (c >> 8) ^ *(lds_u32_t*)(kRepT0 + 128 * (c & 255u));
-  return c;
-}
-
 // One block: stage its chunks (LDS, the wave's 5 KiB at stage0), put the loads of the block two steps ahead into the same
 // registers, then decode it.  b / g / L advance to that block.
 __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* tab, uint8_t* stage0, uint32_t lane,
@@ -266,7 +176,6 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
   slate_block_meta m{};
   const Geo gc = g;
   const uint32_t sh = gc.sh, clen = gc.clen, nout = gc.nout, pad = gc.pad, pin = gc.pin;
-  wait_loads(L);
   if (gc.kind == 0) {
 #pragma unroll
     for (uint32_t q = 0; q < 5; q++) wr128(stage0 + 16 * (64 * q + lane), L.p[q], a.rt_zero);
@@ -275,7 +184,7 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
   const uint32_t bc = b;
   b += step;
   g = geo_of(a, b);
-  if (!SLATE_NONE_ASMLD) issue_loads(g, lane, L);
+  issue_loads(g, lane, L);
   if (gc.kind == 1) {
     m.status = SLATE_E_BLOCK_TOO_SMALL;
     if (lane == 0) a.meta[bc] = m;
@@ -303,9 +212,9 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
         c.w &= (last && r < 16) ? (r <= 12 ? 0u : (1u << (8 * (r - 12))) - 1u) : 0xFFFFFFFFu;
       }
       if (!(dbg_bits(a) & 1)) {  // (profiling variants only: bit 1 skips the CRC, 4 the rows, 8 the output stores)
-        const uint32_t k = SLATE_NONE_REP ? crc_chunk_rep(c, 4 * (lane & 31)) : crc_chunk0(lds, c);
+        const uint32_t k = crc_chunk0(lds, c);
         // Horner over the rows: row q's chunks lie 1024 (4 - q) bytes before row 4's
-        acc = (q == 0 ? 0u : advN<5>(lds, acc)) ^ (none ? 0u : k);
+        acc = (q == 0 ? 0u : adv_tab<5>(lds, acc)) ^ (none ? 0u : k);
       }
     }
     bool crc_ok = true;
@@ -317,26 +226,26 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
       // combined with wave-uniform addresses (broadcast reads)
       {
         uint32_t t = acc;
-        if (!(lane & 1)) t = adv16n(lds, acc);
+        if (!(lane & 1)) t = adv16(lds, acc);
         acc = t ^ row_shl<1>(acc);
         t = acc;
-        if (!(lane & 3)) t = advN<0>(lds, acc);
+        if (!(lane & 3)) t = adv_tab<0>(lds, acc);
         acc = t ^ row_shl<2>(acc);
         t = acc;
-        if (!(lane & 7)) t = advN<1>(lds, acc);
+        if (!(lane & 7)) t = adv_tab<1>(lds, acc);
         acc = t ^ row_shl<4>(acc);
         t = acc;
-        if (!(lane & 15)) t = advN<2>(lds, acc);
+        if (!(lane & 15)) t = adv_tab<2>(lds, acc);
         acc = t ^ row_shl<8>(acc);
       }
       const uint32_t h1 = __builtin_amdgcn_readlane(acc, 16), h2 = __builtin_amdgcn_readlane(acc, 32),
                      h3 = __builtin_amdgcn_readlane(acc, 48);
       uint32_t total = __builtin_amdgcn_readfirstlane(acc);
-      total = __builtin_amdgcn_readfirstlane(advN<3>(lds, total) ^ h1);  // rows 0-1
-      total = __builtin_amdgcn_readfirstlane(advN<3>(lds, total) ^ h2);  // rows 0-2
-      total = __builtin_amdgcn_readfirstlane(advN<3>(lds, total) ^ h3);  // rows 0-3
+      total = __builtin_amdgcn_readfirstlane(adv_tab<3>(lds, total) ^ h1);  // rows 0-1
+      total = __builtin_amdgcn_readfirstlane(adv_tab<3>(lds, total) ^ h2);  // rows 0-2
+      total = __builtin_amdgcn_readfirstlane(adv_tab<3>(lds, total) ^ h3);  // rows 0-3
       const uint32_t stored = __builtin_bswap32(st_u32(stage, sh + clen));
-      crc_ok = total == (SLATE_NONE_REP ? adv_small_rep(~stored, t) : adv_small(tab, ~stored, t));
+      crc_ok = total == adv_small(tab, ~stored, t);
     }
     if (!crc_ok) {
       m.status = SLATE_E_BLOCK_CHECKSUM;
@@ -419,19 +328,12 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
       if (lane == 0) a.meta[bc] = m;
     }
   }
-  if (SLATE_NONE_ASMLD) issue_loads(g, lane, L);
 }
 
 __global__ __launch_bounds__(kNoneThreads) void decode_none_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);  // slicing-by-16 (16 KiB) / SLATE_NONE_REP's tables
-  if constexpr (SLATE_NONE_REP) {
-    for (uint32_t i = threadIdx.x; i < 2 * 256 * 32; i += blockDim.x)
-      tab[kRepT0 / 4 + i] = g_crc16.t[i >> 13][(i >> 5) & 255u];
-    const uint32_t k16 = x8n(16);
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) tab[kRepAdv16 / 4 + i] = gf2_mulmod((i & 255u) << (8 * (i >> 8)), k16);
-    load_adv_tables(tab + kRepAdv / 4);
-  } else {
+  uint32_t* tab = reinterpret_cast<uint32_t*>(smem);  // slicing-by-16 (16 KiB)
+  {
     const uint32_t* src = &g_crc16.t[0][0];
     for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) tab[i] = src[i];
     load_adv_tables(tab + 4096);  // kAdvN x 4 x 256
@@ -453,7 +355,6 @@ __global__ __launch_bounds__(kNoneThreads) void decode_none_kernel(DecodeArgs a)
     if (gB.kind == 3) break;
     none_block(a, tab, stage, lane, 2 * waves_total, bB, gB, LB);
   }
-  if (SLATE_NONE_ASMLD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the last issued loads)
 }
 
 }  // namespace

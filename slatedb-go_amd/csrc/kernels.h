@@ -88,6 +88,9 @@ constexpr uint32_t kZsFseSeqs = 128;
 constexpr uint32_t kZfSeqSlot = 128;  // dwords of z.seq per block (16 x 8 or 128 x 4 bytes)
 constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4, kZfHuf = 8, kZfHuf4 = 16,
                    kZfSeq4 = 32;  // kZfHuf: Huffman literals; kZfSeq4: 4-byte sequence records
+// CodecZlib blocks through the same build phase (zlib_fast.hip): the literal bytes are at the start
+// of the block's output slot, not in the frame; want is the stream's Adler-32, checked in phase B
+constexpr uint32_t kZfOutLit = 64, kZfAdler = 128;
 struct ZsFastRec {
   uint32_t lit;       // frame offset of the raw literals, or the RLE literal byte
   uint32_t nlit;      // literal bytes
@@ -137,6 +140,13 @@ hipError_t launch_lz4_plan(hipStream_t st, const uint8_t* in, const uint64_t* in
 hipError_t launch_zstd_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n, uint64_t* out_sz,
                                  uint64_t* row_sz, uint32_t* list, uint32_t* count);
 hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
+// CodecZlib fast path (zlib_fast.hip): plan sizes lane per block (the rest appended to list for the
+// wave plan); decode: phase Z (lane per block: literals + sequences), then zstd_fast.hip's phases A2
+// and B (launch_zlib_fast), hand-backs to z.list for the exact path.
+hipError_t launch_zlib_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n,
+                                 uint64_t* out_sz, uint64_t* row_sz, uint32_t* list, uint32_t* count, int num_cus);
+hipError_t launch_zlib_fast_parse(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
+hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
 // The rows of a decoded batch, densely in block order, written to `dense` (device memory or
 // page-locked host memory mapped for the device): block i's min(n_rows, capacity) rows when it
 // decoded (status OK), none otherwise; dense_off (n+1 u64) gets the exclusive scan of those

@@ -239,49 +239,6 @@ __device__ __forceinline__ uint32_t pick5(const Win5& w, uint32_t j) {
   return (j & 4) ? w.y4 : r;
 }
 
-// 32-byte variants (the lane-per-block decoder's 32-byte step): ring bytes [p, p+32), and the nine
-// dwords that put them at byte b of a 36-byte window whose first dword keeps `head` below byte b
-struct V8 {
-  uint32_t w[8];
-};
-__device__ __forceinline__ V8 ring_rd32(const uint8_t* ring, uint32_t p, uint32_t m8 = kOR - 8) {
-  const uint32_t a = p & m8;
-  const v2u A = rd64(ring, a, m8), B = rd64(ring, a + 8, m8), C = rd64(ring, a + 16, m8), D = rd64(ring, a + 24, m8),
-            E = rd64(ring, a + 32, m8);
-  const bool q = (p & 4) != 0;
-  const uint32_t e[9] = {q ? A.y : A.x, q ? B.x : A.y, q ? B.y : B.x, q ? C.x : B.y, q ? C.y : C.x,
-                         q ? D.x : C.y, q ? D.y : D.x, q ? E.x : D.y, q ? E.y : E.x};
-  const uint32_t b = p & 3;
-  V8 r;
-#pragma unroll
-  for (int k = 0; k < 8; k++) r.w[k] = alignb(e[k + 1], e[k], b);
-  return r;
-}
-struct Win9 {
-  uint32_t y[9];
-};
-__device__ __forceinline__ Win9 shift_in9(const V8& v, uint32_t head, uint32_t b) {
-  const uint32_t sel = 0x07060504u - b * 0x01010101u;
-  const uint32_t keep = (1u << (8 * b)) - 1u;
-  Win9 w;
-  w.y[0] = (head & keep) | (__builtin_amdgcn_perm(v.w[0], head, sel) & ~keep);
-#pragma unroll
-  for (int k = 1; k < 8; k++) w.y[k] = __builtin_amdgcn_perm(v.w[k], v.w[k - 1], sel);
-  w.y[8] = __builtin_amdgcn_perm(v.w[7], v.w[7], sel);
-  return w;
-}
-__device__ __forceinline__ void store_win9(uint8_t* ring, uint32_t a4, const Win9& w) {
-#pragma unroll
-  for (int k = 0; k < 9; k++) wr32(ring, a4 + 4 * k, w.y[k]);
-}
-// dword j (0..8) of the window, as bit-tested selects
-__device__ __forceinline__ uint32_t pick9(const Win9& w, uint32_t j) {
-  const uint32_t a = (j & 1) ? w.y[1] : w.y[0], b = (j & 1) ? w.y[3] : w.y[2];
-  const uint32_t c = (j & 1) ? w.y[5] : w.y[4], d = (j & 1) ? w.y[7] : w.y[6];
-  const uint32_t lo = (j & 2) ? b : a, hi = (j & 2) ? d : c;
-  const uint32_t r = (j & 4) ? hi : lo;
-  return (j & 8) ? w.y[8] : r;
-}
 
 // Cache policy (gfx950 CPol bits): 0 = default (allocates in L2: a lane reads its block's 128-byte
 // lines 16 bytes at a time, so the line must stay for the next 7 accesses), 16 = sc1 (bypasses the

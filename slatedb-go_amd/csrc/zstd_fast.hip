@@ -843,7 +843,7 @@ __device__ __forceinline__ ZfRaw zf_load(const DecodeArgs& a, const ZsFastArgs& 
 // 4-byte records (kZfSeq4) sequences 2i and 2i + 1 on lane i (slots A and B); a slot past the
 // block's sequences holds zeros.
 struct ZfBlock {
-  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs, s4;
+  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs, s4, outlit, adler, want;
   const uint8_t* gin;
   uint8_t* gout;
   uint32_t llA, mlA, offA, llB, mlB, offB;
@@ -867,6 +867,9 @@ __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r
   k.huf = (fl & kZfHuf) ? ((fl & kZfHuf4) ? 4u : 1u) : 0u;
   k.cs = __builtin_amdgcn_readfirstlane(r.rec.cs);
   k.s4 = (fl & kZfSeq4) ? 1u : 0u;
+  k.outlit = fl & kZfOutLit;  // (CodecZlib: the literals are at the start of the output slot)
+  k.adler = fl & kZfAdler;
+  k.want = __builtin_amdgcn_readfirstlane(r.rec.want);
   if (!k.fast) return k;
   if (k.s4) {
     const bool va = 2 * lane < k.nseq, vb = 2 * lane + 1 < k.nseq;
@@ -889,7 +892,9 @@ __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r
 
 // Build one block in wout from its sequences (lane i: sequence i) and its literals at wout[lb...]
 // (or the RLE byte), write it back, then block.Decode's checks and rows (phases B and B').
-__device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur, uint8_t* wout, uint32_t lb,
+// CodecZlib blocks (kZfAdler) are checked against the stream's Adler-32 first: false = mismatch,
+// nothing written (the caller hands the block to the exact path, which reports it).
+__device__ __forceinline__ bool zf_build(const DecodeArgs& a, const ZfBlock& cur, uint8_t* wout, uint32_t lb,
                                          uint32_t lane, uint32_t dbg) {
   const uint32_t lit = cur.lit;
   slate_block_meta m{};
@@ -979,12 +984,18 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
   // (offset >= length) a dword per lane, the edge dwords merged with the bytes around the
   // match; overlapping ones a byte per lane.
   const uint32_t offA = cur.offA, offB = cur.offB, s4 = cur.s4;
-  for (uint32_t i = 0; i < nseq && !(dbg & (1u << 21)); i++) {
-    const uint32_t li = i >> s4;
-    const bool hB = s4 && (i & 1);  // (wave-uniform)
-    const uint32_t M = __builtin_amdgcn_readlane(hB ? mlB : mlA, li), O = __builtin_amdgcn_readlane(hB ? offB : offA, li);
-    const uint32_t mp = __builtin_amdgcn_readlane(hB ? dposB + llB : dposA + llA, li);
-    if (O >= M) {
+  // (lane li holds sequence li, or with 4-byte records sequences 2li and 2li + 1: slots A and B)
+  const uint32_t pkA = cur.mlA | (offA << 16), pkB = cur.mlB | (offB << 16);  // ml < 2^16, offset <= 4112
+  const uint32_t mpA = dposA + llA, mpB = dposB + llB;
+  auto match = [&](uint32_t pk, uint32_t mp) {
+    const uint32_t M = pk & 0xFFFFu, O = pk >> 16;
+    if (M <= kWave) {
+      // most matches: one byte per lane (an overlapping one repeats every O bytes, all before mp)
+      if (lane < M) {
+        const uint32_t t = O >= M ? lane : lane % O;
+        wout[mp + lane] = wout[mp - O + t];
+      }
+    } else if (O >= M) {
       const uint32_t me = mp + M;
       const uint32_t lo_keep = (1u << (8 * (mp & 3))) - 1u, hi_keep = (me & 3) ? ~((1u << (8 * (me & 3))) - 1u) : 0u;
       for (uint32_t w = (mp & ~3u) + 4 * lane; w < me; w += 4 * kWave) {
@@ -997,8 +1008,34 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
       for (uint32_t j = lane; j < M; j += kWave) wout[mp + j] = wout[mp - O + (j % O)];
     }
     zs_sync();
+  };
+  const uint32_t nl = (dbg & (1u << 21)) ? 0u : (s4 ? (nseq + 1) / 2 : nseq);
+  for (uint32_t li = 0; li < nl; li++) {
+    match(__builtin_amdgcn_readlane(pkA, li), __builtin_amdgcn_readlane(mpA, li));
+    if (s4 && 2 * li + 1 < nseq) match(__builtin_amdgcn_readlane(pkB, li), __builtin_amdgcn_readlane(mpB, li));
   }
   const uint32_t n = cur.produced;
+  if (cur.adler) {
+    // Adler-32 (RFC 1950 8.2) of wout[0, n): a = 1 + sum x_i, b = n + sum (n - i) x_i, mod 65521
+    // (the sums stay below 2^32 for n <= 4112); a dword per lane per step
+    uint32_t sa = 0, sb = 0;
+    for (uint32_t j = lane; 4 * j < n; j += kWave) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(wout + 4 * j);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t i = 4 * j + q;
+        const uint32_t x = i < n ? (w >> (8 * q)) & 0xFFu : 0u;
+        sa += x;
+        sb += (n - i) * x;
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      sa += __shfl_xor(sa, o, 64);
+      sb += __shfl_xor(sb, o, 64);
+    }
+    const uint32_t ad = (((n + sb) % 65521u) << 16) | ((1u + sa) % 65521u);
+    if (__builtin_amdgcn_readfirstlane(ad) != cur.want) return false;
+  }
   {
     uint8_t* gout = cur.gout;
     const uint32_t oc = (dbg & (1u << 27)) ? 0u : (n + 15) / 16;
@@ -1007,6 +1044,7 @@ __device__ __forceinline__ void zf_build(const DecodeArgs& a, const ZfBlock& cur
   }
   if (dbg & (1u << 20)) write_meta(&a.meta[cur.b], m, int(lane));
   else block_finish(a, cur.b, wout, n, int(lane), m);
+  return true;
 }
 
 // One wave per block, the next block's record and sequences loaded while this one is built.  The frame is staged in the output buffer at the 16-byte phase of its address, placed
@@ -1030,20 +1068,26 @@ __global__ __launch_bounds__(kZfBuildThreads, SLATE_ZF_BUILD_WG) void zs_fast_bu
     nr = zf_load(a, z, b + waves, lane);  // in flight while this block is built
     const ZfBlock cur = zf_decode(a, cr, lane);
     if (!cur.fast || cur.huf) continue;  // (Huffman literals: phase B')
-    const uint32_t lbase = cur.cap - cur.nlit, lit = cur.lit, shift = cur.shift;
+    // CodecZlib (kZfOutLit): the literal bytes at the start of the (16-aligned) output slot take
+    // the frame's place: shift 0, literals from byte 0, nlit bytes
+    const uint32_t lbase = cur.cap - cur.nlit, lit = cur.outlit ? 0u : cur.lit, shift = cur.outlit ? 0u : cur.shift;
+    const uint32_t slen = cur.outlit ? cur.nlit : cur.len;
     // frame byte 0 at wout[F], F = 16-aligned base + shift, literals at lb = F + lit >= lbase
     uint32_t base16 = 16;
     if (!cur.rle && lbase > lit + shift + 16) base16 = (lbase - lit - shift + 15) & ~15u;
     const uint32_t F = base16 + shift, lb = F + lit;
     {
-      const uint32_t chunks = (dbg & (1u << 28)) ? 0u : (shift + cur.len + 15) / 16;
-      const uint4* src = reinterpret_cast<const uint4*>(cur.gin - shift);
+      const uint32_t chunks = (dbg & (1u << 28)) ? 0u : (shift + slen + 15) / 16;
+      const uint4* src = reinterpret_cast<const uint4*>(cur.outlit ? cur.gout : cur.gin - shift);
       uint4* dst = reinterpret_cast<uint4*>(wout + base16);
       for (uint32_t c = lane; c < chunks; c += kWave) dst[c] = src[c];
     }
     __builtin_amdgcn_s_waitcnt(0);
     zs_sync();
-    zf_build(a, cur, wout, lb, lane, dbg);  // (the block's CRC32 held: phase A2)
+    if (!zf_build(a, cur, wout, lb, lane, dbg) && lane == 0) {  // (the block's CRC32 held: phase A2)
+      z.rec[cur.b].info = 0;
+      z.list[atomicAdd(z.count, 1u)] = cur.b;  // the Adler-32 failed: the exact path reports it
+    }
   }
 }
 
@@ -1141,7 +1185,7 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
       continue;
     }
     zs_sync();
-    zf_build(a, cur, wout, lbase, lane, 0);
+    (void)zf_build(a, cur, wout, lbase, lane, 0);  // (Zstd frames only: no Adler-32)
   }
 }
 
@@ -1354,6 +1398,24 @@ size_t zstd_fast_parse_lds() { return ((sizeof(ZfShared) + 15) & ~size_t(15)) + 
 // only those), B' keeps a few lanes of few waves busy for about a millisecond per 1 M configs[4]
 // blocks, and B fills the chip.  On the caller's side stream (DecodeArgs::side, owned by its
 // context), forked after phase A2 and joined before phase C.
+// CodecZlib: phase Z (zlib_fast.hip) in place of A / A', then A2 and B (no Huffman-literal or
+// XXH64 phase: B checks the Adler-32)
+hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
+  if (a.n == 0) return hipGetLastError();
+  hipError_t e = launch_zlib_fast_parse(st, a, z, num_cus);
+  if (e != hipSuccess) return e;
+  const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
+  const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
+  zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
+  const size_t lds_b = size_t(kZfBuildThreads / 64) * kZfOutLds;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
+  if (attr != hipSuccess) return attr;
+  const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG);
+  zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
+  return hipGetLastError();
+}
+
 hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
   if (a.n == 0) return hipGetLastError();
   const size_t lds_a = zstd_fast_parse_lds();

@@ -175,3 +175,36 @@ def test_index_seek(ctx, codec):
     got = ctx.index_seek(index, keys)
     want = [ob.index_seek(first_keys, k) for k in keys]
     assert got.tolist() == want
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_point_reads_one_query_per_call(ctx, seed):
+    """One query per call (the point read: slate_block_seek with n = 1 takes the staged,
+    wave-cooperative form, seek.hip seek_one_wave), over blocks with corrupted rows: every result
+    and every warning, in order, as the oracle's NewIteratorAtKey."""
+    rng = random.Random(100 + seed)
+    blocks = []
+    for _ in range(30):
+        kvs = bg.random_kvs(rng, rng.randint(1, 120), klen=(1, 12), vlen=(0, 30), alphabet=rng.choice([3, 256]))
+        kvs = [(k, v) for k, v in kvs if k]
+        if not kvs:
+            continue
+        corrupt = sorted(rng.sample(range(len(kvs)), rng.randint(0, min(5, len(kvs))))) if rng.random() < 0.5 else []
+        blocks.append(_encode(kvs, rng.choice([256, 4096]), corrupt, partial=True))
+    out, out_off, meta = _layout(blocks)
+    cap = 8
+    for b, (_, data, offs) in enumerate(blocks):
+        for _ in range(8):
+            key = (rng.randbytes(rng.randint(0, 12)) if rng.random() < 0.5 else
+                   bytes(rng.choice(b"abc") for _ in range(rng.randint(0, 6))))
+            a, e = int(out_off[b]), int(out_off[b + 1])
+            one_off = np.array([0, e - a], np.uint64)  # the block alone: a point read's few KiB
+            got_w, warns = ctx.block_seek_warn(out[a:e + 16].copy(), one_off, meta[b:b + 1].copy(), [0], [key],
+                                               warn_cap=cap)
+            (st, start, fi, fl, nw), ow = ob.block_seek_warnings(data, offs, key, cap)
+            g = got_w[0]
+            assert (int(g["status"]), int(g["n_warn"])) == (st, nw), (b, key, g, st, nw)
+            if st == 0:
+                assert (int(g["start"]), int(g["first_idx"]), int(g["first_len"])) == (start, fi, fl), (b, key)
+            gw = [(int(w["kind"]), int(w["err"]), int(w["a"]), int(w["b"])) for w in warns[0][: min(nw, cap)]]
+            assert gw == ow, (b, key, gw, ow)

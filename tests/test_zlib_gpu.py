@@ -107,3 +107,49 @@ def test_damaged_zlib_blocks(ctx):
     meta = _compare(ctx, blocks, misalign=1)
     st = set(int(x) for x in meta["status"])
     assert {0, 53, 54} <= st, st
+
+
+@pytest.mark.parametrize("misalign", [0, 3, 9, 15])
+def test_kv100_go_zlib_fast_path(ctx, misalign):
+    """configs[1]'s block shape (4 KiB blocks of 100-byte V-half KVs) as Go's compress/zlib writes
+    it (level 6, then the empty final stored block; tools/benchgen.c go_zlib6): every block takes
+    the lane-per-block fast path (zlib_fast.hip + the build phase; none handed back), the plan's
+    lane-per-block sizes included, bit-exact against the oracle at every input alignment."""
+    import slatecodec as sc
+    from tools import workload as wl
+    dec, doff = wl.decoded_blocks(300, seed=misalign + 1, half=True)
+    blob, off = wl.encode_blocks(ob.ZLIB, dec, doff, threads=4)
+    blocks = [blob[int(off[i]):int(off[i + 1])].tobytes() for i in range(len(off) - 1)]
+    ctx.handbacks(reset=True)
+    meta = _compare(ctx, blocks, misalign=misalign)
+    assert (meta["status"] == 0).all()
+    assert ctx.handbacks() == 0
+    del sc
+
+
+def test_zlib_fast_path_shapes(ctx):
+    """Streams the fast path takes (dynamic and fixed Huffman blocks, several deflate blocks per
+    stream, an empty stored block) and ones it hands back (stored blocks with data, a single
+    distance code, corrupted Adler-32 under a valid block CRC): every block identical to the
+    oracle, statuses included."""
+    rng = random.Random(21)
+    blocks = []
+    for dec in _sst_plain(rng, 2400, 4096):
+        kind = rng.randrange(6)
+        if kind == 0:
+            f = _z(dec, 6, zlib.Z_FIXED)
+        elif kind == 1:  # several deflate blocks: a full flush in the middle
+            co = zlib.compressobj(6)
+            h = len(dec) // 2
+            f = co.compress(dec[:h]) + co.flush(zlib.Z_FULL_FLUSH) + co.compress(dec[h:]) + co.flush()
+        elif kind == 2:
+            f = _z(dec, 0)  # stored blocks with data: handed back
+        elif kind == 3:  # a wrong Adler-32 (valid block CRC): the exact path reports it
+            f = bytearray(_z(dec, 6))
+            f[-1] ^= 0x40
+            f = bytes(f)
+        else:
+            f = _z(dec, rng.choice([1, 6, 9]))
+        blocks.append(_crc(f))
+    meta = _compare(ctx, blocks, misalign=rng.randrange(16))
+    assert set(int(x) for x in meta["status"]) <= {0, 52}, set(int(x) for x in meta["status"])

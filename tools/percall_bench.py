@@ -9,7 +9,7 @@ figures under "per_call" and "configs0"):
     over 64 blocks per call, us per block;
   * BASELINE configs[0]: one SST of 64 x 4 KiB CodecNone blocks (100 B KV) encoded and decoded,
     us per SST, by the oracle on one thread and by the library.
-usage: python tools/percall_bench.py [--calls N]   (prints one JSON object)"""
+usage: python tools/percall_bench.py [--calls N] [--dump PATH: write the C harness's input and stop]"""
 import json
 import os
 import sys
@@ -66,6 +66,9 @@ def per_call(ctx, sc, ob, wl, calls=400):
     def cpu_seek():
         ob.block_seek(data0, offs0, key)
 
+    if "--dump" in sys.argv:  # the C harness's input only (for a rocprofv3 run of tools/build/percall)
+        write_harness_input(sys.argv[sys.argv.index("--dump") + 1], blocks, key)
+        return {"dumped": sys.argv[sys.argv.index("--dump") + 1]}
     res["slate_block_seek_us"] = round(_us(gpu_seek, calls), 1)
     res["oracle_block_seek_us_1thread"] = round(_us(cpu_seek, calls), 1)
     # read-ahead: 64 blocks per call
@@ -82,21 +85,27 @@ def per_call(ctx, sc, ob, wl, calls=400):
     return res
 
 
+def write_harness_input(path, blocks, key):
+    """tools/build/percall's input: the blocks, then the seek key."""
+    import struct
+    with open(path, "wb") as f:
+        f.write(struct.pack("<I", len(blocks)))
+        for b in blocks:
+            f.write(struct.pack("<I", len(b)) + b)
+        f.write(struct.pack("<I", len(key)) + bytes(key))
+
+
 def c_harness(blocks, key, calls):
     """The same blocks and key through tools/build/percall (C, as a cgo shim calls the library),
     slate_block_decode / slate_block_seek against the oracle's or_block_decode / or_block_seek."""
-    import struct
     import subprocess
     import tempfile
     exe = os.path.join(REPO, "tools", "build", "percall")
     if not os.path.exists(exe):
         return {"skipped": "tools/build/percall not built (make -C tools)"}
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
-        f.write(struct.pack("<I", len(blocks)))
-        for b in blocks:
-            f.write(struct.pack("<I", len(b)) + b)
-        f.write(struct.pack("<I", len(key)) + bytes(key))
         path = f.name
+    write_harness_input(path, blocks, key)
     try:
         r = subprocess.run([exe, path, str(max(calls, 200) * 5)], capture_output=True, text=True, timeout=120)
     finally:
@@ -159,7 +168,11 @@ def main():
     from tools import workload as wl
     calls = int(sys.argv[sys.argv.index("--calls") + 1]) if "--calls" in sys.argv else 400
     ctx = sc.Context(0)
-    print(json.dumps({"per_call": per_call(ctx, sc, ob, wl, calls), "configs0": configs0(ctx, sc, ob)}))
+    pc = per_call(ctx, sc, ob, wl, calls)
+    if "--dump" in sys.argv:
+        print(json.dumps(pc))
+        return
+    print(json.dumps({"per_call": pc, "configs0": configs0(ctx, sc, ob)}))
 
 
 if __name__ == "__main__":

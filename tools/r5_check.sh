@@ -3,7 +3,7 @@
 # same-box A/B of decode library builds.  env: TESTS, LEGS ("kv100_zstd:262144 kv100_zlib:65536"),
 # VLIB + VTESTS (tests on a variant library), LIBS, ROUNDS, TAG, PRE (a probe script run first),
 # DESELECT (pytest --deselect options), NLIBS (libraries for a CodecNone A/B), PERCALL=1,
-# ENCTRACE=1, VLIB2 + VTESTS2
+# ENCTRACE=1, VLIB2 + VTESTS2, PROF=1 (tools/r5_prof.sh), COPY=1, RATIO=1
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 OUT=gpurun_out/${TAG:-r5}
@@ -47,5 +47,17 @@ if [ -n "$ENCTRACE" ]; then  # configs[2] host-input split, with the builder's h
     SLATE_HOST_TRACE=1 timeout -k 10 300 python -u tools/bench_encode.py --codec $c --steps 3 > $OUT/enc_$c.json 2> $OUT/enc_$c.trace || { echo ENC_FAILED; tail -20 $OUT/enc_$c.trace; exit 1; }
     python3 -c "import json;d=json.load(open('$OUT/enc_$c.json'));print('$c', d['host_input'], d['device_input'])"
   done
+fi
+
+if [ -n "$PROF" ]; then  # kernel traces of the kv100 legs and the per-call harness
+  TAG=${TAG:-r5}/prof tools/r5_prof.sh || exit 1
+fi
+if [ -n "$COPY" ]; then  # the streaming-copy shapes (bench.py measured_copy_gbps)
+  timeout -k 10 300 python3 -c "import json,torch,bench;print(json.dumps(bench.measured_copy_gbps(torch.device('cuda',0))))" > $OUT/copy.json 2> $OUT/copy.err || { echo COPY_FAILED; tail -20 $OUT/copy.err; exit 1; }
+  cat $OUT/copy.json
+fi
+if [ -n "$RATIO" ]; then  # the codecs' compression ratio against the libraries
+  timeout -k 10 600 python3 tools/codec_ratio.py > $OUT/ratio.json 2> $OUT/ratio.err || { echo RATIO_FAILED; tail -20 $OUT/ratio.err; exit 1; }
+  tail -3 $OUT/ratio.json
 fi
 

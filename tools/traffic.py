@@ -32,11 +32,16 @@ def main():
                         "zs_fast_sum_kernel", "decode_list_kernel", "decode_large_kernel"]}[codec]
     kernel = "+".join(kernels)
     fetch_kib = write_kib = 0.0
+    by_kernel = {}
     for k in kernels:
         f = per_dispatch(os.path.join(out, "fetch", "run_counter_collection.csv"), "FETCH_SIZE", k)
         w = per_dispatch(os.path.join(out, "write", "run_counter_collection.csv"), "WRITE_SIZE", k)
-        fetch_kib += max(f.values()) if f else 0.0  # the launches are identical; the max skips any partial one
-        write_kib += max(w.values()) if w else 0.0
+        fk = max(f.values()) if f else 0.0  # the launches are identical; the max skips any partial one
+        wk = max(w.values()) if w else 0.0
+        fetch_kib += fk
+        write_kib += wk
+        if fk or wk:
+            by_kernel[k] = {"fetch_size_kib": fk, "write_size_kib": wk}
     bench = None
     log = os.path.join(out, "trace.log")
     for line in open(log):
@@ -53,7 +58,8 @@ def main():
            "lib_sha256": sha, "commit": commit or os.environ.get("SLATE_COMMIT", ""),
            "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
            "hbm_bytes_per_launch": int((2 * fetch_kib + write_kib) * 1024),
-           "note": "2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md)"}
+           "note": "2 x FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md)",
+           "by_kernel": by_kernel}
     # SQ counters per launch of the same kernel and build, and per decoded block
     sq = {}
     for grp in ("sq1", "sq2"):
