@@ -1667,9 +1667,19 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   };
   // the index flatbuffer (host work) is built beside the last blocks' D2H and the filter's encode:
   // the final flush starts it once every index entry is queued (b->meta_* are not touched after)
-  std::future<std::vector<uint8_t>> fb_job;
+  // (CodecNone: the thread also takes the payload's CRC, which then needs no GPU round trip)
+  struct IndexFb {
+    std::vector<uint8_t> fb;
+    uint32_t crc = 0;
+  };
+  std::future<IndexFb> fb_job;
   const std::function<void()> start_index = [&] {
-    fb_job = std::async(std::launch::async, [b] { return fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off); });
+    fb_job = std::async(std::launch::async, [b] {
+      IndexFb r;
+      r.fb = fb_encode_index(b->meta_off, b->meta_keys, b->meta_key_off);
+      if (b->cfg.codec == SLATE_CODEC_NONE) r.crc = crc32_host16(r.fb.data(), r.fb.size());
+      return r;
+    });
   };
   int st = builder_flush(b, true, side_filter ? &start_filter : nullptr, &start_index);
   if (side_filter && !fjob.valid() && !st) start_filter(b->n_hashes);  // nothing was pending
@@ -1763,7 +1773,8 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
   std::vector<uint8_t> index;
   double t_fb = 0.0;
   {
-    std::vector<uint8_t> fb = fb_job.get();
+    IndexFb job = fb_job.get();
+    std::vector<uint8_t>& fb = job.fb;
     t_fb = host_trace() ? now_ms() : 0.0;
     if (b->cfg.codec == SLATE_CODEC_SNAPPY) {
       // encoded and CRC'd on the device: the payload comes back once, with its CRC
@@ -1772,9 +1783,11 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
       st = ctx_h2d(ctx, ctx->e_i.p, fb.data(), fb.size(), ctx->stream);
       if (!st) st = ctx_snappy_encode_crc_device(ctx, ctx->e_i.as<uint8_t>(), fb.size(), index);
       if (st) { delete t; return st; }
+    } else if (b->cfg.codec == SLATE_CODEC_NONE) {
+      index.swap(fb);  // (the payload as built: no copy; its CRC from the index thread)
+      put_be32(index, job.crc);
     } else {
-      if (b->cfg.codec == SLATE_CODEC_NONE) index.swap(fb);  // (the payload as built: no copy)
-      else st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
+      st = codec_encode_host(ctx, b->cfg.codec, fb.data(), fb.size(), index);
       if (st) { delete t; return st; }
       uint32_t icrc = 0;
       st = ctx_crc32_host_buffer(ctx, index.data(), index.size(), &icrc);

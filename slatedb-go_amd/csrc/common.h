@@ -78,16 +78,17 @@ __host__ __device__ constexpr uint32_t x8n(uint64_t n) {
   return r;
 }
 
-// The block CRC splits a stripe of 64 lanes x kCrcSeg bytes, end-aligned to the
+// The block CRC splits a stripe of 64 lanes x Seg bytes, end-aligned to the
 // message: lane l's partial R(0, seg_l) is shifted by the bytes after it.
 constexpr uint32_t kCrcSeg = 64;
 constexpr uint32_t kCrcStripe = kWave * kCrcSeg;  // 4096
-struct CrcShift {
-  uint32_t lane[kWave];  // x^(8 * kCrcSeg * (63 - l))
-  uint32_t stripe;       // x^(8 * kCrcStripe)
-  constexpr CrcShift() : lane{}, stripe(0) {
+template <uint32_t Seg>
+struct CrcShiftT {
+  uint32_t lane[kWave];  // x^(8 * Seg * (63 - l))
+  uint32_t stripe;       // x^(8 * 64 * Seg)
+  constexpr CrcShiftT() : lane{}, stripe(0) {
     uint32_t seg = 0x80000000u;
-    for (int k = 0; k < 8 * int(kCrcSeg); k++) seg = (seg & 1) ? (seg >> 1) ^ kCrcPoly : seg >> 1;
+    for (int k = 0; k < 8 * int(Seg); k++) seg = (seg & 1) ? (seg >> 1) ^ kCrcPoly : seg >> 1;
     uint32_t acc = 0x80000000u;
     for (int l = int(kWave) - 1; l >= 0; l--) {
       lane[l] = acc;
@@ -96,8 +97,10 @@ struct CrcShift {
     stripe = acc;
   }
 };
+using CrcShift = CrcShiftT<kCrcSeg>;
 
 // Host CRC (framing of small host-side pieces such as flatbuffer info).
 uint32_t crc32_host(const uint8_t* p, size_t n);
+uint32_t crc32_host16(const uint8_t* p, size_t n);  // slicing-by-16 (large host buffers)
 
 }  // namespace slate

@@ -1702,9 +1702,8 @@ __global__ __launch_bounds__(256) void blocks_to_host_kernel(const uint8_t* __re
 // (a.in), decoded by the large-kernel wave with its LDS budget (the host checks the block fits),
 // and the decoded bytes go to page-locked host memory (host_out) the same way.  a.meta may be
 // host memory too.  Replaces the generic path's plan kernel, scans, transfers and two waits.
-__global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint8_t* __restrict__ host_in,
-                                                        uint64_t in_len, uint64_t out_sz, uint64_t row_sz,
-                                                        uint8_t* __restrict__ host_out) {
+__device__ __forceinline__ void decode_one(DecodeArgs a, const uint8_t* __restrict__ host_in, uint64_t in_len,
+                                           uint64_t out_sz, uint64_t row_sz, uint8_t* __restrict__ host_out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint64_t offs[6];
   const int lane = threadIdx.x;
@@ -1736,6 +1735,11 @@ __global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint
   for (uint64_t k = lane; k < out_sz / 16; k += 64)
     reinterpret_cast<uint4*>(host_out)[k] = reinterpret_cast<const uint4*>(a.out)[k];
 }
+__global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint8_t* __restrict__ host_in,
+                                                        uint64_t in_len, uint64_t out_sz, uint64_t row_sz,
+                                                        uint8_t* __restrict__ host_out) {
+  decode_one(a, host_in, in_len, out_sz, row_sz, host_out);
+}
 
 // One CodecSnappy block for a single-block call (slate_block_decode: sstable.Iterator's one block per
 // nextBlockIter, a point read), by a whole 1024-thread workgroup instead of one wave walking the
@@ -1743,8 +1747,9 @@ __global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint
 // passes over the block staged in LDS:
 //   1. every payload position p: the tag that would start there -- the next tag's position
 //      (END at the payload end, ERR for a tag running past it) and its decoded length;
-//   2. pointer doubling to 4-tag hops, one thread walks the hops from the header (~43 steps), and
-//      the hops are expanded in parallel: the chain's tags with their output offsets;
+//   2. pointer doubling to 4- and 16-tag hops, one thread walks the 16-tag hops from the header
+//      (~11 steps), their 4-tag sub-hops are found in parallel, and those are expanded in parallel:
+//      the chain's tags with their output offsets;
 //   3. every output byte finds its tag (binary search): a literal byte takes its value, a copied
 //      byte points at the byte it repeats; pointer jumping until every byte holds a value;
 // with the CRC32 on wave 0 beside pass 1.  Any check the serial decoder would fail (a tag past the
@@ -1753,8 +1758,9 @@ __global__ __launch_bounds__(64) void decode_one_kernel(DecodeArgs a, const uint
 constexpr uint32_t kOneParIn = 6144, kOneParOut = 12288, kOneParThreads = 1024;
 constexpr uint32_t kOneParTags = kOneParIn / 2;
 constexpr uint16_t kPEnd = 0xFFFE, kPErr = 0xFFFF;
-constexpr size_t kOneParLds = kTabBytes + (kOneParIn + 32) + (kOneParOut + 16) + 6 * 2 * (kOneParIn + 16) +
-                              4 * kOneParTags + 4 * (kOneParTags / 4 + 16) + 64;
+constexpr size_t kOneParLds = kTabBytes + (kOneParIn + 32) + (kOneParOut + 16) + 8 * 2 * (kOneParIn + 16) +
+                              4 * kOneParTags + 4 * (kOneParTags / 4 + 16) + 4 * (kOneParTags / 16 + 16) + 64;
+static_assert(kOneParLds <= 160 * 1024, "decode_one_par_kernel's LDS");
 
 __device__ __forceinline__ void snappy_tag_at(const uint8_t* in, uint32_t p, uint32_t clen, uint32_t* np, uint32_t* dl,
                                               uint32_t* hl, uint32_t* off, bool* lit) {
@@ -1789,9 +1795,11 @@ __device__ __forceinline__ void snappy_tag_at(const uint8_t* in, uint32_t p, uin
   *lit = t == 0;
 }
 
-__global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeArgs a, const uint8_t* __restrict__ host_in,
-                                                                        uint64_t in_len, uint64_t out_sz, uint64_t row_sz,
-                                                                        uint8_t* __restrict__ host_out) {
+__device__ __forceinline__ void decode_one_par(DecodeArgs a, const uint8_t* __restrict__ host_in, uint64_t in_len,
+                                               uint64_t out_sz, uint64_t row_sz, uint8_t* __restrict__ host_out,
+                                               uint32_t stop) {
+  // stop (profiling builds, SLATE_ONE_STOP): end after phase 1 staging, 2 pass 1, 3 the hop walk,
+  // 4 the expansion, 5 pass 3, 6 before block_finish and the copy-out (the time per phase)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint64_t offs[6];
   __shared__ uint32_t sh_crc, sh_bad, sh_ntags, sh_nhops, sh_more;
@@ -1806,9 +1814,14 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
   uint16_t* s2 = j2 + (kOneParIn + 16);
   uint16_t* j4 = s2 + (kOneParIn + 16);
   uint16_t* s4 = j4 + (kOneParIn + 16);
+  uint16_t* j16 = s4 + (kOneParIn + 16);
+  uint16_t* s16 = j16 + (kOneParIn + 16);
+  uint16_t* j8 = j2;  // (8-tag hops: j2 / s2 are not needed once j4 / s4 exist)
+  uint16_t* s8 = s2;
   uint16_t* P = j2;  // the output bytes' pointers reuse j2 / s2 (2 * kOneParOut <= 4 * (kOneParIn + 16))
-  uint32_t* T = reinterpret_cast<uint32_t*>(s4 + (kOneParIn + 16));  // tags: position | output offset << 16
-  uint32_t* H = T + kOneParTags;                                     // 4-tag hops: position | offset << 16
+  uint32_t* T = reinterpret_cast<uint32_t*>(s16 + (kOneParIn + 16));  // tags: position | output offset << 16
+  uint32_t* H = T + kOneParTags;                                      // 4-tag hops: position | offset << 16
+  uint32_t* H16 = H + (kOneParTags / 4 + 16);                         // 16-tag hops
   if (tid < 6) offs[tid] = tid == 1 ? in_len : tid == 3 ? out_sz : tid == 5 ? row_sz : 0;
   if (tid == 0) {
     sh_bad = 0;
@@ -1821,6 +1834,7 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
     reinterpret_cast<uint4*>(in)[c] = reinterpret_cast<const uint4*>(host_in)[c];
   for (uint32_t i = tid; i < 1024; i += kOneParThreads) tab[i] = g_crc_tables.t[0][i];
   __syncthreads();
+  if (stop == 1) return;
   const uint32_t clen = uint32_t(in_len - 4);
   uint64_t dl64 = 0;
   uint32_t hdr = 0;
@@ -1839,6 +1853,7 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
     dln[p] = uint16_t(min(dl, 0xFFFFu));
   }
   __syncthreads();
+  if (stop == 2) return;
   const uint32_t stored = ld_be32(in + clen);
   auto fin = [&](slate_block_meta m, bool decoded) {
     // wave 0: block.Decode's checks and rows over the decoded block (or the status), then the copy-out
@@ -1879,17 +1894,21 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
     __syncthreads();
     hop(j2, s2, j4, s4);
     __syncthreads();
-    // one thread walks the chain in 4-tag hops from the header
+    hop(j4, s4, j8, s8);
+    __syncthreads();
+    hop(j8, s8, j16, s16);
+    __syncthreads();
+    // one thread walks the chain in 16-tag hops from the header
     if (tid == 0) {
       uint32_t p = hdr, o = 0, k = 0, b = 0;
       while (p < clen) {
-        if (k >= kOneParTags / 4 + 16 || o > dn) {
+        if (k >= kOneParTags / 16 + 16 || o > dn) {
           b = 1;
           break;
         }
-        H[k++] = p | (o << 16);
-        o += s4[p];
-        const uint32_t q = j4[p];
+        H16[k++] = p | (o << 16);
+        o += s16[p];
+        const uint32_t q = j16[p];
         p = q == kPEnd ? clen : q;
         if (q == kPErr) {
           b = 1;
@@ -1901,10 +1920,25 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
       sh_bad = b;
     }
     __syncthreads();
+    // each 16-tag hop's four 4-tag sub-hops (all four but in the last: the chain goes on)
+    const uint32_t n16 = sh_bad ? 0u : sh_nhops;
+    for (uint32_t k = tid; k < n16; k += kOneParThreads) {
+      uint32_t p = H16[k] & 0xFFFF, o = H16[k] >> 16, i = 0;
+      for (; i < 4 && p < clen; i++) {
+        H[4 * k + i] = p | (o << 16);
+        o += s4[p];
+        const uint32_t q = j4[p];
+        p = q >= kPEnd ? clen : q;  // (no ERR: the 16-tag hop holds none)
+      }
+      if (k == n16 - 1) sh_ntags = 4 * k + i;  // (sh_ntags: the number of 4-tag hops, until below)
+    }
+    __syncthreads();
+    if (stop == 3) return;
     bad = sh_bad != 0;
   }
   if (!bad) {
-    const uint32_t nh = sh_nhops;
+    const uint32_t nh = sh_ntags;
+    __syncthreads();  // (every thread has read the hop count before sh_ntags becomes the tag count)
     // hops expanded: the chain's tags with their output offsets, checked as decode_other.go does
     uint32_t b = 0;
     for (uint32_t t = tid; t < nh; t += kOneParThreads) {
@@ -1923,6 +1957,7 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
     }
     if (b) sh_bad = 1;
     __syncthreads();
+    if (stop == 4) return;
     bad = sh_bad != 0;
   }
   if (!bad) {
@@ -1958,9 +1993,11 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
       __syncthreads();
       if (!sh_more) break;
     }
+    if (stop == 5) return;
     if (!sh_more) {  // (every byte resolved: 16 rounds cover any chain in kOneParOut bytes)
       for (uint32_t x = tid; x < dn; x += kOneParThreads) out[x] = uint8_t(P[x]);
       __syncthreads();
+      if (stop == 6) return;
       fin(slate_block_meta{}, true);
       return;
     }
@@ -1974,6 +2011,11 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
   st = int(sh_bad);
   m.status = int16_t(st);
   fin(m, st == SLATE_OK);
+}
+__global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeArgs a, const uint8_t* __restrict__ host_in,
+                                                                        uint64_t in_len, uint64_t out_sz, uint64_t row_sz,
+                                                                        uint8_t* __restrict__ host_out, uint32_t stop) {
+  decode_one_par(a, host_in, in_len, out_sz, row_sz, host_out, stop);
 }
 
 hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& args_in, const uint8_t* host_in, uint64_t in_len,
@@ -1992,7 +2034,12 @@ hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& args_in, const ui
     static const hipError_t attr_p = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_one_par_kernel),
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, int(kOneParLds));
     if (attr_p != hipSuccess) return attr_p;
-    decode_one_par_kernel<<<1, kOneParThreads, kOneParLds, st>>>(a, host_in, in_len, out_sz, row_sz, host_out);
+#ifdef SLATE_PROFILING_BUILD
+    static const uint32_t stop = getenv("SLATE_ONE_STOP") ? uint32_t(atoi(getenv("SLATE_ONE_STOP"))) : 0u;
+#else
+    constexpr uint32_t stop = 0;
+#endif
+    decode_one_par_kernel<<<1, kOneParThreads, kOneParLds, st>>>(a, host_in, in_len, out_sz, row_sz, host_out, stop);
     return hipGetLastError();
   }
   constexpr size_t lds = kTabBytes + kLargeInCap + kLargeOutCap;

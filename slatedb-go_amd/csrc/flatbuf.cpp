@@ -6,12 +6,41 @@
 
 namespace slate {
 
-// Host CRC for the ~80-byte info footer only (flatbuf.go:62-124 framing); every
-// block, filter and index CRC runs on the GPU.
+// Host CRC for the ~80-byte info footer (flatbuf.go:62-124 framing); block and filter CRCs run
+// on the GPU, the CodecNone index's on the host (crc32_host16).
 static const CrcTables kHostCrc = CrcTables();
 uint32_t crc32_host(const uint8_t* p, size_t n) {
   uint32_t c = 0xFFFFFFFFu;
   for (size_t i = 0; i < n; i++) c = kHostCrc.t[0][(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return ~c;
+}
+
+// Slicing-by-16 on the host, for the CodecNone index's CRC (~12 MB at configs[2]), taken on the
+// builder's index thread beside the blocks' copy-back instead of through the GPU after it.
+namespace {
+struct HostCrc16 {
+  uint32_t t[16][256];
+  HostCrc16() {
+    for (uint32_t i = 0; i < 256; i++) t[0][i] = kHostCrc.t[0][i];
+    for (uint32_t i = 0; i < 256; i++)
+      for (int s = 1; s < 16; s++) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+  }
+};
+const HostCrc16 kHost16;
+}  // namespace
+uint32_t crc32_host16(const uint8_t* p, size_t n) {
+  const auto& t = kHost16.t;
+  uint32_t c = 0xFFFFFFFFu;
+  for (; n >= 16; p += 16, n -= 16) {
+    uint32_t w[4];
+    memcpy(w, p, 16);  // (little-endian host)
+    const uint32_t x = c ^ w[0];
+    c = t[15][x & 0xff] ^ t[14][(x >> 8) & 0xff] ^ t[13][(x >> 16) & 0xff] ^ t[12][x >> 24] ^
+        t[11][w[1] & 0xff] ^ t[10][(w[1] >> 8) & 0xff] ^ t[9][(w[1] >> 16) & 0xff] ^ t[8][w[1] >> 24] ^
+        t[7][w[2] & 0xff] ^ t[6][(w[2] >> 8) & 0xff] ^ t[5][(w[2] >> 16) & 0xff] ^ t[4][w[2] >> 24] ^
+        t[3][w[3] & 0xff] ^ t[2][(w[3] >> 8) & 0xff] ^ t[1][(w[3] >> 16) & 0xff] ^ t[0][w[3] >> 24];
+  }
+  for (; n; p++, n--) c = t[0][(c ^ *p) & 0xff] ^ (c >> 8);
   return ~c;
 }
 

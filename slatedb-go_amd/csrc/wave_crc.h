@@ -7,6 +7,8 @@ namespace slate {
 // Per translation unit (no relocatable device code): each TU gets its own copy.
 static __constant__ CrcTables g_crc_tables = CrcTables();
 static __constant__ CrcShift g_crc_shift = CrcShift();
+static __constant__ CrcShiftT<16> g_crc_shift16 = CrcShiftT<16>();
+static __constant__ CrcShiftT<32> g_crc_shift32 = CrcShiftT<32>();
 
 constexpr uint32_t kTabBytes = 4096;  // 4 x 256 u32 slicing tables in LDS
 
@@ -91,19 +93,22 @@ __device__ inline uint32_t crc_word(const uint32_t* tab, uint32_t c, uint32_t w)
 // R(init, msg[0..n)) with the CRC register semantics of crc32.ChecksumIEEE but
 // without the final inversion: fold_init = true starts from 0xFFFFFFFF (folded
 // into the first four bytes), false from 0.  n >= 4 when fold_init.
-// 64 lanes x 64-byte segments per 4 KiB stripe, end-aligned so each lane's shift
-// x^(8*64*(63-l)) is a compile-time constant (CrcShift).
-__device__ inline uint32_t wave_crc_raw(const uint32_t* tab, const uint8_t* lds, int32_t msg, uint32_t n, int lane,
-                                        bool fold_init) {
-  uint32_t stripes = (n + kCrcStripe - 1) / kCrcStripe;
+// 64 lanes x Seg-byte segments per (64 Seg)-byte stripe, end-aligned so each lane's shift
+// x^(8*Seg*(63-l)) is a constant (CrcShiftT).  Seg 64 for long messages; short ones take
+// Seg 16 or 32, so a 1 KiB message costs a lane 4 words instead of 16 (wave_crc32).
+template <uint32_t Seg>
+__device__ inline uint32_t wave_crc_seg(const uint32_t* tab, const uint8_t* lds, int32_t msg, uint32_t n, int lane,
+                                        bool fold_init, const CrcShiftT<Seg>& sh) {
+  constexpr uint32_t kStripe = kWave * Seg;
+  uint32_t stripes = (n + kStripe - 1) / kStripe;
   uint32_t acc = 0;
   for (uint32_t k = 0; k < stripes; k++) {
-    if (k) acc = gf2_mulmod(acc, g_crc_shift.stripe);
-    int64_t p0 = int64_t(n) - int64_t(stripes - k) * kCrcStripe + int64_t(lane) * kCrcSeg;
+    if (k) acc = gf2_mulmod(acc, sh.stripe);
+    int64_t p0 = int64_t(n) - int64_t(stripes - k) * kStripe + int64_t(lane) * Seg;
     uint32_t c = 0;
-    if (p0 + int64_t(kCrcSeg) > 0) {
+    if (p0 + int64_t(Seg) > 0) {
 #pragma unroll 4
-      for (uint32_t q = 0; q < kCrcSeg / 4; q++) {
+      for (uint32_t q = 0; q < Seg / 4; q++) {
         int64_t p = p0 + 4 * q;
         uint32_t w = 0;
         if (p > -4) {
@@ -125,7 +130,13 @@ __device__ inline uint32_t wave_crc_raw(const uint32_t* tab, const uint8_t* lds,
     }
     acc ^= c;
   }
-  return wave_xor(gf2_mulmod(acc, g_crc_shift.lane[lane]));
+  return wave_xor(gf2_mulmod(acc, sh.lane[lane]));
+}
+__device__ inline uint32_t wave_crc_raw(const uint32_t* tab, const uint8_t* lds, int32_t msg, uint32_t n, int lane,
+                                        bool fold_init) {
+  if (n <= 64 * 16) return wave_crc_seg<16>(tab, lds, msg, n, lane, fold_init, g_crc_shift16);
+  if (n <= 64 * 32) return wave_crc_seg<32>(tab, lds, msg, n, lane, fold_init, g_crc_shift32);
+  return wave_crc_seg<kCrcSeg>(tab, lds, msg, n, lane, fold_init, g_crc_shift);
 }
 
 // crc32.ChecksumIEEE of msg[0..n) in LDS.

@@ -15,7 +15,8 @@
 //                            streamed in 64-byte runs (slicing-by-16, 64 blocks per instruction)
 //   B  zs_fast_build_kernel  one WAVE per block (the next block's record in flight): stage the
 //                            frame in LDS, place all literal runs, then the matches in order (a
-//                            dword per lane), write the block back, block.Decode checks and rows
+//                            byte or a dword per lane), write the block back, block.Decode checks
+//                            and rows
 //   C  zs_fast_sum_kernel    one LANE per block: the frame's XXH64 over the decoded block,
 //                            streamed in 64-byte runs (the four accumulators' serial chains of
 //                            64 blocks advance in one wave instruction)
@@ -47,7 +48,7 @@ constexpr uint32_t kZfTailChunks = 11;
 constexpr uint32_t kZfTail = 16 * kZfTailChunks + 16;
 constexpr uint32_t kZfLane = kZfHead + kZfTail;
 constexpr uint32_t kZfParseThreads = 256;
-// phase B: one wave per block, eight 4-wave workgroups per CU (64 VGPRs), the decoded block in LDS
+// phase B: one wave per block, seven 4-wave workgroups per CU (72 VGPRs), the decoded block in LDS
 // with the frame staged around its tail (the bytes after the literals and the 16-byte phase: +256)
 constexpr uint32_t kZfBuildThreads = 256;
 #ifndef SLATE_ZF_BUILD_WG
@@ -63,6 +64,10 @@ constexpr uint32_t kZfCrcThreads = 512;
 // workgroups per CU (one-wave workgroups, eleven per CU, measured 18 % slower)
 constexpr uint32_t kZfHufThreads = 256;
 constexpr uint32_t kZfHufWave = kZsFastInCap + 16 + kZfOutLds + kZsHufScratch;
+constexpr uint32_t kZfBuildLds = (kZfBuildThreads / 64) * kZfOutLds;
+constexpr uint32_t kZfHufLds = (kZfHufThreads / 64) * kZfHufWave;
+static_assert(SLATE_ZF_BUILD_WG * kZfBuildLds <= 160 * 1024, "phase B workgroups per CU exceed the LDS");
+static_assert(2 * kZfHufLds <= 160 * 1024, "phase B' workgroups per CU exceed the LDS");
 
 struct ZfShared {
   ZsShared fse;  // the predefined LL / ML / OF decoding tables
@@ -152,14 +157,31 @@ __device__ bool zf_head(const uint8_t* hb, uint32_t clen, ZfHead& h) {
 }
 
 // --------------------------------------------------------------- bits of phase A
-// The sequences bitstream in a lane's tail window (zs_peek / zs_bits over LDS).
+// The sequences bitstream in a lane's tail window (LDS), read as zs_peek reads it.
 struct ZfBits {
   const uint8_t* buf;
   int64_t S, bp;
 };
-__device__ __forceinline__ uint32_t zf_rd(ZfBits& z, uint32_t k) {
-  const uint32_t v = uint32_t(zs_peek(z.buf, z.S, z.bp, k));
-  z.bp -= k;
+// The stream through a 64-bit register window (phases A and A'): c holds stream bits [lo, lo + 64).
+// zf_fill puts at least the 56 bits below bp there (all of them when bp <= 56); zf_take reads
+// k <= bp - lo of them (or, with lo = 0, past the stream's start, as zs_peek: zeros below it).
+// One LDS round trip per fill instead of one per read.
+struct ZfReg {
+  uint64_t c;
+  int64_t lo;
+};
+__device__ __forceinline__ void zf_fill(const ZfBits& z, ZfReg& r) {
+  r.lo = z.bp > 56 ? ((z.bp - 56) & ~int64_t(7)) : 0;
+  const int32_t off = int32_t((z.S + r.lo) >> 3);  // (S is a byte boundary)
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(z.buf + (off & ~3));
+  const uint32_t sh = uint32_t(off) & 3u, w0 = w[0], w1 = w[1], w2 = w[2];
+  r.c = uint64_t(__builtin_amdgcn_alignbyte(w1, w0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32);
+}
+__device__ __forceinline__ uint32_t zf_take(ZfBits& z, const ZfReg& r, uint32_t k) {
+  const int64_t t = z.bp - int64_t(k);
+  const uint64_t x = t >= 0 ? r.c >> uint32_t(t - r.lo) : r.c << uint32_t(-t);
+  const uint32_t v = z.bp > 0 ? uint32_t(x & ((1ull << k) - 1)) : 0u;
+  z.bp = t;
   return v;
 }
 
@@ -376,10 +398,12 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
         ok = ok && last != 0;
         ZfBits bits{tb0, 8 * int64_t(shift + s + sp - 16 * c_lo), ok ? 8 * int64_t(bn - 1) + (31 - __builtin_clz(last)) : 0};
         uint32_t sll = 0, sof = 0, sml = 0;
+        ZfReg rg{};  // (the register window of phase A': one fill per sequence, more for long values)
         if (ok) {
-          sll = zf_rd(bits, m_ll ? 0 : 6);
-          sof = zf_rd(bits, m_of ? 0 : 5);
-          sml = zf_rd(bits, m_ml ? 0 : 6);
+          zf_fill(bits, rg);
+          sll = zf_take(bits, rg, m_ll ? 0 : 6);
+          sof = zf_take(bits, rg, m_of ? 0 : 5);
+          sml = zf_take(bits, rg, m_ml ? 0 : 6);
         }
         uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
         uint2* seqs = reinterpret_cast<uint2*>(z.seq + size_t(b) * kZfSeqSlot);
@@ -392,15 +416,18 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
             ok = false;
             break;
           }
+          zf_fill(bits, rg);  // >= 56 bits: the offset's <= 31
           uint64_t ofv = (1ull << ofc);
           if (ofc > 24) {
-            const uint32_t hi = zf_rd(bits, ofc - 24);
-            ofv += (uint64_t(hi) << 24) + zf_rd(bits, 24);
+            const uint32_t hi = zf_take(bits, rg, ofc - 24);
+            ofv += (uint64_t(hi) << 24) + zf_take(bits, rg, 24);
           } else {
-            ofv += zf_rd(bits, ofc);
+            ofv += zf_take(bits, rg, ofc);
           }
-          const uint32_t ml = sh->ml_base[mlc] + zf_rd(bits, sh->ml_bits[mlc]);
-          const uint32_t ll = sh->ll_base[llc] + zf_rd(bits, sh->ll_bits[llc]);
+          const uint32_t mb = sh->ml_bits[mlc], lb = sh->ll_bits[llc];  // (<= 16 each)
+          if (rg.lo > 0 && bits.bp - rg.lo < int64_t(mb + lb)) zf_fill(bits, rg);
+          const uint32_t ml = sh->ml_base[mlc] + zf_take(bits, rg, mb);
+          const uint32_t ll = sh->ll_base[llc] + zf_take(bits, rg, lb);
           uint64_t offv;
           if (ofv > 3) {
             offv = ofv - 3;
@@ -418,9 +445,10 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
             }
           }
           if (i + 1 < nseq) {
-            sll = uint32_t(ell.base) + zf_rd(bits, ell.nb);
-            sml = uint32_t(eml.base) + zf_rd(bits, eml.nb);
-            sof = uint32_t(eof.base) + zf_rd(bits, eof.nb);
+            if (rg.lo > 0 && bits.bp - rg.lo < 18) zf_fill(bits, rg);  // (predefined logs 6 / 5 / 6)
+            sll = uint32_t(ell.base) + zf_take(bits, rg, ell.nb);
+            sml = uint32_t(eml.base) + zf_take(bits, rg, eml.nb);
+            sof = uint32_t(eof.base) + zf_take(bits, rg, eof.nb);
           }
           if (bits.bp < 0 || ll > nlit - lp || uint64_t(o) + ll + ml > h.bmax || uint64_t(o) + ll + ml > cap ||
               uint64_t(o) + ll + ml > uint64_t(lbase) + lp + ll) {
@@ -481,30 +509,59 @@ constexpr uint32_t kZfFseScr = 112;  // int8 norm[53] + u8 next[53]
 constexpr uint32_t kZfFseLane = kZfHead + kZfFseTail + 2 * kZfFseTab + kZfFseScr;
 static_assert(kZfFseLane % 16 == 0, "lane records stay 16-byte aligned");
 
+// A forward stream base[off, off + n) through a 64-bit register window: c holds stream bits
+// [lo, lo + 64), lo a byte boundary, bits past the stream's end read as zeros (zs_fbits).
+struct ZfFwd {
+  uint64_t c;
+  uint32_t lo;
+};
+__device__ __forceinline__ void zf_ffill(const uint8_t* base, int32_t off, uint32_t n, uint32_t bp, ZfFwd& r) {
+  r.lo = bp & ~7u;
+  const int32_t o = off + int32_t(r.lo >> 3);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (o & ~3));
+  const uint32_t sh = uint32_t(o) & 3u, w0 = w[0], w1 = w[1], w2 = w[2];
+  uint64_t c = uint64_t(__builtin_amdgcn_alignbyte(w1, w0, sh)) | (uint64_t(__builtin_amdgcn_alignbyte(w2, w1, sh)) << 32);
+  const uint32_t end = 8 * n;
+  c = r.lo >= end ? 0ull : (end - r.lo >= 64 ? c : c & ((1ull << (end - r.lo)) - 1));
+  r.c = c;
+}
+// k <= 32 bits at bp, which lie in the window (bp + k <= lo + 64)
+__device__ __forceinline__ uint32_t zf_ftake(const ZfFwd& r, uint32_t bp, uint32_t k) {
+  return uint32_t((r.c >> (bp - r.lo)) & ((1ull << k) - 1));
+}
+
 // FSE_readNCount (oracle zs_ncount, zstd.h zs_ncount) into int8 counts: bytes used or -1 (also for
-// a count above 127, which this parse leaves to the exact path)
+// a count above 127, which this parse leaves to the exact path).  The bits come through a register
+// window that every lane of the wave refills at once (when any lane has fewer than 26 bits left: a
+// symbol takes <= 8 bits, and a run of zero-count flags 2 per read, which refill on their own), so a
+// refill's LDS round trip is paid every few symbols, not per read.
 __device__ int zf_ncount8(const uint8_t* base, int32_t off, uint32_t n, int8_t* norm, int maxs, int maxal) {
   if (n == 0) return -1;
   const int al = (base[off] & 15) + 5;
   if (al > maxal) return -1;
-  uint64_t bp = 4;
+  uint32_t bp = 4;
   int remaining = (1 << al) + 1, threshold = 1 << al, nb = al + 1, s = 0;
   bool prev0 = false;
   for (int i = 0; i <= maxs; i++) norm[i] = 0;
+  ZfFwd r;
+  zf_ffill(base, off, n, bp, r);
   while (remaining > 1 && s <= maxs) {
+    if (__ballot(bp + 26 > r.lo + 64)) zf_ffill(base, off, n, bp, r);
     if (prev0) {
       int n0 = s;
       for (;;) {
-        const uint32_t r = zs_fbits(base, off, n, bp, 2);
+        if (bp + 2 > r.lo + 64) zf_ffill(base, off, n, bp, r);
+        const uint32_t v = zf_ftake(r, bp, 2);
         bp += 2;
-        n0 += int(r);
-        if (r != 3) break;
+        n0 += int(v);
+        if (v != 3) break;
       }
       if (n0 > maxs) return -1;
       s = n0;
       prev0 = false;
     }
-    const uint32_t v = zs_fbits(base, off, n, bp, uint32_t(nb));
+    if (bp + uint32_t(nb) > r.lo + 64) zf_ffill(base, off, n, bp, r);
+    const uint32_t v = zf_ftake(r, bp, uint32_t(nb));
     const int max = (2 * threshold - 1) - remaining;
     int count;
     if (int(v & uint32_t(threshold - 1)) < max) {
@@ -529,32 +586,69 @@ __device__ int zf_ncount8(const uint8_t* base, int32_t off, uint32_t n, int8_t* 
   return int((bp + 7) / 8) | (al << 16) | ((s - 1) << 24);  // used (< 2^16), the log, the last symbol
 }
 
-// FSE decoding table (oracle zs_fse_build) with 16-bit entries sym | nb << 6 | base << 9 (al <= 7)
+// FSE decoding table (oracle zs_fse_build) with 16-bit entries sym | nb << 6 | base << 9 (al <= 7).
+// The LDS reads go eight at a time (one round trip per eight counts or cells): in the last pass the
+// eight cells' next[] reads are issued together and a cell counts the same symbol among the earlier
+// cells of its group; the stores then run in order (the last of a symbol holds its final count).
 __device__ bool zf_fse_build16(uint16_t* t, const int8_t* norm, int last, int al, uint8_t* next) {
   const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
   uint32_t hi = size - 1;
-  for (int s = 0; s <= last; s++) {
-    const int c = norm[s];
-    if (c == -1) {
-      t[hi--] = uint16_t(s);
-      next[s] = 1;
-    } else {
-      next[s] = uint8_t(c > 0 ? c : 0);
+  // (norm has room for 56 counts: groups of eight read past `last` harmlessly)
+  for (int s0 = 0; s0 <= last; s0 += 8) {
+    int c[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = norm[s0 + j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int s = s0 + j;
+      if (s <= last) {
+        if (c[j] == -1) {
+          t[hi--] = uint16_t(s);
+          next[s] = 1;
+        } else {
+          next[s] = uint8_t(c[j] > 0 ? c[j] : 0);
+        }
+      }
     }
   }
   uint32_t pos = 0;
-  for (int s = 0; s <= last; s++)
-    for (int i = 0; i < norm[s]; i++) {
-      t[pos] = uint16_t(s);
-      do pos = (pos + step) & mask;
-      while (pos > hi);
+  for (int s0 = 0; s0 <= last; s0 += 8) {
+    int c[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = norm[s0 + j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int s = s0 + j;
+      const int cn = s <= last ? c[j] : 0;
+      for (int i = 0; i < cn; i++) {
+        t[pos] = uint16_t(s);
+        do pos = (pos + step) & mask;
+        while (pos > hi);
+      }
     }
+  }
   if (pos != 0) return false;
-  for (uint32_t u = 0; u < size; u++) {
-    const uint32_t sym = t[u] & 63u;
-    const uint32_t x = next[sym]++;
-    const uint32_t nbits = uint32_t(al) - (31 - __builtin_clz(x));
-    t[u] = uint16_t(sym | (nbits << 6) | (((x << nbits) - size) << 9));
+  for (uint32_t u0 = 0; u0 < size; u0 += 8) {  // (size >= 32: accuracy logs >= 5)
+    const uint4 q = *reinterpret_cast<const uint4*>(t + u0);
+    const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+    uint32_t sym[8], x[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) sym[j] = (qw[j >> 1] >> (16 * (j & 1))) & 63u;
+#pragma unroll
+    for (int j = 0; j < 8; j++) x[j] = next[sym[j]];
+#pragma unroll
+    for (int j = 1; j < 8; j++)
+#pragma unroll
+      for (int i = 0; i < j; i++) x[j] += sym[i] == sym[j] ? 1u : 0u;
+    uint32_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      next[sym[j]] = uint8_t(x[j] + 1);
+      const uint32_t nbits = uint32_t(al) - (31 - __builtin_clz(x[j]));
+      e[j] = sym[j] | (nbits << 6) | (((x[j] << nbits) - size) << 9);
+    }
+    *reinterpret_cast<uint4*>(t + u0) = make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16),
+                                                   e[6] | (e[7] << 16));
   }
   return true;
 }
@@ -718,35 +812,36 @@ __global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1
         sp += ok ? uint32_t(u & 0xFFFF) : 0u;
         al_ml = ok ? uint32_t(u >> 16) : 0u;
       }
+      ok = ok && !(dbg_bits(a) & (1u << 18));  // profiling: the tables only (every block handed back)
       // zs_bstart
       const uint32_t bn = ok ? sn - sp : 0u;
       const uint32_t last = bn ? uint32_t(tb[s + sn - 1]) : 0u;
       ok = ok && last != 0;
       ZfBits bits{tb0, 8 * int64_t(int32_t(s + sp) + tofs), ok ? 8 * int64_t(bn - 1) + (31 - __builtin_clz(last)) : 0};
       uint32_t sll = 0, sof = 0, sml = 0;
+      ZfReg rg{};
       if (ok) {
-        sll = zf_rd(bits, al_ll);
-        sof = zf_rd(bits, al_of);
-        sml = zf_rd(bits, al_ml);
+        zf_fill(bits, rg);
+        sll = zf_take(bits, rg, al_ll);  // (<= 21 bits: accuracy logs <= 7)
+        sof = zf_take(bits, rg, al_of);
+        sml = zf_take(bits, rg, al_ml);
       }
       uint32_t rep0 = 1, rep1 = 4, rep2 = 8, lp = 0, o = 0;
       const uint32_t lbase = cap - nlit;
       for (uint32_t i = 0; ok && i < nseq; i++) {
+        zf_fill(bits, rg);  // (issued beside the table reads: >= 56 bits for this sequence's values)
         const uint32_t ell = tab[sll], eof = tab[t_of + sof], eml = tab[t_ml + sml];
         const uint32_t llc = ell & 63u, ofc = eof & 63u, mlc = eml & 63u;
-        if (ofc > 31) {
+        // an offset code above 12 gives an offset above 4096, which the record cannot hold (the
+        // check below): the block goes to the exact path either way; so the values take <= 12 +
+        // 16 + 16 bits of the window
+        if (ofc > 12) {
           ok = false;
           break;
         }
-        uint64_t ofv = (1ull << ofc);
-        if (ofc > 24) {
-          const uint32_t hi = zf_rd(bits, ofc - 24);
-          ofv += (uint64_t(hi) << 24) + zf_rd(bits, 24);
-        } else {
-          ofv += zf_rd(bits, ofc);
-        }
-        const uint32_t ml = ml_base[mlc] + zf_rd(bits, ml_bits[mlc]);
-        const uint32_t ll = ll_base[llc] + zf_rd(bits, ll_bits[llc]);
+        const uint32_t ofv = (1u << ofc) + zf_take(bits, rg, ofc);
+        const uint32_t ml = ml_base[mlc] + zf_take(bits, rg, ml_bits[mlc]);
+        const uint32_t ll = ll_base[llc] + zf_take(bits, rg, ll_bits[llc]);
         uint64_t offv;
         if (ofv > 3) {
           offv = ofv - 3;
@@ -764,9 +859,10 @@ __global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1
           }
         }
         if (i + 1 < nseq) {
-          sll = (ell >> 9) + zf_rd(bits, (ell >> 6) & 7u);
-          sml = (eml >> 9) + zf_rd(bits, (eml >> 6) & 7u);
-          sof = (eof >> 9) + zf_rd(bits, (eof >> 6) & 7u);
+          if (rg.lo > 0 && bits.bp - rg.lo < 21) zf_fill(bits, rg);  // (long values only)
+          sll = (ell >> 9) + zf_take(bits, rg, (ell >> 6) & 7u);
+          sml = (eml >> 9) + zf_take(bits, rg, (eml >> 6) & 7u);
+          sof = (eof >> 9) + zf_take(bits, rg, (eof >> 6) & 7u);
         }
         if (bits.bp < 0 || ll > nlit - lp || uint64_t(o) + ll + ml > h.bmax || uint64_t(o) + ll + ml > cap ||
             uint64_t(o) + ll + ml > uint64_t(lbase) + lp + ll) {
@@ -1407,7 +1503,7 @@ hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
-  const size_t lds_b = size_t(kZfBuildThreads / 64) * kZfOutLds;
+  const size_t lds_b = kZfBuildLds;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
   if (attr != hipSuccess) return attr;
@@ -1426,12 +1522,12 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
-  const size_t lds_b = size_t(kZfBuildThreads / 64) * kZfOutLds;
+  const size_t lds_b = kZfBuildLds;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
   if (attr != hipSuccess) return attr;
   const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG);
-  const size_t lds_h = size_t(kZfHufThreads / 64) * kZfHufWave;
+  const size_t lds_h = kZfHufLds;
   static const hipError_t attr_h = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_huf_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_h));
   if (attr_h != hipSuccess) return attr_h;

@@ -63,6 +63,10 @@ int main(int argc, char** argv) {
     if (st) return 4;
   }
   const double gpu_dec = (now_us() - t0) / calls;
+  if (getenv("PERCALL_DECODE_ONLY")) { /* tools/onestop.sh: profiling library, phases cut short */
+    printf("{\"calls\": %d, \"slate_block_decode_us\": %.2f}\n", calls, gpu_dec);
+    return 0;
+  }
   t0 = now_us();
   for (int c = 0; c < calls; c++) {
     st = or_block_decode(blk[c % n], len[c % n], 1, out, cap, &ol, &om, rows, 70000);
