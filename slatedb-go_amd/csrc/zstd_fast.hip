@@ -57,7 +57,7 @@ constexpr uint32_t kZfBuildThreads = 256;
 constexpr uint32_t kZfIn = kZsFastInCap, kZfOut = kZsFastOutCap;
 constexpr uint32_t kZfJunk = kZfOut + 256;      // 64 junk dwords (lanes' discarded writes)
 constexpr uint32_t kZfOutLds = kZfJunk + 256;
-// phase C: 64 bytes of LDS per lane; phase A2: the same + the slicing-by-16 CRC tables
+// phase C: 128 bytes of LDS per lane; phase A2: 64 + the slicing-by-16 CRC tables
 constexpr uint32_t kZfSumThreads = 256;
 constexpr uint32_t kZfCrcThreads = 512;
 // phase B': per wave the frame, the decoded block and the Huffman part of a ZsScratch; two 4-wave
@@ -1293,37 +1293,54 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
 // lanes 4i..4i+3 read one 64-byte run of block 16j+i) issued one iteration ahead into
 // registers; the loading lanes put them into the owner's LDS slot, and every lane runs two
 // 32-byte stripes.
+// kRun = 128 (phase C since round 5): 128-byte runs, lanes 8i..8i+7 of load j reading block 8j+i
+// -- half the address-unit requests per byte of 64-byte runs (tools/scatter_probe.hip: ~98 against
+// ~188 CU cycles per wave-instruction), four stripes per iteration.  Same-box A/B
+// (profiles/round5/ab_zstd_runs.txt): C at 128 B +2.5 % on configs[4]; A2 at 128 B (256 threads,
+// for the LDS) 1 % slower than at 64 B with 512 threads, so A2 keeps 64.
+#ifndef SLATE_ZF_SUM_RUN
+#define SLATE_ZF_SUM_RUN 128
+#endif
+#ifndef SLATE_ZF_CRC_RUN
+#define SLATE_ZF_CRC_RUN 64
+#endif
 namespace {
+template <uint32_t kRun>
 struct ZfGroup {
-  v4u p[4];
+  v4u p[kRun / 16];
 };
-__device__ __forceinline__ ZfGroup zf_load_group(__amdgpu_buffer_rsrc_t R, uint32_t t, uint32_t rel, uint32_t groups,
-                                                 uint32_t lane) {
-  ZfGroup g;
+template <uint32_t kRun>
+__device__ __forceinline__ ZfGroup<kRun> zf_load_group(__amdgpu_buffer_rsrc_t R, uint32_t t, uint32_t rel,
+                                                       uint32_t groups, uint32_t lane) {
+  constexpr uint32_t kL = kRun / 16;  // lanes per block in one load
+  ZfGroup<kRun> g;
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
+  for (uint32_t j = 0; j < kL; j++) {
+    const uint32_t o = (64 / kL) * j + lane / kL, c = lane % kL;
     const uint32_t g_o = __shfl(groups, int(o), 64), rel_o = __shfl(rel, int(o), 64);
-    g.p[j] = bload(R, t < g_o ? rel_o + 64 * t + 16 * c : kOOB);
+    g.p[j] = bload(R, t < g_o ? rel_o + kRun * t + 16 * c : kOOB);
   }
   return g;
 }
-__device__ __forceinline__ void zf_commit_group(const ZfGroup& g, uint8_t* slots0, uint32_t t, uint32_t groups,
+template <uint32_t kRun>
+__device__ __forceinline__ void zf_commit_group(const ZfGroup<kRun>& g, uint8_t* slots0, uint32_t t, uint32_t groups,
                                                 uint32_t lane) {
+  constexpr uint32_t kL = kRun / 16;
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    const uint32_t o = 16 * j + (lane >> 2), c = lane & 3;
-    if (t < uint32_t(__shfl(groups, int(o), 64))) lds_put16(slots0 + o * 64 + 16 * c, g.p[j]);
+  for (uint32_t j = 0; j < kL; j++) {
+    const uint32_t o = (64 / kL) * j + lane / kL, c = lane % kL;
+    if (t < uint32_t(__shfl(groups, int(o), 64))) lds_put16(slots0 + o * kRun + 16 * c, g.p[j]);
   }
 }
 }  // namespace
 
 __global__ __launch_bounds__(kZfSumThreads) void zs_fast_sum_kernel(DecodeArgs a, ZsFastArgs z) {
-  __shared__ __attribute__((aligned(16))) uint8_t slots[kZfSumThreads * 64];
+  constexpr uint32_t kRun = SLATE_ZF_SUM_RUN;
+  __shared__ __attribute__((aligned(16))) uint8_t slots[kZfSumThreads * kRun];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave_lane0 = threadIdx.x - lane;
-  uint8_t* slots0 = slots + wave_lane0 * 64;
-  const uint8_t* mine = slots0 + lane * 64;
+  uint8_t* slots0 = slots + wave_lane0 * kRun;
+  const uint8_t* mine = slots0 + lane * kRun;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
     const uint32_t b = r0 + lane;
@@ -1339,16 +1356,16 @@ __global__ __launch_bounds__(kZfSumThreads) void zs_fast_sum_kernel(DecodeArgs a
       want = rec.want;
       orel = uint32_t(a.out_off[b] - a.out_off[r0]);
     }
-    const uint32_t groups = (len + 63) / 64, stripes = len / 32;
+    const uint32_t groups = (len + kRun - 1) / kRun, stripes = len / 32;
     uint64_t v0 = kX64P1 + kX64P2, v1 = kX64P2, v2 = 0, v3 = 0ull - kX64P1;
-    ZfGroup g = zf_load_group(R, 0, orel, groups, lane);
+    ZfGroup<kRun> g = zf_load_group<kRun>(R, 0, orel, groups, lane);
     for (uint32_t t = 0; __ballot(t < groups); t++) {
-      zf_commit_group(g, slots0, t, groups, lane);
-      g = zf_load_group(R, t + 1, orel, groups, lane);  // in flight during this iteration
+      zf_commit_group<kRun>(g, slots0, t, groups, lane);
+      g = zf_load_group<kRun>(R, t + 1, orel, groups, lane);  // in flight during this iteration
       zs_sync();
 #pragma unroll
-      for (uint32_t h = 0; h < 2; h++) {
-        if (2 * t + h < stripes && !(dbg_bits(a) & (1u << 24))) {
+      for (uint32_t h = 0; h < kRun / 32; h++) {
+        if ((kRun / 32) * t + h < stripes && !(dbg_bits(a) & (1u << 24))) {
           const uint64_t* w = reinterpret_cast<const uint64_t*>(mine + 32 * h);
           v0 = x64round(v0, w[0]);
           v1 = x64round(v1, w[1]);
@@ -1373,7 +1390,7 @@ __global__ __launch_bounds__(kZfSumThreads) void zs_fast_sum_kernel(DecodeArgs a
       }
       hh += len;
       uint32_t i = len & ~31u;
-      const uint8_t* tail = mine - 64 * ((len - 1) / 64);  // tail[i] = decoded byte i (len > 0)
+      const uint8_t* tail = mine - kRun * ((len - 1) / kRun);  // tail[i] = decoded byte i (len > 0)
       for (; i + 8 <= len; i += 8)
         hh = x64rotl(hh ^ x64round(0, *reinterpret_cast<const uint64_t*>(tail + i)), 27) * kX64P1 + kX64P4;
       if (i + 4 <= len) {
@@ -1408,8 +1425,9 @@ __global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a
   }
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave_lane0 = threadIdx.x - lane;
-  uint8_t* slots0 = smem + kTab16Bytes + wave_lane0 * 64;
-  const uint8_t* mine = slots0 + lane * 64;
+  constexpr uint32_t kRun = SLATE_ZF_CRC_RUN;
+  uint8_t* slots0 = smem + kTab16Bytes + wave_lane0 * kRun;
+  const uint8_t* mine = slots0 + lane * kRun;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
     const uint32_t b = r0 + lane;
@@ -1427,7 +1445,7 @@ __global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a
         shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + s0) & 15);
         clen = uint32_t(a.in_off[b + 1] - s0) - 4;
         irel = uint32_t(((a.in + s0) - shift) - ibase);
-        groups = (shift + clen + 63) / 64;
+        groups = (shift + clen + kRun - 1) / kRun;
       }
     }
     uint32_t stored = 0;
@@ -1445,14 +1463,14 @@ __global__ __launch_bounds__(kZfCrcThreads) void zs_fast_crc_kernel(DecodeArgs a
       stored = __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, p & 3));
     }
     uint32_t crc = 0xFFFFFFFFu;
-    ZfGroup g = zf_load_group(R, 0, irel, groups, lane);
+    ZfGroup<kRun> g = zf_load_group<kRun>(R, 0, irel, groups, lane);
     for (uint32_t t = 0; __ballot(t < groups); t++) {
-      zf_commit_group(g, slots0, t, groups, lane);
-      g = zf_load_group(R, t + 1, irel, groups, lane);  // in flight during this iteration
+      zf_commit_group<kRun>(g, slots0, t, groups, lane);
+      g = zf_load_group<kRun>(R, t + 1, irel, groups, lane);  // in flight during this iteration
       zs_sync();
 #pragma unroll
-      for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t c0 = 64 * t + 16 * k;  // aligned offset of the chunk
+      for (uint32_t k = 0; k < kRun / 16; k++) {
+        const uint32_t c0 = kRun * t + 16 * k;  // aligned offset of the chunk
         const v4u v = *reinterpret_cast<const v4u*>(mine + 16 * k);
         const bool whole = t < groups && c0 >= shift && c0 + 16 <= shift + clen;
         const bool part = t < groups && !whole && c0 < shift + clen && c0 + 16 > shift;
@@ -1500,7 +1518,7 @@ hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   if (a.n == 0) return hipGetLastError();
   hipError_t e = launch_zlib_fast_parse(st, a, z, num_cus);
   if (e != hipSuccess) return e;
-  const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
+  const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
   const size_t lds_b = kZfBuildLds;
@@ -1519,7 +1537,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   zs_fast_parse_kernel<<<grid_a, kZfParseThreads, lds_a, st>>>(a, z);
   // phase A': the blocks phase A listed for the FSE parse (three one-wave workgroups per CU)
   zs_fse_parse_kernel<<<uint32_t(num_cus) * 3u, kZfFseThreads, size_t(kZfFseThreads) * kZfFseLane, st>>>(a, z);
-  const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * 64;
+  const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
   const size_t lds_b = kZfBuildLds;
