@@ -456,7 +456,7 @@ def kv100_leg(sc, ctx, stream, wl, args, threads, codec):
                                    int(in_off[-1]))
     name = {sc.ZSTD: "zstd", sc.ZLIB: "zlib"}[codec]
     res["roofline"]["kernel"] = ("zs_fast_parse + zs_fse_parse/crc/build/sum + decode_list_kernel<2> (+ plan)"
-                                 if codec == sc.ZSTD else "decode_fast_kernel<1> (+ plan_zlib_kernel)")
+                                 if codec == sc.ZSTD else "zl_fast_kernel + zs_fast_crc/build + decode_list_kernel<1> (+ zl_fast_kernel<plan>)")
     res["handbacks"] = int(handbacks)
     res["verified"] = leg.verify_against_decoded((dec, dec_off), meta)
     m = min(4096, n)

@@ -5,6 +5,7 @@
 #   PART=3: the per-shape traffic attribution of the headline kernel (tools/traffic_shapes.sh)
 #   PART=2: the default bench line (reading the PMC files committed from part 1) and the same
 #           command under rocprofv3 --kernel-trace --stats
+#   PART=4: the headline launches alone (no extra legs) under the kernel trace
 # env: TAG, PART
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -24,10 +25,15 @@ if [ "${PART:-1}" = 1 ]; then
 elif [ "$PART" = 3 ]; then
   bash tools/traffic_shapes.sh $OUT/shapes > $OUT/shapes.log 2>&1 || { echo SHAPES_FAILED; tail -20 $OUT/shapes.log; exit 1; }
   tail -c 1500 $OUT/shapes.log
-else
+elif [ "$PART" = 2 ]; then
   timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAILED; tail -30 $OUT/bench.err; exit 1; }
   cat $OUT/bench.json
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/benchprof -o bench -- python3 bench.py > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { echo BENCH_PROF_FAILED; tail -30 $OUT/bench_prof.err; exit 1; }
   f=$(ls $OUT/benchprof/*kernel_stats.csv | head -1)
   head -12 $f | cut -c1-200
+fi
+if [ "$PART" = 4 ]; then  # the headline launches alone under the kernel trace (the stats file's average is theirs)
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $OUT/headprof -o head -- python3 bench.py --no-cpu-baseline --no-host-io --no-extras --verify none > $OUT/head.json 2> $OUT/head.err || { echo HEAD_PROF_FAILED; tail -30 $OUT/head.err; exit 1; }
+  cat $OUT/head.json
+  head -6 $OUT/headprof/head_kernel_stats.csv | cut -c1-220
 fi

@@ -14,6 +14,7 @@ export TMPDIR=/tmp
 export SLATE_LIB_VARIANT=libslatecodec_prof.so
 ARGS="--codec snappy --steps 2 --warmup 1 --blocks $BLOCKS --no-cpu-baseline --no-host-io --no-extras --verify none --allow-variant"
 for mode in 0 32768 16384 1024; do
+  mkdir -p "$OUT/m$mode"
   for c in FETCH_SIZE WRITE_SIZE; do
     SLATE_DEBUG_MODE=$mode timeout -s KILL 240 rocprofv3 --pmc $c -f csv -d "$OUT/m$mode/$c" -o run -- python3 bench.py $ARGS > "$OUT/m$mode/$c.log" 2>&1
   done
