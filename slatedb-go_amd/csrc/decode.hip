@@ -1118,6 +1118,8 @@ __global__ __launch_bounds__(kDecodeThreads) void decode_list_kernel(DecodeArgs 
 template <int CK>
 __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t count = *a.large_count;
+  if (blockIdx.x >= count) return;  // (workgroup-uniform) no block: skip the tables (~50 us for Zstd's)
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
   load_crc_tables(tab);
   const int lane = threadIdx.x & 63;
@@ -1128,7 +1130,6 @@ __global__ __launch_bounds__(64) void decode_large_kernel(DecodeArgs a) {
   WaveBufs w{tab, smem + kTabBytes, smem + kTabBytes + kLargeInCap, in_cap, kLargeOutCap};
   if (CK == 1) zlib_lds(w, smem + kTabBytes + in_cap, 1, 0, lane);
   if (CK == 2) zstd_lds(w, smem + kTabBytes + in_cap, 0, lane);
-  uint32_t count = *a.large_count;
   for (uint32_t k = blockIdx.x; k < count; k += gridDim.x) {
     // beyond this kernel's LDS budget (encoded > 64 KiB or decoded > 88 KiB: a block holding one
     // large value): the same wave decoder with input and output in HBM
