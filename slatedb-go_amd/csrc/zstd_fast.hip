@@ -57,7 +57,7 @@ constexpr uint32_t kZfBuildThreads = 256;
 constexpr uint32_t kZfIn = kZsFastInCap, kZfOut = kZsFastOutCap;
 constexpr uint32_t kZfJunk = kZfOut + 256;      // 64 junk dwords (lanes' discarded writes)
 constexpr uint32_t kZfOutLds = kZfJunk + 256;
-// phase C: 128 bytes of LDS per lane; phase A2: 64 + the slicing-by-16 CRC tables
+// phase C: 256 bytes of LDS per lane; phase A2: 64 + the slicing-by-16 CRC tables
 constexpr uint32_t kZfSumThreads = 256;
 constexpr uint32_t kZfCrcThreads = 512;
 // phase B': per wave the frame, the decoded block and the Huffman part of a ZsScratch; two 4-wave
@@ -1293,13 +1293,14 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
 // lanes 4i..4i+3 read one 64-byte run of block 16j+i) issued one iteration ahead into
 // registers; the loading lanes put them into the owner's LDS slot, and every lane runs two
 // 32-byte stripes.
-// kRun = 128 (phase C since round 5): 128-byte runs, lanes 8i..8i+7 of load j reading block 8j+i
-// -- half the address-unit requests per byte of 64-byte runs (tools/scatter_probe.hip: ~98 against
-// ~188 CU cycles per wave-instruction), four stripes per iteration.  Same-box A/B
-// (profiles/round5/ab_zstd_runs.txt): C at 128 B +2.5 % on configs[4]; A2 at 128 B (256 threads,
-// for the LDS) 1 % slower than at 64 B with 512 threads, so A2 keeps 64.
+// kRun = 256 (phase C since round 5): 256-byte runs, lanes 16i..16i+15 of load j reading block 4j+i
+// -- fewer address-unit requests per byte than 64-byte runs (tools/scatter_probe.hip: ~188 CU
+// cycles per wave-instruction for 64-byte runs, ~98 for 128-byte ones), eight stripes per
+// iteration, 64 KiB of LDS per workgroup.  Same-box A/Bs (profiles/round5/ab_zstd_runs.txt): C at
+// 128 B +2.5 % on configs[4], at 256 B another +0.5 % (and +0.3 % on kv100); A2 at 128 B (256
+// threads, for the LDS) 1 % slower than at 64 B with 512 threads, so A2 keeps 64.
 #ifndef SLATE_ZF_SUM_RUN
-#define SLATE_ZF_SUM_RUN 128
+#define SLATE_ZF_SUM_RUN 256
 #endif
 #ifndef SLATE_ZF_CRC_RUN
 #define SLATE_ZF_CRC_RUN 64
