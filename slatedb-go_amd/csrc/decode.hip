@@ -251,40 +251,71 @@ __global__ void scan_reduce_kernel(const uint64_t* __restrict__ a, const uint64_
   if (threadIdx.x == 0) { pa[blockIdx.x] = ta; pb[blockIdx.x] = tb; }
 }
 
-// Single workgroup: exclusive scan of the per-tile partials in place.
-__global__ void scan_partials_kernel(uint64_t* __restrict__ pa, uint64_t* __restrict__ pb, uint32_t m) {
+// CodecNone / CodecSnappy sizes (plan_sizes_kernel) and the scan's tile sums in one pass: the
+// sizes are written and summed by the same threads (one launch and one re-read fewer).
+__global__ void plan_reduce_kernel(int codec, const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                                   uint32_t n, uint64_t* __restrict__ out_sz, uint64_t* __restrict__ row_sz,
+                                   uint64_t* __restrict__ pa, uint64_t* __restrict__ pb) {
   __shared__ uint64_t sh[2][kScanThreads / 64];
-  uint64_t ca = 0, cb = 0;
-  for (uint32_t base = 0; base < m; base += kScanThreads) {
-    uint32_t i = base + threadIdx.x;
-    uint64_t va = i < m ? pa[i] : 0, vb = i < m ? pb[i] : 0;
-    uint64_t ta, tb;
-    uint64_t ea = block_exclusive_scan(va, sh[0], &ta);
-    uint64_t eb = block_exclusive_scan(vb, sh[1], &tb);
-    if (i < m) { pa[i] = ca + ea; pb[i] = cb + eb; }
-    ca += ta;
-    cb += tb;
+  const uint64_t base = uint64_t(blockIdx.x) * kScanTile;
+  uint64_t sa = 0, sb = 0;
+  for (int k = 0; k < kScanItems; k++) {
+    const uint64_t i = base + uint64_t(k) * kScanThreads + threadIdx.x;
+    if (i > n) continue;
+    uint64_t o = 0, r = 0;  // (entry n: the trailing zero the scan turns into the totals)
+    if (i < n) {
+      const uint64_t s0 = in_off[i];
+      uint32_t hdr;
+      uint64_t dl;
+      decoded_len(codec, in + s0, in_off[i + 1] - s0, &dl, &hdr);
+      o = align16(dl);
+      r = row_capacity(dl);
+    }
+    out_sz[i] = o;
+    row_sz[i] = r;
+    sa += o;
+    sb += r;
+  }
+  uint64_t ta, tb;
+  block_exclusive_scan(sa, sh[0], &ta);
+  block_exclusive_scan(sb, sh[1], &tb);
+  if (threadIdx.x == 0) {
+    pa[blockIdx.x] = ta;
+    pb[blockIdx.x] = tb;
   }
 }
 
-__global__ void scan_apply_kernel(uint64_t* __restrict__ a, uint64_t* __restrict__ b, uint32_t n,
-                                  const uint64_t* __restrict__ pa, const uint64_t* __restrict__ pb) {
+// The scan's last pass, each tile first summing the tile sums below it itself (the single-workgroup
+// partials pass is then not needed: ~1000 tiles per 1 M blocks, a few loads per thread).
+__global__ void scan_apply_sum_kernel(uint64_t* __restrict__ a, uint64_t* __restrict__ b, uint32_t n,
+                                      const uint64_t* __restrict__ pa, const uint64_t* __restrict__ pb) {
   __shared__ uint64_t sh[2][kScanThreads / 64];
-  uint64_t base = uint64_t(blockIdx.x) * kScanTile + uint64_t(threadIdx.x) * kScanItems;
+  uint64_t qa = 0, qb = 0;
+  for (uint32_t j = threadIdx.x; j < blockIdx.x; j += kScanThreads) {
+    qa += pa[j];
+    qb += pb[j];
+  }
+  uint64_t ba, bb;
+  block_exclusive_scan(qa, sh[0], &ba);
+  block_exclusive_scan(qb, sh[1], &bb);
+  const uint64_t base = uint64_t(blockIdx.x) * kScanTile + uint64_t(threadIdx.x) * kScanItems;
   uint64_t va[kScanItems], vb[kScanItems], sa = 0, sb = 0;
   for (int k = 0; k < kScanItems; k++) {
-    uint64_t i = base + k;
+    const uint64_t i = base + k;
     va[k] = i < n ? a[i] : 0;
     vb[k] = (b && i < n) ? b[i] : 0;
     sa += va[k];
     sb += vb[k];
   }
   uint64_t ta, tb;
-  uint64_t ea = block_exclusive_scan(sa, sh[0], &ta) + pa[blockIdx.x];
-  uint64_t eb = block_exclusive_scan(sb, sh[1], &tb) + pb[blockIdx.x];
+  uint64_t ea = block_exclusive_scan(sa, sh[0], &ta) + ba;
+  uint64_t eb = block_exclusive_scan(sb, sh[1], &tb) + bb;
   for (int k = 0; k < kScanItems; k++) {
-    uint64_t i = base + k;
-    if (i < n) { a[i] = ea; if (b) b[i] = eb; }
+    const uint64_t i = base + k;
+    if (i < n) {
+      a[i] = ea;
+      if (b) b[i] = eb;
+    }
     ea += va[k];
     eb += vb[k];
   }
@@ -1602,6 +1633,11 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
     if (e != hipSuccess) return e;
     if (n > 0) plan_list_kernel<<<min((n + 255) / 256, 1024u), 256, 0, st>>>(codec, in, in_off, s.zf.list, s.zf.count,
                                                                             out_off, row_base);
+  } else if (codec == SLATE_CODEC_NONE || codec == SLATE_CODEC_SNAPPY) {
+    // sizes + tile sums, then the apply pass with its own prefix of the tile sums: two launches
+    plan_reduce_kernel<<<s.tiles, kScanThreads, 0, st>>>(codec, in, in_off, n, out_off, row_base, s.pa, s.pb);
+    scan_apply_sum_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
+    return hipGetLastError();
   } else {
     plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
   }
@@ -1622,8 +1658,7 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
     plan_zstd_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, s.zf.list, s.zf.count);
   }
   scan_reduce_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
-  scan_partials_kernel<<<1, kScanThreads, 0, st>>>(s.pa, s.pb, s.tiles);
-  scan_apply_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
+  scan_apply_sum_kernel<<<s.tiles, kScanThreads, 0, st>>>(out_off, row_base, m, s.pa, s.pb);
   return hipGetLastError();
 }
 
@@ -1634,8 +1669,7 @@ hipError_t launch_scan_u64(hipStream_t st, uint64_t* a, uint32_t m, void* scratc
   uint64_t* pa = static_cast<uint64_t*>(scratch);
   uint64_t* pb = pa + tiles + 1;
   scan_reduce_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
-  scan_partials_kernel<<<1, kScanThreads, 0, st>>>(pa, pb, tiles);
-  scan_apply_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
+  scan_apply_sum_kernel<<<tiles, kScanThreads, 0, st>>>(a, nullptr, m, pa, pb);
   return hipGetLastError();
 }
 
