@@ -501,13 +501,25 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
 // store.  Anything else -- a larger table, a length or offset the record cannot hold, any failed
 // check -- goes to the exact path, which decodes and reports it.
 namespace {
+// A lane's LDS: the three tables, then one window used three ways in turn -- the frame's first 48
+// bytes (frame and literals headers); the sequences section's first kZfFseHdrChunks chunks (its
+// counts, modes and table descriptions) with the table build's scratch after them; the sequences
+// bitstream, kZfFseBitChunks chunks from the one holding its first byte (+16 bytes slack for 8-byte
+// bit reads).  A 100 B-KV block's headers take <= 31 bytes and its bitstream <= 10 chunks from
+// there (tools/kvwin.py over 20 k blocks); the section's chunks stay in registers between the
+// stages.  624 bytes per lane: four one-wave workgroups per CU, one per SIMD.
 constexpr uint32_t kZfFseThreads = 64;
-constexpr uint32_t kZfFseTailChunks = 12;
-constexpr uint32_t kZfFseTail = 16 * kZfFseTailChunks + 16;
-constexpr uint32_t kZfFseTab = 224;  // u16 entries, the LL, OF and ML tables back to back
-constexpr uint32_t kZfFseScr = 112;  // int8 norm[53] + u8 next[53]
-constexpr uint32_t kZfFseLane = kZfHead + kZfFseTail + 2 * kZfFseTab + kZfFseScr;
+constexpr uint32_t kZfFseHdrChunks = 4;
+constexpr uint32_t kZfFseBitChunks = 10;
+constexpr uint32_t kZfFseRegChunks = 14;  // chunks c_lo .. c_lo + 13 of the section held in registers
+constexpr uint32_t kZfFseTab = 224;       // u16 entries, the LL, OF and ML tables back to back
+constexpr uint32_t kZfFseScr = 112;       // int8 norm[53] + u8 next[53] (groups of eight: 56 each)
+constexpr uint32_t kZfFseWin = 16 * kZfFseBitChunks + 16;
+constexpr uint32_t kZfFseLane = 2 * kZfFseTab + kZfFseWin;
+constexpr uint32_t kZfFseWgs = 4;  // per CU
 static_assert(kZfFseLane % 16 == 0, "lane records stay 16-byte aligned");
+static_assert(16 * kZfFseHdrChunks + kZfFseScr <= kZfFseWin && kZfHead <= kZfFseWin, "the window's three uses");
+static_assert(kZfFseWgs * (kZfFseThreads * kZfFseLane + 512) <= 160 * 1024, "phase A' workgroups per CU exceed the LDS");
 
 // A forward stream base[off, off + n) through a 64-bit register window: c holds stream bits
 // [lo, lo + 64), lo a byte boundary, bits past the stream's end read as zeros (zs_fbits).
@@ -653,6 +665,13 @@ __device__ bool zf_fse_build16(uint16_t* t, const int8_t* norm, int last, int al
   return true;
 }
 
+// The bytes of a table description at frame byte p that the header chunks hold (a description
+// running past them fails its parse: its block goes to the exact path)
+__device__ __forceinline__ uint32_t zf_hdr_n(uint32_t p, uint32_t n, int32_t hend) {
+  const int32_t room = hend - int32_t(p);
+  return room <= 0 ? 0u : (uint32_t(room) < n ? uint32_t(room) : n);
+}
+
 // One table (zs_table): mode 0 = the predefined distribution, 1 = RLE, 2 = FSE_Compressed at
 // base[off, off + n).  Builds it at t (at most `room` entries); returns bytes used | accuracy log
 // << 16, or -1.
@@ -678,7 +697,7 @@ __device__ int zf_table16(uint32_t mode, const uint8_t* base, int32_t off, uint3
 }
 }  // namespace
 
-// (LDS allows three waves per CU: the registers need not be rationed)
+// (one wave per SIMD: the registers need not be rationed)
 __global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void zs_fse_parse_kernel(
     DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -694,10 +713,10 @@ __global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  uint8_t* hb0 = smem + threadIdx.x * kZfFseLane;
-  uint8_t* tb0 = hb0 + kZfHead;
-  uint16_t* tab = reinterpret_cast<uint16_t*>(tb0 + kZfFseTail);
-  int8_t* norm = reinterpret_cast<int8_t*>(tab + kZfFseTab);
+  uint16_t* tab = reinterpret_cast<uint16_t*>(smem + threadIdx.x * kZfFseLane);
+  uint8_t* const hb0 = reinterpret_cast<uint8_t*>(tab + kZfFseTab);  // the window
+  uint8_t* const tb0 = hb0;
+  int8_t* norm = reinterpret_cast<int8_t*>(hb0 + 16 * kZfFseHdrChunks);
   uint8_t* next = reinterpret_cast<uint8_t*>(norm + 56);
   const uint32_t items = z.count[2];
   const uint32_t waves = gridDim.x * (kZfFseThreads / 64);
@@ -752,17 +771,22 @@ __global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1
       pos = hs + (type == 0 ? nlit : 1);
       ok = ok && pos < nb;
     }
-    // the sequences section: kZfFseTailChunks chunks from the one holding its first byte
+    // the sequences section: kZfFseRegChunks chunks from the one holding its first byte, into
+    // registers; the first kZfFseHdrChunks into the window (the head is done with)
     const uint32_t s = body + pos;
     const uint32_t c_lo = (shift + s) >> 4;
-    const uint32_t wend = 16 * (c_lo + kZfFseTailChunks) - shift;
-    ok = ok && body + nb + (h.checksum ? 4u : 0u) <= wend;
+    const uint32_t qend = body + nb + (h.checksum ? 4u : 0u);  // the frame's bytes this parse reads
+    ok = ok && qend <= 16 * (c_lo + kZfFseRegChunks) - shift;
+    v4u R[kZfFseRegChunks];
+#pragma unroll
+    for (uint32_t k = 0; k < kZfFseRegChunks; k++) R[k] = ok && c_lo + k <= lastc ? gal[c_lo + k] : zero4;
     if (ok) {
 #pragma unroll
-      for (uint32_t k = 0; k < kZfFseTailChunks; k++) lds_put16(tb0 + 16 * k, c_lo + k <= lastc ? gal[c_lo + k] : zero4);
+      for (uint32_t k = 0; k < kZfFseHdrChunks; k++) lds_put16(tb0 + 16 * k, R[k]);
     }
-    const uint8_t* tb = tb0 + shift - 16 * c_lo;  // tb[i] = frame byte i for i in [s, wend)
+    const uint8_t* tb = tb0 + shift - 16 * c_lo;  // tb[i] = frame byte i for i in [s, 16 (c_lo + 4) - shift)
     const int32_t tofs = int32_t(shift) - int32_t(16 * c_lo);  // frame byte i = tb0[i + tofs]
+    const int32_t hend = int32_t(16 * kZfFseHdrChunks) - tofs;  // the header chunks' end, in frame bytes
     uint32_t nseq = 0, produced = 0;
     v4u qv = {0, 0, 0, 0};  // the current group of four records
     uint32_t* seqs = z.seq + size_t(b) * kZfSeqSlot;
@@ -790,34 +814,44 @@ __global__ __launch_bounds__(kZfFseThreads) __attribute__((amdgpu_waves_per_eu(1
       // the three tables, LL / OF / ML as they follow each other, back to back in the lane's LDS
       uint32_t al_ll = 0, al_of = 0, al_ml = 0, t_of = 0, t_ml = 0;
       if (ok) {
-        const int u = zf_table16(m_ll, tb0, int32_t(s + sp) + tofs, sn - sp, kZsLLDef, 36, 6, 35, tab, kZfFseTab, norm,
-                                 next);
+        const int u = zf_table16(m_ll, tb0, int32_t(s + sp) + tofs, zf_hdr_n(s + sp, sn - sp, hend), kZsLLDef, 36, 6, 35, tab,
+                                 kZfFseTab, norm, next);
         ok = u >= 0;
         sp += ok ? uint32_t(u & 0xFFFF) : 0u;
         al_ll = ok ? uint32_t(u >> 16) : 0u;
       }
       if (ok) {
         t_of = 1u << al_ll;
-        const int u = zf_table16(m_of, tb0, int32_t(s + sp) + tofs, sn - sp, kZsOFDef, 29, 5, 31, tab + t_of,
-                                 kZfFseTab - t_of, norm, next);
+        const int u = zf_table16(m_of, tb0, int32_t(s + sp) + tofs, zf_hdr_n(s + sp, sn - sp, hend), kZsOFDef, 29, 5, 31,
+                                 tab + t_of, kZfFseTab - t_of, norm, next);
         ok = u >= 0;
         sp += ok ? uint32_t(u & 0xFFFF) : 0u;
         al_of = ok ? uint32_t(u >> 16) : 0u;
       }
       if (ok) {
         t_ml = t_of + (1u << al_of);
-        const int u = zf_table16(m_ml, tb0, int32_t(s + sp) + tofs, sn - sp, kZsMLDef, 53, 6, 52, tab + t_ml,
-                                 kZfFseTab - t_ml, norm, next);
+        const int u = zf_table16(m_ml, tb0, int32_t(s + sp) + tofs, zf_hdr_n(s + sp, sn - sp, hend), kZsMLDef, 53, 6, 52,
+                                 tab + t_ml, kZfFseTab - t_ml, norm, next);
         ok = u >= 0;
         sp += ok ? uint32_t(u & 0xFFFF) : 0u;
         al_ml = ok ? uint32_t(u >> 16) : 0u;
       }
       ok = ok && !(dbg_bits(a) & (1u << 18));  // profiling: the tables only (every block handed back)
+      // the bitstream's chunks from the registers into the window (over the headers and the scratch)
+      const uint32_t d = ((shift + s + sp) >> 4) - c_lo;
+      ok = ok && d + kZfFseBitChunks <= kZfFseRegChunks && qend <= 16 * (c_lo + d + kZfFseBitChunks) - shift;
+      if (ok) {
+#pragma unroll
+        for (uint32_t k = 0; k < kZfFseRegChunks; k++)
+          if (k >= d && k < d + kZfFseBitChunks) lds_put16(tb0 + 16 * (k - d), R[k]);
+      }
+      tb -= 16 * d;  // tb[i] = frame byte i for i in [s + sp, qend)
       // zs_bstart
       const uint32_t bn = ok ? sn - sp : 0u;
       const uint32_t last = bn ? uint32_t(tb[s + sn - 1]) : 0u;
       ok = ok && last != 0;
-      ZfBits bits{tb0, 8 * int64_t(int32_t(s + sp) + tofs), ok ? 8 * int64_t(bn - 1) + (31 - __builtin_clz(last)) : 0};
+      ZfBits bits{tb0, 8 * (int64_t(int32_t(s + sp) + tofs) - 16 * int64_t(d)),
+                  ok ? 8 * int64_t(bn - 1) + (31 - __builtin_clz(last)) : 0};
       uint32_t sll = 0, sof = 0, sml = 0;
       ZfReg rg{};
       if (ok) {
@@ -1537,7 +1571,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const uint32_t grid_a = min((a.n + kZfParseThreads - 1) / kZfParseThreads, uint32_t(num_cus) * 2u);
   zs_fast_parse_kernel<<<grid_a, kZfParseThreads, lds_a, st>>>(a, z);
   // phase A': the blocks phase A listed for the FSE parse (three one-wave workgroups per CU)
-  zs_fse_parse_kernel<<<uint32_t(num_cus) * 3u, kZfFseThreads, size_t(kZfFseThreads) * kZfFseLane, st>>>(a, z);
+  zs_fse_parse_kernel<<<uint32_t(num_cus) * kZfFseWgs, kZfFseThreads, size_t(kZfFseThreads) * kZfFseLane, st>>>(a, z);
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
