@@ -1570,7 +1570,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const size_t lds_a = zstd_fast_parse_lds();
   const uint32_t grid_a = min((a.n + kZfParseThreads - 1) / kZfParseThreads, uint32_t(num_cus) * 2u);
   zs_fast_parse_kernel<<<grid_a, kZfParseThreads, lds_a, st>>>(a, z);
-  // phase A': the blocks phase A listed for the FSE parse (three one-wave workgroups per CU)
+  // phase A': the blocks phase A listed for the FSE parse (four one-wave workgroups per CU)
   zs_fse_parse_kernel<<<uint32_t(num_cus) * kZfFseWgs, kZfFseThreads, size_t(kZfFseThreads) * kZfFseLane, st>>>(a, z);
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
