@@ -223,3 +223,53 @@ def test_kv100_fse_large_batch(ctx):
     meta = _compare(ctx, blocks, misalign=9)
     assert (meta["status"] == 0).all()
     assert ctx.handbacks() == 0
+
+
+def _short_sequences(rng, n):
+    """Bytes of many short literal runs and matches of every length 3..140 (long FSE table
+    descriptions and long sequence bitstreams)."""
+    out = bytearray(rng.randbytes(64))
+    while len(out) < n:
+        out += rng.randbytes(rng.choice([0, 1, 2, 3, 5, 8, 13, 21, 34]))
+        m, o = rng.randint(3, 140), rng.randint(1, min(len(out), 2000))
+        s = len(out) - o
+        for i in range(m):
+            out.append(out[s + i])
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize("misalign", [0, 6, 11, 15])
+def test_fse_window_limits(ctx, misalign):
+    """Phase A''s LDS window (zstd_fast.hip zs_fse_parse_kernel: the table descriptions within the 4
+    chunks from the sequences section's first, the bitstream within the 10 from its own first):
+    frames of many short sequences, raw and as SST blocks, at this alignment.  tests/zsection.py
+    measures each frame's section; the set holds frames A' would take that run past each limit and
+    frames within both.  Every status and decoded byte is the oracle's, and the frames past a limit
+    are handed to the exact path."""
+    from tests import zsection
+    rng = random.Random(40 + misalign)
+    blocks = [_crc(_z(_short_sequences(rng, 4000), rng.choice([3, 19]))) for _ in range(96)]
+    stream = _short_sequences(rng, 120000)
+    kvs, p = [], 0
+    for i in range(700):
+        m = rng.randint(30, 300)
+        kvs.append((b"key%08d" % i, stream[p:p + m]))
+        p += m
+    blocks += [_crc(_z(b[:-4], rng.choice([3, 9, 19]))) for b in bg.sst_blocks(kvs, 4096, ob.NONE)]
+    _, off = bg.pack(blocks, misalign)
+    past_hdr = past_bits = fits = 0
+    for i, blk in enumerate(blocks):
+        z = zsection.section_shape(blk[:-4], int(off[i]) & 15)
+        if z is None or z["nseq"] > 128 or max(z["logs"]) > 7 or z["logs"][0] > 6 or z["logs"][1] > 5:
+            continue
+        if z["hdr_end_in_chunk"] > 64:
+            past_hdr += 1
+        elif z["chunks_from_bitstream"] > 10:
+            past_bits += 1
+        else:
+            fits += 1
+    assert past_hdr and past_bits and fits, (past_hdr, past_bits, fits)
+    ctx.handbacks(reset=True)
+    meta = _compare(ctx, blocks, misalign=misalign)
+    assert all(x == 0 or 3 <= x <= 7 for x in meta["status"].tolist()), meta["status"]  # (decoded: bytes compared)
+    assert ctx.handbacks() >= past_hdr + past_bits
