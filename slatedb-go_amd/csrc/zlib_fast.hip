@@ -14,8 +14,10 @@
 // canonical Huffman decoding (RFC 1951 3.2.2) as in zlib's puff: the code of length L is found by
 // comparing the bit-reversed 15-bit peek with the left-justified limits of lengths 1..14 held in
 // registers, and the symbol read from the lane's table of symbols sorted by (length, value) in LDS
-// (literal/length 288 x u16, distance 32 x u8, code-length 20 x u8: 628 bytes per lane, four waves
-// per CU).  The dynamic header's code lengths are decoded twice (count, then place), so no length
+// (literal/length 288 x u8, distance 32 x u8, code-length 20 x u8: 340 bytes per lane; one-wave
+// workgroups, seven per CU).  A literal/length table byte is the symbol's low 8 bits: within one
+// code length the literals sort before 256..287, so the symbol is >= 256 exactly when its sorted
+// index reaches that length's first non-literal slot (per length, in registers).  The dynamic header's code lengths are decoded twice (count, then place), so no length
 // array is kept.  Only complete codes are taken; a stored block with data, a distance beyond the
 // output or the 4 KiB record limit, more than 128 sequences, a literal run of 1024 or more, a
 // truncated or over-long stream, or anything else unusual is handed to the exact path
@@ -28,13 +30,14 @@ namespace slate {
 
 namespace {
 
-constexpr uint32_t kZlThreads = 256;   // four waves, one workgroup per CU (LDS)
-constexpr uint32_t kZlLane = 628;      // per-lane tables (bytes; 157 dwords: lanes on distinct banks)
-constexpr uint32_t kZlDistOff = 576, kZlClOff = 608;
-constexpr uint32_t kZlFixLit = 0, kZlFixDist = 576;  // the workgroup's fixed-code tables (shared)
-constexpr uint32_t kZlFixBytes = 640;
+constexpr uint32_t kZlThreads = 64;    // one wave per workgroup
+constexpr uint32_t kZlWgPerCu = 7;     // (LDS)
+constexpr uint32_t kZlLane = 340;      // per-lane tables (bytes; 85 dwords: lanes on distinct banks)
+constexpr uint32_t kZlDistOff = 288, kZlClOff = 320;
+constexpr uint32_t kZlFixLit = 0, kZlFixDist = 288;  // the workgroup's fixed-code tables
+constexpr uint32_t kZlFixBytes = 320;
 constexpr uint32_t kZlLds = kZlFixBytes + kZlThreads * kZlLane;
-static_assert(kZlLds <= 163840, "one workgroup per CU");
+static_assert(kZlWgPerCu * kZlLds <= 163840, "workgroups per CU");
 constexpr uint32_t kZlMaxOut = kZsFastOutCap;  // the build phase's LDS window
 constexpr uint32_t kZlMaxSeqs = kZsFseSeqs;    // two records per lane in the build phase
 
@@ -182,7 +185,7 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t s) {
 
 // one wave: the fixed codes' sorted tables (RFC 1951 3.2.6) into the workgroup's shared area
 __device__ void zl_fixed_tables(uint8_t* smem, uint32_t lane) {
-  uint16_t* lit = reinterpret_cast<uint16_t*>(smem + kZlFixLit);
+  uint8_t* lit = smem + kZlFixLit;
   // sorted by (length, symbol): 256..279 (7 bits), 0..143 and 280..287 (8), 144..255 (9)
   for (uint32_t i = lane; i < 288; i += 64) {
     uint32_t s;
@@ -190,9 +193,18 @@ __device__ void zl_fixed_tables(uint8_t* smem, uint32_t lane) {
     else if (i < 24 + 144) s = i - 24;
     else if (i < 24 + 144 + 8) s = 280 + (i - 168);
     else s = 144 + (i - 176);
-    lit[i] = uint16_t(s);
+    lit[i] = uint8_t(s);
   }
   if (lane < 32) smem[kZlFixDist + lane] = uint8_t(lane);
+}
+// the fixed literal/length code's first non-literal slot per length (packed as zl_put's fields):
+// length 7 at 0 (256..279), length 8 at 168 (after 24 + 144 literals), length 9 none (288)
+constexpr uint64_t kZlFixHi0 = 0, kZlFixHi1 = 168ull | (288ull << 9), kZlFixHi2 = 0;
+// the symbol of a literal/length table byte: + 256 from the length's first non-literal slot
+__device__ __forceinline__ uint32_t zl_hi_at(const uint64_t (&hi)[3], uint32_t L) {
+  const uint32_t q = L - 1, w = q >= 14 ? 2u : (q >= 7 ? 1u : 0u), sh = 9 * (q - 7 * w);
+  const uint64_t word = w == 0 ? hi[0] : (w == 1 ? hi[1] : hi[2]);
+  return uint32_t(word >> sh) & 511u;
 }
 __device__ __forceinline__ void zl_fixed_counts(ZlTab& tl, ZlTab& td) {
   uint32_t cl[16] = {}, cd[16] = {};
@@ -211,7 +223,7 @@ __device__ __forceinline__ void zl_fixed_counts(ZlTab& tl, ZlTab& td) {
 // otherwise the literal bytes to the output slot, the sequences and the record (failures to
 // z.list for the exact path).
 template <bool kPlan>
-__global__ __launch_bounds__(kZlThreads) void zl_fast_kernel(DecodeArgs a, ZsFastArgs z, uint64_t* out_sz,
+__global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zl_fast_kernel(DecodeArgs a, ZsFastArgs z, uint64_t* out_sz,
                                                              uint64_t* row_sz, uint32_t* plist, uint32_t* pcount) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   if (threadIdx.x < 64) zl_fixed_tables(smem, threadIdx.x);
@@ -308,6 +320,7 @@ __global__ __launch_bounds__(kZlThreads) void zl_fast_kernel(DecodeArgs a, ZsFas
       dyn = dyn && ok;
       ZlTab tl, td;  // the block's tables (dynamic: built below; fixed: set after)
       bool own = false;  // the lane's own (dynamic) tables
+      uint64_t hi_dyn[3] = {0, 0, 0};  // the dynamic literal/length table's first non-literal slots
       if (__ballot(dyn)) {
         // HLIT, HDIST, HCLEN, then the code-length code's lengths (3 bits each, in kZlClOrder)
         zl_refill(zi, R, irel, dyn);
@@ -347,7 +360,7 @@ __global__ __launch_bounds__(kZlThreads) void zl_fast_kernel(DecodeArgs a, ZsFas
         }
         // the literal/length and distance code lengths, twice: counted, then placed
         const ZlIn save = zi;
-        uint64_t cntl[3] = {0, 0, 0}, cntd[3] = {0, 0, 0}, nxl[3], nxd[3];
+        uint64_t cntl[3] = {0, 0, 0}, cntd[3] = {0, 0, 0}, cnt8[3] = {0, 0, 0}, nxl[3], nxd[3];
         bool eob = false;  // length of symbol 256 nonzero
         for (uint32_t pass = 0; pass < 2; pass++) {
           if (pass == 1) {
@@ -356,6 +369,10 @@ __global__ __launch_bounds__(kZlThreads) void zl_fast_kernel(DecodeArgs a, ZsFas
             zl_unpack(cntl, cl16);
             zl_unpack(cntd, cd16);
             const bool cl_ok = zl_canon(cl16, tl, nxl), cd_ok = zl_canon(cd16, td, nxd);
+            // each length's first slot + its literals (fields < 512: no carries between them)
+            hi_dyn[0] = nxl[0] + cnt8[0];
+            hi_dyn[1] = nxl[1] + cnt8[1];
+            hi_dyn[2] = nxl[2] + cnt8[2];
             ok = ok && !(dyn && (!cl_ok || !cd_ok || !eob));
             dyn = dyn && ok;
           }
@@ -391,13 +408,15 @@ __global__ __launch_bounds__(kZlThreads) void zl_fast_kernel(DecodeArgs a, ZsFas
               if (pass == 0) {
                 zl_count(cntl, val, nlit);
                 zl_count(cntd, val, nd);
+                const uint32_t l8 = min(hlit, 256u);  // the literals 0..255 among them
+                zl_count(cnt8, val, i < l8 ? min(i + rep, l8) - i : 0u);
                 eob = eob || (val != 0 && i <= 256 && 256 < i + nlit);
               } else if (val != 0) {
                 for (uint32_t j = 0; j < rep; j++) {  // (rep <= 138; usually 1)
                   const uint32_t s = i + j;
                   if (s < hlit) {
                     const uint32_t p = zl_put(nxl, val);
-                    reinterpret_cast<uint16_t*>(my16)[p] = uint16_t(s);
+                    my16[p] = uint8_t(s);
                   } else {
                     const uint32_t p = zl_put(nxd, val);
                     my16[kZlDistOff + p] = uint8_t(s - hlit);
@@ -427,13 +446,13 @@ __global__ __launch_bounds__(kZlThreads) void zl_fast_kernel(DecodeArgs a, ZsFas
       kmax = __builtin_amdgcn_readfirstlane(kmax);
       const uint32_t tlit = own ? uint32_t(mine - smem) : kZlFixLit;
       const uint32_t tdist = own ? uint32_t(mine - smem) + kZlDistOff : kZlFixDist;
+      const uint64_t hi[3] = {own ? hi_dyn[0] : kZlFixHi0, own ? hi_dyn[1] : kZlFixHi1, own ? hi_dyn[2] : kZlFixHi2};
       while (__ballot(inb)) {
         zl_refill(zi, R, irel, inb);
         uint32_t L = 1, idx = 0;
         zl_find2(zi, tl, td, st == 1, kmax, L, idx);
-        const uint32_t adr = st == 1 ? tdist + min(idx, 31u) : tlit + 2 * min(idx, 287u);
-        const uint32_t raw = *reinterpret_cast<const uint16_t*>(smem + (adr & ~1u));
-        const uint32_t sym = st == 1 ? ((adr & 1) ? raw >> 8 : raw & 0xFFu) : raw;
+        const uint32_t adr = st == 1 ? tdist + min(idx, 31u) : tlit + min(idx, 287u);
+        const uint32_t sym = uint32_t(smem[adr]) + ((st == 0 && idx >= zl_hi_at(hi, L)) ? 256u : 0u);
         if (inb) (void)zl_take(zi, L);
         const bool lit = inb && st == 0 && sym < 256;
         const bool end = inb && st == 0 && sym == 256;
@@ -526,7 +545,7 @@ hipError_t launch_zlib_fast_parse(hipStream_t st, const DecodeArgs& a, const ZsF
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zl_fast_kernel<false>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kZlLds));
   if (attr != hipSuccess) return attr;
-  const uint32_t grid = min((a.n + kZlThreads - 1) / kZlThreads, uint32_t(num_cus));
+  const uint32_t grid = min((a.n + kZlThreads - 1) / kZlThreads, uint32_t(num_cus) * kZlWgPerCu);
   zl_fast_kernel<false><<<grid, kZlThreads, kZlLds, st>>>(a, z, nullptr, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
@@ -542,7 +561,7 @@ hipError_t launch_zlib_plan_fast(hipStream_t st, const uint8_t* in, const uint64
   a.in_off = in_off;
   a.n = n;
   ZsFastArgs z{};
-  const uint32_t grid = min((n + kZlThreads - 1) / kZlThreads, uint32_t(num_cus > 0 ? num_cus : 256));
+  const uint32_t grid = min((n + kZlThreads - 1) / kZlThreads, uint32_t(num_cus > 0 ? num_cus : 256) * kZlWgPerCu);
   zl_fast_kernel<true><<<grid, kZlThreads, kZlLds, st>>>(a, z, out_sz, row_sz, list, count);
   return hipGetLastError();
 }
