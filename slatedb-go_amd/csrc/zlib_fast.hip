@@ -14,8 +14,9 @@
 // canonical Huffman decoding (RFC 1951 3.2.2) as in zlib's puff: the code of length L is found by
 // comparing the bit-reversed 15-bit peek with the left-justified limits of lengths 1..14 held in
 // registers, and the symbol read from the lane's table of symbols sorted by (length, value) in LDS
-// (literal/length 288 x u8, distance 32 x u8, code-length 20 x u8: 340 bytes per lane; one-wave
-// workgroups, seven per CU).  A literal/length table byte is the symbol's low 8 bits: within one
+// (literal/length 288 x u8 and distance 32 x u8: 320 bytes per lane, byte k of lane l's tables at
+// LDS byte 64 k + l; the code-length code's 19 sorted symbols in two registers, the fixed codes'
+// tables computed; one-wave workgroups, eight per CU: the LDS exactly full).  A literal/length table byte is the symbol's low 8 bits: within one
 // code length the literals sort before 256..287, so the symbol is >= 256 exactly when its sorted
 // index reaches that length's first non-literal slot (per length, in registers).  The dynamic header's code lengths are decoded twice (count, then place), so no length
 // array is kept.  Only complete codes are taken; a stored block with data, a distance beyond the
@@ -31,12 +32,10 @@ namespace slate {
 namespace {
 
 constexpr uint32_t kZlThreads = 64;    // one wave per workgroup
-constexpr uint32_t kZlWgPerCu = 7;     // (LDS)
-constexpr uint32_t kZlLane = 340;      // per-lane tables (bytes; 85 dwords: lanes on distinct banks)
-constexpr uint32_t kZlDistOff = 288, kZlClOff = 320;
-constexpr uint32_t kZlFixLit = 0, kZlFixDist = 288;  // the workgroup's fixed-code tables
-constexpr uint32_t kZlFixBytes = 320;
-constexpr uint32_t kZlLds = kZlFixBytes + kZlThreads * kZlLane;
+constexpr uint32_t kZlWgPerCu = 8;     // (LDS)
+constexpr uint32_t kZlLane = 320;      // per-lane tables (bytes)
+constexpr uint32_t kZlDistOff = 288;
+constexpr uint32_t kZlLds = kZlThreads * kZlLane;
 static_assert(kZlWgPerCu * kZlLds <= 163840, "workgroups per CU");
 constexpr uint32_t kZlMaxOut = kZsFastOutCap;  // the build phase's LDS window
 constexpr uint32_t kZlMaxSeqs = kZsFseSeqs;    // two records per lane in the build phase
@@ -183,23 +182,11 @@ __device__ __forceinline__ uint32_t dist_base(uint32_t s) {
   return s < 4 ? s + 1 : ((2u + (s & 1u)) << ((s >> 1) - 1)) + 1u;
 }
 
-// one wave: the fixed codes' sorted tables (RFC 1951 3.2.6) into the workgroup's shared area
-__device__ void zl_fixed_tables(uint8_t* smem, uint32_t lane) {
-  uint8_t* lit = smem + kZlFixLit;
-  // sorted by (length, symbol): 256..279 (7 bits), 0..143 and 280..287 (8), 144..255 (9)
-  for (uint32_t i = lane; i < 288; i += 64) {
-    uint32_t s;
-    if (i < 24) s = 256 + i;
-    else if (i < 24 + 144) s = i - 24;
-    else if (i < 24 + 144 + 8) s = 280 + (i - 168);
-    else s = 144 + (i - 176);
-    lit[i] = uint8_t(s);
-  }
-  if (lane < 32) smem[kZlFixDist + lane] = uint8_t(lane);
+// the fixed codes' symbol at sorted index ci (RFC 1951 3.2.6; sorted by (length, symbol):
+// 256..279 (7 bits), 0..143 and 280..287 (8), 144..255 (9); distances: the index)
+__device__ __forceinline__ uint32_t zl_fixed_sym(bool dist, uint32_t ci) {
+  return dist ? ci : (ci < 24 ? ci + 256 : (ci < 168 ? ci - 24 : (ci < 176 ? ci + 112 : ci - 32)));
 }
-// the fixed literal/length code's first non-literal slot per length (packed as zl_put's fields):
-// length 7 at 0 (256..279), length 8 at 168 (after 24 + 144 literals), length 9 none (288)
-constexpr uint64_t kZlFixHi0 = 0, kZlFixHi1 = 168ull | (288ull << 9), kZlFixHi2 = 0;
 // the symbol of a literal/length table byte: + 256 from the length's first non-literal slot
 __device__ __forceinline__ uint32_t zl_hi_at(const uint64_t (&hi)[3], uint32_t L) {
   const uint32_t q = L - 1, w = q >= 14 ? 2u : (q >= 7 ? 1u : 0u), sh = 9 * (q - 7 * w);
@@ -226,11 +213,9 @@ template <bool kPlan>
 __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zl_fast_kernel(DecodeArgs a, ZsFastArgs z, uint64_t* out_sz,
                                                              uint64_t* row_sz, uint32_t* plist, uint32_t* pcount) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (threadIdx.x < 64) zl_fixed_tables(smem, threadIdx.x);
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave_lane0 = threadIdx.x - lane;
-  uint8_t* mine = smem + kZlFixBytes + threadIdx.x * kZlLane;
+  uint8_t* mine = smem + threadIdx.x;  // byte k of this lane's tables at mine[64 k]
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t r0 = blockIdx.x * blockDim.x + wave_lane0; r0 < a.n; r0 += stride) {
     const uint32_t b = r0 + lane;
@@ -289,7 +274,6 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     uint32_t o = 0, nl = 0, ll = 0, nseq = 0;
     v4u lbuf = {0, 0, 0, 0}, qv = {0, 0, 0, 0};
     bool more = ok;  // deflate blocks left
-    uint8_t* my16 = mine;  // (LDS tables of this lane)
     while (__ballot(more)) {
       // ---- a block header
       zl_refill(zi, R, irel, more);
@@ -349,14 +333,17 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
           for (uint32_t k = 1; k < 8; k++) cc[k] += l == k ? 1u : 0u;
         }
         ZlTab tc;
-        uint64_t cn[3];
+        uint64_t cn[3], clw0 = 0, clw1 = 0;  // the sorted code-length symbols, 5 bits each
         ok = ok && !(dyn && !zl_canon(cc, tc, cn));
         dyn = dyn && ok;
 #pragma unroll
         for (uint32_t s = 0; s < 19; s++) {
           const uint32_t l = uint32_t(clp >> (3 * s)) & 7u;
           const uint32_t p = zl_put(cn, l);
-          if (dyn && l) my16[kZlClOff + p] = uint8_t(s);
+          if (dyn && l) {
+            clw0 |= p < 12 ? uint64_t(s) << (5 * p) : 0ull;
+            clw1 |= p >= 12 ? uint64_t(s) << (5 * (p - 12)) : 0ull;
+          }
         }
         // the literal/length and distance code lengths, twice: counted, then placed
         const ZlIn save = zi;
@@ -383,7 +370,8 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
             zl_refill(zi, R, irel, go);
             uint32_t L = 1, idx = 0;
             zl_find<7>(zi, tc, L, idx);
-            const uint32_t sym = go ? uint32_t(my16[kZlClOff + min(idx, 19u)]) : 0u;
+            const uint32_t ci = min(idx, 18u);
+            const uint32_t sym = go ? uint32_t((ci < 12 ? clw0 >> (5 * ci) : clw1 >> (5 * (ci - 12))) & 31u) : 0u;
             if (go) (void)zl_take(zi, L);
             uint32_t rep = 1, val = sym;
             const uint32_t xb = sym == 16 ? 2u : (sym == 17 ? 3u : (sym == 18 ? 7u : 0u));
@@ -416,10 +404,10 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
                   const uint32_t s = i + j;
                   if (s < hlit) {
                     const uint32_t p = zl_put(nxl, val);
-                    my16[p] = uint8_t(s);
+                    mine[64 * p] = uint8_t(s);
                   } else {
                     const uint32_t p = zl_put(nxd, val);
-                    my16[kZlDistOff + p] = uint8_t(s - hlit);
+                    mine[64 * (kZlDistOff + p)] = uint8_t(s - hlit);
                   }
                 }
               }
@@ -444,15 +432,13 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       uint32_t kmax = inb ? max(tl.maxl, td.maxl) : 1u;
       for (int sh = 32; sh >= 1; sh >>= 1) kmax = max(kmax, uint32_t(__shfl_xor(int(kmax), sh, 64)));
       kmax = __builtin_amdgcn_readfirstlane(kmax);
-      const uint32_t tlit = own ? uint32_t(mine - smem) : kZlFixLit;
-      const uint32_t tdist = own ? uint32_t(mine - smem) + kZlDistOff : kZlFixDist;
-      const uint64_t hi[3] = {own ? hi_dyn[0] : kZlFixHi0, own ? hi_dyn[1] : kZlFixHi1, own ? hi_dyn[2] : kZlFixHi2};
       while (__ballot(inb)) {
         zl_refill(zi, R, irel, inb);
         uint32_t L = 1, idx = 0;
         zl_find2(zi, tl, td, st == 1, kmax, L, idx);
-        const uint32_t adr = st == 1 ? tdist + min(idx, 31u) : tlit + min(idx, 287u);
-        const uint32_t sym = uint32_t(smem[adr]) + ((st == 0 && idx >= zl_hi_at(hi, L)) ? 256u : 0u);
+        const uint32_t ci = st == 1 ? min(idx, 31u) : min(idx, 287u);
+        const uint32_t tb = uint32_t(mine[64 * ((st == 1 ? kZlDistOff : 0u) + ci)]);  // (own tables)
+        const uint32_t sym = own ? tb + ((st == 0 && idx >= zl_hi_at(hi_dyn, L)) ? 256u : 0u) : zl_fixed_sym(st == 1, ci);
         if (inb) (void)zl_take(zi, L);
         const bool lit = inb && st == 0 && sym < 256;
         const bool end = inb && st == 0 && sym == 256;
