@@ -256,6 +256,7 @@ def main():
         result["kv100_zstd"] = kv100_leg(sc, ctx, stream, wl, args, threads, sc.ZSTD)
         result["kv100_zlib"] = kv100_leg(sc, ctx, stream, wl, args, threads, sc.ZLIB)
         result["configs2_encode"] = encode_leg(sc, ctx, args)
+        result["compaction"] = compaction_leg(sc, ctx, args)
         # the unchanged per-block reader path (one GPU round trip per 4 KiB block) and BASELINE
         # configs[0] (one 64-block CodecNone SST encoded + decoded), next to the oracle on one thread
         from oracle import binding as ob
@@ -562,6 +563,77 @@ def encode_leg(sc, ctx, args):
     for x in (d_keys, d_vals, d_ko, d_vo):
         x.free()
     res["workload"] = "configs[2]: 10 M x 100 B KV (keys k%015d, V-half values) -> SST blocks + bloom, BlockSize 4096"
+    return res
+
+
+def compaction_leg(sc, ctx, args, kv_per_sst=2_500_000, k=4, max_sst=256 << 20):
+    """executeCompaction (slatedb/compaction/executor.go:92-151) end to end: k L0 SSTs of kv_per_sst
+    KV each (keys k%015d over a shared key space with 30 % overlap, 84 B V-half values), host SST
+    bytes in (the object-store GET buffers) -> slate_compact (decode -> row views -> MergeSort ->
+    gather -> SST builders cut at MaxSSTSize) -> host SST bytes out, per codec (CodecNone = the DB's
+    default, CodecSnappy).  Outputs bit-exact against the oracle's C restatement of the same loop
+    (oracle/compact_oracle.c), which is also the CPU baseline, on one thread and on every CPU."""
+    from oracle import binding as ob
+    from tools import bench_compact as bc
+    res = {"workload": f"{k} L0 SSTs x {kv_per_sst} KV (100 B: k%015d keys, 84 B V-half values, 30 % key overlap), "
+                       f"MaxSSTSize {max_sst >> 20} MiB, output codec = input codec",
+           "unit": "input KV/s"}
+    threads = host_cpus()
+    for codec, name in ((sc.NONE, "none"), (sc.SNAPPY, "snappy")):
+        srcs = bc.make_sources(sc, ctx, k, kv_per_sst, 0.3, codec)
+        # the GET buffers as a cgo caller holds them: one host array, SST offsets, source ranges
+        ssts = [x for run in srcs for x in run]
+        blob = np.frombuffer(b"".join(ssts), np.uint8)
+        sst_off = np.zeros(len(ssts) + 1, np.uint64)
+        sst_off[1:] = np.cumsum([len(x) for x in ssts])
+        src_sst = np.arange(len(srcs) + 1, dtype=np.uint32)
+        in_bytes = int(blob.size)
+        sink = np.empty(in_bytes + (1 << 20), np.uint8)  # the PUT buffers, reused
+        sink.fill(0)
+        sc.compact_arrays(ctx, blob, sst_off, src_sst, max_sst, codec=codec, sink=sink)  # warm-up
+        walls, busy, out = [], [], None
+        for _ in range(3):
+            ctx.synchronize()
+            ctx.set_timing(True)
+            ctx.gpu_busy_ms(reset=True)
+            t0 = time.perf_counter()
+            out = sc.compact_arrays(ctx, blob, sst_off, src_sst, max_sst, codec=codec, sink=sink)
+            walls.append(time.perf_counter() - t0)
+            busy.append(ctx.gpu_busy_ms(reset=True))
+            ctx.set_timing(False)
+        # the oracle: the same inputs, the same loop, one thread and every CPU
+        oc = ob.NONE if codec == sc.NONE else ob.SNAPPY
+        t0 = time.perf_counter()
+        st, ref, ref_off = ob.compact_arrays(blob, sst_off, src_sst, max_sst, oc, 1)
+        cpu1 = time.perf_counter() - t0
+        assert st == 0, ob.status_string(st)
+        t0 = time.perf_counter()
+        st, ref_mt, _ = ob.compact_arrays(blob, sst_off, src_sst, max_sst, oc, threads)
+        cpu_mt = time.perf_counter() - t0
+        assert st == 0, ob.status_string(st)
+        got = b"".join(o.tobytes() for o in out)
+        exact = (len(out) == len(ref_off) - 1 and got == ref.tobytes() and ref.tobytes() == ref_mt.tobytes() and
+                 all(len(o) == int(ref_off[i + 1] - ref_off[i]) for i, o in enumerate(out)))
+        assert exact, f"compaction {name}: output SSTs differ from the oracle"
+        n_in = k * kv_per_sst
+        wall = float(np.median(walls))
+        res[name] = {"value": round(n_in / wall, 1), "s_wall": round(wall, 4),
+                     "device_busy_ms": round(float(np.median([b[0] for b in busy])), 3),
+                     "device_busy_ms_summed": round(float(np.median([b[1] for b in busy])), 3),
+                     "input_sst_bytes": in_bytes, "output_ssts": len(out), "output_sst_bytes": len(got),
+                     "bit_exact": exact,
+                     "cpu_baseline": {"value": round(n_in / cpu1, 1), "unit": "input KV/s", "cores": 1, "kind": "port",
+                                      "s": round(cpu1, 3), "value_all_threads": round(n_in / cpu_mt, 1),
+                                      "threads": threads, "s_all_threads": round(cpu_mt, 3),
+                                      "sample": "the same inputs through oracle/compact_oracle.c (or_compact: "
+                                                "block.Decode + block.Iterator keys, iter.MergeSort, the MaxSSTSize "
+                                                "writer loop); all-threads: blocks decoded and outputs built in "
+                                                "parallel, the merge serial"}}
+        del srcs, blob, ref, ref_mt, out
+    res["time"] = ("s_wall: the slate_compact call from host SST bytes to host SST bytes (uploads, every device "
+                   "stage, the output builders) plus slate_sst_table_encode of every output into a reused PUT "
+                   "buffer; device_busy_ms: the union of HIP-event spans around its kernel groups "
+                   "(slate_ctx_gpu_busy)")
     return res
 
 

@@ -233,9 +233,10 @@ int slate_ctx_set_copy_threads(slate_ctx* ctx, uint32_t threads);
  * groups on the filter's side stream overlap the flush, so the sum can exceed the wall time. */
 int slate_ctx_set_timing(slate_ctx* ctx, int on);
 /* Observability (no Go counterpart): the number of blocks this context's decodes handed from a fast
- * path (CodecZstd, CodecLz4) to the exact wave-per-block decoder since the context was made or the
- * count last reset (reset != 0 zeroes it).  Waits for the context's stream.  The results are the
- * same either way; a hand-back only costs time. */
+ * path (CodecZstd, CodecZlib, CodecLz4) to the exact wave-per-block decoder since the context was
+ * made or the count last reset (reset != 0 zeroes it).  Waits for every stream of the context
+ * (its stream, side stream, pipeline lanes).  The results are the same either way; a hand-back
+ * only costs time. */
 int slate_ctx_handbacks(slate_ctx* ctx, uint64_t* n, int reset);
 int slate_ctx_gpu_time(slate_ctx* ctx, double* ms, int reset);
 /* The same spans' union (*busy_ms: device time with overlapping spans of the side streams counted
@@ -283,6 +284,10 @@ int slate_devbuf_download_async(slate_ctx* ctx, slate_hostbuf* dst, uint64_t dst
  *   of block i at d_out + d_out_off[i], its meta and its row descriptors.
  * Both enqueue on the context stream and return without synchronising. */
 size_t slate_decode_scratch_bytes(uint32_t n_blocks);
+/* The scratch one codec needs (<= slate_decode_scratch_bytes): CodecNone / CodecSnappy batches
+ * skip the Zstd / Zlib / LZ4 fast paths' records and sequence slots (~8 B per block instead of
+ * ~560).  Scratch sized this way may be used only with that codec. */
+size_t slate_decode_scratch_bytes_codec(uint32_t n_blocks, int codec);
 int slate_block_decode_plan_device(slate_ctx* ctx, int codec, const uint8_t* d_in,
                                    const uint64_t* d_in_off, uint32_t n_blocks,
                                    uint64_t* d_out_off, uint64_t* d_row_base, void* d_scratch);

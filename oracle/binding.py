@@ -139,6 +139,8 @@ def lib():
             "or_sst_table_bloom": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), u16p, u8p, C.c_size_t, szp]),
             "or_sst_read_info": (C.c_int, [u8p, C.c_size_t, C.POINTER(SstInfo), u8p, C.c_size_t]),
             "or_merge_sort": (C.c_int, [C.c_uint32, u8p, u64p, u64p, u32p, u64p]),
+            "or_compact": (C.c_int, [u8p, u64p, C.c_uint32, u32p, C.c_uint32, C.c_uint64, C.c_int, C.c_uint64,
+                                     C.c_int, u8p, C.c_uint64, u64p, C.c_uint32, u32p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -639,3 +641,36 @@ def merge_sort(sources: list[list[bytes]]) -> np.ndarray:
     ss = np.zeros(len(sources) + 1, np.uint64)
     ss[1:] = np.cumsum([len(s) for s in sources])
     return merge_arrays(kd, ko, ss)
+
+
+def compact_arrays(blob: np.ndarray, sst_off: np.ndarray, src_sst: np.ndarray, max_sst_size: int, codec: int = NONE,
+                   nthreads: int = 1, block_size: int = 4096) -> tuple[int, np.ndarray, np.ndarray]:
+    """executeCompaction over SSTs packed in one array (compact_oracle.c or_compact): -> (status,
+    outputs packed, out_off)."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    sst_off = np.ascontiguousarray(sst_off, np.uint64)
+    src_sst = np.ascontiguousarray(src_sst, np.uint32)
+    cap = int(blob.size) * 2 + (1 << 20)
+    out = np.empty(cap, np.uint8)
+    oo_cap = int(blob.size) // 64 + 64
+    out_off = np.zeros(oo_cap, np.uint64)
+    n_out = C.c_uint32(0)
+    st = lib().or_compact(blob.ctypes.data_as(u8p), sst_off.ctypes.data_as(u64p), len(sst_off) - 1,
+                          src_sst.ctypes.data_as(u32p), len(src_sst) - 1, block_size, codec, max_sst_size, nthreads,
+                          out.ctypes.data_as(u8p), cap, out_off.ctypes.data_as(u64p), oo_cap, C.byref(n_out))
+    n = n_out.value
+    return st, out[: int(out_off[n]) if n else 0], out_off[: n + 1]
+
+
+def compact(sources: list[list[bytes]], max_sst_size: int, codec: int = NONE, nthreads: int = 1,
+            block_size: int = 4096) -> list[bytes]:
+    """compact_arrays over sources of SSTs (lists of bytes): the output SSTs' bytes."""
+    ssts = [s for run in sources for s in run]
+    blob = np.frombuffer(b"".join(ssts) or b"\0", np.uint8)
+    sst_off = np.zeros(len(ssts) + 1, np.uint64)
+    sst_off[1:] = np.cumsum([len(s) for s in ssts])
+    src_sst = np.zeros(len(sources) + 1, np.uint32)
+    src_sst[1:] = np.cumsum([len(r) for r in sources])
+    st, out, off = compact_arrays(blob, sst_off, src_sst, max_sst_size, codec, nthreads, block_size)
+    assert st == 0, status_string(st)
+    return [out[int(off[i]):int(off[i + 1])].tobytes() for i in range(len(off) - 1)]

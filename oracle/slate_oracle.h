@@ -200,6 +200,16 @@ int or_sst_read_info(const uint8_t* sst, size_t n, or_sst_info* info, uint8_t* f
 int or_merge_sort(uint32_t k, const uint8_t* keys, const uint64_t* key_off, const uint64_t* src_start,
                   uint32_t* out_idx, uint64_t* n_out);
 
+/* executeCompaction's codec path (slatedb/compaction/executor.go:92-151) over clean inputs
+ * (compact_oracle.c): n_sst encoded SSTs, sst i = ssts[sst_off[i] .. sst_off[i+1]); n_src sources
+ * in precedence order, source j = SSTs [src_sst[j], src_sst[j+1]).  Outputs built with
+ * (block_size, MinFilterKeys 0, 10 bits per key, codec), cut at max_sst_size as executor.go:119-148,
+ * concatenated into out with out_off[*n_out + 1].  nthreads workers decode blocks and build outputs
+ * (the merge is serial). */
+int or_compact(const uint8_t* ssts, const uint64_t* sst_off, uint32_t n_sst, const uint32_t* src_sst, uint32_t n_src,
+               uint64_t block_size, int codec, uint64_t max_sst_size, int nthreads, uint8_t* out, uint64_t cap,
+               uint64_t* out_off, uint32_t out_off_cap, uint32_t* n_out);
+
 /* block.NewIteratorAtKey (block/iterator.go:31-82) over a decoded block (Data, Offsets):
  * *start = the iterator's offsetIndex, *first_idx = the row firstFullKey returned (its suffix
  * is the iterator's firstKey, *first_len bytes), *n_warn = warnings added.  Returns OR_OK,

@@ -81,12 +81,15 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   DEV(d_in_off, in_off.size() * 8);
   DEV(d_out_off, (size_t(n) + 1) * 8);
   DEV(d_row_base, (size_t(n) + 1) * 8);
-  DEV(d_scr, decode_scratch_bytes(n) + 64);
+  DEV(d_scr, decode_scratch_bytes_codec(n, codec) + 64);
   int s = ctx_h2d(ctx, d_in->b.p, blob.data(), blob.size(), st);
   if (s) return s;
   SLATE_HIP(hipMemcpyAsync(d_in_off->b.p, in_off.data(), in_off.size() * 8, hipMemcpyHostToDevice, st));
-  SLATE_HIP(launch_decode_plan(st, codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n, d_out_off->as<uint64_t>(),
-                               d_row_base->as<uint64_t>(), d_scr->b.p));
+  {
+    GpuSpan gs(ctx, st);  // device time (slate_ctx_set_timing): every kernel group of the compaction
+    SLATE_HIP(launch_decode_plan(st, codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n,
+                                 d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), d_scr->b.p));
+  }
   uint64_t tot[2];
   if ((s = d2h_small(ctx, &tot[0], d_out_off->as<uint64_t>() + n, 8))) return s;
   if ((s = d2h_small(ctx, &tot[1], d_row_base->as<uint64_t>() + n, 8))) return s;
@@ -99,7 +102,10 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
                d_meta->as<slate_block_meta>(), d_rows->as<slate_row>(), d_row_base->as<uint64_t>(), nullptr, nullptr, 0};
   if (st == ctx->stream) a.side = &ctx->side;
   a.handbacks = ctx_handbacks(ctx);
-  SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus));
+  }
   // every block's status: the first failing block of an SST ends that SST's iterator with a
   // warning (iterator.go:62-68 wrapping decode.go:143-144); it and the SST's later blocks keep no
   // rows (their metas are patched to 0 rows for the rows phase)
@@ -134,9 +140,12 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   DEV(d_kvs, kv_scratch_bytes(slots) + 16);
   SLATE_HIP(hipMemsetAsync(d_nkv->b.p, 0, 16, st));
   SLATE_HIP(hipMemsetAsync(d_flags->b.p, 0, 16, st));
-  SLATE_HIP(launch_rows_lengths(st, d_row_base->as<uint64_t>(), n, d_meta->as<slate_block_meta>(),
-                                d_rows->as<slate_row>(), slots, key_off->as<uint64_t>(), val_off->as<uint64_t>(),
-                                tomb->as<uint8_t>(), d_nkv->as<uint64_t>(), d_flags->as<uint32_t>(), d_kvs->b.p));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_rows_lengths(st, d_row_base->as<uint64_t>(), n, d_meta->as<slate_block_meta>(),
+                                  d_rows->as<slate_row>(), slots, key_off->as<uint64_t>(), val_off->as<uint64_t>(),
+                                  tomb->as<uint8_t>(), d_nkv->as<uint64_t>(), d_flags->as<uint32_t>(), d_kvs->b.p));
+  }
   uint32_t flags = 0;
   uint64_t n_kv = 0;
   if ((s = d2h_small(ctx, &flags, d_flags->b.p, 4))) return s;
@@ -168,9 +177,13 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   if ((s = d2h_small(ctx, &vb, val_off->as<uint64_t>() + slots, 8))) return s;
   DEV(keys, kb + 16);
   DEV(vals, vb + 16);
-  SLATE_HIP(launch_rows_copy(st, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), n,
-                             d_rows->as<slate_row>(), slots, d_nkv->as<uint64_t>(), d_kvs->b.p, key_off->as<uint64_t>(),
-                             keys->as<uint8_t>(), val_off->as<uint64_t>(), vals->as<uint8_t>()));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_rows_copy(st, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), n,
+                               d_rows->as<slate_row>(), slots, d_nkv->as<uint64_t>(), d_kvs->b.p,
+                               key_off->as<uint64_t>(), keys->as<uint8_t>(), val_off->as<uint64_t>(),
+                               vals->as<uint8_t>()));
+  }
   SLATE_HIP(hipStreamSynchronize(st));
   // rows of each SST from its blocks' row counts; the warnings in the order its iterator adds them
   uint64_t acc = 0;
@@ -261,6 +274,14 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
   for (uint32_t i = 0; i < n_sst; i++)
     if (sst_off[i + 1] < sst_off[i]) return SLATE_E_INVALID_ARG;
   SLATE_HIP(ctx_bind(ctx));
+  const bool trace = host_trace();  // SLATE_HOST_TRACE: the phases' host wall times on stderr
+  double t_mark = trace ? now_ms() : 0.0;
+  auto mark = [&](const char* what) {
+    if (!trace) return;
+    const double t = now_ms();
+    fprintf(stderr, "[slate compact] %-22s %8.2f ms\n", what, t - t_mark);
+    t_mark = t;
+  };
   // ---- each SST's codec and data-block offsets (ReadInfo, ReadIndex, getBlockRange)
   std::vector<int> codec(n_sst);
   std::vector<std::vector<uint64_t>> offs(n_sst);
@@ -285,6 +306,7 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
       if (offs[i][b + 1] < offs[i][b] || offs[i][b + 1] > len) return SLATE_E_BLOB_RANGE;
     codec[i] = info.codec;
   }
+  mark("info + index");
   std::vector<uint32_t> sst_src(n_sst);
   for (uint32_t j = 0; j < n_src; j++)
     for (uint32_t i = src_sst[j]; i < src_sst[j + 1]; i++) sst_src[i] = j;
@@ -308,9 +330,11 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
       }
       sst_blocks.push_back(uint32_t(in_off.size() - 1));
     }
+    mark("gather blocks (host)");
     if (in_off.size() > 1) {
       View v;
       int s = decode_group(ctx, codec[i], blob, in_off, sst_blocks, i, sst_src, &v, &rows_per_sst, &wl);
+      mark("decode + row views");
       if (s) return s;
       views.push_back(v);
     } else {
@@ -379,11 +403,15 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
   SLATE_HIP(hipMemsetAsync(d_misc->b.p, 0, 64, st));
   uint64_t* d_n = d_misc->as<uint64_t>();
   uint32_t* d_flags = reinterpret_cast<uint32_t*>(d_n + 1);
-  s = slate_merge_sorted_device(ctx, n_src, all.keys->as<uint8_t>(), all.key_off->as<uint64_t>(), src_start.data(),
-                                d_idx->as<uint32_t>(), d_n, d_flags, d_ms->b.p);
+  {
+    GpuSpan gs(ctx, st);
+    s = slate_merge_sorted_device(ctx, n_src, all.keys->as<uint8_t>(), all.key_off->as<uint64_t>(), src_start.data(),
+                                  d_idx->as<uint32_t>(), d_n, d_flags, d_ms->b.p);
+  }
   if (s) return s;
   uint64_t hm[2] = {0, 0};
   if ((s = d2h_small(ctx, hm, d_n, 16))) return s;
+  mark("concat + merge");
   if (uint32_t(hm[1]) & 1) return SLATE_E_MERGE_UNSORTED;
   const uint64_t m = hm[0];
   // ---- the merged entries, gathered in order
@@ -391,19 +419,27 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
   DEV(oval_off, (m + 1) * 8);
   DEV(otomb, m + 1);
   DEV(d_gs, kv_scratch_bytes(m) + 16);
-  SLATE_HIP(launch_gather_lengths(st, d_idx->as<uint32_t>(), m, all.key_off->as<uint64_t>(),
-                                  all.val_off->as<uint64_t>(), all.tomb->as<uint8_t>(), okey_off->as<uint64_t>(),
-                                  oval_off->as<uint64_t>(), otomb->as<uint8_t>(), d_gs->b.p));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_gather_lengths(st, d_idx->as<uint32_t>(), m, all.key_off->as<uint64_t>(),
+                                    all.val_off->as<uint64_t>(), all.tomb->as<uint8_t>(), okey_off->as<uint64_t>(),
+                                    oval_off->as<uint64_t>(), otomb->as<uint8_t>(), d_gs->b.p));
+  }
   std::vector<uint64_t> hko(m + 1), hvo(m + 1);
   if ((s = ctx_d2h(ctx, hko.data(), okey_off->b.p, (m + 1) * 8, st))) return s;
   if ((s = ctx_d2h(ctx, hvo.data(), oval_off->b.p, (m + 1) * 8, st))) return s;
   DEV(okeys, hko[m] + 16);
   DEV(ovals, hvo[m] + 16);
-  SLATE_HIP(launch_gather_copy(st, d_idx->as<uint32_t>(), m, all.keys->as<uint8_t>(), all.key_off->as<uint64_t>(),
-                               all.vals->as<uint8_t>(), all.val_off->as<uint64_t>(), okeys->as<uint8_t>(),
-                               okey_off->as<uint64_t>(), ovals->as<uint8_t>(), oval_off->as<uint64_t>()));
+  {
+    GpuSpan gs(ctx, st);
+    SLATE_HIP(launch_gather_copy(st, d_idx->as<uint32_t>(), m, all.keys->as<uint8_t>(),
+                                 all.key_off->as<uint64_t>(), all.vals->as<uint8_t>(), all.val_off->as<uint64_t>(),
+                                 okeys->as<uint8_t>(), okey_off->as<uint64_t>(), ovals->as<uint8_t>(),
+                                 oval_off->as<uint64_t>()));
+  }
   SLATE_HIP(hipStreamSynchronize(st));
   all = View{};
+  mark("gather");
   // ---- output SSTs: a writer closes right after the entry that takes currentSize past MaxSSTSize
   std::vector<uint64_t> ends;
   {
@@ -442,6 +478,7 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
     if (s) return fail(s);
     out_tables[made++] = t;
     start = end;
+    mark("output SST build");
   }
   *n_out = made;
   return done;

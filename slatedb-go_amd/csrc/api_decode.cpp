@@ -156,7 +156,14 @@ int slate_ctx_handbacks(slate_ctx* ctx, uint64_t* n, int reset) {
   if (!ctx || !n) return SLATE_E_INVALID_ARG;
   *n = 0;
   SLATE_HIP(ctx_bind(ctx));
+  // every stream that can add to the counter: the context stream, its side stream, the pipeline
+  // lanes (host-buffer decodes) and the filter's aux stream; the single-block and compaction
+  // paths run on the context stream or a lane
   SLATE_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->side.s) SLATE_HIP(hipStreamSynchronize(ctx->side.s));
+  if (ctx->aux) SLATE_HIP(hipStreamSynchronize(ctx->aux));
+  for (auto& L : ctx->lanes)
+    if (L.stream) SLATE_HIP(hipStreamSynchronize(L.stream));
   if (!ctx->d_handbacks.p) return SLATE_OK;
   SLATE_HIP(hipMemcpy(n, ctx->d_handbacks.p, 8, hipMemcpyDeviceToHost));
   if (reset) SLATE_HIP(hipMemset(ctx->d_handbacks.p, 0, 8));
@@ -206,6 +213,9 @@ int slate_ctx_synchronize(slate_ctx* ctx) {
 }
 
 size_t slate_decode_scratch_bytes(uint32_t n_blocks) { return decode_scratch_bytes(n_blocks); }
+size_t slate_decode_scratch_bytes_codec(uint32_t n_blocks, int codec) {
+  return decode_scratch_bytes_codec(n_blocks, codec);
+}
 
 int slate_block_decode_plan_device(slate_ctx* ctx, int codec, const uint8_t* d_in, const uint64_t* d_in_off,
                                    uint32_t n, uint64_t* d_out_off, uint64_t* d_row_base, void* d_scratch) {
@@ -222,7 +232,7 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
   if ((reinterpret_cast<uintptr_t>(d_out) & 15) != 0) return SLATE_E_INVALID_ARG;
   SLATE_HIP(ctx_bind(ctx));
   // the scratch is owned by the context for the device-resident call
-  SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes(n)));
+  SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes_codec(n, codec)));
   DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
   a.side = &ctx->side;
   a.handbacks = ctx_handbacks(ctx);

@@ -162,6 +162,8 @@ void sink_map(Sink& o) {
 }
 
 
+}  // namespace
+
 // plan_sizes_kernel's decoded length for CodecNone / CodecSnappy on the host (decode.hip
 // decoded_len: the payload length, or golang/snappy decodedLen's varint header with the same
 // rejections), so that a chunk's place in the outputs needs no GPU round trip.
@@ -186,6 +188,8 @@ uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len) {
   }
   return 0;
 }
+
+namespace {
 
 // SLATE_ONE_LAUNCH=0: slate_block_decode takes the generic plan + decode path for every codec
 // (A/B and tests of both paths)
@@ -357,7 +361,7 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
     SLATE_HIP(L.d_in_off.ensure((size_t(m) + 1) * 8));
     SLATE_HIP(L.d_out_off.ensure((size_t(m) + 1) * 8));
     SLATE_HIP(L.d_row_base.ensure((size_t(m) + 1) * 8));
-    SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes(m) + 64));
+    SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes_codec(m, codec) + 64));
     const double t0 = trace ? now_ms() : 0.0;
     if (gsrc) {
       uint8_t* h = L.h_in.as<uint8_t>();
@@ -566,7 +570,7 @@ int slate_block_decode(slate_ctx* ctx, int codec, const uint8_t* in, size_t in_l
   SLATE_HIP(L.d_in_off.ensure(64));
   SLATE_HIP(L.d_out_off.ensure(64));
   SLATE_HIP(L.d_row_base.ensure(64));
-  SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes(1) + 64));
+  SLATE_HIP(L.d_scratch.ensure(decode_scratch_bytes_codec(1, codec) + 64));
   SLATE_HIP(L.d_meta.ensure(64));
   if (in_len) SLATE_HIP(hipMemcpyAsync(L.d_in.p, hin, in_len, hipMemcpyHostToDevice, s));
   SLATE_HIP(hipMemcpyAsync(L.d_in_off.p, hv, 16, hipMemcpyHostToDevice, s));

@@ -2094,42 +2094,201 @@ int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_in
 // ---------------------------------------------------------------------- read-ahead block reader
 }  // extern "C"
 
-// sstable.Iterator.nextBlockIter (iterator.go:92-118) with read-ahead: batches of read_ahead blocks
-// decoded by slate_read_blocks into reader-owned host buffers, served one block at a time.
+// sstable.Iterator.nextBlockIter (iterator.go:92-118) with read-ahead and double buffering:
+// batches of read_ahead blocks, two in flight.  Each batch is decoded into one of two slots while
+// the caller walks the other: next() asks for the following batch's bytes (NEED_DATA) as soon as a
+// slot is free, before it serves the current batch, so the GPU decodes batch k+1 while the caller
+// consumes batch k.  CodecNone / CodecSnappy batches are planned on the host (the varint header)
+// and decoded by one launch, one workgroup per block, reading the staged bytes and writing decoded
+// bytes, meta and rows through host-mapped page-locked memory (launch_decode_small); other codecs
+// take slate_read_blocks into buffers grown from the plan (kept across batches).
+struct ReaderSlot {
+  uint64_t b0 = 0, b1 = 0;      // blocks [b0, b1)
+  uint64_t fail = UINT64_MAX;   // the first failing block (known once synced)
+  bool fed = false, synced = false, fast = false;
+  hipEvent_t done = nullptr;
+  PinBuf h_in, h_out, h_meta, h_rows, h_desc;  // fast path: host-mapped staging and results
+  DevBuf d_scr;                                // fast path, one-wave blocks: device staging
+  std::vector<uint64_t> out_off, row_base;     // per block, into the slot's outputs
+  std::vector<uint8_t> out;                    // other codecs (slate_read_blocks)
+  std::vector<slate_block_meta> meta;
+  std::vector<slate_row> rows;
+  const uint8_t* out_p = nullptr;
+  const slate_block_meta* meta_p = nullptr;
+  const slate_row* rows_p = nullptr;
+};
+
 struct slate_block_reader {
   slate_ctx* ctx;
   slate_sst_info info;
   const slate_index* index;
   uint64_t next = 0, nblocks = 0;
   uint32_t ahead = 64;
-  uint64_t b0 = 0, b1 = 0;         // the decoded batch: blocks [b0, b1)
-  uint64_t fail = UINT64_MAX;      // its first failing block (served as an error, then the end)
-  uint64_t w0 = 0, w1 = 0;         // the batch the next feed decodes
+  uint64_t fed_end = 0;          // blocks before it were fed
+  uint64_t w0 = 0, w1 = 0;       // the batch the next feed decodes
   bool ended = false;
-  std::vector<uint8_t> out;
-  std::vector<uint64_t> out_off, row_base;
-  std::vector<slate_block_meta> meta;
-  std::vector<slate_row> rows;
+  hipStream_t stream = nullptr;  // the reader's own stream (its batches queue behind each other)
+  ReaderSlot slot[2];
+  ~slate_block_reader() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& x : slot) {
+      if (x.done) (void)hipEventDestroy(x.done);
+      x.h_in.release();
+      x.h_out.release();
+      x.h_meta.release();
+      x.h_rows.release();
+      x.h_desc.release();
+      x.d_scr.release();
+    }
+    if (stream) (void)hipStreamDestroy(stream);
+  }
 };
+
+namespace {
+
+// the SST byte range of block i alone (getBlockRange for [i, i+1))
+inline void block_range(const slate_block_reader* r, uint64_t i, uint64_t* s, uint64_t* e) {
+  *s = r->index->offsets[i];
+  *e = i + 1 < r->nblocks ? r->index->offsets[i + 1] : r->info.filter_offset;
+}
+
+// the next window from fed_end: up to read_ahead blocks, cut before the first block whose own range
+// is inverted (Go reads one block per call and fails only at that block, serving those before it);
+// such a block is a window of its own, whose want() range then fails as Go's ReadRange does
+void reader_window(slate_block_reader* r) {
+  const uint64_t w0 = r->fed_end, lim = std::min<uint64_t>(w0 + r->ahead, r->nblocks);
+  uint64_t s, e;
+  block_range(r, w0, &s, &e);
+  uint64_t w1 = w0 + 1;
+  if (e >= s)
+    for (; w1 < lim; w1++) {
+      block_range(r, w1, &s, &e);
+      if (e < s) break;
+    }
+  r->w0 = w0;
+  r->w1 = w1;
+}
+
+ReaderSlot* reader_holding(slate_block_reader* r, uint64_t b) {
+  for (auto& x : r->slot)
+    if (x.fed && b >= x.b0 && b < x.b1) return &x;
+  return nullptr;
+}
+
+ReaderSlot* reader_free_slot(slate_block_reader* r) {
+  for (auto& x : r->slot)
+    if (!x.fed || x.b1 <= r->next) return &x;
+  return nullptr;
+}
+
+int reader_sync(slate_block_reader* r, ReaderSlot& x) {
+  if (x.synced) return SLATE_OK;
+  if (x.fast) {
+    SLATE_HIP(hipEventSynchronize(x.done));
+    const slate_block_meta* m = x.h_meta.as<slate_block_meta>();
+    for (uint64_t i = 0; i < x.b1 - x.b0; i++)
+      if (m[i].status != SLATE_OK) {
+        x.fail = x.b0 + i;
+        break;
+      }
+  }
+  x.synced = true;
+  return SLATE_OK;
+}
+
+// the fast path: CodecNone / CodecSnappy, every block within the small kernels' LDS windows
+int reader_feed_fast(slate_block_reader* r, ReaderSlot& x, const uint8_t* data, const std::vector<uint64_t>& in_off,
+                     bool* taken) {
+  *taken = false;
+  const int codec = r->info.codec;
+  if (!host_plannable(codec)) return SLATE_OK;
+  const uint64_t n = in_off.size() - 1;
+  std::vector<SmallDesc> par, wave;
+  par.reserve(n);
+  uint64_t in_tot = 0, out_tot = 0, rows_tot = 0;
+  x.out_off.resize(n + 1);
+  x.row_base.resize(n + 1);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t len = in_off[i + 1] - in_off[i];
+    const uint64_t dl = host_decoded_len(codec, data + in_off[i], len);
+    const uint64_t osz = align16(dl), rsz = row_capacity(dl);
+    SmallDesc d{uint32_t(i), uint32_t(len), in_tot, out_tot, osz, rows_tot, rsz, 0};
+    if (small_par_fits(codec, len, osz)) par.push_back(d);
+    else if (small_wave_fits(len, osz) && len < 0xFFFFFFF0ull) wave.push_back(d);
+    else return SLATE_OK;  // a block beyond the windows: the batch path
+    x.out_off[i] = out_tot;
+    x.row_base[i] = rows_tot;
+    in_tot += align16(len) + 16;
+    out_tot += osz;
+    rows_tot += rsz;
+  }
+  x.out_off[n] = out_tot;
+  x.row_base[n] = rows_tot;
+  // the one-wave blocks' decoded bytes in the device scratch after every input
+  const uint64_t dev_out0 = align16(in_tot) + 256;
+  for (auto& d : wave) d.dev_out = dev_out0 + d.out_off;
+  SLATE_HIP(x.h_in.ensure(in_tot + 64));
+  SLATE_HIP(x.h_out.ensure(out_tot + 64));
+  SLATE_HIP(x.h_meta.ensure(n * sizeof(slate_block_meta) + 64));
+  SLATE_HIP(x.h_rows.ensure((rows_tot + 1) * sizeof(slate_row) + 64));
+  SLATE_HIP(x.h_desc.ensure((n + 1) * sizeof(SmallDesc)));
+  if (!wave.empty()) SLATE_HIP(x.d_scr.ensure(dev_out0 + out_tot + 64));
+  uint8_t* hin = x.h_in.as<uint8_t>();
+  for (const auto* v : {&par, &wave})
+    for (const SmallDesc& d : *v) memcpy(hin + d.in_off, data + in_off[d.block], d.in_len);
+  SmallDesc* hd = x.h_desc.as<SmallDesc>();
+  std::copy(par.begin(), par.end(), hd);
+  std::copy(wave.begin(), wave.end(), hd + par.size());
+  auto* hin_d = static_cast<uint8_t*>(mapped_ptr(x.h_in.p));
+  auto* hout_d = static_cast<uint8_t*>(mapped_ptr(x.h_out.p));
+  auto* meta_d = static_cast<slate_block_meta*>(mapped_ptr(x.h_meta.p));
+  auto* rows_d = static_cast<slate_row*>(mapped_ptr(x.h_rows.p));
+  auto* desc_d = static_cast<SmallDesc*>(mapped_ptr(x.h_desc.p));
+  if (!hin_d || !hout_d || !meta_d || !rows_d || !desc_d) return SLATE_OK;
+  DecodeArgs a{codec, nullptr, nullptr, 1, nullptr, nullptr, meta_d, rows_d, nullptr, nullptr, nullptr, 0};
+  SLATE_HIP(launch_decode_small(r->stream, a, desc_d, uint32_t(par.size()), uint32_t(n), hin_d, hout_d,
+                                wave.empty() ? nullptr : x.d_scr.as<uint8_t>()));
+  if (!x.done) SLATE_HIP(hipEventCreateWithFlags(&x.done, hipEventDisableTiming));
+  SLATE_HIP(hipEventRecord(x.done, r->stream));
+  x.out_p = x.h_out.as<uint8_t>();
+  x.meta_p = x.h_meta.as<slate_block_meta>();
+  x.rows_p = x.h_rows.as<slate_row>();
+  x.fast = true;
+  x.synced = false;
+  *taken = true;
+  return SLATE_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
 int slate_block_reader_create(slate_ctx* ctx, const slate_sst_info* info, const slate_index* index,
                               uint64_t first_block, uint32_t read_ahead, slate_block_reader** reader) {
   if (!ctx || !info || !index || !reader || read_ahead == 0) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(ctx));
   slate_block_reader* r = new (std::nothrow) slate_block_reader();
   if (!r) return SLATE_E_OOM;
   r->ctx = ctx;
   r->info = *info;
   r->index = index;
   r->next = first_block;
+  r->fed_end = first_block;
   r->nblocks = index->offsets.size();
   r->ahead = read_ahead;
+  if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+    r->stream = nullptr;
+    delete r;
+    return SLATE_E_HIP;
+  }
   *reader = r;
   return SLATE_OK;
 }
 
-void slate_block_reader_free(slate_block_reader* reader) { delete reader; }
+void slate_block_reader_free(slate_block_reader* reader) {
+  if (reader) (void)ctx_bind(reader->ctx);
+  delete reader;
+}
 
 int slate_block_reader_next(slate_block_reader* r, slate_block_view* view) {
   if (!r || !view) return SLATE_E_INVALID_ARG;
@@ -2137,17 +2296,41 @@ int slate_block_reader_next(slate_block_reader* r, slate_block_view* view) {
     r->ended = true;
     return SLATE_E_READER_END;
   }
-  if (r->next < r->b0 || r->next >= r->b1) {  // not decoded yet: the next batch
-    r->w0 = r->next;
-    r->w1 = std::min<uint64_t>(r->next + r->ahead, r->nblocks);
+  ReaderSlot* cur = reader_holding(r, r->next);
+  // read ahead: while a slot is free and blocks are left, ask for the next batch first -- unless the
+  // current batch is known to end the iteration (a failing block: Go reads no further)
+  if (r->fed_end < r->nblocks && r->w1 <= r->w0) {
+    ReaderSlot* fr = reader_free_slot(r);
+    bool stop = false;
+    if (cur && cur->fast && !cur->synced && hipEventQuery(cur->done) == hipSuccess) {
+      int st = reader_sync(r, *cur);
+      if (st) return st;
+    }
+    if (cur && cur->synced && cur->fail != UINT64_MAX) stop = true;
+    if (fr && fr != cur && !stop) {
+      reader_window(r);
+      // a window whose byte range is inverted (a block Go's ReadRange fails on) is asked for only
+      // when the caller reaches it: the failure must not surface before the blocks in front of it
+      uint64_t s0, e0;
+      block_range(r, r->w0, &s0, &e0);
+      if (!cur || e0 >= s0) return SLATE_E_READER_NEED_DATA;
+      r->w0 = r->w1 = 0;
+    }
+  }
+  if (!cur) {
+    if (r->w1 > r->w0) return SLATE_E_READER_NEED_DATA;  // the window asked for was not fed
+    reader_window(r);
     return SLATE_E_READER_NEED_DATA;
   }
-  const uint64_t i = r->next - r->b0;
+  SLATE_HIP(ctx_bind(r->ctx));
+  int st = reader_sync(r, *cur);
+  if (st) return st;
+  const uint64_t i = r->next - cur->b0;
   view->block = r->next;
-  view->meta = r->meta[i];
-  view->data = r->out.data() + r->out_off[i];
-  view->rows = r->rows.data() + r->row_base[i];
-  if (r->next == r->fail) {  // the SST iterator's warning, and its end (iterator.go:59-68)
+  view->meta = cur->meta_p[i];
+  view->data = cur->out_p + cur->out_off[i];
+  view->rows = cur->rows_p + cur->row_base[i];
+  if (r->next == cur->fail) {  // the SST iterator's warning, and its end (iterator.go:59-68)
     r->ended = true;
     return view->meta.status ? view->meta.status : SLATE_E_HIP;
   }
@@ -2162,26 +2345,59 @@ int slate_block_reader_want(const slate_block_reader* r, uint64_t* range_start, 
 
 int slate_block_reader_feed(slate_block_reader* r, const uint8_t* data, size_t data_len) {
   if (!r || (data_len && !data) || r->w1 <= r->w0) return SLATE_E_INVALID_ARG;
-  const uint64_t n = r->w1 - r->w0;
-  r->out_off.resize(n + 1);
-  r->row_base.resize(n + 1);
-  r->meta.resize(n);
-  if (r->out.empty()) r->out.resize(16);
-  if (r->rows.empty()) r->rows.resize(1);
-  uint64_t failed = UINT64_MAX;
-  int st = SLATE_OK;
-  for (int pass = 0; pass < 2; pass++) {
-    st = slate_read_blocks(r->ctx, &r->info, r->index, r->w0, r->w1, data, data_len, r->out.data(), r->out.size(),
-                           r->out_off.data(), r->meta.data(), r->rows.data(), r->rows.size(), r->row_base.data(),
-                           &failed);
-    if (st != SLATE_E_CAPACITY) break;
-    r->out.resize(r->out_off[n] + 16);  // the sizes the plan reported
-    r->rows.resize(r->row_base[n] + 1);
-  }
+  ReaderSlot* fr = reader_free_slot(r);
+  if (!fr) return SLATE_E_INVALID_ARG;
+  SLATE_HIP(ctx_bind(r->ctx));
+  uint64_t rs, re;
+  int st = slate_read_blocks_range(&r->info, r->index, r->w0, r->w1, &rs, &re);
   if (st) return st;
-  r->b0 = r->w0;
-  r->b1 = r->w1;
-  r->fail = failed;
+  if (re < rs || data_len != re - rs) return SLATE_E_BLOB_RANGE;
+  const uint64_t n = r->w1 - r->w0;
+  std::vector<uint64_t> in_off(n + 1);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t b = r->w0 + i;
+    const uint64_t s0 = r->index->offsets[b] - rs;
+    const uint64_t e0 = (b + 1 == r->nblocks) ? data_len : r->index->offsets[b + 1] - rs;
+    if (s0 > data_len || e0 > data_len || s0 > e0) return SLATE_E_BLOB_RANGE;
+    in_off[i] = s0;
+    in_off[i + 1] = e0;
+  }
+  ReaderSlot& x = *fr;
+  // the slot is free: its previous batch was served (and its decode finished before it was)
+  if (x.fed && x.fast && !x.synced) SLATE_HIP(hipEventSynchronize(x.done));
+  x.fed = false;
+  x.fail = UINT64_MAX;
+  bool taken = false;
+  st = reader_feed_fast(r, x, data, in_off, &taken);
+  if (st) return st;
+  if (!taken) {
+    // other codecs: one batch through slate_read_blocks, buffers sized by the first attempt's plan
+    // and kept (a later batch decodes twice only when it needs more room than any before it)
+    x.fast = false;
+    x.out_off.resize(n + 1);
+    x.row_base.resize(n + 1);
+    x.meta.resize(n);
+    if (x.out.size() < 16) x.out.resize(std::max<uint64_t>(16, 4 * data_len + 16 * n));
+    if (x.rows.empty()) x.rows.resize(std::max<uint64_t>(1, x.out.size() / 15));
+    uint64_t failed = UINT64_MAX;
+    for (int pass = 0; pass < 2; pass++) {
+      st = slate_read_blocks(r->ctx, &r->info, r->index, r->w0, r->w1, data, data_len, x.out.data(), x.out.size(),
+                             x.out_off.data(), x.meta.data(), x.rows.data(), x.rows.size(), x.row_base.data(), &failed);
+      if (st != SLATE_E_CAPACITY) break;
+      x.out.resize(x.out_off[n] + 16);  // the sizes the plan reported
+      x.rows.resize(x.row_base[n] + 1);
+    }
+    if (st) return st;
+    x.fail = failed;
+    x.synced = true;
+    x.out_p = x.out.data();
+    x.meta_p = x.meta.data();
+    x.rows_p = x.rows.data();
+  }
+  x.b0 = r->w0;
+  x.b1 = r->w1;
+  x.fed = true;
+  r->fed_end = r->w1;
   r->w0 = r->w1 = 0;
   return SLATE_OK;
 }

@@ -1592,6 +1592,18 @@ size_t decode_scratch_bytes(uint32_t n) {
          size_t(n) * kZfSeqSlot * sizeof(uint32_t);
 }
 
+// The scratch one codec's plan + decode touch (carve's layout, cut after the last region the
+// codec uses): CodecNone / Snappy need the scan tiles, the large-block list, the round counter and
+// the list count (~8 B per block instead of ~560); LZ4, Zlib and Zstd keep every region (their fast
+// paths' lists, records and sequence slots).
+size_t decode_scratch_bytes_codec(uint32_t n, int codec) {
+  if (codec != SLATE_CODEC_NONE && codec != SLATE_CODEC_SNAPPY) return decode_scratch_bytes(n);
+  const size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
+  // scan tiles, large count, large list, round counter, list count, list
+  return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16 + 16 +
+         align16(size_t(n) * sizeof(uint32_t));
+}
+
 static DecodeScratch carve(void* scratch, uint32_t n) {
   DecodeScratch s;
   size_t tiles = (size_t(n) + 1 + kScanTile - 1) / kScanTile;
@@ -1837,7 +1849,7 @@ __device__ __forceinline__ void decode_one_par(DecodeArgs a, const uint8_t* __re
   // 4 the expansion, 5 pass 3, 6 before block_finish and the copy-out (the time per phase)
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint64_t offs[6];
-  __shared__ uint32_t sh_crc, sh_bad, sh_ntags, sh_nhops, sh_more;
+  __shared__ uint32_t sh_crc, sh_bad, sh_ntags, sh_nhops;
   const uint32_t tid = threadIdx.x;
   const int lane = int(tid & 63), wave = int(tid >> 6);
   uint32_t* tab = reinterpret_cast<uint32_t*>(smem);
@@ -2012,9 +2024,10 @@ __device__ __forceinline__ void decode_one_par(DecodeArgs a, const uint8_t* __re
       P[x] = lit ? uint16_t(0x8000u | in[p + hl + (x - o)]) : uint16_t(x - off);
     }
     __syncthreads();
+    // The round's verdict is the barrier's own OR (one barrier per round, no shared flag that
+    // thread 0 could reset while a late wave still reads the previous round's value).
+    bool resolved = false;
     for (uint32_t round = 0; round < 16; round++) {
-      if (tid == 0) sh_more = 0;
-      __syncthreads();
       uint32_t more = 0;
       for (uint32_t x = tid; x < dn; x += kOneParThreads) {
         const uint32_t v = P[x];
@@ -2024,12 +2037,13 @@ __device__ __forceinline__ void decode_one_par(DecodeArgs a, const uint8_t* __re
           more |= (w & 0x8000u) ? 0u : 1u;
         }
       }
-      if (more) sh_more = 1;
-      __syncthreads();
-      if (!sh_more) break;
+      if (!__syncthreads_or(int(more))) {
+        resolved = true;
+        break;
+      }
     }
     if (stop == 5) return;
-    if (!sh_more) {  // (every byte resolved: 16 rounds cover any chain in kOneParOut bytes)
+    if (resolved) {  // (every byte resolved: 16 rounds cover any chain in kOneParOut bytes)
       for (uint32_t x = tid; x < dn; x += kOneParThreads) out[x] = uint8_t(P[x]);
       __syncthreads();
       if (stop == 6) return;
@@ -2040,6 +2054,7 @@ __device__ __forceinline__ void decode_one_par(DecodeArgs a, const uint8_t* __re
   // ---- anything the passes refused: the serial decoder reports it (or decodes it)
   slate_block_meta m{};
   int st = SLATE_E_SNAPPY_CORRUPT;
+  __syncthreads();  // every wave has read sh_bad (pass 2) before lane 0 of wave 0 rewrites it
   if (wave == 0 && hdr_ok) st = wave_snappy_decode(in, clen, hdr, out, dn, lane);
   if (wave == 0 && lane == 0) sh_bad = uint32_t(st);
   __syncthreads();
@@ -2052,6 +2067,63 @@ __global__ __launch_bounds__(kOneParThreads) void decode_one_par_kernel(DecodeAr
                                                                         uint8_t* __restrict__ host_out, uint32_t stop) {
   decode_one_par(a, host_in, in_len, out_sz, row_sz, host_out, stop);
 }
+
+// Small batches (the read-ahead block reader's read_ahead blocks): one workgroup per block, so a
+// batch of 64 blocks takes one block's latency instead of the lane-per-block kernel's one round
+// (~0.3 ms for 64 blocks on one wave).  Descriptor k (host-mapped, one read per workgroup) names
+// block b's staged input (16-byte aligned), its decoded bytes' place and its row slots; meta and rows
+// are written through host-mapped pointers, the decoded bytes too.  Blocks [0, n_par) take the
+// workgroup-parallel Snappy decoder, [n_par, n) the one-wave decoder (CodecNone, larger blocks),
+// each in its own launch (their LDS budgets differ).
+__global__ __launch_bounds__(kOneParThreads) void decode_small_par_kernel(DecodeArgs a, const SmallDesc* __restrict__ d,
+                                                                          const uint8_t* hin, uint8_t* hout) {
+  const SmallDesc x = d[blockIdx.x];
+  DecodeArgs ab = a;
+  ab.n = 1;
+  ab.meta = a.meta + x.block;
+  ab.rows = a.rows + x.row_base;
+  decode_one_par(ab, hin + x.in_off, x.in_len, x.out_sz, x.row_sz, hout + x.out_off, 0);
+}
+__global__ __launch_bounds__(64) void decode_small_wave_kernel(DecodeArgs a, const SmallDesc* __restrict__ d,
+                                                               const uint8_t* hin, uint8_t* hout, uint8_t* dscr) {
+  const SmallDesc x = d[blockIdx.x];
+  DecodeArgs ab = a;
+  ab.n = 1;
+  ab.meta = a.meta + x.block;
+  ab.rows = a.rows + x.row_base;
+  // device staging for the wave decoder: the block's input at its staging offset, its decoded bytes
+  // at dev_out (after every input)
+  ab.in = dscr + x.in_off;
+  ab.out = dscr + x.dev_out;
+  decode_one(ab, hin + x.in_off, x.in_len, x.out_sz, x.row_sz, hout + x.out_off);
+}
+
+hipError_t launch_decode_small(hipStream_t st, const DecodeArgs& args_in, const SmallDesc* descs, uint32_t n_par,
+                               uint32_t n, const uint8_t* hin, uint8_t* hout, uint8_t* dscr) {
+  DecodeArgs a = args_in;
+  a.debug = 0;
+  a.raw = 0;
+  a.rt_zero = 0;
+  if (n_par) {
+    static const hipError_t attr_p = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_small_par_kernel),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(kOneParLds));
+    if (attr_p != hipSuccess) return attr_p;
+    decode_small_par_kernel<<<n_par, kOneParThreads, kOneParLds, st>>>(a, descs, hin, hout);
+  }
+  if (n > n_par) {
+    constexpr size_t lds = kTabBytes + kLargeInCap + kLargeOutCap;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_small_wave_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (attr != hipSuccess) return attr;
+    decode_small_wave_kernel<<<n - n_par, 64, lds, st>>>(a, descs + n_par, hin, hout, dscr);
+  }
+  return hipGetLastError();
+}
+
+bool small_par_fits(int codec, uint64_t in_len, uint64_t out_sz) {
+  return codec == SLATE_CODEC_SNAPPY && in_len >= 6 && in_len + 16 <= kOneParIn && out_sz <= kOneParOut;
+}
+bool small_wave_fits(uint64_t in_len, uint64_t out_sz) { return in_len + 15 <= kLargeInCap && out_sz <= kLargeOutCap; }
 
 hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& args_in, const uint8_t* host_in, uint64_t in_len,
                              uint64_t out_sz, uint64_t row_sz, uint8_t* host_out) {

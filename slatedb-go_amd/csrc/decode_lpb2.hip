@@ -166,6 +166,27 @@ __device__ v4u row_from_hbm(const uint8_t* data, uint32_t data_len, uint32_t off
   return pack_row(off, pl, sl, vl, flags & 7, o - 4 - sl, SLATE_OK);
 }
 
+// Per-lane flags as wave masks (one bit per lane; wave-uniform, so they live in SGPR pairs).  Kept
+// as bools in the lane's state they lived in VGPRs as 0 / 1: a v_cndmask to write one and a v_cmp
+// to read it at every use (~160 of the loop's ~1360 VALU).  As masks they combine with the ballots
+// of the step's comparisons by SALU ops, and a select reads them directly (msel).
+__device__ __forceinline__ uint64_t bal(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ uint32_t msel(uint64_t m, uint32_t a, uint32_t b);
+__device__ __forceinline__ bool mbit(uint64_t m) { return msel(m, 1u, 0u) != 0; }
+__device__ __forceinline__ uint32_t msel(uint64_t m, uint32_t a, uint32_t b) {  // this lane's bit of m ? a : b
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+  return r;
+}
+__device__ __forceinline__ uint32_t sub_sat(uint32_t a, uint32_t b) { return __builtin_elementwise_sub_sat(a, b); }
+// a > b (unsigned) as a mask, one v_cmp: a comparison LLVM fuses with a subtraction of the same
+// operands becomes the subtraction's borrow, which the ballot then materialises and compares again
+__device__ __forceinline__ uint64_t ugt(uint32_t a, uint32_t b) {
+  uint64_t m;
+  asm("v_cmp_gt_u32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+  return m;
+}
+
 struct Lane {
   // block
   uint32_t in_rel, out_rel, rows_rel;  // offsets of this block in the round's buffer resources
@@ -175,15 +196,16 @@ struct Lane {
   // decode: s = the next tag (payload-relative); src = the current item's source: an input-ring
   // position (sh included) for a literal, an output position for a copy
   uint32_t s, d, rem, src, eff;
-  bool lit, far, dd, err;
+  // masks: the current item is a literal (lit), a far copy (far); the decode is done (dd) or failed (err)
+  uint64_t mlit, mfar, mdd, merr;
   uint32_t T;  // the output ring's dword at d & ~3 (what the next store merges below d)
   uint32_t z;  // a run-time zero (see rd128)
   uint32_t c_issue, c_commit, n_req, fl;
   uint32_t qoff;  // hole source requested this iteration (loaded once, before the flush)
   // pending hole: up to 16 bytes of a copy with offset > kReach reserve output [hd, hd+hl) and
   // decoding goes on; the source is loaded at the end of the iteration and merged at the start
-  // of the next one (hp is set exactly from a hole's step to the next iteration's start)
-  bool hp;
+  // of the next one (mhp's bit is set exactly from a hole's step to the next iteration's start)
+  uint64_t mhp;
   uint32_t hd, hl;
   // row walker: phase 0 = header (prefix/suffix lengths), 1 = flags (+ the value length that
   // follows them), 2 = value length after timestamps, 3 = stopped
@@ -259,11 +281,11 @@ __device__ __forceinline__ W6 ring_rd24(const uint8_t* ring, uint32_t p) {
 // reads the key lengths, phase 1 the flags (+ the value length when there are no
 // timestamps), phase 2 the value length after the timestamps.
 // Returns true with `row`/`ridx` set when the action finished a row.
-__device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
+__device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act, bool hp, v4u& row, uint32_t& ridx) {
   const uint32_t fp = L.R + 4 + L.rsl + 8;
   const bool p0 = L.rphase == 0, p1 = L.rphase == 1;
   const uint32_t rpos = p0 ? L.R : (p1 ? fp : L.R + L.ro);
-  const bool in_hole = L.hp && rpos < L.hd + L.hl && rpos + 8 > L.hd;
+  const bool in_hole = hp && rpos < L.hd + L.hl && rpos + 8 > L.hd;
   const bool wa = act & (L.rphase < 3) & (L.d >= L.rneed) & !in_hole;
   const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
   const W6 q = ring_rd24(ring, rpos);
@@ -277,7 +299,7 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
   const uint32_t vl0 = __builtin_bswap32(vb == 0 ? fw1 : alignb(fw1, fw, vb));
   const bool tomb0 = (fl0 & 1) != 0;
   const uint32_t rlen0 = 4 + sl0 + 9 + (tomb0 ? 0u : 4u);
-  const bool hole0 = L.hp && rpos < L.hd + L.hl && rpos + rlen0 > L.hd;
+  const bool hole0 = hp && rpos < L.hd + L.hl && rpos + rlen0 > L.hd;
   const bool one = p0 & (sl0 <= 7) & !(fl0 & 6) & (L.d >= L.R + rlen0) & !hole0;
   // phase 1: flags, and the value length right after them when there are no timestamps
   const uint32_t fl1 = q.w[0] & 0xff;
@@ -338,9 +360,9 @@ __device__ __forceinline__ bool walk_step(Lane& L, const uint8_t* ring, bool act
 // first 24 bytes, one action), for lanes in phase 0; walk() runs the general walk_step only when
 // some lane is in phase 1 or 2 (a suffix over 7 bytes, timestamps).  Same transitions as
 // walk_step's phase 0.
-__device__ __forceinline__ bool walk_fast(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
+__device__ __forceinline__ bool walk_fast(Lane& L, const uint8_t* ring, bool act, bool hp, v4u& row, uint32_t& ridx) {
   const uint32_t rpos = L.R;
-  const bool in_hole = L.hp & (rpos < L.hd + L.hl) & (rpos + 8 > L.hd);
+  const bool in_hole = hp & (rpos < L.hd + L.hl) & (rpos + 8 > L.hd);
   const bool wa = act & (L.rphase == 0) & (L.d >= L.rneed) & !in_hole;
   const bool lost = L.d - rpos > kReach;  // fell behind the ring: the exact fallback takes over
   const W6 q = ring_rd24(ring, rpos);
@@ -354,7 +376,7 @@ __device__ __forceinline__ bool walk_fast(Lane& L, const uint8_t* ring, bool act
   const uint32_t vl0 = __builtin_bswap32(vb == 0 ? fw1 : fa);
   const bool tomb0 = (fl0 & 1) != 0;
   const uint32_t rlen0 = 4 + sl0 + 9 + (tomb0 ? 0u : 4u);
-  const bool hole0 = L.hp & (rpos < L.hd + L.hl) & (rpos + rlen0 > L.hd);
+  const bool hole0 = hp & (rpos < L.hd + L.hl) & (rpos + rlen0 > L.hd);
   const bool one = (sl0 <= 7) & !(fl0 & 6) & (L.d >= rpos + rlen0) & !hole0;
   const bool done = wa & !lost & one;
   const uint32_t vl = tomb0 ? 0u : vl0;
@@ -391,7 +413,8 @@ __device__ __forceinline__ bool walk_fast(Lane& L, const uint8_t* ring, bool act
 __device__ __forceinline__ bool walk(Lane& L, const uint8_t* ring, bool act, v4u& row, uint32_t& ridx) {
   const bool slow = act & ((L.rphase == 1) | (L.rphase == 2));
   const bool slow_go = slow & (L.d >= L.rneed);
-  bool emit = walk_fast(L, ring, act, row, ridx);
+  const bool hp = mbit(L.mhp);
+  bool emit = walk_fast(L, ring, act, hp, row, ridx);
 #ifdef SLATE_COUNT_FAST_ONLY  // static instruction counts of the common path (tools/loop_mix.py)
   if (false) {
 #else
@@ -399,7 +422,7 @@ __device__ __forceinline__ bool walk(Lane& L, const uint8_t* ring, bool act, v4u
 #endif
     v4u row2;
     uint32_t ridx2;
-    const bool e2 = walk_step(L, ring, slow, row2, ridx2);
+    const bool e2 = walk_step(L, ring, slow, hp, row2, ridx2);
     row = slow ? row2 : row;
     ridx = slow ? ridx2 : ridx;
     emit = slow ? e2 : emit;
@@ -426,6 +449,25 @@ __device__ __forceinline__ void load_one(uint32_t j, uint32_t lane, uint32_t wav
   slot = want ? (wave_lane0 + o) * kInStride + (ci & (kNS - 1)) * 16 : 0xFFFFFFFFu;
 }
 
+// The decode kernel's refill with its loop invariants hoisted: rel_j = the round's input offset of
+// the block lane `lane` serves in load j (shuffled once per round), slot_lane = that block's input
+// ring in load 0 (LDS offset, fixed for the kernel; load j's is 16 j records further, an immediate);
+// S_j = the ring slot's byte offset, or ~0 when the lane loads nothing.
+template <uint32_t kJ>
+__device__ __forceinline__ void commit_j(uint8_t* ins, uint32_t slot_lane, uint32_t S, const v4u& v, uint32_t z) {
+  if (S != 0xFFFFFFFFu) wr128(ins + slot_lane + kJ * 16 * kInStride + S, v, z);
+}
+template <uint32_t kJ>
+__device__ __forceinline__ void load_j(uint32_t lane, uint32_t info, uint32_t rel_j, const Rsrc& R, v4u& P,
+                                       uint32_t& S) {
+  const uint32_t c = lane & 3;
+  const uint32_t info_o = __shfl(info, int(16 * kJ + (lane >> 2)), 64);
+  const uint32_t ci = (info_o >> 3) + c;
+  const bool want = c < (info_o & 7);
+  P = __builtin_amdgcn_raw_buffer_load_b128(R.in, want ? rel_j + 16 * ci : kOOB, 0, 0);
+  S = want ? (ci & (kNS - 1)) * 16 : 0xFFFFFFFFu;
+}
+
 // Start of an iteration, part 2: how many chunks this block asks for (ring room and
 // payload end permitting), then four transposed loads fetch them for the whole wave.
 __device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, uint32_t c_issue, uint32_t last_chunk) {
@@ -438,7 +480,7 @@ __device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, ui
 // iteration (Q) fills the pending hole -- a read-modify-write of the five ring dwords around
 // [hd, hd+hl): the bytes after the hole were decoded meanwhile.
 __device__ __forceinline__ void absorb_hole(Lane& L, const v4u& Q, uint8_t* ring) {
-  if (__builtin_amdgcn_ballot_w64(L.hp)) {
+  if (L.mhp) {
     const uint32_t hd = L.hd, b = hd & 3, a4 = hd & ~3u, a = hd & ~7u;
     const v2u A = rd64(ring, a), B = rd64(ring, a + 8), C = rd64(ring, a + 16);
     const bool q = (hd & 4) != 0;
@@ -463,12 +505,12 @@ __device__ __forceinline__ void absorb_hole(Lane& L, const v4u& Q, uint8_t* ring
     n.y2 = (y.y2 & m2) | (o.y2 & ~m2);
     n.y3 = (y.y3 & m3) | (o.y3 & ~m3);
     n.y4 = (y.y4 & m4) | (o.y4 & ~m4);
-    if (L.hp) store_win(ring, a4, n);
+    if (mbit(L.mhp)) store_win(ring, a4, n);
     // the register copy of d's dword follows a store into that dword
     const uint32_t jd = (((L.d & ~3u) - a4) & (kOR - 1)) >> 2;
-    L.T = (L.hp && jd <= 4) ? pick5(n, jd) : L.T;
+    L.T = msel(L.mhp & bal(jd <= 4), pick5(n, jd), L.T);
   }
-  L.hp = false;
+  L.mhp = 0;
 }
 
 // Appends item to list (wave-aggregated: one atomic per wave); every lane of the wave calls it.
@@ -500,7 +542,7 @@ __device__ __forceinline__ void xxh_absorb(Lane& L, const uint8_t* ring, bool go
 // longer than the 8-byte window, or any failed check, hands the block to the exact path
 // (L.hb), which then decodes and reports it.  A token without literals is parsed with its match.
 __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, int32_t avail, uint32_t lim_d) {
-  const bool need = act && !L.dd && L.rem == 0;
+  const bool need = act && !mbit(L.mdd) && L.rem == 0;
   const bool fin = need && L.lph == 2;
   const bool can = need & (L.lph < 2) & (avail >= int32_t(min(L.s + 8, L.clen))) & (L.d <= lim_d);
   const v2u w = ring_rd8(in, L.sh + L.s, kIR - 8);
@@ -535,12 +577,13 @@ __device__ __forceinline__ void lz4_parse(Lane& L, bool act, const uint8_t* in, 
   const bool bad = ext_bad || (mph ? bad_m : bad_tok);
   const bool ok = can && !bad;
   L.hb |= (can && bad) ? 1u : 0u;
-  L.dd = L.dd || fin || (can && bad);
-  L.lit = ok ? !mph : L.lit;
+  L.mdd |= bal(fin || (can && bad));
+  const uint64_t okm = bal(ok);
+  L.mlit = (okm & bal(!mph)) | (~okm & L.mlit);
   L.rem = ok ? (mph ? ml : len) : L.rem;
   L.src = ok ? (mph ? L.d - off : L.sh + s1) : L.src;
   L.eff = ok ? (mph ? off : kStep) : L.eff;
-  L.far = ok ? (mph && off > kReach) : L.far;
+  L.mfar = (okm & bal(mph && off > kReach)) | (~okm & L.mfar);
   L.s = ok ? (mph ? s1 : lit_end) : L.s;
   L.mtok = (ok && !mph) ? (tok & 15) : L.mtok;
   L.lph = ok ? (mph ? 0u : (last ? 2u : 1u)) : L.lph;
@@ -557,7 +600,7 @@ __device__ __forceinline__ void snappy_parse(Lane& L, bool act, const uint8_t* i
   // written with & | and selects between computed values: short-circuit operators and
   // conditional expressions became divergent branches
   const uint32_t sn = L.clen;
-  const bool need = act & !L.dd & (L.rem == 0);
+  const bool need = act & !mbit(L.mdd) & (L.rem == 0);
   const bool fin = need & (L.s >= sn);
   // throttle (a hole delays the flush): after any step d - 16*fl <= 96, so the ring keeps every
   // unflushed byte and every far source (offset > kReach) is already flushed
@@ -587,25 +630,100 @@ __device__ __forceinline__ void snappy_parse(Lane& L, bool act, const uint8_t* i
   const bool bad_t = tl ? bad_lit : bad_cp;
   const bool bad = (s1 > sn) | (len > room) | bad_t;
   const bool ok = can & !bad, fail = can & bad;
-  L.err = L.err | fail;
-  L.dd = L.dd | fin | fail;
+  L.merr |= bal(fail);
+  L.mdd |= bal(fin | fail);
   const uint32_t src_lit = L.sh + s1, src_cp = L.d - cp_off, s_lit = s1 + len;
   const uint32_t src_new = tl ? src_lit : src_cp, eff_new = tl ? kStep : cp_off, s_new = tl ? s_lit : s1;
   const bool far_new = !tl & (cp_off > kReach);
-  L.lit = ok ? tl : L.lit;
-  L.far = ok ? far_new : L.far;
+  const uint64_t okm = bal(ok);
+  L.mlit = (okm & bal(tl)) | (~okm & L.mlit);
+  L.mfar = (okm & bal(far_new)) | (~okm & L.mfar);
   L.rem = vsel(ok, len, L.rem);
   L.src = vsel(ok, src_new, L.src);
   L.eff = vsel(ok, eff_new, L.eff);
   L.s = vsel(ok, s_new, L.s);
 }
 
+// The tag table (SLATE_LPB_TPARSE): per golang/snappy tag byte c (decode_other.go:19-110), the mask
+// of the header bytes after c that carry a length (long literals) or an offset (copies), and packed:
+// bit 31 literal, bits 24..26 the header length, bits 16..23 the length base (short literal xl + 1,
+// long literal 1, copy-1 4 + (xl & 7), copy-2/4 xl + 1), bits 8..10 copy-1's offset high bits.  One
+// ds_read_b64 per step replaces the tag's arithmetic.  2 KiB after the CRC tables.
+#ifndef SLATE_LPB_TPARSE
+#define SLATE_LPB_TPARSE 1
+#endif
+constexpr uint32_t kTagTabOff = kLpbTabBytes;
+constexpr uint32_t kTagTabBytes = SLATE_LPB_TPARSE ? 2048u : 0u;
+__device__ __forceinline__ v2u tag_entry(uint32_t c) {
+  const uint32_t t = c & 3, xl = c >> 2;
+  uint32_t mask, hl, lb, ohi = 0, lit = 0;
+  if (t == 0) {
+    lit = 1;
+    const uint32_t nb = xl >= 60 ? xl - 59 : 0u;
+    mask = nb ? 0xFFFFFFFFu >> (32 - 8 * nb) : 0u;
+    hl = 1 + nb;
+    lb = nb ? 1u : xl + 1;
+  } else if (t == 1) {
+    mask = 0xffu;
+    hl = 2;
+    lb = 4 + (xl & 7);
+    ohi = (c >> 5) << 8;
+  } else {
+    mask = t == 2 ? 0xffffu : 0xFFFFFFFFu;
+    hl = t == 2 ? 3u : 5u;
+    lb = xl + 1;
+  }
+  v2u e;
+  e.x = mask;
+  e.y = (lit << 31) | (hl << 24) | (lb << 16) | ohi;
+  return e;
+}
+__device__ __forceinline__ uint32_t rd32a(const uint8_t* ring, uint32_t a) {  // a: 4-byte aligned ring offset
+  return *reinterpret_cast<const uint32_t*>(ring + a);
+}
+// snappy_parse's results by the tag table: the window is the two aligned dwords holding bytes s .. s+4
+__device__ __forceinline__ void snappy_parse_t(Lane& L, uint64_t mact, const uint8_t* in, int32_t avail,
+                                               uint32_t lim_d) {
+  const uint32_t sn = L.clen;
+  const uint64_t need = mact & ~L.mdd & bal(L.rem == 0);
+  const uint64_t fin = need & bal(L.s >= sn);
+  const uint32_t s5 = min(L.s + 5, sn);
+  const uint64_t can = need & bal(L.s < sn) & bal(avail >= int32_t(s5)) & bal(L.d <= lim_d);
+  // bytes s .. s+4 lie in the two aligned dwords from (sh + s) & ~3: shifted down as one 64-bit value
+  const uint32_t p = L.sh + L.s;
+  const uint32_t d0 = rd32a(in, p & (kIR - 4)), d1 = rd32a(in, (p + 4) & (kIR - 4));
+  const uint64_t w = ((uint64_t(d1) << 32) | d0) >> ((p << 3) & 24);
+  const uint32_t c = uint32_t(w) & 0xff;
+  const uint32_t b14 = uint32_t(w >> 8);  // bytes s+1 .. s+4
+  const v2u e = *(const __attribute__((address_space(3))) v2u*)(kTagTabOff + 8 * c);
+  const uint32_t payload = b14 & e.x;
+  const uint64_t tl = bal(int32_t(e.y) < 0);
+  const uint32_t lb = (e.y >> 16) & 0xff, hl = (e.y >> 24) & 7;
+  const uint32_t len = __builtin_elementwise_add_sat(lb, msel(tl, payload, 0u));  // a long literal's length saturates
+  const uint32_t cp_off = (e.y & 0x700u) | payload;
+  const uint32_t s1 = L.s + hl;
+  const uint32_t room = L.dn - L.d, left = sn - s1;
+  const uint64_t bad = ugt(s1, sn) | bal(len > room) | (tl & bal(len > left)) | (~tl & (bal(cp_off == 0) | ugt(cp_off, L.d)));
+  const uint64_t ok = can & ~bad, fail = can & bad;
+  L.merr |= fail;
+  L.mdd |= fin | fail;
+  const uint32_t src_new = msel(tl, L.sh + s1, L.d - cp_off), eff_new = msel(tl, kStep, cp_off);
+  const uint32_t s_new = msel(tl, s1 + len, s1);
+  L.mlit = (ok & tl) | (~ok & L.mlit);
+  L.mfar = (ok & ~tl & bal(cp_off > kReach)) | (~ok & L.mfar);
+  L.rem = msel(ok, len, L.rem);
+  L.src = msel(ok, src_new, L.src);
+  L.eff = msel(ok, eff_new, L.eff);
+  L.s = msel(ok, s_new, L.s);
+}
+
 // One step: CRC (two of four steps), parse, a hole or a 16-byte move, and the row walker
 // (the other two steps).
 // kSlot: 0 and 2 absorb a CRC chunk; 1 and (when needed) 3 run the walker
 template <int kSlot, bool kLz4>
-__device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint8_t* in, const uint32_t* tab,
-                                          const Rsrc& R, uint32_t lim_d, uint32_t cend, uint32_t dbg) {
+__device__ __forceinline__ void lane_step(Lane& L, bool act, uint64_t mact, uint8_t* ring, uint8_t* in,
+                                          const uint32_t* tab, const Rsrc& R, uint32_t lim_d, uint32_t cend,
+                                          uint32_t dbg) {
 #ifdef SLATE_FORCE_DBG  // static instruction-count analysis only (tools/loop_mix.py)
   dbg = SLATE_FORCE_DBG;
 #endif
@@ -619,6 +737,7 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
   const int32_t avail = int32_t(cend) - int32_t(L.sh);  // committed payload bytes [0, avail)
   LPB_MARK(parse);
   if constexpr (kLz4) lz4_parse(L, act, in, avail, lim_d);
+  else if constexpr (SLATE_LPB_TPARSE) snappy_parse_t(L, mact, in, avail, lim_d);
   else snappy_parse(L, act, in, avail, lim_d);
   LPB_MARK(hole);
   // ---- a far copy (offset > kReach: its source left the ring and is flushed) goes on as holes
@@ -626,35 +745,38 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
   {
     // (a step before the merge of the previous iteration's hole source makes no hole: the merge
     // would take its pending flag for the old one)
-    const bool mk = (kSlot >= 1) & act & !L.dd & L.far & (L.rem != 0) & !L.hp & (L.d <= lim_d);
+    const uint64_t mk = (kSlot >= 1 ? mact : 0) & ~L.mdd & L.mfar & ~L.mhp & bal(L.rem != 0) & bal(L.d <= lim_d);
     const uint32_t n = min(L.rem, 16u);
-    L.hd = mk ? L.d : L.hd;
-    L.hl = mk ? n : L.hl;
-    L.qoff = mk ? L.out_rel + L.src : L.qoff;
-    L.hp = L.hp || mk;
-    L.d += mk ? n : 0u;
-    L.rem -= mk ? n : 0u;
-    L.src += mk ? n : 0u;
+    L.hd = msel(mk, L.d, L.hd);
+    L.hl = msel(mk, n, L.hl);
+    L.qoff = msel(mk, L.out_rel + L.src, L.qoff);
+    L.mhp |= mk;
+    const uint32_t nn = msel(mk, n, 0u);
+    L.d += nn;
+    L.rem -= nn;
+    L.src += nn;
   }
   // ---- move up to 16 bytes of a literal or a near copy into the output ring
   LPB_MARK(move);
   {
-    const bool cp = act & !L.dd & (L.rem != 0) & !L.far & (L.d <= lim_d);
+    const uint64_t cp = mact & ~L.mdd & ~L.mfar & bal(L.rem != 0) & bal(L.d <= lim_d);
     const uint32_t k16 = min(L.rem, kStep);
-    const uint32_t in_left = cend - L.src;
-    const uint32_t k_lit = min(k16, cend > L.src ? in_left : 0u), k_near = min(k16, L.eff);
-    uint32_t k = L.lit ? k_lit : k_near;
+    const uint32_t k_lit = min(k16, sub_sat(cend, L.src)), k_near = min(k16, L.eff);
+    uint32_t k = msel(L.mlit, k_lit, k_near);
     // a ring copy stops short of the pending hole's bytes
-    const uint32_t to_hole = L.hd - L.src, k_hole = L.src < L.hd ? to_hole : 0u;
-    const bool cut = !L.lit & L.hp & (L.src < L.hd + L.hl) & (L.src + k > L.hd);
-    k = cut ? k_hole : k;
-    k = cp ? k : 0u;
+    const uint32_t k_hole = sub_sat(L.hd, L.src);
+    const uint64_t cut = ~L.mlit & L.mhp & bal(L.src < L.hd + L.hl) & bal(L.src + k > L.hd);
+    k = msel(cut, k_hole, k);
+    k = msel(cp, k, 0u);
     // bytes from d on are not yet output: storing them when k == 0 is harmless; the first
     // dword keeps the bytes below d (L.T)
     const uint32_t b = L.d & 3;
-    const uint32_t m8 = (kOR == kIR || !L.lit) ? kOR - 8 : kIR - 8;
+    const uint32_t m8 = kOR == kIR ? kOR - 8 : msel(L.mlit, kIR - 8, kOR - 8);
     {
-      const v4u v = ring_rd16(L.lit ? in : ring, L.src, m8);
+      // the source ring: the input ring for a literal, the output ring for a copy (LDS offsets)
+      extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+      const uint32_t srb = msel(L.mlit, uint32_t(in - smem), uint32_t(ring - smem));
+      const v4u v = ring_rd16(smem + srb, L.src, m8);
       const Win5 y = shift_in(v, L.T, b);
       store_win(ring, L.d & ~3u, y);
       L.T = pick5(y, (b + k) >> 2);
@@ -662,10 +784,9 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
     L.d += k;
     L.rem -= k;
     // periodic output: once a whole period was copied, the pattern can be read twice as far back
-    const bool step_cp = (k != 0) & (k == L.eff) & !L.lit & (L.eff < kStep);
-    const uint32_t eff2 = step_cp ? 2 * L.eff : L.eff;
-    const uint32_t src_l = L.src + k, src_c = L.d - eff2;
-    L.src = L.lit ? src_l : src_c;
+    const uint64_t step_cp = ~L.mlit & bal(k != 0) & bal(k == L.eff) & bal(L.eff < kStep);
+    const uint32_t eff2 = msel(step_cp, 2 * L.eff, L.eff);
+    L.src = msel(L.mlit, L.src + k, L.d - eff2);
     L.eff = eff2;
   }
   LPB_MARK(walk);
@@ -688,18 +809,20 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint8_t* ring, uint
 // block of lane 16j+i, so every store instruction writes 16 runs of 64 contiguous bytes
 // instead of 64 scattered 16-byte pieces (tools/scatter_probe.hip: ~3.5x cheaper).
 __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
-                                                uint32_t dbg, uint32_t part) {
+                                                uint32_t dbg, uint32_t part, uint32_t flush_lane) {
   const bool mine = kFlushParts == 1 || (lane / kFlushBlocks) == part;
-  const uint32_t done = (act && mine) ? min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu) - L.fl : 0u;
+  const uint32_t done = (act && mine) ? min(L.d >> 4, msel(L.mhp, L.hd >> 4, 0xFFFFFFFFu)) - L.fl : 0u;
   const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
   const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
-  const uint32_t wave_lane0 = threadIdx.x - lane;
+  // the served block's ring: flush_lane (the kernel's constant for part 0, store 0) + the part's and
+  // the store's record offsets (the latter an immediate)
+  const uint8_t* ring_p = outs + flush_lane + part * (kFlushBlocks * kOutStride);
 #pragma unroll
   for (uint32_t j = 0; j < kFlushStores; j++) {
     const uint32_t o = part * kFlushBlocks + (64 / kRun) * j + lane / kRun, c = lane % kRun;
     const uint32_t info_o = __shfl(info, int(o), 64);
     const uint32_t base_o = __shfl(base, int(o), 64);
-    const uint8_t* ring_o = outs + (wave_lane0 + o) * kOutStride;
+    const uint8_t* ring_o = ring_p + (64 / kRun) * j * kOutStride;
     const v4u v = rd128(ring_o + ((((info_o & 127) + c) * 16) & (kOR - 1)), L.z);
     __builtin_amdgcn_raw_buffer_store_b128(v, R.out, (c < (info_o >> 7) && !(dbg & 1024)) ? base_o + 16 * c : kOOB, 0,
                                            kOutCpol);
@@ -761,11 +884,14 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
   {
     const uint32_t* src = &g_crc16.t[0][0];
     for (uint32_t i = threadIdx.x; i < kLpbTabBytes / 4; i += blockDim.x) tab[i] = src[i];
+    if constexpr (kTagTabBytes != 0)
+      for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
+        reinterpret_cast<v2u*>(smem + kTagTabOff)[i] = tag_entry(i);
     __syncthreads();
   }
   const uint32_t* crc_init = g_crc_lt.init;  // used once per round: constant memory
   const uint32_t* crc_tail = g_crc_lt.tail;
-  uint8_t* outs = smem + kLpbTabBytes;
+  uint8_t* outs = smem + kLpbTabBytes + kTagTabBytes;
   uint8_t* ins = outs + kLpb2Threads * kOutStride;
   uint8_t* ring = outs + threadIdx.x * kOutStride;
   uint8_t* in = ins + threadIdx.x * kInStride;
@@ -773,6 +899,9 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
   const uint32_t waves_total = gridDim.x * (kLpb2Threads / 64);
   const uint32_t wave_g = blockIdx.x * (kLpb2Threads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63;
+  // loop invariants of the transposed refill and flush (LDS offsets of the served blocks' rings)
+  const uint32_t slot_lane = (threadIdx.x - lane + (lane >> 2)) * kInStride;
+  const uint32_t flush_lane = (threadIdx.x - lane + lane / kRun) * kOutStride;
 
   // Rounds are handed out by an atomic counter (one dequeue per round, lane 0): waves that
   // finish early take more, so the launch ends when the work does, not when the unluckiest
@@ -811,13 +940,14 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     L.crc = 0xFFFFFFFFu;
     L.crc_pos = 0;
     L.s = L.d = L.rem = L.src = L.T = 0;
-    L.lit = L.far = L.err = false;
+    L.mlit = L.mfar = 0;
+    bool dd0 = true, err0 = false;  // the masks L.mdd / L.merr once every lane has set up
     L.z = a.rt_zero;
     L.eff = 16;
-    L.dd = true;
+
     L.c_issue = L.c_commit = L.n_req = L.fl = 0;
     L.qoff = kOOB;
-    L.hp = false;
+    L.mhp = 0;
     L.hd = L.hl = 0;
     L.R = 0;
     L.rphase = 0;
@@ -870,7 +1000,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
                     q2 = ring_rd8(in, L.sh + 16, kIR - 8);
           const uint32_t dw[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
           const uint32_t cap = uint32_t(min<uint64_t>(a.out_off[b + 1] - a.out_off[b], 0xFFFFFFF0ull));
-          if (lz4_frame_head(L, dw, cap, want_size)) L.dd = false;
+          if (lz4_frame_head(L, dw, cap, want_size)) dd0 = false;
           else L.hb = 1;
         }
       } else if (have) {
@@ -896,15 +1026,20 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
           }
         }
         if (!ok || x > kSnappyMaxExpansion * uint64_t(L.clen)) {
-          L.err = true;
+          err0 = true;
         } else {
           L.dn = uint32_t(x);
           L.s = hdr;
-          L.dd = false;
+          dd0 = false;
         }
       }
     }
 
+    L.mdd = bal(dd0);
+    L.merr = bal(err0);
+    // the refill's per-round invariant: the input offset of the block each lane serves in load j
+    const uint32_t rel0 = __shfl(L.in_rel, int(lane >> 2), 64), rel1 = __shfl(L.in_rel, int(16 + (lane >> 2)), 64),
+                   rel2 = __shfl(L.in_rel, int(32 + (lane >> 2)), 64), rel3 = __shfl(L.in_rel, int(48 + (lane >> 2)), 64);
     // ---------------- streaming decode, 64 blocks in lockstep
     uint32_t iters = 0, fin_iter = 0;
     const uint64_t t_round = (dbg_bits(a) & 512) ? __builtin_amdgcn_s_memtime() : 0;
@@ -914,51 +1049,50 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
     // `budget` iterations; the budget only guarantees that the loop ends (an exhausted
     // lane reports SLATE_E_HIP, never a wrong result).
     const uint32_t budget = have ? (L.clen + L.dn) / 2 + 1024 : 0u;
-    while (__ballot(have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
-                    iters < budget)) {
-      const bool act = have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk) &&
-                       iters < budget;
+    for (;;) {
+      const uint64_t mact =
+          bal(have) & bal(iters < budget) & ~(L.mdd & ~L.mhp & bal(int32_t(L.crc_pos) > L.crc_last) & bal(L.c_commit > L.last_chunk));
+      if (!mact) break;
+      const bool act = mbit(mact);
       LPB_MARK(refill);
-      commit_one(ins, S0, P0, L.z);
-      commit_one(ins, S1, P1, L.z);
-      commit_one(ins, S2, P2, L.z);
-      commit_one(ins, S3, P3, L.z);
+      commit_j<0>(ins, slot_lane, S0, P0, L.z);
+      commit_j<1>(ins, slot_lane, S1, P1, L.z);
+      commit_j<2>(ins, slot_lane, S2, P2, L.z);
+      commit_j<3>(ins, slot_lane, S3, P3, L.z);
       L.c_commit += L.n_req;
       // the next chunks' loads (committed at the next iteration's start)
       {
         // the ring keeps every chunk from the oldest byte still to be read or CRC'd
-        const uint32_t lo_pos = L.dd ? L.sh + L.clen : ((L.rem && L.lit) ? L.src : L.sh + L.s);
+        const uint32_t lo_pos = msel(L.mdd, L.sh + L.clen, msel(L.mlit & bal(L.rem != 0), L.src, L.sh + L.s));
         const uint32_t lo_chunk = min(lo_pos >> 4, L.crc_pos);
         const uint32_t n = refill_count(act, lo_chunk, L.c_issue, L.last_chunk);
         const uint32_t info = (L.c_issue << 3) | n;
-        const uint32_t wave_lane0 = threadIdx.x - lane;
-        const uint32_t rel = L.in_rel;
-        load_one(0, lane, wave_lane0, info, rel, R, P0, S0);
-        load_one(1, lane, wave_lane0, info, rel, R, P1, S1);
-        load_one(2, lane, wave_lane0, info, rel, R, P2, S2);
-        load_one(3, lane, wave_lane0, info, rel, R, P3, S3);
+        load_j<0>(lane, info, rel0, R, P0, S0);
+        load_j<1>(lane, info, rel1, R, P1, S1);
+        load_j<2>(lane, info, rel2, R, P2, S2);
+        load_j<3>(lane, info, rel3, R, P3, S3);
         L.c_issue += n;
         L.n_req = n;
       }
       // per iteration: the throttle's limit on d, and the end of the committed input (ring positions)
       const uint32_t lim_d = 16 * L.fl + kUnflushed, cend = 16 * L.c_commit;
       LPB_MARK(absorb);
-      lane_step<0, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      lane_step<0, kLz4>(L, act, mact, ring, in, tab, R, lim_d, cend, dbg_bits(a));
       absorb_hole(L, Q, ring);
-      lane_step<1, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
-      lane_step<2, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
-      lane_step<3, kLz4>(L, act, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      lane_step<1, kLz4>(L, act, mact, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      lane_step<2, kLz4>(L, act, mact, ring, in, tab, R, lim_d, cend, dbg_bits(a));
+      lane_step<3, kLz4>(L, act, mact, ring, in, tab, R, lim_d, cend, dbg_bits(a));
       // the hole source requested in this iteration (at most one per lane; sc1: L1 bypass),
       // before the flush stores so that vmcnt waits stay static; it is merged at the start of
       // the next iteration
       LPB_MARK(flush);
       Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg_bits(a) & 32768) ? kOOB : L.qoff, 0, 16);
       L.qoff = kOOB;
-      flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts);
+      flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts, flush_lane);
       if constexpr (kLz4) {
         // the content checksum's stripes: the chunks completed so far (up to kStep / 4), still in the ring
 #pragma unroll
-        for (uint32_t j = 0; j < kStep / 4; j++) xxh_absorb(L, ring, L.xp < min(L.d >> 4, L.hp ? L.hd >> 4 : 0xFFFFFFFFu));
+        for (uint32_t j = 0; j < kStep / 4; j++) xxh_absorb(L, ring, L.xp < min(L.d >> 4, msel(L.mhp, L.hd >> 4, 0xFFFFFFFFu)));
       }
       iters++;
       fin_iter = act ? iters : fin_iter;  // profiling (debug 131072): the lane's last active iteration
@@ -967,7 +1101,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
     // ---------------- finalise the round's blocks (SIMD across lanes)
     // iters counts the wave's iterations: a lane that finished early is not exhausted
-    if (have && !(L.dd && !L.hp && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk)) {
+    if (have && !(mbit(L.mdd) && !mbit(L.mhp) && int32_t(L.crc_pos) > L.crc_last && L.c_commit > L.last_chunk)) {
       m.status = SLATE_E_HIP;  // step budget exhausted (see above): a kernel defect, reported loudly
       a.meta[b] = m;
       have = false;
@@ -1003,7 +1137,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
           dec_ok = !hand_back;  // a mismatch: the exact path reports it
         }
       } else {
-        dec_ok = !L.err && L.d == L.dn && L.s == L.clen && L.rem == 0;
+        dec_ok = !mbit(L.merr) && L.d == L.dn && L.s == L.clen && L.rem == 0;
       }
       const uint32_t dn = L.dn;
       if (!crc_ok) {
@@ -1021,7 +1155,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         for (int i = 0; i < 16 && L.rphase < 3 && L.d >= L.rneed; i++) {
           v4u row;
           uint32_t ridx;
-          if (walk_step(L, ring, true, row, ridx)) reinterpret_cast<v4u*>(grows)[ridx] = row;
+          if (walk_step(L, ring, true, mbit(L.mhp), row, ridx)) reinterpret_cast<v4u*>(grows)[ridx] = row;
         }
         if (a.raw) {
           m.data_len = dn;  // a decompressed index / filter buffer
@@ -1174,7 +1308,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
 
 
 size_t lpb2_lds_bytes() {
-  return kLpbTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
+  return kLpbTabBytes + kTagTabBytes + size_t(kLpb2Threads) * (kOutStride + kInStride);
 }
 
 // CodecLz4 plan, lane per block: oracle lz4_frame_len's decoded size (the bytes the in-order

@@ -425,6 +425,10 @@ void par_memcpy(void* dst, const void* src, size_t n);
 hipError_t lane_init(PipeLane& L);
 // Large host <-> device copies through the context's page-locked lane staging (64 MiB pieces,
 // two in flight; stream-ordered on st, synchronous on return); small ones go straight through.
+// CodecNone / CodecSnappy block sizes known on the host (api_host.cpp): the decoded length from the
+// payload length or golang/snappy's varint header (0 for a header the decoder rejects)
+bool host_plannable(int codec);
+uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len);
 int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st);
 int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st);
 

@@ -121,6 +121,7 @@ struct DecodeScratch {
 };
 
 size_t decode_scratch_bytes(uint32_t n);
+size_t decode_scratch_bytes_codec(uint32_t n, int codec);
 hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
                               uint64_t* out_off, uint64_t* row_base, void* scratch);
 hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
@@ -161,6 +162,17 @@ hipError_t launch_blocks_to_host(hipStream_t st, const uint8_t* out, const uint6
 // One CodecNone / CodecSnappy block, one launch (slate_block_decode): host_in / host_out are device
 // addresses of page-locked host memory; out_sz = align16(decoded length), row_sz = its row capacity
 // (the plan the host computed with decoded_len's rules); a.in / a.out / a.rows: device scratch.
+// One small-batch block (launch_decode_small): offsets into the host-mapped staging (in_off: 16-byte
+// aligned input; out_off: decoded bytes), its row slots, and for the one-wave decoder the device
+// scratch offset of its decoded bytes (dev_out; its input goes at in_off, as in the staging).
+struct SmallDesc {
+  uint32_t block, in_len;
+  uint64_t in_off, out_off, out_sz, row_base, row_sz, dev_out;
+};
+hipError_t launch_decode_small(hipStream_t st, const DecodeArgs& a, const SmallDesc* descs, uint32_t n_par, uint32_t n,
+                               const uint8_t* hin, uint8_t* hout, uint8_t* dscr);
+bool small_par_fits(int codec, uint64_t in_len, uint64_t out_sz);
+bool small_wave_fits(uint64_t in_len, uint64_t out_sz);
 hipError_t launch_decode_one(hipStream_t st, const DecodeArgs& a, const uint8_t* host_in, uint64_t in_len,
                              uint64_t out_sz, uint64_t row_sz, uint8_t* host_out);
 hipError_t launch_rows_pack(hipStream_t st, const slate_block_meta* meta, const uint64_t* row_base, uint32_t n,

@@ -211,7 +211,9 @@ struct Win5 {
   uint32_t y0, y1, y2, y3, y4;
 };
 __device__ __forceinline__ Win5 shift_in(const v4u& v, uint32_t head, uint32_t b) {
-  const uint32_t sel = 0x07060504u - b * 0x01010101u;  // v_perm: byte i <- byte (4 - b + i) of {hi:lo}
+  // v_perm: byte i <- byte (4 - b + i) of {hi:lo}; b * 0x01010101 as a byte broadcast (v_perm), not a
+  // quarter-rate v_mul_lo_u32
+  const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, b, 0u);
   const uint32_t keep = (1u << (8 * b)) - 1u;
   Win5 w;
   w.y0 = (head & keep) | (__builtin_amdgcn_perm(v.x, head, sel) & ~keep);

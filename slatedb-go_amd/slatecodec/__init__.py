@@ -84,6 +84,7 @@ _SIGS = {
     "slate_ctx_gpu_busy": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int]),
     "slate_ctx_synchronize": (C.c_int, [vp]),
     "slate_decode_scratch_bytes": (C.c_size_t, [C.c_uint32]),
+    "slate_decode_scratch_bytes_codec": (C.c_size_t, [C.c_uint32, C.c_int]),
     "slate_block_decode_plan_device": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, vp, vp]),
     "slate_block_decode_device": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, vp, vp, vp, vp]),
     "slate_block_decode_batch": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp, C.c_uint64, vp, vp, vp,
@@ -172,7 +173,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise SlateError(E_NO_DEVICE, f"{LIB_PATH} missing (run __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
+        variant = bool(os.environ.get("SLATE_LIB_VARIANT"))
         for name, (res, args) in _SIGS.items():
+            if variant and not hasattr(L, name):  # an older library in an A/B run: entry points it predates
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -593,6 +597,21 @@ def compact(ctx: "Context", sources: list[list[bytes]], max_sst_size: int, block
     blob = np.frombuffer(b"".join(flat) or b"\0", np.uint8)
     off = np.concatenate([[0], np.cumsum([len(s) for s in flat])]).astype(np.uint64)
     src = np.concatenate([[0], np.cumsum([len(r) for r in sources])]).astype(np.uint32)
+    return [a.tobytes() for a in compact_arrays(ctx, blob, off, src, max_sst_size, block_size, min_filter_keys,
+                                                filter_bits_per_key, codec)]
+
+
+def compact_arrays(ctx: "Context", blob: np.ndarray, off: np.ndarray, src: np.ndarray, max_sst_size: int,
+                   block_size: int = 4096, min_filter_keys: int = 0, filter_bits_per_key: int = 10, codec: int = NONE,
+                   sink: np.ndarray | None = None) -> list[np.ndarray]:
+    """slate_compact over SSTs packed in one array (sst i = blob[off[i]:off[i+1]], source j = SSTs
+    src[j]..src[j+1]) as a cgo caller passes them: the output SSTs encoded back to back into `sink`
+    (reused when large enough) -> views of it, one per output."""
+    blob = np.ascontiguousarray(blob, np.uint8)
+    off = np.ascontiguousarray(off, np.uint64)
+    src = np.ascontiguousarray(src, np.uint32)
+    flat = range(len(off) - 1)
+    sources = range(len(src) - 1)
     cfg = SstConfig(block_size, min_filter_keys, filter_bits_per_key, codec)
     cap = 16
     while True:
@@ -604,10 +623,14 @@ def compact(ctx: "Context", sources: list[list[bytes]], max_sst_size: int, block
             cap = n.value
             continue
         _check(st, "slate_compact")
-        out = []
-        for k in range(n.value):
-            t = SstTable(tabs[k])
-            out.append(t.encode())
+        tables = [SstTable(tabs[k]) for k in range(n.value)]
+        sizes = [int(lib().slate_sst_table_encoded_len(t._h)) for t in tables]
+        if sink is None or sink.size < sum(sizes) + 1:
+            sink = np.empty(sum(sizes) + 1, np.uint8)
+        out, at = [], 0
+        for t, z in zip(tables, sizes):
+            out.append(t.encode_array(sink[at:at + z + 1])[:z])
+            at += z
         return out
 
 
@@ -852,8 +875,10 @@ def read_info(sst: bytes) -> tuple[int, "SstInfo", bytes]:
     return st, info, fk[: info.first_key_len].tobytes()
 
 
-def decode_scratch_bytes(n: int) -> int:
-    return lib().slate_decode_scratch_bytes(n)
+def decode_scratch_bytes(n: int, codec: int = None) -> int:
+    if codec is None:
+        return lib().slate_decode_scratch_bytes(n)
+    return lib().slate_decode_scratch_bytes_codec(n, codec)
 
 
 def header_symbols() -> list[str]:

@@ -2,8 +2,13 @@
  * (tooling for bench.py's per_call leg; tools/percall_bench.py writes the input file):
  *   slate_block_decode  (block.Decode, internal/sstable/block/block.go:78) against the oracle's
  *                       or_block_decode (CPU baseline, one thread), same blocks, same order;
- *   slate_block_seek    (block.NewIteratorAtKey) over one decoded block against or_block_seek.
- * Input file: u32 n, n x (u32 len, bytes) Snappy blocks, then u32 klen, key bytes (a key of block 0).
+ *   slate_block_seek    (block.NewIteratorAtKey) over one decoded block against or_block_seek;
+ *   slate_block_reader  (sstable.Iterator.nextBlockIter, iterator.go:92-118, with read-ahead) over
+ *                       every block of one Snappy SST: us per block, the caller's loop as a cgo shim
+ *                       runs it (next; on NEED_DATA want + the range's bytes + feed), the object
+ *                       store's GetRange standing in as a pointer into the SST in memory.
+ * Input file: u32 n, n x (u32 len, bytes) Snappy blocks, then u32 klen, key bytes (a key of block 0),
+ * then (optional) u64 sst_len, the SST's bytes, u32 read_ahead.
  * usage: percall FILE CALLS   -> one JSON object on stdout */
 #include <stdint.h>
 #include <stdio.h>
@@ -42,6 +47,14 @@ int main(int argc, char** argv) {
   const uint32_t klen = rd32(f);
   uint8_t* key = malloc(klen + 1);
   if (fread(key, 1, klen, f) != klen) return 2;
+  uint64_t sst_len = 0;
+  uint8_t* sst = NULL;
+  uint32_t ahead = 64;
+  if (fread(&sst_len, 8, 1, f) == 1 && sst_len) {
+    sst = malloc(sst_len);
+    if (fread(sst, 1, sst_len, f) != sst_len) return 2;
+    ahead = rd32(f);
+  }
   fclose(f);
 
   int st = 0;
@@ -97,9 +110,64 @@ int main(int argc, char** argv) {
   }
   const double cpu_seek = (now_us() - t0) / calls;
   if (s0 != res.start || fi != res.first_idx) return 9;
+  /* sstable.Iterator over one SST through the read-ahead reader: every block, in order */
+  double reader_us = -1.0, reader_oracle_us = -1.0;
+  uint64_t reader_blocks = 0, reader_rows = 0;
+  if (sst) {
+    slate_sst_info info;
+    slate_index* index = NULL;
+    uint8_t* fk = malloc(sst_len);
+    if (slate_sst_read_info(sst, sst_len, &info, fk, sst_len)) return 10;
+    free(fk);
+    if (slate_decode_index(ctx, sst + info.index_offset, info.index_len, info.codec, &index)) return 11;
+    const uint64_t nb = slate_index_num_blocks(index);
+    double best = 1e30;
+    for (int pass = 0; pass < 6; pass++) { /* pass 0 warms up (staging allocations, code objects) */
+      slate_block_reader* r = NULL;
+      if (slate_block_reader_create(ctx, &info, index, 0, ahead, &r)) return 12;
+      uint64_t got = 0, rows = 0;
+      const double t = now_us();
+      for (;;) {
+        slate_block_view v;
+        st = slate_block_reader_next(r, &v);
+        if (st == SLATE_E_READER_END) break;
+        if (st == SLATE_E_READER_NEED_DATA) {
+          uint64_t rs, re;
+          if (slate_block_reader_want(r, &rs, &re)) return 13;
+          if (slate_block_reader_feed(r, sst + rs, re - rs)) return 14;
+          continue;
+        }
+        if (st || v.block != got) return 15;
+        rows += v.meta.n_rows; /* the caller reads the block: its meta and rows */
+        got++;
+      }
+      const double us = (now_us() - t) / (double)nb;
+      slate_block_reader_free(r);
+      if (got != nb) return 16;
+      if (pass && us < best) best = us;
+      reader_rows = rows;
+    }
+    reader_us = best;
+    reader_blocks = nb;
+    /* the oracle: the same blocks, one thread, block.Decode per block (what nextBlockIter calls) */
+    uint64_t* offs = malloc(8 * (nb + 1));
+    if (slate_index_block_offsets(index, offs, nb)) return 17;
+    offs[nb] = info.filter_offset;
+    t0 = now_us();
+    for (uint64_t b = 0; b < nb; b++) {
+      st = or_block_decode(sst + offs[b], offs[b + 1] - offs[b], info.codec, out, cap, &ol, &om, rows, 70000);
+      if (st || om.status) return 18;
+    }
+    reader_oracle_us = (now_us() - t0) / (double)nb;
+    free(offs);
+    slate_index_free(index);
+  }
   printf("{\"calls\": %d, \"slate_block_decode_us\": %.2f, \"oracle_block_decode_us_1thread\": %.2f, "
-         "\"slate_block_seek_us\": %.2f, \"oracle_block_seek_us_1thread\": %.2f}\n",
-         calls, gpu_dec, cpu_dec, gpu_seek, cpu_seek);
+         "\"slate_block_seek_us\": %.2f, \"oracle_block_seek_us_1thread\": %.2f, "
+         "\"reader_blocks\": %llu, \"reader_rows\": %llu, \"reader_read_ahead\": %u, "
+         "\"slate_block_reader_us_per_block\": %.3f, \"oracle_block_decode_us_per_block_1thread\": %.3f}\n",
+         calls, gpu_dec, cpu_dec, gpu_seek, cpu_seek, (unsigned long long)reader_blocks,
+         (unsigned long long)reader_rows, ahead, reader_us, reader_oracle_us);
   slate_ctx_destroy(ctx);
   return 0;
 }

@@ -81,23 +81,38 @@ def per_call(ctx, sc, ob, wl, calls=400):
     res["slate_block_decode_batch64_us_per_block"] = round(_us(gpu_batch64, max(calls // 8, 10)) / 64, 2)
     res["python_binding_overhead_note"] = ("the *_us figures above are per Python call (ctypes, numpy "
                                            "allocations) for both sides; c_abi has the same calls from C")
-    res["c_abi"] = c_harness(blocks, key, calls)
+    res["c_abi"] = c_harness(blocks, key, calls, reader_sst(ctx, sc))
     return res
 
 
-def write_harness_input(path, blocks, key):
-    """tools/build/percall's input: the blocks, then the seek key."""
+def write_harness_input(path, blocks, key, sst=None, read_ahead=64):
+    """tools/build/percall's input: the blocks, then the seek key, then (optional) one SST for the
+    read-ahead reader."""
     import struct
     with open(path, "wb") as f:
         f.write(struct.pack("<I", len(blocks)))
         for b in blocks:
             f.write(struct.pack("<I", len(b)) + b)
         f.write(struct.pack("<I", len(key)) + bytes(key))
+        if sst is not None:
+            f.write(struct.pack("<Q", len(sst)) + bytes(sst) + struct.pack("<I", read_ahead))
 
 
-def c_harness(blocks, key, calls):
+def reader_sst(ctx, sc, n_blocks=2048):
+    """A Snappy SST of configs[1]-shaped blocks (k%015d keys, 84 B V-half values, 38 rows per 4 KiB
+    block) for the reader leg, built by the library's SstBuilder."""
+    rng = np.random.default_rng(20250307)
+    b = sc.SstBuilder(ctx, 4096, 0, 10, sc.SNAPPY)
+    for i in range(38 * n_blocks):
+        r = rng.integers(0, 256, 42, dtype=np.uint8).tobytes()
+        assert b.add_value(b"k%015d" % i, r + r) == 0
+    return b.build().encode()
+
+
+def c_harness(blocks, key, calls, sst=None):
     """The same blocks and key through tools/build/percall (C, as a cgo shim calls the library),
-    slate_block_decode / slate_block_seek against the oracle's or_block_decode / or_block_seek."""
+    slate_block_decode / slate_block_seek against the oracle's or_block_decode / or_block_seek, and
+    the read-ahead reader over every block of `sst` against the oracle's block.Decode per block."""
     import subprocess
     import tempfile
     exe = os.path.join(REPO, "tools", "build", "percall")
@@ -105,7 +120,7 @@ def c_harness(blocks, key, calls):
         return {"skipped": "tools/build/percall not built (make -C tools)"}
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
         path = f.name
-    write_harness_input(path, blocks, key)
+    write_harness_input(path, blocks, key, sst)
     try:
         r = subprocess.run([exe, path, str(max(calls, 200) * 5)], capture_output=True, text=True, timeout=120)
     finally:
