@@ -72,34 +72,62 @@ struct Warn {
 // block.Decode ends its SST (sstable.Iterator.Next, iterator.go:59-68), a row that fails ends its
 // block (block/iterator.go:92-96); each adds a warning.  blocks: the SSTs' data-block byte ranges,
 // gathered on the host; sst0 / sst_src: the first SST's index and every SST's source.
-int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, const std::vector<uint64_t>& in_off,
+// One host range of the group's data blocks (an SST's [offs[0], FilterOffset)), uploaded as it lies
+// in the caller's buffer: no host-side gather of the blocks first.
+struct Piece {
+  const uint8_t* p;
+  uint64_t len;
+};
+
+int decode_group(slate_ctx* ctx, int codec, const std::vector<Piece>& pieces, const std::vector<uint64_t>& in_off,
                  const std::vector<uint32_t>& sst_blocks, uint32_t sst0, const std::vector<uint32_t>& sst_src, View* v,
                  std::vector<uint64_t>* rows_per_sst, std::vector<Warn>* warns) {
   const uint32_t n = uint32_t(in_off.size() - 1);
   hipStream_t st = ctx->stream;
-  DEV(d_in, blob.size() + 16);
+  const uint64_t total = in_off.back();
+  DEV(d_in, total + 16);
   DEV(d_in_off, in_off.size() * 8);
   DEV(d_out_off, (size_t(n) + 1) * 8);
   DEV(d_row_base, (size_t(n) + 1) * 8);
   DEV(d_scr, decode_scratch_bytes_codec(n, codec) + 64);
-  int s = ctx_h2d(ctx, d_in->b.p, blob.data(), blob.size(), st);
-  if (s) return s;
-  SLATE_HIP(hipMemcpyAsync(d_in_off->b.p, in_off.data(), in_off.size() * 8, hipMemcpyHostToDevice, st));
-  {
-    GpuSpan gs(ctx, st);  // device time (slate_ctx_set_timing): every kernel group of the compaction
-    SLATE_HIP(launch_decode_plan(st, codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n,
-                                 d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), d_scr->b.p));
+  int s = SLATE_OK;
+  uint64_t at = 0;
+  for (const Piece& pc : pieces) {
+    if ((s = ctx_h2d(ctx, d_in->as<uint8_t>() + at, pc.p, pc.len, st))) return s;
+    at += pc.len;
   }
-  uint64_t tot[2];
-  if ((s = d2h_small(ctx, &tot[0], d_out_off->as<uint64_t>() + n, 8))) return s;
-  if ((s = d2h_small(ctx, &tot[1], d_row_base->as<uint64_t>() + n, 8))) return s;
+  SLATE_HIP(hipMemcpyAsync(d_in_off->b.p, in_off.data(), in_off.size() * 8, hipMemcpyHostToDevice, st));
+  // CodecNone: block.Decode's Data aliases the input (block.go:122), so the decoded blocks are the
+  // uploaded bytes themselves -- no plan, no decoded copy; the row slots from the payload lengths
+  const bool alias = codec == SLATE_CODEC_NONE;
+  uint64_t tot[2] = {0, 0};
+  if (alias) {
+    std::vector<uint64_t> rb(size_t(n) + 1, 0);
+    for (uint32_t i = 0; i < n; i++) {
+      const uint64_t len = in_off[i + 1] - in_off[i];
+      rb[i + 1] = rb[i] + row_capacity(len >= 6 ? len - 4 : 0);  // plan_reduce_kernel's CodecNone sizes
+    }
+    tot[1] = rb[n];
+    SLATE_HIP(hipMemcpyAsync(d_row_base->b.p, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, st));
+  } else {
+    {
+      GpuSpan gs(ctx, st);  // device time (slate_ctx_set_timing): every kernel group of the compaction
+      SLATE_HIP(launch_decode_plan(st, codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n,
+                                   d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), d_scr->b.p));
+    }
+    if ((s = d2h_small(ctx, &tot[0], d_out_off->as<uint64_t>() + n, 8))) return s;
+    if ((s = d2h_small(ctx, &tot[1], d_row_base->as<uint64_t>() + n, 8))) return s;
+  }
   const uint64_t slots = tot[1];
   if (slots >= 0xFFFFFFFFull) return SLATE_E_LIMIT;
-  DEV(d_out, tot[0] + 16);
+  DEV(d_out, alias ? 16 : tot[0] + 16);
   DEV(d_meta, size_t(n) * sizeof(slate_block_meta));
   DEV(d_rows, (slots + 1) * sizeof(slate_row));
-  DecodeArgs a{codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(),
+  uint8_t* data = alias ? d_in->as<uint8_t>() : d_out->as<uint8_t>();
+  const uint64_t* data_off = alias ? d_in_off->as<uint64_t>() : d_out_off->as<uint64_t>();
+  DecodeArgs a{codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n, data, data_off,
                d_meta->as<slate_block_meta>(), d_rows->as<slate_row>(), d_row_base->as<uint64_t>(), nullptr, nullptr, 0};
+  a.no_data = alias ? 1u : 0u;
   if (st == ctx->stream) a.side = &ctx->side;
   a.handbacks = ctx_handbacks(ctx);
   {
@@ -179,7 +207,7 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<uint8_t>& blob, co
   DEV(vals, vb + 16);
   {
     GpuSpan gs(ctx, st);
-    SLATE_HIP(launch_rows_copy(st, d_out->as<uint8_t>(), d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), n,
+    SLATE_HIP(launch_rows_copy(st, data, data_off, d_row_base->as<uint64_t>(), n,
                                d_rows->as<slate_row>(), slots, d_nkv->as<uint64_t>(), d_kvs->b.p,
                                key_off->as<uint64_t>(), keys->as<uint8_t>(), val_off->as<uint64_t>(),
                                vals->as<uint8_t>()));
@@ -317,23 +345,23 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
   for (uint32_t i = 0; i < n_sst;) {
     uint32_t e = i;
     while (e < n_sst && codec[e] == codec[i]) e++;
-    std::vector<uint8_t> blob;
+    std::vector<Piece> pieces;
     std::vector<uint64_t> in_off{0};
     std::vector<uint32_t> sst_blocks{0};
+    uint64_t base = 0;
     for (uint32_t j = i; j < e; j++) {
       const std::vector<uint64_t>& o = offs[j];
       if (o.size() > 1) {  // the data blocks are contiguous: [offs[0], FilterOffset)
-        const uint8_t* sst = ssts + sst_off[j];
-        const uint64_t base = blob.size();
-        blob.insert(blob.end(), sst + o[0], sst + o.back());
+        pieces.push_back({ssts + sst_off[j] + o[0], o.back() - o[0]});
         for (size_t b = 1; b < o.size(); b++) in_off.push_back(base + (o[b] - o[0]));
+        base += o.back() - o[0];
       }
       sst_blocks.push_back(uint32_t(in_off.size() - 1));
     }
     mark("gather blocks (host)");
     if (in_off.size() > 1) {
       View v;
-      int s = decode_group(ctx, codec[i], blob, in_off, sst_blocks, i, sst_src, &v, &rows_per_sst, &wl);
+      int s = decode_group(ctx, codec[i], pieces, in_off, sst_blocks, i, sst_src, &v, &rows_per_sst, &wl);
       mark("decode + row views");
       if (s) return s;
       views.push_back(v);
@@ -428,8 +456,10 @@ int slate_compact_ex(slate_ctx* ctx, const uint8_t* ssts, const uint64_t* sst_of
   std::vector<uint64_t> hko(m + 1), hvo(m + 1);
   if ((s = ctx_d2h(ctx, hko.data(), okey_off->b.p, (m + 1) * 8, st))) return s;
   if ((s = ctx_d2h(ctx, hvo.data(), oval_off->b.p, (m + 1) * 8, st))) return s;
+  mark("gather: offsets D2H");
   DEV(okeys, hko[m] + 16);
   DEV(ovals, hvo[m] + 16);
+  mark("gather: allocations");
   {
     GpuSpan gs(ctx, st);
     SLATE_HIP(launch_gather_copy(st, d_idx->as<uint32_t>(), m, all.keys->as<uint8_t>(),

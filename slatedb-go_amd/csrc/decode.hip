@@ -1046,8 +1046,10 @@ __device__ bool decode_block_wave(const DecodeArgs& a, uint32_t b, const WaveBuf
     return true;
   }
   __builtin_amdgcn_wave_barrier();
-  // ---- write the decoded buffer back (16-aligned destination)
-  if (G) {
+  // ---- write the decoded buffer back (16-aligned destination); a.no_data (CodecNone aliased in
+  // place): the bytes are already there
+  if (a.no_data) {
+  } else if (G) {
     if (buf != w.out)
       for (uint32_t c = lane; c < n; c += kWave) w.out[c] = buf[c];
   } else if (!(dbg_bits(a) & 8)) {

@@ -47,6 +47,13 @@ constexpr int kNoneCpol = SLATE_NONE_CPOL;
 #define SLATE_NONE_LDPOL 2
 #endif
 constexpr int kNoneLdpol = SLATE_NONE_LDPOL;
+// The decoded block is stored as soon as its chunks are formed, before the CRC's lane tree, so the
+// stores drain while the tree's dependent lookups run (round 6).  A block whose CRC then fails has
+// its meta say so; its output slot's bytes are unspecified, as Go sets no Block.Data on an error
+// (block.go:85-88) and the parity tests compare bytes only of blocks that decoded.
+#ifndef SLATE_NONE_EARLY_STORE
+#define SLATE_NONE_EARLY_STORE 1
+#endif
 static_assert(kNoneWgPerCu * kNoneLds <= 163840, "workgroups per CU");
 
 // 4 bytes at byte position p of a wave's LDS stage (two aligned dword reads)
@@ -217,6 +224,15 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
         acc = (q == 0 ? 0u : adv_tab<5>(lds, acc)) ^ (none ? 0u : k);
       }
     }
+    if (SLATE_NONE_EARLY_STORE) {
+      const __amdgpu_buffer_rsrc_t RO = make_rsrc(a.out + sload(a.out_off + bc), 16 * uint64_t(nout));
+#pragma unroll
+      for (uint32_t q = 0; q < 5; q++) {
+        const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
+        __builtin_amdgcn_raw_buffer_store_b128(O[q], RO, (j >= 0 && !(dbg_bits(a) & 8) && !a.no_data) ? uint32_t(16 * j) : kOOB,
+                                               0, kNoneCpol);
+      }
+    }
     bool crc_ok = true;
     if (!(dbg_bits(a) & 1)) {
       // lane tree: lane l's chunks end 16 (63 - l) bytes before lane 63's; inside rows of 16 lanes
@@ -254,10 +270,10 @@ __device__ __forceinline__ void none_block(const DecodeArgs& a, const uint32_t* 
       // ---- the decoded block (16-byte slots; bytes after the data are padding)
       const __amdgpu_buffer_rsrc_t RO = make_rsrc(a.out + sload(a.out_off + bc), 16 * uint64_t(nout));
 #pragma unroll
-      for (uint32_t q = 0; q < 5; q++) {
+      for (uint32_t q = 0; q < 5 && !SLATE_NONE_EARLY_STORE; q++) {
         const int32_t j = int32_t(64 * q + lane) - int32_t(pad);
-        __builtin_amdgcn_raw_buffer_store_b128(O[q], RO, (j >= 0 && !(dbg_bits(a) & 8)) ? uint32_t(16 * j) : kOOB, 0,
-                                               kNoneCpol);
+        __builtin_amdgcn_raw_buffer_store_b128(O[q], RO, (j >= 0 && !(dbg_bits(a) & 8) && !a.no_data) ? uint32_t(16 * j) : kOOB,
+                                               0, kNoneCpol);
       }
       // ---- block.go:101-134 and the rows (rows.h block_finish arithmetic)
       const uint32_t n = clen;

@@ -68,6 +68,10 @@ struct DecodeArgs {
   uint32_t* round_counter = nullptr;  // decode_lpb2: rounds handed out so far (launcher zeroes it)
   SideStream* side = nullptr;         // host only: the caller's side stream (nullptr: one stream)
   uint64_t* handbacks = nullptr;      // device counter: blocks a fast path handed to the exact path
+  // CodecNone only: the decoded bytes are not written -- out / out_off alias in / in_off, as
+  // block.Decode aliases the input for CodecNone (block.go:122, compression.go:128-129); meta and
+  // rows as always (slate_compact's row views read the uploaded SSTs)
+  uint32_t no_data = 0;
 };
 
 // Ablation bits.  The shipped library is built without SLATE_PROFILING_BUILD, so every

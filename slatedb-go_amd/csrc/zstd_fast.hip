@@ -1589,7 +1589,12 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   hipStream_t sh = st;
   if (f && f->get() && hipEventRecord(f->fork, st) == hipSuccess && hipStreamWaitEvent(f->s, f->fork, 0) == hipSuccess)
     sh = f->s;
-  zs_fast_huf_kernel<<<uint32_t(num_cus) * 2u, kZfHufThreads, lds_h, sh>>>(a, z);
+  static const uint32_t huf_wg = [] {  // phase B' workgroups per CU (A/B runs: SLATE_ZF_HUF_WG, 1..3)
+    const char* e = getenv("SLATE_ZF_HUF_WG");
+    const uint32_t v = e ? uint32_t(atoi(e)) : 2u;
+    return v >= 1 && v <= 163840 / kZfHufLds ? v : 2u;
+  }();
+  zs_fast_huf_kernel<<<uint32_t(num_cus) * huf_wg, kZfHufThreads, lds_h, sh>>>(a, z);
   zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
   if (sh != st) {
     hipError_t e = hipEventRecord(f->join, sh);

@@ -67,7 +67,7 @@ def per_call(ctx, sc, ob, wl, calls=400):
         ob.block_seek(data0, offs0, key)
 
     if "--dump" in sys.argv:  # the C harness's input only (for a rocprofv3 run of tools/build/percall)
-        write_harness_input(sys.argv[sys.argv.index("--dump") + 1], blocks, key)
+        write_harness_input(sys.argv[sys.argv.index("--dump") + 1], blocks, key, reader_sst(ctx, sc))
         return {"dumped": sys.argv[sys.argv.index("--dump") + 1]}
     res["slate_block_seek_us"] = round(_us(gpu_seek, calls), 1)
     res["oracle_block_seek_us_1thread"] = round(_us(cpu_seek, calls), 1)
