@@ -282,7 +282,13 @@ int slate_devbuf_download_async(slate_ctx* ctx, slate_hostbuf* dst, uint64_t dst
  *   d_out_off[n] and d_row_base[n].  d_scratch must hold slate_decode_scratch_bytes(n).
  * Step 2 (decode): writes the decoded buffer (rows || BE16 offsets || BE16 count)
  *   of block i at d_out + d_out_off[i], its meta and its row descriptors.
- * Both enqueue on the context stream and return without synchronising. */
+ * Both enqueue on the context stream and return without synchronising.
+ * CodecZlib (n >= 64): a zlib stream carries no decoded size, so the plan inflates every block
+ * (lane per block) and keeps what it parsed -- literals, matches, the Adler-32 -- in the context;
+ * the next decode call on the context with the same d_in, d_in_off, d_out_off and n, on the same
+ * stream, builds the blocks from it instead of inflating again (each stream inflated once per
+ * plan + decode).  As for every codec, the input must not change between the two calls (the
+ * plan's sizes depend on it).  Any other decode call inflates by itself. */
 size_t slate_decode_scratch_bytes(uint32_t n_blocks);
 /* The scratch one codec needs (<= slate_decode_scratch_bytes): CodecNone / CodecSnappy batches
  * skip the Zstd / Zlib / LZ4 fast paths' records and sequence slots (~8 B per block instead of
@@ -447,7 +453,9 @@ int slate_read_blocks(slate_ctx* ctx, const slate_sst_info* info, const slate_in
  * asks ReadBlocksUsingIndex for one block per call; this reader keeps that contract -- the blocks
  * in order from first_block, one at a time, an iteration that ends at the first failing block
  * with that block's status -- but fetches and decodes read_ahead blocks per GPU call (one object-
- * store range read and one batch).  The caller's loop:
+ * store range read and one batch), up to three batches held: next asks for the following batch as
+ * soon as a slot is free, before serving the current one, so fetch and decode run ahead of the
+ * walk (feed queues the decode and returns).  The caller's loop:
  *   st = slate_block_reader_next(r, &view):
  *     SLATE_OK                 view is the next block (pointers valid until the next feed);
  *     SLATE_E_READER_NEED_DATA slate_block_reader_want(r, &rs, &re) gives the SST byte range to

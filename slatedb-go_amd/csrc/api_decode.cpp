@@ -221,6 +221,23 @@ int slate_block_decode_plan_device(slate_ctx* ctx, int codec, const uint8_t* d_i
                                    uint32_t n, uint64_t* d_out_off, uint64_t* d_row_base, void* d_scratch) {
   if (!ctx || !d_in_off || !d_out_off || !d_row_base || !d_scratch) return SLATE_E_INVALID_ARG;
   SLATE_HIP(ctx_bind(ctx));
+  ctx->zl_armed = false;
+  // CodecZlib: the plan is phase Z itself (the stream has no decoded size to read off), its output
+  // kept in the context for the decode call that follows (each stream inflated once, not twice)
+  // (SLATE_ZL_NO_STAGE, read per call: same-process A/B runs, tools/zlib_ab.py)
+  if (codec == SLATE_CODEC_ZLIB && n >= 64 && d_in && !getenv("SLATE_ZL_NO_STAGE")) {
+    SLATE_HIP(ctx->zl_stage.ensure(zl_stage_bytes(n)));
+    const ZlStage g = zl_stage_carve(ctx->zl_stage.p, n);
+    SLATE_HIP(launch_decode_plan(ctx->stream, codec, d_in, d_in_off, n, d_out_off, d_row_base, d_scratch, &g,
+                                 ctx->num_cus));
+    ctx->zl_plan.in = d_in;
+    ctx->zl_plan.in_off = d_in_off;
+    ctx->zl_plan.out_off = d_out_off;
+    ctx->zl_plan.n = n;
+    ctx->zl_plan.stream = ctx->stream;
+    ctx->zl_armed = true;
+    return SLATE_OK;
+  }
   SLATE_HIP(launch_decode_plan(ctx->stream, codec, d_in, d_in_off, n, d_out_off, d_row_base, d_scratch));
   return SLATE_OK;
 }
@@ -236,7 +253,14 @@ int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, co
   DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
   a.side = &ctx->side;
   a.handbacks = ctx_handbacks(ctx);
-  SLATE_HIP(launch_decode(ctx->stream, a, ctx->d_scratch.p, ctx->num_cus));
+  // the staged plan of exactly these inputs and plan outputs, on this stream, not yet used
+  const bool staged = ctx->zl_armed && codec == SLATE_CODEC_ZLIB && ctx->zl_plan.in == d_in &&
+                      ctx->zl_plan.in_off == d_in_off && ctx->zl_plan.out_off == d_out_off &&
+                      ctx->zl_plan.n == n && ctx->zl_plan.stream == ctx->stream;
+  ctx->zl_armed = false;
+  ZlStage g{};
+  if (staged) g = zl_stage_carve(ctx->zl_stage.p, n);
+  SLATE_HIP(launch_decode(ctx->stream, a, ctx->d_scratch.p, ctx->num_cus, staged ? &g : nullptr));
   return SLATE_OK;
 }
 

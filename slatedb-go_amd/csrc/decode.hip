@@ -1635,8 +1635,29 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   return s;
 }
 
+size_t zl_stage_bytes(uint32_t n) {
+  return align16(size_t(n) * sizeof(ZsFastRec)) + size_t(n) * kZfSeqSlot * sizeof(uint32_t) +
+         align16(size_t(n) * sizeof(uint32_t)) + 16 + size_t(n) * kZlStageStride;
+}
+
+ZlStage zl_stage_carve(void* base, uint32_t n) {
+  ZlStage g;
+  uint8_t* p = static_cast<uint8_t*>(base);
+  g.rec = reinterpret_cast<ZsFastRec*>(p);
+  p += align16(size_t(n) * sizeof(ZsFastRec));
+  g.seq = reinterpret_cast<uint32_t*>(p);
+  p += size_t(n) * kZfSeqSlot * sizeof(uint32_t);
+  g.list = reinterpret_cast<uint32_t*>(p);
+  p += align16(size_t(n) * sizeof(uint32_t));
+  g.count = reinterpret_cast<uint32_t*>(p);
+  p += 16;
+  g.lit = p;
+  return g;
+}
+
 hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
-                              uint64_t* out_off, uint64_t* row_base, void* scratch) {
+                              uint64_t* out_off, uint64_t* row_base, void* scratch, const ZlStage* stage,
+                              int num_cus) {
   DecodeScratch s = carve(scratch, n);
   uint32_t m = n + 1;
   if (codec == SLATE_CODEC_LZ4 && n >= 64) {
@@ -1656,11 +1677,14 @@ hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, cons
     plan_sizes_kernel<<<(m + 255) / 256, 256, 0, st>>>(codec, in, in_off, n, out_off, row_base);
   }
   if (codec == SLATE_CODEC_ZLIB && n >= 64) {
-    // block-sized streams lane per block (zlib_fast.hip); the rest: the wave plan
-    (void)hipMemsetAsync(s.zf.count, 0, sizeof(uint32_t), st);
-    hipError_t e = launch_zlib_plan_fast(st, in, in_off, n, out_off, row_base, s.zf.list, s.zf.count, 0);
+    // block-sized streams lane per block (zlib_fast.hip; staged: parsed once, for the decode too);
+    // the rest: the wave plan
+    uint32_t* list = stage ? stage->list : s.zf.list;
+    uint32_t* count = stage ? stage->count : s.zf.count;
+    (void)hipMemsetAsync(count, 0, stage ? 3 * sizeof(uint32_t) : sizeof(uint32_t), st);
+    hipError_t e = launch_zlib_plan_fast(st, in, in_off, n, out_off, row_base, list, count, num_cus, stage);
     if (e != hipSuccess) return e;
-    plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, s.zf.list, s.zf.count);
+    plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, list, count);
   } else if (codec == SLATE_CODEC_ZLIB && n > 0) {
     plan_zlib_kernel<<<min((n + 3) / 4, 4096u), 256, 0, st>>>(in, in_off, n, out_off, row_base, nullptr, nullptr);
   }
@@ -2195,7 +2219,7 @@ hipError_t launch_decode_payload(hipStream_t st, const DecodeArgs& args_in, int 
   return hipGetLastError();
 }
 
-hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratch, int num_cus) {
+hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratch, int num_cus, const ZlStage* stage) {
   DecodeArgs a = args_in;
 #ifdef SLATE_PROFILING_BUILD
   const char* dbg = getenv("SLATE_DEBUG_MODE");  // profiling variants only (tools/variant.sh)
@@ -2223,9 +2247,18 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
   const size_t lds_large = kTabBytes + size_t(kLargeInCap) + kLargeOutCap;
   if (a.codec == SLATE_CODEC_ZLIB && !a.raw && !(dbg_bits(a) & 16)) {
     // the fast path (zlib_fast.hip phase Z + zstd_fast.hip phases A2 and B), then the exact path
-    // over the blocks it handed back
-    (void)hipMemsetAsync(s.zf.count, 0, 3 * sizeof(uint32_t), st);
-    hipError_t e = launch_zlib_fast(st, a, s.zf, num_cus);
+    // over the blocks it handed back.  After a staged plan, phase Z's output is the plan's: records,
+    // sequences, literals and hand-back list from the stage
+    if (stage) {
+      s.zf.rec = stage->rec;
+      s.zf.seq = stage->seq;
+      s.zf.list = stage->list;
+      s.zf.count = stage->count;
+      s.zf.lit = stage->lit;
+    } else {
+      (void)hipMemsetAsync(s.zf.count, 0, 3 * sizeof(uint32_t), st);
+    }
+    hipError_t e = launch_zlib_fast(st, a, s.zf, num_cus, stage != nullptr);
     if (e != hipSuccess) return e;
     decode_list_kernel<1><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);
     decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);

@@ -272,6 +272,17 @@ struct slate_ctx {
   hipStream_t aux = nullptr;
   slate::SideStream side;  // the context stream's second stream (DecodeArgs::side)
   DevBuf d_handbacks;      // DecodeArgs::handbacks of every decode through this context (u64)
+  // the staged CodecZlib plan (slate_block_decode_plan_device): phase Z's output, consumed by the
+  // next slate_block_decode_device over the same inputs on the same stream (zl_armed)
+  DevBuf zl_stage;
+  struct {
+    const uint8_t* in = nullptr;
+    const uint64_t* in_off = nullptr;
+    const uint64_t* out_off = nullptr;
+    uint32_t n = 0;
+    hipStream_t stream = nullptr;
+  } zl_plan;
+  bool zl_armed = false;
   DevBuf x_words, x_enc, x_slots, x_asm, x_crc, x_bkt;
   std::shared_ptr<SegPool> seg_pool = std::make_shared<SegPool>();
   // device time of the builder's GPU passes (slate_ctx_set_timing): nanoseconds, summed over the
@@ -323,7 +334,7 @@ struct slate_ctx {
     for (DevBuf* b : {&d_in, &d_in_off, &d_out, &d_out_off, &d_meta, &d_rows, &d_row_base, &d_scratch, &e_a,
                       &e_b, &e_c, &e_d, &e_e, &e_f, &e_g, &e_h, &e_i, &e_j, &e_k, &s_slots, &s_raw, &s_aux, &c_meta,
                       &c_tags, &c_bodies, &c_seqs, &c_out, &c_in, &x_words, &x_enc, &x_slots, &x_asm, &x_crc, &x_bkt,
-                      &d_handbacks})
+                      &d_handbacks, &zl_stage})
       b->release();
     if (aux) (void)hipStreamDestroy(aux);
     aux = nullptr;

@@ -112,7 +112,23 @@ struct ZsFastArgs {
   uint32_t* count;  // count[0]: list, count[1]: hlist, count[2]: flist entries
   uint32_t* hlist;  // kZfHuf blocks (phase B': Huffman literals)
   uint32_t* flist;  // blocks for the FSE parse (phase A')
+  // CodecZlib after a staged plan: the literal bytes of block b at lit + kZlStageStride b (phase
+  // B reads them there instead of the start of the output slot); nullptr otherwise
+  const uint8_t* lit = nullptr;
 };
+// The staged CodecZlib plan (zlib_fast.hip kZlStage): phase Z's records, sequences, literals and
+// the hand-back list of n blocks, written by the plan and consumed by the decode that follows it
+constexpr uint32_t kZlStageStride = kZsFastOutCap;  // literal bytes <= decoded bytes <= the fast path's cap
+static_assert(kZlStageStride % 16 == 0, "stage slots stay 16-byte aligned");
+struct ZlStage {
+  ZsFastRec* rec;
+  uint32_t* seq;    // n * kZfSeqSlot dwords
+  uint32_t* list;   // n: the blocks phase Z left to the exact path (and the plan's wave plan)
+  uint32_t* count;  // list entries (then two unused counters)
+  uint8_t* lit;     // n * kZlStageStride bytes
+};
+size_t zl_stage_bytes(uint32_t n);
+ZlStage zl_stage_carve(void* p, uint32_t n);
 
 struct DecodeScratch {
   uint64_t* pa;
@@ -126,9 +142,14 @@ struct DecodeScratch {
 
 size_t decode_scratch_bytes(uint32_t n);
 size_t decode_scratch_bytes_codec(uint32_t n, int codec);
+// stage (CodecZlib, n >= 64 only; nullptr elsewhere): the plan parses each stream once into it
 hipError_t launch_decode_plan(hipStream_t st, int codec, const uint8_t* in, const uint64_t* in_off, uint32_t n,
-                              uint64_t* out_off, uint64_t* row_base, void* scratch);
-hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus);
+                              uint64_t* out_off, uint64_t* row_base, void* scratch, const ZlStage* stage = nullptr,
+                              int num_cus = 0);
+// stage: a staged plan's (the same inputs, the same stream, nothing written to it since): the
+// CodecZlib decode builds from it without phase Z
+hipError_t launch_decode(hipStream_t st, const DecodeArgs& a, void* scratch, int num_cus,
+                         const ZlStage* stage = nullptr);
 hipError_t launch_decode_lpb2(hipStream_t st, const DecodeArgs& a, int num_cus);
 // CodecNone blocks (not raw payloads): one wave per block, streaming (decode_none.hip); blocks with
 // more than 5104 or fewer than 4 data bytes are appended to a.large_list for decode_large_kernel<0>.
@@ -149,9 +170,11 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
 // wave plan); decode: phase Z (lane per block: literals + sequences), then zstd_fast.hip's phases A2
 // and B (launch_zlib_fast), hand-backs to z.list for the exact path.
 hipError_t launch_zlib_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n,
-                                 uint64_t* out_sz, uint64_t* row_sz, uint32_t* list, uint32_t* count, int num_cus);
+                                 uint64_t* out_sz, uint64_t* row_sz, uint32_t* list, uint32_t* count, int num_cus,
+                                 const ZlStage* stage = nullptr);
 hipError_t launch_zlib_fast_parse(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
-hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus);
+// parsed: phase Z already ran (a staged plan; z points into the stage)
+hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus, bool parsed = false);
 // The rows of a decoded batch, densely in block order, written to `dense` (device memory or
 // page-locked host memory mapped for the device): block i's min(n_rows, capacity) rows when it
 // decoded (status OK), none otherwise; dense_off (n+1 u64) gets the exclusive scan of those

@@ -8,7 +8,11 @@
 //     Adler-32, checked by the build phase over the decoded block in LDS).
 // Then phase A2 (the SST block CRC32, zstd_fast.hip) and phase B (wave per block: literal runs
 // placed, matches in order, write-back, block.Decode's checks and rows) run unchanged.
-// Plan mode: the same decode with no writes gives each block's decoded size.
+// Plan mode: the same decode with no writes gives each block's decoded size.  Staged plan mode
+// (slate_block_decode_plan_device for CodecZlib): the plan IS phase Z -- sizes as in plan mode, and
+// the literals, sequences and record of each block kept in the context's stage (ZlStage, literals
+// at a fixed kZlStageStride per block), so the decode call that follows runs only A2 and B over
+// them (each stream inflated once per plan + decode, not twice).
 //
 // Per lane: a 64-bit bit buffer fed from 16-byte chunks of the block (two chunks loaded ahead);
 // canonical Huffman decoding (RFC 1951 3.2.2) as in zlib's puff: the code of length L is found by
@@ -206,12 +210,17 @@ __device__ __forceinline__ void zl_fixed_counts(ZlTab& tl, ZlTab& td) {
 
 }  // namespace
 
-// One lane per block.  kPlan: sizes only (out_sz / row_sz; failures to list for the wave plan);
-// otherwise the literal bytes to the output slot, the sequences and the record (failures to
-// z.list for the exact path).
-template <bool kPlan>
+// One lane per block.  kMode kZlDecode: the literal bytes to the output slot, the sequences and
+// the record (failures to z.list for the exact path); kZlPlan: sizes only (out_sz / row_sz;
+// failures to plist for the wave plan); kZlStage: both -- the sizes, and the literals to the
+// stage slot (z.lit + kZlStageStride b), sequences and record (failures to plist, which is also
+// the decode's exact-path list)
+constexpr int kZlDecode = 0, kZlPlan = 1, kZlStage = 2;
+template <int kMode>
 __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void zl_fast_kernel(DecodeArgs a, ZsFastArgs z, uint64_t* out_sz,
                                                              uint64_t* row_sz, uint32_t* plist, uint32_t* pcount) {
+  constexpr bool kPlan = kMode == kZlPlan;     // no literal / sequence writes
+  constexpr bool kSizes = kMode != kZlDecode;  // out_sz / row_sz / plist
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave_lane0 = threadIdx.x - lane;
@@ -225,10 +234,9 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const uint8_t* ibase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(ilo) & ~uintptr_t(15));
     const __amdgpu_buffer_rsrc_t R = make_rsrc(ibase, align16(uint64_t((a.in + a.in_off[rend]) - ibase)));
     __amdgpu_buffer_rsrc_t RO = R, RS = R;
-    if (!kPlan) {
-      RO = make_rsrc(a.out + a.out_off[r0], a.out_off[rend] - a.out_off[r0]);
-      RS = make_rsrc(z.seq + size_t(r0) * kZfSeqSlot, uint64_t(rend - r0) * kZfSeqSlot * 4);
-    }
+    if (kMode == kZlDecode) RO = make_rsrc(a.out + a.out_off[r0], a.out_off[rend] - a.out_off[r0]);
+    if (kMode == kZlStage) RO = make_rsrc(z.lit + size_t(r0) * kZlStageStride, uint64_t(rend - r0) * kZlStageStride);
+    if (!kPlan) RS = make_rsrc(z.seq + size_t(r0) * kZfSeqSlot, uint64_t(rend - r0) * kZfSeqSlot * 4);
     bool act = b < a.n, ok = act;
     uint32_t clen = 0, shift = 0, irel = 0, cap = 0, orel = 0;
     if (act) {
@@ -237,11 +245,15 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       irel = uint32_t(((a.in + s0) - shift) - ibase);
       ok = len >= 6 && len - 4 <= 0xFFFFFFu;
       clen = ok ? uint32_t(len - 4) : 0u;
-      if (!kPlan) {
+      if (kMode == kZlDecode) {
         const uint64_t c64 = a.out_off[b + 1] - a.out_off[b];
         cap = uint32_t(min(c64, uint64_t(kZlMaxOut)));
         ok = ok && c64 <= kZlMaxOut;
         orel = uint32_t(a.out_off[b] - a.out_off[r0]);
+      }
+      if (kMode == kZlStage) {
+        cap = kZlMaxOut;
+        orel = (b - r0) * kZlStageStride;
       }
     }
     // the bit reader at the stream's first byte
@@ -500,13 +512,14 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       want = __builtin_bswap32(w);
       ok = zi.used <= ubits;
     }
-    if (kPlan) {
+    if (kSizes) {
       if (act && ok) {
         out_sz[b] = align16(o);
         row_sz[b] = row_capacity(o);
       }
       zl_list_append(act && !ok, b, plist, pcount);
-    } else {
+    }
+    if (!kPlan) {
       // the last literals and the last sequences
       __builtin_amdgcn_raw_buffer_store_b128(lbuf, RO, (ok && (nl & 15)) ? orel + (nl & ~15u) : kOOB, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(qv, RS, (ok && (nseq & 3)) ? (b - r0) * kZfSeqSlot * 4 + 16 * (nseq >> 2) : kOOB,
@@ -522,33 +535,45 @@ __global__ __launch_bounds__(kZlThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         reinterpret_cast<v4u*>(z.rec + b)[0] = w0;
         reinterpret_cast<v4u*>(z.rec + b)[1] = w1;
       }
-      zl_list_append(act && !ok, b, z.list, z.count);
+      if (!kSizes) zl_list_append(act && !ok, b, z.list, z.count);
     }
   }
 }
 
 hipError_t launch_zlib_fast_parse(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zl_fast_kernel<false>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zl_fast_kernel<kZlDecode>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kZlLds));
   if (attr != hipSuccess) return attr;
   const uint32_t grid = min((a.n + kZlThreads - 1) / kZlThreads, uint32_t(num_cus) * kZlWgPerCu);
-  zl_fast_kernel<false><<<grid, kZlThreads, kZlLds, st>>>(a, z, nullptr, nullptr, nullptr, nullptr);
+  zl_fast_kernel<kZlDecode><<<grid, kZlThreads, kZlLds, st>>>(a, z, nullptr, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
 
 hipError_t launch_zlib_plan_fast(hipStream_t st, const uint8_t* in, const uint64_t* in_off, uint32_t n,
-                                 uint64_t* out_sz, uint64_t* row_sz, uint32_t* list, uint32_t* count, int num_cus) {
+                                 uint64_t* out_sz, uint64_t* row_sz, uint32_t* list, uint32_t* count, int num_cus,
+                                 const ZlStage* stage) {
   if (n == 0) return hipGetLastError();
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zl_fast_kernel<true>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zl_fast_kernel<kZlPlan>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(kZlLds));
+  static const hipError_t attr_s = hipFuncSetAttribute(reinterpret_cast<const void*>(&zl_fast_kernel<kZlStage>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(kZlLds));
   if (attr != hipSuccess) return attr;
+  if (attr_s != hipSuccess) return attr_s;
   DecodeArgs a{};
   a.in = in;
   a.in_off = in_off;
   a.n = n;
-  ZsFastArgs z{};
   const uint32_t grid = min((n + kZlThreads - 1) / kZlThreads, uint32_t(num_cus > 0 ? num_cus : 256) * kZlWgPerCu);
-  zl_fast_kernel<true><<<grid, kZlThreads, kZlLds, st>>>(a, z, out_sz, row_sz, list, count);
+  if (stage) {
+    ZsFastArgs z{};
+    z.rec = stage->rec;
+    z.seq = stage->seq;
+    z.lit = stage->lit;
+    zl_fast_kernel<kZlStage><<<grid, kZlThreads, kZlLds, st>>>(a, z, out_sz, row_sz, list, count);
+  } else {
+    ZsFastArgs z{};
+    zl_fast_kernel<kZlPlan><<<grid, kZlThreads, kZlLds, st>>>(a, z, out_sz, row_sz, list, count);
+  }
   return hipGetLastError();
 }
 

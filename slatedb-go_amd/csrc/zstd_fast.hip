@@ -1208,7 +1208,8 @@ __global__ __launch_bounds__(kZfBuildThreads, SLATE_ZF_BUILD_WG) void zs_fast_bu
     const uint32_t F = base16 + shift, lb = F + lit;
     {
       const uint32_t chunks = (dbg & (1u << 28)) ? 0u : (shift + slen + 15) / 16;
-      const uint4* src = reinterpret_cast<const uint4*>(cur.outlit ? cur.gout : cur.gin - shift);
+      const uint8_t* lsrc = z.lit ? z.lit + size_t(cur.b) * kZlStageStride : cur.gout;  // (a staged plan's)
+      const uint4* src = reinterpret_cast<const uint4*>(cur.outlit ? lsrc : cur.gin - shift);
       uint4* dst = reinterpret_cast<uint4*>(wout + base16);
       for (uint32_t c = lane; c < chunks; c += kWave) dst[c] = src[c];
     }
@@ -1549,10 +1550,12 @@ size_t zstd_fast_parse_lds() { return ((sizeof(ZfShared) + 15) & ~size_t(15)) + 
 // context), forked after phase A2 and joined before phase C.
 // CodecZlib: phase Z (zlib_fast.hip) in place of A / A', then A2 and B (no Huffman-literal or
 // XXH64 phase: B checks the Adler-32)
-hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus) {
+hipError_t launch_zlib_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArgs& z, int num_cus, bool parsed) {
   if (a.n == 0) return hipGetLastError();
-  hipError_t e = launch_zlib_fast_parse(st, a, z, num_cus);
-  if (e != hipSuccess) return e;
+  if (!parsed) {
+    hipError_t e = launch_zlib_fast_parse(st, a, z, num_cus);
+    if (e != hipSuccess) return e;
+  }
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);

@@ -32,10 +32,62 @@ def _z(data: bytes, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, wbits=15) -> byte
     return co.compress(data) + co.flush()
 
 
+class _Device:
+    """One device-resident batch (slate_block_decode_plan_device + _device, bench.py's entries): with
+    CodecZlib and >= 64 blocks the plan is phase Z itself, staged in the context for the decode."""
+
+    def __init__(self, ctx, blob, off):
+        import slatecodec as sc
+        self.ctx, self.n = ctx, len(off) - 1
+        self.d_in, self.d_off = sc.devbuf_from(ctx, blob), sc.devbuf_from(ctx, off)
+        self.d_oo, self.d_rb = sc.DevBuf(ctx, 8 * (self.n + 1)), sc.DevBuf(ctx, 8 * (self.n + 1))
+        self.d_sc = sc.DevBuf(ctx, sc.decode_scratch_bytes(self.n) + 64)
+        self.plan()
+        self.d_out, self.d_meta = sc.DevBuf(ctx, self.d_oo.u64(self.n) + 16), sc.DevBuf(ctx, 16 * max(self.n, 1))
+        self.d_rows = sc.DevBuf(ctx, 16 * self.d_rb.u64(self.n) + 16)
+
+    def plan(self):
+        self.ctx.decode_plan_device(ob.ZLIB, self.d_in.ptr, self.d_off.ptr, self.n, self.d_oo.ptr, self.d_rb.ptr,
+                                    self.d_sc.ptr)
+
+    def decode(self):
+        import slatecodec as sc
+        self.d_out.memset(0xEE)
+        self.d_meta.memset(0xEE)
+        self.ctx.decode_device(ob.ZLIB, self.d_in.ptr, self.d_off.ptr, self.n, self.d_out.ptr, self.d_oo.ptr,
+                               self.d_meta.ptr, self.d_rows.ptr, self.d_rb.ptr)
+        return (self.d_out.download(), self.d_oo.download(dtype=np.uint64),
+                self.d_meta.download().view(sc.META_DTYPE)[:self.n], self.d_rows.download().view(sc.ROW_DTYPE),
+                self.d_rb.download(dtype=np.uint64))
+
+
+def _check_same(blocks, got, want):
+    g_out, g_off, g_meta, g_rows, g_rb = got
+    o_out, o_off, o_meta, o_rows, o_rb = want
+    assert np.array_equal(g_off, o_off), "plan: out_off"
+    assert np.array_equal(g_rb, o_rb), "plan: row_base"
+    for i, blk in enumerate(blocks):
+        gm, om = g_meta[i], o_meta[i]
+        assert gm.tobytes() == om.tobytes(), (i, gm, om)
+        st = int(om["status"])
+        if st == 0 or 3 <= st <= 7:
+            dec = ob.zlib_decode(blk[:-4])[1]
+            a = int(o_off[i])
+            assert g_out[a:a + len(dec)].tobytes() == dec == o_out[a:a + len(dec)].tobytes(), i
+        if st == 0:
+            r0 = int(o_rb[i])
+            nr = min(int(om["n_rows"]), int(o_rb[i + 1]) - r0)
+            assert g_rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+
+
 def _compare(ctx, blocks, misalign=0):
+    """The host batch (slate_block_decode_batch) and the device-resident plan + decode, each against
+    the oracle."""
     blob, off = bg.pack(blocks, misalign)
+    want = ob.block_decode_batch(ob.ZLIB, blob, off)
+    _check_same(blocks, _Device(ctx, blob, off).decode(), want)
     g_out, g_off, g_meta, g_rows, g_rb = ctx.decode_batch(ob.ZLIB, blob, off)
-    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(ob.ZLIB, blob, off)
+    o_out, o_off, o_meta, o_rows, o_rb = want
     assert np.array_equal(g_off, o_off), "plan: out_off"
     assert np.array_equal(g_rb, o_rb), "plan: row_base"
     for i, blk in enumerate(blocks):
@@ -153,3 +205,29 @@ def test_zlib_fast_path_shapes(ctx):
         blocks.append(_crc(f))
     meta = _compare(ctx, blocks, misalign=rng.randrange(16))
     assert set(int(x) for x in meta["status"]) <= {0, 52}, set(int(x) for x in meta["status"])
+
+
+def test_staged_plan_pairing(ctx):
+    """The staged CodecZlib plan is used by the one decode that follows it over the same inputs and
+    plan outputs; a second decode, a decode of other inputs in between, or a later plan of other
+    inputs each decode on their own (phase Z again) -- every result identical to the oracle."""
+    from tools import workload as wl
+    batches = []
+    for seed in (3, 4):
+        dec, doff = wl.decoded_blocks(200, seed=seed, half=True)
+        blob, off = wl.encode_blocks(ob.ZLIB, dec, doff, threads=4)
+        blob, off = np.ascontiguousarray(blob), np.ascontiguousarray(off, np.uint64)
+        blocks = [blob[int(off[i]):int(off[i + 1])].tobytes() for i in range(len(off) - 1)]
+        batches.append((blocks, _Device(ctx, blob, off), ob.block_decode_batch(ob.ZLIB, blob, off)))
+    (ba, da, wa), (bb, db, wb) = batches
+    ctx.handbacks(reset=True)
+    da.plan()
+    _check_same(ba, da.decode(), wa)   # staged
+    _check_same(ba, da.decode(), wa)   # the stage was consumed: phase Z again
+    da.plan()
+    db.plan()                          # a later plan of other inputs replaces the stage
+    _check_same(ba, da.decode(), wa)
+    _check_same(bb, db.decode(), wb)   # (not armed: a's decode disarmed it)
+    db.plan()
+    _check_same(bb, db.decode(), wb)
+    assert ctx.handbacks() == 0
