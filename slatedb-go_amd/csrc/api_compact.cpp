@@ -101,6 +101,8 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<Piece>& pieces, co
   // uploaded bytes themselves -- no plan, no decoded copy; the row slots from the payload lengths
   const bool alias = codec == SLATE_CODEC_NONE;
   uint64_t tot[2] = {0, 0};
+  ZlStage zl_g{};
+  const ZlStage* zg = (codec == SLATE_CODEC_ZLIB && n >= 64 && !getenv("SLATE_ZL_NO_STAGE")) ? &zl_g : nullptr;
   if (alias) {
     std::vector<uint64_t> rb(size_t(n) + 1, 0);
     for (uint32_t i = 0; i < n; i++) {
@@ -110,10 +112,16 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<Piece>& pieces, co
     tot[1] = rb[n];
     SLATE_HIP(hipMemcpyAsync(d_row_base->b.p, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, st));
   } else {
+    if (zg) {  // CodecZlib: the plan is phase Z, staged in the context for this decode
+      SLATE_HIP(ctx->zl_stage.ensure(zl_stage_bytes(n)));
+      ctx->zl_armed = false;  // (the device API's pending plan, if any, is overwritten)
+      zl_g = zl_stage_carve(ctx->zl_stage.p, n);
+    }
     {
       GpuSpan gs(ctx, st);  // device time (slate_ctx_set_timing): every kernel group of the compaction
       SLATE_HIP(launch_decode_plan(st, codec, d_in->as<uint8_t>(), d_in_off->as<uint64_t>(), n,
-                                   d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), d_scr->b.p));
+                                   d_out_off->as<uint64_t>(), d_row_base->as<uint64_t>(), d_scr->b.p, zg,
+                                   ctx->num_cus));
     }
     if ((s = d2h_small(ctx, &tot[0], d_out_off->as<uint64_t>() + n, 8))) return s;
     if ((s = d2h_small(ctx, &tot[1], d_row_base->as<uint64_t>() + n, 8))) return s;
@@ -132,7 +140,7 @@ int decode_group(slate_ctx* ctx, int codec, const std::vector<Piece>& pieces, co
   a.handbacks = ctx_handbacks(ctx);
   {
     GpuSpan gs(ctx, st);
-    SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus));
+    SLATE_HIP(launch_decode(st, a, d_scr->b.p, ctx->num_cus, zg));
   }
   // every block's status: the first failing block of an SST ends that SST's iterator with a
   // warning (iterator.go:62-68 wrapping decode.go:143-144); it and the SST's later blocks keep no

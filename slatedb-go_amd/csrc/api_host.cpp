@@ -380,8 +380,16 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
     hipStream_t s = L.stream;
     if (bytes) SLATE_HIP(hipMemcpyAsync(L.d_in.p, L.h_in.p, bytes, hipMemcpyHostToDevice, s));
     SLATE_HIP(hipMemcpyAsync(L.d_in_off.p, ho, (size_t(m) + 1) * 8, hipMemcpyHostToDevice, s));
+    // CodecZlib: the plan is phase Z, staged for this chunk's decode (as slate_block_decode_plan_device)
+    const bool zl_staged = codec == SLATE_CODEC_ZLIB && m >= 64 && !getenv("SLATE_ZL_NO_STAGE");
+    ZlStage zg{};
+    if (zl_staged) {
+      SLATE_HIP(L.d_zlstage.ensure(zl_stage_bytes(m)));
+      zg = zl_stage_carve(L.d_zlstage.p, m);
+    }
     SLATE_HIP(launch_decode_plan(s, codec, L.d_in.as<uint8_t>(), L.d_in_off.as<uint64_t>(), m,
-                                 L.d_out_off.as<uint64_t>(), L.d_row_base.as<uint64_t>(), L.d_scratch.p));
+                                 L.d_out_off.as<uint64_t>(), L.d_row_base.as<uint64_t>(), L.d_scratch.p,
+                                 zl_staged ? &zg : nullptr, ctx->num_cus));
     uint64_t* po = L.h_plan.as<uint64_t>();
     uint64_t* pr = po + m + 1;
     if (host_plannable(codec)) {
@@ -435,7 +443,7 @@ int host_decode_body(slate_ctx* ctx, int codec, const uint8_t* in, const uint64_
                    L.d_row_base.as<uint64_t>(), nullptr, nullptr, 0};
       a.side = &L.side;
       a.handbacks = ctx_handbacks(ctx);
-      SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus));
+      SLATE_HIP(launch_decode(s, a, L.d_scratch.p, ctx->num_cus, zl_staged ? &zg : nullptr));
       L.direct = o.out_dev != nullptr;
       if (L.direct) {
         // page-locked caller buffers: the GPU writes the chunk's bytes and rows in place

@@ -1591,7 +1591,9 @@ size_t decode_scratch_bytes(uint32_t n) {
   return align16(2 * tiles * sizeof(uint64_t)) + 16 + align16(size_t(n) * sizeof(uint32_t)) + 16 +
          // CodecZstd fast path: count, list, records, sequences
          16 + 3 * align16(size_t(n) * sizeof(uint32_t)) + size_t(n) * sizeof(ZsFastRec) +
-         size_t(n) * kZfSeqSlot * sizeof(uint32_t);
+         size_t(n) * kZfSeqSlot * sizeof(uint32_t) +
+         // its Huffman-literal slots (H1 -> H2): tables and stream records
+         size_t(zf_huf_cap(n)) * (kZhTab + 64);
 }
 
 // The scratch one codec's plan + decode touch (carve's layout, cut after the last region the
@@ -1631,6 +1633,11 @@ static DecodeScratch carve(void* scratch, uint32_t n) {
   p += size_t(n) * sizeof(ZsFastRec);
   s.zf.seq = reinterpret_cast<uint32_t*>(p);
   p += size_t(n) * kZfSeqSlot * sizeof(uint32_t);
+  s.zf.hcap = zf_huf_cap(n);
+  s.zf.htab = p;
+  p += size_t(s.zf.hcap) * kZhTab;
+  s.zf.hdesc = reinterpret_cast<uint32_t*>(p);
+  p += size_t(s.zf.hcap) * 64;
   s.tiles = uint32_t(tiles);
   return s;
 }

@@ -131,6 +131,7 @@ struct PipeLane {
   hipStream_t stream = nullptr;
   hipEvent_t planned = nullptr, done = nullptr;
   DevBuf d_in, d_in_off, d_out_off, d_row_base, d_scratch, d_out, d_meta, d_rows, d_dense, d_gmap;
+  DevBuf d_zlstage;  // CodecZlib chunks: the staged plan (phase Z once, for the chunk's decode)
   PinBuf h_in, h_in_off, h_plan, h_out, h_meta, h_rows, h_gmap;  // h_rows: the chunk's rows, dense (rows_pack)
   bool direct = false;  // the chunk's bytes and rows went straight to the caller's page-locked buffers
   // the chunk in flight: blocks [b0, b0+n), its place in the caller's outputs
@@ -141,7 +142,7 @@ struct PipeLane {
   void release() {
     side.release();
     for (DevBuf* b : {&d_in, &d_in_off, &d_out_off, &d_row_base, &d_scratch, &d_out, &d_meta, &d_rows, &d_dense,
-                      &d_gmap})
+                      &d_gmap, &d_zlstage})
       b->release();
     for (PinBuf* b : {&h_in, &h_in_off, &h_plan, &h_out, &h_meta, &h_rows, &h_gmap}) b->release();
     if (planned) (void)hipEventDestroy(planned);

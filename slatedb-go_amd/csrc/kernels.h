@@ -115,7 +115,16 @@ struct ZsFastArgs {
   // CodecZlib after a staged plan: the literal bytes of block b at lit + kZlStageStride b (phase
   // B reads them there instead of the start of the output slot); nullptr otherwise
   const uint8_t* lit = nullptr;
+  // CodecZstd Huffman-literal blocks (phases H1 / H2): hlist entries k < hcap get their decoding
+  // table at htab + kZhTab k and four stream records at hdesc + 16 k (dwords); the rest phase B'
+  uint8_t* htab = nullptr;
+  uint32_t* hdesc = nullptr;
+  uint32_t hcap = 0;
 };
+constexpr uint32_t kZhTab = 4096;  // a Huffman decoding table: 2^11 16-bit entries
+// hlist entries with an H1 / H2 slot: every one for small batches, ~6 % of the blocks beyond
+// (configs[4]: 1.1 % of blocks have Huffman literals); the rest take phase B'
+__host__ __device__ inline uint32_t zf_huf_cap(uint32_t n) { return n <= 1024 ? n : min(n, n / 16 + 64); }
 // The staged CodecZlib plan (zlib_fast.hip kZlStage): phase Z's records, sequences, literals and
 // the hand-back list of n blocks, written by the plan and consumed by the decode that follows it
 constexpr uint32_t kZlStageStride = kZsFastOutCap;  // literal bytes <= decoded bytes <= the fast path's cap

@@ -1229,13 +1229,14 @@ __global__ __launch_bounds__(kZfBuildThreads, SLATE_ZF_BUILD_WG) void zs_fast_bu
 // Any failed check hands the block to the exact path.
 __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // (the list's first z.hcap entries are phases H1 / H2's)
   const uint32_t items = z.count[1];
-  if (blockIdx.x * (kZfHufThreads / 64) >= items) return;  // (workgroup-uniform)
+  if (z.hcap + blockIdx.x * (kZfHufThreads / 64) >= items) return;  // (workgroup-uniform)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* win = smem + wave * kZfHufWave;
   uint8_t* wout = win + kZfIn + 16;
   ZsScratch* sc = reinterpret_cast<ZsScratch*>(wout + kZfOutLds);
-  for (uint32_t k = blockIdx.x * (kZfHufThreads / 64) + wave; k < items; k += gridDim.x * (kZfHufThreads / 64)) {
+  for (uint32_t k = z.hcap + blockIdx.x * (kZfHufThreads / 64) + wave; k < items; k += gridDim.x * (kZfHufThreads / 64)) {
     const uint32_t b = z.hlist[k];
     const ZfBlock cur = zf_decode(a, zf_load(a, z, b, lane), lane);
     if (!cur.fast) continue;  // the CRC32 failed (phase A2)
@@ -1317,6 +1318,198 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
     }
     zs_sync();
     (void)zf_build(a, cur, wout, lbase, lane, 0);  // (Zstd frames only: no Adler-32)
+  }
+}
+
+// ------------------------------------------------------------------------------ phases H1, H2
+// Huffman-literal blocks (zs_block literal type 2 with a new tree; configs[4]: ~1.1 % of blocks)
+// in two passes instead of phase B's wave per block with four busy lanes:
+//   H1 zs_huf_tree_kernel    one WAVE per block, many per CU: the tree description (zs_huf_read)
+//                            into the block's decoding table in HBM (2^tl 16-bit entries) and its
+//                            one or four streams' records (start, length, symbols, output place)
+//   H2 zs_huf_stream_kernel  one LANE per stream, 16 blocks per wave: the 16 tables in LDS, each
+//                            lane's backward bitstream through a 64-bit register window fed from a
+//                            per-lane LDS ring of 16-byte chunks (one chunk prefetched), a table
+//                            read per symbol, the literal bytes to the start of the block's output
+//                            slot; the block then leaves as a kZfOutLit block (phase B builds it
+//                            from there, as it builds CodecZlib blocks) or, on any failed check
+//                            (the stream does not end exactly at its first bit), to the exact path.
+// Both run on the main stream after A2 (the rec flags they rewrite are A2's too). Entries of the
+// Huffman list beyond the slots (zf_huf_cap) take phase B'.
+constexpr uint32_t kZhTreeThreads = 256;
+constexpr uint32_t kZhWin = 192;  // the tree description's window: <= 15 + 1 + 127 bytes + 8 slack
+constexpr uint32_t kZhTreeWave = kZhWin + kZsHufScratch;
+constexpr uint32_t kZhTreeLds = (kZhTreeThreads / 64) * kZhTreeWave;
+constexpr uint32_t kZhBlocks = 16;  // blocks per H2 wave (four stream lanes each)
+constexpr uint32_t kZhRing = 64;    // per-lane LDS ring: four 16-byte chunks
+constexpr uint32_t kZhStreamLds = kZhBlocks * kZhTab + 64 * kZhRing;
+static_assert(2 * kZhStreamLds <= 160 * 1024, "phase H2 workgroups per CU exceed the LDS");
+
+__global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t items = min(z.count[1], z.hcap);
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* win = smem + wave * kZhTreeWave;
+  ZsScratch* sc = reinterpret_cast<ZsScratch*>(win + kZhWin);
+  const uint32_t waves = gridDim.x * (kZhTreeThreads / 64);
+  for (uint32_t k = blockIdx.x * (kZhTreeThreads / 64) + wave; k < items; k += waves) {
+    const uint32_t b = z.hlist[k];
+    const ZsFastRec rec = z.rec[b];
+    const uint32_t fl = zrfl(rec.info >> 16);
+    uint4* dk = reinterpret_cast<uint4*>(z.hdesc + 16 * size_t(k));
+    if (!(fl & kZfFast)) {  // the CRC32 failed (phase A2): H2 skips it
+      continue;
+    }
+    const uint64_t i0 = a.in_off[b];
+    const uint32_t len = uint32_t(a.in_off[b + 1] - i0);
+    const uint32_t shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + i0) & 15);
+    const uint8_t* F = a.in + i0 - shift;
+    const __amdgpu_buffer_rsrc_t R = make_rsrc(F, align16(uint64_t(shift) + len));
+    const uint32_t lit = zrfl(rec.lit), cs = zrfl(rec.cs), nlit = zrfl(rec.nlit);
+    const uint32_t nstr = (fl & kZfHuf4) ? 4u : 1u;
+    // the tree description's window: chunks from the one holding its first byte
+    const uint32_t c0 = (shift + lit) >> 4, off = (shift + lit) & 15;
+    if (lane < kZhWin / 16) lds_put16(win + 16 * lane, bload(R, 16 * (c0 + lane)));
+    __builtin_amdgcn_s_waitcnt(0);
+    zs_sync();
+    uint32_t tl = 0;
+    const int t = zs_huf_read(win, int32_t(off), cs, sc, int(lane), &tl);
+    bool fail = t < 0;
+    uint32_t sb = 0, sl = 0, m = 0, lo = 0;  // lane l < nstr: stream l
+    if (!fail) {
+      const uint32_t q = off + uint32_t(t), qn = cs - uint32_t(t), fq = lit + uint32_t(t);
+      if (nstr == 1) {
+        sb = fq;
+        sl = qn;
+        m = nlit;
+      } else if (qn < 10) {
+        fail = true;
+      } else {
+        auto bN = [&](uint32_t i) -> uint32_t { return zrfl(uint32_t(win[q + i])); };
+        const uint32_t l1 = bN(0) | (bN(1) << 8), l2 = bN(2) | (bN(3) << 8), l3 = bN(4) | (bN(5) << 8);
+        const uint32_t seg = (nlit + 3) / 4;
+        fail = l1 + l2 + l3 + 6 > qn || 3 * seg > nlit;
+        const uint32_t l4 = qn - 6 - l1 - l2 - l3, s0 = fq + 6;
+        sb = lane == 0 ? s0 : lane == 1 ? s0 + l1 : lane == 2 ? s0 + l1 + l2 : s0 + l1 + l2 + l3;
+        sl = lane == 0 ? l1 : lane == 1 ? l2 : lane == 2 ? l3 : l4;
+        m = lane < 3 ? seg : nlit - 3 * seg;
+        lo = seg * (lane < 3 ? lane : 3u);
+      }
+    }
+    if (fail) {  // to the exact path, as phase B' hands a block back
+      if (lane == 0) {
+        z.rec[b].info = 0;
+        z.list[atomicAdd(z.count, 1u)] = b;
+      }
+      continue;
+    }
+    // the table (2^tl entries) to the slot; the stream records (absolute frame-relative starts)
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(sc->huf);
+      uint4* dst = reinterpret_cast<uint4*>(z.htab + size_t(k) * kZhTab);
+      for (uint32_t c = lane; c < ((2u << tl) + 15) / 16; c += kWave) dst[c] = src[c];
+    }
+    if (lane < 4) dk[lane] = lane < nstr ? make_uint4(shift + sb, sl, m, lo | (tl << 16)) : make_uint4(0, 0, 0, 0);
+    zs_sync();
+  }
+}
+
+namespace {
+__device__ __forceinline__ uint4 zh_chunk(const uint8_t* F, int32_t c) {
+  return c >= 0 ? *reinterpret_cast<const uint4*>(F + 16 * c) : make_uint4(0, 0, 0, 0);
+}
+}  // namespace
+
+__global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t items = min(z.count[1], z.hcap);
+  const uint32_t lane = threadIdx.x & 63, j = lane >> 2, l = lane & 3;
+  uint8_t* ring = smem + kZhBlocks * kZhTab + lane * kZhRing;
+  uint32_t* rd = reinterpret_cast<uint32_t*>(ring);
+  for (uint32_t k0 = blockIdx.x * kZhBlocks; k0 < items; k0 += gridDim.x * kZhBlocks) {
+    // the 16 blocks' tables (whole slots; entries past 2^tl are never read)
+    {
+      const uint32_t nb = min(kZhBlocks, items - k0);
+      const uint4* src = reinterpret_cast<const uint4*>(z.htab + size_t(k0) * kZhTab);
+      uint4* dst = reinterpret_cast<uint4*>(smem);
+      for (uint32_t c = lane; c < nb * (kZhTab / 16); c += kWave) dst[c] = src[c];
+    }
+    const uint32_t k = k0 + j;
+    uint32_t b = 0, fl = 0;
+    uint4 d = make_uint4(0, 0, 0, 0);
+    if (k < items) {
+      b = z.hlist[k];
+      fl = z.rec[b].info >> 16;
+      d = reinterpret_cast<const uint4*>(z.hdesc + 16 * size_t(k))[l];
+    }
+    const uint32_t tl = d.w >> 16, lo = d.w & 0xFFFFu, m = d.z, sl = d.y, fs = d.x;
+    // the lane's stream: frame bytes [fs, fs + sl) from the 16-aligned frame base F
+    bool act = k < items && (fl & kZfFast) && tl != 0;
+    const uint8_t* F = nullptr;
+    uint8_t* out = nullptr;
+    if (act) {
+      const uint64_t i0 = a.in_off[b];
+      F = a.in + i0 - (reinterpret_cast<uintptr_t>(a.in + i0) & 15);
+      out = a.out + a.out_off[b] + lo;
+    }
+    bool bad = act && sl == 0;
+    act = act && !bad;
+    // the top chunk (the stream's last byte: zs_bstart) and the one below into the ring
+    const int32_t T = act ? int32_t((fs + sl - 1) >> 4) : 0;
+    const uint4 cT = act ? zh_chunk(F, T) : make_uint4(0, 0, 0, 0);
+    const uint4 cT1 = act ? zh_chunk(F, T - 1) : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(ring + 16 * (T & 3)) = cT;
+    *reinterpret_cast<uint4*>(ring + 16 * ((T - 1) & 3)) = cT1;
+    int32_t lowc = T - 1;
+    uint4 pf = act ? zh_chunk(F, T - 2) : make_uint4(0, 0, 0, 0);
+    const uint32_t lb = (fs + sl - 1) & 15;
+    const uint32_t lw = lb < 4 ? cT.x : lb < 8 ? cT.y : lb < 12 ? cT.z : cT.w;
+    const uint32_t lastb = (lw >> (8 * (lb & 3))) & 0xFFu;
+    bad = bad || (act && lastb == 0);
+    act = act && lastb != 0;
+    int32_t bp = act ? int32_t(8 * (sl - 1) + (31 - __builtin_clz(lastb | 1u))) : 0;  // bits left
+    int32_t P = int32_t(8 * fs) + bp;  // frame-relative bit just above the next code
+    int32_t clo = 0;
+    uint64_t cv = 0;
+    const uint32_t tmask = (1u << tl) - 1u;
+    const uint16_t* tab = reinterpret_cast<const uint16_t*>(smem + j * kZhTab);
+    zs_sync();
+    // the window's first fill (below)
+    clo = INT32_MAX;
+    for (uint32_t i = 0; __ballot(act && i < m); i++) {
+      const bool go = act && i < m;
+      if (go && P - int32_t(tl) < clo) {
+        // 64 bits from the dword boundary at or above P, down: two ring dwords
+        clo = ((P + 31) & ~31) - 64;
+        const int32_t D = clo >> 5;
+        if ((D >> 2) < lowc) {  // one chunk lower: commit the prefetched one, fetch the next
+          lowc -= 1;
+          *reinterpret_cast<uint4*>(ring + 16 * (lowc & 3)) = pf;
+          pf = zh_chunk(F, lowc - 1);
+        }
+        cv = uint64_t(rd[D & 15]) | (uint64_t(rd[(D + 1) & 15]) << 32);
+      }
+      uint32_t v = uint32_t(cv >> uint32_t(P - int32_t(tl) - clo)) & tmask;
+      if (bp < int32_t(tl)) v = bp > 0 ? v & ~((1u << (int32_t(tl) - bp)) - 1u) : 0u;  // zeros below the stream
+      const uint32_t e = tab[v];
+      if (go) {
+        out[i] = uint8_t(e);
+        bp -= int32_t(e >> 8);
+        P -= int32_t(e >> 8);
+      }
+    }
+    bad = bad || (act && bp != 0);
+    // per block: any failing stream hands it back; else phase B builds it from the output slot
+    const uint32_t bm = uint32_t(__ballot(bad) >> (4 * j)) & 15u;
+    if (l == 0 && k < items && (fl & kZfFast) && tl != 0) {
+      if (bm) {
+        z.rec[b].info = 0;
+        z.list[atomicAdd(z.count, 1u)] = b;
+      } else {
+        z.rec[b].info = (z.rec[b].info & ~((kZfHuf | kZfHuf4) << 16)) | (kZfOutLit << 16);
+      }
+    }
+    zs_sync();
   }
 }
 
@@ -1578,6 +1771,22 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
   const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
   zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
+  // phases H1 / H2: the Huffman-literal blocks' trees, then their streams lane per stream (the
+  // workgroups of an empty list exit at once); SLATE_ZF_NO_H (A/B runs): phase B' takes them all
+  const bool no_h = getenv("SLATE_ZF_NO_H") != nullptr;  // (read per call: same-process A/B)
+  ZsFastArgs zh = z;
+  if (no_h) {
+    zh.hcap = 0;
+  } else {
+    static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_stream_kernel),
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhStreamLds));
+    if (attr_t != hipSuccess) return attr_t;
+    const uint32_t hmax = min(a.n, z.hcap);
+    if (hmax) {
+      zs_huf_tree_kernel<<<min((hmax + 3) / 4, uint32_t(num_cus) * 6u), kZhTreeThreads, kZhTreeLds, st>>>(a, z);
+      zs_huf_stream_kernel<<<min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u), 64, kZhStreamLds, st>>>(a, z);
+    }
+  }
   const size_t lds_b = kZfBuildLds;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
@@ -1597,7 +1806,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
     const uint32_t v = e ? uint32_t(atoi(e)) : 2u;
     return v >= 1 && v <= 163840 / kZfHufLds ? v : 2u;
   }();
-  zs_fast_huf_kernel<<<uint32_t(num_cus) * huf_wg, kZfHufThreads, lds_h, sh>>>(a, z);
+  zs_fast_huf_kernel<<<uint32_t(num_cus) * huf_wg, kZfHufThreads, lds_h, sh>>>(a, zh);
   zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
   if (sh != st) {
     hipError_t e = hipEventRecord(f->join, sh);

@@ -145,6 +145,13 @@ def random_sources(rng: random.Random, n_sources: int, n_keys: int, space: int, 
                    tomb: float = 0.05, run_ssts: int = 1, key_fmt="k%015d"):
     """n_sources sorted runs (each of run_ssts SSTs over consecutive key ranges) drawn from a
     shared key space, values of random length (0..120), some tombstones."""
+    return [[build_sst(part, codec) for part in run]
+            for run in random_kv_runs(rng, n_sources, n_keys, space, tomb, run_ssts, key_fmt)]
+
+
+def random_kv_runs(rng: random.Random, n_sources: int, n_keys: int, space: int, tomb: float = 0.05,
+                   run_ssts: int = 1, key_fmt="k%015d"):
+    """random_sources' KVs before encoding: per source, its SSTs' sorted (key, value|None) lists."""
     srcs = []
     for _ in range(n_sources):
         ids = sorted(rng.sample(range(space), n_keys))
@@ -157,5 +164,5 @@ def random_sources(rng: random.Random, n_sources: int, n_keys: int, space: int, 
                 kvs.append((k, rng.randbytes(rng.randint(1, 120))))
         kvs.sort(key=lambda kv: kv[0])
         step = max(1, (len(kvs) + run_ssts - 1) // run_ssts)
-        srcs.append([build_sst(kvs[j:j + step], codec) for j in range(0, len(kvs), step)])
+        srcs.append([kvs[j:j + step] for j in range(0, len(kvs), step)])
     return srcs

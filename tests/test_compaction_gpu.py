@@ -175,3 +175,25 @@ def test_compaction_corrupt_inputs_warn(ctx, case):
     with pytest.raises(SlateError) as e:
         sc.compact(ctx, srcs, 30_000)
     assert e.value.status == want_w[0][4]
+
+
+@pytest.mark.parametrize("n_keys", [300, 4000])
+def test_compaction_zlib_sources(ctx, compact_fn, n_keys):
+    """Input SSTs in CodecZlib (built by this library's sstable.Builder; the oracle's reader decodes
+    them): the compaction's decode takes the staged Zlib plan (phase Z once) when an input batch has
+    >= 64 blocks; outputs bit-exact against the oracle's executeCompaction, in both output codecs."""
+    import slatecodec as sc
+    rng = random.Random(60 + n_keys)
+
+    def gpu_sst(kvs):
+        b = sc.SstBuilder(ctx, 4096, 0, 10, ob.ZLIB)
+        for k, v in kvs:
+            assert b.add(k, v) == 0
+        return b.build().encode()
+
+    srcs = []
+    for kvs in cg.random_kv_runs(rng, 3, n_keys, 3 * n_keys, run_ssts=2):
+        srcs.append([gpu_sst(part) for part in kvs])
+    for out_codec in (ob.NONE, ob.SNAPPY):
+        got = compact_fn(ctx, srcs, 1 << 30, codec=out_codec)
+        assert got == cg.oracle_compact(srcs, 1 << 30, codec=out_codec)

@@ -273,3 +273,60 @@ def test_fse_window_limits(ctx, misalign):
     meta = _compare(ctx, blocks, misalign=misalign)
     assert all(x == 0 or 3 <= x <= 7 for x in meta["status"].tolist()), meta["status"]  # (decoded: bytes compared)
     assert ctx.handbacks() >= past_hdr + past_bits
+
+
+def _huf_blocks(rng, n_kv, vlen, block_size, alpha=256, zipf=0.8):
+    """SST blocks whose level-3 frames have Huffman-coded literals (a new tree; 4 streams, and 1
+    stream for small sections) and few sequences with predefined tables: the fast path's phases
+    H1 / H2 (zstd_fast.hip)."""
+    w = [1.0 / ((i + 1) ** zipf) for i in range(alpha)]
+    keys = sorted({bytes(rng.randrange(256) for _ in range(rng.randint(4, 20))) for _ in range(n_kv)})
+    kvs = [(k, bytes(rng.choices(range(alpha), w, k=rng.randint(*vlen)))) for k in keys]
+    return [b[:-4] for b in bg.sst_blocks(kvs, block_size, ob.NONE)]
+
+
+def _lit_type(frame: bytes) -> int:
+    """The first block's literals section type (2: Huffman with a new tree) and stream count."""
+    fhd = frame[4]
+    fcsf, ss, dif = fhd >> 6, (fhd >> 5) & 1, fhd & 3
+    p = 5 + (0 if ss else 1) + (0, 1, 2, 4)[dif] + ((0, 2, 4, 8)[fcsf] if fcsf else ss)
+    b0 = frame[p + 3]
+    return (b0 & 3, 1 if ((b0 >> 2) & 3) == 0 else 4)
+
+
+@pytest.mark.parametrize("misalign", [0, 5, 11])
+def test_huffman_literal_blocks(ctx, misalign):
+    """Huffman-literal frames (4- and 1-stream) through phases H1 / H2, none handed back, and the
+    same frames with a flipped byte in the literal streams under a recomputed block CRC (the stream
+    no longer ends at its first bit, or the frame checksum fails: the exact path reports it); every
+    status, byte and row identical to the oracle."""
+    rng = random.Random(70 + misalign)
+    decs = _huf_blocks(rng, 500, (800, 1100), 4096) + _huf_blocks(rng, 300, (30, 60), 512, 200, 1.1)
+    frames = [_z(d, 3) for d in decs]
+    kinds = [_lit_type(f) for f in frames]
+    assert sum(1 for t in kinds if t == (2, 4)) >= 100 and sum(1 for t in kinds if t == (2, 1)) >= 5, kinds
+    ctx.handbacks(reset=True)
+    meta = _compare(ctx, [_crc(f) for f in frames], misalign=misalign)
+    assert (meta["status"] == 0).all()
+    assert ctx.handbacks() == 0
+    damaged = []
+    for f in frames:
+        g = bytearray(f)
+        g[rng.randrange(len(g) // 3, len(g) - 16)] ^= 1 << rng.randrange(8)
+        damaged.append(_crc(bytes(g)))
+    meta = _compare(ctx, damaged + [_crc(f) for f in frames[:50]], misalign=misalign)
+    assert (meta["status"][-50:] == 0).all() and (meta["status"][:-50] != 0).any()
+
+
+def test_huffman_literal_blocks_beyond_slots(ctx):
+    """More Huffman-literal blocks in one batch than H1 / H2 have slots for (zf_huf_cap: n / 16 + 64
+    past 1024 blocks): the rest take phase B'; every block identical to the oracle."""
+    rng = random.Random(77)
+    decs = []
+    while len(decs) < 1500:
+        decs += _huf_blocks(rng, 600, (800, 1100), 4096)
+    blocks = [_crc(_z(d, 3)) for d in decs[:1500]]
+    ctx.handbacks(reset=True)
+    meta = _compare(ctx, blocks, misalign=9)
+    assert (meta["status"] == 0).all()
+    assert ctx.handbacks() == 0
