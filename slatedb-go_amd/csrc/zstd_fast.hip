@@ -1340,7 +1340,8 @@ constexpr uint32_t kZhTreeThreads = 256;
 constexpr uint32_t kZhWin = 192;  // the tree description's window: <= 15 + 1 + 127 bytes + 8 slack
 constexpr uint32_t kZhTreeWave = kZhWin + kZsHufScratch;
 constexpr uint32_t kZhTreeLds = (kZhTreeThreads / 64) * kZhTreeWave;
-constexpr uint32_t kZhBlocks = 16;  // blocks per H2 wave (four stream lanes each)
+constexpr uint32_t kZhBlocks = 15;  // blocks per H2 wave (four stream lanes each; 64 KiB of LDS with
+                                    // the rings, so it fits beside two phase-A2 workgroups)
 constexpr uint32_t kZhRing = 64;    // per-lane LDS ring: four 16-byte chunks
 constexpr uint32_t kZhStreamLds = kZhBlocks * kZhTab + 64 * kZhRing;
 static_assert(2 * kZhStreamLds <= 160 * 1024, "phase H2 workgroups per CU exceed the LDS");
@@ -1435,16 +1436,17 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
       for (uint32_t c = lane; c < nb * (kZhTab / 16); c += kWave) dst[c] = src[c];
     }
     const uint32_t k = k0 + j;
+    const bool mine = j < kZhBlocks && k < items;  // (lanes 60..63 idle)
     uint32_t b = 0, fl = 0;
     uint4 d = make_uint4(0, 0, 0, 0);
-    if (k < items) {
+    if (mine) {
       b = z.hlist[k];
       fl = z.rec[b].info >> 16;
       d = reinterpret_cast<const uint4*>(z.hdesc + 16 * size_t(k))[l];
     }
     const uint32_t tl = d.w >> 16, lo = d.w & 0xFFFFu, m = d.z, sl = d.y, fs = d.x;
     // the lane's stream: frame bytes [fs, fs + sl) from the 16-aligned frame base F
-    bool act = k < items && (fl & kZfFast) && tl != 0;
+    bool act = mine && (fl & kZfFast) && tl != 0;
     const uint8_t* F = nullptr;
     uint8_t* out = nullptr;
     if (act) {
@@ -1472,10 +1474,26 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
     int32_t clo = 0;
     uint64_t cv = 0;
     const uint32_t tmask = (1u << tl) - 1u;
-    const uint16_t* tab = reinterpret_cast<const uint16_t*>(smem + j * kZhTab);
+    const uint16_t* tab = reinterpret_cast<const uint16_t*>(smem + min(j, kZhBlocks - 1) * kZhTab);
     zs_sync();
     // the window's first fill (below)
     clo = INT32_MAX;
+    // the output through a 16-byte register stage aligned to the address (a store per 16 bytes,
+    // so the chunk commit's wait finds the last store long done); the stage's partly covered
+    // pieces at the stream's two ends go out as byte stores (the neighbouring stream owns the rest)
+    const uint32_t ph = uint32_t(reinterpret_cast<uintptr_t>(out)) & 15u;
+    uint64_t sg0 = 0, sg1 = 0;
+    auto flush = [&](uint32_t i_last) {  // the stage holds output bytes up to symbol i_last
+      const uint32_t e = ph + i_last + 1, c0 = (e - 1) & ~15u;  // the stage's piece [c0, c0 + 16)
+      uint8_t* dst = out - ph + c0;
+      const uint32_t lo_b = c0 < ph ? ph - c0 : 0u, hi_b = e - c0;  // covered bytes [lo_b, hi_b)
+      if (lo_b == 0 && hi_b == 16) {
+        *reinterpret_cast<uint4*>(dst) = make_uint4(uint32_t(sg0), uint32_t(sg0 >> 32), uint32_t(sg1), uint32_t(sg1 >> 32));
+      } else {
+        for (uint32_t q = lo_b; q < hi_b; q++) dst[q] = uint8_t((q < 8 ? sg0 >> (8 * q) : sg1 >> (8 * (q - 8))) & 0xFF);
+      }
+      sg0 = sg1 = 0;
+    };
     for (uint32_t i = 0; __ballot(act && i < m); i++) {
       const bool go = act && i < m;
       if (go && P - int32_t(tl) < clo) {
@@ -1493,7 +1511,11 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
       if (bp < int32_t(tl)) v = bp > 0 ? v & ~((1u << (int32_t(tl) - bp)) - 1u) : 0u;  // zeros below the stream
       const uint32_t e = tab[v];
       if (go) {
-        out[i] = uint8_t(e);
+        const uint32_t q = (ph + i) & 15u;
+        const uint64_t by = uint64_t(e & 0xFFu) << (8 * (q & 7));
+        sg0 |= q < 8 ? by : 0ull;
+        sg1 |= q < 8 ? 0ull : by;
+        if (q == 15 || i + 1 == m) flush(i);
         bp -= int32_t(e >> 8);
         P -= int32_t(e >> 8);
       }
@@ -1501,12 +1523,15 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
     bad = bad || (act && bp != 0);
     // per block: any failing stream hands it back; else phase B builds it from the output slot
     const uint32_t bm = uint32_t(__ballot(bad) >> (4 * j)) & 15u;
-    if (l == 0 && k < items && (fl & kZfFast) && tl != 0) {
+    if (l == 0 && mine && (fl & kZfFast) && tl != 0) {
       if (bm) {
         z.rec[b].info = 0;
         z.list[atomicAdd(z.count, 1u)] = b;
       } else {
-        z.rec[b].info = (z.rec[b].info & ~((kZfHuf | kZfHuf4) << 16)) | (kZfOutLit << 16);
+        // (atomics: phase A2 may clear the record at the same time on the main stream; a cleared
+        // record stays without kZfFast, and B / C skip it)
+        atomicAnd(&z.rec[b].info, ~((kZfHuf | kZfHuf4) << 16));
+        atomicOr(&z.rec[b].info, kZfOutLit << 16);
       }
     }
     zs_sync();
@@ -1769,22 +1794,40 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   // phase A': the blocks phase A listed for the FSE parse (four one-wave workgroups per CU)
   zs_fse_parse_kernel<<<uint32_t(num_cus) * kZfFseWgs, kZfFseThreads, size_t(kZfFseThreads) * kZfFseLane, st>>>(a, z);
   const size_t lds_crc = kTab16Bytes + size_t(kZfCrcThreads) * SLATE_ZF_CRC_RUN;
-  const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * 3u);
-  zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
-  // phases H1 / H2: the Huffman-literal blocks' trees, then their streams lane per stream (the
-  // workgroups of an empty list exit at once); SLATE_ZF_NO_H (A/B runs): phase B' takes them all
-  const bool no_h = getenv("SLATE_ZF_NO_H") != nullptr;  // (read per call: same-process A/B)
+  // (read per call, for same-process A/B runs) SLATE_ZF_NO_H: phase B' takes every Huffman-literal
+  // block; SLATE_ZF_H_SERIAL: phases H1 / H2 after A2 on the main stream instead of beside it;
+  // SLATE_ZF_CRC_WG: phase A2's workgroups per CU (2 leave room for H1 / H2 beside it)
+  const bool no_h = getenv("SLATE_ZF_NO_H") != nullptr;
+  const bool h_serial = getenv("SLATE_ZF_H_SERIAL") != nullptr;
+  const char* crc_wg_env = getenv("SLATE_ZF_CRC_WG");
+  const uint32_t crc_wg = crc_wg_env && atoi(crc_wg_env) >= 1 && atoi(crc_wg_env) <= 3 ? uint32_t(atoi(crc_wg_env)) : 2u;
+  const uint32_t grid_crc = min((a.n + kZfCrcThreads - 1) / kZfCrcThreads, uint32_t(num_cus) * crc_wg);
   ZsFastArgs zh = z;
-  if (no_h) {
-    zh.hcap = 0;
+  const uint32_t hmax = no_h ? 0u : min(a.n, z.hcap);
+  if (no_h) zh.hcap = 0;
+  SideStream* fh = (h_serial || !a.side || !hmax) ? nullptr : a.side;
+  hipStream_t hs = st;
+  if (fh && fh->get() && hipEventRecord(fh->fork, st) == hipSuccess && hipStreamWaitEvent(fh->s, fh->fork, 0) == hipSuccess)
+    hs = fh->s;
+  // phases H1 / H2: the Huffman-literal blocks' trees, then their streams lane per stream (the
+  // workgroups of an empty list exit at once): beside A2 on the side stream, or after it
+  static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_stream_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhStreamLds));
+  if (attr_t != hipSuccess) return attr_t;
+  const uint32_t grid_h1 = min((hmax + 3) / 4, uint32_t(num_cus) * 6u);
+  const uint32_t grid_h2 = min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u);
+  if (hs != st) {
+    zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, hs>>>(a, z);
+    zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, hs>>>(a, z);
+    zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
+    hipError_t e = hipEventRecord(fh->join, hs);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, fh->join, 0);
+    if (e != hipSuccess) return e;
   } else {
-    static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_stream_kernel),
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhStreamLds));
-    if (attr_t != hipSuccess) return attr_t;
-    const uint32_t hmax = min(a.n, z.hcap);
+    zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
     if (hmax) {
-      zs_huf_tree_kernel<<<min((hmax + 3) / 4, uint32_t(num_cus) * 6u), kZhTreeThreads, kZhTreeLds, st>>>(a, z);
-      zs_huf_stream_kernel<<<min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u), 64, kZhStreamLds, st>>>(a, z);
+      zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, st>>>(a, z);
+      zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, st>>>(a, z);
     }
   }
   const size_t lds_b = kZfBuildLds;

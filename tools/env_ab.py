@@ -1,7 +1,10 @@
-"""Same-process A/B of a per-call library switch (an environment variable the library reads on
-every call: SLATE_ZL_NO_STAGE, SLATE_ZF_NO_H) on one of bench.py's decode workloads, rounds
-alternating, a step = plan + decode timed with HIP events on the context's stream.
-usage: python tools/env_ab.py WORKLOAD ENVVAR [BLOCKS] [ROUNDS] [STEPS]
+"""Same-process A/B of per-call library switches (environment variables the library reads on every
+call: SLATE_ZL_NO_STAGE, SLATE_ZF_NO_H, SLATE_ZF_H_SERIAL, SLATE_ZF_CRC_WG) on one of bench.py's
+decode workloads, rounds alternating, a step = plan + decode timed with HIP events on the
+context's stream.
+usage: python tools/env_ab.py WORKLOAD ENVVAR [BLOCKS] [ROUNDS] [STEPS]   (on = unset, off = ENVVAR=1)
+       python tools/env_ab.py WORKLOAD MODE1 MODE2 ... --blocks N --rounds R --steps S
+         MODE = name:VAR=VAL,VAR=VAL (name: alone = no variables set)
   WORKLOAD: kv100_zlib | kv100_zstd (configs[1]'s V-half blocks) | configs4_zstd (bench --codec zstd)"""
 import json
 import os
@@ -18,10 +21,27 @@ def main():
     import bench
     import slatecodec as sc
     from tools import workload as wl
-    wk, var = sys.argv[1], sys.argv[2]
-    n = int(sys.argv[3]) if len(sys.argv) > 3 else 1_000_000
-    rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 3
-    steps = int(sys.argv[5]) if len(sys.argv) > 5 else 5
+    argv = sys.argv[1:]
+    opts = {"--blocks": 1_000_000, "--rounds": 3, "--steps": 5}
+    for k in list(opts):
+        if k in argv:
+            i = argv.index(k)
+            opts[k] = int(argv[i + 1])
+            del argv[i:i + 2]
+    wk = argv[0]
+    if ":" in argv[1]:
+        modes = []
+        for spec in argv[1:]:
+            name, _, body = spec.partition(":")
+            modes.append((name, dict(kv.split("=", 1) for kv in body.split(",") if kv)))
+        n, rounds, steps = opts["--blocks"], opts["--rounds"], opts["--steps"]
+    else:
+        var = argv[1]
+        modes = [("on", {}), ("off", {var: "1"})]
+        n = int(argv[2]) if len(argv) > 2 else 1_000_000
+        rounds = int(argv[3]) if len(argv) > 3 else 3
+        steps = int(argv[4]) if len(argv) > 4 else 5
+    allvars = sorted({v for _, m in modes for v in m})
     t0 = time.time()
     if wk == "configs4_zstd":
         codec = sc.ZSTD
@@ -36,30 +56,27 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     leg = bench.DecodeLeg(sc, ctx, codec, blob, in_off, time_plan=True)
-    res = {"on": [], "off": []}
+    res = {name: [] for name, _ in modes}
+    dec_bytes = int(dec_off[-1])
     for r in range(rounds):
-        for name in ("on", "off"):
-            if name == "off":
-                os.environ[var] = "1"
-            else:
-                os.environ.pop(var, None)
+        for name, env in modes:
+            for v in allvars:
+                os.environ.pop(v, None)
+            os.environ.update(env)
             ctx.handbacks(reset=True)
             kern, wall = leg.timed(torch, stream, steps, 1)
             hb = ctx.handbacks(reset=True)
             meta = leg.d_meta.download().view(sc.META_DTYPE)
             res[name].append(kern)
-            print(json.dumps({"round": r, var: name == "off", "step_ms": round(kern, 4), "wall_ms": round(wall, 4),
-                              "handbacks": int(hb), "all_ok": bool((meta["status"] == 0).all())}), flush=True)
-        verified = leg.verify_against_decoded((dec, dec_off), leg.d_meta.download().view(sc.META_DTYPE))
-        print(json.dumps({"round": r, "verified_blocks_last_off": verified}), flush=True)
-    os.environ.pop(var, None)
-    leg.step()
-    torch.cuda.synchronize()
-    verified = leg.verify_against_decoded((dec, dec_off), leg.d_meta.download().view(sc.META_DTYPE))
-    dec_bytes = int(dec_off[-1])
-    on, off = float(np.median(res["on"])), float(np.median(res["off"]))
-    print(json.dumps({"workload": wk, "blocks": n, "switch": var, "on_ms": round(on, 4), "off_ms": round(off, 4),
-                      "on_gib_s": round(dec_bytes / (on * 1e-3) / 2**30, 1), "verified_blocks_on": verified}), flush=True)
+            verified = leg.verify_against_decoded((dec, dec_off), meta) if r == rounds - 1 else 0
+            print(json.dumps({"round": r, "mode": name, "env": env, "step_ms": round(kern, 4), "wall_ms": round(wall, 4),
+                              "handbacks": int(hb), "all_ok": bool((meta["status"] == 0).all()),
+                              "verified_blocks": verified}), flush=True)
+    for v in allvars:
+        os.environ.pop(v, None)
+    print(json.dumps({"workload": wk, "blocks": n, "median_ms": {k: round(float(np.median(x)), 4) for k, x in res.items()},
+                      "median_gib_s": {k: round(dec_bytes / (float(np.median(x)) * 1e-3) / 2**30, 1)
+                                       for k, x in res.items()}}), flush=True)
     leg.free()
 
 
