@@ -256,9 +256,10 @@ __device__ int zs_weights_fse(const uint8_t* base, int32_t off, uint32_t hb, ZsS
   return 0;
 }
 
-// Huffman_Tree_Description at base[off, off+n): bytes used or -1; fills sc->huf, *tl
+// Huffman_Tree_Description at base[off, off+n): bytes used or -1; fills the decoding table (sc->huf,
+// or huf_out when given: then sc->huf is never touched), *tl
 __device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScratch* sc, int lane, uint32_t* tl_out,
-                           uint32_t dbg = 0) {  // dbg: profiling ablations (1<<25 no table fill, 1<<23 no weight decode)
+                           uint32_t dbg = 0, uint16_t* huf_out = nullptr) {  // dbg: profiling ablations (1<<25 no table fill, 1<<23 no weight decode)
   if (n < 1) return -1;
   const uint32_t hb = zrfl(uint32_t(base[off]));
   int nw, used;
@@ -330,7 +331,8 @@ __device__ int zs_huf_read(const uint8_t* base, int32_t off, uint32_t n, ZsScrat
     }
     if (my && !(dbg & (1u << 25))) {
       const uint16_t e = uint16_t(((tl + 1 - my) << 8) | uint32_t(s));
-      for (uint32_t i = 0; i < (1u << (my - 1)); i++) sc->huf[pos + i] = e;
+      uint16_t* huf = huf_out ? huf_out : sc->huf;
+      for (uint32_t i = 0; i < (1u << (my - 1)); i++) huf[pos + i] = e;
     }
   }
   zs_sync();

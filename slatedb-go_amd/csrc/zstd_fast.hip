@@ -1338,7 +1338,10 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
 // Huffman list beyond the slots (zf_huf_cap) take phase B'.
 constexpr uint32_t kZhTreeThreads = 256;
 constexpr uint32_t kZhWin = 192;  // the tree description's window: <= 15 + 1 + 127 bytes + 8 slack
-constexpr uint32_t kZhTreeWave = kZhWin + kZsHufScratch;
+// the tree decode's scratch without its 4 KiB table (H1 writes the table straight to HBM): small
+// waves, so many fit beside phase A2 on the side stream
+constexpr uint32_t kZhScrTail = kZsHufScratch - uint32_t(offsetof(ZsScratch, wt));
+constexpr uint32_t kZhTreeWave = kZhWin + kZhScrTail;
 constexpr uint32_t kZhTreeLds = (kZhTreeThreads / 64) * kZhTreeWave;
 constexpr uint32_t kZhBlocks = 15;  // blocks per H2 wave (four stream lanes each; 64 KiB of LDS with
                                     // the rings, so it fits beside two phase-A2 workgroups)
@@ -1351,7 +1354,8 @@ __global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs 
   const uint32_t items = min(z.count[1], z.hcap);
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* win = smem + wave * kZhTreeWave;
-  ZsScratch* sc = reinterpret_cast<ZsScratch*>(win + kZhWin);
+  // sc's fields from wt on lie in this wave's tail; its huf table is never touched (huf_out below)
+  ZsScratch* sc = reinterpret_cast<ZsScratch*>(win + kZhWin - offsetof(ZsScratch, wt));
   const uint32_t waves = gridDim.x * (kZhTreeThreads / 64);
   for (uint32_t k = blockIdx.x * (kZhTreeThreads / 64) + wave; k < items; k += waves) {
     const uint32_t b = z.hlist[k];
@@ -1374,7 +1378,8 @@ __global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs 
     __builtin_amdgcn_s_waitcnt(0);
     zs_sync();
     uint32_t tl = 0;
-    const int t = zs_huf_read(win, int32_t(off), cs, sc, int(lane), &tl);
+    const int t = zs_huf_read(win, int32_t(off), cs, sc, int(lane), &tl, 0u,
+                              reinterpret_cast<uint16_t*>(z.htab + size_t(k) * kZhTab));
     bool fail = t < 0;
     uint32_t sb = 0, sl = 0, m = 0, lo = 0;  // lane l < nstr: stream l
     if (!fail) {
@@ -1404,12 +1409,7 @@ __global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs 
       }
       continue;
     }
-    // the table (2^tl entries) to the slot; the stream records (absolute frame-relative starts)
-    {
-      const uint4* src = reinterpret_cast<const uint4*>(sc->huf);
-      uint4* dst = reinterpret_cast<uint4*>(z.htab + size_t(k) * kZhTab);
-      for (uint32_t c = lane; c < ((2u << tl) + 15) / 16; c += kWave) dst[c] = src[c];
-    }
+    // (the table went to the slot); the stream records (absolute frame-relative starts)
     if (lane < 4) dk[lane] = lane < nstr ? make_uint4(shift + sb, sl, m, lo | (tl << 16)) : make_uint4(0, 0, 0, 0);
     zs_sync();
   }
@@ -1814,7 +1814,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_stream_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhStreamLds));
   if (attr_t != hipSuccess) return attr_t;
-  const uint32_t grid_h1 = min((hmax + 3) / 4, uint32_t(num_cus) * 6u);
+  const uint32_t grid_h1 = min((hmax + 3) / 4, uint32_t(num_cus) * 8u);
   const uint32_t grid_h2 = min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u);
   if (hs != st) {
     zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, hs>>>(a, z);
