@@ -283,6 +283,7 @@ class DecodeLeg:
         # time_plan: the kernel-time events bracket the plan too (CodecZlib: the plan is phase Z,
         # the inflate itself, staged for the decode call)
         self.sc, self.ctx, self.codec, self.time_plan = sc, ctx, codec, time_plan
+        self.alias = False  # CodecNone: decode without a copy (d_out = NULL: block.go:122's aliasing)
         self.n = n = len(in_off) - 1
         self.d_in = sc.devbuf_from(ctx, blob)
         self.d_in_off = sc.devbuf_from(ctx, np.ascontiguousarray(in_off, np.uint64))
@@ -303,8 +304,8 @@ class DecodeLeg:
                              self.d_row_base.ptr, self.d_scratch.ptr)
         if ev is not None and not self.time_plan:
             ev[0].record(stream)
-        c.decode_device(self.codec, self.d_in.ptr, self.d_in_off.ptr, self.n, self.d_out.ptr, self.d_out_off.ptr,
-                        self.d_meta.ptr, self.d_rows.ptr, self.d_row_base.ptr)
+        c.decode_device(self.codec, self.d_in.ptr, self.d_in_off.ptr, self.n, 0 if self.alias else self.d_out.ptr,
+                        0 if self.alias else self.d_out_off.ptr, self.d_meta.ptr, self.d_rows.ptr, self.d_row_base.ptr)
         if ev is not None:
             ev[1].record(stream)
 
@@ -401,6 +402,25 @@ def codec_none_leg(sc, ctx, stream, wl, args, threads):
     res["roofline"]["traffic"], res["roofline"]["traffic_source"] = pmc_traffic(
         os.path.join(REPO, "profiles", "pmc_decode_none_latest.json"), n, "none")
     res["verified"] = leg.verify_against_generator(wl, (0, 1, n), "all", meta, threads, True)
+    # the same blocks decoded as Go decodes CodecNone, without a copy (block.go:122: Data aliases the
+    # input; d_out = NULL): metas and rows only, checked equal to the copying decode's
+    leg.alias = True
+    rows_copy = leg.d_rows.download()
+    leg.d_meta.memset(0)
+    kern_a, wall_a = leg.timed(torch, stream, args.extra_steps, 2)
+    meta_a = leg.d_meta.download().view(sc.META_DTYPE)
+    same = meta_a.tobytes() == meta.tobytes() and np.array_equal(leg.d_rows.download(), rows_copy)
+    assert same, "CodecNone aliased decode: metas / rows differ from the copying decode"
+    alg_a = int(in_off[-1]) + 16 * int(meta["n_rows"].astype(np.int64).sum()) + 16 * n
+    res["aliased"] = {"ms_per_step": round(wall_a, 4), "kernel_ms": round(kern_a, 4),
+                      "GiBps_decoded": round(res["decoded_bytes"] / (wall_a * 1e-3) / 2**30, 1),
+                      "alg_bytes_per_launch": alg_a, "GBps_alg": round(alg_a / (kern_a * 1e-3) / 1e9, 1),
+                      "same_metas_and_rows": same,
+                      "what": "slate_block_decode_device with d_out = NULL (block.Decode's aliasing for CodecNone, "
+                              "block.go:122): CRC32, offsets and rows checked and described, no decoded copy written; "
+                              "alg bytes = the blocks read + the row descriptors and metas written. The leg's value "
+                              "and roofline above are the copying decode's"}
+    leg.alias = False
     res["workload"] = f"{n} x 4 KiB CodecNone blocks (configs[1] keys and V-half values), device-resident decode"
     leg.free()
     return res

@@ -281,7 +281,9 @@ int slate_devbuf_download_async(slate_ctx* ctx, slate_hostbuf* dst, uint64_t dst
  *   d_out_off[n+1] (bytes) and d_row_base[n+1] (slate_row slots); the totals are
  *   d_out_off[n] and d_row_base[n].  d_scratch must hold slate_decode_scratch_bytes(n).
  * Step 2 (decode): writes the decoded buffer (rows || BE16 offsets || BE16 count)
- *   of block i at d_out + d_out_off[i], its meta and its row descriptors.
+ *   of block i at d_out + d_out_off[i], its meta and its row descriptors.  CodecNone with
+ *   d_out == NULL decodes as Go does, without a copy (block.go:122 aliases the input): block i's
+ *   data is d_in + d_in_off[i] itself, d_out_off may be NULL, metas and rows as always.
  * Both enqueue on the context stream and return without synchronising.
  * CodecZlib (n >= 64): a zlib stream carries no decoded size, so the plan inflates every block
  * (lane per block) and keeps what it parsed -- literals, matches, the Adler-32 -- in the context;

@@ -245,12 +245,18 @@ int slate_block_decode_plan_device(slate_ctx* ctx, int codec, const uint8_t* d_i
 int slate_block_decode_device(slate_ctx* ctx, int codec, const uint8_t* d_in, const uint64_t* d_in_off, uint32_t n,
                               uint8_t* d_out, const uint64_t* d_out_off, slate_block_meta* d_meta, slate_row* d_rows,
                               const uint64_t* d_row_base) {
-  if (!ctx || !d_in_off || !d_out_off || !d_meta || !d_row_base) return SLATE_E_INVALID_ARG;
-  if ((reinterpret_cast<uintptr_t>(d_out) & 15) != 0) return SLATE_E_INVALID_ARG;
+  // CodecNone with d_out == NULL: block.Decode's aliasing (block.go:122, compression.go:128-129) --
+  // block i's Data is the input itself, d_in + d_in_off[i] (meta.data_len bytes; the offsets after
+  // it), so nothing is copied and d_out_off is not used; metas and rows as always
+  const bool alias = codec == SLATE_CODEC_NONE && d_out == nullptr && d_in != nullptr;
+  if (!ctx || !d_in_off || (!d_out_off && !alias) || !d_meta || !d_row_base) return SLATE_E_INVALID_ARG;
+  if ((reinterpret_cast<uintptr_t>(d_out) & 15) != 0 || (!d_out && !alias && n)) return SLATE_E_INVALID_ARG;
   SLATE_HIP(ctx_bind(ctx));
   // the scratch is owned by the context for the device-resident call
   SLATE_HIP(ctx->d_scratch.ensure(decode_scratch_bytes_codec(n, codec)));
-  DecodeArgs a{codec, d_in, d_in_off, n, d_out, d_out_off, d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
+  DecodeArgs a{codec, d_in, d_in_off, n, alias ? const_cast<uint8_t*>(d_in) : d_out, alias ? d_in_off : d_out_off,
+               d_meta, d_rows, d_row_base, nullptr, nullptr, 0};
+  a.no_data = alias ? 1u : 0u;
   a.side = &ctx->side;
   a.handbacks = ctx_handbacks(ctx);
   // the staged plan of exactly these inputs and plan outputs, on this stream, not yet used

@@ -1415,6 +1415,201 @@ __global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs 
   }
 }
 
+// H1, lane per block (shipped; the wave-per-block zs_huf_tree_kernel above stays for A/B runs,
+// SLATE_ZF_H1_WAVE): the tree description as zs_huf_read reads it -- direct 4-bit weights, or
+// FSE-coded ones (zf_ncount8 / zf_fse_build16 as phase A' builds its tables, then the two-state
+// decode of zs_weights_fse) -- the weight checks, and the weight-major table written to the slot
+// with stores of 1, 2, 4 or 8 entries (a weight-w symbol's 2^(w-1) entries start at a multiple of
+// 2^(w-1)).  Stricter than the exact path where it is cheaper (more than 16 weight symbols, counts
+// above 127): such blocks go to the exact path, which decodes and reports them.  One wave per
+// 64 blocks: configs[4]'s ~11 k Huffman blocks are ~170 waves, so the LDS is not rationed.
+constexpr uint32_t kZhLWin = 176;  // 11 chunks from the one holding the description's first byte
+constexpr uint32_t kZhLNorm = kZhLWin, kZhLNext = kZhLNorm + 32, kZhLFt = kZhLNext + 64, kZhLW = kZhLFt + 128;
+constexpr uint32_t kZhLane = kZhLW + 256;  // weights w[0 .. 255]
+static_assert(kZhLane % 16 == 0, "lane records stay 16-byte aligned");
+
+__global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsFastArgs z) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t items = min(z.count[1], z.hcap);
+  const uint32_t lane = threadIdx.x & 63;
+  uint8_t* win = smem + lane * kZhLane;
+  int8_t* norm = reinterpret_cast<int8_t*>(win + kZhLNorm);
+  uint8_t* next = win + kZhLNext;
+  uint16_t* ft = reinterpret_cast<uint16_t*>(win + kZhLFt);
+  uint8_t* w = win + kZhLW;
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(win + kZhLNorm);  // (after the FSE build: norm / next reused)
+  uint16_t* cur = cnt + 16;
+  for (uint32_t r0 = blockIdx.x * 64; r0 < items; r0 += gridDim.x * 64) {
+    const uint32_t k = r0 + lane;
+    uint32_t b = 0, fl = 0;
+    ZsFastRec rec{};
+    if (k < items) {
+      b = z.hlist[k];
+      rec = z.rec[b];
+      fl = rec.info >> 16;
+    }
+    const bool act = k < items && (fl & kZfFast);  // (else the CRC32 failed in phase A2)
+    bool ok = act;
+    uint32_t shift = 0, off = 0, lit = rec.lit, cs = rec.cs, nlit = rec.nlit;
+    const uint8_t* F = nullptr;
+    if (act) {
+      const uint64_t i0 = a.in_off[b];
+      const uint32_t len = uint32_t(a.in_off[b + 1] - i0);
+      shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + i0) & 15);
+      F = a.in + i0 - shift;
+      const uint32_t c0 = (shift + lit) >> 4, cend = (shift + len + 15) >> 4;
+      off = (shift + lit) & 15;
+#pragma unroll
+      for (uint32_t c = 0; c < kZhLWin / 16; c++)
+        lds_put16(win + 16 * c, c0 + c < cend ? *reinterpret_cast<const v4u*>(F + 16 * (c0 + c)) : v4u{0, 0, 0, 0});
+    }
+    // ---- the weights (zs_huf_read / zs_weights_fse)
+    uint32_t nw = 0, used = 0;
+    ok = ok && cs >= 1;
+    const uint32_t hb = ok ? uint32_t(win[off]) : 0u;
+    if (ok && hb >= 128) {
+      nw = hb - 127;
+      const uint32_t nbytes = (nw + 1) / 2;
+      ok = 1 + nbytes <= cs;
+      for (uint32_t i = 0; ok && i < nw; i++) {
+        const uint32_t by = win[off + 1 + i / 2];
+        w[i] = uint8_t((i & 1) ? (by & 15) : (by >> 4));
+      }
+      used = 1 + nbytes;
+    } else if (ok) {
+      ok = 1 + hb <= cs;
+      int r = -1;
+      if (ok) r = zf_ncount8(win, int32_t(off + 1), hb, norm, 15, 6);
+      ok = ok && r >= 0;
+      const uint32_t hs = ok ? uint32_t(r & 0xFFFF) : 0u, al = ok ? uint32_t((r >> 16) & 0xFF) : 0u;
+      const int last = ok ? (r >> 24) : 0;
+      ok = ok && zf_fse_build16(ft, norm, last, int(al), next);
+      const uint32_t so = off + 1 + hs, bn = hb - hs;
+      ok = ok && bn != 0;
+      const uint32_t lastb = ok ? uint32_t(win[so + bn - 1]) : 0u;
+      ok = ok && lastb != 0;
+      int32_t pos = ok ? int32_t(8 * (bn - 1) + (31 - __builtin_clz(lastb | 1u))) : 0;
+      auto rd = [&](uint32_t kb) -> uint32_t {
+        uint32_t v = 0;
+        // (zs_bits reads aligned dwords from its base: the lane record, not the stream's first byte)
+        const int64_t sbit = 8 * int64_t(so);
+        if (kb && pos > 0)
+          v = pos >= int32_t(kb) ? uint32_t(zs_bits(win, sbit + pos - int32_t(kb), kb))
+                                 : uint32_t(zs_bits(win, sbit, uint32_t(pos))) << (kb - uint32_t(pos));
+        pos -= int32_t(kb);
+        return v;
+      };
+      if (ok) {
+        uint32_t s1 = rd(al), s2 = rd(al);
+        for (;;) {  // two interleaved states until the stream overreads (FSE_decompress tail)
+          if (nw > 253) {
+            ok = false;
+            break;
+          }
+          uint32_t e = ft[s1];
+          w[nw++] = uint8_t(e & 63u);
+          s1 = (e >> 9) + rd((e >> 6) & 7u);
+          if (pos < 0) {
+            w[nw++] = uint8_t(ft[s2] & 63u);
+            break;
+          }
+          if (nw > 253) {
+            ok = false;
+            break;
+          }
+          e = ft[s2];
+          w[nw++] = uint8_t(e & 63u);
+          s2 = (e >> 9) + rd((e >> 6) & 7u);
+          if (pos < 0) {
+            w[nw++] = uint8_t(ft[s1] & 63u);
+            break;
+          }
+        }
+      }
+      used = 1 + hb;
+    }
+    // ---- weight statistics (zs_huf_read): counts per weight, the implied last weight, tl
+    uint32_t tl = 0;
+    if (ok) {
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++) cnt[q] = 0;
+      uint32_t total = 0;
+      for (uint32_t i = 0; i < nw; i++) {
+        const uint32_t my = w[i];
+        ok = ok && my <= 11;
+        total += (my && my <= 11) ? (1u << (my - 1)) : 0u;
+        cnt[my & 15] += 1;
+      }
+      ok = ok && total != 0;
+      tl = 32 - __builtin_clz(total | 1u);
+      ok = ok && tl <= 11;
+      const uint32_t rest = (1u << tl) - total;
+      ok = ok && !(rest & (rest - 1)) && rest != 0;
+      const uint32_t lastw = 32 - __builtin_clz(rest | 1u);
+      if (ok) {
+        w[nw] = uint8_t(lastw);
+        cnt[lastw] += 1;
+      }
+      ok = ok && cnt[1] >= 2 && !(cnt[1] & 1);
+    }
+    // ---- the weight-major table into the slot: symbol s of weight my at cur[my], 2^(my-1) entries
+    if (ok) {
+      uint32_t acc = 0;
+      for (uint32_t q = 1; q <= tl; q++) {
+        cur[q] = uint16_t(acc);
+        acc += uint32_t(cnt[q]) << (q - 1);
+      }
+      uint8_t* tab = z.htab + size_t(k) * kZhTab;
+      for (uint32_t sy = 0; sy <= nw; sy++) {
+        const uint32_t my = w[sy];
+        if (!my) continue;
+        const uint32_t p = cur[my], ne = 1u << (my - 1);
+        cur[my] = uint16_t(p + ne);
+        const uint32_t e = ((tl + 1 - my) << 8) | sy, e2 = e | (e << 16);
+        uint8_t* dst = tab + 2 * p;
+        if (ne >= 8) {
+          for (uint32_t c = 0; c < ne / 8; c++) *reinterpret_cast<uint4*>(dst + 16 * c) = make_uint4(e2, e2, e2, e2);
+        } else if (ne == 4) {
+          *reinterpret_cast<uint2*>(dst) = make_uint2(e2, e2);
+        } else if (ne == 2) {
+          *reinterpret_cast<uint32_t*>(dst) = e2;
+        } else {
+          *reinterpret_cast<uint16_t*>(dst) = uint16_t(e);
+        }
+      }
+    }
+    // ---- the streams (as phase B': one, or four behind a 6-byte jump table)
+    const uint32_t nstr = (fl & kZfHuf4) ? 4u : 1u;
+    uint4 sd[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (ok) {
+      const uint32_t q = off + used, qn = cs - used, fq = lit + used;
+      if (nstr == 1) {
+        sd[0] = make_uint4(shift + fq, qn, nlit, tl << 16);
+      } else if (qn < 10) {
+        ok = false;
+      } else {
+        const uint32_t l1 = win[q] | (uint32_t(win[q + 1]) << 8), l2 = win[q + 2] | (uint32_t(win[q + 3]) << 8),
+                       l3 = win[q + 4] | (uint32_t(win[q + 5]) << 8);
+        const uint32_t seg = (nlit + 3) / 4;
+        ok = !(l1 + l2 + l3 + 6 > qn || 3 * seg > nlit);
+        const uint32_t l4 = qn - 6 - l1 - l2 - l3, s0 = shift + fq + 6;
+        sd[0] = make_uint4(s0, l1, seg, 0 | (tl << 16));
+        sd[1] = make_uint4(s0 + l1, l2, seg, seg | (tl << 16));
+        sd[2] = make_uint4(s0 + l1 + l2, l3, seg, (2 * seg) | (tl << 16));
+        sd[3] = make_uint4(s0 + l1 + l2 + l3, l4, nlit - 3 * seg, (3 * seg) | (tl << 16));
+      }
+    }
+    if (ok) {
+      uint4* dk = reinterpret_cast<uint4*>(z.hdesc + 16 * size_t(k));
+#pragma unroll
+      for (uint32_t i = 0; i < 4; i++) dk[i] = sd[i];
+    }
+    // any failed check: to the exact path, as phase B' hands a block back
+    if (act && !ok) z.rec[b].info = 0;
+    list_append(act && !ok, b, z.list, z.count);
+  }
+}
+
 namespace {
 __device__ __forceinline__ uint4 zh_chunk(const uint8_t* F, int32_t c) {
   return c >= 0 ? *reinterpret_cast<const uint4*>(F + 16 * c) : make_uint4(0, 0, 0, 0);
@@ -1814,10 +2009,15 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_stream_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhStreamLds));
   if (attr_t != hipSuccess) return attr_t;
-  const uint32_t grid_h1 = min((hmax + 3) / 4, uint32_t(num_cus) * 8u);
+  const bool h1_wave = getenv("SLATE_ZF_H1_WAVE") != nullptr;
+  const uint32_t grid_h1 = h1_wave ? min((hmax + 3) / 4, uint32_t(num_cus) * 8u) : min((hmax + 63) / 64, uint32_t(num_cus));
+  auto launch_h1 = [&](hipStream_t q) {
+    if (h1_wave) zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, q>>>(a, z);
+    else zs_huf_tree_lanes_kernel<<<grid_h1, 64, size_t(64) * kZhLane, q>>>(a, z);
+  };
   const uint32_t grid_h2 = min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u);
   if (hs != st) {
-    zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, hs>>>(a, z);
+    launch_h1(hs);
     zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, hs>>>(a, z);
     zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
     hipError_t e = hipEventRecord(fh->join, hs);
@@ -1826,7 +2026,7 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   } else {
     zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
     if (hmax) {
-      zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, st>>>(a, z);
+      launch_h1(st);
       zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, st>>>(a, z);
     }
   }

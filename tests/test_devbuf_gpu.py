@@ -86,3 +86,44 @@ def test_headline_decode_on_devbufs(ctx):
             assert out[a:a + dl].tobytes() == o_out[a:a + dl].tobytes(), i
             r0, nr = int(o_rb[i]), int(o_meta["n_rows"][i])
             assert rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+
+
+def test_codec_none_aliased_decode(ctx):
+    """CodecNone with d_out = NULL decodes as Go's block.Decode does, without a copy (block.go:122
+    aliases the input): metas and rows identical to the oracle's, every row descriptor read against
+    the input bytes themselves (a block's data starts at its input offset); blocks beyond the
+    one-wave kernel's window (large values) take the large-block path in the same mode; a damaged
+    CRC reports as in the copying mode."""
+    import random
+    import slatecodec as sc
+    rng = random.Random(5)
+    kvs = bg.kv_synthetic(38 * 120, half=True, tomb_every=11)
+    blocks = bg.sst_blocks(kvs, 4096, ob.NONE)
+    blocks += bg.sst_blocks([(b"big%03d" % i, bytes(rng.randrange(256) for _ in range(7000))) for i in range(3)],
+                            4096, ob.NONE)
+    bad = bytearray(blocks[5])
+    bad[-1] ^= 1
+    blocks[5] = bytes(bad)
+    blob, off = bg.pack(blocks, misalign=3)
+    n = len(blocks)
+    d_in, d_off = sc.devbuf_from(ctx, blob), sc.devbuf_from(ctx, off)
+    d_oo, d_rb = sc.DevBuf(ctx, 8 * (n + 1)), sc.DevBuf(ctx, 8 * (n + 1))
+    d_sc = sc.DevBuf(ctx, sc.decode_scratch_bytes(n) + 64)
+    ctx.decode_plan_device(ob.NONE, d_in.ptr, d_off.ptr, n, d_oo.ptr, d_rb.ptr, d_sc.ptr)
+    d_meta, d_rows = sc.DevBuf(ctx, 16 * n), sc.DevBuf(ctx, 16 * d_rb.u64(n) + 16)
+    ctx.decode_device(ob.NONE, d_in.ptr, d_off.ptr, n, 0, 0, d_meta.ptr, d_rows.ptr, d_rb.ptr)
+    o_out, o_off, o_meta, o_rows, o_rb = ob.block_decode_batch(ob.NONE, blob, off)
+    meta = d_meta.download().view(sc.META_DTYPE)
+    assert meta.tobytes() == o_meta.tobytes()
+    assert int(meta["status"][5]) != 0 and (np.delete(meta["status"], 5) == 0).all()
+    rows = d_rows.download().view(sc.ROW_DTYPE)
+    for i in range(n):
+        if int(o_meta["status"][i]):
+            continue
+        r0, nr = int(o_rb[i]), int(o_meta["n_rows"][i])
+        assert rows[r0:r0 + nr].tobytes() == o_rows[r0:r0 + nr].tobytes(), i
+        a, dl = int(o_off[i]), int(o_meta["data_len"][i])
+        assert blob[int(off[i]):int(off[i]) + dl].tobytes() == o_out[a:a + dl].tobytes(), i
+    # other codecs still need an output buffer
+    assert sc.lib().slate_block_decode_device(ctx.handle, ob.SNAPPY, d_in.ptr, d_off.ptr, n, None, d_oo.ptr,
+                                              d_meta.ptr, d_rows.ptr, d_rb.ptr) == sc.E_INVALID_ARG
