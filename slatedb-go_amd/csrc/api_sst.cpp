@@ -1293,13 +1293,15 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
   }
   // ---- queue the finished blocks (builder.go:169-176, finishBlock :192-213; their index
   // entries went in before the D2H)
+  // (views moved, not copied: ~270 k blocks per 10 M-KV build, each copy of the segment's
+  // shared_ptr an atomic round trip on one cache line)
   for (uint64_t k = 0; k < nb; k++) {
     ByteView v{seg, out_off[k], out_off[k + 1] - out_off[k]};
     if (final && k + 1 == nb) {
-      b->last_block = v;  // Build: the last block opens the final chunk
+      b->last_block = std::move(v);  // Build: the last block opens the final chunk
     } else {
       b->current_len += v.len;
-      b->blocks.push_back(v);
+      b->blocks.push_back(std::move(v));
     }
   }
   const uint64_t consumed = final ? n64 : starts[nb_total - 1];
@@ -1702,6 +1704,7 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
       delete t;
       return b->sticky = f.st;
     }
+    buf.reserve(buf.size() + f.section.size() + 16);  // (one copy of the section, no regrowth)
     buf.insert(buf.end(), f.section.begin(), f.section.end());
     t->bloom_bits.swap(f.bits);
     t->has_bloom = true;
@@ -1829,7 +1832,8 @@ int slate_sst_builder_build(slate_sst_builder* b, slate_sst_table** table) {
     delete t;
     return SLATE_E_OOM;
   }
-  t->chunks.assign(b->blocks.begin(), b->blocks.end());
+  t->chunks.reserve(b->blocks.size() + 1);
+  t->chunks.assign(std::make_move_iterator(b->blocks.begin()), std::make_move_iterator(b->blocks.end()));
   b->blocks.clear();
   if (!buf.empty()) par_memcpy(fin->p, buf.data(), buf.size());
   if (!index.empty()) par_memcpy(fin->p + buf.size(), index.data(), index.size());

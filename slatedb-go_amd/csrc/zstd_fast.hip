@@ -1345,8 +1345,12 @@ constexpr uint32_t kZhTreeWave = kZhWin + kZhScrTail;
 constexpr uint32_t kZhTreeLds = (kZhTreeThreads / 64) * kZhTreeWave;
 constexpr uint32_t kZhBlocks = 15;  // blocks per H2 wave (four stream lanes each; 64 KiB of LDS with
                                     // the rings, so it fits beside two phase-A2 workgroups)
-constexpr uint32_t kZhRing = 64;    // per-lane LDS ring: four 16-byte chunks
-constexpr uint32_t kZhStreamLds = kZhBlocks * kZhTab + 64 * kZhRing;
+// per-lane LDS ring: four 16-byte chunks at a 17-dword stride (an odd stride puts the lanes' ring
+// dwords at one offset in distinct banks; a 16-dword one put all of them in two), written as dwords;
+// lanes 60..63 hold no stream and no ring
+constexpr uint32_t kZhRing = 68;
+constexpr uint32_t kZhStreamLds = kZhBlocks * kZhTab + 4 * kZhBlocks * kZhRing;
+static_assert(4 * kZhBlocks * kZhRing <= 4096, "the rings fit the 4 KiB after the tables");
 static_assert(2 * kZhStreamLds <= 160 * 1024, "phase H2 workgroups per CU exceed the LDS");
 
 __global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs a, ZsFastArgs z) {
@@ -1423,22 +1427,38 @@ __global__ __launch_bounds__(kZhTreeThreads) void zs_huf_tree_kernel(DecodeArgs 
 // 2^(w-1)).  Stricter than the exact path where it is cheaper (more than 16 weight symbols, counts
 // above 127): such blocks go to the exact path, which decodes and reports them.  One wave per
 // 64 blocks: configs[4]'s ~11 k Huffman blocks are ~170 waves, so the LDS is not rationed.
-constexpr uint32_t kZhLWin = 176;  // 11 chunks from the one holding the description's first byte
-constexpr uint32_t kZhLNorm = kZhLWin, kZhLNext = kZhLNorm + 32, kZhLFt = kZhLNext + 64, kZhLW = kZhLFt + 128;
-constexpr uint32_t kZhLane = kZhLW + 256;  // weights w[0 .. 255]
-static_assert(kZhLane % 16 == 0, "lane records stay 16-byte aligned");
+constexpr uint32_t kZhLWin = 176;   // 11 chunks from the one holding the description's first byte
+// LDS, by region (per-lane accesses at one offset land in distinct banks where they are hot):
+//   window   lane l at 180 l (45 dwords: odd), written as dwords -- the weight decode's bit reads
+//   norm/next lane l at kZhLNn + 96 l (the FSE build's counts, brief)
+//   ft       lane l at kZhLFt + 144 l (the FSE table as zf_fse_build16 builds it: 16-byte aligned)
+//   fti      entry i of lane l at kZhLFti + 2 (64 i + l) (the same table interleaved: the decode's reads)
+//   w        weight k of lane l at kZhLW + 64 k + l (interleaved bytes)
+constexpr uint32_t kZhLWinStride = 180;
+constexpr uint32_t kZhLNn = 64 * kZhLWinStride, kZhLFt = kZhLNn + 64 * 96, kZhLFti = kZhLFt + 64 * 144,
+                   kZhLW = kZhLFti + 64 * 64 * 2, kZhLLds = kZhLW + 64 * 256;
+static_assert(kZhLWinStride % 4 == 0 && (kZhLWinStride / 4) % 2 == 1 && kZhLWinStride >= kZhLWin, "window stride");
+
+// packed per-weight counters (9 bits each, weights 1..11) and table cursors (12 bits each)
+__device__ __forceinline__ void zh_cnt_add(uint64_t& c0, uint64_t& c1, uint32_t my) {
+  c0 += (my >= 1 && my <= 6) ? uint64_t(1) << (9 * (my - 1)) : 0ull;
+  c1 += (my >= 7 && my <= 11) ? uint64_t(1) << (9 * (my - 7)) : 0ull;
+}
+__device__ __forceinline__ uint32_t zh_cnt(uint64_t c0, uint64_t c1, uint32_t q) {
+  return uint32_t((q <= 6 ? c0 >> (9 * (q - 1)) : c1 >> (9 * (q - 7))) & 511u);
+}
 
 __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsFastArgs z) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t items = min(z.count[1], z.hcap);
   const uint32_t lane = threadIdx.x & 63;
-  uint8_t* win = smem + lane * kZhLane;
-  int8_t* norm = reinterpret_cast<int8_t*>(win + kZhLNorm);
-  uint8_t* next = win + kZhLNext;
-  uint16_t* ft = reinterpret_cast<uint16_t*>(win + kZhLFt);
-  uint8_t* w = win + kZhLW;
-  uint16_t* cnt = reinterpret_cast<uint16_t*>(win + kZhLNorm);  // (after the FSE build: norm / next reused)
-  uint16_t* cur = cnt + 16;
+  uint8_t* win = smem + lane * kZhLWinStride;
+  uint32_t* wind = reinterpret_cast<uint32_t*>(win);
+  int8_t* norm = reinterpret_cast<int8_t*>(smem + kZhLNn + 96 * lane);
+  uint8_t* next = smem + kZhLNn + 96 * lane + 32;
+  uint16_t* ft = reinterpret_cast<uint16_t*>(smem + kZhLFt + 144 * lane);
+  uint16_t* fti = reinterpret_cast<uint16_t*>(smem + kZhLFti) + lane;  // entry i at fti[64 i]
+  uint8_t* w = smem + kZhLW + lane;                                      // weight k at w[64 k]
   for (uint32_t r0 = blockIdx.x * 64; r0 < items; r0 += gridDim.x * 64) {
     const uint32_t k = r0 + lane;
     uint32_t b = 0, fl = 0;
@@ -1451,17 +1471,24 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
     const bool act = k < items && (fl & kZfFast);  // (else the CRC32 failed in phase A2)
     bool ok = act;
     uint32_t shift = 0, off = 0, lit = rec.lit, cs = rec.cs, nlit = rec.nlit;
-    const uint8_t* F = nullptr;
     if (act) {
       const uint64_t i0 = a.in_off[b];
       const uint32_t len = uint32_t(a.in_off[b + 1] - i0);
       shift = uint32_t(reinterpret_cast<uintptr_t>(a.in + i0) & 15);
-      F = a.in + i0 - shift;
+      const uint8_t* F = a.in + i0 - shift;
       const uint32_t c0 = (shift + lit) >> 4, cend = (shift + len + 15) >> 4;
       off = (shift + lit) & 15;
+      v4u ch[kZhLWin / 16];
 #pragma unroll
       for (uint32_t c = 0; c < kZhLWin / 16; c++)
-        lds_put16(win + 16 * c, c0 + c < cend ? *reinterpret_cast<const v4u*>(F + 16 * (c0 + c)) : v4u{0, 0, 0, 0});
+        ch[c] = c0 + c < cend ? *reinterpret_cast<const v4u*>(F + 16 * (c0 + c)) : v4u{0, 0, 0, 0};
+#pragma unroll
+      for (uint32_t c = 0; c < kZhLWin / 16; c++) {
+        wind[4 * c] = ch[c].x;
+        wind[4 * c + 1] = ch[c].y;
+        wind[4 * c + 2] = ch[c].z;
+        wind[4 * c + 3] = ch[c].w;
+      }
     }
     // ---- the weights (zs_huf_read / zs_weights_fse)
     uint32_t nw = 0, used = 0;
@@ -1473,7 +1500,7 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
       ok = 1 + nbytes <= cs;
       for (uint32_t i = 0; ok && i < nw; i++) {
         const uint32_t by = win[off + 1 + i / 2];
-        w[i] = uint8_t((i & 1) ? (by & 15) : (by >> 4));
+        w[64 * i] = uint8_t((i & 1) ? (by & 15) : (by >> 4));
       }
       used = 1 + nbytes;
     } else if (ok) {
@@ -1484,15 +1511,17 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
       const uint32_t hs = ok ? uint32_t(r & 0xFFFF) : 0u, al = ok ? uint32_t((r >> 16) & 0xFF) : 0u;
       const int last = ok ? (r >> 24) : 0;
       ok = ok && zf_fse_build16(ft, norm, last, int(al), next);
+      if (ok)
+        for (uint32_t i = 0; i < (1u << al); i++) fti[64 * i] = ft[i];
       const uint32_t so = off + 1 + hs, bn = hb - hs;
       ok = ok && bn != 0;
       const uint32_t lastb = ok ? uint32_t(win[so + bn - 1]) : 0u;
       ok = ok && lastb != 0;
       int32_t pos = ok ? int32_t(8 * (bn - 1) + (31 - __builtin_clz(lastb | 1u))) : 0;
+      const int64_t sbit = 8 * int64_t(so);
       auto rd = [&](uint32_t kb) -> uint32_t {
+        // (zs_bits reads aligned dwords from its base: the lane's window, not the stream's first byte)
         uint32_t v = 0;
-        // (zs_bits reads aligned dwords from its base: the lane record, not the stream's first byte)
-        const int64_t sbit = 8 * int64_t(so);
         if (kb && pos > 0)
           v = pos >= int32_t(kb) ? uint32_t(zs_bits(win, sbit + pos - int32_t(kb), kb))
                                  : uint32_t(zs_bits(win, sbit, uint32_t(pos))) << (kb - uint32_t(pos));
@@ -1506,22 +1535,22 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
             ok = false;
             break;
           }
-          uint32_t e = ft[s1];
-          w[nw++] = uint8_t(e & 63u);
+          uint32_t e = fti[64 * s1];
+          w[64 * nw++] = uint8_t(e & 63u);
           s1 = (e >> 9) + rd((e >> 6) & 7u);
           if (pos < 0) {
-            w[nw++] = uint8_t(ft[s2] & 63u);
+            w[64 * nw++] = uint8_t(fti[64 * s2] & 63u);
             break;
           }
           if (nw > 253) {
             ok = false;
             break;
           }
-          e = ft[s2];
-          w[nw++] = uint8_t(e & 63u);
+          e = fti[64 * s2];
+          w[64 * nw++] = uint8_t(e & 63u);
           s2 = (e >> 9) + rd((e >> 6) & 7u);
           if (pos < 0) {
-            w[nw++] = uint8_t(ft[s1] & 63u);
+            w[64 * nw++] = uint8_t(fti[64 * s1] & 63u);
             break;
           }
         }
@@ -1530,41 +1559,50 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
     }
     // ---- weight statistics (zs_huf_read): counts per weight, the implied last weight, tl
     uint32_t tl = 0;
+    uint64_t c0 = 0, c1 = 0;
     if (ok) {
-#pragma unroll
-      for (uint32_t q = 0; q < 16; q++) cnt[q] = 0;
       uint32_t total = 0;
       for (uint32_t i = 0; i < nw; i++) {
-        const uint32_t my = w[i];
+        const uint32_t my = w[64 * i];
         ok = ok && my <= 11;
         total += (my && my <= 11) ? (1u << (my - 1)) : 0u;
-        cnt[my & 15] += 1;
+        zh_cnt_add(c0, c1, my);
       }
       ok = ok && total != 0;
       tl = 32 - __builtin_clz(total | 1u);
       ok = ok && tl <= 11;
       const uint32_t rest = (1u << tl) - total;
-      ok = ok && !(rest & (rest - 1)) && rest != 0;
+      ok = ok && rest != 0 && !(rest & (rest - 1));
       const uint32_t lastw = 32 - __builtin_clz(rest | 1u);
       if (ok) {
-        w[nw] = uint8_t(lastw);
-        cnt[lastw] += 1;
+        w[64 * nw] = uint8_t(lastw);
+        zh_cnt_add(c0, c1, lastw);
       }
-      ok = ok && cnt[1] >= 2 && !(cnt[1] & 1);
+      const uint32_t r1 = zh_cnt(c0, c1, 1);
+      ok = ok && r1 >= 2 && !(r1 & 1);
     }
     // ---- the weight-major table into the slot: symbol s of weight my at cur[my], 2^(my-1) entries
     if (ok) {
+      uint64_t p0 = 0, p1 = 0, p2 = 0;  // cursors, 12 bits each: weights 1..5, 6..10, 11
       uint32_t acc = 0;
       for (uint32_t q = 1; q <= tl; q++) {
-        cur[q] = uint16_t(acc);
-        acc += uint32_t(cnt[q]) << (q - 1);
+        const uint64_t v = uint64_t(acc);
+        p0 |= q <= 5 ? v << (12 * (q - 1)) : 0ull;
+        p1 |= (q >= 6 && q <= 10) ? v << (12 * (q - 6)) : 0ull;
+        p2 |= q == 11 ? v : 0ull;
+        acc += zh_cnt(c0, c1, q) << (q - 1);
       }
       uint8_t* tab = z.htab + size_t(k) * kZhTab;
       for (uint32_t sy = 0; sy <= nw; sy++) {
-        const uint32_t my = w[sy];
+        const uint32_t my = w[64 * sy];
         if (!my) continue;
-        const uint32_t p = cur[my], ne = 1u << (my - 1);
-        cur[my] = uint16_t(p + ne);
+        const uint32_t sh = my <= 5 ? 12 * (my - 1) : (my <= 10 ? 12 * (my - 6) : 0u);
+        const uint64_t word = my <= 5 ? p0 : (my <= 10 ? p1 : p2);
+        const uint32_t p = uint32_t(word >> sh) & 4095u, ne = 1u << (my - 1);
+        const uint64_t inc = uint64_t(ne) << sh;
+        p0 += my <= 5 ? inc : 0ull;
+        p1 += (my >= 6 && my <= 10) ? inc : 0ull;
+        p2 += my == 11 ? inc : 0ull;
         const uint32_t e = ((tl + 1 - my) << 8) | sy, e2 = e | (e << 16);
         uint8_t* dst = tab + 2 * p;
         if (ne >= 8) {
@@ -1620,7 +1658,7 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t items = min(z.count[1], z.hcap);
   const uint32_t lane = threadIdx.x & 63, j = lane >> 2, l = lane & 3;
-  uint8_t* ring = smem + kZhBlocks * kZhTab + lane * kZhRing;
+  uint8_t* ring = smem + kZhBlocks * kZhTab + min(lane, 4 * kZhBlocks - 1) * kZhRing;
   uint32_t* rd = reinterpret_cast<uint32_t*>(ring);
   for (uint32_t k0 = blockIdx.x * kZhBlocks; k0 < items; k0 += gridDim.x * kZhBlocks) {
     // the 16 blocks' tables (whole slots; entries past 2^tl are never read)
@@ -1655,8 +1693,17 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
     const int32_t T = act ? int32_t((fs + sl - 1) >> 4) : 0;
     const uint4 cT = act ? zh_chunk(F, T) : make_uint4(0, 0, 0, 0);
     const uint4 cT1 = act ? zh_chunk(F, T - 1) : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(ring + 16 * (T & 3)) = cT;
-    *reinterpret_cast<uint4*>(ring + 16 * ((T - 1) & 3)) = cT1;
+    auto put = [&](int32_t c, const uint4& v) {  // (dwords: the ring is 4-byte aligned)
+      uint32_t* q = rd + 4 * (c & 3);
+      q[0] = v.x;
+      q[1] = v.y;
+      q[2] = v.z;
+      q[3] = v.w;
+    };
+    if (mine) {
+      put(T, cT);
+      put(T - 1, cT1);
+    }
     int32_t lowc = T - 1;
     uint4 pf = act ? zh_chunk(F, T - 2) : make_uint4(0, 0, 0, 0);
     const uint32_t lb = (fs + sl - 1) & 15;
@@ -1697,7 +1744,7 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
         const int32_t D = clo >> 5;
         if ((D >> 2) < lowc) {  // one chunk lower: commit the prefetched one, fetch the next
           lowc -= 1;
-          *reinterpret_cast<uint4*>(ring + 16 * (lowc & 3)) = pf;
+          put(lowc, pf);
           pf = zh_chunk(F, lowc - 1);
         }
         cv = uint64_t(rd[D & 15]) | (uint64_t(rd[(D + 1) & 15]) << 32);
@@ -2009,11 +2056,14 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   static const hipError_t attr_t = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_stream_kernel),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhStreamLds));
   if (attr_t != hipSuccess) return attr_t;
+  static const hipError_t attr_l = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_huf_tree_lanes_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(kZhLLds));
+  if (attr_l != hipSuccess) return attr_l;
   const bool h1_wave = getenv("SLATE_ZF_H1_WAVE") != nullptr;
   const uint32_t grid_h1 = h1_wave ? min((hmax + 3) / 4, uint32_t(num_cus) * 8u) : min((hmax + 63) / 64, uint32_t(num_cus));
   auto launch_h1 = [&](hipStream_t q) {
     if (h1_wave) zs_huf_tree_kernel<<<grid_h1, kZhTreeThreads, kZhTreeLds, q>>>(a, z);
-    else zs_huf_tree_lanes_kernel<<<grid_h1, 64, size_t(64) * kZhLane, q>>>(a, z);
+    else zs_huf_tree_lanes_kernel<<<grid_h1, 64, kZhLLds, q>>>(a, z);
   };
   const uint32_t grid_h2 = min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u);
   if (hs != st) {
