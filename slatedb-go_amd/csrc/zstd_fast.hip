@@ -1518,14 +1518,21 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
       const uint32_t lastb = ok ? uint32_t(win[so + bn - 1]) : 0u;
       ok = ok && lastb != 0;
       int32_t pos = ok ? int32_t(8 * (bn - 1) + (31 - __builtin_clz(lastb | 1u))) : 0;
-      const int64_t sbit = 8 * int64_t(so);
+      // the backward stream's bits through a 64-bit register window [wlo, wlo + 64) (wlo a multiple
+      // of 32; stream dword d = bytes so + 4d .. +3, zeros below the stream's first bit: rd's
+      // semantics for pos < kb), refilled from the lane's window when a read would leave it
+      int32_t wlo = INT32_MAX;
+      uint64_t wv = 0;
+      auto sdw = [&](int32_t d) -> uint32_t { return d >= 0 ? lds_u32(win, int32_t(so) + 4 * d) : 0u; };
       auto rd = [&](uint32_t kb) -> uint32_t {
-        // (zs_bits reads aligned dwords from its base: the lane's window, not the stream's first byte)
-        uint32_t v = 0;
-        if (kb && pos > 0)
-          v = pos >= int32_t(kb) ? uint32_t(zs_bits(win, sbit + pos - int32_t(kb), kb))
-                                 : uint32_t(zs_bits(win, sbit, uint32_t(pos))) << (kb - uint32_t(pos));
-        pos -= int32_t(kb);
+        const int32_t lo = pos - int32_t(kb);
+        if (lo < wlo) {
+          wlo = ((pos + 31) & ~31) - 64;
+          const int32_t d = wlo >> 5;
+          wv = uint64_t(sdw(d)) | (uint64_t(sdw(d + 1)) << 32);
+        }
+        const uint32_t v = uint32_t(wv >> uint32_t(lo - wlo)) & ((1u << kb) - 1u);
+        pos = lo;
         return v;
       };
       if (ok) {
@@ -1649,8 +1656,25 @@ __global__ __launch_bounds__(64) void zs_huf_tree_lanes_kernel(DecodeArgs a, ZsF
 }
 
 namespace {
-__device__ __forceinline__ uint4 zh_chunk(const uint8_t* F, int32_t c) {
-  return c >= 0 ? *reinterpret_cast<const uint4*>(F + 16 * c) : make_uint4(0, 0, 0, 0);
+// chunk c of the frame (16-byte aligned base F) as a stream starting at frame byte fs sees it: the
+// bytes before fs read as zeros (a backward stream's bits below its start: zs_peek), so a peek
+// needs no end-of-stream case
+__device__ __forceinline__ uint4 zh_chunk(const uint8_t* F, int32_t c, uint32_t fs) {
+  const int32_t c0 = int32_t(fs >> 4);
+  if (c < c0) return make_uint4(0, 0, 0, 0);
+  uint4 v = *reinterpret_cast<const uint4*>(F + 16 * c);
+  if (c == c0) {
+    const uint32_t z = fs & 15;  // bytes [0, z) zeroed
+    auto keep = [&](uint32_t k) -> uint32_t {  // dword k's mask
+      const int32_t n = int32_t(z) - int32_t(4 * k);  // its bytes below fs
+      return n <= 0 ? 0xFFFFFFFFu : (n >= 4 ? 0u : ~((1u << (8 * n)) - 1u));
+    };
+    v.x &= keep(0);
+    v.y &= keep(1);
+    v.z &= keep(2);
+    v.w &= keep(3);
+  }
+  return v;
 }
 }  // namespace
 
@@ -1691,8 +1715,8 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
     act = act && !bad;
     // the top chunk (the stream's last byte: zs_bstart) and the one below into the ring
     const int32_t T = act ? int32_t((fs + sl - 1) >> 4) : 0;
-    const uint4 cT = act ? zh_chunk(F, T) : make_uint4(0, 0, 0, 0);
-    const uint4 cT1 = act ? zh_chunk(F, T - 1) : make_uint4(0, 0, 0, 0);
+    const uint4 cT = act ? zh_chunk(F, T, fs) : make_uint4(0, 0, 0, 0);
+    const uint4 cT1 = act ? zh_chunk(F, T - 1, fs) : make_uint4(0, 0, 0, 0);
     auto put = [&](int32_t c, const uint4& v) {  // (dwords: the ring is 4-byte aligned)
       uint32_t* q = rd + 4 * (c & 3);
       q[0] = v.x;
@@ -1705,14 +1729,15 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
       put(T - 1, cT1);
     }
     int32_t lowc = T - 1;
-    uint4 pf = act ? zh_chunk(F, T - 2) : make_uint4(0, 0, 0, 0);
+    uint4 pf = act ? zh_chunk(F, T - 2, fs) : make_uint4(0, 0, 0, 0);
     const uint32_t lb = (fs + sl - 1) & 15;
     const uint32_t lw = lb < 4 ? cT.x : lb < 8 ? cT.y : lb < 12 ? cT.z : cT.w;
     const uint32_t lastb = (lw >> (8 * (lb & 3))) & 0xFFu;
     bad = bad || (act && lastb == 0);
     act = act && lastb != 0;
-    int32_t bp = act ? int32_t(8 * (sl - 1) + (31 - __builtin_clz(lastb | 1u))) : 0;  // bits left
-    int32_t P = int32_t(8 * fs) + bp;  // frame-relative bit just above the next code
+    // P: the frame-relative bit just above the next code; the stream ends exactly at P0 = 8 fs
+    const int32_t P0 = int32_t(8 * fs);
+    int32_t P = act ? P0 + int32_t(8 * (sl - 1) + (31 - __builtin_clz(lastb | 1u))) : P0;
     int32_t clo = 0;
     uint64_t cv = 0;
     const uint32_t tmask = (1u << tl) - 1u;
@@ -1745,12 +1770,11 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
         if ((D >> 2) < lowc) {  // one chunk lower: commit the prefetched one, fetch the next
           lowc -= 1;
           put(lowc, pf);
-          pf = zh_chunk(F, lowc - 1);
+          pf = zh_chunk(F, lowc - 1, fs);
         }
         cv = uint64_t(rd[D & 15]) | (uint64_t(rd[(D + 1) & 15]) << 32);
       }
-      uint32_t v = uint32_t(cv >> uint32_t(P - int32_t(tl) - clo)) & tmask;
-      if (bp < int32_t(tl)) v = bp > 0 ? v & ~((1u << (int32_t(tl) - bp)) - 1u) : 0u;  // zeros below the stream
+      const uint32_t v = uint32_t(cv >> uint32_t(P - int32_t(tl) - clo)) & tmask;  // (zeros below the stream)
       const uint32_t e = tab[v];
       if (go) {
         const uint32_t q = (ph + i) & 15u;
@@ -1758,11 +1782,10 @@ __global__ __launch_bounds__(64) void zs_huf_stream_kernel(DecodeArgs a, ZsFastA
         sg0 |= q < 8 ? by : 0ull;
         sg1 |= q < 8 ? 0ull : by;
         if (q == 15 || i + 1 == m) flush(i);
-        bp -= int32_t(e >> 8);
         P -= int32_t(e >> 8);
       }
     }
-    bad = bad || (act && bp != 0);
+    bad = bad || (act && P != P0);
     // per block: any failing stream hands it back; else phase B builds it from the output slot
     const uint32_t bm = uint32_t(__ballot(bad) >> (4 * j)) & 15u;
     if (l == 0 && mine && (fl & kZfFast) && tl != 0) {
