@@ -1585,7 +1585,10 @@ static FilterOut build_filter_aux(slate_sst_builder* b, uint64_t n_hashes) {
     nb = bloom_filter_bytes(b->num_keys, b->cfg.filter_bits_per_key);
     if (nb * 8 == 0 || nb * 8 > 0xFFFFFFFFull) return fail(SLATE_E_INVALID_ARG);  // Go: divide by zero / uint32 bits
   }
-  auto hip = [&](hipError_t e) { return e == hipSuccess ? SLATE_OK : hip_status(e); };
+  auto hip = [&](hipError_t e) {
+    if (e != hipSuccess) fprintf(stderr, "[slate hip] %s in the filter job\n", hipGetErrorString(e));
+    return e == hipSuccess ? SLATE_OK : hip_status(e);
+  };
   int s = hip(ctx->x_words.ensure(((nb + 3) & ~uint64_t(3)) + 16));
   if (!s) s = hip(ctx->x_enc.ensure(nb + 2 + 16));
   const size_t bkt = nb ? bloom_bucket_scratch_bytes(n_hashes, f.np, uint32_t(nb * 8)) : 0;
@@ -2313,9 +2316,13 @@ int slate_block_reader_next(slate_block_reader* r, slate_block_view* view) {
   if (r->fed_end < r->nblocks && r->w1 <= r->w0) {
     ReaderSlot* fr = reader_free_slot(r);
     bool stop = false;
-    if (cur && cur->fast && !cur->synced && hipEventQuery(cur->done) == hipSuccess) {
-      int st = reader_sync(r, *cur);
-      if (st) return st;
+    if (cur && cur->fast && !cur->synced) {
+      if (hipEventQuery(cur->done) == hipSuccess) {
+        int st = reader_sync(r, *cur);
+        if (st) return st;
+      } else {
+        (void)hipGetLastError();  // (not ready is not an error: keep it out of the next launch's check)
+      }
     }
     if (cur && cur->synced && cur->fail != UINT64_MAX) stop = true;
     if (fr && fr != cur && !stop) {

@@ -391,7 +391,7 @@ struct GpuSpan {
   do {                                                                                                \
     hipError_t _e = (expr);                                                                           \
     if (_e != hipSuccess) {                                                                           \
-      if (host_trace()) fprintf(stderr, "[slate hip] %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+      fprintf(stderr, "[slate hip] %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__);               \
       return hip_status(_e);                                                                          \
     }                                                                                                 \
   } while (0)
