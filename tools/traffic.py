@@ -28,7 +28,8 @@ def main():
     # the kernels of one decode launch (configs[4] Zstd: the fast-path phases and the exact path
     # over the blocks they hand back; the plan kernels run outside the timed region)
     kernels = {"snappy": ["decode_lpb2_kernel"], "none": ["decode_none_kernel"],
-               "zstd": ["zs_fast_parse_kernel", "zs_fse_parse_kernel", "zs_fast_crc_kernel", "zs_fast_build_kernel", "zs_fast_huf_kernel",
+               "zstd": ["zs_fast_parse_kernel", "zs_fse_parse_kernel", "zs_fast_crc_kernel", "zs_huf_tree_lanes_kernel",
+                        "zs_huf_tree_kernel", "zs_huf_stream_kernel", "zs_fast_build_kernel", "zs_fast_huf_kernel",
                         "zs_fast_sum_kernel", "decode_list_kernel", "decode_large_kernel"]}[codec]
     kernel = "+".join(kernels)
     fetch_kib = write_kib = 0.0
