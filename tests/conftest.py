@@ -42,3 +42,14 @@ def _torch_hip_first(request):
         except ImportError:
             pass
     yield
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _free_contexts_between_modules():
+    """Each GPU module makes its own contexts, and each context holds page-locked staging (the
+    host-decode lanes' pieces, reader slots): collect the module's objects when it ends, so that
+    one module's page-locked memory is released before the next one allocates its own (a context
+    kept alive by a reference cycle until some later collection would otherwise hold it)."""
+    yield
+    import gc
+    gc.collect()
