@@ -470,10 +470,18 @@ __device__ __forceinline__ void load_j(uint32_t lane, uint32_t info, uint32_t re
 
 // Start of an iteration, part 2: how many chunks this block asks for (ring room and
 // payload end permitting), then four transposed loads fetch them for the whole wave.
+// A block asks only when it can take four chunks (or its last ones): every refill is a 64-byte run,
+// where asking for whatever was free gave runs of 1-4 chunks -- the same bytes in ~twice the runs,
+// and the address unit's time goes by runs (round 6, same-box A/B of SLATE_LPB_REFILL_MIN = 1..4,
+// profiling variants, 1 M blocks: 4.230 / 4.150 / 4.138 / 4.130 ms, profiles/round6/ab/)
+#ifndef SLATE_LPB_REFILL_MIN
+#define SLATE_LPB_REFILL_MIN 4
+#endif
 __device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, uint32_t c_issue, uint32_t last_chunk) {
   const uint32_t room = lo_chunk + kNS - c_issue;
   const uint32_t left = last_chunk + 1 - c_issue;
-  return act ? min(min(room, left), 4u) : 0u;
+  const uint32_t n = min(min(room, left), 4u);
+  return (act && (n >= SLATE_LPB_REFILL_MIN || n == left)) ? n : 0u;
 }
 
 // Start of an iteration, after the refill: the hole source loaded at the end of the previous
