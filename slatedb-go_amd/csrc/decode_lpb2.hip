@@ -470,18 +470,31 @@ __device__ __forceinline__ void load_j(uint32_t lane, uint32_t info, uint32_t re
 
 // Start of an iteration, part 2: how many chunks this block asks for (ring room and
 // payload end permitting), then four transposed loads fetch them for the whole wave.
-// A block asks only when it can take four chunks (or its last ones): every refill is a 64-byte run,
-// where asking for whatever was free gave runs of 1-4 chunks -- the same bytes in ~twice the runs,
-// and the address unit's time goes by runs (round 6, same-box A/B of SLATE_LPB_REFILL_MIN = 1..4,
-// profiling variants, 1 M blocks: 4.230 / 4.150 / 4.138 / 4.130 ms, profiles/round6/ab/)
+// A block asks only for a whole 64-byte segment of the payload's address (its first and last
+// segments excepted): a refill is one run that never straddles a cache line.  Asking for whatever
+// was free gave runs of 1-4 chunks at any alignment -- the same bytes in ~twice the runs, and the
+// address unit's time goes by runs and lines (round 6, same-box A/Bs on profiling variants, 1 M
+// blocks: REFILL_MIN = 1..4 4.230 / 4.150 / 4.138 / 4.130 ms; aligned segments 4.053 ms,
+// profiles/round6/ab/).  SLATE_LPB_REFILL_ALIGN=0 restores the unaligned minimum-run rule.
 #ifndef SLATE_LPB_REFILL_MIN
 #define SLATE_LPB_REFILL_MIN 4
 #endif
-__device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, uint32_t c_issue, uint32_t last_chunk) {
+#ifndef SLATE_LPB_REFILL_ALIGN
+#define SLATE_LPB_REFILL_ALIGN 1
+#endif
+__device__ __forceinline__ uint32_t refill_count(bool act, uint32_t lo_chunk, uint32_t c_issue, uint32_t last_chunk,
+                                                 uint32_t phase) {
   const uint32_t room = lo_chunk + kNS - c_issue;
   const uint32_t left = last_chunk + 1 - c_issue;
+#if SLATE_LPB_REFILL_ALIGN
+  // runs end on 64-byte boundaries of the payload's address (phase = the first chunk's slot in its
+  // 64-byte line), so no run straddles a cache line
+  const uint32_t seg = min(4u - ((phase + c_issue) & 3u), left);
+  return (act && room >= seg) ? seg : 0u;
+#else
   const uint32_t n = min(min(room, left), 4u);
   return (act && (n >= SLATE_LPB_REFILL_MIN || n == left)) ? n : 0u;
+#endif
 }
 
 // Start of an iteration, after the refill: the hole source loaded at the end of the previous
@@ -816,10 +829,27 @@ __device__ __forceinline__ void lane_step(Lane& L, bool act, uint64_t mact, uint
 // The chunks are written transposed: in store j, lanes 4i..4i+3 write chunks 0..3 of the
 // block of lane 16j+i, so every store instruction writes 16 runs of 64 contiguous bytes
 // instead of 64 scattered 16-byte pieces (tools/scatter_probe.hip: ~3.5x cheaper).
+// The same for the output: until a block's decode is done its flush run ends at the last 64-byte
+// boundary of the output's address it reaches, so the stores are whole 64-byte segments (round 6,
+// same-box A/B with aligned refills: 4.053 ms -> 3.790 ms at 4-chunk segments, 3.840 ms at 8;
+// profiles/round6/ab/).  The throttle (lim_d) holds the ring's bound whatever the flush keeps back.
+#ifndef SLATE_LPB_FLUSH_SEG
+#define SLATE_LPB_FLUSH_SEG 4
+#endif
 __device__ __forceinline__ void flush_iteration(Lane& L, bool act, uint8_t* outs, uint32_t lane, const Rsrc& R,
-                                                uint32_t dbg, uint32_t part, uint32_t flush_lane) {
+                                                uint32_t dbg, uint32_t part, uint32_t flush_lane, uint32_t ophase) {
   const bool mine = kFlushParts == 1 || (lane / kFlushBlocks) == part;
-  const uint32_t done = (act && mine) ? min(L.d >> 4, msel(L.mhp, L.hd >> 4, 0xFFFFFFFFu)) - L.fl : 0u;
+  uint32_t done = (act && mine) ? min(L.d >> 4, msel(L.mhp, L.hd >> 4, 0xFFFFFFFFu)) - L.fl : 0u;
+#if SLATE_LPB_FLUSH_SEG > 1
+  // until the block's decode is done, a run stops at the last SLATE_LPB_FLUSH_SEG-chunk boundary
+  // of the output's address it reaches (the chunks after it wait for the next flush)
+  {
+    const uint32_t n = min(done, kRun), keep = (ophase + L.fl + n) & (SLATE_LPB_FLUSH_SEG - 1);
+    done = msel(L.mdd, done, n > keep ? n - keep : 0u);
+  }
+#else
+  (void)ophase;
+#endif
   const uint32_t base = L.out_rel + 16 * L.fl;       // where this lane's next chunk goes
   const uint32_t info = (done << 7) | ((L.fl * 16) & (kOR - 1)) >> 4;  // count | ring slot of fl
   // the served block's ring: flush_lane (the kernel's constant for part 0, store 0) + the part's and
@@ -1050,6 +1080,8 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
                    rel2 = __shfl(L.in_rel, int(32 + (lane >> 2)), 64), rel3 = __shfl(L.in_rel, int(48 + (lane >> 2)), 64);
     // ---------------- streaming decode, 64 blocks in lockstep
     uint32_t iters = 0, fin_iter = 0;
+    const uint32_t phase = uint32_t((reinterpret_cast<uintptr_t>(in_base) >> 4) + (L.in_rel >> 4)) & 3u;
+    const uint32_t ophase = uint32_t((reinterpret_cast<uintptr_t>(out_base) >> 4) + (L.out_rel >> 4)) & 7u;
     const uint64_t t_round = (dbg_bits(a) & 512) ? __builtin_amdgcn_s_memtime() : 0;
     // a lane is done when its decode is finished, no hole is pending, and every chunk
     // is committed and in the CRC.  Every step consumes input, produces output or waits
@@ -1073,7 +1105,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
         // the ring keeps every chunk from the oldest byte still to be read or CRC'd
         const uint32_t lo_pos = msel(L.mdd, L.sh + L.clen, msel(L.mlit & bal(L.rem != 0), L.src, L.sh + L.s));
         const uint32_t lo_chunk = min(lo_pos >> 4, L.crc_pos);
-        const uint32_t n = refill_count(act, lo_chunk, L.c_issue, L.last_chunk);
+        const uint32_t n = refill_count(act, lo_chunk, L.c_issue, L.last_chunk, phase);
         const uint32_t info = (L.c_issue << 3) | n;
         load_j<0>(lane, info, rel0, R, P0, S0);
         load_j<1>(lane, info, rel1, R, P1, S1);
@@ -1096,7 +1128,7 @@ __global__ __launch_bounds__(kLpb2Threads) void decode_lpb2_kernel(DecodeArgs a,
       LPB_MARK(flush);
       Q = __builtin_amdgcn_raw_buffer_load_b128(R.out, (dbg_bits(a) & 32768) ? kOOB : L.qoff, 0, 16);
       L.qoff = kOOB;
-      flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts, flush_lane);
+      flush_iteration(L, act, outs, lane, R, dbg_bits(a), iters % kFlushParts, flush_lane, ophase);
       if constexpr (kLz4) {
         // the content checksum's stripes: the chunks completed so far (up to kStep / 4), still in the ring
 #pragma unroll
@@ -1401,7 +1433,8 @@ __global__ __launch_bounds__(kLz4PlanThreads) void plan_lz4_lane_kernel(const ui
       commit_one(smem, S3, P3, z);
       c_commit += n_req;
       const uint32_t lo_chunk = (sh + min(s, tail)) >> 4;
-      const uint32_t nq = refill_count(act, lo_chunk, c_issue, last_chunk);
+      const uint32_t nq = refill_count(act, lo_chunk, c_issue, last_chunk,
+                                        uint32_t((reinterpret_cast<uintptr_t>(in_base) >> 4) + (rel >> 4)) & 3u);
       const uint32_t info = (c_issue << 3) | nq;
       load_one(0, lane, wave_lane0, info, rel, R, P0, S0);
       load_one(1, lane, wave_lane0, info, rel, R, P1, S1);
