@@ -84,9 +84,8 @@ int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st
   return SLATE_OK;
 }
 
-int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st) {
+static int d2h_pipe(PipeLane* lanes, void* dst, const void* src, size_t n, hipStream_t st) {
   if (n == 0) return SLATE_OK;
-  PoolScope pool(ctx);
   if (n <= kXferDirect) {
     SLATE_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
     SLATE_HIP(hipStreamSynchronize(st));
@@ -94,7 +93,7 @@ int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st
   }
   const size_t pieces = (n + kXferPiece - 1) / kXferPiece;
   auto issue = [&](size_t k) -> hipError_t {
-    PipeLane& L = ctx->lanes[k % kPipeLanes];
+    PipeLane& L = lanes[k % kPipeLanes];
     hipError_t e = lane_init(L);
     if (e == hipSuccess) e = L.h_in.ensure(kXferPiece);
     const size_t o = k * kXferPiece, len = std::min(kXferPiece, n - o);
@@ -105,12 +104,29 @@ int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st
   SLATE_HIP(issue(0));
   for (size_t k = 0; k < pieces; k++) {
     if (k + 1 < pieces) SLATE_HIP(issue(k + 1));  // the next piece moves while this one is copied out
-    PipeLane& L = ctx->lanes[k % kPipeLanes];
+    PipeLane& L = lanes[k % kPipeLanes];
     SLATE_HIP(hipEventSynchronize(L.planned));
     const size_t o = k * kXferPiece, len = std::min(kXferPiece, n - o);
     par_memcpy(static_cast<uint8_t*>(dst) + o, L.h_in.p, len);
   }
   return SLATE_OK;
+}
+
+int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st) {
+  PoolScope pool(ctx);
+  return d2h_pipe(ctx->lanes, dst, src, n, st);
+}
+
+int ctx_d2h_side(slate_ctx* ctx, void* dst, const void* src, size_t n, hipEvent_t after) {
+  SLATE_HIP(ctx_bind(ctx));
+  PipeLane& L0 = ctx->d2h_lanes[0];
+  SLATE_HIP(lane_init(L0));
+  SLATE_HIP(lane_init(ctx->d2h_lanes[1]));
+  SLATE_HIP(hipStreamWaitEvent(L0.stream, after, 0));
+  // half the context's copy threads: the caller's thread keeps the pool for its uploads
+  if (!ctx->d2h_pool) ctx->d2h_pool.reset(new CopyPool(std::max<size_t>(1, ctx->copy_threads / 2)));
+  PoolScope pool(ctx->d2h_pool.get());
+  return d2h_pipe(ctx->d2h_lanes, dst, src, n, L0.stream);
 }
 
 namespace {

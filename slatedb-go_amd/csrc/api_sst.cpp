@@ -934,7 +934,10 @@ int ctx_payload_decode_buffer(slate_ctx* ctx, int codec, const uint8_t* buf, siz
 void SegPool::close() {
   std::lock_guard<std::mutex> g(mu);
   open = false;
-  for (auto& f : free_list) munmap(f.first, f.second);
+  for (auto& f : free_list) {
+    if (f.pinned) (void)hipHostUnregister(f.p);
+    munmap(f.p, f.cap);
+  }
   free_list.clear();
 }
 
@@ -946,10 +949,10 @@ void SegPool::close() {
 struct HostBytes {
   uint8_t* p = nullptr;
   size_t n = 0, cap = 0;
-  bool mapped = false;
+  bool mapped = false, pinned = false;
   std::shared_ptr<SegPool> pool;
   explicit HostBytes(size_t len, std::shared_ptr<SegPool> pl = nullptr) : n(len), pool(std::move(pl)) {
-    if (pool && pool->take(len, &p, &cap)) {
+    if (pool && pool->take(len, &p, &cap, &pinned)) {
       mapped = true;
       return;
     }
@@ -968,10 +971,17 @@ struct HostBytes {
     if (!p) cap = 0;  // callers check ok(): a host OOM becomes SLATE_E_OOM, not a fault
   }
   bool ok() const { return p != nullptr; }
+  // a pooled mapping registered once (kept registered in the pool): the GPU writes it directly
+  bool pin() {
+    if (!pinned && mapped && pool) pinned = hipHostRegister(p, cap, hipHostRegisterDefault) == hipSuccess;
+    if (!pinned) (void)hipGetLastError();
+    return pinned;
+  }
   ~HostBytes() {
     if (!mapped) {
       free(p);
-    } else if (!pool || !pool->give(p, cap)) {
+    } else if (!pool || !pool->give(p, cap, pinned)) {
+      if (pinned) (void)hipHostUnregister(p);
       munmap(p, cap);
     }
   }
@@ -1030,7 +1040,17 @@ struct slate_sst_builder {
   ByteView last_block;    // the final block (Build keeps it in the last chunk)
   int sticky = SLATE_OK;
   bool built = false;
+  // a non-final flush's blocks on their way to the host (ctx_d2h_side on a worker thread): joined
+  // before anything reads them or the device buffers they come from (builder_join_d2h)
+  std::future<int> d2h_job;
 };
+
+static int builder_join_d2h(slate_sst_builder* b) {
+  if (!b->d2h_job.valid()) return SLATE_OK;
+  const int s = b->d2h_job.get();
+  if (s && !b->sticky) b->sticky = s;
+  return s;
+}
 
 // Append n KVs (offsets relative to their byte arrays, key_off[0] / value_off[0] need not be 0)
 // to the device-resident pending set.  dev: the arrays are device pointers.  tomb may be null
@@ -1100,10 +1120,17 @@ static int pending_push_host(slate_sst_builder* b) {
   return st;
 }
 
+// async_d2h (non-final flushes of a chunked host batch, slate_sst_builder_add_batch): the finished
+// blocks leave through the context's second download pipe on a worker thread, and the call returns
+// once they are packed, so the caller's next upload overlaps their transfer.
 static int builder_flush(slate_sst_builder* b, bool final, const std::function<void(uint64_t)>* after_hashes = nullptr,
-                         const std::function<void()>* after_meta = nullptr) {
+                         const std::function<void()>* after_meta = nullptr, bool async_d2h = false) {
   slate_ctx* ctx = b->ctx;
   hipStream_t st = ctx->stream;
+  {
+    const int js = builder_join_d2h(b);  // (the pack below rewrites the buffer it reads)
+    if (js) return js;
+  }
   int pst = pending_push_host(b);
   if (pst) return pst;
   const uint64_t n64 = b->n_pend;
@@ -1212,6 +1239,41 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     if (final && after_meta) (*after_meta)();
   };
   std::shared_ptr<HostBytes> seg;
+  static const bool pin_segs = [] {  // SLATE_PIN_SEGS=0: blocks through the staging pipe (A/B runs)
+    const char* e = getenv("SLATE_PIN_SEGS");
+    return !(e && *e == '0');
+  }();
+  auto blocks_d2h = [&](const std::shared_ptr<HostBytes>& sg, const void* src, size_t len) -> int {
+    if (len >= (8u << 20) && pin_segs && sg->pin()) {
+      // straight into the registered segment: no staging copy on the host's cores (they are busy
+      // with the next piece's upload); async: the caller joins the copy's event
+      if (!async_d2h || final) {
+        SLATE_HIP(hipMemcpyAsync(sg->p, src, len, hipMemcpyDeviceToHost, st));
+        SLATE_HIP(hipStreamSynchronize(st));
+        return SLATE_OK;
+      }
+      if (!ctx->d2h_after) SLATE_HIP(hipEventCreateWithFlags(&ctx->d2h_after, hipEventDisableTiming));
+      SLATE_HIP(hipEventRecord(ctx->d2h_after, st));
+      b->d2h_job = std::async(std::launch::async, [ctx, sg, src, len]() -> int {
+        SLATE_HIP(ctx_bind(ctx));
+        PipeLane& L0 = ctx->d2h_lanes[0];
+        SLATE_HIP(lane_init(L0));
+        SLATE_HIP(hipStreamWaitEvent(L0.stream, ctx->d2h_after, 0));
+        SLATE_HIP(hipMemcpyAsync(sg->p, src, len, hipMemcpyDeviceToHost, L0.stream));
+        SLATE_HIP(hipStreamSynchronize(L0.stream));
+        return SLATE_OK;
+      });
+      return SLATE_OK;
+    }
+    if (!async_d2h || final || len == 0) return ctx_d2h(ctx, sg->p, src, len, st);
+    if (!ctx->d2h_after) SLATE_HIP(hipEventCreateWithFlags(&ctx->d2h_after, hipEventDisableTiming));
+    SLATE_HIP(hipEventRecord(ctx->d2h_after, st));
+    // (the job holds the segment; src stays valid until the join at the next flush)
+    b->d2h_job = std::async(std::launch::async, [ctx, sg, src, len] {
+      return ctx_d2h_side(ctx, sg->p, src, len, ctx->d2h_after);
+    });
+    return SLATE_OK;
+  };
   if (nb && b->cfg.codec == SLATE_CODEC_SNAPPY) {
     // raw sizes -> per-block slots; golang/snappy + CRC per block; scan of the
     // compressed sizes; compaction into back-to-back blocks
@@ -1255,7 +1317,7 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     seg = std::make_shared<HostBytes>(out_off[nb], ctx->seg_pool);
     if (!seg->ok()) return SLATE_E_OOM;
     queue_meta(out_off);
-    int s = ctx_d2h(ctx, seg->p, ctx->e_e.p, out_off[nb], st);
+    int s = blocks_d2h(seg, ctx->e_e.p, out_off[nb]);
     mark("blocks D2H");
     if (s) return s;
   } else if (nb) {
@@ -1287,7 +1349,7 @@ static int builder_flush(slate_sst_builder* b, bool final, const std::function<v
     seg = std::make_shared<HostBytes>(out_off[nb], ctx->seg_pool);
     if (!seg->ok()) return SLATE_E_OOM;
     queue_meta(out_off);
-    int s = ctx_d2h(ctx, seg->p, src, out_off[nb], st);
+    int s = blocks_d2h(seg, src, out_off[nb]);
     mark("blocks D2H");
     if (s) return s;
   }
@@ -1364,6 +1426,7 @@ slate_sst_builder* slate_sst_builder_new(slate_ctx* ctx, const slate_sst_config*
 
 void slate_sst_builder_free(slate_sst_builder* b) {
   if (!b) return;
+  (void)builder_join_d2h(b);
   (void)hipSetDevice(b->ctx->device);
   for (DevBuf* d : {&b->d_hashes, &b->d_keys, &b->d_vals, &b->d_koff, &b->d_voff, &b->d_tomb, &b->d_tmp})
     d->release();
@@ -1423,13 +1486,37 @@ int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const
   if (b->built) return SLATE_E_INVALID_ARG;
   if (n == 0) return SLATE_OK;
   // the same effect as n calls of slate_sst_builder_add, up to the first empty key
-  // (block.go:163), which fails; a tombstone's value bytes are not kept
-  uint64_t m = 0, lower = 0;
-  while (m < n && key_off[m + 1] > key_off[m]) {
-    const bool tomb = is_tomb ? is_tomb[m] != 0 : value_off[m + 1] == value_off[m];
-    const uint64_t vl = value_off[m + 1] - value_off[m];
-    lower += 2 + 13 + (tomb ? 0 : 4 + vl);
-    m++;
+  // (block.go:163), which fails; a tombstone's value bytes are not kept.  The scan for that key and
+  // the encoded size's lower bound runs in pieces on the context's copy threads (one core takes
+  // ~10 ms over 10 M offsets, all of it before the upload starts): piece k stops at its first
+  // empty key, and the first piece that stopped early sets m.
+  uint64_t m = n, lower = 0;
+  {
+    const size_t T = n >= (1u << 20) ? std::min<size_t>(b->ctx->pool()->size(), 64) : 1;
+    std::vector<uint64_t> stop(T), part(T);
+    auto piece = [&](size_t k) {
+      const uint64_t lo = n * k / T, hi = n * (k + 1) / T;
+      uint64_t i = lo, low = 0;
+      for (; i < hi && key_off[i + 1] > key_off[i]; i++) {
+        const uint64_t vl = value_off[i + 1] - value_off[i];
+        const bool tomb = is_tomb ? is_tomb[i] != 0 : vl == 0;
+        low += 2 + 13 + (tomb ? 0 : 4 + vl);
+      }
+      stop[k] = i;
+      part[k] = low;
+    };
+    if (T == 1) {
+      piece(0);
+    } else {
+      b->ctx->pool()->run(T, piece);
+    }
+    for (size_t k = 0; k < T; k++) {
+      lower += part[k];
+      if (stop[k] < n * (k + 1) / T) {
+        m = stop[k];
+        break;
+      }
+    }
   }
   if (m) {
     b->track = false;
@@ -1452,10 +1539,43 @@ int slate_sst_builder_add_batch(slate_sst_builder* b, const uint8_t* keys, const
       b->first_key.assign(keys + key_off[0], keys + key_off[1]);
       b->has_first_key = true;
     }
-    st = pending_append(b, keys, key_off, values, value_off, is_tomb, m, false, key_off[0], key_off[m], value_off[0],
-                        value_off[m]);
-    if (st) return b->sticky = st;
-    b->pending_lower += lower;
+    // SLATE_ADD_PIECE (KVs per piece; unset or 0 = one piece): a large batch goes up in pieces, each
+    // followed by a flush of the blocks it finished, whose download (the context's second pipe, a
+    // worker thread) overlaps the next piece's upload; the last piece stays pending for Build's
+    // final flush.  Off by default: on the MI355X boxes the two directions at once ran slower than
+    // one after the other (10 M KV CodecNone: add 25 -> 53-56 ms for build 33 -> 19-22 ms;
+    // profiles/round6/ab/ab_encode_pieces_pin.txt).  (read per call: tests set it)
+    const char* piece_env = getenv("SLATE_ADD_PIECE");
+    const uint64_t piece_kv = piece_env ? uint64_t(strtoull(piece_env, nullptr, 10)) : uint64_t(0);
+    const bool pieces = piece_kv && m >= 2 * piece_kv &&
+                        (b->cfg.codec == SLATE_CODEC_NONE || b->cfg.codec == SLATE_CODEC_SNAPPY);
+    const uint64_t np = pieces ? (m + piece_kv - 1) / piece_kv : 1;
+    for (uint64_t k = 0; k < np; k++) {
+      const uint64_t a = m * k / np, e = m * (k + 1) / np;
+      st = pending_append(b, keys, key_off + a, values, value_off + a, is_tomb ? is_tomb + a : nullptr, e - a, false,
+                          key_off[a], key_off[e], value_off[a], value_off[e]);
+      if (st) {
+        (void)builder_join_d2h(b);
+        return b->sticky = st;
+      }
+      if (k + 1 < np) {
+        st = builder_flush(b, false, nullptr, nullptr, true);  // (it resets pending_lower to its remainder)
+        if (st) {
+          (void)builder_join_d2h(b);
+          return b->sticky = st;
+        }
+      }
+    }
+    st = builder_join_d2h(b);
+    if (st) return st;
+    if (np > 1) {
+      // the last piece's lower bound without a second scan: 15 bytes per row, plus the value bytes
+      // when no tombstone flags are given (an empty value is then the only tombstone)
+      const uint64_t a = m * (np - 1) / np;
+      b->pending_lower += 15 * (m - a) + (is_tomb ? 0 : value_off[m] - value_off[a]);
+    } else {
+      b->pending_lower += lower;
+    }
   }
   return m == n ? SLATE_OK : SLATE_E_INVALID_ARG;
 }
@@ -1503,6 +1623,7 @@ int slate_sst_builder_add_batch_device(slate_sst_builder* b, const uint8_t* d_ke
 int slate_sst_builder_next_block(slate_sst_builder* b, uint8_t* out, size_t out_cap, size_t* len, int* present) {
   if (!b || !present) return SLATE_E_INVALID_ARG;
   *present = 0;
+  (void)builder_join_d2h(b);
   if (b->sticky) return b->sticky;
   // A finished block exists only once the pending KVs overflow one block: single adds know exactly
   // when Go finished one (the replayed block.Builder); after batch adds, the lower bound avoids a

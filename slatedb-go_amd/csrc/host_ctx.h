@@ -159,27 +159,33 @@ constexpr int kPipeLanes = 2;
 // of them and the context goes last.
 constexpr size_t kSegHuge = 2u << 20;
 struct SegPool {
+  struct Seg {
+    void* p;
+    size_t cap;
+    bool pinned;  // registered with the runtime (hipHostRegister): the blocks' D2H lands in it directly
+  };
   std::mutex mu;
-  std::vector<std::pair<void*, size_t>> free_list;
+  std::vector<Seg> free_list;
   bool open = true;
-  static constexpr size_t kKeep = 4;
-  bool take(size_t len, uint8_t** p, size_t* cap) {
+  static constexpr size_t kKeep = 8;  // (a build in pieces releases five: four block segments, the final chunk)
+  bool take(size_t len, uint8_t** p, size_t* cap, bool* pinned) {
     std::lock_guard<std::mutex> g(mu);
     size_t best = free_list.size();
     for (size_t i = 0; i < free_list.size(); i++)
-      if (free_list[i].second >= len && free_list[i].second <= 2 * len + kSegHuge &&
-          (best == free_list.size() || free_list[i].second < free_list[best].second))
+      if (free_list[i].cap >= len && free_list[i].cap <= 2 * len + kSegHuge &&
+          (best == free_list.size() || free_list[i].cap < free_list[best].cap))
         best = i;
     if (best == free_list.size()) return false;
-    *p = static_cast<uint8_t*>(free_list[best].first);
-    *cap = free_list[best].second;
+    *p = static_cast<uint8_t*>(free_list[best].p);
+    *cap = free_list[best].cap;
+    *pinned = free_list[best].pinned;
     free_list.erase(free_list.begin() + long(best));
     return true;
   }
-  bool give(void* p, size_t cap) {  // false: the caller unmaps it
+  bool give(void* p, size_t cap, bool pinned) {  // false: the caller unmaps it
     std::lock_guard<std::mutex> g(mu);
     if (!open || free_list.size() >= kKeep) return false;
-    free_list.emplace_back(p, cap);
+    free_list.push_back(Seg{p, cap, pinned});
     return true;
   }
   void close();  // unmaps the kept buffers (api_sst.cpp)
@@ -259,6 +265,11 @@ struct slate_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   PipeLane lanes[kPipeLanes];
+  // a second download pipe (ctx_d2h_side): its own stream, page-locked pieces and copy threads, so
+  // that a builder's finished blocks leave while the caller's thread uploads the next KVs
+  PipeLane d2h_lanes[kPipeLanes];
+  hipEvent_t d2h_after = nullptr;
+  std::unique_ptr<CopyPool> d2h_pool;
   PinBuf h_small;  // single-block staging (slate_block_decode)
   PinBuf h_seek;   // slate_block_seek(_warn) inputs (one upload) and results (written by the kernel)
   // decode batch buffers
@@ -343,6 +354,9 @@ struct slate_ctx {
     if (t_ref) (void)hipEventDestroy(t_ref);
     t_ref = nullptr;
     for (PipeLane& l : lanes) l.release();
+    for (PipeLane& l : d2h_lanes) l.release();
+    if (d2h_after) (void)hipEventDestroy(d2h_after);
+    d2h_after = nullptr;
     h_small.release();
     h_seek.release();
   }
@@ -443,6 +457,9 @@ bool host_plannable(int codec);
 uint64_t host_decoded_len(int codec, const uint8_t* p, uint64_t len);
 int ctx_h2d(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st);
 int ctx_d2h(slate_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t st);
+// ctx_d2h through the context's second download pipe, after `after` (an event recorded on the
+// stream that produced src); for a worker thread while the caller's thread runs ctx_h2d
+int ctx_d2h_side(slate_ctx* ctx, void* dst, const void* src, size_t n, hipEvent_t after);
 
 // compress.Decode of one `payload || BE32 CRC` buffer (an index or filter) on the GPU, CRC
 // first: *bstatus = SLATE_OK, SLATE_E_BLOCK_CHECKSUM or the codec's status (api_sst.cpp).

@@ -132,6 +132,41 @@ def test_next_block_after_each_add(sc, ctx, seed):
     assert g.build().encode() == (o.build(), o.encode_table())[1]
 
 
+@pytest.mark.parametrize("codec", [ob.NONE, ob.SNAPPY])
+@pytest.mark.parametrize("seed", range(3))
+def test_batch_in_pieces(sc, ctx, monkeypatch, codec, seed):
+    """slate_sst_builder_add_batch in pieces (SLATE_ADD_PIECE KVs each, a flush after every piece but
+    the last, its blocks downloaded on the context's second pipe while the next piece uploads): the
+    SST, its chunks, info and bloom equal the oracle's, as do the blocks NextBlock hands out after
+    the batch and after a second batch (tombstones by empty values and by flags)."""
+    rng = random.Random(300 + seed)
+    kvs = bg.random_kvs(rng, rng.randint(3000, 6000), alphabet=rng.choice([3, 256]), tomb_p=0.1)
+    bs = rng.choice([256, 1024, 4096])
+    monkeypatch.setenv("SLATE_ADD_PIECE", str(rng.choice([500, 900, 1500])))
+    half = len(kvs) // 2
+    g = sc.SstBuilder(ctx, bs, 0, 10, codec)
+    o = ob.SstBuilder(bs, 0, 10, codec)
+    for part, flags in ((kvs[:half], False), (kvs[half:], True)):
+        kd, ko = sc._arena([k for k, _ in part])
+        vd, vo = sc._arena([v for _, v in part])
+        tomb = np.array([1 if not v else 0 for _, v in part], np.uint8) if flags else None
+        assert g.add_batch(kd, ko, vd, vo, tomb) == 0
+        for k, v in part:
+            assert o.add_value(k, v) == 0
+        gb, obl = [], []
+        while (b := g.next_block()) is not None:
+            gb.append(b)
+        while (b := o.next_block()) is not None:
+            obl.append(b)
+        assert gb == obl
+    t = g.build()
+    assert o.build() == 0
+    assert t.chunks() == o.chunks()
+    assert t.encode() == o.encode_table()
+    assert t.info() == o.info()
+    assert t.bloom() == o.bloom()
+
+
 def test_unsorted_and_duplicate_keys(sc, ctx):
     rng = random.Random(9)
     kvs = [(bytes(rng.randrange(3) for _ in range(rng.randint(1, 6))), b"v" * rng.randint(0, 40)) for _ in range(800)]
