@@ -51,6 +51,9 @@ constexpr int kNoneLdpol = SLATE_NONE_LDPOL;
 // stores drain while the tree's dependent lookups run (round 6).  A block whose CRC then fails has
 // its meta say so; its output slot's bytes are unspecified, as Go sets no Block.Data on an error
 // (block.go:85-88) and the parity tests compare bytes only of blocks that decoded.
+#ifndef SLATE_NONE_ALIGN_LOADS
+#define SLATE_NONE_ALIGN_LOADS 0
+#endif
 #ifndef SLATE_NONE_EARLY_STORE
 #define SLATE_NONE_EARLY_STORE 1
 #endif
@@ -137,6 +140,14 @@ __device__ __forceinline__ Geo geo_of(const DecodeArgs& a, uint32_t b) {
   g.nout = (g.clen + 15) / 16;
   g.pad = kNoneSlots - g.nout;
   g.pin = kNoneSlots - 1 - ((g.sh + g.clen + 3) >> 4);  // (kind 0: <= 319 - (nout - 1) - 2)
+#if SLATE_NONE_ALIGN_LOADS
+  // up to three slots earlier, so that every load instruction's 1 KiB starts on a 64-byte boundary of
+  // the address (16 segments, not 17); the stage only moves with it
+  {
+    const uint32_t d = (g.pin - uint32_t(reinterpret_cast<uintptr_t>(g.base) >> 4)) & 3u;
+    g.pin -= g.pin >= d ? d : 0u;
+  }
+#endif
   return g;
 }
 
