@@ -13,7 +13,7 @@ for f in build/*.o; do
   b=$(basename $f)
   case $b in
     decode_lpb2.hip.o|decode.hip.o|decode_none.hip.o|zstd_fast.hip.o|api_sst.cpp.o|encode.hip.o|encode_codecs.hip.o)
-      extra=""; [ $b = decode_lpb2.hip.o ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"  # as the Makefile
+      extra=""; [ $b = decode_lpb2.hip.o ] && extra="${LPB_SCHED--mllvm -amdgpu-sched-strategy=max-ilp}"  # as the Makefile (LPB_SCHED overrides)
       /opt/rocm/bin/hipcc $HIPFLAGS $extra $FLAGS -c csrc/${b%.o} -o build/var_$TAG/$b; objs="$objs build/var_$TAG/$b";;
     *) objs="$objs $f";;
   esac
