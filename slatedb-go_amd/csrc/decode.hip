@@ -2274,7 +2274,7 @@ hipError_t launch_decode(hipStream_t st, const DecodeArgs& args_in, void* scratc
     decode_large_kernel<1><<<uint32_t(num_cus), 64, lds_large, st>>>(a);
   } else if (a.codec == SLATE_CODEC_ZSTD) {
     // the fast path (zstd_fast.hip), then the exact path over the blocks it handed back
-    (void)hipMemsetAsync(s.zf.count, 0, 3 * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(s.zf.count, 0, 4 * sizeof(uint32_t), st);
     hipError_t e = launch_zstd_fast(st, a, s.zf, num_cus);
     if (e != hipSuccess) return e;
     decode_list_kernel<2><<<grid, kDecodeThreads, lds, st>>>(a, s.zf.list, s.zf.count);

@@ -95,6 +95,9 @@ constexpr uint32_t kZfFast = 1, kZfRle = 2, kZfSum = 4, kZfHuf = 8, kZfHuf4 = 16
 // CodecZlib blocks through the same build phase (zlib_fast.hip): the literal bytes are at the start
 // of the block's output slot, not in the frame; want is the stream's Adler-32, checked in phase B
 constexpr uint32_t kZfOutLit = 64, kZfAdler = 128;
+// set with kZfHuf by phase A and never cleared (H2 clears kZfHuf once it has placed the literals):
+// the main stream's phase B skips these blocks whatever H2 has done so far
+constexpr uint32_t kZfHufOrig = 256;
 struct ZsFastRec {
   uint32_t lit;       // frame offset of the raw literals, or the RLE literal byte
   uint32_t nlit;      // literal bytes
@@ -120,6 +123,13 @@ struct ZsFastArgs {
   uint8_t* htab = nullptr;
   uint32_t* hdesc = nullptr;
   uint32_t hcap = 0;
+  // phase B: blist != nullptr builds only blist[k] for k < min(count[1], hcap) (the Huffman-literal
+  // blocks phase H2 prepared); skip_hufo skips every kZfHufOrig block (they are the list's)
+  const uint32_t* blist = nullptr;
+  uint32_t skip_hufo = 0;
+  // phase B draws its blocks `draw` at a time from count[3] (zeroed with the others) instead of a
+  // static stride: workgroups that start late (CUs held by H1 / H2) take fewer
+  uint32_t draw = 0;
 };
 constexpr uint32_t kZhTab = 4096;  // a Huffman decoding table: 2^11 16-bit entries
 // hlist entries with an H1 / H2 slot: every one for small batches, ~6 % of the blocks beyond

@@ -475,7 +475,7 @@ __global__ __launch_bounds__(kZfParseThreads) void zs_fast_parse_kernel(DecodeAr
       rec.lit = lit;
       rec.nlit = nlit;
       rec.produced = produced;
-      rec.info = nseq | ((kZfFast | (rle ? kZfRle : 0u) | (h.checksum ? kZfSum : 0u) | (huf ? kZfHuf : 0u) |
+      rec.info = nseq | ((kZfFast | (rle ? kZfRle : 0u) | (h.checksum ? kZfSum : 0u) | (huf ? kZfHuf | kZfHufOrig : 0u) |
                           (huf == 4 ? kZfHuf4 : 0u))
                          << 16);
       rec.cs = cs;
@@ -973,7 +973,7 @@ __device__ __forceinline__ ZfRaw zf_load(const DecodeArgs& a, const ZsFastArgs& 
 // 4-byte records (kZfSeq4) sequences 2i and 2i + 1 on lane i (slots A and B); a slot past the
 // block's sequences holds zeros.
 struct ZfBlock {
-  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs, s4, outlit, adler, want;
+  uint32_t b, fast, shift, len, cap, nseq, nlit, produced, lit, rle, huf, cs, s4, outlit, adler, want, hufo;
   const uint8_t* gin;
   uint8_t* gout;
   uint32_t llA, mlA, offA, llB, mlB, offB;
@@ -995,6 +995,7 @@ __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r
   k.lit = __builtin_amdgcn_readfirstlane(r.rec.lit);
   k.rle = fl & kZfRle;
   k.huf = (fl & kZfHuf) ? ((fl & kZfHuf4) ? 4u : 1u) : 0u;
+  k.hufo = fl & kZfHufOrig;
   k.cs = __builtin_amdgcn_readfirstlane(r.rec.cs);
   k.s4 = (fl & kZfSeq4) ? 1u : 0u;
   k.outlit = fl & kZfOutLit;  // (CodecZlib: the literals are at the start of the output slot)
@@ -1192,12 +1193,28 @@ __global__ __launch_bounds__(kZfBuildThreads, SLATE_ZF_BUILD_WG) void zs_fast_bu
   // 1<<27 no output write, 1<<28 no frame staging
   const uint32_t dbg = dbg_bits(a);
   const uint32_t first = blockIdx.x * (kZfBuildThreads / 64) + wave;
-  ZfRaw nr = zf_load(a, z, first, lane);
-  for (uint32_t b = first; b < a.n; b += waves) {
+  // list mode (z.blist): item i is block blist[i], for the H2-prepared blocks only
+  const uint32_t i_end = z.blist ? min(z.count[1], z.hcap) : a.n;
+  auto block_at = [&](uint32_t i) { return z.blist ? (i < i_end ? z.blist[i] : a.n) : i; };
+  uint32_t g0 = 0, gi = 0;
+  auto draw4 = [&]() { return __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(z.count + 3, z.draw) : 0u); };
+  auto next_of = [&](uint32_t i) {
+    if (!z.draw) return i + waves;
+    if (++gi == z.draw) {
+      g0 = draw4();
+      gi = 0;
+    }
+    return g0 + gi;
+  };
+  uint32_t i = first;
+  if (z.draw) i = g0 = draw4();
+  ZfRaw nr = zf_load(a, z, block_at(i), lane);
+  while (i < i_end) {
     const ZfRaw cr = nr;
-    nr = zf_load(a, z, b + waves, lane);  // in flight while this block is built
+    i = next_of(i);
+    nr = zf_load(a, z, block_at(i), lane);  // in flight while this block is built
     const ZfBlock cur = zf_decode(a, cr, lane);
-    if (!cur.fast || cur.huf) continue;  // (Huffman literals: phase B')
+    if (!cur.fast || cur.huf || (z.skip_hufo && cur.hufo)) continue;  // (Huffman literals: phase B' / the list pass)
     // CodecZlib (kZfOutLit): the literal bytes at the start of the (16-aligned) output slot take
     // the frame's place: shift 0, literals from byte 0, nlit bytes
     const uint32_t lbase = cur.cap - cur.nlit, lit = cur.outlit ? 0u : cur.lit, shift = cur.outlit ? 0u : cur.shift;
@@ -2089,6 +2106,54 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
     else zs_huf_tree_lanes_kernel<<<grid_h1, 64, kZhLLds, q>>>(a, z);
   };
   const uint32_t grid_h2 = min((hmax + kZhBlocks - 1) / kZhBlocks, uint32_t(num_cus) * 2u);
+  const size_t lds_b = kZfBuildLds;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
+  if (attr != hipSuccess) return attr;
+  const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG);
+  const size_t lds_h = kZfHufLds;
+  static const hipError_t attr_h = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_huf_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_h));
+  if (attr_h != hipSuccess) return attr_h;
+  static const uint32_t huf_wg = [] {  // phase B' workgroups per CU (A/B runs: SLATE_ZF_HUF_WG, 1..3)
+    const char* e = getenv("SLATE_ZF_HUF_WG");
+    const uint32_t v = e ? uint32_t(atoi(e)) : 2u;
+    return v >= 1 && v <= 163840 / kZfHufLds ? v : 2u;
+  }();
+  const uint32_t grid_c = min((a.n + kZfSumThreads - 1) / kZfSumThreads, uint32_t(num_cus) * 4u);
+  // SLATE_ZF_B_EARLY=1 (read per call; off: slower on configs[4], profiles/round6/ab/ab_zstd_b_early.txt):
+  // the main stream's B starts after A2 and skips the Huffman-literal blocks (kZfHufOrig); the side
+  // stream runs H1, H2, then -- once A2 is done -- B over H2's blocks (list mode) and B' over the
+  // list's rest, joined before C
+  const char* early_env = getenv("SLATE_ZF_B_EARLY");
+  const bool early = early_env && *early_env == '1';
+  // SLATE_ZF_B_DRAW=G: phase B (main stream) draws G blocks at a time from a counter (0: static stride)
+  const char* draw_env = getenv("SLATE_ZF_B_DRAW");
+  const uint32_t bdraw = draw_env ? uint32_t(atoi(draw_env)) : 0u;
+  ZsFastArgs zb = z;
+  zb.draw = bdraw;
+  if (hs != st && early) {
+    launch_h1(hs);
+    zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, hs>>>(a, z);
+    zs_fast_crc_kernel<<<grid_crc, kZfCrcThreads, lds_crc, st>>>(a, z);
+    hipError_t e = hipEventRecord(fh->fork, st);  // A2 done (fork's first wait was enqueued above)
+    if (e == hipSuccess) e = hipStreamWaitEvent(hs, fh->fork, 0);
+    if (e != hipSuccess) return e;
+    ZsFastArgs zl = z;
+    zl.blist = z.hlist;
+    zs_fast_build_kernel<<<min((hmax + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG),
+                           kZfBuildThreads, lds_b, hs>>>(a, zl);
+    zs_fast_huf_kernel<<<uint32_t(num_cus) * huf_wg, kZfHufThreads, lds_h, hs>>>(a, zh);
+    ZsFastArgs zm = z;
+    zm.skip_hufo = 1;
+    zm.draw = bdraw;
+    zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, zm);
+    e = hipEventRecord(fh->join, hs);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, fh->join, 0);
+    if (e != hipSuccess) return e;
+    zs_fast_sum_kernel<<<grid_c, kZfSumThreads, 0, st>>>(a, z);
+    return hipGetLastError();
+  }
   if (hs != st) {
     launch_h1(hs);
     zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, hs>>>(a, z);
@@ -2103,33 +2168,18 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
       zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, st>>>(a, z);
     }
   }
-  const size_t lds_b = kZfBuildLds;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_build_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_b));
-  if (attr != hipSuccess) return attr;
-  const uint32_t grid_b = min((a.n + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG);
-  const size_t lds_h = kZfHufLds;
-  static const hipError_t attr_h = hipFuncSetAttribute(reinterpret_cast<const void*>(&zs_fast_huf_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, int(lds_h));
-  if (attr_h != hipSuccess) return attr_h;
   static const bool serial = getenv("SLATE_ZF_SERIAL") != nullptr;  // one stream (A/B runs)
   SideStream* f = (serial || !a.side) ? nullptr : a.side;
   hipStream_t sh = st;
   if (f && f->get() && hipEventRecord(f->fork, st) == hipSuccess && hipStreamWaitEvent(f->s, f->fork, 0) == hipSuccess)
     sh = f->s;
-  static const uint32_t huf_wg = [] {  // phase B' workgroups per CU (A/B runs: SLATE_ZF_HUF_WG, 1..3)
-    const char* e = getenv("SLATE_ZF_HUF_WG");
-    const uint32_t v = e ? uint32_t(atoi(e)) : 2u;
-    return v >= 1 && v <= 163840 / kZfHufLds ? v : 2u;
-  }();
   zs_fast_huf_kernel<<<uint32_t(num_cus) * huf_wg, kZfHufThreads, lds_h, sh>>>(a, zh);
-  zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, z);
+  zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, zb);
   if (sh != st) {
     hipError_t e = hipEventRecord(f->join, sh);
     if (e == hipSuccess) e = hipStreamWaitEvent(st, f->join, 0);
     if (e != hipSuccess) return e;
   }
-  const uint32_t grid_c = min((a.n + kZfSumThreads - 1) / kZfSumThreads, uint32_t(num_cus) * 4u);
   zs_fast_sum_kernel<<<grid_c, kZfSumThreads, 0, st>>>(a, z);
   return hipGetLastError();
 }
