@@ -103,14 +103,20 @@ constexpr uint32_t kInStride = kIR + SLATE_LPB_IPAD;
 #define SLATE_VERIFY_BATCH 4
 #endif
 constexpr uint32_t kVerifyBatch = SLATE_VERIFY_BATCH;
-// cache policy of the flush and row-descriptor stores (lpb_common.h bstore: sc1 = 16)
+// cache policy of the flush and row-descriptor stores (lpb_common.h bstore: sc1 = 16, nt = 2): the
+// flush as nt, the rows sc1 (round 6, same-box A/Bs over 1 M blocks: flush nt 3.792 -> 3.752 and
+// 3.785 -> 3.751 ms; rows nt 4.263; refills nt 3.758 alone, 3.776 with the flush nt;
+// profiles/round6/ab/ab_lpb2_cpol.txt)
 #ifndef SLATE_OUT_CPOL
-#define SLATE_OUT_CPOL 16
+#define SLATE_OUT_CPOL 2
 #endif
 #ifndef SLATE_ROW_CPOL
 #define SLATE_ROW_CPOL 16
 #endif
-constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL;
+#ifndef SLATE_IN_CPOL  // the refills' loads
+#define SLATE_IN_CPOL 0
+#endif
+constexpr int kOutCpol = SLATE_OUT_CPOL, kRowCpol = SLATE_ROW_CPOL, kInCpol = SLATE_IN_CPOL;
 // the previous iteration's hole source is merged before step 1 (measured, configs[1], 1 M blocks,
 // round 4: before step 0 4.535 ms, step 1 4.469, step 2 4.524): a step more for the load to arrive
 #ifndef SLATE_WALK_LAG
@@ -464,7 +470,7 @@ __device__ __forceinline__ void load_j(uint32_t lane, uint32_t info, uint32_t re
   const uint32_t info_o = __shfl(info, int(16 * kJ + (lane >> 2)), 64);
   const uint32_t ci = (info_o >> 3) + c;
   const bool want = c < (info_o & 7);
-  P = __builtin_amdgcn_raw_buffer_load_b128(R.in, want ? rel_j + 16 * ci : kOOB, 0, 0);
+  P = __builtin_amdgcn_raw_buffer_load_b128(R.in, want ? rel_j + 16 * ci : kOOB, 0, kInCpol);
   S = want ? (ci & (kNS - 1)) * 16 : 0xFFFFFFFFu;
 }
 
