@@ -130,6 +130,7 @@ struct ZsFastArgs {
   // phase B draws its blocks `draw` at a time from count[3] (zeroed with the others) instead of a
   // static stride: workgroups that start late (CUs held by H1 / H2) take fewer
   uint32_t draw = 0;
+  uint32_t out_nt = 0;  // phase B's output stores non-temporal
 };
 constexpr uint32_t kZhTab = 4096;  // a Huffman decoding table: 2^11 16-bit entries
 // hlist entries with an H1 / H2 slot: every one for small batches, ~6 % of the blocks beyond

@@ -1025,7 +1025,7 @@ __device__ __forceinline__ ZfBlock zf_decode(const DecodeArgs& a, const ZfRaw& r
 // (or the RLE byte), write it back, then block.Decode's checks and rows (phases B and B').
 // CodecZlib blocks (kZfAdler) are checked against the stream's Adler-32 first: false = mismatch,
 // nothing written (the caller hands the block to the exact path, which reports it).
-__device__ __forceinline__ bool zf_build(const DecodeArgs& a, const ZfBlock& cur, uint8_t* wout, uint32_t lb,
+__device__ __forceinline__ bool zf_build(const DecodeArgs& a, const ZfBlock& cur, uint8_t* wout, uint32_t lb, uint32_t out_nt,
                                          uint32_t lane, uint32_t dbg) {
   const uint32_t lit = cur.lit;
   slate_block_meta m{};
@@ -1171,7 +1171,12 @@ __device__ __forceinline__ bool zf_build(const DecodeArgs& a, const ZfBlock& cur
     uint8_t* gout = cur.gout;
     const uint32_t oc = (dbg & (1u << 27)) ? 0u : (n + 15) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(wout);
-    for (uint32_t c = lane; c < oc; c += kWave) reinterpret_cast<uint4*>(gout)[c] = src[c];
+    if (out_nt) {
+      const v4u* s4 = reinterpret_cast<const v4u*>(wout);
+      for (uint32_t c = lane; c < oc; c += kWave) __builtin_nontemporal_store(s4[c], reinterpret_cast<v4u*>(gout) + c);
+    } else {
+      for (uint32_t c = lane; c < oc; c += kWave) reinterpret_cast<uint4*>(gout)[c] = src[c];
+    }
   }
   if (dbg & (1u << 20)) write_meta(&a.meta[cur.b], m, int(lane));
   else block_finish(a, cur.b, wout, n, int(lane), m);
@@ -1232,7 +1237,7 @@ __global__ __launch_bounds__(kZfBuildThreads, SLATE_ZF_BUILD_WG) void zs_fast_bu
     }
     __builtin_amdgcn_s_waitcnt(0);
     zs_sync();
-    if (!zf_build(a, cur, wout, lb, lane, dbg) && lane == 0) {  // (the block's CRC32 held: phase A2)
+    if (!zf_build(a, cur, wout, lb, z.out_nt, lane, dbg) && lane == 0) {  // (the block's CRC32 held: phase A2)
       z.rec[cur.b].info = 0;
       z.list[atomicAdd(z.count, 1u)] = cur.b;  // the Adler-32 failed: the exact path reports it
     }
@@ -1334,7 +1339,7 @@ __global__ __launch_bounds__(kZfHufThreads) void zs_fast_huf_kernel(DecodeArgs a
       continue;
     }
     zs_sync();
-    (void)zf_build(a, cur, wout, lbase, lane, 0);  // (Zstd frames only: no Adler-32)
+    (void)zf_build(a, cur, wout, lbase, z.out_nt, lane, 0);  // (Zstd frames only: no Adler-32)
   }
 }
 
@@ -2132,6 +2137,10 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
   const uint32_t bdraw = draw_env ? uint32_t(atoi(draw_env)) : 0u;
   ZsFastArgs zb = z;
   zb.draw = bdraw;
+  // phase B's output stores non-temporal (SLATE_ZF_OUT_NT=0: default policy; read per call):
+  // configs[4] 4.52 -> 4.33 ms, kv100 9.09 -> 9.04 (profiles/round6/ab/ab_zstd_out_nt.txt)
+  const char* nt_env = getenv("SLATE_ZF_OUT_NT");
+  zb.out_nt = nt_env && *nt_env == '0' ? 0u : 1u;
   if (hs != st && early) {
     launch_h1(hs);
     zs_huf_stream_kernel<<<grid_h2, 64, kZhStreamLds, hs>>>(a, z);
@@ -2139,12 +2148,13 @@ hipError_t launch_zstd_fast(hipStream_t st, const DecodeArgs& a, const ZsFastArg
     hipError_t e = hipEventRecord(fh->fork, st);  // A2 done (fork's first wait was enqueued above)
     if (e == hipSuccess) e = hipStreamWaitEvent(hs, fh->fork, 0);
     if (e != hipSuccess) return e;
-    ZsFastArgs zl = z;
+    ZsFastArgs zl = zb;
+    zl.draw = 0;
     zl.blist = z.hlist;
     zs_fast_build_kernel<<<min((hmax + kZfBuildThreads / 64 - 1) / (kZfBuildThreads / 64), uint32_t(num_cus) * SLATE_ZF_BUILD_WG),
                            kZfBuildThreads, lds_b, hs>>>(a, zl);
     zs_fast_huf_kernel<<<uint32_t(num_cus) * huf_wg, kZfHufThreads, lds_h, hs>>>(a, zh);
-    ZsFastArgs zm = z;
+    ZsFastArgs zm = zb;
     zm.skip_hufo = 1;
     zm.draw = bdraw;
     zs_fast_build_kernel<<<grid_b, kZfBuildThreads, lds_b, st>>>(a, zm);
