@@ -85,8 +85,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   const uint32_t n = __builtin_amdgcn_readfirstlane(bytes < kOOB ? uint32_t(bytes) : kOOB);
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0, int(n), 0x00020000);
 }
+#ifndef SLATE_ZF_LDPOL  // cache policy of the phases' streaming loads (0 default, 2 nt)
+#define SLATE_ZF_LDPOL 0
+#endif
 __device__ __forceinline__ v4u bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SLATE_ZF_LDPOL);
 }
 __device__ __forceinline__ void lds_put16(uint8_t* p, const v4u& v) { *reinterpret_cast<v4u*>(p) = v; }
 
