@@ -43,9 +43,9 @@ constexpr uint32_t kNoneLds = kNoneTabBytes + (kNoneThreads / 64) * kNoneStage;
 #define SLATE_NONE_CPOL 2
 #endif
 constexpr int kNoneCpol = SLATE_NONE_CPOL;
-#ifndef SLATE_NONE_LDPOL  // cache policy of the block loads (0 default, 2 nt)
-#define SLATE_NONE_LDPOL 2
-#endif
+#ifndef SLATE_NONE_LDPOL  // cache policy of the block loads (0 default, 2 nt): default since round 6
+#define SLATE_NONE_LDPOL 0   // (same-box A/Bs, 1 M blocks: nt 2.158 / 2.153 ms, default 2.082 / 2.074;
+#endif                       // profiles/round6/ab/ab_none_policy.txt)
 constexpr int kNoneLdpol = SLATE_NONE_LDPOL;
 // The decoded block is stored as soon as its chunks are formed, before the CRC's lane tree, so the
 // stores drain while the tree's dependent lookups run (round 6).  A block whose CRC then fails has
